@@ -1,0 +1,230 @@
+#!/usr/bin/env python3
+"""bench.py -- hydra bucket-reduction hot path on MI355X.
+
+Metric (BASELINE.json): chunk-sum GB/s (fp32) vs HBM peak; ring-allreduce GB/s at 1/2/4/8 GPU.
+
+  N = 1  (BASELINE config 2): one step = one device-resident, in-place fp32 chunk-sum
+         c = a + b over 64 Mi elements (gloo::sum<float>, math.h:15-23, in the ring's c == a
+         form).  value = 12 B/element x elements x steps / wall time of the timed region.
+  N > 1  (BASELINE config 4): one step = one allreduce of a 64 Mi-element fp32 bucket per rank
+         over RCCL/xGMI with the HIP sum fused into every reduce-scatter hop (hydra_amd.ring).
+         value = N x bucket bytes / time (whole-job bucket bytes reduced per second); algbw and
+         busbw = algbw x 2(N-1)/N are reported beside it.
+
+Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under torch.distributed.run.
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+XGMI_LINK_GBS = 153.0      # per xGMI link, per direction (task brief)
+N_MICRO = 64 << 20         # config 2 largest size; config 4 bucket
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--warmup", type=int, default=20)
+    p.add_argument("--elements", type=int, default=N_MICRO)
+    p.add_argument("--dtype", default="f32", choices=["f32", "i32"])
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=10.0,
+                   help="bounded CPU-baseline sample (seconds of reference gloo::sum work)")
+    p.add_argument("--sweep", action="store_true", help="add the 4 Ki..64 Mi size sweep")
+    p.add_argument("--variants", action="store_true", help="A/B all kernel variants (tuning)")
+    p.add_argument("--algo", default="auto", help="ring algorithm for N>1 (see hydra_amd.ring)")
+    return p.parse_args()
+
+
+def dist_env():
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    return ws, rank, local
+
+
+# ------------------------------------------------------------------------------- N = 1
+def time_chunk_sum(torch, L, dev, n, code, steps, warmup, variant=None):
+    """Returns (wall_seconds for `steps` launches, per-launch kernel ms list)."""
+    from hydra_amd import _lib
+    from hydra_amd import synth
+
+    if code == _lib.FLOAT32:
+        a = torch.from_numpy(synth.bew_inputs(0, n)).to(dev)
+        b = torch.from_numpy(synth.uniform_f32(n, 42)).to(dev)
+    else:
+        a = torch.from_numpy(synth.int32_bucket(8, 0, n)).to(dev)
+        b = torch.from_numpy(synth.int32_bucket(8, 1, n)).to(dev)
+    s = torch.cuda.current_stream(dev)
+    sp = s.cuda_stream
+    pa, pb = a.data_ptr(), b.data_ptr()
+    prev = L.hydra_set_variant(variant) if variant is not None else None
+    try:
+        for _ in range(warmup):
+            _lib.check(L.hydra_chunk_sum(code, pa, pa, pb, n, sp))
+        torch.cuda.synchronize(dev)
+        # timed region: exactly `steps` launches, synchronised on both sides
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            _lib.check(L.hydra_chunk_sum(code, pa, pa, pb, n, sp))
+        torch.cuda.synchronize(dev)
+        wall = time.perf_counter() - t0
+        # per-launch device time with HIP events recorded on the launch stream
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(steps)]
+        for e0, e1 in ev:
+            e0.record(s)
+            _lib.check(L.hydra_chunk_sum(code, pa, pa, pb, n, sp))
+            e1.record(s)
+        torch.cuda.synchronize(dev)
+        ms = [e0.elapsed_time(e1) for e0, e1 in ev]
+    finally:
+        if prev is not None:
+            L.hydra_set_variant(prev)
+    del a, b
+    return wall, ms
+
+
+def pmc_traffic():
+    """HBM bytes per launch of the 64 Mi chunk-sum from the committed rocprofv3 PMC summary
+    (profiles/pmc_chunk_sum.json, written by profiles/collect.sh: FETCH_SIZE x2 gfx950
+    correction + WRITE_SIZE, MI355X_MICROARCH.md §HBM).  None if absent."""
+    p = os.path.join(ROOT, "profiles", "pmc_chunk_sum.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        return d.get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def cpu_baseline(n_total, seconds):
+    """The reference's own gloo::sum<float> (oracle/_ref, compiled from /root/reference) timed
+    single-threaded on this host; falls back to the C restatement (oracle/liboracle.so)."""
+    from oracle import oracle as O
+
+    sample_n = 16 << 20  # bounded sample: 16 Mi fp32 in place (192 MB of traffic per call)
+    a = np.arange(sample_n, dtype=np.float32)
+    b = np.ones(sample_n, dtype=np.float32)
+    kind = "reference" if O.ref_available() else "port"
+    # calibrate, then run ~`seconds` of work
+    if kind == "reference":
+        per = O.ref_time_sum(6, a, a, b, 2, 1)
+        iters = max(1, int(seconds / max(per, 1e-6) / 3))
+        per = O.ref_time_sum(6, a, a, b, iters, 3)
+    else:
+        t0 = time.perf_counter()
+        k = 0
+        while time.perf_counter() - t0 < seconds:
+            O.orc().orc_op(0, 6, a.ctypes.data, a.ctypes.data, b.ctypes.data, sample_n)
+            k += 1
+        per = (time.perf_counter() - t0) / k
+    gbs = 12.0 * sample_n / per / 1e9
+    return {"value": round(gbs, 3), "unit": "GB/s", "cores": 1, "kind": kind,
+            "sample": f"gloo::sum<float> in place over 16 Mi fp32 (12 B/element), "
+                      f"single thread, ~{seconds:.0f} s of repetitions, best-of-3 mean",
+            "per_call_ms_at_64Mi": round(per * 4 * 1e3, 2)}
+
+
+def run_single(args):
+    import torch
+
+    from hydra_amd import _lib
+
+    L = _lib.lib()
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    code = _lib.FLOAT32 if args.dtype == "f32" else _lib.INT32
+    n = args.elements
+    wall, ms = time_chunk_sum(torch, L, dev, n, code, args.steps, args.warmup)
+    algo_bytes = 12.0 * n
+    value = algo_bytes * args.steps / wall / 1e9
+    avg_ms = float(np.mean(ms))
+    achieved = algo_bytes / (avg_ms * 1e-3) / 1e9
+    traffic = pmc_traffic()
+    out = {
+        "metric": "chunk-sum GB/s (fp32) vs HBM peak",
+        "value": round(value, 2), "unit": "GB/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(wall / args.steps * 1e3, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "f32" if code == _lib.FLOAT32 else "i32", "data": "synthetic",
+        "config": {"workload": "device-resident in-place chunk sum c=a+b (gloo::sum<float> "
+                               "ring form), BASELINE config 2", "elements": n,
+                   "bytes_per_element": 12, "parallelism": "single GPU"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": traffic, "kernel_ms_avg": round(avg_ms, 5),
+                     "kernel_ms_min": round(float(np.min(ms)), 5),
+                     "timing": "HIP events around each launch on the launch stream"},
+    }
+    if args.sweep:
+        sweep = []
+        for k in range(12, 27, 2):
+            nn = 1 << k
+            w, m = time_chunk_sum(torch, L, dev, nn, code, 200, 20)
+            sweep.append({"elements": nn, "kernel_us": round(float(np.median(m)) * 1e3, 2),
+                          "GBps": round(12.0 * nn / (float(np.median(m)) * 1e-3) / 1e9, 1)})
+        out["sweep"] = sweep
+    if args.variants:
+        var = {}
+        for rnd in range(3):
+            for v in range(1, 8):
+                _, m = time_chunk_sum(torch, L, dev, n, code, 50, 5, variant=v)
+                var.setdefault(v, []).append(float(np.median(m)))
+        out["variants_median_ms"] = {str(k): [round(x, 5) for x in v] for k, v in var.items()}
+    if not args.no_cpu_baseline:
+        try:
+            out["cpu_baseline"] = cpu_baseline(n, args.cpu_seconds)
+        except Exception as e:  # the baseline is reported, never the product
+            out["cpu_baseline"] = {"value": None, "error": str(e)}
+    print(json.dumps(out), flush=True)
+
+
+# ------------------------------------------------------------------------------- N > 1
+def run_multi(args):
+    import torch
+    import torch.distributed as dist
+
+    from hydra_amd import ring
+
+    ws, rank, local = dist_env()
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist.init_process_group("nccl", device_id=dev)
+    try:
+        res = ring.bench_allreduce(args, dev)
+    finally:
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+
+
+def main():
+    args = parse()
+    ws, _, _ = dist_env()
+    if ws != args.gpus and not (ws == 1 and args.gpus == 1):
+        if ws == 1:
+            raise SystemExit(f"--gpus {args.gpus} needs torch.distributed.run with "
+                             f"--nproc-per-node {args.gpus}")
+    if ws > 1:
+        run_multi(args)
+    else:
+        run_single(args)
+
+
+if __name__ == "__main__":
+    main()

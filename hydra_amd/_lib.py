@@ -1,0 +1,114 @@
+"""ctypes binding of libhydra_hip.so (include/hydra_hip.h).
+
+The library is built in-tree (hydra_amd/csrc/Makefile -> hydra_amd/libhydra_hip.so).  There is no
+fallback: if the shared object is missing or fails to load, every entry point raises
+HydraError -- the hot path never silently runs on the CPU.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+import threading
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libhydra_hip.so")
+CSRC = os.path.join(HERE, "csrc")
+
+# hydra_dtype_t / hydra_op_t
+INT8, UINT8, INT32, UINT32, INT64, UINT64, FLOAT32, FLOAT64, FLOAT16, BFLOAT16 = range(10)
+SUM, PRODUCT, MAX, MIN = range(4)
+OPS = {"sum": SUM, "product": PRODUCT, "max": MAX, "min": MIN}
+ESIZE = {INT8: 1, UINT8: 1, INT32: 4, UINT32: 4, INT64: 8, UINT64: 8, FLOAT32: 4, FLOAT64: 8,
+         FLOAT16: 2, BFLOAT16: 2}
+
+EXPORTS = [  # every symbol include/hydra_hip.h declares
+    "hydra_abi_version", "hydra_last_error", "hydra_device_count", "hydra_device_arch",
+    "hydra_reduce", "hydra_chunk_sum", "hydra_acc_bf16_f32", "hydra_f32_to_bf16",
+    "hydra_set_variant", "hydra_ctx_create", "hydra_ctx_destroy", "hydra_reduce_host",
+    "hydra_chunk_sum_host", "hydra_host_register", "hydra_host_unregister",
+    "hydra_stream_create", "hydra_stream_destroy", "hydra_stream_synchronize", "hydra_malloc",
+    "hydra_free", "hydra_memcpy", "hydra_ring_plan",
+]
+
+
+class HydraError(RuntimeError):
+    """A non-zero hydra_status_t (or a missing library)."""
+
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"hydra error {code}: {msg}")
+        self.code = code
+
+
+_lock = threading.Lock()
+_lib = None
+
+
+def build(force: bool = False) -> str:
+    """Compile libhydra_hip.so for gfx950 (hipcc cross-compiles without a GPU)."""
+    if force:
+        subprocess.check_call(["make", "-s", "-C", CSRC, "clean"])
+    subprocess.check_call(["make", "-s", "-j4", "-C", CSRC])
+    return LIB_PATH
+
+
+def _declare(L) -> None:
+    vp, sz, i = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
+    L.hydra_abi_version.restype = i
+    L.hydra_last_error.restype = ctypes.c_char_p
+    L.hydra_device_count.argtypes = [ctypes.POINTER(i)]
+    L.hydra_device_arch.argtypes = [i, ctypes.c_char_p, sz]
+    L.hydra_reduce.argtypes = [i, i, vp, vp, vp, sz, vp]
+    L.hydra_chunk_sum.argtypes = [i, vp, vp, vp, sz, vp]
+    L.hydra_acc_bf16_f32.argtypes = [vp, vp, sz, vp]
+    L.hydra_f32_to_bf16.argtypes = [vp, vp, sz, vp]
+    L.hydra_set_variant.argtypes = [i]
+    L.hydra_ctx_create.argtypes = [i, ctypes.POINTER(vp)]
+    L.hydra_ctx_destroy.argtypes = [vp]
+    L.hydra_reduce_host.argtypes = [vp, i, i, vp, vp, vp, sz]
+    L.hydra_chunk_sum_host.argtypes = [vp, i, vp, vp, vp, sz]
+    L.hydra_host_register.argtypes = [vp, sz]
+    L.hydra_host_unregister.argtypes = [vp]
+    L.hydra_stream_create.argtypes = [i, ctypes.POINTER(vp)]
+    L.hydra_stream_destroy.argtypes = [vp]
+    L.hydra_stream_synchronize.argtypes = [vp]
+    L.hydra_malloc.argtypes = [i, sz, ctypes.POINTER(vp)]
+    L.hydra_free.argtypes = [vp]
+    L.hydra_memcpy.argtypes = [vp, vp, sz]
+    L.hydra_ring_plan.argtypes = [i, sz, sz, sz] + [ctypes.POINTER(sz)] * 3
+    L.hydra_ring_plan.restype = None
+
+
+def lib():
+    """Load (once) and return the ctypes handle.  torch must be imported first on a GPU box so
+    that this library binds to the same HIP runtime as torch (same soname)."""
+    global _lib
+    if _lib is None:
+        with _lock:
+            if _lib is None:
+                if not os.path.exists(LIB_PATH):
+                    raise HydraError(-1, f"{LIB_PATH} is not built (hydra_amd._lib.build())")
+                try:
+                    import torch  # noqa: F401  (bind to torch's libamdhip64 when present)
+                except ImportError:
+                    pass
+                L = ctypes.CDLL(LIB_PATH)
+                _declare(L)
+                _lib = L
+    return _lib
+
+
+def check(rc: int) -> None:
+    if rc != 0:
+        raise HydraError(rc, lib().hydra_last_error().decode(errors="replace"))
+
+
+def ring_plan(P: int, n: int, esize: int, max_segment: int = 1 << 20):
+    ns, sb, S = ctypes.c_size_t(), ctypes.c_size_t(), ctypes.c_size_t()
+    lib().hydra_ring_plan(P, n, esize, max_segment, ctypes.byref(ns), ctypes.byref(sb),
+                          ctypes.byref(S))
+    return ns.value, sb.value, S.value
+
+
+def set_variant(v: int) -> int:
+    return lib().hydra_set_variant(v)

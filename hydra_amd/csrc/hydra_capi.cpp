@@ -1,0 +1,308 @@
+// hydra_capi.cpp -- the extern "C" boundary of libhydra_hip.so (declared in include/hydra_hip.h).
+//
+// Argument checking, error reporting (thread-local message + status code), the host-resident
+// staging context, and the ring geometry.  Kernels live in reduce_kernels.hip.
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+
+#include "../../include/hydra_hip.h"
+#include "reduce_kernels.h"
+
+namespace {
+
+thread_local std::string g_err;
+std::atomic<int> g_variant{0};
+
+int ok() {
+  g_err.clear();
+  return HYDRA_OK;
+}
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+  return fail(HYDRA_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define HIP_TRY(expr)                                   \
+  do {                                                  \
+    hipError_t e__ = (expr);                            \
+    if (e__ != hipSuccess) return hip_fail(e__, #expr); \
+  } while (0)
+
+bool overlaps(const void* x, const void* y, size_t bytes) {
+  const char* a = static_cast<const char*>(x);
+  const char* b = static_cast<const char*>(y);
+  return a < b + bytes && b < a + bytes;
+}
+
+// Shared argument contract of hydra_reduce / hydra_reduce_host.
+int check_args(int op, int dtype, const void* c, const void* a, const void* b, size_t n) {
+  if (op < HYDRA_SUM || op > HYDRA_MIN) return fail(HYDRA_ERR_INVALID, "invalid op");
+  const size_t es = hydra::dtype_size(dtype);
+  if (!es) return fail(HYDRA_ERR_INVALID, "invalid dtype " + std::to_string(dtype));
+  if (n == 0) return HYDRA_OK;
+  if (!c || !a || !b) return fail(HYDRA_ERR_INVALID, "null pointer");
+  const uintptr_t m = es - 1;
+  if ((reinterpret_cast<uintptr_t>(c) | reinterpret_cast<uintptr_t>(a) |
+       reinterpret_cast<uintptr_t>(b)) & m)
+    return fail(HYDRA_ERR_INVALID, "pointer not aligned to the element size");
+  const size_t bytes = n * es;
+  if (c != a && overlaps(c, a, bytes))
+    return fail(HYDRA_ERR_INVALID, "c partially overlaps a (only c == a is allowed)");
+  if (c != b && overlaps(c, b, bytes))
+    return fail(HYDRA_ERR_INVALID, "c partially overlaps b (only c == b is allowed)");
+  return HYDRA_OK;
+}
+
+}  // namespace
+
+// ---- host staging context ----------------------------------------------------------------
+// Two streams ping-pong over fixed-size chunks: H2D(a,b) -> reduce -> D2H(c) on stream k%2, so
+// chunk k+1's copies overlap chunk k's kernel and copy-back.
+struct hydra_ctx {
+  int device = 0;
+  hipStream_t stream[2] = {nullptr, nullptr};
+  void* da[2] = {nullptr, nullptr};
+  void* db[2] = {nullptr, nullptr};
+  void* dc[2] = {nullptr, nullptr};  // only for float16 with c != a
+  size_t chunk_bytes = 0;
+};
+
+namespace {
+constexpr size_t kChunkBytes = 8u << 20;
+
+void ctx_release(hydra_ctx* x) {
+  for (int i = 0; i < 2; i++) {
+    if (x->stream[i]) (void)hipStreamDestroy(x->stream[i]);
+    if (x->da[i]) (void)hipFree(x->da[i]);
+    if (x->db[i]) (void)hipFree(x->db[i]);
+    if (x->dc[i]) (void)hipFree(x->dc[i]);
+  }
+}
+}  // namespace
+
+extern "C" {
+
+int hydra_abi_version(void) { return HYDRA_ABI_VERSION; }
+
+const char* hydra_last_error(void) { return g_err.c_str(); }
+
+int hydra_device_count(int* count) {
+  if (!count) return fail(HYDRA_ERR_INVALID, "null count");
+  int c = 0;
+  hipError_t e = hipGetDeviceCount(&c);
+  if (e != hipSuccess) {
+    *count = 0;
+    return hip_fail(e, "hipGetDeviceCount");
+  }
+  *count = c;
+  return ok();
+}
+
+int hydra_device_arch(int device, char* buf, size_t len) {
+  hipDeviceProp_t p;
+  HIP_TRY(hipGetDeviceProperties(&p, device));
+  if (buf && len) {
+    std::strncpy(buf, p.gcnArchName, len - 1);
+    buf[len - 1] = 0;
+  }
+  return ok();
+}
+
+int hydra_set_variant(int variant) { return g_variant.exchange(variant); }
+
+int hydra_reduce(int op, int dtype, void* c, const void* a, const void* b, size_t n,
+                 hydra_stream_t stream) {
+  int rc = check_args(op, dtype, c, a, b, n);
+  if (rc) return rc;
+  if (n == 0) return ok();
+  hipError_t e = hydra::launch_reduce(g_variant.load(std::memory_order_relaxed), op, dtype, c, a,
+                                      b, n, static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return hip_fail(e, "reduce kernel launch");
+  return ok();
+}
+
+int hydra_chunk_sum(int dtype, void* c, const void* a, const void* b, size_t n,
+                    hydra_stream_t stream) {
+  return hydra_reduce(HYDRA_SUM, dtype, c, a, b, n, stream);
+}
+
+int hydra_acc_bf16_f32(float* acc, const void* b_bf16, size_t n, hydra_stream_t stream) {
+  if (n == 0) return ok();
+  if (!acc || !b_bf16) return fail(HYDRA_ERR_INVALID, "null pointer");
+  if ((reinterpret_cast<uintptr_t>(acc) & 15) || (reinterpret_cast<uintptr_t>(b_bf16) & 1))
+    return fail(HYDRA_ERR_INVALID, "acc must be 16-B aligned, b 2-B aligned");
+  hipError_t e = hydra::launch_acc_bf16_f32(acc, b_bf16, n, static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return hip_fail(e, "acc_bf16 kernel launch");
+  return ok();
+}
+
+int hydra_f32_to_bf16(void* out_bf16, const float* acc, size_t n, hydra_stream_t stream) {
+  if (n == 0) return ok();
+  if (!acc || !out_bf16) return fail(HYDRA_ERR_INVALID, "null pointer");
+  hipError_t e = hydra::launch_f32_to_bf16(out_bf16, acc, n, static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return hip_fail(e, "f32_to_bf16 kernel launch");
+  return ok();
+}
+
+// ---- host-resident ------------------------------------------------------------------------
+int hydra_ctx_create(int device, hydra_ctx_t* out) {
+  if (!out) return fail(HYDRA_ERR_INVALID, "null out");
+  *out = nullptr;
+  int count = 0;
+  HIP_TRY(hipGetDeviceCount(&count));
+  if (device < 0 || device >= count) return fail(HYDRA_ERR_NO_DEVICE, "no such device");
+  auto* x = new hydra_ctx();
+  x->device = device;
+  x->chunk_bytes = kChunkBytes;
+  hipError_t e = hipSetDevice(device);
+  for (int i = 0; i < 2 && e == hipSuccess; i++) {
+    e = hipStreamCreateWithFlags(&x->stream[i], hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipMalloc(&x->da[i], kChunkBytes);
+    if (e == hipSuccess) e = hipMalloc(&x->db[i], kChunkBytes);
+  }
+  if (e != hipSuccess) {
+    ctx_release(x);
+    delete x;
+    return hip_fail(e, "hydra_ctx_create");
+  }
+  *out = x;
+  return ok();
+}
+
+int hydra_ctx_destroy(hydra_ctx_t ctx) {
+  if (!ctx) return ok();
+  (void)hipSetDevice(ctx->device);
+  for (int i = 0; i < 2; i++)
+    if (ctx->stream[i]) (void)hipStreamSynchronize(ctx->stream[i]);
+  ctx_release(ctx);
+  delete ctx;
+  return ok();
+}
+
+int hydra_reduce_host(hydra_ctx_t ctx, int op, int dtype, void* c, const void* a, const void* b,
+                      size_t n) {
+  if (!ctx) return fail(HYDRA_ERR_INVALID, "null context");
+  int rc = check_args(op, dtype, c, a, b, n);
+  if (rc) return rc;
+  if (n == 0) return ok();
+  HIP_TRY(hipSetDevice(ctx->device));
+  const size_t es = hydra::dtype_size(dtype);
+  const size_t per = ctx->chunk_bytes / es;
+  const int variant = g_variant.load(std::memory_order_relaxed);
+  size_t k = 0;
+  for (size_t off = 0; off < n; off += per, k++) {
+    const size_t cnt = std::min(per, n - off);
+    const size_t bytes = cnt * es;
+    const int s = (int)(k & 1);
+    hipStream_t st = ctx->stream[s];
+    const char* pa = static_cast<const char*>(a) + off * es;
+    const char* pb = static_cast<const char*>(b) + off * es;
+    char* pc = static_cast<char*>(c) + off * es;
+    HIP_TRY(hipMemcpyAsync(ctx->da[s], pa, bytes, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(ctx->db[s], pb, bytes, hipMemcpyHostToDevice, st));
+    void* dc = ctx->da[s];  // in place on the staged a: c == a, the ring's form
+    if (dtype == HYDRA_FLOAT16 && c != a) {
+      // float16 stores depend on c's old bits (gloo store quirk): stage them too
+      if (!ctx->dc[s]) HIP_TRY(hipMalloc(&ctx->dc[s], ctx->chunk_bytes));
+      dc = ctx->dc[s];
+      HIP_TRY(hipMemcpyAsync(dc, pc, bytes, hipMemcpyHostToDevice, st));
+    }
+    hipError_t e = hydra::launch_reduce(variant, op, dtype, dc, ctx->da[s], ctx->db[s], cnt, st);
+    if (e != hipSuccess) return hip_fail(e, "reduce kernel launch");
+    HIP_TRY(hipMemcpyAsync(pc, dc, bytes, hipMemcpyDeviceToHost, st));
+  }
+  HIP_TRY(hipStreamSynchronize(ctx->stream[0]));
+  HIP_TRY(hipStreamSynchronize(ctx->stream[1]));
+  return ok();
+}
+
+int hydra_chunk_sum_host(hydra_ctx_t ctx, int dtype, void* c, const void* a, const void* b,
+                         size_t n) {
+  return hydra_reduce_host(ctx, HYDRA_SUM, dtype, c, a, b, n);
+}
+
+int hydra_host_register(void* ptr, size_t bytes) {
+  if (!ptr || !bytes) return fail(HYDRA_ERR_INVALID, "null/empty range");
+  hipError_t e = hipHostRegister(ptr, bytes, hipHostRegisterDefault);
+  if (e == hipErrorHostMemoryAlreadyRegistered) {
+    (void)hipGetLastError();
+    return ok();
+  }
+  if (e != hipSuccess) return hip_fail(e, "hipHostRegister");
+  return ok();
+}
+
+int hydra_host_unregister(void* ptr) {
+  hipError_t e = hipHostUnregister(ptr);
+  if (e != hipSuccess && e != hipErrorHostMemoryNotRegistered) return hip_fail(e, "unregister");
+  (void)hipGetLastError();
+  return ok();
+}
+
+// ---- helpers --------------------------------------------------------------------------------
+int hydra_stream_create(int device, hydra_stream_t* out) {
+  if (!out) return fail(HYDRA_ERR_INVALID, "null out");
+  HIP_TRY(hipSetDevice(device));
+  hipStream_t s = nullptr;
+  HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  *out = s;
+  return ok();
+}
+
+int hydra_stream_destroy(hydra_stream_t s) {
+  if (s) HIP_TRY(hipStreamDestroy(static_cast<hipStream_t>(s)));
+  return ok();
+}
+
+int hydra_stream_synchronize(hydra_stream_t s) {
+  HIP_TRY(hipStreamSynchronize(static_cast<hipStream_t>(s)));
+  return ok();
+}
+
+int hydra_malloc(int device, size_t bytes, void** out) {
+  if (!out) return fail(HYDRA_ERR_INVALID, "null out");
+  HIP_TRY(hipSetDevice(device));
+  HIP_TRY(hipMalloc(out, bytes));
+  return ok();
+}
+
+int hydra_free(void* p) {
+  if (p) HIP_TRY(hipFree(p));
+  return ok();
+}
+
+int hydra_memcpy(void* dst, const void* src, size_t bytes) {
+  HIP_TRY(hipMemcpy(dst, src, bytes, hipMemcpyDefault));
+  return ok();
+}
+
+// allreduce.cc:199-221 -- identical integer arithmetic.
+void hydra_ring_plan(int P, size_t n, size_t esize, size_t max_segment, size_t* num_segments,
+                     size_t* segment_bytes, size_t* segments_per_rank) {
+  auto round_up = [](size_t v, size_t m) {
+    const size_t r = v % m;
+    return r ? v + m - r : v;
+  };
+  const size_t total = n * esize;
+  const size_t max_seg_bytes = esize * std::max<size_t>(1, max_segment / esize);
+  const size_t ns = round_up(std::max((total + max_seg_bytes - 1) / max_seg_bytes,
+                                      (size_t)P * 2),
+                             (size_t)P);
+  if (num_segments) *num_segments = ns;
+  if (segments_per_rank) *segments_per_rank = ns / (size_t)P;
+  if (segment_bytes) *segment_bytes = round_up((total + ns - 1) / ns, esize);
+}
+
+}  // extern "C"

@@ -1,0 +1,394 @@
+// reduce_kernels.hip -- gfx950 (MI355X, CDNA4) streaming element-wise reduction kernels.
+//
+// The hot path is c[i] = op(a[i], b[i]) over one ring segment (gloo::sum<T>, math.h:15-23, called
+// in place c == a at allreduce.cc:301-305).  It is a pure HBM stream: 12 B per fp32 element
+// (read a, read b, write c), no reuse, no MFMA.  Design:
+//   * 16 B per lane per access (global_load_dwordx4 / global_store_dwordx4), wave64 lanes on
+//     consecutive 16-B slots -> every wave-instruction moves 1 KiB, fully coalesced;
+//   * UNROLL independent vectors per operand per lane in flight before the first use;
+//   * aligned on the *store* stream c; a and b may sit at any element alignment relative to c
+//     (the ring's tmp slot 1 is at +segmentBytes, a multiple of 4 only: allreduce.cc:236) --
+//     gfx950 runs under unaligned-access mode, so under-aligned 16-B loads stay dwordx4;
+//   * the ragged head (until c is 16-B aligned) and tail (< one vector) are done lane-per-element
+//     by two wavefronts of block 0, so the vector loop carries no per-element predicate;
+//   * a grid-stride loop over contiguous tiles; the launcher picks the grid from the size.
+// Numerics reproduce the reference's x86 build bit for bit: IEEE RNE, subnormals
+// kept (no FTZ), x86 NaN propagation (first NaN operand quieted, else default NaN 0xFFC00000),
+// integer wrap, and gloo::float16's store quirk.
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "reduce_kernels.h"
+
+namespace hydra {
+namespace {
+
+// -------------------------------------------------------------------------------------------
+// element ops
+// -------------------------------------------------------------------------------------------
+struct f16_t { uint16_t x; };
+struct bf16_t { uint16_t x; };
+
+__device__ __forceinline__ uint32_t fbits(float f) { return __builtin_bit_cast(uint32_t, f); }
+__device__ __forceinline__ float bitsf(uint32_t u) { return __builtin_bit_cast(float, u); }
+__device__ __forceinline__ uint64_t dbits(double f) { return __builtin_bit_cast(uint64_t, f); }
+__device__ __forceinline__ double bitsd(uint64_t u) { return __builtin_bit_cast(double, u); }
+
+// x86 SSE NaN result of a binary arithmetic op: first NaN operand, quieted; else default NaN.
+__device__ __forceinline__ float x86_nan(float a, float b) {
+  if (a != a) return bitsf(fbits(a) | 0x00400000u);
+  if (b != b) return bitsf(fbits(b) | 0x00400000u);
+  return bitsf(0xFFC00000u);
+}
+__device__ __forceinline__ double x86_nan(double a, double b) {
+  if (a != a) return bitsd(dbits(a) | 0x0008000000000000ull);
+  if (b != b) return bitsd(dbits(b) | 0x0008000000000000ull);
+  return bitsd(0xFFF8000000000000ull);
+}
+
+template <int OP, typename T>
+__device__ __forceinline__ T fop(T a, T b) {  // float / double
+  T r;
+  if (OP == kSum) r = a + b;
+  else if (OP == kProduct) r = a * b;
+  else if (OP == kMax) return (a < b) ? b : a;  // std::max operand order (math.h:50-56)
+  else return (b < a) ? b : a;                  // std::min (math.h:64-70)
+  return (r != r) ? x86_nan(a, b) : r;
+}
+
+template <int OP, typename T, typename U>
+__device__ __forceinline__ T iop(T a, T b) {  // integers, modulo 2^bits
+  if (OP == kSum) return (T)((U)a + (U)b);
+  if (OP == kProduct) return (T)((U)a * (U)b);
+  if (OP == kMax) return (a < b) ? b : a;
+  return (b < a) ? b : a;
+}
+
+// gloo::float16 conversions (types.h:207-320): RNE; NaN -> 0x7fff.  The hardware converts
+// exactly like the reference for every non-NaN input (RNE, subnormals, overflow at 65520).
+__device__ __forceinline__ float h2f(uint16_t h) {
+  return (float)__builtin_bit_cast(_Float16, h);
+}
+__device__ __forceinline__ uint16_t f2h(float f) {
+  if (f != f) return 0x7fffu;
+  return __builtin_bit_cast(uint16_t, (_Float16)f);
+}
+// float16::operator= skips the store when new == f2h((float)old_bits) (types.h:112-130).
+__device__ __forceinline__ uint16_t f16_assign(uint16_t old_bits, uint16_t new_bits) {
+  return (new_bits == f2h((float)old_bits)) ? old_bits : new_bits;
+}
+template <int OP>
+__device__ __forceinline__ uint16_t f16op(uint16_t L, uint16_t R, uint16_t C0) {
+  float x = h2f(L), y = h2f(R);
+  uint16_t res;
+  if (OP == kSum) res = f16_assign(L, f2h(x + y));
+  else if (OP == kProduct) res = f16_assign(L, f2h(x * y));
+  else if (OP == kMax) res = (x < y) ? R : L;
+  else res = (y < x) ? R : L;
+  return f16_assign(C0, res);
+}
+
+// bf16: fp32 compute (x86 NaN rules), RNE back, NaN kept quiet (oracle/hydra_oracle.c orc_f2bf)
+__device__ __forceinline__ float bf2f(uint16_t h) { return bitsf((uint32_t)h << 16); }
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  uint32_t u = fbits(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40u);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+template <int OP>
+__device__ __forceinline__ uint16_t bf16op(uint16_t a, uint16_t b) {
+  float x = bf2f(a), y = bf2f(b);
+  if (OP == kMax) return (x < y) ? b : a;
+  if (OP == kMin) return (y < x) ? b : a;
+  return f2bf(fop<OP>(x, y));
+}
+
+// Uniform element interface: E = storage type; apply(L, R, C0).
+template <typename E, int OP> struct Elem;
+#define HYDRA_IELEM(E, U)                                                                 \
+  template <int OP> struct Elem<E, OP> {                                                  \
+    static constexpr bool kNeedsOld = false;                                              \
+    __device__ __forceinline__ static E apply(E a, E b, E) { return iop<OP, E, U>(a, b); } \
+  };
+HYDRA_IELEM(int8_t, uint32_t)
+HYDRA_IELEM(uint8_t, uint32_t)
+HYDRA_IELEM(int32_t, uint32_t)
+HYDRA_IELEM(uint32_t, uint32_t)
+HYDRA_IELEM(int64_t, uint64_t)
+HYDRA_IELEM(uint64_t, uint64_t)
+template <int OP> struct Elem<float, OP> {
+  static constexpr bool kNeedsOld = false;
+  __device__ __forceinline__ static float apply(float a, float b, float) { return fop<OP>(a, b); }
+};
+template <int OP> struct Elem<double, OP> {
+  static constexpr bool kNeedsOld = false;
+  __device__ __forceinline__ static double apply(double a, double b, double) {
+    return fop<OP>(a, b);
+  }
+};
+template <int OP> struct Elem<f16_t, OP> {
+  static constexpr bool kNeedsOld = true;
+  __device__ __forceinline__ static f16_t apply(f16_t a, f16_t b, f16_t c0) {
+    return f16_t{f16op<OP>(a.x, b.x, c0.x)};
+  }
+};
+template <int OP> struct Elem<bf16_t, OP> {
+  static constexpr bool kNeedsOld = false;
+  __device__ __forceinline__ static bf16_t apply(bf16_t a, bf16_t b, bf16_t) {
+    return bf16_t{bf16op<OP>(a.x, b.x)};
+  }
+};
+
+// -------------------------------------------------------------------------------------------
+// 16-byte vectors
+// -------------------------------------------------------------------------------------------
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4_u __attribute__((ext_vector_type(4), aligned(1)));  // may be unaligned
+
+template <typename E>
+struct Vec {
+  static constexpr int N = 16 / sizeof(E);
+  union { u32x4 raw; E e[N]; };
+};
+
+template <bool NT>
+__device__ __forceinline__ u32x4 ld_u(const void* p) {  // element-aligned 16-B load
+  if (NT) return __builtin_nontemporal_load(reinterpret_cast<const u32x4_u*>(p));
+  return *reinterpret_cast<const u32x4_u*>(p);
+}
+template <bool NT>
+__device__ __forceinline__ void st_a(void* p, u32x4 v) {  // 16-B aligned store
+  if (NT) __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
+  else *reinterpret_cast<u32x4*>(p) = v;
+}
+
+template <typename E, int OP>
+__device__ __forceinline__ u32x4 vapply(u32x4 ra, u32x4 rb, u32x4 rc) {
+  Vec<E> va, vb, vc, vo;
+  va.raw = ra;
+  vb.raw = rb;
+  vc.raw = rc;
+#pragma unroll
+  for (int k = 0; k < Vec<E>::N; k++) vo.e[k] = Elem<E, OP>::apply(va.e[k], vb.e[k], vc.e[k]);
+  return vo.raw;
+}
+
+// -------------------------------------------------------------------------------------------
+// the streaming kernel
+//   c, a, b   : element pointers at the first element of the vector body (c 16-B aligned)
+//   nvec      : number of 16-B vectors in the body
+//   head/tail : scalar elements before (at c - head) / after the body, each < Vec<E>::N
+//   C_OLD     : load c's old bits (float16 store quirk when c is not a)
+// -------------------------------------------------------------------------------------------
+template <typename E, int OP, int UNROLL, bool NT, bool C_OLD>
+__global__ __launch_bounds__(kBlock) void k_reduce(E* c_, const E* a_, const E* b_,
+                                                   size_t nvec, int head, int tail) {
+  constexpr int N = Vec<E>::N;
+  constexpr size_t TILE = (size_t)kBlock * UNROLL;
+  char* c = reinterpret_cast<char*>(c_);
+  const char* a = reinterpret_cast<const char*>(a_);
+  const char* b = reinterpret_cast<const char*>(b_);
+  const int t = threadIdx.x;
+
+  // ragged edges: wave 0 of block 0 takes the head, wave 1 the tail (one element per lane)
+  if (blockIdx.x == 0) {
+    if (t < head) {
+      const int i = t - head;
+      E ea = a_[i], eb = b_[i];
+      E ec = C_OLD ? c_[i] : ea;
+      c_[i] = Elem<E, OP>::apply(ea, eb, ec);
+    } else if (t >= 64 && t - 64 < tail) {
+      const size_t i = nvec * N + (size_t)(t - 64);
+      E ea = a_[i], eb = b_[i];
+      E ec = C_OLD ? c_[i] : ea;
+      c_[i] = Elem<E, OP>::apply(ea, eb, ec);
+    }
+  }
+
+  const size_t ntiles = (nvec + TILE - 1) / TILE;
+  for (size_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const size_t v0 = tile * TILE + t;
+    if (v0 + (UNROLL - 1) * kBlock < nvec) {  // full tile for this lane: no predicates
+      u32x4 ra[UNROLL], rb[UNROLL], rc[UNROLL];
+#pragma unroll
+      for (int u = 0; u < UNROLL; u++) {
+        const size_t off = (v0 + (size_t)u * kBlock) * 16;
+        ra[u] = ld_u<NT>(a + off);
+        rb[u] = ld_u<NT>(b + off);
+        if (C_OLD) rc[u] = ld_u<NT>(c + off);
+      }
+#pragma unroll
+      for (int u = 0; u < UNROLL; u++) {
+        const size_t off = (v0 + (size_t)u * kBlock) * 16;
+        st_a<NT>(c + off, vapply<E, OP>(ra[u], rb[u], C_OLD ? rc[u] : ra[u]));
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < UNROLL; u++) {
+        const size_t v = v0 + (size_t)u * kBlock;
+        if (v < nvec) {
+          const size_t off = v * 16;
+          u32x4 x = ld_u<NT>(a + off), y = ld_u<NT>(b + off);
+          u32x4 z = C_OLD ? ld_u<NT>(c + off) : x;
+          st_a<NT>(c + off, vapply<E, OP>(x, y, z));
+        }
+      }
+    }
+  }
+}
+
+// -------------------------------------------------------------------------------------------
+// bf16 bucket, fp32 accumulate (BASELINE config 5): acc[i] += float(b[i]); 10 B / element.
+// acc 16-B aligned (we own it), b element-aligned.  8 elements per lane per step.
+// -------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_acc_bf16(float* __restrict__ acc,
+                                                     const uint16_t* __restrict__ b, size_t n) {
+  const size_t stride = (size_t)gridDim.x * kBlock;
+  const size_t n8 = n / 8;
+  for (size_t v = (size_t)blockIdx.x * kBlock + threadIdx.x; v < n8; v += stride) {
+    u32x4 bb = *reinterpret_cast<const u32x4_u*>(b + v * 8);
+    u32x4 a0 = *reinterpret_cast<const u32x4*>(acc + v * 8);
+    u32x4 a1 = *reinterpret_cast<const u32x4*>(acc + v * 8 + 4);
+    Vec<float> x0, x1;
+    x0.raw = a0;
+    x1.raw = a1;
+    x0.e[0] = fop<kSum>(x0.e[0], bitsf(bb[0] << 16));
+    x0.e[1] = fop<kSum>(x0.e[1], bitsf(bb[0] & 0xffff0000u));
+    x0.e[2] = fop<kSum>(x0.e[2], bitsf(bb[1] << 16));
+    x0.e[3] = fop<kSum>(x0.e[3], bitsf(bb[1] & 0xffff0000u));
+    x1.e[0] = fop<kSum>(x1.e[0], bitsf(bb[2] << 16));
+    x1.e[1] = fop<kSum>(x1.e[1], bitsf(bb[2] & 0xffff0000u));
+    x1.e[2] = fop<kSum>(x1.e[2], bitsf(bb[3] << 16));
+    x1.e[3] = fop<kSum>(x1.e[3], bitsf(bb[3] & 0xffff0000u));
+    *reinterpret_cast<u32x4*>(acc + v * 8) = x0.raw;
+    *reinterpret_cast<u32x4*>(acc + v * 8 + 4) = x1.raw;
+  }
+  if (blockIdx.x == 0 && threadIdx.x < (n & 7)) {
+    const size_t i = n8 * 8 + threadIdx.x;
+    acc[i] = fop<kSum>(acc[i], bf2f(b[i]));
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_f32_to_bf16(uint16_t* __restrict__ out,
+                                                        const float* __restrict__ acc, size_t n) {
+  const size_t stride = (size_t)gridDim.x * kBlock;
+  for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride)
+    out[i] = f2bf(acc[i]);
+}
+
+// -------------------------------------------------------------------------------------------
+// launch
+// -------------------------------------------------------------------------------------------
+int g_cu_count = 0;
+
+int cu_count() {
+  if (!g_cu_count) {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
+      g_cu_count = cus;
+    else
+      g_cu_count = 256;
+  }
+  return g_cu_count;
+}
+
+template <typename E, int OP, int UNROLL, bool NT>
+hipError_t launch_t(void* c, const void* a, const void* b, size_t n, hipStream_t s,
+                    int max_blocks) {
+  constexpr int N = Vec<E>::N;
+  const uintptr_t cp = reinterpret_cast<uintptr_t>(c);
+  // elements until c is 16-B aligned
+  int head = (int)(((16 - (cp & 15)) & 15) / sizeof(E));
+  if ((size_t)head > n) head = (int)n;
+  const size_t body = n - head;
+  const size_t nvec = body / N;
+  const int tail = (int)(body - nvec * N);
+  E* cb = reinterpret_cast<E*>(c) + head;
+  const E* ab = reinterpret_cast<const E*>(a) + head;
+  const E* bb = reinterpret_cast<const E*>(b) + head;
+  constexpr size_t TILE = (size_t)kBlock * UNROLL;
+  size_t tiles = (nvec + TILE - 1) / TILE;
+  if (tiles == 0) tiles = 1;
+  size_t grid = tiles;
+  if (max_blocks > 0 && grid > (size_t)max_blocks) grid = (size_t)max_blocks;
+  const bool c_old = Elem<E, OP>::kNeedsOld && c != a;
+  if (c_old)
+    hipLaunchKernelGGL((k_reduce<E, OP, UNROLL, NT, true>), dim3((unsigned)grid), dim3(kBlock), 0,
+                       s, cb, ab, bb, nvec, head, tail);
+  else
+    hipLaunchKernelGGL((k_reduce<E, OP, UNROLL, NT, false>), dim3((unsigned)grid), dim3(kBlock),
+                       0, s, cb, ab, bb, nvec, head, tail);
+  return hipGetLastError();
+}
+
+template <typename E, int OP>
+hipError_t launch_variant(int variant, void* c, const void* a, const void* b, size_t n,
+                          hipStream_t s) {
+  const int cus = cu_count();
+  switch (variant) {
+    case 1: return launch_t<E, OP, 1, false>(c, a, b, n, s, 0);            // 1 vec/lane, no cap
+    case 2: return launch_t<E, OP, 4, false>(c, a, b, n, s, 0);            // 4 vec/lane, no cap
+    case 3: return launch_t<E, OP, 4, false>(c, a, b, n, s, cus * 8);      // persistent x8/CU
+    case 4: return launch_t<E, OP, 4, true>(c, a, b, n, s, 0);             // nontemporal
+    case 5: return launch_t<E, OP, 2, false>(c, a, b, n, s, 0);            // 2 vec/lane
+    case 6: return launch_t<E, OP, 8, false>(c, a, b, n, s, 0);            // 8 vec/lane
+    case 7: return launch_t<E, OP, 4, false>(c, a, b, n, s, cus * 4);      // persistent x4/CU
+    default: return launch_t<E, OP, 4, false>(c, a, b, n, s, 0);
+  }
+}
+
+template <int OP>
+hipError_t dispatch_dtype(int variant, int dtype, void* c, const void* a, const void* b, size_t n,
+                          hipStream_t s) {
+  switch (dtype) {
+    case kI8: return launch_variant<int8_t, OP>(variant, c, a, b, n, s);
+    case kU8: return launch_variant<uint8_t, OP>(variant, c, a, b, n, s);
+    case kI32: return launch_variant<int32_t, OP>(variant, c, a, b, n, s);
+    case kU32: return launch_variant<uint32_t, OP>(variant, c, a, b, n, s);
+    case kI64: return launch_variant<int64_t, OP>(variant, c, a, b, n, s);
+    case kU64: return launch_variant<uint64_t, OP>(variant, c, a, b, n, s);
+    case kF32: return launch_variant<float, OP>(variant, c, a, b, n, s);
+    case kF64: return launch_variant<double, OP>(variant, c, a, b, n, s);
+    case kF16: return launch_variant<f16_t, OP>(variant, c, a, b, n, s);
+    case kBF16: return launch_variant<bf16_t, OP>(variant, c, a, b, n, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+}  // namespace
+
+hipError_t launch_reduce(int variant, int op, int dtype, void* c, const void* a, const void* b,
+                         size_t n, hipStream_t s) {
+  switch (op) {
+    case kSum: return dispatch_dtype<kSum>(variant, dtype, c, a, b, n, s);
+    case kProduct: return dispatch_dtype<kProduct>(variant, dtype, c, a, b, n, s);
+    case kMax: return dispatch_dtype<kMax>(variant, dtype, c, a, b, n, s);
+    case kMin: return dispatch_dtype<kMin>(variant, dtype, c, a, b, n, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_acc_bf16_f32(float* acc, const void* b, size_t n, hipStream_t s) {
+  size_t blocks = (n / 8 + kBlock - 1) / kBlock;
+  const size_t cap = (size_t)cu_count() * 16;
+  if (blocks > cap) blocks = cap;
+  if (blocks == 0) blocks = 1;
+  hipLaunchKernelGGL(k_acc_bf16, dim3((unsigned)blocks), dim3(kBlock), 0, s, acc,
+                     reinterpret_cast<const uint16_t*>(b), n);
+  return hipGetLastError();
+}
+
+hipError_t launch_f32_to_bf16(void* out, const float* acc, size_t n, hipStream_t s) {
+  size_t blocks = (n + kBlock - 1) / kBlock;
+  const size_t cap = (size_t)cu_count() * 16;
+  if (blocks > cap) blocks = cap;
+  if (blocks == 0) blocks = 1;
+  hipLaunchKernelGGL(k_f32_to_bf16, dim3((unsigned)blocks), dim3(kBlock), 0, s,
+                     reinterpret_cast<uint16_t*>(out), acc, n);
+  return hipGetLastError();
+}
+
+}  // namespace hydra

@@ -1,0 +1,121 @@
+/*
+ * hydra_hip.h -- C-ABI of the MI355X (gfx950) bucket-reduction hot path.
+ *
+ * libhydra_hip.so replaces the element-wise reduction that hydra/Gloo folds into every arriving
+ * ring segment (new_allreduce_ring / bew_allreduce_a).  Plain C: pointers, sizes, ints; no HIP or
+ * torch types in any signature (streams are opaque `hydra_stream_t` = hipStream_t).
+ *
+ * Every entry point returns 0 (HYDRA_OK) or a hydra_status_t; the message of the last failure on
+ * the calling thread is hydra_last_error().  The C++ shim include/hydra/gloo_reduce.h turns
+ * non-zero codes into exceptions, matching the reference's GLOO_ENFORCE -> gloo::EnforceNotMet
+ * (gloo/gloo/common/logging.h:21,42) error model.
+ *
+ * Reference interfaces replaced (file:line under /root/reference):
+ *   hydra_reduce / hydra_chunk_sum
+ *       gloo::sum<T>(void* c, const void* a, const void* b, size_t n)  gloo/gloo/math.h:15-23
+ *       gloo::product/max/min<T>                                        gloo/gloo/math.h:30-73
+ *       the AllreduceOptions::Func plug-point it is bound to            gloo/gloo/allreduce.h:36,179-181
+ *       (called at gloo/gloo/allreduce.cc:301-305 ring, :61-80 local reduce, :615-621 bcube)
+ *       and cudaSum<T>(T* dst, const T* src, size_t n, stream)          gloo/gloo/cuda.cu:315-336
+ *       as CudaReductionFunction<T>'s device function                    gloo/gloo/cuda.h:286-350
+ *   hydra_reduce_host / hydra_chunk_sum_host
+ *       the same gloo::sum<T> contract on HOST buffers (synchronous, like the reference), the form
+ *       the ring actually hands over: c = out[0]+recvOffset, b = tmp scratch (allreduce.cc:301-305)
+ *   hydra_acc_bf16_f32
+ *       no reference counterpart: fp32 accumulate of a bf16 bucket (BASELINE config 5)
+ *   hydra_ring_plan
+ *       segment geometry of ring()                                      gloo/gloo/allreduce.cc:199-221
+ */
+#ifndef HYDRA_HIP_H_
+#define HYDRA_HIP_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HYDRA_ABI_VERSION 1
+
+typedef enum {
+  HYDRA_INT8 = 0,
+  HYDRA_UINT8 = 1,
+  HYDRA_INT32 = 2,
+  HYDRA_UINT32 = 3,
+  HYDRA_INT64 = 4,
+  HYDRA_UINT64 = 5,
+  HYDRA_FLOAT32 = 6,
+  HYDRA_FLOAT64 = 7,
+  HYDRA_FLOAT16 = 8,  /* gloo::float16 semantics, incl. its store quirk */
+  HYDRA_BFLOAT16 = 9  /* fp32 compute, RNE back to bf16 (no reference counterpart) */
+} hydra_dtype_t;
+
+typedef enum { HYDRA_SUM = 0, HYDRA_PRODUCT = 1, HYDRA_MAX = 2, HYDRA_MIN = 3 } hydra_op_t;
+
+typedef enum {
+  HYDRA_OK = 0,
+  HYDRA_ERR_INVALID = 1,     /* bad argument (dtype, op, misaligned pointer, partial overlap) */
+  HYDRA_ERR_HIP = 2,         /* HIP runtime error (message carries hipGetErrorString) */
+  HYDRA_ERR_UNSUPPORTED = 3, /* op/dtype combination not provided */
+  HYDRA_ERR_NO_DEVICE = 4    /* no gfx950 device visible */
+} hydra_status_t;
+
+typedef void* hydra_stream_t; /* hipStream_t; NULL = the legacy default stream */
+typedef struct hydra_ctx* hydra_ctx_t;
+
+/* ---- library ---------------------------------------------------------------------------- */
+int hydra_abi_version(void);
+const char* hydra_last_error(void);      /* thread-local; "" when the last call succeeded */
+int hydra_device_count(int* count);
+int hydra_device_arch(int device, char* buf, size_t len); /* e.g. "gfx950:sramecc+:xnack-" */
+
+/* ---- device-resident reduction (the hot path) ---------------------------------------------
+ * c[i] = op(a[i], b[i]) for i < n, enqueued on `stream` (asynchronous, graph-capturable: no
+ * allocation, no synchronisation).  Pointers are device (or peer-accessible) addresses aligned
+ * to the element size.  c may equal a or b exactly (the ring always calls c == a); partial
+ * overlap is rejected.  n == 0 is a no-op.  Integer ops wrap modulo 2^bits; float ops round to
+ * nearest even with subnormals kept, and NaNs propagate as on the reference's x86 build.      */
+int hydra_reduce(int op, int dtype, void* c, const void* a, const void* b, size_t n,
+                 hydra_stream_t stream);
+int hydra_chunk_sum(int dtype, void* c, const void* a, const void* b, size_t n,
+                    hydra_stream_t stream);
+
+/* Mixed-precision bucket (BASELINE config 5): acc[i] = acc[i] + (float)b_bf16[i]. */
+int hydra_acc_bf16_f32(float* acc, const void* b_bf16, size_t n, hydra_stream_t stream);
+/* out_bf16[i] = bf16_rne(acc[i]) */
+int hydra_f32_to_bf16(void* out_bf16, const float* acc, size_t n, hydra_stream_t stream);
+
+/* Kernel variant selection for measurement (0 = tuned default).  Returns the previous value. */
+int hydra_set_variant(int variant);
+
+/* ---- host-resident reduction --------------------------------------------------------------
+ * Same contract on HOST buffers, synchronous like gloo::sum<T>: the context stages a and b to
+ * the device, reduces, and copies c back, pipelined in chunks over two HIP streams.  One
+ * context per calling thread (bew_allreduce_a runs two rails concurrently: one context each). */
+int hydra_ctx_create(int device, hydra_ctx_t* out);
+int hydra_ctx_destroy(hydra_ctx_t ctx);
+int hydra_reduce_host(hydra_ctx_t ctx, int op, int dtype, void* c, const void* a, const void* b,
+                      size_t n);
+int hydra_chunk_sum_host(hydra_ctx_t ctx, int dtype, void* c, const void* a, const void* b,
+                         size_t n);
+/* Page-lock caller memory so staging copies run at full PCIe rate (optional, idempotent). */
+int hydra_host_register(void* ptr, size_t bytes);
+int hydra_host_unregister(void* ptr);
+
+/* ---- streams / memory helpers for C callers (the Python layer uses torch instead) -------- */
+int hydra_stream_create(int device, hydra_stream_t* out);
+int hydra_stream_destroy(hydra_stream_t s);
+int hydra_stream_synchronize(hydra_stream_t s);
+int hydra_malloc(int device, size_t bytes, void** out);
+int hydra_free(void* p);
+int hydra_memcpy(void* dst, const void* src, size_t bytes); /* hipMemcpyDefault, synchronous */
+
+/* ---- ring geometry (allreduce.cc:199-221), shared by the host ring and the xGMI ring ----- */
+void hydra_ring_plan(int P, size_t n, size_t esize, size_t max_segment, size_t* num_segments,
+                     size_t* segment_bytes, size_t* segments_per_rank);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HYDRA_HIP_H_ */

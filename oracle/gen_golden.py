@@ -1,0 +1,179 @@
+#!/usr/bin/env python3
+"""oracle/gen_golden.py -- TEST INFRASTRUCTURE ONLY.
+
+Regenerates tests/golden/* from the REFERENCE ITSELF (oracle/_ref/libgloo_ref.so, built from
+/root/reference/gloo by oracle/Makefile).  Run in the survey/build container, where
+/root/reference exists:
+
+    make -C oracle all && python3 oracle/gen_golden.py
+
+Fixtures are data only (inputs + the reference's outputs); inputs for the ring cases come from
+hydra_amd.synth (deterministic integer hashing), so only their sha256 is stored next to the
+reference outputs.
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[0] = ROOT  # run as a script from oracle/: import the package, not oracle.py
+
+from hydra_amd import synth  # noqa: E402
+from oracle import oracle as O  # noqa: E402
+
+GOLD = os.path.join(ROOT, "tests", "golden")
+
+REF_TYPES = {  # name -> (numpy dtype, hydra dtype code)
+    "i8": (np.int8, 0), "u8": (np.uint8, 1), "i32": (np.int32, 2), "u32": (np.uint32, 3),
+    "i64": (np.int64, 4), "u64": (np.uint64, 5), "f32": (np.float32, 6), "f64": (np.float64, 7),
+    "f16": (np.uint16, 8),
+}
+
+
+def sha(a: np.ndarray) -> str:
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def operands(name: str, n: int, rng: np.random.Generator):
+    dt, _ = REF_TYPES[name]
+    if name in ("f32", "f64"):
+        a = rng.uniform(-1e3, 1e3, n).astype(dt)
+        b = rng.uniform(-1e3, 1e3, n).astype(dt)
+        specials = np.array([0.0, -0.0, np.inf, -np.inf, np.nan, 1e-45 if dt == np.float32
+                             else 5e-324, -1e-40, 3.4e38, -3.4e38, 1.0, 2.0 ** -24], dtype=dt)
+        k = len(specials)
+        a[:k * k] = np.repeat(specials, k)
+        b[:k * k] = np.tile(specials, k)
+    elif name == "f16":
+        vals = rng.uniform(-70000, 70000, n).astype(np.float32)
+        a = np.array([O.f2h(float(v)) for v in vals], dtype=np.uint16)
+        vals = rng.uniform(-1000, 1000, n).astype(np.float32)
+        b = np.array([O.f2h(float(v)) for v in vals], dtype=np.uint16)
+        specials = np.array([0x0000, 0x8000, 0x7C00, 0xFC00, 0x7E00, 0x0001, 0x8001, 0x7BFF,
+                             0xFBFF, 0x3C00, 0x03FF, 0x7D00], dtype=np.uint16)
+        k = len(specials)
+        a[:k * k] = np.repeat(specials, k)
+        b[:k * k] = np.tile(specials, k)
+    else:
+        info = np.iinfo(dt)
+        lo, hi = (max(info.min, -(1 << 20)), min(info.max, 1 << 20)) if info.bits > 16 else \
+            (info.min, info.max)
+        a = rng.integers(lo, hi, n, dtype=np.int64, endpoint=True).astype(dt)
+        b = rng.integers(lo, hi, n, dtype=np.int64, endpoint=True).astype(dt)
+        if info.bits <= 8:  # exercise the reference's narrowing wrap on 8-bit types
+            a[:4] = [info.max, info.min, info.max, info.min]
+            b[:4] = [1, -1 if info.min < 0 else 0, info.max, info.min]
+    return a, b
+
+
+def gen_ops(out: dict, meta: dict) -> None:
+    rng = np.random.default_rng(20240212)
+    n = 1000
+    for name, (dt, code) in REF_TYPES.items():
+        a, b = operands(name, n, rng)
+        out[f"ops_{name}_a"] = a
+        out[f"ops_{name}_b"] = b
+        for kind in ("sum", "product", "max", "min"):
+            if kind == "product" and name == "i32":
+                # signed overflow is UB in the reference: keep |a*b| < 2^31 for int32
+                pa, pb = (a % 40000).astype(dt), (b % 40000).astype(dt)
+                out[f"ops_{name}_pa"], out[f"ops_{name}_pb"] = pa, pb
+                out[f"ops_{name}_{kind}"] = O.op(pa, pb, kind, code, lib="ref")
+                continue
+            c = O.op(a, b, kind, code, lib="ref")
+            out[f"ops_{name}_{kind}"] = c
+    meta["ops_n"] = n
+
+
+RING_CASES = [(P, n, ms) for P in (1, 2, 3, 4, 5, 7, 8) for n in (1, 7, 100, 1000, 4099)
+              for ms in (128, 1 << 20)]
+RING_BIG = [(2, 262145, 1 << 20), (3, 262145, 1 << 20), (8, 262145, 1 << 20),
+            (4, 1048577, 1 << 20), (8, 1048576 + 12345, 1 << 20), (5, 3000001, 1 << 20)]
+
+
+def gen_ring(out: dict, meta: dict) -> None:
+    rows = []
+    for (P, n, ms) in RING_CASES + RING_BIG:
+        xs = [synth.stress_f32(P, r, n) for r in range(P)]
+        outs = [[x.copy()] for x in xs]
+        O.ref_allreduce(P, outs, None, max_segment=ms)
+        res = outs[0][0]
+        for r in range(1, P):
+            assert np.array_equal(outs[r][0].view(np.uint32), res.view(np.uint32))
+        key = f"ring_f32_P{P}_n{n}_ms{ms}"
+        row = {"P": P, "n": n, "max_segment": ms, "inputs_sha256": sha(np.stack(xs)),
+               "output_sha256": sha(res), "key": key}
+        if n <= 4099:
+            out[key] = res
+        else:
+            out[key + "_head"] = res[:1024]
+            out[key + "_tail"] = res[-1024:]
+        rows.append(row)
+    # int32 stress (wraps never happen: |x| < 2^20, P <= 8)
+    for (P, n) in [(2, 1000), (3, 1000), (8, 1000), (7, 4099)]:
+        xs = [synth.int32_bucket(P, r, n) for r in range(P)]
+        outs = [[x.copy()] for x in xs]
+        O.ref_allreduce(P, outs, None, max_segment=128)
+        key = f"ring_i32_P{P}_n{n}"
+        out[key] = outs[0][0]
+        rows.append({"P": P, "n": n, "max_segment": 128, "key": key,
+                     "inputs_sha256": sha(np.stack(xs)), "output_sha256": sha(outs[0][0])})
+    meta["ring"] = rows
+
+
+def gen_new_test(meta: dict) -> None:
+    """AllreduceNewTest.Default (test/allreduce_test.cc:302-362): confirm the reference meets the
+    closed form k*stride^2 + stride(stride-1)/2 for uint64, every combination we test."""
+    checked = 0
+    for P in (1, 2, 4, 7):
+        for nptr in (1, 2, 3):
+            for n in (1, 10, 100, 1000):
+                for inplace in (True, False):
+                    stride = P * nptr
+                    vals = [[(np.arange(n, dtype=np.uint64) * stride + r * nptr + i)
+                             for i in range(nptr)] for r in range(P)]
+                    if inplace:
+                        outs = [[v.copy() for v in vr] for vr in vals]
+                        ins = None
+                    else:
+                        outs = [[np.zeros(n, np.uint64) for _ in range(nptr)] for _ in range(P)]
+                        ins = vals
+                    O.ref_allreduce(P, outs, ins, max_segment=128)
+                    exp = (np.arange(n, dtype=np.uint64) * stride * stride
+                           + np.uint64(stride * (stride - 1) // 2))
+                    for r in range(P):
+                        for i in range(nptr):
+                            assert np.array_equal(outs[r][i], exp), (P, nptr, n, inplace)
+                    checked += 1
+    meta["allreduce_new_test_closed_form_cases"] = checked
+
+
+def main() -> None:
+    if not O.ref_available():
+        raise SystemExit("oracle/_ref/libgloo_ref.so missing: make -C oracle ref")
+    os.makedirs(GOLD, exist_ok=True)
+    out: dict = {}
+    meta: dict = {"generator": "oracle/gen_golden.py",
+                  "reference": "hydra-ppopp2024/hydra snapshot 2025-02-12, gloo core built by "
+                               "oracle/Makefile (g++ -O3 -DNDEBUG)"}
+    gen_ops(out, meta)
+    gen_ring(out, meta)
+    gen_new_test(meta)
+    import ctypes
+    buf = ctypes.create_string_buffer(512)
+    rc = O.ref().ref_allreduce_timeout(10, buf, 512)
+    meta["timeout_probe"] = {"rc": rc, "what": buf.value.decode()}
+    np.savez_compressed(os.path.join(GOLD, "golden.npz"), **out)
+    with open(os.path.join(GOLD, "golden.json"), "w") as f:
+        json.dump(meta, f, indent=1)
+    sz = os.path.getsize(os.path.join(GOLD, "golden.npz"))
+    print(f"wrote {len(out)} arrays ({sz/1e6:.2f} MB) + golden.json")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,366 @@
+/*
+ * oracle/hydra_oracle.c -- TEST INFRASTRUCTURE ONLY.
+ *
+ * A plain-C restatement of the reference's bucket-reduction hot path, used as the checker by
+ * tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg.  It is never linked into,
+ * called by, or substituted for the product (hydra_amd/libhydra_hip.so).
+ *
+ * Pinned against: tests/golden/*.npz, produced by oracle/gen_golden.py from the reference itself
+ * (oracle/_ref/libgloo_ref.so, compiled from /root/reference/gloo sources by oracle/Makefile),
+ * and against the reference's own known-answer tests (tests/test_oracle.py).
+ *
+ * What is restated (reference file:line):
+ *   orc_op            gloo::sum/product/max/min<T>      gloo/gloo/math.h:15-73
+ *   f16 conversions   cpu_float2half_rn/cpu_half2float  gloo/gloo/types.h:207-320
+ *   orc_ring_plan     segment geometry of ring()        gloo/gloo/allreduce.cc:199-221
+ *   orc_allreduce     local reduce + ring RS/AG result  gloo/gloo/allreduce.cc:46-146, 147-422
+ *   orc_split_aa/_ag  bew_allreduce_a rail split        gloo/gloo/pipeallreduce-a.h:137-376
+ * bf16 (dtype 9) has no reference counterpart: c = bf16_rne(float(a) + float(b)) (our spec).
+ */
+#include <math.h>
+#include <stddef.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+enum { D_INT8 = 0, D_UINT8, D_INT32, D_UINT32, D_INT64, D_UINT64, D_FLOAT32, D_FLOAT64,
+       D_FLOAT16, D_BFLOAT16 };
+enum { OP_SUM = 0, OP_PRODUCT = 1, OP_MAX = 2, OP_MIN = 3 };
+
+size_t orc_esize(int dtype) {
+  static const size_t sz[] = {1, 1, 4, 4, 8, 8, 4, 8, 2, 2};
+  return (dtype >= 0 && dtype <= 9) ? sz[dtype] : 0;
+}
+
+/* ---- fp16 exactly as gloo/gloo/types.h:207-320 (RNE, NaN -> 0x7fff / 0x7fffffff) ---- */
+uint16_t orc_f2h(float f) {
+  uint32_t x;
+  memcpy(&x, &f, 4);
+  uint32_t u = x & 0x7fffffffu, sign, exponent, mantissa, shift, lsb, lsb_s1, lsb_m1, rem;
+  if (u > 0x7f800000u) return 0x7fffu;
+  sign = (x >> 16) & 0x8000u;
+  if (u > 0x477fefffu) return (uint16_t)(sign | 0x7c00u);
+  if (u < 0x33000001u) return (uint16_t)sign;
+  exponent = (u >> 23) & 0xffu;
+  mantissa = u & 0x7fffffu;
+  if (exponent > 0x70u) {
+    shift = 13;
+    exponent -= 0x70u;
+  } else {
+    shift = 0x7eu - exponent;
+    exponent = 0;
+    mantissa |= 0x800000u;
+  }
+  lsb = 1u << shift;
+  lsb_s1 = lsb >> 1;
+  lsb_m1 = lsb - 1;
+  rem = mantissa & lsb_m1;
+  mantissa >>= shift;
+  if (rem > lsb_s1 || (rem == lsb_s1 && (mantissa & 1u))) {
+    ++mantissa;
+    if (!(mantissa & 0x3ffu)) {
+      ++exponent;
+      mantissa = 0;
+    }
+  }
+  return (uint16_t)(sign | (exponent << 10) | mantissa);
+}
+
+float orc_h2f(uint16_t h) {
+  uint32_t sign = (h >> 15) & 1u, exponent = (h >> 10) & 0x1fu, mantissa = (uint32_t)(h & 0x3ffu) << 13;
+  if (exponent == 0x1fu) {
+    if (mantissa) { sign = 0; mantissa = 0x7fffffu; }
+    exponent = 0xffu;
+  } else if (!exponent) {
+    if (mantissa) {
+      uint32_t msb;
+      exponent = 0x71u;
+      do {
+        msb = mantissa & 0x400000u;
+        mantissa <<= 1;
+        --exponent;
+      } while (!msb);
+      mantissa &= 0x7fffffu;
+    }
+  } else {
+    exponent += 0x70u;
+  }
+  uint32_t t = (sign << 31) | (exponent << 23) | mantissa;
+  float f;
+  memcpy(&f, &t, 4);
+  return f;
+}
+
+/* bf16: round-to-nearest-even from fp32, NaN kept a (quiet) NaN. */
+uint16_t orc_f2bf(float f) {
+  uint32_t u;
+  memcpy(&u, &f, 4);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40u);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+float orc_bf2f(uint16_t h) {
+  uint32_t u = (uint32_t)h << 16;
+  float f;
+  memcpy(&f, &u, 4);
+  return f;
+}
+
+/* ---- element-wise ops: math.h:15-73.  max/min keep std::max/std::min operand semantics:
+ *      std::max(a,b) = (a < b) ? b : a ;  std::min(a,b) = (b < a) ? b : a.               ---- */
+#define DEF_OPS(NAME, T)                                                                  \
+  static void NAME(int op, T* c, const T* a, const T* b, size_t n) {                      \
+    size_t i;                                                                             \
+    switch (op) {                                                                         \
+      case OP_SUM: for (i = 0; i < n; i++) c[i] = (T)(a[i] + b[i]); break;                \
+      case OP_PRODUCT: for (i = 0; i < n; i++) c[i] = (T)(a[i] * b[i]); break;            \
+      case OP_MAX: for (i = 0; i < n; i++) c[i] = (a[i] < b[i]) ? b[i] : a[i]; break;     \
+      case OP_MIN: for (i = 0; i < n; i++) c[i] = (b[i] < a[i]) ? b[i] : a[i]; break;     \
+    }                                                                                     \
+  }
+DEF_OPS(ops_f32, float)
+DEF_OPS(ops_f64, double)
+
+/* Integer ops wrap modulo 2^bits (the reference's C++ int8/16 promotion + narrowing does this;
+ * for int32/int64 overflow is UB in the reference, fixtures stay in range). */
+#define DEF_IOPS(NAME, T, U)                                                              \
+  static void NAME(int op, T* c, const T* a, const T* b, size_t n) {                      \
+    size_t i;                                                                             \
+    switch (op) {                                                                         \
+      case OP_SUM: for (i = 0; i < n; i++) c[i] = (T)((U)a[i] + (U)b[i]); break;          \
+      case OP_PRODUCT: for (i = 0; i < n; i++) c[i] = (T)((U)a[i] * (U)b[i]); break;      \
+      case OP_MAX: for (i = 0; i < n; i++) c[i] = (a[i] < b[i]) ? b[i] : a[i]; break;     \
+      case OP_MIN: for (i = 0; i < n; i++) c[i] = (b[i] < a[i]) ? b[i] : a[i]; break;     \
+    }                                                                                     \
+  }
+DEF_IOPS(ops_i8, int8_t, uint32_t)
+DEF_IOPS(ops_u8, uint8_t, uint32_t)
+DEF_IOPS(ops_i32, int32_t, uint32_t)
+DEF_IOPS(ops_u32, uint32_t, uint32_t)
+DEF_IOPS(ops_i64, int64_t, uint64_t)
+DEF_IOPS(ops_u64, uint64_t, uint64_t)
+
+/* float16: every op converts to fp32, computes, converts back (types.h:163-228) -- and every
+ * store goes through float16::operator= (types.h:112-118), whose guard `if (rhs != *this)`
+ * resolves to rhs.x == cpu_float2half_rn((float)this->x) (operator!= -> operator==(const int&),
+ * types.h:123-130): the store is SKIPPED when the new bits equal the half of the old bits read
+ * as an integer.  operator+ stores twice (result = lhs; result += rhs: types.h:196-200), then
+ * c[i] = result stores into c.  So the output depends on c's previous bits; in the ring c == a. */
+static uint16_t f16_assign(uint16_t old_bits, uint16_t new_bits) {
+  return (new_bits == orc_f2h((float)old_bits)) ? old_bits : new_bits;
+}
+
+static void ops_f16(int op, uint16_t* c, const uint16_t* a, const uint16_t* b, size_t n) {
+  for (size_t i = 0; i < n; i++) {
+    uint16_t L = a[i], R = b[i], C0 = c[i], res = 0;
+    float x = orc_h2f(L), y = orc_h2f(R);
+    switch (op) {
+      case OP_SUM: res = f16_assign(L, orc_f2h(x + y)); break;
+      case OP_PRODUCT: res = f16_assign(L, orc_f2h(x * y)); break;
+      case OP_MAX: res = (x < y) ? R : L; break;
+      case OP_MIN: res = (y < x) ? R : L; break;
+    }
+    c[i] = f16_assign(C0, res);
+  }
+}
+
+static void ops_bf16(int op, uint16_t* c, const uint16_t* a, const uint16_t* b, size_t n) {
+  for (size_t i = 0; i < n; i++) {
+    float x = orc_bf2f(a[i]), y = orc_bf2f(b[i]);
+    switch (op) {
+      case OP_SUM: c[i] = orc_f2bf(x + y); break;
+      case OP_PRODUCT: c[i] = orc_f2bf(x * y); break;
+      case OP_MAX: c[i] = (x < y) ? b[i] : a[i]; break;
+      case OP_MIN: c[i] = (y < x) ? b[i] : a[i]; break;
+    }
+  }
+}
+
+/* c[i] = op(a[i], b[i]);  c may alias a or b exactly (element-wise, forward order). */
+int orc_op(int op, int dtype, void* c, const void* a, const void* b, size_t n) {
+  switch (dtype) {
+    case D_INT8: ops_i8(op, c, a, b, n); return 0;
+    case D_UINT8: ops_u8(op, c, a, b, n); return 0;
+    case D_INT32: ops_i32(op, c, a, b, n); return 0;
+    case D_UINT32: ops_u32(op, c, a, b, n); return 0;
+    case D_INT64: ops_i64(op, c, a, b, n); return 0;
+    case D_UINT64: ops_u64(op, c, a, b, n); return 0;
+    case D_FLOAT32: ops_f32(op, c, a, b, n); return 0;
+    case D_FLOAT64: ops_f64(op, c, a, b, n); return 0;
+    case D_FLOAT16: ops_f16(op, c, a, b, n); return 0;
+    case D_BFLOAT16: ops_bf16(op, c, a, b, n); return 0;
+  }
+  return 1;
+}
+
+/* Mixed precision accumulate (BASELINE config 5, no reference counterpart):
+ * acc_f32[i] = acc_f32[i] + float(b_bf16[i]). */
+void orc_acc_bf16_f32(float* acc, const uint16_t* b, size_t n) {
+  for (size_t i = 0; i < n; i++) acc[i] = acc[i] + orc_bf2f(b[i]);
+}
+
+/* ---- ring geometry, allreduce.cc:199-221 ---- */
+static size_t round_up(size_t v, size_t m) { size_t r = v % m; return r ? v + m - r : v; }
+
+void orc_ring_plan(int P, size_t n, size_t esize, size_t max_segment, size_t* num_segments,
+                   size_t* segment_bytes, size_t* segments_per_rank) {
+  size_t total = n * esize;
+  size_t per = max_segment / esize;
+  size_t max_seg_bytes = esize * (per > 1 ? per : 1);
+  size_t want = (total + max_seg_bytes - 1) / max_seg_bytes;
+  if (want < (size_t)P * 2) want = (size_t)P * 2;
+  size_t ns = round_up(want, (size_t)P);
+  *num_segments = ns;
+  *segments_per_rank = ns / (size_t)P;
+  *segment_bytes = round_up((total + ns - 1) / ns, esize);
+}
+
+/* ---- allreduce result, allreduce.cc:46-422 ----
+ * ranks: P, each with nptr output buffers (and nptr inputs when in != NULL), layout [rank][ptr].
+ * Local reduce (genLocalReduceFunction, :46-83):
+ *   1 input      -> x_r = in[0]
+ *   >=2 inputs   -> x_r = op(op(in0,in1),in2)...
+ *   no inputs    -> x_r = op(op(out0,out1),out2)...
+ * Ring fold (reduce-scatter, :284-344; recv from rank+1, send to rank-1; c = op(local, recv)):
+ *   segment k is owned by rank q = k / S and ends as
+ *   op(x_q, op(x_{q+1}, ... op(x_{q-2}, x_{q-1})))   (indices mod P)
+ * All-gather + genLocalBroadcastFunction then copy that into every output of every rank.
+ * P == 1 short-circuits to local reduce + broadcast (:129-133).                           */
+int orc_allreduce(int P, int nptr, int op, int dtype, size_t n, void** in, void** out,
+                  size_t max_segment) {
+  size_t es = orc_esize(dtype);
+  if (!es || P < 1 || nptr < 1) return 1;
+  size_t bytes = n * es;
+  unsigned char* x = (unsigned char*)malloc(bytes * (size_t)P + 1);
+  unsigned char* acc = (unsigned char*)malloc(bytes + 1);
+  if (!x || !acc) { free(x); free(acc); return 2; }
+  for (int r = 0; r < P; r++) {
+    unsigned char* xr = x + (size_t)r * bytes;
+    void** src = in ? in + r * nptr : out + r * nptr;
+    if (in && nptr == 1) {
+      memcpy(xr, src[0], bytes);
+    } else {
+      if (in) {
+        /* fn(out0, in0, in1): out0's old bits matter for float16 stores (see ops_f16) */
+        memcpy(xr, out[r * nptr], bytes);
+        orc_op(op, dtype, xr, src[0], src[1], n);
+        for (int i = 2; i < nptr; i++) orc_op(op, dtype, xr, xr, src[i], n);
+      } else {
+        memcpy(xr, src[0], bytes);
+        for (int i = 1; i < nptr; i++) orc_op(op, dtype, xr, xr, src[i], n);
+      }
+    }
+  }
+  if (P == 1) {
+    memcpy(acc, x, bytes);
+  } else {
+    size_t ns, sb, S;
+    orc_ring_plan(P, n, es, max_segment ? max_segment : (1u << 20), &ns, &sb, &S);
+    unsigned char* tmp = (unsigned char*)malloc(sb + 1);
+    if (!tmp) { free(x); free(acc); return 2; }
+    for (size_t k = 0; k < ns; k++) {
+      size_t off = k * sb;
+      if (off >= bytes) break;
+      size_t len = (bytes - off < sb) ? bytes - off : sb;
+      size_t cnt = len / es;
+      int q = (int)(k / S);
+      /* start with x_{q-1}, fold leftwards: acc = op(x_j, acc) for j = q-2, ..., q, each
+       * computed in place on a copy of the local x_j, as the ring does (c == a == local). */
+      memcpy(acc + off, x + (size_t)((q + P - 1) % P) * bytes + off, len);
+      for (int d = P - 2; d >= 0; d--) {
+        int j = (q + d) % P;
+        memcpy(tmp, x + (size_t)j * bytes + off, len);
+        orc_op(op, dtype, tmp, tmp, acc + off, cnt);
+        memcpy(acc + off, tmp, len);
+      }
+    }
+    free(tmp);
+  }
+  for (int r = 0; r < P; r++)
+    for (int i = 0; i < nptr; i++) memcpy(out[r * nptr + i], acc, bytes);
+  free(x);
+  free(acc);
+  return 0;
+}
+
+/* ---- bew_allreduce_a rail split, pipeallreduce-a.h:296-376 (AA, default) and :137-294 (AG,
+ *      env ALLREDUCE_GLEX).  e1 -> rail 1 (opts3/context), e2 -> rail 2 (opts2/context2).   ---- */
+static void split_finish(size_t n, int cout_ele, int w_2, size_t* e1, size_t* e2) {
+  int cout_mode = (int)(n % (size_t)cout_ele);
+  if (cout_mode == 0) *e2 = (size_t)w_2 * n / (size_t)cout_ele;
+  else *e2 = (size_t)w_2 * (n - (size_t)cout_mode) / (size_t)cout_ele;
+  *e1 = n - *e2;
+}
+
+void orc_split_aa(int P, size_t n, size_t* e1, size_t* e2) {
+  int ce, w;
+  if (P == 2) {
+    if (n < 65536) { ce = 1; w = 1; }
+    else if (1048576 < n && n < 2097153) { ce = 100; w = 48; }
+    else { ce = 2; w = 1; }
+  } else if (P == 3) {
+    if (n < 131072) { ce = 1; w = 1; } else { ce = 2; w = 1; }
+  } else if (P == 4) {
+    if (n < 65537) { ce = 1; w = 1; }
+    else if (524287 < n && n < 16777217) { ce = 100; w = 52; }
+    else { ce = 2; w = 1; }
+  } else if (P == 6) {
+    if (n < 65537) { ce = 1; w = 1; } else { ce = 2; w = 1; }
+  } else {
+    if (n < 131072) { ce = 1; w = 1; } else { ce = 2; w = 1; }
+  }
+  split_finish(n, ce, w, e1, e2);
+}
+
+void orc_split_ag(int P, size_t n, size_t* e1, size_t* e2) {
+  int ce = 1, w = 1;
+  if (P == 2) {
+    ce = 100;
+    if (n < 262145) { ce = 1; w = 1; }
+    else if (262144 < n && n < 524289) { ce = 1; w = 1; }
+    else if (524288 < n && n < 1048577) w = 75;
+    else if (1048576 < n && n < 2097153) w = 74;
+    else if (2097152 < n && n < 4194305) w = 72;
+    else if (4194304 < n && n < 8388609) w = 69;
+    else if (8388608 < n && n < 16777217) w = 67;
+    else if (16777216 < n && n < 33554433) w = 65;
+    else if (33554432 < n && n < 67108865) w = 65;
+    else w = 60;
+  } else if (P == 3) {
+    ce = 100;
+    if (n < 524289) { ce = 1; w = 1; }
+    else if (524288 < n && n < 1048577) w = 80;
+    else if (1048576 < n && n < 2097153) { ce = 15; w = 11; }
+    else if (2097152 < n && n < 4194305) w = 70;
+    else if (4194304 < n && n < 8388609) w = 68;
+    else if (8388608 < n && n < 16777217) w = 64;
+    else if (16777216 < n && n < 33554433) w = 65;
+    else if (8388608 < n && n < 67108865) w = 64;
+    else { ce = 2; w = 1; }
+  } else if (P == 4) {
+    ce = 100;
+    if (n < 828344) { ce = 1; w = 1; }
+    else if (828343 < n && n < 1048577) w = 81;
+    else if (1048576 < n && n < 2097153) w = 73;
+    else if (2097152 < n && n < 4194305) w = 70;
+    else if (4194304 < n && n < 8388609) w = 67;
+    else if (8388608 < n && n < 16777217) w = 65;
+    else if (16777216 < n && n < 33554433) w = 65;
+    else if (33554432 < n && n < 67108865) w = 66;
+    else { ce = 2; w = 1; }
+  } else if (P == 6) {
+    ce = 100;
+    if (n < 1048577) { ce = 1; w = 1; }
+    else if (1048576 < n && n < 2097153) w = 73;
+    else if (2097152 < n && n < 4194305) w = 70;
+    else if (4194304 < n && n < 8388609) w = 66;
+    else if (8388608 < n && n < 16777217) w = 66;
+    else if (16777216 < n && n < 33554433) w = 64;
+    else if (33554432 < n && n < 67108865) w = 66;
+    else { ce = 2; w = 1; }
+  } else {
+    if (n < 6145) { ce = 1; w = 0; }
+    else { ce = 1; w = 1; }
+  }
+  split_finish(n, ce, w, e1, e2);
+}

@@ -1,0 +1,210 @@
+"""oracle/oracle.py -- TEST INFRASTRUCTURE ONLY.
+
+numpy front-end for
+  * ``liboracle.so``          our plain-C restatement of the hot path (oracle/hydra_oracle.c)
+  * ``_ref/libgloo_ref.so``   the reference's own code compiled from /root/reference (Makefile)
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this module; the
+product (hydra_amd) never does.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIBORACLE = os.path.join(HERE, "liboracle.so")
+LIBREF = os.path.join(HERE, "_ref", "libgloo_ref.so")
+
+DTYPES = {  # hydra_dtype_t numbering (include/hydra_hip.h)
+    np.dtype(np.int8): 0, np.dtype(np.uint8): 1, np.dtype(np.int32): 2, np.dtype(np.uint32): 3,
+    np.dtype(np.int64): 4, np.dtype(np.uint64): 5, np.dtype(np.float32): 6,
+    np.dtype(np.float64): 7,
+}
+F16, BF16 = 8, 9
+OPS = {"sum": 0, "product": 1, "max": 2, "min": 3}
+
+_c = ctypes.c_size_t
+_vp = ctypes.c_void_p
+
+
+def build(force: bool = False) -> None:
+    """Compile the C restatement (always possible) and, when the reference tree is present,
+    the reference core.  Prebuilt files travel to the GPU box with the repo snapshot."""
+    if force or not os.path.exists(LIBORACLE):
+        subprocess.check_call(["make", "-s", "-C", HERE, "oracle"])
+    if os.path.isdir("/root/reference/gloo") and (force or not os.path.exists(LIBREF)):
+        subprocess.check_call(["make", "-s", "-j8", "-C", HERE, "ref"])
+
+
+def _load(path):
+    if not os.path.exists(path):
+        raise FileNotFoundError(f"{path} not built (run oracle.build())")
+    return ctypes.CDLL(path)
+
+
+_orc = None
+_ref = None
+
+
+def orc():
+    global _orc
+    if _orc is None:
+        _orc = _load(LIBORACLE)
+        _orc.orc_op.argtypes = [ctypes.c_int, ctypes.c_int, _vp, _vp, _vp, _c]
+        _orc.orc_allreduce.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                       _c, _vp, _vp, _c]
+        _orc.orc_ring_plan.argtypes = [ctypes.c_int, _c, _c, _c] + [ctypes.POINTER(_c)] * 3
+        _orc.orc_split_aa.argtypes = [ctypes.c_int, _c, ctypes.POINTER(_c), ctypes.POINTER(_c)]
+        _orc.orc_split_ag.argtypes = _orc.orc_split_aa.argtypes
+        _orc.orc_f2h.argtypes = [ctypes.c_float]
+        _orc.orc_f2h.restype = ctypes.c_uint16
+        _orc.orc_h2f.argtypes = [ctypes.c_uint16]
+        _orc.orc_h2f.restype = ctypes.c_float
+        _orc.orc_acc_bf16_f32.argtypes = [_vp, _vp, _c]
+    return _orc
+
+
+def ref_available() -> bool:
+    return os.path.exists(LIBREF)
+
+
+def ref():
+    global _ref
+    if _ref is None:
+        _ref = _load(LIBREF)
+        _ref.ref_op.argtypes = [ctypes.c_int, ctypes.c_int, _vp, _vp, _vp, _c]
+        _ref.ref_allreduce.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _c,
+                                       _vp, _vp, _c, ctypes.c_int, ctypes.c_long,
+                                       ctypes.c_char_p, _c]
+        _ref.ref_allreduce_timeout.argtypes = [ctypes.c_long, ctypes.c_char_p, _c]
+        _ref.ref_time_op.argtypes = [ctypes.c_int, ctypes.c_int, _vp, _vp, _vp, _c,
+                                     ctypes.c_int, ctypes.c_int]
+        _ref.ref_time_op.restype = ctypes.c_double
+        _ref.ref_bench_ring.argtypes = [ctypes.c_int, _c, ctypes.c_int, ctypes.c_int, _vp,
+                                        ctypes.c_char_p, _c]
+        _ref.ref_float2half.argtypes = [ctypes.c_float]
+        _ref.ref_float2half.restype = ctypes.c_uint16
+    return _ref
+
+
+def _dt(arr: np.ndarray, dtype_code: int | None) -> int:
+    if dtype_code is not None:
+        return dtype_code
+    return DTYPES[arr.dtype]
+
+
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+# ---------------------------------------------------------------- element-wise
+def op(a: np.ndarray, b: np.ndarray, kind: str = "sum", dtype_code: int | None = None,
+       lib: str = "oracle") -> np.ndarray:
+    """c = op(a, b) via the C restatement (lib='oracle') or the reference (lib='ref').
+    c starts as a copy of a: the in-place form the ring uses (allreduce.cc:301-305), which
+    matters for float16, whose stores depend on the destination's old bits (types.h:112-130).
+    fp16/bf16 operands are passed as uint16 bit patterns with dtype_code F16/BF16."""
+    a = np.ascontiguousarray(a)
+    b = np.ascontiguousarray(b)
+    c = a.copy()
+    L = orc() if lib == "oracle" else ref()
+    fn = L.orc_op if lib == "oracle" else L.ref_op
+    rc = fn(OPS[kind], _dt(a, dtype_code), _ptr(c), _ptr(a), _ptr(b), a.size)
+    if rc:
+        raise ValueError(f"unsupported op/dtype rc={rc}")
+    return c
+
+
+def ring_plan(P: int, n: int, esize: int, max_segment: int = 1 << 20):
+    ns, sb, S = _c(), _c(), _c()
+    orc().orc_ring_plan(P, n, esize, max_segment, ctypes.byref(ns), ctypes.byref(sb),
+                        ctypes.byref(S))
+    return ns.value, sb.value, S.value
+
+
+def _allreduce(fn_is_ref, P, outs, ins, kind, dtype_code, max_segment, algorithm=1):
+    """outs/ins: list over ranks of list over pointers of arrays (modified in place)."""
+    nptr = len(outs[0])
+    n = outs[0][0].size
+    code = _dt(outs[0][0], dtype_code)
+    optrs = (_vp * (P * nptr))(*[_ptr(o) for r in outs for o in r])
+    iptrs = (_vp * (P * nptr))(*[_ptr(i) for r in ins for i in r]) if ins is not None else None
+    if fn_is_ref:
+        err = ctypes.create_string_buffer(512)
+        rc = ref().ref_allreduce(P, nptr, OPS[kind], code, n,
+                                 ctypes.cast(iptrs, _vp) if iptrs is not None else None,
+                                 ctypes.cast(optrs, _vp), max_segment, algorithm, 0, err, 512)
+        if rc:
+            raise RuntimeError(f"reference allreduce failed: {err.value.decode()}")
+    else:
+        rc = orc().orc_allreduce(P, nptr, OPS[kind], code, n,
+                                 ctypes.cast(iptrs, _vp) if iptrs is not None else None,
+                                 ctypes.cast(optrs, _vp), max_segment)
+        if rc:
+            raise RuntimeError("oracle allreduce failed")
+    return outs
+
+
+def allreduce(P, outs, ins=None, kind="sum", dtype_code=None, max_segment=1 << 20):
+    """C restatement of gloo::allreduce(RING) over P ranks; returns outs (in place)."""
+    return _allreduce(False, P, outs, ins, kind, dtype_code, max_segment)
+
+
+def ref_allreduce(P, outs, ins=None, kind="sum", dtype_code=None, max_segment=1 << 20,
+                  algorithm=1):
+    """The reference's own gloo::allreduce over P loopback thread-ranks."""
+    return _allreduce(True, P, outs, ins, kind, dtype_code, max_segment, algorithm)
+
+
+def ring_result(xs: list[np.ndarray], max_segment: int = 1 << 20, kind: str = "sum",
+                dtype_code: int | None = None) -> np.ndarray:
+    """Convenience: reduced bucket of in-place single-pointer ranks xs (not modified)."""
+    outs = [[x.copy()] for x in xs]
+    allreduce(len(xs), outs, None, kind, dtype_code, max_segment)
+    return outs[0][0]
+
+
+def split_aa(P: int, n: int):
+    e1, e2 = _c(), _c()
+    orc().orc_split_aa(P, n, ctypes.byref(e1), ctypes.byref(e2))
+    return e1.value, e2.value
+
+
+def split_ag(P: int, n: int):
+    e1, e2 = _c(), _c()
+    orc().orc_split_ag(P, n, ctypes.byref(e1), ctypes.byref(e2))
+    return e1.value, e2.value
+
+
+def acc_bf16_f32(acc: np.ndarray, b_bits: np.ndarray) -> np.ndarray:
+    acc = np.ascontiguousarray(acc, dtype=np.float32).copy()
+    b_bits = np.ascontiguousarray(b_bits, dtype=np.uint16)
+    orc().orc_acc_bf16_f32(_ptr(acc), _ptr(b_bits), acc.size)
+    return acc
+
+
+def f2h(x: float) -> int:
+    return orc().orc_f2h(x)
+
+
+def h2f(h: int) -> float:
+    return orc().orc_h2f(h)
+
+
+# ---------------------------------------------------------------- timing (cpu_baseline)
+def ref_time_sum(dtype_code: int, c: np.ndarray, a: np.ndarray, b: np.ndarray, iters: int,
+                 reps: int) -> float:
+    """Seconds per call of the reference's gloo::sum<T> (single thread, best of reps)."""
+    return ref().ref_time_op(0, dtype_code, _ptr(c), _ptr(a), _ptr(b), a.size, iters, reps)
+
+
+def ref_bench_ring(P: int, n: int, warmup: int, iters: int) -> np.ndarray:
+    s = np.zeros(iters, dtype=np.float64)
+    err = ctypes.create_string_buffer(512)
+    rc = ref().ref_bench_ring(P, n, warmup, iters, _ptr(s), err, 512)
+    if rc:
+        raise RuntimeError(err.value.decode())
+    return s

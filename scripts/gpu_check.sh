@@ -1,0 +1,43 @@
+#!/bin/bash
+# One GPU-box session: parity tests, bench, rocprofv3 kernel trace + PMC passes.
+# Every GPU step runs under its own timeout; a crash/timeout/abort ends the script there.
+# Usage (via gpurun): bash scripts/gpu_check.sh [tag]
+set -u
+TAG=${1:-r01}
+ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$ROOT/gpurun_out/$TAG
+mkdir -p "$OUT"
+cd "$ROOT"
+
+fatal() {  # exit codes that mean the GPU step crashed or hung: stop everything
+  case $1 in 124|137|134|139|143) echo "FATAL step $2 rc=$1" | tee -a "$OUT/status"; exit $1;; esac
+}
+step() {  # step NAME TIMEOUT CMD...
+  local name=$1 t=$2; shift 2
+  echo "== $name: $*" >> "$OUT/status"
+  timeout -k 10 "$t" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "   rc=$rc" >> "$OUT/status"
+  fatal $rc "$name"
+  return $rc
+}
+
+rocminfo 2>/dev/null | grep -m2 -E "gfx|Marketing" > "$OUT/device.txt" || true
+nproc > "$OUT/host.txt"; grep -m1 "model name" /proc/cpuinfo >> "$OUT/host.txt" || true
+
+if [ "${SKIP_TESTS:-0}" != "1" ]; then
+  step pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider
+fi
+step bench 600 python bench.py --steps 200 --warmup 20 ${BENCH_ARGS:-}
+cp "$OUT/bench.log" "$OUT/bench.json" 2>/dev/null
+
+if [ "${SKIP_PROF:-0}" != "1" ]; then
+  export TMPDIR=/tmp
+  step rocprof_kt 600 rocprofv3 --kernel-trace --stats --output-format csv \
+      -d "$OUT/prof_kt" -o run -- python3 "$ROOT/bench.py" --steps 100 --warmup 10 --no-cpu-baseline
+  step rocprof_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv \
+      -d "$OUT/prof_fetch" -o run -- python3 "$ROOT/bench.py" --steps 20 --warmup 2 --no-cpu-baseline
+  step rocprof_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv \
+      -d "$OUT/prof_write" -o run -- python3 "$ROOT/bench.py" --steps 20 --warmup 2 --no-cpu-baseline
+fi
+echo done >> "$OUT/status"

@@ -1,0 +1,57 @@
+"""Shared test setup.  `-m gpu` tests need a real MI355X; everything else runs on CPU."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU")
+    config.addinivalue_line("markers", "slow: long-running")
+
+
+@pytest.fixture(scope="session")
+def golden():
+    return np.load(os.path.join(GOLDEN, "golden.npz"), allow_pickle=False)
+
+
+@pytest.fixture(scope="session")
+def golden_meta():
+    import json
+
+    with open(os.path.join(GOLDEN, "golden.json")) as f:
+        return json.load(f)
+
+
+@pytest.fixture(scope="session")
+def O():
+    """The oracle (test infrastructure): C restatement + (when built) the reference itself."""
+    from oracle import oracle
+
+    oracle.build()
+    return oracle
+
+
+@pytest.fixture(scope="session")
+def gpu():
+    """cuda:0 with libhydra_hip.so loaded; the HIP path must be the one that runs."""
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from hydra_amd import _lib
+
+    L = _lib.lib()
+    import ctypes
+
+    buf = ctypes.create_string_buffer(128)
+    _lib.check(L.hydra_device_arch(0, buf, 128))
+    assert buf.value.decode().startswith("gfx950"), buf.value
+    return torch.device("cuda", 0)

@@ -1,0 +1,76 @@
+"""C-ABI boundary checks that need no GPU: the library loads, exports exactly what
+include/hydra_hip.h declares, validates arguments before touching HIP, and computes the ring
+geometry of allreduce.cc:199-221 identically to the oracle."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from hydra_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_functions():
+    txt = open(os.path.join(ROOT, "include", "hydra_hip.h")).read()
+    return sorted(set(re.findall(r"\b(hydra_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_header_symbols_exported():
+    declared = header_functions()
+    assert set(declared) == set(_lib.EXPORTS), set(declared) ^ set(_lib.EXPORTS)
+    out = subprocess.check_output(["nm", "-D", "--defined-only", _lib.LIB_PATH], text=True)
+    exported = {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
+    missing = [f for f in declared if f not in exported]
+    assert not missing, missing
+    L = _lib.lib()
+    for f in declared:
+        assert hasattr(L, f)
+    assert L.hydra_abi_version() == 1
+
+
+def test_no_hip_types_in_abi():
+    """Plain C at the boundary: no HIP/torch headers or types outside comments."""
+    txt = open(os.path.join(ROOT, "include", "hydra_hip.h")).read()
+    code = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    assert not re.search(r"#include\s*<(hip|torch|c10|ATen)", code)
+    assert not re.search(r"\bhip[A-Z]\w*", code)
+
+
+@pytest.mark.parametrize("op,dtype,rc", [(9, 6, 1), (0, 42, 1), (-1, 6, 1)])
+def test_invalid_args_rejected_before_hip(op, dtype, rc):
+    L = _lib.lib()
+    a = np.zeros(8, np.float32)
+    assert L.hydra_reduce(op, dtype, a.ctypes.data, a.ctypes.data, a.ctypes.data, 8, None) == rc
+    assert L.hydra_last_error()
+
+
+def test_alignment_and_overlap_rejected():
+    L = _lib.lib()
+    buf = np.zeros(64, np.float32)
+    p = buf.ctypes.data
+    assert L.hydra_reduce(0, 6, p + 2, p + 2, p + 2, 4, None) == 1  # not 4-B aligned
+    assert b"aligned" in L.hydra_last_error()
+    assert L.hydra_reduce(0, 6, p + 4, p, p + 128, 8, None) == 1    # c partially overlaps a
+    assert b"overlap" in L.hydra_last_error()
+    assert L.hydra_reduce(0, 6, p, p, p, 0, None) == 0               # n == 0: no-op, no HIP
+
+
+@pytest.mark.parametrize("P", [1, 2, 3, 4, 5, 7, 8, 16])
+def test_ring_plan_matches_oracle(O, P):
+    rng = np.random.default_rng(P)
+    for n in list(rng.integers(1, 1 << 27, 40)) + [1, 2, 3, 100, 262144, 1 << 26, (1 << 28) + 3]:
+        for es in (1, 2, 4, 8):
+            for ms in (128, 1000, 1 << 20):
+                assert _lib.ring_plan(P, int(n), es, ms) == O.ring_plan(P, int(n), es, ms)
+
+
+def test_missing_library_fails_loudly(monkeypatch, tmp_path):
+    """No silent fallback: a missing .so raises HydraError."""
+    monkeypatch.setattr(_lib, "LIB_PATH", str(tmp_path / "nope.so"))
+    monkeypatch.setattr(_lib, "_lib", None)
+    with pytest.raises(_lib.HydraError):
+        _lib.lib()

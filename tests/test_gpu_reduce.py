@@ -1,0 +1,292 @@
+"""GPU parity of the HIP chunk-sum (libhydra_hip.so) against the oracle / reference fixtures.
+
+Bar: bit-exact for every dtype (integers, fp32/fp64 incl. inf/NaN/-0/subnormals, gloo float16
+incl. its store quirk).  All calls go through the C-ABI (hydra_reduce / hydra_reduce_host)."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from hydra_amd import _lib, synth
+from hydra_amd.reduce import HostContext
+
+pytestmark = pytest.mark.gpu
+
+TYPES = [("i8", 0, np.int8), ("u8", 1, np.uint8), ("i32", 2, np.int32), ("u32", 3, np.uint32),
+         ("i64", 4, np.int64), ("u64", 5, np.uint64), ("f32", 6, np.float32),
+         ("f64", 7, np.float64), ("f16", 8, np.uint16)]
+KINDS = ["sum", "product", "max", "min"]
+OPC = {"sum": 0, "product": 1, "max": 2, "min": 3}
+
+
+def bits(x):
+    return np.ascontiguousarray(x).view(f"u{x.itemsize}")
+
+
+class Dev:
+    """Raw device byte buffers so tests can place operands at arbitrary byte offsets."""
+
+    def __init__(self, gpu):
+        import torch
+
+        self.torch = torch
+        self.gpu = gpu
+
+    def put(self, arr, off_bytes=0, pad=64):
+        t = self.torch.zeros(arr.nbytes + off_bytes + pad, dtype=self.torch.uint8, device=self.gpu)
+        if arr.nbytes:
+            t[off_bytes:off_bytes + arr.nbytes] = self.torch.from_numpy(
+                np.ascontiguousarray(arr).view(np.uint8).copy()).to(self.gpu)
+        return t, t.data_ptr() + off_bytes
+
+    def get(self, t, off_bytes, like):
+        raw = t[off_bytes:off_bytes + like.nbytes].cpu().numpy()
+        return raw.view(like.dtype).copy()
+
+
+def dev_reduce(dev, kind, code, a, b, c0=None, offs=(0, 0, 0), inplace=True, variant=None):
+    """Run hydra_reduce on device copies; returns c.  inplace: c is a's buffer."""
+    L = _lib.lib()
+    ta, pa = dev.put(a, offs[1])
+    tb, pb = dev.put(b, offs[2])
+    if inplace:
+        tc, pc, oc = ta, pa, offs[1]
+    else:
+        tc, pc = dev.put(c0 if c0 is not None else np.zeros_like(a), offs[0])
+        oc = offs[0]
+    prev = None
+    if variant is not None:
+        prev = L.hydra_set_variant(variant)
+    try:
+        _lib.check(L.hydra_reduce(OPC[kind], code, pc, pa, pb, a.size, None))
+    finally:
+        if prev is not None:
+            L.hydra_set_variant(prev)
+    dev.torch.cuda.synchronize()
+    return dev.get(tc, oc, a)
+
+
+@pytest.fixture(scope="module")
+def dev(gpu):
+    return Dev(gpu)
+
+
+@pytest.mark.parametrize("name,code,dt", TYPES)
+@pytest.mark.parametrize("kind", KINDS)
+def test_ops_golden(dev, golden, name, code, dt, kind):
+    """Every type x op against the reference's own outputs (in place, the ring's form)."""
+    if name == "i32" and kind == "product":
+        a, b = golden[f"ops_{name}_pa"], golden[f"ops_{name}_pb"]
+    else:
+        a, b = golden[f"ops_{name}_a"], golden[f"ops_{name}_b"]
+    c = dev_reduce(dev, kind, code, a, b)
+    assert np.array_equal(bits(c), bits(golden[f"ops_{name}_{kind}"]))
+
+
+@pytest.mark.parametrize("kind", KINDS)
+def test_bf16_vs_oracle(dev, O, kind):
+    rng = np.random.default_rng(3)
+    a = synth.bf16_bits(rng.uniform(-100, 100, 3001).astype(np.float32))
+    b = synth.bf16_bits(rng.uniform(-100, 100, 3001).astype(np.float32))
+    a[:4] = [0x7F80, 0xFF80, 0x7FC0, 0x0001]
+    b[:4] = [0xFF80, 0x7F80, 0x3F80, 0x8001]
+    c = dev_reduce(dev, kind, 9, a, b)
+    assert np.array_equal(c, O.op(a, b, kind, 9))
+
+
+SIZES = [0, 1, 2, 3, 4, 5, 7, 8, 15, 16, 17, 31, 33, 63, 64, 65, 255, 256, 257, 1000, 1023,
+         1025, 4097, 65537, 262145]
+
+
+@pytest.mark.parametrize("name,code,dt", [t for t in TYPES if t[0] in ("i8", "i32", "f32",
+                                                                         "f64", "f16")])
+def test_sizes_and_alignment(dev, O, name, code, dt):
+    """Ragged sizes x every relative misalignment of c/a/b (the ring's tmp slot 1 sits at
+    +segmentBytes, a multiple of the element size only: allreduce.cc:236)."""
+    rng = np.random.default_rng(code)
+    es = np.dtype(dt).itemsize
+    for n in SIZES:
+        if dt == np.uint16:
+            a = np.array([O.f2h(float(v)) for v in rng.uniform(-500, 500, n)], np.uint16)
+            b = np.array([O.f2h(float(v)) for v in rng.uniform(-500, 500, n)], np.uint16)
+        elif np.issubdtype(dt, np.integer):
+            a = rng.integers(-100, 100, n).astype(dt)
+            b = rng.integers(-100, 100, n).astype(dt)
+        else:
+            a = rng.standard_normal(n).astype(dt)
+            b = rng.standard_normal(n).astype(dt)
+        exp = O.op(a, b, "sum", code)
+        for offs in [(0, 0, 0), (es, es, es), (0, es, 2 * es), (3 * es, 0, es), (es, 2 * es, 0),
+                     (8, 4 if es <= 4 else 8, 12 if es <= 4 else 16)]:
+            offs = tuple(o - o % es for o in offs)
+            c = dev_reduce(dev, "sum", code, a, b, offs=offs, inplace=True)
+            assert np.array_equal(bits(c), bits(exp)), (n, offs, "inplace")
+            c0 = a.copy()  # out of place with c's old bits == a's (f16 quirk-neutral)
+            c = dev_reduce(dev, "sum", code, a, b, c0=c0, offs=offs, inplace=False)
+            assert np.array_equal(bits(c), bits(exp)), (n, offs, "out of place")
+
+
+def test_f16_out_of_place_old_bits(dev, O):
+    """gloo::float16 output depends on c's previous bits (types.h:112-130): reproduce it."""
+    rng = np.random.default_rng(9)
+    n = 5000
+    a = np.array([O.f2h(float(v)) for v in rng.uniform(-3, 3, n)], np.uint16)
+    b = np.array([O.f2h(float(v)) for v in rng.uniform(-3, 3, n)], np.uint16)
+    c0 = np.arange(n, dtype=np.uint16)
+    a[:300] = [O.f2h(float(v)) for v in rng.integers(0, 4, 300)]  # integer sums 0..6
+    b[:300] = [O.f2h(float(v)) for v in rng.integers(0, 4, 300)]
+    # make the quirk fire: old bits whose f2h((float)bits) equals the new value
+    s = O.op(a, b, "sum", 8)
+    inv = {}
+    for cand in range(65536):
+        inv.setdefault(O.f2h(float(cand)), cand)
+    hits = 0
+    for i in range(300):
+        if int(s[i]) in inv:
+            c0[i] = inv[int(s[i])]
+            hits += 1
+    assert hits > 0
+    exp = c0.copy()
+    O.orc().orc_op(0, 8, exp.ctypes.data, a.ctypes.data, b.ctypes.data, n)
+    c = dev_reduce(dev, "sum", 8, a, b, c0=c0, inplace=False)
+    assert np.array_equal(c, exp)
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7])
+def test_variants_equal(dev, O, variant):
+    rng = np.random.default_rng(variant)
+    for n in (1, 77, 4096 + 3, 1 << 20, (1 << 21) + 5):
+        a = rng.standard_normal(n).astype(np.float32)
+        b = rng.standard_normal(n).astype(np.float32)
+        c = dev_reduce(dev, "sum", 6, a, b, offs=(4, 4, 8), variant=variant)
+        assert np.array_equal(bits(c), bits(O.op(a, b, "sum", 6)))
+
+
+@pytest.mark.parametrize("name,code,dt", [("f32", 6, np.float32), ("i32", 2, np.int32)])
+def test_full_size_64mi(dev, O, name, code, dt):
+    """BASELINE config 2 at its largest size: 64 Mi elements, in place, bit-exact."""
+    n = 64 << 20
+    if dt == np.float32:
+        a = synth.bew_inputs(3, n)
+        b = synth.uniform_f32(n, 42)
+    else:
+        a = synth.int32_bucket(8, 0, n)
+        b = synth.int32_bucket(8, 1, n)
+    c = dev_reduce(dev, "sum", code, a, b)
+    exp = O.op(a, b, "sum", code)
+    assert np.array_equal(bits(c), bits(exp))
+
+
+def test_ring_call_pattern(dev, O):
+    """Drive hydra_reduce exactly as ring() calls opts.reduce (allreduce.cc:301-305): c = a =
+    out + recvOffset, b = tmp + {0, segmentBytes}, n = recvLength / E, for P=2..8 on the stress
+    inputs; every rank's folded block must equal the oracle's ring result."""
+    for P, n, ms in [(2, 100, 1 << 20), (3, 1001, 128), (4, 262145, 1 << 20), (8, 5003, 256)]:
+        xs = [synth.stress_f32(P, r, n) for r in range(P)]
+        exp = O.ring_result(xs, ms)
+        ns, sb, S = _lib.ring_plan(P, n, 4, ms)
+        es = 4
+        total = n * es
+        # each rank's buffer, folded right-to-left exactly as the ring delivers it
+        for q in range(P):
+            out = xs[q].copy()
+            acc = None
+            for k in range(q * S, (q + 1) * S):
+                off = k * sb
+                if off >= total:
+                    break
+                cnt = min(sb, total - off) // es
+                lo = off // es
+                blk = xs[(q + P - 1) % P][lo:lo + cnt].copy()
+                for d in range(P - 2, -1, -1):
+                    j = (q + d) % P
+                    loc = xs[j][lo:lo + cnt].copy()
+                    tmp = np.zeros(2 * sb // es + 1, np.float32)  # tmp scratch, slot k & 1
+                    slot = (k & 1) * (sb // es)
+                    tmp[slot:slot + cnt] = blk
+                    blk = dev_reduce(dev, "sum", 6, loc, tmp[slot:slot + cnt],
+                                     offs=(off % 16, off % 16, (slot * es) % 16))
+                out[lo:lo + cnt] = blk
+                acc = True
+            if acc:
+                lo = q * S * sb // es
+                hi = min(n, (q + 1) * S * sb // es)
+                assert np.array_equal(bits(out[lo:hi]), bits(exp[lo:hi])), (P, n, q)
+
+
+@pytest.mark.parametrize("n", [1, 1000, 3 * (1 << 20) + 7, 9 * (1 << 20)])
+def test_host_path(gpu, O, n):
+    """hydra_reduce_host: host buffers staged H2D -> kernel -> D2H over 8 MiB chunks."""
+    a = synth.stress_f32(2, 0, n)
+    b = synth.stress_f32(2, 1, n)
+    ctx = HostContext(0)
+    try:
+        c = a.copy()
+        _lib.check(_lib.lib().hydra_reduce_host(ctx.handle, 0, 6, c.ctypes.data, c.ctypes.data,
+                                                b.ctypes.data, n))
+        assert np.array_equal(bits(c), bits(O.op(a, b, "sum", 6)))
+        c = np.full(n, 7, np.float32)  # out of place
+        _lib.check(_lib.lib().hydra_reduce_host(ctx.handle, 0, 6, c.ctypes.data, a.ctypes.data,
+                                                b.ctypes.data, n))
+        assert np.array_equal(bits(c), bits(O.op(a, b, "sum", 6)))
+    finally:
+        ctx.close()
+
+
+def test_host_path_f16_quirk(gpu, O):
+    rng = np.random.default_rng(1)
+    n = 20000
+    a = np.array([O.f2h(float(v)) for v in rng.uniform(-3, 3, n)], np.uint16)
+    b = np.array([O.f2h(float(v)) for v in rng.uniform(-3, 3, n)], np.uint16)
+    c = np.zeros(n, np.uint16)
+    exp = c.copy()
+    O.orc().orc_op(0, 8, exp.ctypes.data, a.ctypes.data, b.ctypes.data, n)
+    ctx = HostContext(0)
+    try:
+        _lib.check(_lib.lib().hydra_reduce_host(ctx.handle, 0, 8, c.ctypes.data, a.ctypes.data,
+                                                b.ctypes.data, n))
+    finally:
+        ctx.close()
+    assert np.array_equal(c, exp)
+
+
+def test_acc_bf16_f32(dev, O):
+    """Config 5 building block: fp32 accumulate of a bf16 bucket, then one RNE to bf16."""
+    torch = dev.torch
+    for n in (1, 7, 8, 1000, (1 << 20) + 3):
+        acc = synth.uniform_f32(n, 5) * 3
+        b = synth.bf16_bits(synth.uniform_f32(n, 6))
+        tacc = torch.from_numpy(acc.copy()).to(dev.gpu)
+        tb = torch.from_numpy(b.view(np.int16).copy()).to(dev.gpu)
+        _lib.check(_lib.lib().hydra_acc_bf16_f32(tacc.data_ptr(), tb.data_ptr(), n, None))
+        exp = O.acc_bf16_f32(acc, b)
+        got = tacc.cpu().numpy()
+        assert np.array_equal(bits(got), bits(exp)), n
+        out = torch.zeros(n, dtype=torch.int16, device=dev.gpu)
+        _lib.check(_lib.lib().hydra_f32_to_bf16(out.data_ptr(), tacc.data_ptr(), n, None))
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy().view(np.uint16), synth.bf16_bits(exp))
+
+
+def test_misaligned_pointer_fails_loudly(gpu):
+    import torch
+
+    t = torch.zeros(64, dtype=torch.float32, device=gpu)
+    with pytest.raises(_lib.HydraError):
+        _lib.check(_lib.lib().hydra_reduce(0, 6, t.data_ptr() + 2, t.data_ptr() + 2,
+                                           t.data_ptr() + 2, 4, None))
+
+
+def test_torch_stream_api(gpu, O):
+    """hydra_amd.reduce on torch tensors, on a non-default stream."""
+    import torch
+    from hydra_amd import reduce as R
+
+    a = torch.randn(1 << 16, device=gpu)
+    b = torch.randn(1 << 16, device=gpu)
+    exp = O.op(a.cpu().numpy(), b.cpu().numpy(), "sum", 6)
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        R.sum_(a, a, b)
+    s.synchronize()
+    assert np.array_equal(bits(a.cpu().numpy()), bits(exp))
