@@ -182,7 +182,7 @@ def run_single(args):
     if args.variants:
         var = {}
         for rnd in range(3):
-            for v in range(1, 8):
+            for v in range(0, 20):
                 _, m = time_chunk_sum(torch, L, dev, n, code, 50, 5, variant=v)
                 var.setdefault(v, []).append(float(np.median(m)))
         out["variants_median_ms"] = {str(k): [round(x, 5) for x in v] for k, v in var.items()}

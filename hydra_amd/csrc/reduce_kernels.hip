@@ -36,15 +36,14 @@ __device__ __forceinline__ uint64_t dbits(double f) { return __builtin_bit_cast(
 __device__ __forceinline__ double bitsd(uint64_t u) { return __builtin_bit_cast(double, u); }
 
 // x86 SSE NaN result of a binary arithmetic op: first NaN operand, quieted; else default NaN.
+// Branch-free (selects only): the NaN fix-up must not put execz branches in the stream loop.
 __device__ __forceinline__ float x86_nan(float a, float b) {
-  if (a != a) return bitsf(fbits(a) | 0x00400000u);
-  if (b != b) return bitsf(fbits(b) | 0x00400000u);
-  return bitsf(0xFFC00000u);
+  const uint32_t qa = fbits(a) | 0x00400000u, qb = fbits(b) | 0x00400000u;
+  return bitsf((a != a) ? qa : ((b != b) ? qb : 0xFFC00000u));
 }
 __device__ __forceinline__ double x86_nan(double a, double b) {
-  if (a != a) return bitsd(dbits(a) | 0x0008000000000000ull);
-  if (b != b) return bitsd(dbits(b) | 0x0008000000000000ull);
-  return bitsd(0xFFF8000000000000ull);
+  const uint64_t qa = dbits(a) | 0x0008000000000000ull, qb = dbits(b) | 0x0008000000000000ull;
+  return bitsd((a != a) ? qa : ((b != b) ? qb : 0xFFF8000000000000ull));
 }
 
 template <int OP, typename T>
@@ -153,16 +152,40 @@ struct Vec {
   union { u32x4 raw; E e[N]; };
 };
 
-template <bool NT>
-__device__ __forceinline__ u32x4 ld_u(const void* p) {  // element-aligned 16-B load
-  if (NT) return __builtin_nontemporal_load(reinterpret_cast<const u32x4_u*>(p));
-  return *reinterpret_cast<const u32x4_u*>(p);
+// Memory policies of the 16-B accesses: plain global, global nontemporal ("nt"), or a buffer
+// access with explicit gfx950 cache-policy bits (aux: 1 = sc0, 2 = nt, 16 = sc1).
+enum Pol { kPlain = 0, kNT = 1, kBuf = 0x100 };
+
+template <int POL>
+__device__ __forceinline__ u32x4 ld(const char* base, __amdgpu_buffer_rsrc_t r, uint32_t off) {
+  if constexpr (POL == kNT) {
+    return __builtin_nontemporal_load(reinterpret_cast<const u32x4_u*>(base + off));
+  } else if constexpr (POL & kBuf) {
+    return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, POL & 0xff);
+  } else {
+    return *reinterpret_cast<const u32x4_u*>(base + off);
+  }
 }
-template <bool NT>
-__device__ __forceinline__ void st_a(void* p, u32x4 v) {  // 16-B aligned store
-  if (NT) __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
-  else *reinterpret_cast<u32x4*>(p) = v;
+template <int POL>
+__device__ __forceinline__ void st(char* base, __amdgpu_buffer_rsrc_t r, uint32_t off, u32x4 v) {
+  if constexpr (POL == kNT) {
+    __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(base + off));
+  } else if constexpr (POL & kBuf) {
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, POL & 0xff);
+  } else {
+    *reinterpret_cast<u32x4*>(base + off) = v;
+  }
 }
+template <int POL>
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const char* base, uint32_t bytes) {
+  if constexpr ((POL & kBuf) != 0)
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(base), 0, bytes, 0x00020000);
+  else
+    return __builtin_amdgcn_make_buffer_rsrc(nullptr, 0, 0, 0);
+}
+// plain element-aligned 16-B accesses for the predicated paths
+__device__ __forceinline__ u32x4 ld_u(const void* p) { return *reinterpret_cast<const u32x4_u*>(p); }
+__device__ __forceinline__ void st_a(void* p, u32x4 v) { *reinterpret_cast<u32x4*>(p) = v; }
 
 template <typename E, int OP>
 __device__ __forceinline__ u32x4 vapply(u32x4 ra, u32x4 rb, u32x4 rc) {
@@ -182,7 +205,7 @@ __device__ __forceinline__ u32x4 vapply(u32x4 ra, u32x4 rb, u32x4 rc) {
 //   head/tail : scalar elements before (at c - head) / after the body, each < Vec<E>::N
 //   C_OLD     : load c's old bits (float16 store quirk when c is not a)
 // -------------------------------------------------------------------------------------------
-template <typename E, int OP, int UNROLL, bool NT, bool C_OLD>
+template <typename E, int OP, int UNROLL, int LDP, int STP, bool C_OLD>
 __global__ __launch_bounds__(kBlock) void k_reduce(E* c_, const E* a_, const E* b_,
                                                    size_t nvec, int head, int tail) {
   constexpr int N = Vec<E>::N;
@@ -209,32 +232,123 @@ __global__ __launch_bounds__(kBlock) void k_reduce(E* c_, const E* a_, const E* 
 
   const size_t ntiles = (nvec + TILE - 1) / TILE;
   for (size_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const size_t v0 = tile * TILE + t;
-    if (v0 + (UNROLL - 1) * kBlock < nvec) {  // full tile for this lane: no predicates
+    const size_t tbase = tile * TILE * 16;  // byte offset of this tile
+    if ((tile + 1) * TILE <= nvec) {        // full tile: no predicates
+      const char* at = a + tbase;
+      const char* bt = b + tbase;
+      char* ct = c + tbase;
+      const auto ra_ = rsrc<LDP>(at, TILE * 16), rb_ = rsrc<LDP>(bt, TILE * 16);
+      const auto rc_ = rsrc<LDP>(ct, TILE * 16), wc_ = rsrc<STP>(ct, TILE * 16);
       u32x4 ra[UNROLL], rb[UNROLL], rc[UNROLL];
 #pragma unroll
       for (int u = 0; u < UNROLL; u++) {
-        const size_t off = (v0 + (size_t)u * kBlock) * 16;
-        ra[u] = ld_u<NT>(a + off);
-        rb[u] = ld_u<NT>(b + off);
-        if (C_OLD) rc[u] = ld_u<NT>(c + off);
+        const uint32_t off = (uint32_t)(u * kBlock + t) * 16;
+        ra[u] = ld<LDP>(at, ra_, off);
+        rb[u] = ld<LDP>(bt, rb_, off);
+        if (C_OLD) rc[u] = ld<LDP>(ct, rc_, off);
       }
 #pragma unroll
       for (int u = 0; u < UNROLL; u++) {
-        const size_t off = (v0 + (size_t)u * kBlock) * 16;
-        st_a<NT>(c + off, vapply<E, OP>(ra[u], rb[u], C_OLD ? rc[u] : ra[u]));
+        const uint32_t off = (uint32_t)(u * kBlock + t) * 16;
+        st<STP>(ct, wc_, off, vapply<E, OP>(ra[u], rb[u], C_OLD ? rc[u] : ra[u]));
       }
     } else {
 #pragma unroll
       for (int u = 0; u < UNROLL; u++) {
-        const size_t v = v0 + (size_t)u * kBlock;
+        const size_t v = tile * TILE + (size_t)u * kBlock + t;
         if (v < nvec) {
           const size_t off = v * 16;
-          u32x4 x = ld_u<NT>(a + off), y = ld_u<NT>(b + off);
-          u32x4 z = C_OLD ? ld_u<NT>(c + off) : x;
-          st_a<NT>(c + off, vapply<E, OP>(x, y, z));
+          u32x4 x = ld_u(a + off), y = ld_u(b + off);
+          u32x4 z = C_OLD ? ld_u(c + off) : x;
+          st_a(c + off, vapply<E, OP>(x, y, z));
         }
       }
+    }
+  }
+}
+
+// -------------------------------------------------------------------------------------------
+// LDS-DMA double-buffered variant (the staging the north star names; A/B'd against k_reduce).
+// Each wave streams its own wave-tiles (64 lanes x 16 B x U per operand) with
+// global_load_lds_dwordx4 (nt) into a private 2-deep LDS ring, so no workgroup barrier is
+// needed: the wave's own counted vmcnt orders its ds_reads behind its DMA.  Loads of wave-tile
+// k+1 are in flight while tile k is read back, summed and stored.  Full wave-tiles only; the
+// remainder (< 64*U vectors) is done by the register path of global wave 0.
+// -------------------------------------------------------------------------------------------
+template <int U>
+__device__ __forceinline__ void wait_vm(int k_gt0, int has_next) {
+  // vector-memory ops younger than wave-tile k's loads: stores of k-1 (U) + loads of k+1 (2U)
+  if (k_gt0) {
+    if (has_next) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * U) : "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(U) : "memory");
+  } else {
+    if (has_next) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * U) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+}
+
+template <typename E, int OP, int U, bool C_OLD>
+__global__ __launch_bounds__(kBlock) void k_reduce_lds(E* c_, const E* a_, const E* b_,
+                                                       size_t nvec, int head, int tail) {
+  constexpr int N = Vec<E>::N;
+  constexpr int WT = 64 * U;                  // vectors per wave-tile
+  constexpr int SLOT = 64 * U;                // u32x4 per (buffer, operand) per wave
+  __shared__ u32x4 lds[4][2][2][SLOT];        // [wave][buffer][a|b][..]
+  char* c = reinterpret_cast<char*>(c_);
+  const char* a = reinterpret_cast<const char*>(a_);
+  const char* b = reinterpret_cast<const char*>(b_);
+  const int t = threadIdx.x, lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+
+  if (blockIdx.x == 0) {
+    if (t < head) {
+      const int i = t - head;
+      E ea = a_[i], eb = b_[i];
+      c_[i] = Elem<E, OP>::apply(ea, eb, C_OLD ? c_[i] : ea);
+    } else if (t >= 64 && t - 64 < tail) {
+      const size_t i = nvec * N + (size_t)(t - 64);
+      E ea = a_[i], eb = b_[i];
+      c_[i] = Elem<E, OP>::apply(ea, eb, C_OLD ? c_[i] : ea);
+    }
+  }
+
+  const size_t nwt = nvec / WT;                       // full wave-tiles
+  const size_t gw = (size_t)blockIdx.x * 4 + wave;    // global wave id
+  const size_t GW = (size_t)gridDim.x * 4;
+  using lds_ptr = __attribute__((address_space(3))) void*;
+  auto issue = [&](size_t wt, int buf) {
+    const size_t base = wt * WT * 16;
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const size_t off = base + (size_t)(u * 64 + lane) * 16;
+      __builtin_amdgcn_global_load_lds(a + off, (lds_ptr)&lds[wave][buf][0][u * 64], 16, 0, 2);
+      __builtin_amdgcn_global_load_lds(b + off, (lds_ptr)&lds[wave][buf][1][u * 64], 16, 0, 2);
+    }
+  };
+  size_t wt = gw;
+  int k = 0;
+  if (wt < nwt) issue(wt, 0);
+  for (; wt < nwt; wt += GW, k++) {
+    const int buf = k & 1;
+    const int has_next = (wt + GW < nwt);
+    if (has_next) issue(wt + GW, buf ^ 1);
+    wait_vm<U>(k > 0, has_next);
+    const size_t base = wt * WT * 16;
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const size_t off = base + (size_t)(u * 64 + lane) * 16;
+      u32x4 x = lds[wave][buf][0][u * 64 + lane];
+      u32x4 y = lds[wave][buf][1][u * 64 + lane];
+      u32x4 z = C_OLD ? ld_u(c + off) : x;
+      __builtin_nontemporal_store(vapply<E, OP>(x, y, z), reinterpret_cast<u32x4*>(c + off));
+    }
+  }
+  // remainder vectors (< WT), register path, global wave 0
+  if (gw == 0) {
+    for (size_t v = nwt * WT + lane; v < nvec; v += 64) {
+      const size_t off = v * 16;
+      u32x4 x = ld_u(a + off), y = ld_u(b + off);
+      st_a(c + off, vapply<E, OP>(x, y, C_OLD ? ld_u(c + off) : x));
     }
   }
 }
@@ -295,32 +409,65 @@ int cu_count() {
   return g_cu_count;
 }
 
-template <typename E, int OP, int UNROLL, bool NT>
-hipError_t launch_t(void* c, const void* a, const void* b, size_t n, hipStream_t s,
-                    int max_blocks) {
+struct Split {  // head / vector body / tail of one call, aligned on c
+  int head, tail;
+  size_t nvec;
+};
+
+template <typename E>
+Split split_call(const void* c, size_t n) {
   constexpr int N = Vec<E>::N;
   const uintptr_t cp = reinterpret_cast<uintptr_t>(c);
-  // elements until c is 16-B aligned
-  int head = (int)(((16 - (cp & 15)) & 15) / sizeof(E));
-  if ((size_t)head > n) head = (int)n;
-  const size_t body = n - head;
-  const size_t nvec = body / N;
-  const int tail = (int)(body - nvec * N);
-  E* cb = reinterpret_cast<E*>(c) + head;
-  const E* ab = reinterpret_cast<const E*>(a) + head;
-  const E* bb = reinterpret_cast<const E*>(b) + head;
+  Split s;
+  s.head = (int)(((16 - (cp & 15)) & 15) / sizeof(E));  // elements until c is 16-B aligned
+  if ((size_t)s.head > n) s.head = (int)n;
+  const size_t body = n - s.head;
+  s.nvec = body / N;
+  s.tail = (int)(body - s.nvec * N);
+  return s;
+}
+
+template <typename E, int OP, int UNROLL, int LDP, int STP>
+hipError_t launch_t(void* c, const void* a, const void* b, size_t n, hipStream_t s,
+                    int max_blocks) {
+  const Split sp = split_call<E>(c, n);
+  E* cb = reinterpret_cast<E*>(c) + sp.head;
+  const E* ab = reinterpret_cast<const E*>(a) + sp.head;
+  const E* bb = reinterpret_cast<const E*>(b) + sp.head;
   constexpr size_t TILE = (size_t)kBlock * UNROLL;
-  size_t tiles = (nvec + TILE - 1) / TILE;
+  size_t tiles = (sp.nvec + TILE - 1) / TILE;
   if (tiles == 0) tiles = 1;
   size_t grid = tiles;
   if (max_blocks > 0 && grid > (size_t)max_blocks) grid = (size_t)max_blocks;
   const bool c_old = Elem<E, OP>::kNeedsOld && c != a;
   if (c_old)
-    hipLaunchKernelGGL((k_reduce<E, OP, UNROLL, NT, true>), dim3((unsigned)grid), dim3(kBlock), 0,
-                       s, cb, ab, bb, nvec, head, tail);
+    hipLaunchKernelGGL((k_reduce<E, OP, UNROLL, LDP, STP, true>), dim3((unsigned)grid),
+                       dim3(kBlock), 0, s, cb, ab, bb, sp.nvec, sp.head, sp.tail);
   else
-    hipLaunchKernelGGL((k_reduce<E, OP, UNROLL, NT, false>), dim3((unsigned)grid), dim3(kBlock),
-                       0, s, cb, ab, bb, nvec, head, tail);
+    hipLaunchKernelGGL((k_reduce<E, OP, UNROLL, LDP, STP, false>), dim3((unsigned)grid),
+                       dim3(kBlock), 0, s, cb, ab, bb, sp.nvec, sp.head, sp.tail);
+  return hipGetLastError();
+}
+
+template <typename E, int OP, int U>
+hipError_t launch_lds(void* c, const void* a, const void* b, size_t n, hipStream_t s,
+                      int blocks_per_cu) {
+  const Split sp = split_call<E>(c, n);
+  E* cb = reinterpret_cast<E*>(c) + sp.head;
+  const E* ab = reinterpret_cast<const E*>(a) + sp.head;
+  const E* bb = reinterpret_cast<const E*>(b) + sp.head;
+  size_t wts = sp.nvec / (64 * U);
+  size_t grid = (wts + 3) / 4;
+  const size_t cap = (size_t)cu_count() * blocks_per_cu;
+  if (grid > cap) grid = cap;
+  if (grid == 0) grid = 1;
+  const bool c_old = Elem<E, OP>::kNeedsOld && c != a;
+  if (c_old)
+    hipLaunchKernelGGL((k_reduce_lds<E, OP, U, true>), dim3((unsigned)grid), dim3(kBlock), 0, s,
+                       cb, ab, bb, sp.nvec, sp.head, sp.tail);
+  else
+    hipLaunchKernelGGL((k_reduce_lds<E, OP, U, false>), dim3((unsigned)grid), dim3(kBlock), 0,
+                       s, cb, ab, bb, sp.nvec, sp.head, sp.tail);
   return hipGetLastError();
 }
 
@@ -328,15 +475,28 @@ template <typename E, int OP>
 hipError_t launch_variant(int variant, void* c, const void* a, const void* b, size_t n,
                           hipStream_t s) {
   const int cus = cu_count();
+  constexpr int B = kBuf;
   switch (variant) {
-    case 1: return launch_t<E, OP, 1, false>(c, a, b, n, s, 0);            // 1 vec/lane, no cap
-    case 2: return launch_t<E, OP, 4, false>(c, a, b, n, s, 0);            // 4 vec/lane, no cap
-    case 3: return launch_t<E, OP, 4, false>(c, a, b, n, s, cus * 8);      // persistent x8/CU
-    case 4: return launch_t<E, OP, 4, true>(c, a, b, n, s, 0);             // nontemporal
-    case 5: return launch_t<E, OP, 2, false>(c, a, b, n, s, 0);            // 2 vec/lane
-    case 6: return launch_t<E, OP, 8, false>(c, a, b, n, s, 0);            // 8 vec/lane
-    case 7: return launch_t<E, OP, 4, false>(c, a, b, n, s, cus * 4);      // persistent x4/CU
-    default: return launch_t<E, OP, 4, false>(c, a, b, n, s, 0);
+    case 1: return launch_t<E, OP, 1, kPlain, kPlain>(c, a, b, n, s, 0);
+    case 2: return launch_t<E, OP, 4, kPlain, kPlain>(c, a, b, n, s, 0);
+    case 3: return launch_t<E, OP, 4, kPlain, kPlain>(c, a, b, n, s, cus * 8);
+    case 4: return launch_t<E, OP, 4, kNT, kNT>(c, a, b, n, s, 0);
+    case 5: return launch_t<E, OP, 2, kPlain, kPlain>(c, a, b, n, s, 0);
+    case 6: return launch_t<E, OP, 8, kPlain, kPlain>(c, a, b, n, s, 0);
+    case 7: return launch_t<E, OP, 4, kPlain, kPlain>(c, a, b, n, s, cus * 4);
+    case 8: return launch_t<E, OP, 8, kNT, kNT>(c, a, b, n, s, 0);
+    case 9: return launch_t<E, OP, 2, kNT, kNT>(c, a, b, n, s, 0);
+    case 10: return launch_t<E, OP, 4, kNT, kNT>(c, a, b, n, s, cus * 8);
+    case 11: return launch_t<E, OP, 4, kNT, kPlain>(c, a, b, n, s, 0);
+    case 12: return launch_t<E, OP, 4, kPlain, kNT>(c, a, b, n, s, 0);
+    case 13: return launch_lds<E, OP, 2>(c, a, b, n, s, 5);
+    case 14: return launch_t<E, OP, 4, B | 19, B | 2>(c, a, b, n, s, 0);   // ld sc0 sc1 nt
+    case 15: return launch_t<E, OP, 4, B | 2, B | 18>(c, a, b, n, s, 0);   // st sc1 nt
+    case 16: return launch_t<E, OP, 4, B | 3, B | 3>(c, a, b, n, s, 0);    // sc0 nt both
+    case 17: return launch_t<E, OP, 1, kNT, kNT>(c, a, b, n, s, 0);
+    case 18: return launch_lds<E, OP, 4>(c, a, b, n, s, 2);
+    case 19: return launch_t<E, OP, 4, kNT, kNT>(c, a, b, n, s, cus * 16);
+    default: return launch_t<E, OP, 4, kNT, kNT>(c, a, b, n, s, 0);
   }
 }
 

@@ -1,0 +1,49 @@
+#!/usr/bin/env python3
+"""Interleaved A/B of the chunk-sum kernel variants in ONE process (methodology rule 24).
+Prints a JSON dict: variant -> median kernel us per (size, mode) over rounds."""
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from hydra_amd import _lib  # noqa: E402
+
+L = _lib.lib()
+dev = torch.device("cuda", 0)
+variants = [int(v) for v in os.environ.get("VARIANTS", ",".join(map(str, range(20)))).split(",")]
+sizes = [int(s) for s in os.environ.get("SIZES", str(64 << 20)).split(",")]
+rounds = int(os.environ.get("ROUNDS", "5"))
+reps = int(os.environ.get("REPS", "20"))
+res = {}
+s = torch.cuda.current_stream(dev)
+for n in sizes:
+    a = torch.rand(n, device=dev)
+    b = torch.rand(n, device=dev)
+    c = torch.empty(n, device=dev)
+    for mode in ("inplace", "outofplace"):
+        pc = a.data_ptr() if mode == "inplace" else c.data_ptr()
+        for r in range(rounds):
+            for v in variants:
+                L.hydra_set_variant(v)
+                for _ in range(3):
+                    _lib.check(L.hydra_chunk_sum(6, pc, a.data_ptr(), b.data_ptr(), n, s.cuda_stream))
+                ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                      for _ in range(reps)]
+                for e0, e1 in ev:
+                    e0.record(s)
+                    _lib.check(L.hydra_chunk_sum(6, pc, a.data_ptr(), b.data_ptr(), n, s.cuda_stream))
+                    e1.record(s)
+                torch.cuda.synchronize()
+                t = float(np.median([e0.elapsed_time(e1) for e0, e1 in ev])) * 1e3
+                res.setdefault(f"{n}/{mode}", {}).setdefault(v, []).append(t)
+    del a, b, c
+L.hydra_set_variant(0)
+out = {}
+for k, d in res.items():
+    n = int(k.split("/")[0])
+    out[k] = {v: {"us": round(float(np.median(t)), 2), "min_us": round(float(np.min(t)), 2),
+                  "GBps": round(12 * n / (np.median(t) * 1e-6) / 1e9, 1)} for v, t in d.items()}
+print(json.dumps(out))
