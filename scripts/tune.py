@@ -23,8 +23,9 @@ for n in sizes:
     a = torch.rand(n, device=dev)
     b = torch.rand(n, device=dev)
     c = torch.empty(n, device=dev)
-    for mode in ("inplace", "outofplace"):
-        pc = a.data_ptr() if mode == "inplace" else c.data_ptr()
+    flush = torch.empty(1 << 28, dtype=torch.float32, device=dev)  # 1 GiB: evicts the 256 MiB MALL
+    for mode in os.environ.get("MODES", "inplace,outofplace").split(","):
+        pc = c.data_ptr() if mode == "outofplace" else a.data_ptr()
         for r in range(rounds):
             for v in variants:
                 L.hydra_set_variant(v)
@@ -33,13 +34,15 @@ for n in sizes:
                 ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                       for _ in range(reps)]
                 for e0, e1 in ev:
+                    if mode == "cold":
+                        flush.fill_(1.0)
                     e0.record(s)
                     _lib.check(L.hydra_chunk_sum(6, pc, a.data_ptr(), b.data_ptr(), n, s.cuda_stream))
                     e1.record(s)
                 torch.cuda.synchronize()
                 t = float(np.median([e0.elapsed_time(e1) for e0, e1 in ev])) * 1e3
                 res.setdefault(f"{n}/{mode}", {}).setdefault(v, []).append(t)
-    del a, b, c
+    del a, b, c, flush
 L.hydra_set_variant(0)
 out = {}
 for k, d in res.items():
