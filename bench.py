@@ -43,7 +43,6 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0,
                    help="bounded CPU-baseline sample (seconds of reference gloo::sum work)")
     p.add_argument("--sweep", action="store_true", help="add the 4 Ki..64 Mi size sweep")
-    p.add_argument("--variants", action="store_true", help="A/B all kernel variants (tuning)")
     p.add_argument("--algo", default="auto", help="ring algorithm for N>1 (see hydra_amd.ring)")
     return p.parse_args()
 
@@ -56,8 +55,8 @@ def dist_env():
 
 
 # ------------------------------------------------------------------------------- N = 1
-def time_chunk_sum(torch, L, dev, n, code, steps, warmup, variant=None):
-    """Returns (wall_seconds for `steps` launches, per-launch kernel ms list)."""
+def time_chunk_sum(torch, L, dev, n, code, steps, warmup, variant=None, cold_reps=0):
+    """Returns (wall_seconds for `steps` launches, per-launch kernel ms, cold-cache ms)."""
     from hydra_amd import _lib
     from hydra_amd import synth
 
@@ -90,11 +89,25 @@ def time_chunk_sum(torch, L, dev, n, code, steps, warmup, variant=None):
             e1.record(s)
         torch.cuda.synchronize(dev)
         ms = [e0.elapsed_time(e1) for e0, e1 in ev]
+        # cold: evict the 256 MiB Infinity Cache (1 GiB fill) before each timed launch
+        cold = []
+        if cold_reps:
+            flush = torch.empty(1 << 28, dtype=torch.float32, device=dev)
+            evc = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                   for _ in range(cold_reps)]
+            for e0, e1 in evc:
+                flush.fill_(1.0)
+                e0.record(s)
+                _lib.check(L.hydra_chunk_sum(code, pa, pa, pb, n, sp))
+                e1.record(s)
+            torch.cuda.synchronize(dev)
+            cold = [e0.elapsed_time(e1) for e0, e1 in evc]
+            del flush
     finally:
         if prev is not None:
             L.hydra_set_variant(prev)
     del a, b
-    return wall, ms
+    return wall, ms, cold
 
 
 def pmc_traffic():
@@ -150,7 +163,8 @@ def run_single(args):
     torch.cuda.set_device(dev)
     code = _lib.FLOAT32 if args.dtype == "f32" else _lib.INT32
     n = args.elements
-    wall, ms = time_chunk_sum(torch, L, dev, n, code, args.steps, args.warmup)
+    wall, ms, cold = time_chunk_sum(torch, L, dev, n, code, args.steps, args.warmup,
+                                    cold_reps=20)
     algo_bytes = 12.0 * n
     value = algo_bytes * args.steps / wall / 1e9
     avg_ms = float(np.mean(ms))
@@ -169,23 +183,19 @@ def run_single(args):
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "kernel_ms_avg": round(avg_ms, 5),
                      "kernel_ms_min": round(float(np.min(ms)), 5),
-                     "timing": "HIP events around each launch on the launch stream"},
+                     "timing": "HIP events around each launch on the launch stream",
+                     "cold_achieved": round(algo_bytes / (float(np.median(cold)) * 1e-3) / 1e9, 1),
+                     "cold_note": "median over 20 launches, each after a 1 GiB fill that "
+                                  "evicts the 256 MiB Infinity Cache"},
     }
     if args.sweep:
         sweep = []
         for k in range(12, 27, 2):
             nn = 1 << k
-            w, m = time_chunk_sum(torch, L, dev, nn, code, 200, 20)
+            w, m, _ = time_chunk_sum(torch, L, dev, nn, code, 200, 20)
             sweep.append({"elements": nn, "kernel_us": round(float(np.median(m)) * 1e3, 2),
                           "GBps": round(12.0 * nn / (float(np.median(m)) * 1e-3) / 1e9, 1)})
         out["sweep"] = sweep
-    if args.variants:
-        var = {}
-        for rnd in range(3):
-            for v in range(0, 20):
-                _, m = time_chunk_sum(torch, L, dev, n, code, 50, 5, variant=v)
-                var.setdefault(v, []).append(float(np.median(m)))
-        out["variants_median_ms"] = {str(k): [round(x, 5) for x in v] for k, v in var.items()}
     if not args.no_cpu_baseline:
         try:
             out["cpu_baseline"] = cpu_baseline(n, args.cpu_seconds)
