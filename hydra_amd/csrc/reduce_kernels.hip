@@ -395,6 +395,98 @@ __global__ __launch_bounds__(kBlock) void k_f32_to_bf16(uint16_t* __restrict__ o
 }
 
 // -------------------------------------------------------------------------------------------
+// P-way fold (the DIRECT allreduce's owner step, xgmi_plan.h):
+//   dst = src[0] + (src[1] + (... + (src[P-2] + src[P-1])))
+// with src[0] = this rank's own block (x_q) and src[j] = rank q+j's contribution, i.e. exactly
+// the per-element sequence of c = local + received hops that the reference's ring performs on
+// the owner's block (allreduce.cc:301-305), so the result is bit-identical to the ring.
+// dst may equal src[0].  ACC32: bf16 inputs, fp32 accumulation, one RNE rounding to bf16.
+// -------------------------------------------------------------------------------------------
+struct FoldSrcs {
+  const char* p[kMaxRanks];
+};
+
+template <typename E, int OP, bool ACC32>
+__device__ __forceinline__ u32x4 fold_vec(const FoldSrcs& S, int nsrc, size_t off) {
+  if constexpr (ACC32) {
+    static_assert(sizeof(E) == 2, "ACC32 is the bf16 form");
+    u32x4 last = ld_u(S.p[nsrc - 1] + off);
+    float acc[8];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      acc[2 * k] = bitsf(last[k] << 16);
+      acc[2 * k + 1] = bitsf(last[k] & 0xffff0000u);
+    }
+    for (int j = nsrc - 2; j >= 0; j--) {
+      u32x4 x = ld_u(S.p[j] + off);
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        acc[2 * k] = fop<OP>(bitsf(x[k] << 16), acc[2 * k]);
+        acc[2 * k + 1] = fop<OP>(bitsf(x[k] & 0xffff0000u), acc[2 * k + 1]);
+      }
+    }
+    u32x4 o;
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+      o[k] = (uint32_t)f2bf(acc[2 * k]) | ((uint32_t)f2bf(acc[2 * k + 1]) << 16);
+    return o;
+  } else {
+    u32x4 acc = ld_u(S.p[nsrc - 1] + off);
+    for (int j = nsrc - 2; j >= 0; j--) {
+      u32x4 x = ld_u(S.p[j] + off);
+      acc = vapply<E, OP>(x, acc, x);  // c = local + received, in place on local (C0 = local)
+    }
+    return acc;
+  }
+}
+
+template <typename E, int OP, bool ACC32>
+__device__ __forceinline__ E fold_elem(const FoldSrcs& S, int nsrc, ptrdiff_t i) {
+  if constexpr (ACC32) {
+    float acc = bf2f(reinterpret_cast<const uint16_t*>(S.p[nsrc - 1])[i]);
+    for (int j = nsrc - 2; j >= 0; j--)
+      acc = fop<OP>(bf2f(reinterpret_cast<const uint16_t*>(S.p[j])[i]), acc);
+    E r;
+    uint16_t h = f2bf(acc);
+    __builtin_memcpy(&r, &h, 2);
+    return r;
+  } else {
+    E acc = reinterpret_cast<const E*>(S.p[nsrc - 1])[i];
+    for (int j = nsrc - 2; j >= 0; j--) {
+      const E x = reinterpret_cast<const E*>(S.p[j])[i];
+      acc = Elem<E, OP>::apply(x, acc, x);
+    }
+    return acc;
+  }
+}
+
+// S.p[*] and dst already advanced by `head` elements (dst 16-B aligned at the body).
+template <typename E, int OP, bool ACC32>
+__global__ __launch_bounds__(kBlock) void k_fold(E* dst, FoldSrcs S, int nsrc, size_t nvec,
+                                                 int head, int tail) {
+  constexpr int N = Vec<E>::N;
+  const int t = threadIdx.x;
+  if (blockIdx.x == 0) {
+    if (t < head) {
+      dst[t - head] = fold_elem<E, OP, ACC32>(S, nsrc, (ptrdiff_t)t - head);
+    } else if (t >= 64 && t - 64 < tail) {
+      const ptrdiff_t i = (ptrdiff_t)(nvec * N) + (t - 64);
+      dst[i] = fold_elem<E, OP, ACC32>(S, nsrc, i);
+    }
+  }
+  char* d = reinterpret_cast<char*>(dst);
+  const size_t stride = (size_t)gridDim.x * kBlock;
+  for (size_t vb = (size_t)blockIdx.x * kBlock; vb < nvec; vb += stride) {  // wave-uniform
+    const size_t v = vb + t;
+    // write-through (sc1) store through a block-uniform descriptor, as the chunk-sum default
+    const auto w = __builtin_amdgcn_make_buffer_rsrc(d + vb * 16, 0, kBlock * 16, 0x00020000);
+    if (v < nvec)
+      __builtin_amdgcn_raw_buffer_store_b128(fold_vec<E, OP, ACC32>(S, nsrc, v * 16), w,
+                                             (uint32_t)t * 16, 0, 16);
+  }
+}
+
+// -------------------------------------------------------------------------------------------
 // launch
 // -------------------------------------------------------------------------------------------
 int g_cu_count = 0;
@@ -570,6 +662,59 @@ hipError_t launch_reduce(int variant, int op, int dtype, void* c, const void* a,
     case kProduct: return dispatch_dtype<kProduct>(variant, dtype, c, a, b, n, s);
     case kMax: return dispatch_dtype<kMax>(variant, dtype, c, a, b, n, s);
     case kMin: return dispatch_dtype<kMin>(variant, dtype, c, a, b, n, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+namespace {
+template <typename E, int OP, bool ACC32>
+hipError_t launch_fold_t(void* dst, const void* const* srcs, int nsrc, size_t n, hipStream_t s) {
+  const Split sp = split_call<E>(dst, n);
+  FoldSrcs S;
+  for (int j = 0; j < kMaxRanks; j++)
+    S.p[j] = j < nsrc ? reinterpret_cast<const char*>(srcs[j]) + (size_t)sp.head * sizeof(E)
+                      : nullptr;
+  E* d = reinterpret_cast<E*>(dst) + sp.head;
+  size_t blocks = (sp.nvec + kBlock - 1) / kBlock;
+  const size_t cap = (size_t)cu_count() * 8;
+  if (blocks > cap) blocks = cap;
+  if (blocks == 0) blocks = 1;
+  hipLaunchKernelGGL((k_fold<E, OP, ACC32>), dim3((unsigned)blocks), dim3(kBlock), 0, s, d, S,
+                     nsrc, sp.nvec, sp.head, sp.tail);
+  return hipGetLastError();
+}
+
+template <int OP>
+hipError_t fold_dtype(int dtype, bool acc32, void* dst, const void* const* srcs, int nsrc,
+                      size_t n, hipStream_t s) {
+  if (acc32) {
+    if (dtype != kBF16) return hipErrorInvalidValue;
+    return launch_fold_t<bf16_t, OP, true>(dst, srcs, nsrc, n, s);
+  }
+  switch (dtype) {
+    case kI8: return launch_fold_t<int8_t, OP, false>(dst, srcs, nsrc, n, s);
+    case kU8: return launch_fold_t<uint8_t, OP, false>(dst, srcs, nsrc, n, s);
+    case kI32: return launch_fold_t<int32_t, OP, false>(dst, srcs, nsrc, n, s);
+    case kU32: return launch_fold_t<uint32_t, OP, false>(dst, srcs, nsrc, n, s);
+    case kI64: return launch_fold_t<int64_t, OP, false>(dst, srcs, nsrc, n, s);
+    case kU64: return launch_fold_t<uint64_t, OP, false>(dst, srcs, nsrc, n, s);
+    case kF32: return launch_fold_t<float, OP, false>(dst, srcs, nsrc, n, s);
+    case kF64: return launch_fold_t<double, OP, false>(dst, srcs, nsrc, n, s);
+    case kF16: return launch_fold_t<f16_t, OP, false>(dst, srcs, nsrc, n, s);
+    case kBF16: return launch_fold_t<bf16_t, OP, false>(dst, srcs, nsrc, n, s);
+  }
+  return hipErrorInvalidValue;
+}
+}  // namespace
+
+hipError_t launch_fold(int op, int dtype, bool acc32, void* dst, const void* const* srcs,
+                       int nsrc, size_t n, hipStream_t s) {
+  if (nsrc < 1 || nsrc > kMaxRanks) return hipErrorInvalidValue;
+  switch (op) {
+    case kSum: return fold_dtype<kSum>(dtype, acc32, dst, srcs, nsrc, n, s);
+    case kProduct: return fold_dtype<kProduct>(dtype, acc32, dst, srcs, nsrc, n, s);
+    case kMax: return fold_dtype<kMax>(dtype, acc32, dst, srcs, nsrc, n, s);
+    case kMin: return fold_dtype<kMin>(dtype, acc32, dst, srcs, nsrc, n, s);
   }
   return hipErrorInvalidValue;
 }

@@ -1,0 +1,243 @@
+// xgmi_plan.h -- data-only schedules of the multi-GPU bucket allreduce.
+//
+// A plan is the op list ONE rank executes.  Executors interpret it: the RCCL executor
+// (xgmi_allreduce.cpp) maps SEND/RECV/GROUP onto ncclSend/ncclRecv/ncclGroup* on a comm stream
+// and REDUCE/FOLD onto the HIP kernels on a compute stream; the one-GPU simulator runs every
+// rank's plan in lock-step with device copies standing in for xGMI; tests/ interpret plans on
+// the CPU with numpy.  All three see exactly the same schedule.
+//
+// Block ownership and fold order are the reference's (gloo/gloo/allreduce.cc:147-422):
+//   numSegments / segmentBytes / S from allreduce.cc:199-221 (hydra_ring_plan), block q =
+//   segments [qS, (q+1)S) clipped to the bucket, owned by rank q; its reduced value is
+//   x_q + (x_{q+1} + (... + (x_{q-2} + x_{q-1})))   (indices mod P).
+//
+// Algorithms
+//   RING   the reference's schedule on device: reduce-scatter hop s (s = 0..P-2) sends block
+//          (r+1+s) to r-1 and receives block (r+2+s) from r+1, folding c = local + received
+//          with the HIP sum (allreduce.cc:284-344); all-gather hop s sends block (r+s) to r-1,
+//          receives block (r+1+s) from r+1 (:385-421).  Blocks are cut into chunks so hop s of
+//          chunk c overlaps the sum of chunk c-1.  Uses one xGMI link per direction.
+//   DIRECT MI355X-first: the node is fully connected (7 xGMI links per GPU), so every rank
+//          sends each owner its block in ONE p2p group (all links busy), and the owner folds the
+//          P contributions in the reference's order in ONE kernel (FOLD), then sends its block to
+//          every peer (direct all-gather).  Same per-element arithmetic as RING, so bit-exact.
+#pragma once
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include <algorithm>
+#include <vector>
+
+namespace hydra {
+
+enum PlanKind : int32_t {
+  kOpSend = 1,    // send `bytes` from buffer `buf` at `off` to `peer`
+  kOpRecv = 2,    // receive `bytes` from `peer` into buffer `buf` at `off`
+  kOpGroup = 3,   // end of a p2p group: every SEND/RECV since the previous GROUP is one group
+  kOpReduce = 4,  // user[off .. +bytes] = op(user[off..], scratch[src_off..])          (ring hop)
+  kOpFold = 5,    // user[off..] = fold(user[off..], scratch[src_off + k*slot_stride], k=0..nsrc-2)
+};
+enum PlanBuf : int32_t { kBufUser = 0, kBufScratch = 1 };
+enum Algo : int32_t { kAlgoAuto = 0, kAlgoRing = 1, kAlgoDirect = 2, kAlgoRccl = 3 };
+
+// Mirrored by hydra_plan_op_t in include/hydra_xgmi.h (same layout).
+struct PlanOp {
+  int32_t kind;
+  int32_t peer;
+  int32_t buf;
+  int32_t nsrc;         // FOLD: number of contributions incl. the local one
+  int64_t off;          // user/scratch byte offset (SEND/RECV: in `buf`; REDUCE/FOLD: user dst)
+  int64_t bytes;
+  int64_t src_off;      // REDUCE/FOLD: scratch byte offset of the (first) received operand
+  int64_t slot_stride;  // FOLD: bytes between consecutive contributions in scratch
+  int32_t wait0;        // indices of earlier ops this op must wait for (cross-stream), -1 none
+  int32_t wait1;
+};
+
+struct PlanGeom {
+  int P = 1;
+  size_t n = 0, esize = 4, total = 0;
+  size_t num_segments = 0, segment_bytes = 0, S = 0;
+  size_t chunk = 0;  // pipelining chunk (bytes, multiple of esize and 16)
+  size_t block_begin(int q) const { return std::min(total, (size_t)q * S * segment_bytes); }
+  size_t block_end(int q) const { return std::min(total, (size_t)(q + 1) * S * segment_bytes); }
+  size_t block_bytes(int q) const { return block_end(q) - block_begin(q); }
+  size_t max_block() const {
+    size_t m = 0;
+    for (int q = 0; q < P; q++) m = std::max(m, block_bytes(q));
+    return m;
+  }
+  size_t nchunks() const {  // chunks of the largest block (every block uses this count)
+    const size_t mb = max_block();
+    return mb ? (mb + chunk - 1) / chunk : 0;
+  }
+  // chunk c of block q: [begin, begin+len) relative to the bucket; len may be 0
+  void chunk_of(int q, size_t c, size_t* begin, size_t* len) const {
+    const size_t b = block_begin(q), e = block_end(q);
+    const size_t lo = std::min(e, b + c * chunk), hi = std::min(e, lo + chunk);
+    *begin = lo;
+    *len = hi - lo;
+  }
+};
+
+inline size_t round_up_sz(size_t v, size_t m) {
+  const size_t r = v % m;
+  return r ? v + m - r : v;
+}
+
+// allreduce.cc:199-221
+inline void ring_geometry(int P, size_t n, size_t esize, size_t max_segment, size_t* ns,
+                          size_t* sb, size_t* S) {
+  const size_t total = n * esize;
+  const size_t max_seg_bytes = esize * std::max<size_t>(1, max_segment / esize);
+  *ns = round_up_sz(std::max((total + max_seg_bytes - 1) / max_seg_bytes, (size_t)P * 2),
+                    (size_t)P);
+  *S = *ns / (size_t)P;
+  *sb = round_up_sz((total + *ns - 1) / *ns, esize);
+}
+
+inline PlanGeom make_geom(int P, size_t n, size_t esize, size_t max_segment, size_t chunk) {
+  PlanGeom g;
+  g.P = P;
+  g.n = n;
+  g.esize = esize;
+  g.total = n * esize;
+  ring_geometry(P, n, esize, max_segment ? max_segment : (1u << 20), &g.num_segments,
+                &g.segment_bytes, &g.S);
+  const size_t unit = esize * 16 / std::__gcd(esize, (size_t)16);  // lcm(esize, 16)
+  g.chunk = round_up_sz(std::max<size_t>(chunk ? chunk : (4u << 20), unit), unit);
+  return g;
+}
+
+// Scratch bytes one rank needs for `algo` (wire element size = esize).
+inline size_t plan_scratch_bytes(int algo, const PlanGeom& g) {
+  if (g.P <= 1) return 0;
+  if (algo == kAlgoRing) return 2 * g.chunk;
+  if (algo == kAlgoDirect) return 2 * (size_t)(g.P - 1) * g.chunk;
+  return 0;
+}
+
+class PlanBuilder {
+ public:
+  std::vector<PlanOp> ops;
+  int add(int32_t kind, int32_t peer, int32_t buf, int64_t off, int64_t bytes, int64_t src_off = 0,
+          int64_t slot_stride = 0, int32_t nsrc = 0, int32_t w0 = -1, int32_t w1 = -1) {
+    PlanOp o{kind, peer, buf, nsrc, off, bytes, src_off, slot_stride, w0, w1};
+    ops.push_back(o);
+    return (int)ops.size() - 1;
+  }
+};
+
+// ---- RING ----------------------------------------------------------------------------------
+inline std::vector<PlanOp> plan_ring(const PlanGeom& g, int r) {
+  PlanBuilder pb;
+  const int P = g.P;
+  if (P <= 1 || g.total == 0) return pb.ops;
+  const int send_to = (r + P - 1) % P, recv_from = (r + 1) % P;
+  const size_t C = g.nchunks();
+  // last compute op that wrote chunk c of any block (the block sent next hop), per chunk
+  std::vector<int> wrote(C, -1);
+  int reader[2] = {-1, -1};  // last REDUCE that read scratch slot 0/1
+  size_t k = 0;              // global chunk counter (scratch slot = k & 1)
+  for (int s = 0; s < P - 1; s++) {
+    const int sq = (r + 1 + s) % P, rq = (r + 2 + s) % P;
+    for (size_t c = 0; c < C; c++, k++) {
+      size_t sb, sl, rb, rl;
+      g.chunk_of(sq, c, &sb, &sl);
+      g.chunk_of(rq, c, &rb, &rl);
+      const int slot = (int)(k & 1);
+      const int64_t soff = (int64_t)slot * (int64_t)g.chunk;
+      if (sl == 0 && rl == 0) continue;
+      if (sl) pb.add(kOpSend, send_to, kBufUser, sb, sl);
+      if (rl) pb.add(kOpRecv, recv_from, kBufScratch, soff, rl);
+      // the group sends a chunk the previous hop reduced, and overwrites a scratch slot that an
+      // earlier REDUCE read: wait for both
+      const int grp = pb.add(kOpGroup, -1, 0, 0, 0, 0, 0, 0, s > 0 ? wrote[c] : -1,
+                             reader[slot]);
+      if (rl) {
+        const int red = pb.add(kOpReduce, -1, kBufUser, rb, rl, soff, 0, 2, grp);
+        wrote[c] = red;
+        reader[slot] = red;
+      } else {
+        wrote[c] = -1;
+      }
+    }
+  }
+  // all-gather: pure copies on the comm stream; hop 0 sends the block this rank just folded
+  for (int s = 0; s < P - 1; s++) {
+    const int sq = (r + s) % P, rq = (r + 1 + s) % P;
+    for (size_t c = 0; c < C; c++) {
+      size_t sb, sl, rb, rl;
+      g.chunk_of(sq, c, &sb, &sl);
+      g.chunk_of(rq, c, &rb, &rl);
+      if (sl == 0 && rl == 0) continue;
+      if (sl) pb.add(kOpSend, send_to, kBufUser, sb, sl);
+      if (rl) pb.add(kOpRecv, recv_from, kBufUser, rb, rl);
+      pb.add(kOpGroup, -1, 0, 0, 0, 0, 0, 0, s == 0 ? wrote[c] : -1);
+    }
+  }
+  return pb.ops;
+}
+
+// ---- DIRECT --------------------------------------------------------------------------------
+// Scratch layout per chunk parity p: slot j (j = 1..P-1) at (p*(P-1) + (j-1)) * chunk holds the
+// contribution of rank (r+j)%P to this rank's block, so FOLD reads them in the reference's order.
+inline std::vector<PlanOp> plan_direct(const PlanGeom& g, int r) {
+  PlanBuilder pb;
+  const int P = g.P;
+  if (P <= 1 || g.total == 0) return pb.ops;
+  const size_t C = g.nchunks();
+  int reader[2] = {-1, -1};
+  std::vector<int> folded(C, -1);
+  for (size_t c = 0; c < C; c++) {
+    const int par = (int)(c & 1);
+    const int64_t base = (int64_t)par * (P - 1) * (int64_t)g.chunk;
+    bool any = false;
+    // send my contribution to every other owner q (it lands in q's slot j = (r - q) mod P)
+    for (int d = 1; d < P; d++) {
+      const int q = (r + d) % P;
+      size_t b, l;
+      g.chunk_of(q, c, &b, &l);
+      if (l) { pb.add(kOpSend, q, kBufUser, b, l); any = true; }
+    }
+    size_t mb, ml;
+    g.chunk_of(r, c, &mb, &ml);
+    if (ml) {
+      for (int j = 1; j < P; j++) {
+        const int p = (r + j) % P;
+        pb.add(kOpRecv, p, kBufScratch, base + (int64_t)(j - 1) * (int64_t)g.chunk, ml);
+        any = true;
+      }
+    }
+    if (!any) continue;
+    const int grp = pb.add(kOpGroup, -1, 0, 0, 0, 0, 0, 0, reader[par]);
+    if (ml) {
+      const int f = pb.add(kOpFold, -1, kBufUser, mb, ml, base, (int64_t)g.chunk, P, grp);
+      reader[par] = f;
+      folded[c] = f;
+    }
+  }
+  // direct all-gather, per chunk, as soon as that chunk is folded
+  for (size_t c = 0; c < C; c++) {
+    bool any = false;
+    size_t mb, ml;
+    g.chunk_of(r, c, &mb, &ml);
+    if (ml)
+      for (int d = 1; d < P; d++) { pb.add(kOpSend, (r + d) % P, kBufUser, mb, ml); any = true; }
+    for (int d = 1; d < P; d++) {
+      const int q = (r + d) % P;
+      size_t b, l;
+      g.chunk_of(q, c, &b, &l);
+      if (l) { pb.add(kOpRecv, q, kBufUser, b, l); any = true; }
+    }
+    if (any) pb.add(kOpGroup, -1, 0, 0, 0, 0, 0, 0, folded[c]);
+  }
+  return pb.ops;
+}
+
+inline std::vector<PlanOp> make_plan(int algo, const PlanGeom& g, int r) {
+  return algo == kAlgoRing ? plan_ring(g, r) : plan_direct(g, r);
+}
+
+}  // namespace hydra
