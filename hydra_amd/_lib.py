@@ -29,7 +29,25 @@ EXPORTS = [  # every symbol include/hydra_hip.h declares
     "hydra_chunk_sum_host", "hydra_host_register", "hydra_host_unregister",
     "hydra_stream_create", "hydra_stream_destroy", "hydra_stream_synchronize", "hydra_malloc",
     "hydra_free", "hydra_memcpy", "hydra_ring_plan",
+    "hydra_comm_get_unique_id", "hydra_comm_init", "hydra_comm_destroy", "hydra_allreduce",
+    "hydra_plan", "hydra_allreduce_simulate",
 ]
+
+ALGO_AUTO, ALGO_RING, ALGO_DIRECT, ALGO_RCCL = range(4)
+ALGOS = {"auto": ALGO_AUTO, "ring": ALGO_RING, "direct": ALGO_DIRECT, "rccl": ALGO_RCCL}
+ACC_F32 = 1
+UNIQUE_ID_BYTES = 128
+
+
+class PlanOp(ctypes.Structure):
+    """hydra_plan_op_t (include/hydra_hip.h)."""
+    _fields_ = [("kind", ctypes.c_int32), ("peer", ctypes.c_int32), ("buf", ctypes.c_int32),
+                ("nsrc", ctypes.c_int32), ("off", ctypes.c_int64), ("bytes", ctypes.c_int64),
+                ("src_off", ctypes.c_int64), ("slot_stride", ctypes.c_int64),
+                ("wait0", ctypes.c_int32), ("wait1", ctypes.c_int32)]
+
+
+OP_SEND, OP_RECV, OP_GROUP, OP_REDUCE, OP_FOLD = 1, 2, 3, 4, 5
 
 
 class HydraError(RuntimeError):
@@ -77,6 +95,13 @@ def _declare(L) -> None:
     L.hydra_memcpy.argtypes = [vp, vp, sz]
     L.hydra_ring_plan.argtypes = [i, sz, sz, sz] + [ctypes.POINTER(sz)] * 3
     L.hydra_ring_plan.restype = None
+    L.hydra_comm_get_unique_id.argtypes = [vp]
+    L.hydra_comm_init.argtypes = [ctypes.POINTER(vp), i, i, vp, i]
+    L.hydra_comm_destroy.argtypes = [vp]
+    L.hydra_allreduce.argtypes = [vp, i, i, i, i, vp, sz, sz, sz, vp]
+    L.hydra_plan.argtypes = [i, i, i, sz, sz, sz, sz, ctypes.POINTER(PlanOp), sz,
+                             ctypes.POINTER(sz), ctypes.POINTER(sz)]
+    L.hydra_allreduce_simulate.argtypes = [i, i, i, i, i, ctypes.POINTER(vp), sz, sz, sz]
 
 
 def lib():

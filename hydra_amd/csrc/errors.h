@@ -1,0 +1,18 @@
+// errors.h -- status/message plumbing shared by the C-ABI translation units.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <string>
+
+namespace hydra {
+int ok();                                     // clears the thread's message, returns HYDRA_OK
+int fail(int code, const std::string& msg);   // sets the thread's message, returns code
+int hip_fail(hipError_t e, const char* what);
+int current_variant();
+}  // namespace hydra
+
+#define HIP_TRY(expr)                                           \
+  do {                                                          \
+    hipError_t e__ = (expr);                                    \
+    if (e__ != hipSuccess) return ::hydra::hip_fail(e__, #expr); \
+  } while (0)

@@ -13,32 +13,34 @@
 #include <string>
 
 #include "../../include/hydra_hip.h"
+#include "errors.h"
 #include "reduce_kernels.h"
 
 namespace {
-
 thread_local std::string g_err;
 std::atomic<int> g_variant{0};
+}  // namespace
 
+namespace hydra {
 int ok() {
   g_err.clear();
   return HYDRA_OK;
 }
-
 int fail(int code, const std::string& msg) {
   g_err = msg;
   return code;
 }
-
 int hip_fail(hipError_t e, const char* what) {
   return fail(HYDRA_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
 }
+int current_variant() { return g_variant.load(std::memory_order_relaxed); }
+}  // namespace hydra
 
-#define HIP_TRY(expr)                                   \
-  do {                                                  \
-    hipError_t e__ = (expr);                            \
-    if (e__ != hipSuccess) return hip_fail(e__, #expr); \
-  } while (0)
+using hydra::fail;
+using hydra::hip_fail;
+using hydra::ok;
+
+namespace {
 
 bool overlaps(const void* x, const void* y, size_t bytes) {
   const char* a = static_cast<const char*>(x);

@@ -1,0 +1,477 @@
+// xgmi_allreduce.cpp -- multi-GPU bucket allreduce: RCCL p2p over xGMI + fused HIP reductions.
+//
+// The schedule is data (xgmi_plan.h).  This file interprets it:
+//   * run_plan_rccl   one rank: SEND/RECV groups -> ncclGroupStart/ncclSend/ncclRecv/ncclGroupEnd
+//                     on the comm stream; REDUCE/FOLD -> HIP kernels on the compute stream; the
+//                     plan's wait0/wait1 edges -> hipEventRecord / hipStreamWaitEvent.  No host
+//                     synchronisation: the whole allreduce is enqueued asynchronously on the
+//                     caller's stream (graph-capturable).
+//   * simulate        every rank's plan on one GPU in lock-step, device copies on a "fabric"
+//                     stream standing in for xGMI -- the multi-GPU path's test bench.
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstring>
+#include <deque>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/hydra_hip.h"
+#include "errors.h"
+#include "reduce_kernels.h"
+#include "xgmi_plan.h"
+
+using hydra::fail;
+using hydra::ok;
+
+namespace {
+
+int nccl_fail(ncclResult_t r, const char* what) {
+  return fail(HYDRA_ERR_HIP, std::string(what) + ": " + ncclGetErrorString(r));
+}
+
+#define NCCL_TRY(expr)                                 \
+  do {                                                 \
+    ncclResult_t r__ = (expr);                         \
+    if (r__ != ncclSuccess) return nccl_fail(r__, #expr); \
+  } while (0)
+
+ncclDataType_t nccl_type(int dtype) {
+  switch (dtype) {
+    case HYDRA_INT8: return ncclInt8;
+    case HYDRA_UINT8: return ncclUint8;
+    case HYDRA_INT32: return ncclInt32;
+    case HYDRA_UINT32: return ncclUint32;
+    case HYDRA_INT64: return ncclInt64;
+    case HYDRA_UINT64: return ncclUint64;
+    case HYDRA_FLOAT32: return ncclFloat32;
+    case HYDRA_FLOAT64: return ncclFloat64;
+    case HYDRA_FLOAT16: return ncclFloat16;
+    case HYDRA_BFLOAT16: return ncclBfloat16;
+  }
+  return ncclUint8;
+}
+
+ncclRedOp_t nccl_op(int op) {
+  switch (op) {
+    case HYDRA_PRODUCT: return ncclProd;
+    case HYDRA_MAX: return ncclMax;
+    case HYDRA_MIN: return ncclMin;
+  }
+  return ncclSum;
+}
+
+int check_plan_args(int algo, int op, int dtype, int flags, size_t* esize) {
+  *esize = hydra::dtype_size(dtype);
+  if (!*esize) return fail(HYDRA_ERR_INVALID, "invalid dtype");
+  if (op < HYDRA_SUM || op > HYDRA_MIN) return fail(HYDRA_ERR_INVALID, "invalid op");
+  if (algo < HYDRA_ALGO_AUTO || algo > HYDRA_ALGO_RCCL)
+    return fail(HYDRA_ERR_INVALID, "invalid algorithm");
+  if (flags & HYDRA_ACC_F32) {
+    if (dtype != HYDRA_BFLOAT16)
+      return fail(HYDRA_ERR_UNSUPPORTED, "HYDRA_ACC_F32 needs a bf16 bucket");
+    if (algo == HYDRA_ALGO_RING)
+      return fail(HYDRA_ERR_UNSUPPORTED, "HYDRA_ACC_F32 runs on the DIRECT algorithm");
+  }
+  return HYDRA_OK;
+}
+
+int resolve_algo(int algo) { return algo == HYDRA_ALGO_AUTO ? HYDRA_ALGO_DIRECT : algo; }
+
+// ops that another op waits on need an event
+std::vector<char> waited_set(const std::vector<hydra::PlanOp>& ops) {
+  std::vector<char> w(ops.size(), 0);
+  for (const auto& o : ops) {
+    if (o.wait0 >= 0) w[o.wait0] = 1;
+    if (o.wait1 >= 0) w[o.wait1] = 1;
+  }
+  return w;
+}
+
+hipError_t launch_compute(const hydra::PlanOp& o, int op, int dtype, bool acc32, char* user,
+                          char* scratch, size_t esize, hipStream_t st) {
+  if (o.kind == hydra::kOpReduce)
+    return hydra::launch_reduce(0, op, dtype, user + o.off, user + o.off, scratch + o.src_off,
+                                (size_t)o.bytes / esize, st);
+  const void* srcs[hydra::kMaxRanks];
+  srcs[0] = user + o.off;
+  for (int j = 1; j < o.nsrc; j++) srcs[j] = scratch + o.src_off + (int64_t)(j - 1) * o.slot_stride;
+  return hydra::launch_fold(op, dtype, acc32, user + o.off, srcs, o.nsrc, (size_t)o.bytes / esize,
+                            st);
+}
+
+}  // namespace
+
+// ---- communicator ----------------------------------------------------------------------------
+struct hydra_comm {
+  int rank = 0, nranks = 1, device = 0;
+  ncclComm_t nccl = nullptr;
+  hipStream_t cs = nullptr, ks = nullptr;  // comm stream, compute stream
+  void* scratch = nullptr;
+  size_t scratch_bytes = 0;
+  std::vector<hipEvent_t> events;
+  hipEvent_t ev_start = nullptr, ev_cs = nullptr, ev_ks = nullptr;
+  // plan cache
+  int key_algo = -1;
+  size_t key_n = 0, key_es = 0, key_ms = 0, key_chunk = 0;
+  std::vector<hydra::PlanOp> plan;
+  std::vector<char> waited;
+};
+
+namespace {
+
+int ensure_events(hydra_comm* c, size_t n) {
+  while (c->events.size() < n) {
+    hipEvent_t e;
+    HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    c->events.push_back(e);
+  }
+  return HYDRA_OK;
+}
+
+void wait_on(hipStream_t st, const hydra::PlanOp& o, const std::vector<hipEvent_t>& ev) {
+  if (o.wait0 >= 0) (void)hipStreamWaitEvent(st, ev[o.wait0], 0);
+  if (o.wait1 >= 0) (void)hipStreamWaitEvent(st, ev[o.wait1], 0);
+}
+
+int run_plan_rccl(hydra_comm* c, int op, int dtype, bool acc32, char* user, hipStream_t user_st) {
+  const auto& ops = c->plan;
+  const size_t es = hydra::dtype_size(dtype);
+  char* scratch = static_cast<char*>(c->scratch);
+  HIP_TRY(hipEventRecord(c->ev_start, user_st));
+  HIP_TRY(hipStreamWaitEvent(c->cs, c->ev_start, 0));
+  HIP_TRY(hipStreamWaitEvent(c->ks, c->ev_start, 0));
+  size_t i = 0;
+  while (i < ops.size()) {
+    const hydra::PlanOp& o = ops[i];
+    if (o.kind == hydra::kOpSend || o.kind == hydra::kOpRecv || o.kind == hydra::kOpGroup) {
+      size_t g = i;
+      while (g < ops.size() && ops[g].kind != hydra::kOpGroup) g++;
+      if (g == ops.size()) return fail(HYDRA_ERR_INVALID, "plan: unterminated p2p group");
+      wait_on(c->cs, ops[g], c->events);
+      NCCL_TRY(ncclGroupStart());
+      for (size_t j = i; j < g; j++) {
+        const hydra::PlanOp& p = ops[j];
+        char* base = (p.buf == hydra::kBufUser ? user : scratch) + p.off;
+        if (p.kind == hydra::kOpSend)
+          NCCL_TRY(ncclSend(base, (size_t)p.bytes, ncclUint8, p.peer, c->nccl, c->cs));
+        else
+          NCCL_TRY(ncclRecv(base, (size_t)p.bytes, ncclUint8, p.peer, c->nccl, c->cs));
+      }
+      NCCL_TRY(ncclGroupEnd());
+      if (c->waited[g]) HIP_TRY(hipEventRecord(c->events[g], c->cs));
+      i = g + 1;
+    } else {
+      wait_on(c->ks, o, c->events);
+      hipError_t e = launch_compute(o, op, dtype, acc32, user, scratch, es, c->ks);
+      if (e != hipSuccess) return hydra::hip_fail(e, "fused reduction kernel");
+      if (c->waited[i]) HIP_TRY(hipEventRecord(c->events[i], c->ks));
+      i++;
+    }
+  }
+  HIP_TRY(hipEventRecord(c->ev_cs, c->cs));
+  HIP_TRY(hipEventRecord(c->ev_ks, c->ks));
+  HIP_TRY(hipStreamWaitEvent(user_st, c->ev_cs, 0));
+  HIP_TRY(hipStreamWaitEvent(user_st, c->ev_ks, 0));
+  return HYDRA_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int hydra_comm_get_unique_id(void* id) {
+  if (!id) return fail(HYDRA_ERR_INVALID, "null id");
+  ncclUniqueId u;
+  NCCL_TRY(ncclGetUniqueId(&u));
+  std::memcpy(id, &u, sizeof(u));
+  return ok();
+}
+
+int hydra_comm_init(hydra_comm_t* out, int nranks, int rank, const void* id, int device) {
+  if (!out || !id) return fail(HYDRA_ERR_INVALID, "null argument");
+  if (nranks < 1 || nranks > hydra::kMaxRanks || rank < 0 || rank >= nranks)
+    return fail(HYDRA_ERR_INVALID, "bad rank/nranks");
+  *out = nullptr;
+  HIP_TRY(hipSetDevice(device));
+  auto* c = new hydra_comm();
+  c->rank = rank;
+  c->nranks = nranks;
+  c->device = device;
+  ncclUniqueId u;
+  std::memcpy(&u, id, sizeof(u));
+  ncclResult_t r = ncclCommInitRank(&c->nccl, nranks, u, rank);
+  if (r != ncclSuccess) {
+    delete c;
+    return nccl_fail(r, "ncclCommInitRank");
+  }
+  hipError_t e = hipStreamCreateWithFlags(&c->cs, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->ks, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_start, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_cs, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_ks, hipEventDisableTiming);
+  if (e != hipSuccess) {
+    hydra_comm_destroy(c);
+    return hydra::hip_fail(e, "hydra_comm_init streams");
+  }
+  *out = c;
+  return ok();
+}
+
+int hydra_comm_destroy(hydra_comm_t c) {
+  if (!c) return ok();
+  (void)hipSetDevice(c->device);
+  if (c->cs) (void)hipStreamSynchronize(c->cs);
+  if (c->ks) (void)hipStreamSynchronize(c->ks);
+  if (c->nccl) (void)ncclCommDestroy(c->nccl);
+  for (auto e : c->events) (void)hipEventDestroy(e);
+  for (auto e : {c->ev_start, c->ev_cs, c->ev_ks})
+    if (e) (void)hipEventDestroy(e);
+  if (c->cs) (void)hipStreamDestroy(c->cs);
+  if (c->ks) (void)hipStreamDestroy(c->ks);
+  if (c->scratch) (void)hipFree(c->scratch);
+  delete c;
+  return ok();
+}
+
+int hydra_allreduce(hydra_comm_t c, int algo, int op, int dtype, int flags, void* buf, size_t n,
+                    size_t max_segment, size_t chunk_bytes, hydra_stream_t stream) {
+  if (!c) return fail(HYDRA_ERR_INVALID, "null comm");
+  size_t es;
+  int rc = check_plan_args(algo, op, dtype, flags, &es);
+  if (rc) return rc;
+  if (n == 0 || c->nranks == 1) return ok();  // allreduce.cc:129-133 (single process: no-op)
+  if (!buf) return fail(HYDRA_ERR_INVALID, "null buffer");
+  if (reinterpret_cast<uintptr_t>(buf) % es)
+    return fail(HYDRA_ERR_INVALID, "buffer not aligned to the element size");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  algo = resolve_algo(algo);
+  if (algo == HYDRA_ALGO_RCCL) {
+    if (flags & HYDRA_ACC_F32) return fail(HYDRA_ERR_UNSUPPORTED, "ACC_F32 with RCCL");
+    NCCL_TRY(ncclAllReduce(buf, buf, n, nccl_type(dtype), nccl_op(op), c->nccl, st));
+    return ok();
+  }
+  const size_t ms = max_segment ? max_segment : (1u << 20);
+  if (c->key_algo != algo || c->key_n != n || c->key_es != es || c->key_ms != ms ||
+      c->key_chunk != chunk_bytes) {
+    const hydra::PlanGeom g = hydra::make_geom(c->nranks, n, es, ms, chunk_bytes);
+    c->plan = hydra::make_plan(algo, g, c->rank);
+    c->waited = waited_set(c->plan);
+    const size_t need = hydra::plan_scratch_bytes(algo, g);
+    if (need > c->scratch_bytes) {
+      // (re)allocation happens outside any capture: first call with a new geometry
+      HIP_TRY(hipDeviceSynchronize());
+      if (c->scratch) HIP_TRY(hipFree(c->scratch));
+      c->scratch = nullptr;
+      c->scratch_bytes = 0;
+      HIP_TRY(hipMalloc(&c->scratch, need));
+      c->scratch_bytes = need;
+    }
+    rc = ensure_events(c, c->plan.size());
+    if (rc) return rc;
+    c->key_algo = algo;
+    c->key_n = n;
+    c->key_es = es;
+    c->key_ms = ms;
+    c->key_chunk = chunk_bytes;
+  }
+  rc = run_plan_rccl(c, op, dtype, (flags & HYDRA_ACC_F32) != 0, static_cast<char*>(buf), st);
+  if (rc) return rc;
+  return ok();
+}
+
+int hydra_plan(int algo, int P, int rank, size_t n, size_t esize, size_t max_segment,
+               size_t chunk_bytes, hydra_plan_op_t* ops, size_t cap, size_t* count,
+               size_t* scratch_bytes) {
+  if (P < 1 || P > hydra::kMaxRanks || rank < 0 || rank >= P)
+    return fail(HYDRA_ERR_INVALID, "bad rank/P");
+  if (esize != 1 && esize != 2 && esize != 4 && esize != 8)
+    return fail(HYDRA_ERR_INVALID, "bad element size");
+  algo = resolve_algo(algo);
+  if (algo == HYDRA_ALGO_RCCL) return fail(HYDRA_ERR_UNSUPPORTED, "RCCL has no plan");
+  const hydra::PlanGeom g =
+      hydra::make_geom(P, n, esize, max_segment ? max_segment : (1u << 20), chunk_bytes);
+  const auto plan = hydra::make_plan(algo, g, rank);
+  if (count) *count = plan.size();
+  if (scratch_bytes) *scratch_bytes = hydra::plan_scratch_bytes(algo, g);
+  if (ops) {
+    static_assert(sizeof(hydra_plan_op_t) == sizeof(hydra::PlanOp), "layout");
+    const size_t k = plan.size() < cap ? plan.size() : cap;
+    std::memcpy(ops, plan.data(), k * sizeof(hydra::PlanOp));
+  }
+  return ok();
+}
+
+// ---- one-GPU simulation of P ranks ---------------------------------------------------------
+int hydra_allreduce_simulate(int algo, int op, int dtype, int flags, int P, void** bufs, size_t n,
+                             size_t max_segment, size_t chunk_bytes) {
+  size_t es;
+  int rc = check_plan_args(algo, op, dtype, flags, &es);
+  if (rc) return rc;
+  if (P < 1 || P > hydra::kMaxRanks || !bufs) return fail(HYDRA_ERR_INVALID, "bad P/bufs");
+  algo = resolve_algo(algo);
+  if (algo == HYDRA_ALGO_RCCL) return fail(HYDRA_ERR_UNSUPPORTED, "no RCCL in the simulator");
+  if (n == 0 || P == 1) return ok();
+  const bool acc32 = (flags & HYDRA_ACC_F32) != 0;
+  const hydra::PlanGeom g =
+      hydra::make_geom(P, n, es, max_segment ? max_segment : (1u << 20), chunk_bytes);
+  const size_t sbytes = hydra::plan_scratch_bytes(algo, g);
+
+  struct Rank {
+    std::vector<hydra::PlanOp> ops;
+    std::vector<char> waited;
+    std::vector<hipEvent_t> ev;
+    hipStream_t cs = nullptr, ks = nullptr;
+    char* scratch = nullptr;
+    size_t pc = 0;
+    bool posted = false;
+    size_t group_end = 0;
+    int outstanding = 0;
+    hipEvent_t start = nullptr;
+    std::vector<hipEvent_t> done;  // copy-completion events of the posted group
+  };
+  std::vector<Rank> R(P);
+  std::vector<hipEvent_t> all_events;
+  hipStream_t fabric = nullptr;
+  auto cleanup = [&]() {
+    (void)hipDeviceSynchronize();
+    for (auto& r : R) {
+      if (r.cs) (void)hipStreamDestroy(r.cs);
+      if (r.ks) (void)hipStreamDestroy(r.ks);
+      if (r.scratch) (void)hipFree(r.scratch);
+    }
+    for (auto e : all_events) (void)hipEventDestroy(e);
+    if (fabric) (void)hipStreamDestroy(fabric);
+  };
+  auto new_event = [&](hipEvent_t* e) -> hipError_t {
+    hipError_t x = hipEventCreateWithFlags(e, hipEventDisableTiming);
+    if (x == hipSuccess) all_events.push_back(*e);
+    return x;
+  };
+#define SIM_TRY(expr)                               \
+  do {                                              \
+    hipError_t e__ = (expr);                        \
+    if (e__ != hipSuccess) {                        \
+      int rc__ = hydra::hip_fail(e__, #expr);       \
+      cleanup();                                    \
+      return rc__;                                  \
+    }                                               \
+  } while (0)
+
+  SIM_TRY(hipDeviceSynchronize());
+  SIM_TRY(hipStreamCreateWithFlags(&fabric, hipStreamNonBlocking));
+  for (int r = 0; r < P; r++) {
+    R[r].ops = hydra::make_plan(algo, g, r);
+    R[r].waited = waited_set(R[r].ops);
+    R[r].ev.resize(R[r].ops.size(), nullptr);
+    for (size_t i = 0; i < R[r].ops.size(); i++)
+      if (R[r].waited[i]) SIM_TRY(new_event(&R[r].ev[i]));
+    SIM_TRY(hipStreamCreateWithFlags(&R[r].cs, hipStreamNonBlocking));
+    SIM_TRY(hipStreamCreateWithFlags(&R[r].ks, hipStreamNonBlocking));
+    if (sbytes) SIM_TRY(hipMalloc(&R[r].scratch, sbytes));
+  }
+  struct Posted {
+    int rank;
+    size_t idx;
+  };
+  std::map<std::pair<int, int>, std::deque<Posted>> sends, recvs;  // key (src, dst)
+  auto wait_ev = [&](hipStream_t st, Rank& rk, const hydra::PlanOp& o) {
+    if (o.wait0 >= 0) (void)hipStreamWaitEvent(st, rk.ev[o.wait0], 0);
+    if (o.wait1 >= 0) (void)hipStreamWaitEvent(st, rk.ev[o.wait1], 0);
+  };
+  for (;;) {
+    bool progress = false, all_done = true;
+    for (int r = 0; r < P; r++) {
+      Rank& rk = R[r];
+      while (rk.pc < rk.ops.size()) {
+        const hydra::PlanOp& o = rk.ops[rk.pc];
+        if (o.kind == hydra::kOpReduce || o.kind == hydra::kOpFold) {
+          wait_ev(rk.ks, rk, o);
+          SIM_TRY(launch_compute(o, op, dtype, acc32, static_cast<char*>(bufs[r]), rk.scratch,
+                                 es, rk.ks));
+          if (rk.waited[rk.pc]) SIM_TRY(hipEventRecord(rk.ev[rk.pc], rk.ks));
+          rk.pc++;
+          progress = true;
+          continue;
+        }
+        if (!rk.posted) {  // post the whole group
+          size_t gi = rk.pc;
+          while (gi < rk.ops.size() && rk.ops[gi].kind != hydra::kOpGroup) gi++;
+          if (gi == rk.ops.size()) {
+            cleanup();
+            return fail(HYDRA_ERR_INVALID, "plan: unterminated group");
+          }
+          wait_ev(rk.cs, rk, rk.ops[gi]);
+          SIM_TRY(new_event(&rk.start));
+          SIM_TRY(hipEventRecord(rk.start, rk.cs));
+          rk.group_end = gi;
+          rk.outstanding = 0;
+          rk.done.clear();
+          for (size_t j = rk.pc; j < gi; j++) {
+            const hydra::PlanOp& p = rk.ops[j];
+            if (p.kind == hydra::kOpSend) sends[{r, p.peer}].push_back({r, j});
+            else recvs[{p.peer, r}].push_back({r, j});
+            rk.outstanding++;
+          }
+          rk.posted = true;
+          progress = true;
+          // match everything now matchable
+          for (auto& kv : sends) {
+            auto& sq = kv.second;
+            auto& rq = recvs[kv.first];
+            while (!sq.empty() && !rq.empty()) {
+              Posted s = sq.front(), d = rq.front();
+              sq.pop_front();
+              rq.pop_front();
+              Rank& S = R[s.rank];
+              Rank& D = R[d.rank];
+              const hydra::PlanOp& so = S.ops[s.idx];
+              const hydra::PlanOp& ro = D.ops[d.idx];
+              if (so.bytes != ro.bytes) {
+                cleanup();
+                return fail(HYDRA_ERR_INVALID, "plan: send/recv size mismatch");
+              }
+              const char* src = (so.buf == hydra::kBufUser ? static_cast<char*>(bufs[s.rank])
+                                                           : S.scratch) + so.off;
+              char* dst = (ro.buf == hydra::kBufUser ? static_cast<char*>(bufs[d.rank])
+                                                     : D.scratch) + ro.off;
+              SIM_TRY(hipStreamWaitEvent(fabric, S.start, 0));
+              SIM_TRY(hipStreamWaitEvent(fabric, D.start, 0));
+              SIM_TRY(hipMemcpyAsync(dst, src, (size_t)so.bytes, hipMemcpyDeviceToDevice, fabric));
+              hipEvent_t ce;
+              SIM_TRY(new_event(&ce));
+              SIM_TRY(hipEventRecord(ce, fabric));
+              S.done.push_back(ce);
+              D.done.push_back(ce);
+              S.outstanding--;
+              D.outstanding--;
+            }
+          }
+        }
+        if (rk.outstanding == 0) {  // group complete
+          for (auto e : rk.done) SIM_TRY(hipStreamWaitEvent(rk.cs, e, 0));
+          if (rk.waited[rk.group_end]) SIM_TRY(hipEventRecord(rk.ev[rk.group_end], rk.cs));
+          rk.pc = rk.group_end + 1;
+          rk.posted = false;
+          progress = true;
+          continue;
+        }
+        break;  // stalled on peers
+      }
+      if (rk.pc < rk.ops.size()) all_done = false;
+    }
+    if (all_done) break;
+    if (!progress) {
+      cleanup();
+      return fail(HYDRA_ERR_INVALID, "plan deadlock in simulation");
+    }
+  }
+  SIM_TRY(hipDeviceSynchronize());
+  cleanup();
+#undef SIM_TRY
+  return ok();
+}
+
+}  // extern "C"

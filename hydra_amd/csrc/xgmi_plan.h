@@ -105,8 +105,10 @@ inline PlanGeom make_geom(int P, size_t n, size_t esize, size_t max_segment, siz
   g.total = n * esize;
   ring_geometry(P, n, esize, max_segment ? max_segment : (1u << 20), &g.num_segments,
                 &g.segment_bytes, &g.S);
-  const size_t unit = esize * 16 / std::__gcd(esize, (size_t)16);  // lcm(esize, 16)
+  const size_t unit = 16;  // every element size (1, 2, 4, 8) divides 16
   g.chunk = round_up_sz(std::max<size_t>(chunk ? chunk : (4u << 20), unit), unit);
+  // never pipeline in chunks larger than a block (small buckets keep a small scratch)
+  g.chunk = std::min(g.chunk, round_up_sz(std::max<size_t>(g.max_block(), 1), unit));
   return g;
 }
 

@@ -115,6 +115,57 @@ int hydra_memcpy(void* dst, const void* src, size_t bytes); /* hipMemcpyDefault,
 void hydra_ring_plan(int P, size_t n, size_t esize, size_t max_segment, size_t* num_segments,
                      size_t* segment_bytes, size_t* segments_per_rank);
 
+/* ---- multi-GPU bucket allreduce over RCCL / xGMI ------------------------------------------
+ * One process per GPU.  Replaces gloo::allreduce(opts) with RING (allreduce.cc:99-422) for
+ * device-resident buckets: block ownership and per-element fold order are the reference's, so
+ * results are bit-identical to the reference ring for every dtype/op.
+ *   HYDRA_ALGO_RING    the reference schedule: P-1 reduce-scatter hops to rank-1 with the HIP
+ *                      sum fused into each hop, then P-1 all-gather hops (one link per direction)
+ *   HYDRA_ALGO_DIRECT  all-to-all reduce-scatter in one p2p group (all 7 xGMI links), then ONE
+ *                      fold kernel per chunk in the reference order, then a direct all-gather
+ *   HYDRA_ALGO_RCCL    ncclAllReduce (RCCL's own fold order: a tolerance, not bit-exact)
+ *   HYDRA_ALGO_AUTO    DIRECT
+ * max_segment: the reference's maxSegmentSize (0 = 1 MiB, allreduce.h:78) -- it fixes block
+ * ownership; chunk_bytes: pipelining granularity (0 = 4 MiB), does not change results.
+ * flags: HYDRA_ACC_F32 -- bf16 bucket, fp32 accumulation, one rounding (BASELINE config 5;
+ * DIRECT/AUTO only). */
+#define HYDRA_UNIQUE_ID_BYTES 128
+#define HYDRA_ACC_F32 1
+typedef enum {
+  HYDRA_ALGO_AUTO = 0,
+  HYDRA_ALGO_RING = 1,
+  HYDRA_ALGO_DIRECT = 2,
+  HYDRA_ALGO_RCCL = 3
+} hydra_algo_t;
+typedef struct hydra_comm* hydra_comm_t;
+
+/* A plan op (one rank's schedule entry; see hydra_amd/csrc/xgmi_plan.h). */
+typedef struct {
+  int32_t kind; /* 1 SEND, 2 RECV, 3 GROUP end, 4 REDUCE (ring hop), 5 FOLD (direct owner) */
+  int32_t peer;
+  int32_t buf;  /* 0 user bucket, 1 scratch */
+  int32_t nsrc;
+  int64_t off, bytes, src_off, slot_stride;
+  int32_t wait0, wait1;
+} hydra_plan_op_t;
+
+int hydra_comm_get_unique_id(void* id /* HYDRA_UNIQUE_ID_BYTES */);
+int hydra_comm_init(hydra_comm_t* out, int nranks, int rank, const void* id, int device);
+int hydra_comm_destroy(hydra_comm_t comm);
+int hydra_allreduce(hydra_comm_t comm, int algo, int op, int dtype, int flags, void* buf,
+                    size_t n, size_t max_segment, size_t chunk_bytes, hydra_stream_t stream);
+
+/* The schedule rank `rank` of P executes (for inspection / host-side tests). */
+int hydra_plan(int algo, int P, int rank, size_t n, size_t esize, size_t max_segment,
+               size_t chunk_bytes, hydra_plan_op_t* ops, size_t cap, size_t* count,
+               size_t* scratch_bytes);
+
+/* All P ranks' plans on ONE GPU (device copies stand in for xGMI, same kernels, same
+ * cross-stream dependencies): bufs[r] is rank r's bucket.  Synchronous.  For testing the
+ * multi-GPU path on a single-GPU machine. */
+int hydra_allreduce_simulate(int algo, int op, int dtype, int flags, int P, void** bufs,
+                             size_t n, size_t max_segment, size_t chunk_bytes);
+
 #ifdef __cplusplus
 }
 #endif

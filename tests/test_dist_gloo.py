@@ -1,0 +1,104 @@
+"""World-size-2 (and 3) CPU runs of the N>1 path over torch.distributed gloo: the rank-local
+plans from libhydra_hip.so executed with real inter-process p2p (batch_isend_irecv), the
+oracle's reduction standing in for the HIP kernels (CPU-only test of the distributed
+orchestration), plus the bench harness helpers (unique-id broadcast, max-over-ranks timing)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+SEND, RECV, GROUP, REDUCE, FOLD = 1, 2, 3, 4, 5
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, algo, n, ms, ch, q):
+    import sys
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch
+    import torch.distributed as dist
+
+    from hydra_amd import ring, synth
+    from oracle import oracle as O
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        x = synth.stress_f32(world, rank, n)
+        ops, scr = ring.plan(algo, world, rank, n, 4, ms, ch)
+        user = torch.from_numpy(x.copy().view(np.uint8))
+        scratch = torch.zeros(scr + 16, dtype=torch.uint8)
+        i = 0
+        while i < len(ops):
+            o = ops[i]
+            if o["kind"] in (REDUCE, FOLD):
+                u = user.numpy()
+                sc = scratch.numpy()
+                local = u[o["off"]:o["off"] + o["bytes"]].view(np.float32).copy()
+                if o["kind"] == REDUCE:
+                    recv = sc[o["src_off"]:o["src_off"] + o["bytes"]].view(np.float32)
+                    out = O.op(local, recv, "sum")
+                else:
+                    slots = [sc[o["src_off"] + k * o["slot_stride"]:o["src_off"] + k *
+                                o["slot_stride"] + o["bytes"]].view(np.float32)
+                             for k in range(o["nsrc"] - 1)]
+                    acc = slots[-1].copy()
+                    for s in reversed(slots[:-1]):
+                        acc = O.op(s.copy(), acc, "sum")
+                    out = O.op(local, acc, "sum")
+                u[o["off"]:o["off"] + o["bytes"]] = out.view(np.uint8)
+                i += 1
+                continue
+            g = i
+            p2p = []
+            while ops[g]["kind"] != GROUP:
+                it = ops[g]
+                t = (user if it["buf"] == 0 else scratch)[it["off"]:it["off"] + it["bytes"]]
+                p2p.append(dist.P2POp(dist.isend if it["kind"] == SEND else dist.irecv, t,
+                                      it["peer"]))
+                g += 1
+            for req in dist.batch_isend_irecv(p2p):
+                req.wait()
+            i = g + 1
+        got = user.numpy().view(np.float32)
+        # harness helpers
+        uid = ring.exchange_unique_id(rank, make_id=lambda: bytes(range(128)))
+        assert uid == bytes(range(128))
+        mx = ring.max_over_ranks(float(rank + 1))
+        assert mx == float(world)
+        wall = ring.timed_steps(lambda: None, 3, 1, lambda: None, dist.barrier)
+        assert wall >= 0
+        xs = [synth.stress_f32(world, r, n) for r in range(world)]
+        exp = O.ring_result(xs, ms or (1 << 20))
+        q.put((rank, bool(np.array_equal(got.view(np.uint32), exp.view(np.uint32)))))
+    except Exception as e:  # report instead of hanging the parent
+        q.put((rank, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("algo", ["ring", "direct"])
+def test_gloo_multiprocess_plan(algo, world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    n, ms, ch = 100003, 4096, 16384
+    procs = [ctx.Process(target=_worker, args=(r, world, port, algo, n, ms, ch, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    assert all(v is True for v in res.values()), res

@@ -1,0 +1,224 @@
+"""The multi-GPU schedules (hydra_amd/csrc/xgmi_plan.h), checked on the CPU.
+
+1. Functional: every rank's plan, interpreted with numpy copies for the p2p groups and the
+   oracle's reduction for REDUCE/FOLD, reproduces the reference ring's result bit-exactly
+   (fold order!) for P = 2..8, ragged sizes, maxSegmentSize 128 / 1 MiB and several chunk sizes.
+2. Races: on the two-stream execution model the RCCL executor uses (comm stream: p2p groups;
+   compute stream: REDUCE/FOLD; cross-stream edges: the plan's wait0/wait1), every pair of
+   conflicting accesses (same bytes, at least one write) is ordered by happens-before.
+"""
+import numpy as np
+import pytest
+
+from hydra_amd import _lib, ring, synth
+
+SEND, RECV, GROUP, REDUCE, FOLD = 1, 2, 3, 4, 5
+
+
+def interpret(plans, bufs, scratch, reduce_fn):
+    """Sequential lock-step execution of all ranks (p2p groups matched per (src,dst) FIFO)."""
+    P = len(plans)
+    pcs = [0] * P
+    sends, recvs = {}, {}
+    posted = [None] * P
+    while any(pcs[r] < len(plans[r]) for r in range(P)):
+        progress = False
+        for r in range(P):
+            ops = plans[r]
+            while pcs[r] < len(ops):
+                o = ops[pcs[r]]
+                if o["kind"] in (REDUCE, FOLD):
+                    reduce_fn(r, o)
+                    pcs[r] += 1
+                    progress = True
+                    continue
+                if posted[r] is None:
+                    g = pcs[r]
+                    while ops[g]["kind"] != GROUP:
+                        g += 1
+                    items = ops[pcs[r]:g]
+                    posted[r] = [g, len(items)]
+                    for it in items:
+                        key = (r, it["peer"]) if it["kind"] == SEND else (it["peer"], r)
+                        (sends if it["kind"] == SEND else recvs).setdefault(key, []).append((r, it))
+                    progress = True
+                    for key in list(sends):
+                        sq, rq = sends[key], recvs.setdefault(key, [])
+                        while sq and rq:
+                            (sr, so), (dr, ro) = sq.pop(0), rq.pop(0)
+                            assert so["bytes"] == ro["bytes"]
+                            src = (bufs if so["buf"] == 0 else scratch)[sr]
+                            dst = (bufs if ro["buf"] == 0 else scratch)[dr]
+                            dst[ro["off"]:ro["off"] + ro["bytes"]] = \
+                                src[so["off"]:so["off"] + so["bytes"]]
+                            posted[sr][1] -= 1
+                            posted[dr][1] -= 1
+                if posted[r][1] == 0:
+                    pcs[r] = posted[r][0] + 1
+                    posted[r] = None
+                    progress = True
+                    continue
+                break
+        assert progress, "deadlock"
+
+
+def run_plan_numpy(O, algo, xs, max_segment, chunk, code=6):
+    P = len(xs)
+    es = xs[0].itemsize
+    n = xs[0].size
+    plans, scr = [], 0
+    for r in range(P):
+        ops, s = ring.plan(algo, P, r, n, es, max_segment, chunk)
+        plans.append(ops)
+        scr = max(scr, s)
+    bufs = [x.copy().view(np.uint8) for x in xs]
+    scratch = [np.zeros(scr + 16, np.uint8) for _ in range(P)]
+    dt = xs[0].dtype
+
+    def reduce_fn(r, o):
+        u, sc = bufs[r], scratch[r]
+        cnt = o["bytes"] // es
+        local = u[o["off"]:o["off"] + o["bytes"]].view(dt).copy()
+        if o["kind"] == REDUCE:
+            recv = sc[o["src_off"]:o["src_off"] + o["bytes"]].view(dt)
+            out = O.op(local, recv, "sum", code)
+        else:
+            slots = [sc[o["src_off"] + k * o["slot_stride"]:
+                        o["src_off"] + k * o["slot_stride"] + o["bytes"]].view(dt)
+                     for k in range(o["nsrc"] - 1)]
+            acc = slots[-1].copy()
+            for s in reversed(slots[:-1]):
+                acc = O.op(s.copy(), acc, "sum", code)
+            out = O.op(local, acc, "sum", code)
+        assert out.size == cnt
+        u[o["off"]:o["off"] + o["bytes"]] = out.view(np.uint8)
+
+    interpret(plans, bufs, scratch, reduce_fn)
+    return [b.view(dt) for b in bufs]
+
+
+CASES = [(P, n, ms, ch) for P in (2, 3, 4, 5, 8) for (n, ms, ch) in
+         [(1, 0, 0), (7, 128, 0), (1000, 128, 64), (4099, 128, 1024), (10007, 1 << 20, 4096),
+          (262145, 0, 0), (262145, 0, 65536)]]
+
+
+@pytest.mark.parametrize("algo", ["ring", "direct"])
+@pytest.mark.parametrize("P,n,ms,ch", CASES)
+def test_plan_matches_reference_fold(O, algo, P, n, ms, ch):
+    xs = [synth.stress_f32(P, r, n) for r in range(P)]
+    outs = run_plan_numpy(O, algo, xs, ms, ch)
+    exp = O.ring_result(xs, ms or (1 << 20))
+    for r in range(P):
+        assert np.array_equal(outs[r].view(np.uint32), exp.view(np.uint32)), (algo, r)
+
+
+@pytest.mark.parametrize("algo", ["ring", "direct"])
+def test_plan_int32_and_f16(O, algo):
+    P, n = 4, 5003
+    xs = [synth.int32_bucket(P, r, n) for r in range(P)]
+    outs = run_plan_numpy(O, algo, xs, 256, 512, code=2)
+    exp = O.ring_result(xs, 256)
+    assert all(np.array_equal(o, exp) for o in outs)
+    rng = np.random.default_rng(2)
+    hs = [np.array([O.f2h(float(v)) for v in rng.uniform(-4, 4, n)], np.uint16) for _ in range(P)]
+    outs = run_plan_numpy(O, algo, hs, 256, 512, code=8)
+    exp = O.ring_result(hs, 256, dtype_code=8)
+    assert all(np.array_equal(o, exp) for o in outs)
+
+
+def _accesses(o, scratch_id=1):
+    """(buffer, lo, hi, is_write) byte ranges an op touches."""
+    if o["kind"] in (SEND, RECV):
+        return [(o["buf"], o["off"], o["off"] + o["bytes"], o["kind"] == RECV)]
+    acc = [(0, o["off"], o["off"] + o["bytes"], True), (0, o["off"], o["off"] + o["bytes"], False)]
+    if o["kind"] == REDUCE:
+        acc.append((1, o["src_off"], o["src_off"] + o["bytes"], False))
+    else:
+        for k in range(o["nsrc"] - 1):
+            lo = o["src_off"] + k * o["slot_stride"]
+            acc.append((1, lo, lo + o["bytes"], False))
+    return acc
+
+
+def race_check(ops):
+    """Units: each p2p group (its SEND/RECVs + GROUP) on the comm stream; each REDUCE/FOLD on
+    the compute stream.  Edges: stream order + wait0/wait1.  Every conflicting pair of units on
+    different streams must be ordered (in plan order) by happens-before."""
+    units = []  # (stream, accesses, waits(list of op idx), op index of unit end)
+    unit_of = {}
+    i = 0
+    while i < len(ops):
+        o = ops[i]
+        if o["kind"] in (REDUCE, FOLD):
+            units.append(("k", _accesses(o), [o["wait0"], o["wait1"]], i))
+            unit_of[i] = len(units) - 1
+            i += 1
+        else:
+            g = i
+            acc = []
+            while ops[g]["kind"] != GROUP:
+                acc += _accesses(ops[g])
+                g += 1
+            units.append(("c", acc, [ops[g]["wait0"], ops[g]["wait1"]], g))
+            for j in range(i, g + 1):
+                unit_of[j] = len(units) - 1
+            i = g + 1
+    U = len(units)
+    preds = [set() for _ in range(U)]
+    last = {"c": None, "k": None}
+    for u, (st, _, waits, _) in enumerate(units):
+        if last[st] is not None:
+            preds[u].add(last[st])
+        for w in waits:
+            if w >= 0:
+                preds[u].add(unit_of[w])
+        last[st] = u
+    hb = [set() for _ in range(U)]  # transitive predecessors
+    for u in range(U):
+        for p in preds[u]:
+            hb[u] |= hb[p] | {p}
+    for b in range(U):
+        for a in range(b):
+            if units[a][0] == units[b][0] or a in hb[b]:
+                continue
+            for (ba, la, ha, wa) in units[a][1]:
+                for (bb, lb, hb_, wb) in units[b][1]:
+                    if ba == bb and la < hb_ and lb < ha and (wa or wb):
+                        raise AssertionError(f"race: unit {a} {units[a][0]} vs {b} {units[b][0]}")
+
+
+@pytest.mark.parametrize("algo", ["ring", "direct"])
+@pytest.mark.parametrize("P,n,ms,ch", [c for c in CASES if c[1] > 100])
+def test_plan_is_race_free(algo, P, n, ms, ch):
+    for r in range(P):
+        ops, _ = ring.plan(algo, P, r, n, 4, ms, ch)
+        race_check(ops)
+
+
+def test_race_checker_catches_missing_wait():
+    ops, _ = ring.plan("direct", 4, 0, 100000, 4, 1024, 4096)
+    bad = [dict(o) for o in ops]
+    for o in bad:
+        if o["kind"] == FOLD:
+            o["wait0"] = -1
+            break
+    with pytest.raises(AssertionError):
+        race_check(bad)
+
+
+def test_scratch_is_small_for_small_buckets():
+    ops, scr = ring.plan("direct", 8, 0, 1000, 4)
+    assert scr <= 2 * 7 * 512
+
+
+def test_plan_geometry_matches_ring_plan():
+    """Block ownership comes from allreduce.cc:199-221: the FOLD/REDUCE of the last hop covers
+    exactly this rank's block [rS*sb, (r+1)S*sb)."""
+    P, n = 5, 3000001
+    ns, sb, S = _lib.ring_plan(P, n, 4, 1 << 20)
+    for r in range(P):
+        ops, _ = ring.plan("direct", P, r, n, 4, 0, 0)
+        folds = [o for o in ops if o["kind"] == FOLD]
+        lo = min(o["off"] for o in folds)
+        hi = max(o["off"] + o["bytes"] for o in folds)
+        assert lo == min(4 * n, r * S * sb) and hi == min(4 * n, (r + 1) * S * sb)
