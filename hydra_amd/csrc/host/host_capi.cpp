@@ -1,0 +1,181 @@
+// host_capi.cpp -- extern "C" drivers of the host runtime (include/hydra_host.h).
+#include <chrono>
+#include <condition_variable>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../../include/hydra/allreduce.h"
+#include "../../../include/hydra/gloo_reduce.h"
+#include "../../../include/hydra_host.h"
+
+namespace {
+
+void set_err(char* err, size_t len, const std::string& s) {
+  if (err && len) {
+    std::strncpy(err, s.c_str(), len - 1);
+    err[len - 1] = 0;
+  }
+}
+
+hydra::AllreduceOptions::Func make_reducer(int reducer, int op, int dtype, hydra_reduce_fn fn) {
+  if (reducer == HYDRA_REDUCER_FN) {
+    if (!fn) throw hydra::EnforceNotMet("null reduce function");
+    return [fn](void* c, const void* a, const void* b, size_t n) { fn(c, a, b, n); };
+  }
+  return hydra::gloo_compat::hostReduce(op, dtype, 0);
+}
+
+size_t esize_of(int dtype) {
+  static const size_t sz[] = {1, 1, 4, 4, 8, 8, 4, 8, 2, 2};
+  return (dtype >= 0 && dtype <= 9) ? sz[dtype] : 0;
+}
+
+// Spawn P threads; each gets a connected context (two when rails == 2).
+int spawn(int P, int rails, char* err, size_t errlen,
+          const std::function<void(int, std::vector<std::shared_ptr<hydra::Context>>&)>& body) {
+  hydra::HashStore store;
+  std::mutex mu;
+  std::condition_variable cv;
+  int arrived = 0;
+  std::string first;
+  std::vector<std::thread> th;
+  for (int r = 0; r < P; r++) {
+    th.emplace_back([&, r] {
+      std::vector<std::shared_ptr<hydra::Context>> ctx;
+      try {
+        for (int k = 0; k < rails; k++) {
+          ctx.push_back(std::make_shared<hydra::Context>(r, P));
+          ctx.back()->connectFullMesh(store, "127.0.0.1", "rail" + std::to_string(k));
+        }
+        body(r, ctx);
+      } catch (const std::exception& e) {
+        std::lock_guard<std::mutex> g(mu);
+        if (first.empty()) first = e.what();
+      }
+      // every rank finishes before any connection closes (base_test.h:142-155)
+      std::unique_lock<std::mutex> l(mu);
+      arrived++;
+      cv.notify_all();
+      cv.wait(l, [&] { return arrived == P; });
+    });
+  }
+  for (auto& t : th) t.join();
+  if (!first.empty()) {
+    set_err(err, errlen, first);
+    return 1;
+  }
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int hydra_host_allreduce_threads(int P, int nptr, int op, int dtype, size_t n, void** in,
+                                 void** out, size_t max_segment, int reducer, hydra_reduce_fn fn,
+                                 long timeout_ms, char* err, size_t errlen) {
+  const size_t es = esize_of(dtype);
+  if (!es || P < 1 || nptr < 1 || !out) {
+    set_err(err, errlen, "invalid arguments");
+    return 2;
+  }
+  return spawn(P, 1, err, errlen, [&](int r, std::vector<std::shared_ptr<hydra::Context>>& c) {
+    hydra::AllreduceOptions o(c[0]);
+    o.setAlgorithm(hydra::AllreduceOptions::RING);
+    o.setOutputsRaw(out + r * nptr, nptr, n, es);
+    if (in) o.setInputsRaw(in + r * nptr, nptr, n, es);
+    o.setReduceFunction(make_reducer(reducer, op, dtype, fn));
+    if (max_segment) o.setMaxSegmentSize(max_segment);
+    if (timeout_ms > 0) o.setTimeout(std::chrono::milliseconds(timeout_ms));
+    hydra::allreduce(o);
+  });
+}
+
+int hydra_host_apipe_threads(int P, int dtype, size_t n, void** in, void** out, int table,
+                             int reducer, hydra_reduce_fn fn, char* err, size_t errlen) {
+  const size_t es = esize_of(dtype);
+  if (!es || P < 1 || !out || !in) {
+    set_err(err, errlen, "invalid arguments");
+    return 2;
+  }
+  return spawn(P, 2, err, errlen, [&](int r, std::vector<std::shared_ptr<hydra::Context>>& c) {
+    hydra::APipeAllreduceOptions o(c[0], c[1]);
+    o.setSplitTable(table == HYDRA_SPLIT_AG ? hydra::SplitTable::AG : hydra::SplitTable::AA);
+    o.setInputRaw(in[r], n, es);
+    o.setOutputRaw(out[r], n, es);
+    o.setAlgorithm(hydra::AllreduceOptions::RING);
+    o.setReduceFunction(make_reducer(reducer, HYDRA_SUM, dtype, fn));
+    hydra::apipe_allreduce(o);
+  });
+}
+
+int hydra_host_bench(int config, int P, size_t n, int warmup, int iters, int reducer,
+                     hydra_reduce_fn fn, double* samples_ns, char* err, size_t errlen) {
+  if ((config != 1 && config != 3) || P < 1 || !samples_ns) {
+    set_err(err, errlen, "invalid arguments");
+    return 2;
+  }
+  return spawn(P, config == 3 ? 2 : 1, err, errlen,
+               [&](int r, std::vector<std::shared_ptr<hydra::Context>>& c) {
+    std::vector<float> in(n), out(n);
+    auto time_it = [&](const std::function<void()>& run) {
+      for (int i = 0; i < warmup; i++) run();
+      for (int i = 0; i < iters; i++) {
+        const auto t0 = std::chrono::steady_clock::now();
+        run();
+        const auto t1 = std::chrono::steady_clock::now();
+        if (r == 0) samples_ns[i] = std::chrono::duration<double, std::nano>(t1 - t0).count();
+      }
+    };
+    if (config == 1) {  // NewAllreduceBenchmark: in[j] = j*P + r, out of place (main.cc:329-358)
+      for (size_t j = 0; j < n; j++) in[j] = float(j * (size_t)P + (size_t)r);
+      hydra::AllreduceOptions o(c[0]);
+      o.setInput(in.data(), n);
+      o.setOutput(out.data(), n);
+      o.setAlgorithm(hydra::AllreduceOptions::RING);
+      o.setReduceFunction(make_reducer(reducer, HYDRA_SUM, HYDRA_FLOAT32, fn));
+      time_it([&] { hydra::allreduce(o); });
+    } else {  // aAllreduceBenchmark: in[i] = i*(rank+1.0), out = 0 (main.cc:629-664)
+      for (size_t j = 0; j < n; j++) in[j] = float((double)j * (r + 1.0));
+      hydra::APipeAllreduceOptions o(c[0], c[1]);
+      o.setInput(in.data(), n);
+      o.setOutput(out.data(), n);
+      o.setAlgorithm(hydra::AllreduceOptions::RING);
+      o.setReduceFunction(make_reducer(reducer, HYDRA_SUM, HYDRA_FLOAT32, fn));
+      time_it([&] { hydra::apipe_allreduce(o); });
+    }
+  });
+}
+
+void hydra_host_calculate_elements(int table, int P, size_t n, size_t* e1, size_t* e2) {
+  hydra::calculateElements(table == HYDRA_SPLIT_AG ? hydra::SplitTable::AG : hydra::SplitTable::AA,
+                           P, n, e1, e2);
+}
+
+int hydra_host_timeout_probe(long timeout_ms, char* what, size_t len) {
+  int rc = 3;
+  spawn(2, 1, nullptr, 0, [&](int r, std::vector<std::shared_ptr<hydra::Context>>& c) {
+    if (r != 0) return;
+    uint64_t buf = 0;
+    hydra::AllreduceOptions o(c[0]);
+    o.setOutput(&buf, 1);
+    o.setReduceFunction([](void* x, const void* a, const void* b, size_t n) {
+      for (size_t i = 0; i < n; i++)
+        static_cast<uint64_t*>(x)[i] =
+            static_cast<const uint64_t*>(a)[i] + static_cast<const uint64_t*>(b)[i];
+    });
+    o.setTimeout(std::chrono::milliseconds(timeout_ms));
+    try {
+      hydra::allreduce(o);
+    } catch (const hydra::IoException& e) {
+      set_err(what, len, e.what());
+      rc = 0;
+    }
+  });
+  return rc;
+}
+
+}  // extern "C"

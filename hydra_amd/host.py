@@ -1,0 +1,110 @@
+"""ctypes face of libhydra_host.so (include/hydra_host.h): the C++ host runtime that mirrors
+hydra/Gloo's new_allreduce_ring / bew_allreduce_a over loopback TCP, reducing each segment on
+the MI355X through libhydra_hip.so."""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+from . import _lib
+
+LIB_PATH = os.path.join(_lib.HERE, "libhydra_host.so")
+REDUCER_GPU, REDUCER_FN = 0, 1
+SPLIT_AA, SPLIT_AG = 0, 1
+REDUCE_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                             ctypes.c_size_t)
+_h = None
+
+
+def lib():
+    global _h
+    if _h is None:
+        _lib.lib()  # libhydra_hip.so first (binds to torch's HIP runtime when present)
+        if not os.path.exists(LIB_PATH):
+            raise _lib.HydraError(-1, f"{LIB_PATH} is not built")
+        L = ctypes.CDLL(LIB_PATH)
+        vp, sz, i = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
+        L.hydra_host_allreduce_threads.argtypes = [i, i, i, i, sz, vp, vp, sz, i, vp,
+                                                   ctypes.c_long, ctypes.c_char_p, sz]
+        L.hydra_host_apipe_threads.argtypes = [i, i, sz, vp, vp, i, i, vp, ctypes.c_char_p, sz]
+        L.hydra_host_bench.argtypes = [i, i, sz, i, i, i, vp, vp, ctypes.c_char_p, sz]
+        L.hydra_host_calculate_elements.argtypes = [i, i, sz, ctypes.POINTER(sz),
+                                                    ctypes.POINTER(sz)]
+        L.hydra_host_calculate_elements.restype = None
+        L.hydra_host_timeout_probe.argtypes = [ctypes.c_long, ctypes.c_char_p, sz]
+        _h = L
+    return _h
+
+
+def _ptrs(arrs):
+    return (ctypes.c_void_p * len(arrs))(*[a.ctypes.data for a in arrs])
+
+
+def _fn(reducer_fn):
+    """reducer_fn: None -> GPU; an int address of a C function with the Func signature."""
+    if reducer_fn is None:
+        return REDUCER_GPU, None
+    return REDUCER_FN, ctypes.c_void_p(reducer_fn)
+
+
+def allreduce_threads(outs, ins=None, dtype_code=None, op="sum", max_segment=0, reducer_fn=None,
+                      timeout_ms=0):
+    """gloo::allreduce(RING) on len(outs) thread-ranks; outs/ins: [rank][ptr] numpy arrays."""
+    P, nptr = len(outs), len(outs[0])
+    n = outs[0][0].size
+    code = dtype_code if dtype_code is not None else _np_code(outs[0][0].dtype)
+    red, fp = _fn(reducer_fn)
+    err = ctypes.create_string_buffer(512)
+    rc = lib().hydra_host_allreduce_threads(
+        P, nptr, _lib.OPS[op], code, n,
+        ctypes.cast(_ptrs([a for r in ins for a in r]), ctypes.c_void_p) if ins else None,
+        ctypes.cast(_ptrs([a for r in outs for a in r]), ctypes.c_void_p), max_segment, red, fp,
+        timeout_ms, err, 512)
+    if rc:
+        raise _lib.HydraError(rc, err.value.decode())
+    return outs
+
+
+def apipe_threads(ins, outs, table=SPLIT_AA, reducer_fn=None, dtype_code=_lib.FLOAT32):
+    P, n = len(ins), ins[0].size
+    red, fp = _fn(reducer_fn)
+    err = ctypes.create_string_buffer(512)
+    rc = lib().hydra_host_apipe_threads(P, dtype_code, n,
+                                        ctypes.cast(_ptrs(ins), ctypes.c_void_p),
+                                        ctypes.cast(_ptrs(outs), ctypes.c_void_p), table, red, fp,
+                                        err, 512)
+    if rc:
+        raise _lib.HydraError(rc, err.value.decode())
+    return outs
+
+
+def bench(config: int, P: int, n: int, warmup: int, iters: int, reducer_fn=None) -> np.ndarray:
+    s = np.zeros(iters, np.float64)
+    red, fp = _fn(reducer_fn)
+    err = ctypes.create_string_buffer(512)
+    rc = lib().hydra_host_bench(config, P, n, warmup, iters, red, fp, s.ctypes.data, err, 512)
+    if rc:
+        raise _lib.HydraError(rc, err.value.decode())
+    return s
+
+
+def calculate_elements(table: int, P: int, n: int):
+    e1, e2 = ctypes.c_size_t(), ctypes.c_size_t()
+    lib().hydra_host_calculate_elements(table, P, n, ctypes.byref(e1), ctypes.byref(e2))
+    return e1.value, e2.value
+
+
+def timeout_probe(ms: int):
+    buf = ctypes.create_string_buffer(512)
+    rc = lib().hydra_host_timeout_probe(ms, buf, 512)
+    return rc, buf.value.decode()
+
+
+def _np_code(dt):
+    return {np.dtype(np.float32): _lib.FLOAT32, np.dtype(np.int32): _lib.INT32,
+            np.dtype(np.uint64): _lib.UINT64, np.dtype(np.int64): _lib.INT64,
+            np.dtype(np.float64): _lib.FLOAT64, np.dtype(np.uint16): _lib.FLOAT16,
+            np.dtype(np.int8): _lib.INT8, np.dtype(np.uint8): _lib.UINT8,
+            np.dtype(np.uint32): _lib.UINT32}[np.dtype(dt)]

@@ -1,0 +1,215 @@
+// include/hydra/allreduce.h -- C++ host runtime mirroring hydra/Gloo's new-style allreduce API
+// for the bucket-reduction path (libhydra_host.so, built with g++; talks to the GPU only through
+// the C-ABI in include/hydra_hip.h).
+//
+// Mirrors (same names, argument meaning and error behaviour):
+//   gloo::Context(rank, size) + rendezvous::Context::connectFullMesh   gloo/gloo/context.h:26-58,
+//                                                                       rendezvous/context.cc:32-69
+//   gloo::AllreduceOptions {setInput(s), setOutput(s), setReduceFunction, setAlgorithm, setTag,
+//                           setMaxSegmentSize, setTimeout}          gloo/gloo/allreduce.h:89-199
+//   gloo::allreduce(opts)  (RING; P==1 short circuit)                 gloo/gloo/allreduce.cc:99-422
+//   gloo::APipeAllreduceOptions / apipe_allreduce (bew_allreduce_a)   gloo/gloo/pipeallreduce-a.h:32-397,
+//                                                                       pipeallreduce-a.cc:27-61
+//   gloo::EnforceNotMet / gloo::IoException ("Timed out ...")        common/logging.h:21, common/error.h:45
+// Transport: loopback/LAN TCP, one reader and one writer thread per pair, FIFO per pair,
+// receives land directly in the posted buffer (gloo/gloo/transport/tcp/pair.cc:486-533 idea).
+#pragma once
+
+#include <chrono>
+#include <cstddef>
+#include <cstdint>
+#include <functional>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+namespace hydra {
+
+class EnforceNotMet : public std::runtime_error {
+ public:
+  using std::runtime_error::runtime_error;
+};
+
+class IoException : public std::runtime_error {
+ public:
+  using std::runtime_error::runtime_error;
+};
+
+// ---- rendezvous stores (HashStore: threads of one process; FileStore: processes) ----------
+class Store {
+ public:
+  virtual ~Store() = default;
+  virtual void set(const std::string& key, const std::string& value) = 0;
+  virtual std::string get(const std::string& key, std::chrono::milliseconds timeout) = 0;
+};
+
+class HashStore : public Store {
+ public:
+  void set(const std::string& key, const std::string& value) override;
+  std::string get(const std::string& key, std::chrono::milliseconds timeout) override;
+
+ private:
+  std::mutex mu_;
+  std::map<std::string, std::string> kv_;
+};
+
+class FileStore : public Store {
+ public:
+  explicit FileStore(std::string dir) : dir_(std::move(dir)) {}
+  void set(const std::string& key, const std::string& value) override;
+  std::string get(const std::string& key, std::chrono::milliseconds timeout) override;
+
+ private:
+  std::string dir_;
+};
+
+namespace transport {
+class Pair;
+class Device;
+}  // namespace transport
+
+// A buffer registered with the context: non-owning (ptr, size) view that can be the source of
+// sends and the target of receives (gloo::transport::UnboundBuffer, unbound_buffer.h:32-120).
+class UnboundBuffer {
+ public:
+  UnboundBuffer(class Context* ctx, void* ptr, size_t size) : ctx_(ctx), ptr(ptr), size(size) {}
+  ~UnboundBuffer();
+  void send(int dst, uint64_t slot, size_t offset, size_t nbytes);
+  void recv(int src, uint64_t slot, size_t offset, size_t nbytes);
+  void waitSend(std::chrono::milliseconds timeout);  // oldest outstanding send completes
+  void waitRecv(std::chrono::milliseconds timeout);  // oldest outstanding recv completes
+
+  Context* const ctx_;
+  void* const ptr;
+  const size_t size;
+
+  struct Op;
+  std::mutex mu_;
+  std::vector<std::shared_ptr<Op>> sends_, recvs_;
+};
+
+class Context {
+ public:
+  Context(int rank, int size);
+  ~Context();
+  Context(const Context&) = delete;
+  Context& operator=(const Context&) = delete;
+
+  // Full mesh over TCP on `host` (ephemeral ports published through the store under `prefix`).
+  void connectFullMesh(Store& store, const std::string& host = "127.0.0.1",
+                       const std::string& prefix = "hydra");
+  std::unique_ptr<UnboundBuffer> createUnboundBuffer(void* ptr, size_t size) {
+    return std::unique_ptr<UnboundBuffer>(new UnboundBuffer(this, ptr, size));
+  }
+  void setTimeout(std::chrono::milliseconds t) { timeout_ = t; }
+  std::chrono::milliseconds getTimeout() const { return timeout_; }
+  transport::Pair* getPair(int peer);
+  void closeConnections();
+
+  const int rank;
+  const int size;
+
+ private:
+  std::chrono::milliseconds timeout_{30000};  // gloo/gloo/context.cc:18
+  std::vector<std::unique_ptr<transport::Pair>> pairs_;
+};
+
+class AllreduceOptions {
+ public:
+  using Func = std::function<void(void*, const void*, const void*, size_t)>;
+  enum Algorithm { UNSPECIFIED = 0, RING = 1, BCUBE = 2 };
+  static constexpr size_t kMaxSegmentSize = 1024 * 1024;  // allreduce.h:78
+
+  explicit AllreduceOptions(const std::shared_ptr<Context>& context)
+      : context(context), timeout(context->getTimeout()) {}
+
+  void setAlgorithm(Algorithm a) { algorithm = a; }
+  template <typename T>
+  void setInput(T* ptr, size_t n) { setInputs(&ptr, 1, n); }
+  template <typename T>
+  void setInputs(std::vector<T*> ptrs, size_t n) { setInputs(ptrs.data(), ptrs.size(), n); }
+  template <typename T>
+  void setInputs(T** ptrs, size_t len, size_t n) {
+    setBufs(in, reinterpret_cast<void**>(ptrs), len, n, sizeof(T));
+  }
+  template <typename T>
+  void setOutput(T* ptr, size_t n) { setOutputs(&ptr, 1, n); }
+  template <typename T>
+  void setOutputs(std::vector<T*> ptrs, size_t n) { setOutputs(ptrs.data(), ptrs.size(), n); }
+  template <typename T>
+  void setOutputs(T** ptrs, size_t len, size_t n) {
+    setBufs(out, reinterpret_cast<void**>(ptrs), len, n, sizeof(T));
+  }
+  // untyped forms (element size explicit), for C callers
+  void setInputsRaw(void** ptrs, size_t len, size_t n, size_t esize) {
+    setBufs(in, ptrs, len, n, esize);
+  }
+  void setOutputsRaw(void** ptrs, size_t len, size_t n, size_t esize) {
+    setBufs(out, ptrs, len, n, esize);
+  }
+  void setReduceFunction(Func fn) { reduce = std::move(fn); }
+  void setTag(uint32_t t) { tag = t; }
+  void setMaxSegmentSize(size_t s) { maxSegmentSize = s; }
+  void setTimeout(std::chrono::milliseconds t) { timeout = t; }
+
+  std::shared_ptr<Context> context;
+  std::chrono::milliseconds timeout;
+  Algorithm algorithm = UNSPECIFIED;
+  std::vector<std::unique_ptr<UnboundBuffer>> in, out;
+  size_t elements = 0, elementSize = 0;
+  Func reduce;
+  uint32_t tag = 0;
+  size_t maxSegmentSize = kMaxSegmentSize;
+
+ private:
+  void setBufs(std::vector<std::unique_ptr<UnboundBuffer>>& v, void** ptrs, size_t len, size_t n,
+               size_t esize) {
+    elements = n;
+    elementSize = esize;
+    v.clear();
+    for (size_t i = 0; i < len; i++) v.push_back(context->createUnboundBuffer(ptrs[i], n * esize));
+  }
+};
+
+void allreduce(const AllreduceOptions& opts);
+
+// ---- bew_allreduce_a: the buffer split over two rails, two concurrent rings ----------------
+enum class SplitTable { AA, AG };  // calculateElements_AA (default) / _AG (env ALLREDUCE_GLEX)
+void calculateElements(SplitTable t, int P, size_t n, size_t* e1, size_t* e2);
+
+class APipeAllreduceOptions {
+ public:
+  APipeAllreduceOptions(const std::shared_ptr<Context>& context,
+                        const std::shared_ptr<Context>& context2)
+      : opts3(context), opts2(context2), size_(context->size) {}
+  template <typename T>
+  void setInput(T* ptr, size_t n) { setSplit(reinterpret_cast<char*>(ptr), n, sizeof(T), true); }
+  template <typename T>
+  void setOutput(T* ptr, size_t n) { setSplit(reinterpret_cast<char*>(ptr), n, sizeof(T), false); }
+  void setInputRaw(void* p, size_t n, size_t es) { setSplit(static_cast<char*>(p), n, es, true); }
+  void setOutputRaw(void* p, size_t n, size_t es) { setSplit(static_cast<char*>(p), n, es, false); }
+  void setReduceFunction(AllreduceOptions::Func fn) {
+    opts2.setReduceFunction(fn);
+    opts3.setReduceFunction(fn);
+  }
+  void setAlgorithm(AllreduceOptions::Algorithm a) {
+    opts2.setAlgorithm(a);
+    opts3.setAlgorithm(a);
+  }
+  void setSplitTable(SplitTable t) { table_ = t; }
+
+  AllreduceOptions opts3;  // rail 1: elements [0, e1) on `context`   (pipeallreduce-a.h:51-53)
+  AllreduceOptions opts2;  // rail 2: elements [e1, n) on `context2`
+
+ private:
+  void setSplit(char* p, size_t n, size_t es, bool input);
+  int size_;
+  SplitTable table_ = SplitTable::AA;
+};
+
+void apipe_allreduce(APipeAllreduceOptions& opts);
+
+}  // namespace hydra

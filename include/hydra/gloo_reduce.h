@@ -1,0 +1,119 @@
+// include/hydra/gloo_reduce.h -- header-only C++ shim: libhydra_hip.so behind Gloo's
+// reduction plug-points.  Drop-in for a Gloo/hydra build (no Gloo headers needed here: the
+// shim produces the exact callable shapes Gloo consumes).
+//
+//   gloo::AllreduceOptions::Func = std::function<void(void*, const void*, const void*, size_t)>
+//       (gloo/gloo/allreduce.h:36, set with setReduceFunction :179-181, called at
+//        allreduce.cc:301-305 with c == a == out[0]+recvOffset, b == tmp scratch)
+//     -> hydra::gloo_compat::hostSum<T>()      host buffers (what gloo's ring hands over):
+//                                               staged H2D -> gfx950 kernel -> D2H, synchronous
+//     -> hydra::gloo_compat::deviceSum<T>(s)   device buffers, enqueued on stream s
+//   gloo::ReductionFunction<T>::Function = void(T*, const T*, size_t)  (algorithm.h:59-96)
+//     -> hydra::gloo_compat::hostSumInPlace<T>  (for ReductionFunction<T>{SUM, &fn})
+//   gloo::CudaReductionFunction<T> device fn  void(T*, const T*, size_t, stream) (cuda.h:286-350)
+//     -> hydra::gloo_compat::deviceSumInPlace<T>
+//
+// Errors: a non-zero hydra status throws hydra::gloo_compat::EnforceNotMet carrying
+// hydra_last_error(), like GLOO_ENFORCE -> gloo::EnforceNotMet (gloo/gloo/common/logging.h:21,42).
+// Threading: one staging context per calling thread (thread_local), so the two rails of
+// bew_allreduce_a (pipeallreduce-a.cc:32-50) reduce concurrently without sharing state.
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+#include <functional>
+#include <stdexcept>
+#include <string>
+#include <type_traits>
+
+#include "../hydra_hip.h"
+
+namespace hydra {
+namespace gloo_compat {
+
+class EnforceNotMet : public std::runtime_error {
+ public:
+  EnforceNotMet(int code, const std::string& what)
+      : std::runtime_error("[hydra_hip] " + what + " (status " + std::to_string(code) + ")"),
+        code_(code) {}
+  int code() const { return code_; }
+
+ private:
+  int code_;
+};
+
+inline void enforce(int rc) {
+  if (rc != HYDRA_OK) throw EnforceNotMet(rc, hydra_last_error());
+}
+
+// dtype tag of a C++ element type (gloo::float16 is a 2-byte struct: pass HYDRA_FLOAT16 via
+// the explicit overloads below; bf16 likewise).
+template <typename T>
+constexpr int dtype_of() {
+  static_assert(std::is_arithmetic<T>::value, "use the explicit-dtype overloads for f16/bf16");
+  return std::is_same<T, float>::value      ? HYDRA_FLOAT32
+         : std::is_same<T, double>::value   ? HYDRA_FLOAT64
+         : std::is_same<T, int8_t>::value   ? HYDRA_INT8
+         : std::is_same<T, uint8_t>::value  ? HYDRA_UINT8
+         : std::is_same<T, int32_t>::value  ? HYDRA_INT32
+         : std::is_same<T, uint32_t>::value ? HYDRA_UINT32
+         : std::is_same<T, int64_t>::value  ? HYDRA_INT64
+         : std::is_same<T, uint64_t>::value ? HYDRA_UINT64
+         : (sizeof(T) == 8 && std::is_unsigned<T>::value) ? HYDRA_UINT64
+         : (sizeof(T) == 8) ? HYDRA_INT64
+                            : -1;
+}
+
+// Per-thread staging context for host-resident buffers.
+class ThreadContext {
+ public:
+  static hydra_ctx_t get(int device = 0) {
+    thread_local ThreadContext tc(device);
+    return tc.ctx_;
+  }
+  ~ThreadContext() { hydra_ctx_destroy(ctx_); }
+
+ private:
+  explicit ThreadContext(int device) { enforce(hydra_ctx_create(device, &ctx_)); }
+  hydra_ctx_t ctx_ = nullptr;
+};
+
+using Func = std::function<void(void*, const void*, const void*, size_t)>;
+
+// --- AllreduceOptions::Func ------------------------------------------------------------------
+inline Func hostReduce(int op, int dtype, int device = 0) {
+  return [op, dtype, device](void* c, const void* a, const void* b, size_t n) {
+    enforce(hydra_reduce_host(ThreadContext::get(device), op, dtype, c, a, b, n));
+  };
+}
+
+template <typename T>
+Func hostSum(int device = 0) {
+  return hostReduce(HYDRA_SUM, dtype_of<T>(), device);
+}
+
+inline Func deviceReduce(int op, int dtype, hydra_stream_t stream = nullptr) {
+  return [op, dtype, stream](void* c, const void* a, const void* b, size_t n) {
+    enforce(hydra_reduce(op, dtype, c, a, b, n, stream));
+  };
+}
+
+template <typename T>
+Func deviceSum(hydra_stream_t stream = nullptr) {
+  return deviceReduce(HYDRA_SUM, dtype_of<T>(), stream);
+}
+
+// --- ReductionFunction<T>::Function (x = op(x, y)) ---------------------------------------------
+template <typename T>
+void hostSumInPlace(T* x, const T* y, size_t n) {
+  enforce(hydra_reduce_host(ThreadContext::get(), HYDRA_SUM, dtype_of<T>(), x, x, y, n));
+}
+
+// --- CudaReductionFunction<T> device function shape (x = op(x, y) on a stream) ---------------
+template <typename T>
+void deviceSumInPlace(T* x, const T* y, size_t n, hydra_stream_t stream) {
+  enforce(hydra_reduce(HYDRA_SUM, dtype_of<T>(), x, x, y, n, stream));
+}
+
+}  // namespace gloo_compat
+}  // namespace hydra

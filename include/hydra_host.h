@@ -1,0 +1,53 @@
+/*
+ * hydra_host.h -- C entry points of libhydra_host.so, the C++ host runtime (include/hydra/allreduce.h)
+ * that mirrors hydra/Gloo's new_allreduce_ring and bew_allreduce_a over loopback TCP with the
+ * per-segment reduction offloaded to the MI355X through include/hydra_hip.h.
+ *
+ * Ranks run as threads of the calling process, sharing an in-process store -- the reference's own
+ * test harness (gloo/gloo/test/base_test.h:116-156).  Used by tests/ and bench.py.
+ *
+ * reducer: HYDRA_REDUCER_GPU  -> hydra_reduce_host (H2D -> gfx950 kernel -> D2H, synchronous)
+ *          HYDRA_REDUCER_FN   -> the caller's function (CPU-side tests plug the oracle in here)
+ */
+#ifndef HYDRA_HOST_H_
+#define HYDRA_HOST_H_
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void (*hydra_reduce_fn)(void* c, const void* a, const void* b, size_t n);
+#define HYDRA_REDUCER_GPU 0
+#define HYDRA_REDUCER_FN 1
+#define HYDRA_SPLIT_AA 0 /* calculateElements_AA, pipeallreduce-a.h:296-376 (default) */
+#define HYDRA_SPLIT_AG 1 /* calculateElements_AG, pipeallreduce-a.h:137-294 (ALLREDUCE_GLEX) */
+
+/* gloo::allreduce (RING) on P thread-ranks.  in/out: P*nptr pointers [rank][ptr]; in == NULL is
+ * in place (allreduce_test.cc:302-350).  timeout_ms <= 0: context default (30 s). */
+int hydra_host_allreduce_threads(int P, int nptr, int op, int dtype, size_t n, void** in,
+                                 void** out, size_t max_segment, int reducer, hydra_reduce_fn fn,
+                                 long timeout_ms, char* err, size_t errlen);
+
+/* gloo::apipe_allreduce (bew_allreduce_a) on P thread-ranks with two loopback rails each.
+ * in/out: P pointers each. */
+int hydra_host_apipe_threads(int P, int dtype, size_t n, void** in, void** out, int table,
+                             int reducer, hydra_reduce_fn fn, char* err, size_t errlen);
+
+/* The reference benchmark bodies on P thread-ranks: config 1 = NewAllreduceBenchmark
+ * (benchmark/main.cc:321-358), config 3 = aAllreduceBenchmark (main.cc:629-664).  Rank 0's
+ * per-iteration wall time in ns goes to samples_ns[iters]. */
+int hydra_host_bench(int config, int P, size_t n, int warmup, int iters, int reducer,
+                     hydra_reduce_fn fn, double* samples_ns, char* err, size_t errlen);
+
+void hydra_host_calculate_elements(int table, int P, size_t n, size_t* e1, size_t* e2);
+
+/* AllreduceNewTest.TestTimeout (allreduce_test.cc:381-397): rank 0 of 2 times out; returns 0 and
+ * the IoException text if it was raised. */
+int hydra_host_timeout_probe(long timeout_ms, char* what, size_t len);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HYDRA_HOST_H_ */

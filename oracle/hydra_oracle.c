@@ -364,3 +364,10 @@ void orc_split_ag(int P, size_t n, size_t* e1, size_t* e2) {
   }
   split_finish(n, ce, w, e1, e2);
 }
+
+/* ---- AllreduceOptions::Func-shaped entry points (void(void*, const void*, const void*, size_t),
+ *      gloo/gloo/allreduce.h:36) so host-runtime tests can plug the oracle in as the reducer. ---- */
+void orc_sum_f32(void* c, const void* a, const void* b, size_t n) { orc_op(OP_SUM, D_FLOAT32, c, a, b, n); }
+void orc_sum_i32(void* c, const void* a, const void* b, size_t n) { orc_op(OP_SUM, D_INT32, c, a, b, n); }
+void orc_sum_u64(void* c, const void* a, const void* b, size_t n) { orc_op(OP_SUM, D_UINT64, c, a, b, n); }
+void orc_sum_f16(void* c, const void* a, const void* b, size_t n) { orc_op(OP_SUM, D_FLOAT16, c, a, b, n); }

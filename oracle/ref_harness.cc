@@ -240,3 +240,9 @@ int ref_bench_ring(int P, size_t n, int warmup, int iters, double* samples_ns, c
 }
 
 }  // extern "C"
+
+// AllreduceOptions::Func-shaped handle on the reference's own gloo::sum<float> (math.h:15-23),
+// so the host runtime's bench can use the reference reduction as its CPU baseline reducer.
+extern "C" void ref_sum_f32(void* c, const void* a, const void* b, size_t n) {
+  gloo::sum<float>(c, a, b, n);
+}

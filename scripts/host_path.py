@@ -1,0 +1,91 @@
+#!/usr/bin/env python3
+"""Host-resident path measurements: what the reduction costs when the segment
+lives in host memory, as it does in the reference's TCP ring.
+
+  1. isolated: hydra_reduce_host on 1 MiB / 16 MiB / 64 MiB fp32 segments, pageable vs
+     hipHostRegister'ed buffers, vs the reference's gloo::sum<float> on the same host core
+  2. config 1: new_allreduce_ring, 2 ranks, loopback TCP -- the reference itself (oracle/_ref)
+     vs the hydra C++ host runtime with the GPU reducer
+  3. config 3: bew_allreduce_a, 2 ranks x 2 loopback rails -- hydra host runtime with the
+     reference's gloo::sum<float> as reducer vs the GPU reducer (H2D + sum + D2H per segment)
+Prints one JSON document.
+"""
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import torch  # noqa: E402,F401
+
+from hydra_amd import _lib, host  # noqa: E402
+from hydra_amd.reduce import HostContext  # noqa: E402
+from oracle import oracle as O  # noqa: E402  (CPU baseline only)
+
+L = _lib.lib()
+out = {"host": {"cpus": os.cpu_count()}}
+try:
+    out["host"]["model"] = [ln.split(":")[1].strip() for ln in open("/proc/cpuinfo")
+                            if ln.startswith("model name")][0]
+except Exception:
+    pass
+
+# 1. isolated
+iso = []
+ctx = HostContext(0)
+for n in (1 << 18, 1 << 22, 1 << 24):
+    a = np.arange(n, dtype=np.float32)
+    b = np.ones(n, dtype=np.float32)
+    for mode in ("pageable", "registered"):
+        if mode == "registered":
+            _lib.check(L.hydra_host_register(a.ctypes.data, a.nbytes))
+            _lib.check(L.hydra_host_register(b.ctypes.data, b.nbytes))
+        reps = max(3, int(2e8 / (12 * n)))
+        _lib.check(L.hydra_reduce_host(ctx.handle, 0, 6, a.ctypes.data, a.ctypes.data,
+                                       b.ctypes.data, n))
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            _lib.check(L.hydra_reduce_host(ctx.handle, 0, 6, a.ctypes.data, a.ctypes.data,
+                                           b.ctypes.data, n))
+        dt = (time.perf_counter() - t0) / reps
+        if mode == "registered":
+            L.hydra_host_unregister(a.ctypes.data)
+            L.hydra_host_unregister(b.ctypes.data)
+        iso.append({"elements": n, "mode": mode, "us": round(dt * 1e6, 1),
+                    "GBps_12B": round(12 * n / dt / 1e9, 2)})
+    cpu = O.ref_time_sum(6, a, a, b, max(3, int(1e8 / (12 * n))), 3) if O.ref_available() else None
+    if cpu:
+        iso.append({"elements": n, "mode": "reference gloo::sum<float>, 1 core",
+                    "us": round(cpu * 1e6, 1), "GBps_12B": round(12 * n / cpu / 1e9, 2)})
+ctx.close()
+out["isolated"] = iso
+
+
+def dist(s, n):
+    s = np.sort(s)
+    return {"elements": n, "min_us": round(s[0] / 1e3, 1),
+            "p50_us": round(float(np.percentile(s, 50)) / 1e3, 1),
+            "p99_us": round(float(np.percentile(s, 99)) / 1e3, 1),
+            "avg_us": round(float(s.mean()) / 1e3, 1),
+            "GiBps": round(4 * n * len(s) / (s.sum() * 1e-9) / 2**30, 3)}  # runner.cc:631-635
+
+
+ref_fn = ctypes.cast(O.ref().ref_sum_f32, ctypes.c_void_p).value if O.ref_available() else None
+sizes = [4, 4096, 262144, 1 << 20, 1 << 22, 1 << 24]
+c1, c3 = [], []
+for n in sizes:
+    iters = 20 if n >= 1 << 22 else 50
+    if O.ref_available():
+        c1.append({"impl": "reference (gloo, CPU sum)", **dist(O.ref_bench_ring(2, n, 3, iters), n)})
+    c1.append({"impl": "hydra host runtime, GPU sum", **dist(host.bench(1, 2, n, 3, iters), n)})
+    if ref_fn:
+        c3.append({"impl": "hydra split + reference gloo::sum (CPU)",
+                   **dist(host.bench(3, 2, n, 3, iters, reducer_fn=ref_fn), n)})
+    c3.append({"impl": "hydra split, GPU sum (H2D+sum+D2H)", **dist(host.bench(3, 2, n, 3, iters), n)})
+out["config1_new_allreduce_ring_P2"] = c1
+out["config3_bew_allreduce_a_P2"] = c3
+print(json.dumps(out))

@@ -1,0 +1,51 @@
+"""Host-resident path on the GPU: the C++ host runtime's ring and two-rail split with every
+segment reduced on the MI355X (hydra_reduce_host: H2D -> gfx950 kernel -> D2H), bit-exact vs
+the reference ring."""
+import numpy as np
+import pytest
+
+from hydra_amd import host, synth
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("P,n,ms", [(2, 100, 0), (2, 262145, 0), (3, 100003, 4096),
+                                    (4, 1 << 20, 0)])
+def test_host_ring_gpu_reducer(gpu, O, P, n, ms):
+    xs = [synth.stress_f32(P, r, n) for r in range(P)]
+    outs = [[x.copy()] for x in xs]
+    host.allreduce_threads(outs, None, max_segment=ms)  # GPU reducer
+    exp = O.ring_result(xs, ms or (1 << 20))
+    for r in range(P):
+        assert np.array_equal(outs[r][0].view(np.uint32), exp.view(np.uint32))
+
+
+def test_host_ring_gpu_reducer_multi_input(gpu, O):
+    """2 inputs per rank out of place: local pre-reduction also runs on the GPU."""
+    P, n = 2, 50001
+    ins = [[synth.stress_f32(P, r, n, seed=7 + i) for i in range(2)] for r in range(P)]
+    outs = [[np.zeros(n, np.float32) for _ in range(2)] for _ in range(P)]
+    host.allreduce_threads(outs, ins, max_segment=8192)
+    o2 = [[np.zeros(n, np.float32) for _ in range(2)] for _ in range(P)]
+    O.allreduce(P, o2, ins, max_segment=8192)
+    for r in range(P):
+        for i in range(2):
+            assert np.array_equal(outs[r][i].view(np.uint32), o2[r][i].view(np.uint32))
+
+
+@pytest.mark.parametrize("n", [1000, 1500001])
+def test_apipe_gpu_reducer(gpu, O, n):
+    """bew_allreduce_a with both rails reducing concurrently on one GPU (one staging context
+    per rail thread)."""
+    P = 2
+    ins = [synth.stress_f32(P, r, n) for r in range(P)]
+    outs = [np.zeros(n, np.float32) for _ in range(P)]
+    host.apipe_threads(ins, outs)
+    e1, e2 = O.split_aa(P, n)
+    exp = np.empty(n, np.float32)
+    if e1:
+        exp[:e1] = O.ring_result([x[:e1].copy() for x in ins])
+    if e2:
+        exp[e1:] = O.ring_result([x[e1:].copy() for x in ins])
+    for r in range(P):
+        assert np.array_equal(outs[r].view(np.uint32), exp.view(np.uint32))

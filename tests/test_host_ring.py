@@ -1,0 +1,100 @@
+"""The C++ host runtime (libhydra_host.so) on the CPU: thread-per-rank over loopback TCP, as the
+reference's own tests run (gloo/gloo/test/base_test.h:116-156).  The reducer is the oracle here
+(the GPU reducer is exercised by tests/test_gpu_host.py); what is tested is the ring schedule,
+the segment geometry, local reduce/broadcast, the transport, timeouts and the rail split."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from hydra_amd import host, synth
+
+
+def fnptr(O, name):
+    return ctypes.cast(getattr(O.orc(), name), ctypes.c_void_p).value
+
+
+@pytest.mark.parametrize("P", [1, 2, 4, 7])
+@pytest.mark.parametrize("nptr", [1, 2, 3])
+@pytest.mark.parametrize("inplace", [True, False])
+def test_allreduce_new_test_default(O, P, nptr, inplace):
+    """AllreduceNewTest.Default (test/allreduce_test.cc:302-362): uint64, maxSegmentSize=128."""
+    for n in (1, 10, 100, 1000):
+        stride = P * nptr
+        vals = [[np.arange(n, dtype=np.uint64) * stride + r * nptr + i for i in range(nptr)]
+                for r in range(P)]
+        if inplace:
+            outs, ins = [[v.copy() for v in vr] for vr in vals], None
+        else:
+            outs = [[np.zeros(n, np.uint64) for _ in range(nptr)] for _ in range(P)]
+            ins = vals
+        host.allreduce_threads(outs, ins, max_segment=128, reducer_fn=fnptr(O, "orc_sum_u64"))
+        exp = np.arange(n, dtype=np.uint64) * stride * stride + np.uint64(stride * (stride - 1) // 2)
+        for r in range(P):
+            for i in range(nptr):
+                assert np.array_equal(outs[r][i], exp), (P, nptr, n, inplace)
+
+
+@pytest.mark.parametrize("P,n,ms", [(2, 100, 0), (3, 1001, 128), (4, 262145, 0),
+                                    (5, 10007, 4096), (8, 40009, 1024)])
+def test_fold_order_bit_exact(O, P, n, ms):
+    """fp32 stress inputs: the host ring equals the reference ring bit for bit."""
+    xs = [synth.stress_f32(P, r, n) for r in range(P)]
+    outs = [[x.copy()] for x in xs]
+    host.allreduce_threads(outs, None, max_segment=ms, reducer_fn=fnptr(O, "orc_sum_f32"))
+    exp = O.ring_result(xs, ms or (1 << 20))
+    for r in range(P):
+        assert np.array_equal(outs[r][0].view(np.uint32), exp.view(np.uint32))
+
+
+def test_float16_quirk_through_ring(O):
+    P, n = 3, 5000
+    rng = np.random.default_rng(8)
+    hs = [np.array([O.f2h(float(v)) for v in rng.integers(0, 5, n)], np.uint16) for _ in range(P)]
+    outs = [[h.copy()] for h in hs]
+    host.allreduce_threads(outs, None, dtype_code=8, max_segment=256,
+                           reducer_fn=fnptr(O, "orc_sum_f16"))
+    exp = O.ring_result(hs, 256, dtype_code=8)
+    assert all(np.array_equal(o[0], exp) for o in outs)
+
+
+@pytest.mark.parametrize("table", [host.SPLIT_AA, host.SPLIT_AG])
+@pytest.mark.parametrize("P", [2, 3, 4, 6, 8])
+def test_split_tables_match_restatement(O, table, P):
+    fn = O.split_aa if table == host.SPLIT_AA else O.split_ag
+    ns = [1, 1000, 6144, 6145, 65535, 65536, 65537, 131071, 131072, 262144, 262145, 524288,
+          524289, 828343, 828344, 1048576, 1048577, 1500000, 1500001, 2097152, 2097153, 4194304,
+          4194305, 8388608, 16777216, 16777217, 33554432, 33554433, 67108864, 67108865]
+    for n in ns:
+        assert host.calculate_elements(table, P, n) == fn(P, n), (P, n)
+
+
+@pytest.mark.parametrize("P,n", [(2, 1000), (2, 65536), (2, 1500001), (3, 200003),
+                                 (4, 1 << 20)])
+def test_apipe_two_rails(O, P, n):
+    """bew_allreduce_a: split by calculateElements_AA, two concurrent rings on two rails
+    (pipeallreduce-a.cc:27-61); each part equals an independent reference ring on its slice."""
+    ins = [synth.stress_f32(P, r, n) for r in range(P)]
+    outs = [np.zeros(n, np.float32) for _ in range(P)]
+    host.apipe_threads(ins, outs, reducer_fn=fnptr(O, "orc_sum_f32"))
+    e1, e2 = O.split_aa(P, n)
+    exp = np.empty(n, np.float32)
+    if e1:
+        exp[:e1] = O.ring_result([x[:e1].copy() for x in ins])
+    if e2:
+        exp[e1:] = O.ring_result([x[e1:].copy() for x in ins])
+    for r in range(P):
+        assert np.array_equal(outs[r].view(np.uint32), exp.view(np.uint32))
+
+
+def test_timeout_raises_io_exception():
+    """AllreduceNewTest.TestTimeout (allreduce_test.cc:381-397)."""
+    rc, what = host.timeout_probe(10)
+    assert rc == 0 and "Timed out" in what
+
+
+def test_bench_bodies_run(O):
+    s = host.bench(1, 2, 1 << 16, 1, 3, reducer_fn=fnptr(O, "orc_sum_f32"))
+    assert s.shape == (3,) and np.all(s > 0)
+    s = host.bench(3, 2, 1 << 16, 1, 3, reducer_fn=fnptr(O, "orc_sum_f32"))
+    assert np.all(s > 0)
