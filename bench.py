@@ -44,6 +44,8 @@ def parse():
                    help="bounded CPU-baseline sample (seconds of reference gloo::sum work)")
     p.add_argument("--sweep", action="store_true", help="add the 4 Ki..64 Mi size sweep")
     p.add_argument("--algo", default="auto", help="ring algorithm for N>1 (see hydra_amd.ring)")
+    p.add_argument("--force-dist", action="store_true",
+                   help="run the N>1 (RCCL) path even at world size 1 (code-path check)")
     return p.parse_args()
 
 
@@ -212,6 +214,11 @@ def run_multi(args):
     from hydra_amd import ring
 
     ws, rank, local = dist_env()
+    if ws == 1:  # --force-dist without a launcher
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist.init_process_group("nccl", device_id=dev)
@@ -230,7 +237,7 @@ def main():
         if ws == 1:
             raise SystemExit(f"--gpus {args.gpus} needs torch.distributed.run with "
                              f"--nproc-per-node {args.gpus}")
-    if ws > 1:
+    if ws > 1 or args.force_dist:
         run_multi(args)
     else:
         run_single(args)

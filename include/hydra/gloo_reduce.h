@@ -15,16 +15,18 @@
 //
 // Errors: a non-zero hydra status throws hydra::gloo_compat::EnforceNotMet carrying
 // hydra_last_error(), like GLOO_ENFORCE -> gloo::EnforceNotMet (gloo/gloo/common/logging.h:21,42).
-// Threading: one staging context per calling thread (thread_local), so the two rails of
-// bew_allreduce_a (pipeallreduce-a.cc:32-50) reduce concurrently without sharing state.
+// Threading: staging contexts come from a process-wide pool (one per concurrent caller), so the
+// two rails of bew_allreduce_a (pipeallreduce-a.cc:32-50) reduce concurrently without sharing.
 #pragma once
 
 #include <cstddef>
 #include <cstdint>
 #include <functional>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <type_traits>
+#include <vector>
 
 #include "../hydra_hip.h"
 
@@ -64,18 +66,58 @@ constexpr int dtype_of() {
                             : -1;
 }
 
-// Per-thread staging context for host-resident buffers.
-class ThreadContext {
+// Staging contexts for host-resident buffers: a process-wide pool.  A reduce call takes a free
+// context for its duration, so concurrent callers (the two rails of bew_allreduce_a) never share
+// one, and callers on short-lived threads (apipe_allreduce spawns its rail threads per call,
+// pipeallreduce-a.cc:32-50) reuse contexts instead of creating device buffers every time.
+class ContextPool {
  public:
-  static hydra_ctx_t get(int device = 0) {
-    thread_local ThreadContext tc(device);
-    return tc.ctx_;
+  class Lease {
+   public:
+    Lease(ContextPool* p, hydra_ctx_t c) : p_(p), c_(c) {}
+    Lease(Lease&& o) noexcept : p_(o.p_), c_(o.c_) { o.c_ = nullptr; }
+    Lease(const Lease&) = delete;
+    Lease& operator=(const Lease&) = delete;
+    ~Lease() {
+      if (c_) p_->release(c_);
+    }
+    hydra_ctx_t get() const { return c_; }
+
+   private:
+    ContextPool* p_;
+    hydra_ctx_t c_;
+  };
+
+  static ContextPool& instance(int device = 0) {
+    static ContextPool pool(device);  // one pool per process (device of the first caller)
+    return pool;
   }
-  ~ThreadContext() { hydra_ctx_destroy(ctx_); }
+  Lease acquire() {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      if (!free_.empty()) {
+        hydra_ctx_t c = free_.back();
+        free_.pop_back();
+        return Lease(this, c);
+      }
+    }
+    hydra_ctx_t c = nullptr;
+    enforce(hydra_ctx_create(device_, &c));
+    return Lease(this, c);
+  }
+  ~ContextPool() {
+    for (auto c : free_) hydra_ctx_destroy(c);
+  }
 
  private:
-  explicit ThreadContext(int device) { enforce(hydra_ctx_create(device, &ctx_)); }
-  hydra_ctx_t ctx_ = nullptr;
+  explicit ContextPool(int device) : device_(device) {}
+  void release(hydra_ctx_t c) {
+    std::lock_guard<std::mutex> g(mu_);
+    free_.push_back(c);
+  }
+  int device_;
+  std::mutex mu_;
+  std::vector<hydra_ctx_t> free_;
 };
 
 using Func = std::function<void(void*, const void*, const void*, size_t)>;
@@ -83,7 +125,8 @@ using Func = std::function<void(void*, const void*, const void*, size_t)>;
 // --- AllreduceOptions::Func ------------------------------------------------------------------
 inline Func hostReduce(int op, int dtype, int device = 0) {
   return [op, dtype, device](void* c, const void* a, const void* b, size_t n) {
-    enforce(hydra_reduce_host(ThreadContext::get(device), op, dtype, c, a, b, n));
+    auto lease = ContextPool::instance(device).acquire();
+    enforce(hydra_reduce_host(lease.get(), op, dtype, c, a, b, n));
   };
 }
 
@@ -106,7 +149,8 @@ Func deviceSum(hydra_stream_t stream = nullptr) {
 // --- ReductionFunction<T>::Function (x = op(x, y)) ---------------------------------------------
 template <typename T>
 void hostSumInPlace(T* x, const T* y, size_t n) {
-  enforce(hydra_reduce_host(ThreadContext::get(), HYDRA_SUM, dtype_of<T>(), x, x, y, n));
+  auto lease = ContextPool::instance().acquire();
+  enforce(hydra_reduce_host(lease.get(), HYDRA_SUM, dtype_of<T>(), x, x, y, n));
 }
 
 // --- CudaReductionFunction<T> device function shape (x = op(x, y) on a stream) ---------------
