@@ -181,17 +181,40 @@ def bench_allreduce(args, dev) -> dict:
             x, torch.from_numpy(((j % 1024) * (world * (world + 1) // 2)).astype(np.float32))
             .to(dev))
         full_ok = max_over_ranks(0.0 if full_ok else 1.0, dev) == 0.0
-        # 3) timed region
+        # 3) timed region (the reported value: args.algo, auto = direct)
         wall = timed_steps(step, args.steps, args.warmup, sync, dist.barrier)
         wall = max_over_ranks(wall, dev)
         ms = wall / args.steps * 1e3
-        # 4) context: RCCL's own allreduce on the same bucket
-        def rstep():
-            comm.allreduce_(x, algo="rccl")
+        # 4) context: the other algorithms on the same bucket (fewer steps)
+        others = {}
+        k = max(5, args.steps // 4)
+        for a in ("ring", "direct", "rccl"):
+            if a == algo:
+                continue
 
-        rwall = max_over_ranks(timed_steps(rstep, max(5, args.steps // 2), 3, sync,
-                                           dist.barrier), dev)
-        rms = rwall / max(5, args.steps // 2) * 1e3
+            def ostep(a=a):
+                comm.allreduce_(x, algo=a)
+
+            ow = max_over_ranks(timed_steps(ostep, k, 3, sync, dist.barrier), dev)
+            others[a] = round(ow / k * 1e3, 4)
+        # 5) BASELINE config 5: bf16 bucket of 256 Mi elements, fp32 accumulation
+        c5 = None
+        if not getattr(args, "no_config5", False):
+            n5 = 256 << 20
+            xb = torch.from_numpy(synth.bf16_bits((j[: 1 << 20] % 7 - 3).astype(np.float32))
+                                  .view(np.int16)).to(dev).repeat(n5 >> 20)
+
+            def bstep():
+                comm.allreduce_(xb, algo="direct", dtype_code=_lib.BFLOAT16, flags=_lib.ACC_F32)
+
+            k5 = max(5, args.steps // 10)
+            bw = max_over_ranks(timed_steps(bstep, k5, 2, sync, dist.barrier), dev)
+            bms = bw / k5 * 1e3
+            b_alg = 2.0 * n5 / (bms * 1e-3) / 1e9
+            c5 = {"elements": n5, "dtype": "bf16 (fp32 accumulate, one rounding)",
+                  "ms": round(bms, 4), "algbw_GBps": round(b_alg, 2),
+                  "busbw_GBps": round(b_alg * 2 * (world - 1) / world, 2)}
+            del xb
     finally:
         comm.close()
     bucket = 4.0 * n
@@ -209,11 +232,11 @@ def bench_allreduce(args, dev) -> dict:
                    "parallelism": f"dp{world}"},
         "algbw_GBps": round(algbw, 2), "busbw_GBps": round(busbw, 2),
         "roofline": {"bound": "xgmi", "achieved": round(busbw, 2),
-                     "peak": round(link * (world - 1), 1), "unit": "GB/s",
-                     "frac": round(busbw / (link * (world - 1)), 4), "traffic": None,
+                     "peak": round(link * max(1, world - 1), 1), "unit": "GB/s",
+                     "frac": round(busbw / (link * max(1, world - 1)), 4), "traffic": None,
                      "note": "busbw vs (P-1) xGMI links x 153 GB/s; a single ring is bound by "
                              "1 link (153 GB/s)"},
-        "rccl_allreduce_ms": round(rms, 4),
-        "rccl_allreduce_busbw_GBps": round(bucket / (rms * 1e-3) / 1e9 * 2 * (world - 1) / world, 2),
+        "other_algos_ms": others,
+        "config5_bf16": c5,
         "parity": {"fold_order_1M": parity, "full_size_exact": bool(full_ok)},
     }
