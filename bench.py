@@ -44,6 +44,9 @@ def parse():
                    help="bounded CPU-baseline sample (seconds of reference gloo::sum work)")
     p.add_argument("--sweep", action="store_true", help="add the 4 Ki..64 Mi size sweep")
     p.add_argument("--algo", default="auto", help="ring algorithm for N>1 (see hydra_amd.ring)")
+    p.add_argument("--watchdog-s", type=float, default=900.0,
+                   help="N>1: abort (exit 3) if the run exceeds this many seconds")
+    p.add_argument("--no-config5", action="store_true", help="N>1: skip the bf16 config-5 leg")
     p.add_argument("--force-dist", action="store_true",
                    help="run the N>1 (RCCL) path even at world size 1 (code-path check)")
     return p.parse_args()
@@ -173,7 +176,7 @@ def run_single(args):
     achieved = algo_bytes / (avg_ms * 1e-3) / 1e9
     traffic = pmc_traffic()
     out = {
-        "metric": "chunk-sum GB/s (fp32) vs HBM peak",
+        "metric": "chunk-sum GB/s (fp32) vs HBM peak; ring-allreduce GB/s at 1/2/4/8 GPU",
         "value": round(value, 2), "unit": "GB/s", "n_gpus": 1, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(wall / args.steps * 1e3, 4),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None,

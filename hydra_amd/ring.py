@@ -150,6 +150,19 @@ def bench_allreduce(args, dev) -> dict:
     from . import synth
 
     rank, world = dist.get_rank(), dist.get_world_size()
+    # a hung collective must fail the run, not stall it: hard exit after `watchdog_s`
+    import os
+    import sys
+    import threading
+
+    def _expire():
+        sys.stderr.write(f"[hydra bench] rank {rank}: watchdog expired, aborting\n")
+        sys.stderr.flush()
+        os._exit(3)
+
+    dog = threading.Timer(float(getattr(args, "watchdog_s", 900)), _expire)
+    dog.daemon = True
+    dog.start()
     uid = exchange_unique_id(rank, dev)
     comm = XgmiComm(rank, world, dev.index, uid)
     n = args.elements
@@ -217,12 +230,13 @@ def bench_allreduce(args, dev) -> dict:
             del xb
     finally:
         comm.close()
+        dog.cancel()
     bucket = 4.0 * n
     algbw = bucket / (ms * 1e-3) / 1e9
     busbw = algbw * 2 * (world - 1) / world
     link = 153.0
     return {
-        "metric": "ring-allreduce GB/s (fp32, whole job) at N GPUs",
+        "metric": "chunk-sum GB/s (fp32) vs HBM peak; ring-allreduce GB/s at 1/2/4/8 GPU",
         "value": round(world * algbw, 2), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",

@@ -93,3 +93,44 @@ def test_single_rank_comm(gpu):
         assert torch.equal(t, torch.arange(1000, dtype=torch.float32, device=gpu))
     finally:
         comm.close()
+
+
+@pytest.mark.parametrize("op", ["sum", "product", "max", "min"])
+@pytest.mark.parametrize("name,code,dt", [("i8", 0, np.int8), ("u64", 5, np.uint64),
+                                          ("f64", 7, np.float64), ("f32", 6, np.float32)])
+def test_simulated_ops_dtypes(gpu, O, op, name, code, dt):
+    """Every op through both plans: the fold kernel and the ring hop keep the reference's
+    c = op(local, received) order for product/max/min too."""
+    import torch
+
+    P, n = 3, 30011
+    rng = np.random.default_rng(code * 7 + len(op))
+    if np.issubdtype(dt, np.integer):
+        xs = [rng.integers(-5 if dt == np.int8 else 0, 6, n).astype(dt) for _ in range(P)]
+    else:
+        xs = [rng.uniform(0.5, 1.5, n).astype(dt) for _ in range(P)]
+    for algo in ("ring", "direct"):
+        bufs = [torch.from_numpy(x.copy().view(np.uint8)).to(gpu) for x in xs]
+        ring.simulate(bufs, algo=algo, op=op, dtype_code=code, max_segment=2048,
+                      chunk_bytes=4096)
+        outs = [[x.copy()] for x in xs]
+        O.allreduce(P, outs, None, kind=op, dtype_code=code, max_segment=2048)
+        for b in bufs:
+            got = b.cpu().numpy().view(dt)
+            assert np.array_equal(got.view(f"u{got.itemsize}"),
+                                  outs[0][0].view(f"u{got.itemsize}")), (algo, op, name)
+
+
+def test_allreduce_argument_checks(gpu):
+    import torch
+
+    uid = ring._rccl_unique_id()
+    comm = ring.XgmiComm(0, 1, gpu.index or 0, uid)
+    try:
+        t = torch.zeros(16, device=gpu)
+        with pytest.raises(_lib.HydraError):
+            comm.allreduce_(t, dtype_code=42)
+        with pytest.raises(_lib.HydraError):
+            comm.allreduce_(t, dtype_code=_lib.FLOAT32, flags=_lib.ACC_F32)
+    finally:
+        comm.close()
