@@ -61,9 +61,11 @@ def reduce_(op: str, c, a, b, n: int | None = None, dtype_code: int | None = Non
     if not (c.is_cuda and a.is_cuda and b.is_cuda):
         raise HydraError(1, "hydra reduce: device tensors required (use reduce_host for host)")
     code = dtype_code if dtype_code is not None else _torch_dtype_code(c)
+    es = _lib.ESIZE[code]
+    cap = min(t.numel() * t.element_size() for t in (c, a, b)) // es  # elements of `code`
     if n is None:
-        n = c.numel()
-    if n > min(c.numel(), a.numel(), b.numel()):
+        n = (c.numel() * c.element_size()) // es
+    if n > cap:
         raise HydraError(1, "n exceeds a tensor's length")
     if not (c.is_contiguous() and a.is_contiguous() and b.is_contiguous()):
         raise HydraError(1, "contiguous tensors required")
@@ -78,11 +80,15 @@ def sum_(c, a, b, n: int | None = None, **kw) -> None:
 
 def acc_bf16_f32_(acc, b_bf16, stream: int | None = None) -> None:
     """acc(fp32) += float(b_bf16): the fp32-accumulate form of a bf16 bucket (config 5)."""
+    if b_bf16.numel() * b_bf16.element_size() < 2 * acc.numel() or acc.dtype.itemsize != 4:
+        raise HydraError(1, "acc must be fp32 and b_bf16 hold at least acc.numel() bf16 values")
     s = stream if stream is not None else _stream_ptr(acc.device)
     check(_lib.lib().hydra_acc_bf16_f32(acc.data_ptr(), b_bf16.data_ptr(), acc.numel(), s))
 
 
 def f32_to_bf16_(out_bf16, acc, stream: int | None = None) -> None:
+    if out_bf16.numel() * out_bf16.element_size() < 2 * acc.numel() or acc.dtype.itemsize != 4:
+        raise HydraError(1, "acc must be fp32 and out_bf16 hold at least acc.numel() values")
     s = stream if stream is not None else _stream_ptr(acc.device)
     check(_lib.lib().hydra_f32_to_bf16(out_bf16.data_ptr(), acc.data_ptr(), acc.numel(), s))
 

@@ -37,9 +37,21 @@ def simulate(bufs, algo: str = "auto", op: str = "sum", dtype_code: int | None =
 
     P = len(bufs)
     code = dtype_code if dtype_code is not None else _torch_dtype_code(bufs[0])
+    n = _count(bufs[0], code)
+    for b in bufs:
+        if _count(b, code) != n or not b.is_contiguous():
+            raise HydraError(1, "simulate: buckets must be contiguous and equally sized")
     ptrs = (ctypes.c_void_p * P)(*[b.data_ptr() for b in bufs])
-    check(_lib.lib().hydra_allreduce_simulate(ALGOS[algo], OPS[op], code, flags, P, ptrs,
-                                              bufs[0].numel(), max_segment, chunk_bytes))
+    check(_lib.lib().hydra_allreduce_simulate(ALGOS[algo], OPS[op], code, flags, P, ptrs, n,
+                                              max_segment, chunk_bytes))
+
+
+def _count(t, code: int) -> int:
+    """elements of dtype `code` in tensor t (t may hold the bits in another dtype)."""
+    nbytes = t.numel() * t.element_size()
+    if nbytes % _lib.ESIZE[code]:
+        raise HydraError(1, "tensor size is not a multiple of the element size")
+    return nbytes // _lib.ESIZE[code]
 
 
 def _rccl_unique_id() -> bytes:
@@ -83,9 +95,12 @@ class XgmiComm:
         from .reduce import _torch_dtype_code
 
         code = dtype_code if dtype_code is not None else _torch_dtype_code(t)
+        if not t.is_contiguous():
+            raise HydraError(1, "allreduce_: contiguous tensor required")
         s = stream if stream is not None else torch.cuda.current_stream(t.device).cuda_stream
         check(_lib.lib().hydra_allreduce(self._h, ALGOS[algo], OPS[op], code, flags,
-                                         t.data_ptr(), t.numel(), max_segment, chunk_bytes, s))
+                                         t.data_ptr(), _count(t, code), max_segment,
+                                         chunk_bytes, s))
 
     def close(self) -> None:
         if self._h:
