@@ -112,6 +112,11 @@ class HostContext:
             self._h = ctypes.c_void_p()
 
     def __del__(self):
+        # never call into HIP/RCCL while the interpreter is finalizing (the runtime may be gone)
+        import sys
+
+        if sys.is_finalizing():
+            return
         try:
             self.close()
         except Exception:

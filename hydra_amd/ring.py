@@ -48,6 +48,8 @@ def simulate(bufs, algo: str = "auto", op: str = "sum", dtype_code: int | None =
 
 def _count(t, code: int) -> int:
     """elements of dtype `code` in tensor t (t may hold the bits in another dtype)."""
+    if code not in _lib.ESIZE:
+        raise HydraError(1, f"invalid dtype code {code}")
     nbytes = t.numel() * t.element_size()
     if nbytes % _lib.ESIZE[code]:
         raise HydraError(1, "tensor size is not a multiple of the element size")
@@ -108,6 +110,11 @@ class XgmiComm:
             self._h = ctypes.c_void_p()
 
     def __del__(self):
+        # never call into HIP/RCCL while the interpreter is finalizing (the runtime may be gone)
+        import sys
+
+        if sys.is_finalizing():
+            return
         try:
             self.close()
         except Exception:

@@ -89,8 +89,10 @@ class ContextPool {
   };
 
   static ContextPool& instance(int device = 0) {
-    static ContextPool pool(device);  // one pool per process (device of the first caller)
-    return pool;
+    // one pool per process (device of the first caller); deliberately never destroyed: at
+    // process exit the HIP runtime may already be torn down, so no HIP call may run then
+    static ContextPool* pool = new ContextPool(device);
+    return *pool;
   }
   Lease acquire() {
     {
@@ -105,10 +107,6 @@ class ContextPool {
     enforce(hydra_ctx_create(device_, &c));
     return Lease(this, c);
   }
-  ~ContextPool() {
-    for (auto c : free_) hydra_ctx_destroy(c);
-  }
-
  private:
   explicit ContextPool(int device) : device_(device) {}
   void release(hydra_ctx_t c) {
