@@ -33,8 +33,9 @@ EXPORTS = [  # every symbol include/hydra_hip.h declares
     "hydra_plan", "hydra_allreduce_simulate",
 ]
 
-ALGO_AUTO, ALGO_RING, ALGO_DIRECT, ALGO_RCCL = range(4)
-ALGOS = {"auto": ALGO_AUTO, "ring": ALGO_RING, "direct": ALGO_DIRECT, "rccl": ALGO_RCCL}
+ALGO_AUTO, ALGO_RING, ALGO_DIRECT, ALGO_RCCL, ALGO_A2A = range(5)
+ALGOS = {"auto": ALGO_AUTO, "ring": ALGO_RING, "direct": ALGO_DIRECT, "rccl": ALGO_RCCL,
+         "a2a": ALGO_A2A}
 ACC_F32 = 1
 UNIQUE_ID_BYTES = 128
 
@@ -47,7 +48,7 @@ class PlanOp(ctypes.Structure):
                 ("wait0", ctypes.c_int32), ("wait1", ctypes.c_int32)]
 
 
-OP_SEND, OP_RECV, OP_GROUP, OP_REDUCE, OP_FOLD = 1, 2, 3, 4, 5
+OP_SEND, OP_RECV, OP_GROUP, OP_REDUCE, OP_FOLD, OP_ALLTOALL, OP_ALLGATHER = 1, 2, 3, 4, 5, 6, 7
 
 
 class HydraError(RuntimeError):

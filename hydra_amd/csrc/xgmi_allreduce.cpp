@@ -67,18 +67,25 @@ int check_plan_args(int algo, int op, int dtype, int flags, size_t* esize) {
   *esize = hydra::dtype_size(dtype);
   if (!*esize) return fail(HYDRA_ERR_INVALID, "invalid dtype");
   if (op < HYDRA_SUM || op > HYDRA_MIN) return fail(HYDRA_ERR_INVALID, "invalid op");
-  if (algo < HYDRA_ALGO_AUTO || algo > HYDRA_ALGO_RCCL)
+  if (algo < HYDRA_ALGO_AUTO || algo > HYDRA_ALGO_A2A)
     return fail(HYDRA_ERR_INVALID, "invalid algorithm");
   if (flags & HYDRA_ACC_F32) {
     if (dtype != HYDRA_BFLOAT16)
       return fail(HYDRA_ERR_UNSUPPORTED, "HYDRA_ACC_F32 needs a bf16 bucket");
     if (algo == HYDRA_ALGO_RING)
-      return fail(HYDRA_ERR_UNSUPPORTED, "HYDRA_ACC_F32 runs on the DIRECT algorithm");
+      return fail(HYDRA_ERR_UNSUPPORTED, "HYDRA_ACC_F32 runs on the DIRECT/A2A algorithms");
   }
   return HYDRA_OK;
 }
 
 int resolve_algo(int algo) { return algo == HYDRA_ALGO_AUTO ? HYDRA_ALGO_DIRECT : algo; }
+
+int check_geometry(int algo, const hydra::PlanGeom& g) {
+  if (algo == HYDRA_ALGO_A2A && !hydra::blocks_equal(g))
+    return fail(HYDRA_ERR_UNSUPPORTED,
+                "A2A needs equal blocks (n*esize a multiple of P*S*segmentBytes)");
+  return HYDRA_OK;
+}
 
 // ops that another op waits on need an event
 std::vector<char> waited_set(const std::vector<hydra::PlanOp>& ops) {
@@ -97,7 +104,7 @@ hipError_t launch_compute(const hydra::PlanOp& o, int op, int dtype, bool acc32,
                                 (size_t)o.bytes / esize, st);
   const void* srcs[hydra::kMaxRanks];
   srcs[0] = user + o.off;
-  for (int j = 1; j < o.nsrc; j++) srcs[j] = scratch + o.src_off + (int64_t)(j - 1) * o.slot_stride;
+  for (int j = 1; j < o.nsrc; j++) srcs[j] = scratch + hydra::fold_slot(o, j);
   return hydra::launch_fold(op, dtype, acc32, user + o.off, srcs, o.nsrc, (size_t)o.bytes / esize,
                             st);
 }
@@ -146,6 +153,18 @@ int run_plan_rccl(hydra_comm* c, int op, int dtype, bool acc32, char* user, hipS
   size_t i = 0;
   while (i < ops.size()) {
     const hydra::PlanOp& o = ops[i];
+    if (o.kind == hydra::kOpAllToAll || o.kind == hydra::kOpAllGather) {
+      wait_on(c->cs, o, c->events);
+      if (o.kind == hydra::kOpAllToAll)
+        NCCL_TRY(ncclAllToAll(user + o.off, scratch + o.src_off, (size_t)o.bytes, ncclUint8,
+                              c->nccl, c->cs));
+      else
+        NCCL_TRY(ncclAllGather(user + o.off + (int64_t)c->rank * o.bytes, user + o.off,
+                               (size_t)o.bytes, ncclUint8, c->nccl, c->cs));
+      if (c->waited[i]) HIP_TRY(hipEventRecord(c->events[i], c->cs));
+      i++;
+      continue;
+    }
     if (o.kind == hydra::kOpSend || o.kind == hydra::kOpRecv || o.kind == hydra::kOpGroup) {
       size_t g = i;
       while (g < ops.size() && ops[g].kind != hydra::kOpGroup) g++;
@@ -257,6 +276,8 @@ int hydra_allreduce(hydra_comm_t c, int algo, int op, int dtype, int flags, void
   if (c->key_algo != algo || c->key_n != n || c->key_es != es || c->key_ms != ms ||
       c->key_chunk != chunk_bytes) {
     const hydra::PlanGeom g = hydra::make_geom(c->nranks, n, es, ms, chunk_bytes);
+    rc = check_geometry(algo, g);
+    if (rc) return rc;
     c->plan = hydra::make_plan(algo, g, c->rank);
     c->waited = waited_set(c->plan);
     const size_t need = hydra::plan_scratch_bytes(algo, g);
@@ -293,6 +314,7 @@ int hydra_plan(int algo, int P, int rank, size_t n, size_t esize, size_t max_seg
   if (algo == HYDRA_ALGO_RCCL) return fail(HYDRA_ERR_UNSUPPORTED, "RCCL has no plan");
   const hydra::PlanGeom g =
       hydra::make_geom(P, n, esize, max_segment ? max_segment : (1u << 20), chunk_bytes);
+  if (int rc = check_geometry(algo, g)) return rc;
   const auto plan = hydra::make_plan(algo, g, rank);
   if (count) *count = plan.size();
   if (scratch_bytes) *scratch_bytes = hydra::plan_scratch_bytes(algo, g);
@@ -317,6 +339,8 @@ int hydra_allreduce_simulate(int algo, int op, int dtype, int flags, int P, void
   const bool acc32 = (flags & HYDRA_ACC_F32) != 0;
   const hydra::PlanGeom g =
       hydra::make_geom(P, n, es, max_segment ? max_segment : (1u << 20), chunk_bytes);
+  rc = check_geometry(algo, g);
+  if (rc) return rc;
   const size_t sbytes = hydra::plan_scratch_bytes(algo, g);
 
   struct Rank {
@@ -331,7 +355,10 @@ int hydra_allreduce_simulate(int algo, int op, int dtype, int flags, int P, void
     int outstanding = 0;
     hipEvent_t start = nullptr;
     std::vector<hipEvent_t> done;  // copy-completion events of the posted group
+    int coll_posted = 0;            // collectives posted so far (sequence number)
   };
+  int coll_done = 0;               // collectives completed (all ranks matched)
+  hipEvent_t coll_ev = nullptr;    // completion of the last completed collective
   std::vector<Rank> R(P);
   std::vector<hipEvent_t> all_events;
   hipStream_t fabric = nullptr;
@@ -395,6 +422,46 @@ int hydra_allreduce_simulate(int algo, int op, int dtype, int flags, int P, void
           rk.pc++;
           progress = true;
           continue;
+        }
+        if (o.kind == hydra::kOpAllToAll || o.kind == hydra::kOpAllGather) {
+          if (!rk.posted) {  // post this rank's participation
+            wait_ev(rk.cs, rk, o);
+            SIM_TRY(new_event(&rk.start));
+            SIM_TRY(hipEventRecord(rk.start, rk.cs));
+            rk.posted = true;
+            rk.coll_posted++;
+            progress = true;
+          }
+          bool all = true;
+          for (int q = 0; q < P; q++) all = all && R[q].coll_posted == coll_done + 1;
+          if (all) {  // every rank reached it: perform the collective on the fabric stream
+            for (int q = 0; q < P; q++) SIM_TRY(hipStreamWaitEvent(fabric, R[q].start, 0));
+            const int64_t B = o.bytes;
+            for (int sr = 0; sr < P; sr++)
+              for (int dr = 0; dr < P; dr++) {
+                char* su = static_cast<char*>(bufs[sr]);
+                char* du = static_cast<char*>(bufs[dr]);
+                if (o.kind == hydra::kOpAllToAll)
+                  SIM_TRY(hipMemcpyAsync(R[dr].scratch + o.src_off + sr * B, su + o.off + dr * B,
+                                         (size_t)B, hipMemcpyDeviceToDevice, fabric));
+                else if (sr != dr)
+                  SIM_TRY(hipMemcpyAsync(du + o.off + sr * B, su + o.off + sr * B, (size_t)B,
+                                         hipMemcpyDeviceToDevice, fabric));
+              }
+            SIM_TRY(new_event(&coll_ev));
+            SIM_TRY(hipEventRecord(coll_ev, fabric));
+            coll_done++;
+            progress = true;
+          }
+          if (rk.posted && rk.coll_posted == coll_done) {  // this rank's collective completed
+            SIM_TRY(hipStreamWaitEvent(rk.cs, coll_ev, 0));
+            if (rk.waited[rk.pc]) SIM_TRY(hipEventRecord(rk.ev[rk.pc], rk.cs));
+            rk.posted = false;
+            rk.pc++;
+            progress = true;
+            continue;
+          }
+          break;  // waiting for the other ranks to reach the collective
         }
         if (!rk.posted) {  // post the whole group
           size_t gi = rk.pc;

@@ -36,15 +36,18 @@ enum PlanKind : int32_t {
   kOpRecv = 2,    // receive `bytes` from `peer` into buffer `buf` at `off`
   kOpGroup = 3,   // end of a p2p group: every SEND/RECV since the previous GROUP is one group
   kOpReduce = 4,  // user[off .. +bytes] = op(user[off..], scratch[src_off..])          (ring hop)
-  kOpFold = 5,    // user[off..] = fold(user[off..], scratch[src_off + k*slot_stride], k=0..nsrc-2)
+  kOpFold = 5,    // user[off..] = fold(user[off..], contributions in scratch, see slot_of)
+  kOpAllToAll = 6,   // collective: user[off + q*bytes, bytes] -> rank q's scratch[src_off + r*bytes]
+  kOpAllGather = 7,  // collective, in place: user[off + r*bytes, bytes] -> every rank's same range
 };
 enum PlanBuf : int32_t { kBufUser = 0, kBufScratch = 1 };
-enum Algo : int32_t { kAlgoAuto = 0, kAlgoRing = 1, kAlgoDirect = 2, kAlgoRccl = 3 };
+enum Algo : int32_t { kAlgoAuto = 0, kAlgoRing = 1, kAlgoDirect = 2, kAlgoRccl = 3, kAlgoA2A = 4 };
 
 // Mirrored by hydra_plan_op_t in include/hydra_xgmi.h (same layout).
 struct PlanOp {
   int32_t kind;
-  int32_t peer;
+  int32_t peer;         // SEND/RECV: peer rank; FOLD: -1 = slots in contributor order
+                        // (slot j-1 holds rank r+j), >= 0 = slots in rank order rotated by peer
   int32_t buf;
   int32_t nsrc;         // FOLD: number of contributions incl. the local one
   int64_t off;          // user/scratch byte offset (SEND/RECV: in `buf`; REDUCE/FOLD: user dst)
@@ -112,11 +115,28 @@ inline PlanGeom make_geom(int P, size_t n, size_t esize, size_t max_segment, siz
   return g;
 }
 
+// Byte offset in scratch of contribution j (1..nsrc-1) of a FOLD op.
+inline int64_t fold_slot(const PlanOp& o, int j) {
+  if (o.peer < 0) return o.src_off + (int64_t)(j - 1) * o.slot_stride;
+  return o.src_off + (int64_t)((o.peer + j) % o.nsrc) * o.slot_stride;
+}
+
+// A2A needs the reference's blocks to be equal and to tile the bucket (true for every
+// BASELINE bucket: 64 Mi fp32 / 256 Mi bf16 at P = 2..8).
+inline bool blocks_equal(const PlanGeom& g) {
+  const size_t b = g.block_bytes(0);
+  if (b == 0 || (size_t)g.P * b != g.total) return false;
+  for (int q = 1; q < g.P; q++)
+    if (g.block_bytes(q) != b) return false;
+  return true;
+}
+
 // Scratch bytes one rank needs for `algo` (wire element size = esize).
 inline size_t plan_scratch_bytes(int algo, const PlanGeom& g) {
   if (g.P <= 1) return 0;
   if (algo == kAlgoRing) return 2 * g.chunk;
   if (algo == kAlgoDirect) return 2 * (size_t)(g.P - 1) * g.chunk;
+  if (algo == kAlgoA2A) return g.total;
   return 0;
 }
 
@@ -238,8 +258,25 @@ inline std::vector<PlanOp> plan_direct(const PlanGeom& g, int r) {
   return pb.ops;
 }
 
+// ---- A2A -----------------------------------------------------------------------------------
+// Equal blocks of B bytes: the reduce-scatter exchange IS an all-to-all (block q of every rank
+// to rank q, landing in rank order), the owner folds the P contributions in the reference order
+// (FOLD with rank-ordered slots rotated by r), and the all-gather is RCCL's in-place all-gather.
+// Three launches per allreduce; RCCL picks the link schedule for both collectives.
+inline std::vector<PlanOp> plan_a2a(const PlanGeom& g, int r) {
+  PlanBuilder pb;
+  if (g.P <= 1 || g.total == 0) return pb.ops;
+  const int64_t B = (int64_t)g.block_bytes(0);
+  const int x = pb.add(kOpAllToAll, -1, kBufUser, 0, B, 0);
+  const int f = pb.add(kOpFold, r, kBufUser, (int64_t)r * B, B, 0, B, g.P, x);
+  pb.add(kOpAllGather, -1, kBufUser, 0, B, 0, 0, 0, f);
+  return pb.ops;
+}
+
 inline std::vector<PlanOp> make_plan(int algo, const PlanGeom& g, int r) {
-  return algo == kAlgoRing ? plan_ring(g, r) : plan_direct(g, r);
+  if (algo == kAlgoRing) return plan_ring(g, r);
+  if (algo == kAlgoA2A) return plan_a2a(g, r);
+  return plan_direct(g, r);
 }
 
 }  // namespace hydra

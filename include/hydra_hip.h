@@ -124,25 +124,29 @@ void hydra_ring_plan(int P, size_t n, size_t esize, size_t max_segment, size_t* 
  *   HYDRA_ALGO_DIRECT  all-to-all reduce-scatter in one p2p group (all 7 xGMI links), then ONE
  *                      fold kernel per chunk in the reference order, then a direct all-gather
  *   HYDRA_ALGO_RCCL    ncclAllReduce (RCCL's own fold order: a tolerance, not bit-exact)
+ *   HYDRA_ALGO_A2A     equal blocks only: ncclAllToAll of the blocks, ONE fold kernel in the
+ *                      reference order, ncclAllGather in place (bit-exact, 3 launches)
  *   HYDRA_ALGO_AUTO    DIRECT
  * max_segment: the reference's maxSegmentSize (0 = 1 MiB, allreduce.h:78) -- it fixes block
  * ownership; chunk_bytes: pipelining granularity (0 = 4 MiB), does not change results.
  * flags: HYDRA_ACC_F32 -- bf16 bucket, fp32 accumulation, one rounding (BASELINE config 5;
- * DIRECT/AUTO only). */
+ * DIRECT/A2A/AUTO). */
 #define HYDRA_UNIQUE_ID_BYTES 128
 #define HYDRA_ACC_F32 1
 typedef enum {
   HYDRA_ALGO_AUTO = 0,
   HYDRA_ALGO_RING = 1,
   HYDRA_ALGO_DIRECT = 2,
-  HYDRA_ALGO_RCCL = 3
+  HYDRA_ALGO_RCCL = 3,
+  HYDRA_ALGO_A2A = 4
 } hydra_algo_t;
 typedef struct hydra_comm* hydra_comm_t;
 
 /* A plan op (one rank's schedule entry; see hydra_amd/csrc/xgmi_plan.h). */
 typedef struct {
-  int32_t kind; /* 1 SEND, 2 RECV, 3 GROUP end, 4 REDUCE (ring hop), 5 FOLD (direct owner) */
-  int32_t peer;
+  int32_t kind; /* 1 SEND, 2 RECV, 3 GROUP end, 4 REDUCE (ring hop), 5 FOLD (owner),
+                   6 ALLTOALL, 7 ALLGATHER (collectives over the whole bucket) */
+  int32_t peer; /* FOLD: -1 contributor-ordered slots, >= 0 rank-ordered slots rotated by it */
   int32_t buf;  /* 0 user bucket, 1 scratch */
   int32_t nsrc;
   int64_t off, bytes, src_off, slot_stride;

@@ -9,7 +9,13 @@ import numpy as np
 import pytest
 import torch.multiprocessing as mp
 
-SEND, RECV, GROUP, REDUCE, FOLD = 1, 2, 3, 4, 5
+SEND, RECV, GROUP, REDUCE, FOLD, ALLTOALL, ALLGATHER = 1, 2, 3, 4, 5, 6, 7
+
+
+def fold_slot(o, j):
+    if o["peer"] < 0:
+        return o["src_off"] + (j - 1) * o["slot_stride"]
+    return o["src_off"] + ((o["peer"] + j) % o["nsrc"]) * o["slot_stride"]
 
 
 def _free_port():
@@ -41,6 +47,31 @@ def _worker(rank, world, port, algo, n, ms, ch, q):
         i = 0
         while i < len(ops):
             o = ops[i]
+            if o["kind"] == ALLTOALL:  # ncclAllToAll semantics via p2p (gloo has no alltoall)
+                B = o["bytes"]
+                scratch[o["src_off"] + rank * B:o["src_off"] + (rank + 1) * B] = \
+                    user[o["off"] + rank * B:o["off"] + (rank + 1) * B]
+                p2p = []
+                for pr in range(world):
+                    if pr == rank:
+                        continue
+                    p2p.append(dist.P2POp(dist.isend,
+                                          user[o["off"] + pr * B:o["off"] + (pr + 1) * B], pr))
+                    p2p.append(dist.P2POp(dist.irecv, scratch[o["src_off"] + pr * B:
+                                                              o["src_off"] + (pr + 1) * B], pr))
+                for req in dist.batch_isend_irecv(p2p):
+                    req.wait()
+                i += 1
+                continue
+            if o["kind"] == ALLGATHER:
+                B = o["bytes"]
+                mine = user[o["off"] + rank * B:o["off"] + (rank + 1) * B].clone()
+                parts = [torch.empty_like(mine) for _ in range(world)]
+                dist.all_gather(parts, mine)
+                for pr in range(world):
+                    user[o["off"] + pr * B:o["off"] + (pr + 1) * B] = parts[pr]
+                i += 1
+                continue
             if o["kind"] in (REDUCE, FOLD):
                 u = user.numpy()
                 sc = scratch.numpy()
@@ -49,9 +80,8 @@ def _worker(rank, world, port, algo, n, ms, ch, q):
                     recv = sc[o["src_off"]:o["src_off"] + o["bytes"]].view(np.float32)
                     out = O.op(local, recv, "sum")
                 else:
-                    slots = [sc[o["src_off"] + k * o["slot_stride"]:o["src_off"] + k *
-                                o["slot_stride"] + o["bytes"]].view(np.float32)
-                             for k in range(o["nsrc"] - 1)]
+                    slots = [sc[fold_slot(o, j):fold_slot(o, j) + o["bytes"]].view(np.float32)
+                             for j in range(1, o["nsrc"])]
                     acc = slots[-1].copy()
                     for s in reversed(slots[:-1]):
                         acc = O.op(s.copy(), acc, "sum")
@@ -88,17 +118,21 @@ def _worker(rank, world, port, algo, n, ms, ch, q):
 
 
 @pytest.mark.parametrize("world", [2, 3])
-@pytest.mark.parametrize("algo", ["ring", "direct"])
+@pytest.mark.parametrize("algo", ["ring", "direct", "a2a"])
 def test_gloo_multiprocess_plan(algo, world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    n, ms, ch = 100003, 4096, 16384
+    n, ms, ch = (100003, 4096, 16384) if algo != "a2a" else (3 << 16, 4096, 0)
     procs = [ctx.Process(target=_worker, args=(r, world, port, algo, n, ms, ch, q))
              for r in range(world)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=240) for _ in range(world))
-    for p in procs:
-        p.join(timeout=60)
+    try:
+        res = dict(q.get(timeout=120) for _ in range(world))
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
     assert all(v is True for v in res.values()), res

@@ -12,7 +12,14 @@ import pytest
 
 from hydra_amd import _lib, ring, synth
 
-SEND, RECV, GROUP, REDUCE, FOLD = 1, 2, 3, 4, 5
+SEND, RECV, GROUP, REDUCE, FOLD, ALLTOALL, ALLGATHER = 1, 2, 3, 4, 5, 6, 7
+
+
+def fold_slot(o, j):
+    """xgmi_plan.h fold_slot: scratch offset of contribution j of a FOLD."""
+    if o["peer"] < 0:
+        return o["src_off"] + (j - 1) * o["slot_stride"]
+    return o["src_off"] + ((o["peer"] + j) % o["nsrc"]) * o["slot_stride"]
 
 
 def interpret(plans, bufs, scratch, reduce_fn):
@@ -21,12 +28,32 @@ def interpret(plans, bufs, scratch, reduce_fn):
     pcs = [0] * P
     sends, recvs = {}, {}
     posted = [None] * P
+    coll_wait = [False] * P
     while any(pcs[r] < len(plans[r]) for r in range(P)):
         progress = False
         for r in range(P):
             ops = plans[r]
             while pcs[r] < len(ops):
                 o = ops[pcs[r]]
+                if o["kind"] in (ALLTOALL, ALLGATHER):
+                    coll_wait[r] = True
+                    if all(coll_wait[q] and plans[q][pcs[q]]["kind"] == o["kind"]
+                           for q in range(P)):
+                        B, off = o["bytes"], o["off"]
+                        for sr in range(P):
+                            for dr in range(P):
+                                if o["kind"] == ALLTOALL:
+                                    d0 = o["src_off"] + sr * B
+                                    scratch[dr][d0:d0 + B] = bufs[sr][off + dr * B:off + dr * B + B]
+                                elif sr != dr:
+                                    bufs[dr][off + sr * B:off + sr * B + B] = \
+                                        bufs[sr][off + sr * B:off + sr * B + B]
+                        for q in range(P):
+                            coll_wait[q] = False
+                            pcs[q] += 1
+                        progress = True
+                        continue
+                    break
                 if o["kind"] in (REDUCE, FOLD):
                     reduce_fn(r, o)
                     pcs[r] += 1
@@ -83,9 +110,8 @@ def run_plan_numpy(O, algo, xs, max_segment, chunk, code=6):
             recv = sc[o["src_off"]:o["src_off"] + o["bytes"]].view(dt)
             out = O.op(local, recv, "sum", code)
         else:
-            slots = [sc[o["src_off"] + k * o["slot_stride"]:
-                        o["src_off"] + k * o["slot_stride"] + o["bytes"]].view(dt)
-                     for k in range(o["nsrc"] - 1)]
+            slots = [sc[fold_slot(o, j):fold_slot(o, j) + o["bytes"]].view(dt)
+                     for j in range(1, o["nsrc"])]
             acc = slots[-1].copy()
             for s in reversed(slots[:-1]):
                 acc = O.op(s.copy(), acc, "sum", code)
@@ -100,6 +126,36 @@ def run_plan_numpy(O, algo, xs, max_segment, chunk, code=6):
 CASES = [(P, n, ms, ch) for P in (2, 3, 4, 5, 8) for (n, ms, ch) in
          [(1, 0, 0), (7, 128, 0), (1000, 128, 64), (4099, 128, 1024), (10007, 1 << 20, 4096),
           (262145, 0, 0), (262145, 0, 65536)]]
+
+
+A2A_CASES = [(P, n, ms) for P in (2, 3, 4, 5, 8) for (n, ms) in
+             [(1 << 16, 0), (3 * 5 * 7 * 1024, 1024), (1 << 20, 4096)]]
+
+
+def _a2a_ok(P, n, ms, es=4):
+    ns, sb, S = _lib.ring_plan(P, n, es, ms or (1 << 20))
+    return S * sb * P == n * es
+
+
+@pytest.mark.parametrize("P,n,ms", A2A_CASES)
+def test_a2a_plan_matches_reference_fold(O, P, n, ms):
+    if not _a2a_ok(P, n, ms):
+        with pytest.raises(_lib.HydraError):
+            ring.plan("a2a", P, 0, n, 4, ms, 0)
+        return
+    xs = [synth.stress_f32(P, r, n) for r in range(P)]
+    outs = run_plan_numpy(O, "a2a", xs, ms, 0)
+    exp = O.ring_result(xs, ms or (1 << 20))
+    for r in range(P):
+        assert np.array_equal(outs[r].view(np.uint32), exp.view(np.uint32))
+    for r in range(P):
+        race_check(ring.plan("a2a", P, r, n, 4, ms, 0)[0])
+
+
+def test_a2a_covers_baseline_buckets():
+    """BASELINE config 4 (64 Mi fp32) and 5 (256 Mi bf16) have equal blocks at P = 2..8."""
+    for P in (2, 4, 8):
+        assert _a2a_ok(P, 64 << 20, 0, 4) and _a2a_ok(P, 256 << 20, 0, 2)
 
 
 @pytest.mark.parametrize("algo", ["ring", "direct"])
@@ -126,16 +182,23 @@ def test_plan_int32_and_f16(O, algo):
     assert all(np.array_equal(o, exp) for o in outs)
 
 
-def _accesses(o, scratch_id=1):
-    """(buffer, lo, hi, is_write) byte ranges an op touches."""
+def _accesses(o, P=None):
+    """(buffer, lo, hi, is_write) byte ranges an op touches (collectives: conservatively the
+    whole region they read/write on this rank)."""
     if o["kind"] in (SEND, RECV):
         return [(o["buf"], o["off"], o["off"] + o["bytes"], o["kind"] == RECV)]
+    if o["kind"] in (ALLTOALL, ALLGATHER):
+        span = o["bytes"] * (P or 1)
+        if o["kind"] == ALLTOALL:
+            return [(0, o["off"], o["off"] + span, False),
+                    (1, o["src_off"], o["src_off"] + span, True)]
+        return [(0, o["off"], o["off"] + span, True), (0, o["off"], o["off"] + span, False)]
     acc = [(0, o["off"], o["off"] + o["bytes"], True), (0, o["off"], o["off"] + o["bytes"], False)]
     if o["kind"] == REDUCE:
         acc.append((1, o["src_off"], o["src_off"] + o["bytes"], False))
     else:
-        for k in range(o["nsrc"] - 1):
-            lo = o["src_off"] + k * o["slot_stride"]
+        for j in range(1, o["nsrc"]):
+            lo = fold_slot(o, j)
             acc.append((1, lo, lo + o["bytes"], False))
     return acc
 
@@ -146,9 +209,15 @@ def race_check(ops):
     different streams must be ordered (in plan order) by happens-before."""
     units = []  # (stream, accesses, waits(list of op idx), op index of unit end)
     unit_of = {}
+    P = max([o["nsrc"] for o in ops if o["kind"] == FOLD] + [1])
     i = 0
     while i < len(ops):
         o = ops[i]
+        if o["kind"] in (ALLTOALL, ALLGATHER):
+            units.append(("c", _accesses(o, P), [o["wait0"], o["wait1"]], i))
+            unit_of[i] = len(units) - 1
+            i += 1
+            continue
         if o["kind"] in (REDUCE, FOLD):
             units.append(("k", _accesses(o), [o["wait0"], o["wait1"]], i))
             unit_of[i] = len(units) - 1
