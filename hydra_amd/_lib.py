@@ -30,7 +30,7 @@ EXPORTS = [  # every symbol include/hydra_hip.h declares
     "hydra_stream_create", "hydra_stream_destroy", "hydra_stream_synchronize", "hydra_malloc",
     "hydra_free", "hydra_memcpy", "hydra_ring_plan",
     "hydra_comm_get_unique_id", "hydra_comm_init", "hydra_comm_destroy", "hydra_allreduce",
-    "hydra_plan", "hydra_allreduce_simulate",
+    "hydra_plan", "hydra_allreduce_simulate", "hydra_fold",
 ]
 
 ALGO_AUTO, ALGO_RING, ALGO_DIRECT, ALGO_RCCL, ALGO_A2A = range(5)
@@ -103,6 +103,7 @@ def _declare(L) -> None:
     L.hydra_plan.argtypes = [i, i, i, sz, sz, sz, sz, ctypes.POINTER(PlanOp), sz,
                              ctypes.POINTER(sz), ctypes.POINTER(sz)]
     L.hydra_allreduce_simulate.argtypes = [i, i, i, i, i, ctypes.POINTER(vp), sz, sz, sz]
+    L.hydra_fold.argtypes = [i, i, i, vp, ctypes.POINTER(vp), i, sz, vp]
 
 
 def lib():

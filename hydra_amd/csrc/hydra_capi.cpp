@@ -140,6 +140,30 @@ int hydra_chunk_sum(int dtype, void* c, const void* a, const void* b, size_t n,
   return hydra_reduce(HYDRA_SUM, dtype, c, a, b, n, stream);
 }
 
+int hydra_fold(int op, int dtype, int flags, void* dst, const void* const* srcs, int nsrc,
+               size_t n, hydra_stream_t stream) {
+  if (op < HYDRA_SUM || op > HYDRA_MIN) return fail(HYDRA_ERR_INVALID, "invalid op");
+  const size_t es = hydra::dtype_size(dtype);
+  if (!es) return fail(HYDRA_ERR_INVALID, "invalid dtype");
+  if (nsrc < 1 || nsrc > hydra::kMaxRanks || !srcs || !dst)
+    return fail(HYDRA_ERR_INVALID, "need 1..16 sources and a destination");
+  const bool acc32 = (flags & HYDRA_ACC_F32) != 0;
+  if (acc32 && dtype != HYDRA_BFLOAT16)
+    return fail(HYDRA_ERR_UNSUPPORTED, "HYDRA_ACC_F32 needs bf16 data");
+  if (n == 0) return ok();
+  for (int j = 0; j < nsrc; j++) {
+    if (!srcs[j] || reinterpret_cast<uintptr_t>(srcs[j]) % es)
+      return fail(HYDRA_ERR_INVALID, "source null or not element-aligned");
+    if (srcs[j] != dst && overlaps(dst, srcs[j], n * es))
+      return fail(HYDRA_ERR_INVALID, "dst partially overlaps a source");
+  }
+  if (reinterpret_cast<uintptr_t>(dst) % es) return fail(HYDRA_ERR_INVALID, "dst not aligned");
+  hipError_t e = hydra::launch_fold(op, dtype, acc32, dst, srcs, nsrc, n,
+                                    static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return hip_fail(e, "fold kernel launch");
+  return ok();
+}
+
 int hydra_acc_bf16_f32(float* acc, const void* b_bf16, size_t n, hydra_stream_t stream) {
   if (n == 0) return ok();
   if (!acc || !b_bf16) return fail(HYDRA_ERR_INVALID, "null pointer");

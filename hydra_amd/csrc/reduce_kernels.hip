@@ -21,6 +21,7 @@
 
 #include <type_traits>
 
+#include "errors.h"
 #include "reduce_kernels.h"
 
 namespace hydra {
@@ -406,11 +407,17 @@ struct FoldSrcs {
   const char* p[kMaxRanks];
 };
 
-template <typename E, int OP, bool ACC32>
+template <bool NT>
+__device__ __forceinline__ u32x4 ld_src(const char* p) {
+  if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const u32x4_u*>(p));
+  else return ld_u(p);
+}
+
+template <typename E, int OP, bool ACC32, bool NT>
 __device__ __forceinline__ u32x4 fold_vec(const FoldSrcs& S, int nsrc, size_t off) {
   if constexpr (ACC32) {
     static_assert(sizeof(E) == 2, "ACC32 is the bf16 form");
-    u32x4 last = ld_u(S.p[nsrc - 1] + off);
+    u32x4 last = ld_src<NT>(S.p[nsrc - 1] + off);
     float acc[8];
 #pragma unroll
     for (int k = 0; k < 4; k++) {
@@ -418,7 +425,7 @@ __device__ __forceinline__ u32x4 fold_vec(const FoldSrcs& S, int nsrc, size_t of
       acc[2 * k + 1] = bitsf(last[k] & 0xffff0000u);
     }
     for (int j = nsrc - 2; j >= 0; j--) {
-      u32x4 x = ld_u(S.p[j] + off);
+      u32x4 x = ld_src<NT>(S.p[j] + off);
 #pragma unroll
       for (int k = 0; k < 4; k++) {
         acc[2 * k] = fop<OP>(bitsf(x[k] << 16), acc[2 * k]);
@@ -431,9 +438,9 @@ __device__ __forceinline__ u32x4 fold_vec(const FoldSrcs& S, int nsrc, size_t of
       o[k] = (uint32_t)f2bf(acc[2 * k]) | ((uint32_t)f2bf(acc[2 * k + 1]) << 16);
     return o;
   } else {
-    u32x4 acc = ld_u(S.p[nsrc - 1] + off);
+    u32x4 acc = ld_src<NT>(S.p[nsrc - 1] + off);
     for (int j = nsrc - 2; j >= 0; j--) {
-      u32x4 x = ld_u(S.p[j] + off);
+      u32x4 x = ld_src<NT>(S.p[j] + off);
       acc = vapply<E, OP>(x, acc, x);  // c = local + received, in place on local (C0 = local)
     }
     return acc;
@@ -461,7 +468,7 @@ __device__ __forceinline__ E fold_elem(const FoldSrcs& S, int nsrc, ptrdiff_t i)
 }
 
 // S.p[*] and dst already advanced by `head` elements (dst 16-B aligned at the body).
-template <typename E, int OP, bool ACC32>
+template <typename E, int OP, bool ACC32, bool NT>
 __global__ __launch_bounds__(kBlock) void k_fold(E* dst, FoldSrcs S, int nsrc, size_t nvec,
                                                  int head, int tail) {
   constexpr int N = Vec<E>::N;
@@ -481,7 +488,7 @@ __global__ __launch_bounds__(kBlock) void k_fold(E* dst, FoldSrcs S, int nsrc, s
     // write-through (sc1) store through a block-uniform descriptor, as the chunk-sum default
     const auto w = __builtin_amdgcn_make_buffer_rsrc(d + vb * 16, 0, kBlock * 16, 0x00020000);
     if (v < nvec)
-      __builtin_amdgcn_raw_buffer_store_b128(fold_vec<E, OP, ACC32>(S, nsrc, v * 16), w,
+      __builtin_amdgcn_raw_buffer_store_b128(fold_vec<E, OP, ACC32, NT>(S, nsrc, v * 16), w,
                                              (uint32_t)t * 16, 0, 16);
   }
 }
@@ -667,8 +674,9 @@ hipError_t launch_reduce(int variant, int op, int dtype, void* c, const void* a,
 }
 
 namespace {
-template <typename E, int OP, bool ACC32>
-hipError_t launch_fold_t(void* dst, const void* const* srcs, int nsrc, size_t n, hipStream_t s) {
+template <typename E, int OP, bool ACC32, bool NT>
+hipError_t launch_fold_v(void* dst, const void* const* srcs, int nsrc, size_t n, hipStream_t s,
+                         size_t cap_per_cu) {
   const Split sp = split_call<E>(dst, n);
   FoldSrcs S;
   for (int j = 0; j < kMaxRanks; j++)
@@ -676,12 +684,24 @@ hipError_t launch_fold_t(void* dst, const void* const* srcs, int nsrc, size_t n,
                       : nullptr;
   E* d = reinterpret_cast<E*>(dst) + sp.head;
   size_t blocks = (sp.nvec + kBlock - 1) / kBlock;
-  const size_t cap = (size_t)cu_count() * 8;
-  if (blocks > cap) blocks = cap;
+  const size_t cap = (size_t)cu_count() * cap_per_cu;
+  if (cap_per_cu && blocks > cap) blocks = cap;
   if (blocks == 0) blocks = 1;
-  hipLaunchKernelGGL((k_fold<E, OP, ACC32>), dim3((unsigned)blocks), dim3(kBlock), 0, s, d, S,
-                     nsrc, sp.nvec, sp.head, sp.tail);
+  hipLaunchKernelGGL((k_fold<E, OP, ACC32, NT>), dim3((unsigned)blocks), dim3(kBlock), 0, s, d,
+                     S, nsrc, sp.nvec, sp.head, sp.tail);
   return hipGetLastError();
+}
+
+// Fold variants (hydra_set_variant, measurement only; 0 = default): 1 plain loads, grid capped
+// at 8 blocks/CU; 2 nontemporal loads, capped; 3 nontemporal, one block per 256 vectors.
+template <typename E, int OP, bool ACC32>
+hipError_t launch_fold_t(void* dst, const void* const* srcs, int nsrc, size_t n, hipStream_t s) {
+  switch (current_variant()) {
+    case 1: return launch_fold_v<E, OP, ACC32, false>(dst, srcs, nsrc, n, s, 8);
+    case 2: return launch_fold_v<E, OP, ACC32, true>(dst, srcs, nsrc, n, s, 8);
+    case 3: return launch_fold_v<E, OP, ACC32, true>(dst, srcs, nsrc, n, s, 0);
+    default: return launch_fold_v<E, OP, ACC32, false>(dst, srcs, nsrc, n, s, 8);
+  }
 }
 
 template <int OP>

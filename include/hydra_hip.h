@@ -53,6 +53,8 @@ typedef enum {
 
 typedef enum { HYDRA_SUM = 0, HYDRA_PRODUCT = 1, HYDRA_MAX = 2, HYDRA_MIN = 3 } hydra_op_t;
 
+#define HYDRA_ACC_F32 1 /* flag: bf16 data, fp32 accumulation, one rounding */
+
 typedef enum {
   HYDRA_OK = 0,
   HYDRA_ERR_INVALID = 1,     /* bad argument (dtype, op, misaligned pointer, partial overlap) */
@@ -85,6 +87,14 @@ int hydra_chunk_sum(int dtype, void* c, const void* a, const void* b, size_t n,
 int hydra_acc_bf16_f32(float* acc, const void* b_bf16, size_t n, hydra_stream_t stream);
 /* out_bf16[i] = bf16_rne(acc[i]) */
 int hydra_f32_to_bf16(void* out_bf16, const float* acc, size_t n, hydra_stream_t stream);
+
+/* P-way reduction in the reference ring's fold order (the owner step of the DIRECT/A2A
+ * allreduce): dst[i] = srcs[0][i] op (srcs[1][i] op (... op srcs[nsrc-1][i])), where srcs[0]
+ * is the owner's block x_q and srcs[j] rank q+j's contribution -- bit-identical to the
+ * owner's P-1 in-place ring hops (allreduce.cc:301-305).  dst may equal srcs[0]; 1 <= nsrc <=
+ * 16.  flags HYDRA_ACC_F32: bf16 data, fp32 accumulation, one rounding. */
+int hydra_fold(int op, int dtype, int flags, void* dst, const void* const* srcs, int nsrc,
+               size_t n, hydra_stream_t stream);
 
 /* Kernel variant selection for measurement (0 = tuned default).  Returns the previous value. */
 int hydra_set_variant(int variant);
@@ -132,7 +142,6 @@ void hydra_ring_plan(int P, size_t n, size_t esize, size_t max_segment, size_t* 
  * flags: HYDRA_ACC_F32 -- bf16 bucket, fp32 accumulation, one rounding (BASELINE config 5;
  * DIRECT/A2A/AUTO). */
 #define HYDRA_UNIQUE_ID_BYTES 128
-#define HYDRA_ACC_F32 1
 typedef enum {
   HYDRA_ALGO_AUTO = 0,
   HYDRA_ALGO_RING = 1,

@@ -1,0 +1,49 @@
+#!/usr/bin/env python3
+"""Interleaved A/B of the P-way fold kernel variants (DIRECT/A2A owner step) in one process.
+Bytes per element of the owner block: (nsrc + 1) x esize (read every contribution, write dst)."""
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from hydra_amd import _lib  # noqa: E402
+
+L = _lib.lib()
+dev = torch.device("cuda", 0)
+s = torch.cuda.current_stream(dev)
+res = {}
+for (P, n, code, flags) in [(8, 8 << 20, 6, 0), (8, 32 << 20, 9, 1), (4, 16 << 20, 6, 0),
+                            (2, 32 << 20, 6, 0)]:
+    es = _lib.ESIZE[code]
+    srcs = [torch.randint(0, 1 << 14, (n * es // 2,), dtype=torch.int16, device=dev)
+            for _ in range(P)]
+    ptrs = (ctypes.c_void_p * P)(*[t.data_ptr() for t in srcs])
+    key = f"P{P}/n{n}/{'bf16acc32' if flags else 'f32'}"
+    for rnd in range(5):
+        for v in (0, 1, 2, 3):
+            L.hydra_set_variant(v)
+            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                  for _ in range(15)]
+            for e0, e1 in ev:
+                e0.record(s)
+                _lib.check(L.hydra_fold(0, code, flags, srcs[0].data_ptr(), ptrs, P, n,
+                                        s.cuda_stream))
+                e1.record(s)
+            torch.cuda.synchronize()
+            t = float(np.median([a.elapsed_time(b) for a, b in ev[3:]]))
+            res.setdefault(key, {}).setdefault(v, []).append(t)
+    del srcs
+L.hydra_set_variant(0)
+out = {}
+for k, d in res.items():
+    P = int(k.split("/")[0][1:])
+    n = int(k.split("/")[1][1:])
+    es = 2 if "bf16" in k else 4
+    out[k] = {v: {"us": round(float(np.median(t)) * 1e3, 2),
+                  "GBps": round((P + 1) * n * es / (np.median(t) * 1e-3) / 1e9, 1)}
+              for v, t in d.items()}
+print(json.dumps(out))

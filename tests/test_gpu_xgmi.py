@@ -167,3 +167,31 @@ def test_a2a_rejects_unequal_blocks(gpu):
     bufs = [torch.zeros(1001, device=gpu) for _ in range(3)]
     with pytest.raises(_lib.HydraError):
         ring.simulate(bufs, algo="a2a")
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("P", [1, 2, 5, 8, 16])
+def test_fold_abi_reference_order(gpu, O, P, variant):
+    """hydra_fold == the owner's P-1 in-place ring hops, every fold variant, ragged sizes and
+    misaligned sources."""
+    import ctypes
+
+    import torch
+
+    for n in (1, 13, 4099, 1 << 18):
+        xs = [synth.stress_f32(P, r, n) for r in range(P)]
+        bufs = [torch.from_numpy(np.concatenate([np.zeros(r % 4, np.float32), x])).to(gpu)
+                for r, x in enumerate(xs)]
+        ptrs = (ctypes.c_void_p * P)(*[b.data_ptr() + 4 * (r % 4) for r, b in enumerate(bufs)])
+        dst = torch.zeros(n + 3, dtype=torch.float32, device=gpu)
+        L = _lib.lib()
+        prev = L.hydra_set_variant(variant)
+        try:
+            _lib.check(L.hydra_fold(0, 6, 0, dst.data_ptr() + 4, ptrs, P, n, None))
+        finally:
+            L.hydra_set_variant(prev)
+        torch.cuda.synchronize()
+        acc = xs[P - 1].copy()
+        for j in range(P - 2, -1, -1):
+            acc = O.op(xs[j], acc, "sum", 6)
+        assert np.array_equal(dst.cpu().numpy()[1:n + 1].view(np.uint32), acc.view(np.uint32))
