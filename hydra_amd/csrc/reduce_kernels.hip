@@ -700,7 +700,9 @@ hipError_t launch_fold_t(void* dst, const void* const* srcs, int nsrc, size_t n,
     case 1: return launch_fold_v<E, OP, ACC32, false>(dst, srcs, nsrc, n, s, 8);
     case 2: return launch_fold_v<E, OP, ACC32, true>(dst, srcs, nsrc, n, s, 8);
     case 3: return launch_fold_v<E, OP, ACC32, true>(dst, srcs, nsrc, n, s, 0);
-    default: return launch_fold_v<E, OP, ACC32, false>(dst, srcs, nsrc, n, s, 8);
+    default:  // tuned (profiles/r01_tune_fold.json): fp32 6.6 TB/s plain; bf16->fp32 6.3 nt
+      if constexpr (ACC32) return launch_fold_v<E, OP, ACC32, true>(dst, srcs, nsrc, n, s, 0);
+      else return launch_fold_v<E, OP, ACC32, false>(dst, srcs, nsrc, n, s, 8);
   }
 }
 

@@ -290,3 +290,33 @@ def test_torch_stream_api(gpu, O):
         R.sum_(a, a, b)
     s.synchronize()
     assert np.array_equal(bits(a.cpu().numpy()), bits(exp))
+
+
+def test_graph_capture_replay(gpu, O):
+    """hydra_chunk_sum enqueues with no allocation or synchronisation: it can be captured in a
+    HIP graph (torch.cuda.CUDAGraph) and replayed."""
+    import torch
+
+    n = (1 << 20) + 3
+    a = torch.from_numpy(synth.uniform_f32(n, 1)).to(gpu)
+    b = torch.from_numpy(synth.uniform_f32(n, 2)).to(gpu)
+    a0 = a.cpu().numpy().copy()
+    L = _lib.lib()
+    _lib.check(L.hydra_chunk_sum(6, a.data_ptr(), a.data_ptr(), b.data_ptr(), 16,
+                                 torch.cuda.current_stream().cuda_stream))  # warm (cu count)
+    torch.cuda.synchronize()
+    a.copy_(torch.from_numpy(a0).to(gpu))
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            _lib.check(L.hydra_chunk_sum(6, a.data_ptr(), a.data_ptr(), b.data_ptr(), n,
+                                         s.cuda_stream))
+    torch.cuda.synchronize()
+    exp = a0.copy()
+    bb = b.cpu().numpy()
+    for _ in range(3):
+        g.replay()
+        exp = O.op(exp, bb, "sum", 6)
+    torch.cuda.synchronize()
+    assert np.array_equal(a.cpu().numpy().view(np.uint32), exp.view(np.uint32))
