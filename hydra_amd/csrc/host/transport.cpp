@@ -372,7 +372,10 @@ void wait_oldest(std::mutex& mu, std::vector<std::shared_ptr<UnboundBuffer::Op>>
   }
   {
     std::unique_lock<std::mutex> l(op->mu);
-    if (!op->cv.wait_for(l, timeout, [&] { return op->done; })) {
+    // system_clock deadline: lowers to pthread_cond_timedwait (steady_clock's
+    // pthread_cond_clockwait is invisible to GCC 11's ThreadSanitizer)
+    const auto deadline = std::chrono::system_clock::now() + timeout;
+    if (!op->cv.wait_until(l, deadline, [&] { return op->done; })) {
       // the reference's message (gloo/gloo/transport/tcp/unbound_buffer.cc:80-84)
       throw IoException("Timed out waiting " + std::to_string(timeout.count()) + "ms for " +
                         what + " operation to complete");

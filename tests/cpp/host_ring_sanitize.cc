@@ -1,0 +1,98 @@
+// Sanitizer driver for the host runtime (transport + ring + rail split), built by
+// tests/test_sanitizers.py with -fsanitize=thread and with -fsanitize=address,undefined.
+// Mirrors AllreduceNewTest.Default (gloo/gloo/test/allreduce_test.cc:302-362) and the
+// bew_allreduce_a split on thread-ranks over loopback TCP, with a plain CPU sum as the reducer
+// (the product's GPU reducer is exercised by the GPU tests).  Exit 0 = all results correct.
+#include <cstdint>
+#include <cstdio>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "hydra/allreduce.h"
+
+static void sum_u64(void* c, const void* a, const void* b, size_t n) {
+  for (size_t i = 0; i < n; i++)
+    static_cast<uint64_t*>(c)[i] = static_cast<const uint64_t*>(a)[i] +
+                                   static_cast<const uint64_t*>(b)[i];
+}
+
+static int run(int P, int nptr, size_t n, bool inplace, bool apipe) {
+  hydra::HashStore store;
+  std::vector<std::thread> th;
+  std::vector<int> bad(P, 0);
+  for (int r = 0; r < P; r++) {
+    th.emplace_back([&, r] {
+      try {
+        auto c1 = std::make_shared<hydra::Context>(r, P);
+        c1->connectFullMesh(store, "127.0.0.1", "a");
+        std::shared_ptr<hydra::Context> c2;
+        if (apipe) {
+          c2 = std::make_shared<hydra::Context>(r, P);
+          c2->connectFullMesh(store, "127.0.0.1", "b");
+        }
+        const size_t stride = (size_t)P * nptr;
+        std::vector<std::vector<uint64_t>> in(nptr, std::vector<uint64_t>(n)),
+            out(nptr, std::vector<uint64_t>(n, 0));
+        for (int i = 0; i < nptr; i++)
+          for (size_t k = 0; k < n; k++) in[i][k] = k * stride + (size_t)r * nptr + i;
+        if (apipe) {
+          hydra::APipeAllreduceOptions o(c1, c2);
+          o.setInput(in[0].data(), n);
+          o.setOutput(out[0].data(), n);
+          o.setReduceFunction(&sum_u64);
+          hydra::apipe_allreduce(o);
+        } else {
+          hydra::AllreduceOptions o(c1);
+          std::vector<uint64_t*> optr, iptr;
+          for (int i = 0; i < nptr; i++) {
+            if (inplace) out[i] = in[i];
+            optr.push_back(out[i].data());
+            iptr.push_back(in[i].data());
+          }
+          o.setOutputs(optr, n);
+          if (!inplace) o.setInputs(iptr, n);
+          o.setReduceFunction(&sum_u64);
+          o.setMaxSegmentSize(128);
+          hydra::allreduce(o);
+        }
+        const size_t base = stride * (stride - 1) / 2;
+        const int nout = apipe ? 1 : nptr;
+        const size_t s2 = apipe ? (size_t)P * P : stride * stride;
+        const size_t b2 = apipe ? (size_t)P * (P - 1) / 2 : base;
+        for (int i = 0; i < nout; i++)
+          for (size_t k = 0; k < n; k++)
+            if (out[i][k] != k * s2 + b2) bad[r] = 1;
+      } catch (const std::exception& e) {
+        std::fprintf(stderr, "rank %d: %s\n", r, e.what());
+        bad[r] = 1;
+      }
+    });
+  }
+  for (auto& t : th) t.join();
+  for (int b : bad)
+    if (b) return 1;
+  return 0;
+}
+
+int main() {
+  int fails = 0;
+  for (int P : {1, 2, 3, 4})
+    for (int nptr : {1, 2})
+      for (bool inplace : {true, false})
+        for (size_t n : {(size_t)1, (size_t)100, (size_t)10000}) {
+          if (run(P, nptr, n, inplace, false)) {
+            std::fprintf(stderr, "FAIL allreduce P=%d nptr=%d n=%zu inplace=%d\n", P, nptr, n,
+                         (int)inplace);
+            fails++;
+          }
+        }
+  for (int P : {2, 3})
+    for (size_t n : {(size_t)1000, (size_t)70000})
+      if (run(P, 1, n, false, true)) {
+        std::fprintf(stderr, "FAIL apipe P=%d n=%zu\n", P, n);
+        fails++;
+      }
+  std::printf("%s\n", fails ? "FAILED" : "OK");
+  return fails ? 1 : 0;
+}
