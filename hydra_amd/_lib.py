@@ -33,9 +33,9 @@ EXPORTS = [  # every symbol include/hydra_hip.h declares
     "hydra_plan", "hydra_allreduce_simulate", "hydra_fold",
 ]
 
-ALGO_AUTO, ALGO_RING, ALGO_DIRECT, ALGO_RCCL, ALGO_A2A = range(5)
+ALGO_AUTO, ALGO_RING, ALGO_DIRECT, ALGO_RCCL, ALGO_A2A, ALGO_RING_OLD = range(6)
 ALGOS = {"auto": ALGO_AUTO, "ring": ALGO_RING, "direct": ALGO_DIRECT, "rccl": ALGO_RCCL,
-         "a2a": ALGO_A2A}
+         "a2a": ALGO_A2A, "ring_old": ALGO_RING_OLD}
 ACC_F32 = 1
 UNIQUE_ID_BYTES = 128
 

@@ -72,6 +72,32 @@ int spawn(int P, int rails, char* err, size_t errlen,
 
 }  // namespace
 
+namespace {
+template <typename T>
+int old_ring(int P, int nptr, size_t n, void** bufs, int reducer, hydra_inplace_fn fn, char* err,
+             size_t errlen) {
+  using RF = hydra::ReductionFunction<T>;
+  const RF* rf = nullptr;
+  std::unique_ptr<RF> custom;
+  if (reducer == HYDRA_REDUCER_FN) {
+    if (!fn) {
+      set_err(err, errlen, "null reduce function");
+      return 2;
+    }
+    custom.reset(new RF(hydra::CUSTOM, reinterpret_cast<typename RF::Function*>(fn)));
+    rf = custom.get();
+  } else {
+    rf = hydra::gloo_compat::gpuReductionFunction<RF, T>(hydra::SUM);
+  }
+  return spawn(P, 1, err, errlen, [&](int r, std::vector<std::shared_ptr<hydra::Context>>& c) {
+    std::vector<T*> ptrs;
+    for (int i = 0; i < nptr; i++) ptrs.push_back(static_cast<T*>(bufs[r * nptr + i]));
+    hydra::AllreduceRing<T> algo(c[0], ptrs, (int)n, rf);
+    algo.run();
+  });
+}
+}  // namespace
+
 extern "C" {
 
 int hydra_host_allreduce_threads(int P, int nptr, int op, int dtype, size_t n, void** in,
@@ -148,6 +174,25 @@ int hydra_host_bench(int config, int P, size_t n, int warmup, int iters, int red
       time_it([&] { hydra::apipe_allreduce(o); });
     }
   });
+}
+
+int hydra_host_allreduce_ring_old_threads(int P, int nptr, int dtype, size_t n, void** bufs,
+                                          int reducer, hydra_inplace_fn fn, char* err,
+                                          size_t errlen) {
+  if (P < 1 || nptr < 1 || !bufs) {
+    set_err(err, errlen, "invalid arguments");
+    return 2;
+  }
+  switch (dtype) {
+    case HYDRA_FLOAT32: return old_ring<float>(P, nptr, n, bufs, reducer, fn, err, errlen);
+    case HYDRA_INT32: return old_ring<int32_t>(P, nptr, n, bufs, reducer, fn, err, errlen);
+    case HYDRA_FLOAT64: return old_ring<double>(P, nptr, n, bufs, reducer, fn, err, errlen);
+    case HYDRA_FLOAT16:
+      if (reducer != HYDRA_REDUCER_FN) break;
+      return old_ring<uint16_t>(P, nptr, n, bufs, reducer, fn, err, errlen);
+  }
+  set_err(err, errlen, "unsupported dtype for AllreduceRing");
+  return 3;
 }
 
 void hydra_host_calculate_elements(int table, int P, size_t n, size_t* e1, size_t* e2) {

@@ -41,7 +41,9 @@ enum PlanKind : int32_t {
   kOpAllGather = 7,  // collective, in place: user[off + r*bytes, bytes] -> every rank's same range
 };
 enum PlanBuf : int32_t { kBufUser = 0, kBufScratch = 1 };
-enum Algo : int32_t { kAlgoAuto = 0, kAlgoRing = 1, kAlgoDirect = 2, kAlgoRccl = 3, kAlgoA2A = 4 };
+enum Algo : int32_t {
+  kAlgoAuto = 0, kAlgoRing = 1, kAlgoDirect = 2, kAlgoRccl = 3, kAlgoA2A = 4, kAlgoRingOld = 5
+};
 
 // Mirrored by hydra_plan_op_t in include/hydra_xgmi.h (same layout).
 struct PlanOp {
@@ -137,6 +139,7 @@ inline size_t plan_scratch_bytes(int algo, const PlanGeom& g) {
   if (algo == kAlgoRing) return 2 * g.chunk;
   if (algo == kAlgoDirect) return 2 * (size_t)(g.P - 1) * g.chunk;
   if (algo == kAlgoA2A) return g.total;
+  if (algo == kAlgoRingOld) return 2 * round_up_sz(g.total, 16);
   return 0;
 }
 
@@ -273,7 +276,38 @@ inline std::vector<PlanOp> plan_a2a(const PlanGeom& g, int r) {
   return pb.ops;
 }
 
+// ---- RING_OLD: old-style gloo::AllreduceRing<T> (allreduce_ring.h:71-106) -------------------
+// P-1 rounds over the WHOLE bucket: round k sends rank+1 what this rank received in round k-1
+// (round 0: its own bucket), receives rank-1's into scratch slot k%2 and folds it in place
+// (x = x op inbox).  Rank r ends with x_r op x_{r-1} op ... op x_{r-P+1} -- its own order, as
+// in the reference.  Chunked so round k of chunk c overlaps the fold of chunk c-1.
+inline std::vector<PlanOp> plan_ring_old(const PlanGeom& g, int r) {
+  PlanBuilder pb;
+  const int P = g.P;
+  if (P <= 1 || g.total == 0) return pb.ops;
+  const int right = (r + 1) % P, left = (r + P - 1) % P;
+  const int64_t slot_bytes = (int64_t)round_up_sz(g.total, 16);
+  const size_t C = (g.total + g.chunk - 1) / g.chunk;
+  std::vector<int> reader[2] = {std::vector<int>(C, -1), std::vector<int>(C, -1)};
+  for (int k = 0; k < P - 1; k++) {
+    const int in_slot = k & 1;
+    for (size_t c = 0; c < C; c++) {
+      const int64_t off = (int64_t)(c * g.chunk);
+      const int64_t len = (int64_t)std::min(g.chunk, g.total - c * g.chunk);
+      if (k == 0) pb.add(kOpSend, right, kBufUser, off, len);
+      else pb.add(kOpSend, right, kBufScratch, (int64_t)((k - 1) & 1) * slot_bytes + off, len);
+      pb.add(kOpRecv, left, kBufScratch, (int64_t)in_slot * slot_bytes + off, len);
+      const int grp = pb.add(kOpGroup, -1, 0, 0, 0, 0, 0, 0, reader[in_slot][c]);
+      reader[in_slot][c] =
+          pb.add(kOpReduce, -1, kBufUser, off, len, (int64_t)in_slot * slot_bytes + off, 0, 2,
+                 grp);
+    }
+  }
+  return pb.ops;
+}
+
 inline std::vector<PlanOp> make_plan(int algo, const PlanGeom& g, int r) {
+  if (algo == kAlgoRingOld) return plan_ring_old(g, r);
   if (algo == kAlgoRing) return plan_ring(g, r);
   if (algo == kAlgoA2A) return plan_a2a(g, r);
   return plan_direct(g, r);

@@ -164,6 +164,16 @@ def expected_fold_f32(xs: list[np.ndarray], max_segment: int = 1 << 20) -> np.nd
     return out
 
 
+def expected_old_ring_f32(xs: list[np.ndarray], rank: int) -> np.ndarray:
+    """Self-check for the bench: the old-style AllreduceRing<T> result on `rank` -- its own left
+    fold x_r + x_{r-1} + ... + x_{r-P+1} (allreduce_ring.h:71-106)."""
+    P = len(xs)
+    acc = xs[rank].astype(np.float32)
+    for d in range(1, P):
+        acc = acc + xs[(rank - d) % P]
+    return acc
+
+
 def bench_allreduce(args, dev) -> dict:
     """bench.py --gpus N (N > 1): BASELINE config 4 (fp32 64 Mi per rank) on this rank."""
     import torch
@@ -206,6 +216,13 @@ def bench_allreduce(args, dev) -> dict:
             ok = bool(np.array_equal(t.cpu().numpy().view(np.uint32), exp.view(np.uint32)))
             ok_all = max_over_ranks(0.0 if ok else 1.0, dev) == 0.0
             parity[a] = "bit-exact" if ok_all else "MISMATCH"
+        t = torch.from_numpy(xs[rank].copy()).to(dev)
+        comm.allreduce_(t, algo="ring_old")
+        torch.cuda.synchronize(dev)
+        ok = bool(np.array_equal(t.cpu().numpy().view(np.uint32),
+                                 expected_old_ring_f32(xs, rank).view(np.uint32)))
+        parity["ring_old"] = ("bit-exact" if max_over_ranks(0.0 if ok else 1.0, dev) == 0.0
+                              else "MISMATCH")
         # 2) exactness at full size: integer-valued inputs whose sums are exact in fp32
         j = np.arange(n, dtype=np.int64)
         x = torch.from_numpy(((j % 1024) * (rank + 1)).astype(np.float32)).to(dev)
@@ -252,7 +269,7 @@ def bench_allreduce(args, dev) -> dict:
         # 4) context: the other algorithms on the same bucket (fewer steps)
         others = {}
         k = max(5, args.steps // 4)
-        for a in ("ring", "direct", "a2a", "rccl"):
+        for a in ("ring", "direct", "a2a", "rccl", "ring_old"):
             if a == chosen:
                 continue
 

@@ -18,6 +18,7 @@
 #include <chrono>
 #include <cstddef>
 #include <cstdint>
+#include <cstring>
 #include <functional>
 #include <map>
 #include <memory>
@@ -211,5 +212,71 @@ class APipeAllreduceOptions {
 };
 
 void apipe_allreduce(APipeAllreduceOptions& opts);
+
+// ---- old-style Algorithm API (gloo/gloo/algorithm.h:20-96, allreduce_ring.h:20-125) --------
+enum ReductionType { SUM = 1, PRODUCT = 2, MAX = 3, MIN = 4, CUSTOM = 1000 };
+
+// gloo::ReductionFunction<T>: a (type, fn) pair, fn(x, y, n) computes x = op(x, y).  hydra's
+// GPU instances come from include/hydra/gloo_reduce.h (gpuReductionFunction<T>()).
+template <typename T>
+class ReductionFunction {
+ public:
+  using Function = void(T*, const T*, size_t);
+  ReductionFunction(ReductionType type, Function* fn) : type_(type), fn_(fn) {}
+  ReductionType type() const { return type_; }
+  void call(T* x, const T* y, size_t n) const { fn_(x, y, n); }
+
+ private:
+  ReductionType type_;
+  Function* fn_;
+};
+
+// gloo::AllreduceRing<T>: P-1 rounds, each sends the full outbox to rank+1 and folds the inbox
+// from rank-1 into ptrs[0] (x = x op inbox), so rank r ends with x_r op x_{r-1} op ... (its own
+// left fold -- ranks differ in the last bits for floats, exactly like the reference).  The
+// reference's notification handshake (allreduce_ring.h:97-103) is implicit here: a receive is
+// only posted once this rank's inbox is free, and the FIFO transport holds the sender's bytes.
+template <typename T>
+class AllreduceRing {
+ public:
+  AllreduceRing(const std::shared_ptr<Context>& context, const std::vector<T*>& ptrs, int count,
+                const ReductionFunction<T>* fn)
+      : ctx_(context), ptrs_(ptrs), count_(count), bytes_((size_t)count * sizeof(T)), fn_(fn) {
+    if (!fn_) throw EnforceNotMet("AllreduceRing: null reduction function");
+    if (ptrs_.empty()) throw EnforceNotMet("AllreduceRing: no pointers");
+    boxes_[0].resize(bytes_);
+    boxes_[1].resize(bytes_);
+  }
+
+  void run() {
+    for (size_t i = 1; i < ptrs_.size(); i++) fn_->call(ptrs_[0], ptrs_[i], count_);
+    const int P = ctx_->size;
+    if (P > 1 && count_ > 0) {
+      const int right = (ctx_->rank + 1) % P, left = (ctx_->rank + P - 1) % P;
+      std::memcpy(boxes_[0].data(), ptrs_[0], bytes_);  // outbox = local value
+      int out = 0;
+      for (int round = 0; round < P - 1; round++) {
+        auto ob = ctx_->createUnboundBuffer(boxes_[out].data(), bytes_);
+        auto ib = ctx_->createUnboundBuffer(boxes_[out ^ 1].data(), bytes_);
+        ib->recv(left, kSlot, 0, bytes_);
+        ob->send(right, kSlot, 0, bytes_);
+        ib->waitRecv(ctx_->getTimeout());
+        fn_->call(ptrs_[0], reinterpret_cast<const T*>(boxes_[out ^ 1].data()), count_);
+        ob->waitSend(ctx_->getTimeout());
+        out ^= 1;  // next round forwards what was just received (allreduce_ring.h:92-94)
+      }
+    }
+    for (size_t i = 1; i < ptrs_.size(); i++) std::memcpy(ptrs_[i], ptrs_[0], bytes_);
+  }
+
+ private:
+  static constexpr uint64_t kSlot = uint64_t(0x10) << 56;
+  std::shared_ptr<Context> ctx_;
+  std::vector<T*> ptrs_;
+  int count_;
+  size_t bytes_;
+  const ReductionFunction<T>* fn_;
+  std::vector<char> boxes_[2];
+};
 
 }  // namespace hydra

@@ -151,6 +151,16 @@ void hostSumInPlace(T* x, const T* y, size_t n) {
   enforce(hydra_reduce_host(lease.get(), HYDRA_SUM, dtype_of<T>(), x, x, y, n));
 }
 
+// --- an old-style ReductionFunction<T> whose fn is the GPU sum ------------------------------
+// Works for gloo::ReductionFunction<T> (algorithm.h:59-96) and hydra::ReductionFunction<T>
+// (include/hydra/allreduce.h):  gpuReductionFunction<gloo::ReductionFunction<float>, float>(
+// gloo::SUM)  ->  a pointer usable wherever ReductionFunction<float>::sum is.
+template <typename RF, typename T, typename Enum>
+const RF* gpuReductionFunction(Enum sum) {
+  static const RF fn(sum, &hostSumInPlace<T>);
+  return &fn;
+}
+
 // --- CudaReductionFunction<T> device function shape (x = op(x, y) on a stream) ---------------
 template <typename T>
 void deviceSumInPlace(T* x, const T* y, size_t n, hydra_stream_t stream) {

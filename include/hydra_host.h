@@ -43,6 +43,15 @@ int hydra_host_bench(int config, int P, size_t n, int warmup, int iters, int red
 
 void hydra_host_calculate_elements(int table, int P, size_t n, size_t* e1, size_t* e2);
 
+/* Old-style gloo::AllreduceRing<T>::run() (allreduce_ring.h:20-125) on P thread-ranks, in place
+ * on bufs ([rank][ptr]).  fn, when reducer == HYDRA_REDUCER_FN, has the
+ * ReductionFunction<T>::Function shape void(T* x, const T* y, size_t n). dtype: float32, int32,
+ * float64 (GPU or custom reducer), float16 (custom reducer only). */
+typedef void (*hydra_inplace_fn)(void* x, const void* y, size_t n);
+int hydra_host_allreduce_ring_old_threads(int P, int nptr, int dtype, size_t n, void** bufs,
+                                          int reducer, hydra_inplace_fn fn, char* err,
+                                          size_t errlen);
+
 /* AllreduceNewTest.TestTimeout (allreduce_test.cc:381-397): rank 0 of 2 times out; returns 0 and
  * the IoException text if it was raised. */
 int hydra_host_timeout_probe(long timeout_ms, char* what, size_t len);

@@ -126,6 +126,31 @@ def gen_ring(out: dict, meta: dict) -> None:
     meta["ring"] = rows
 
 
+def gen_old_ring(out: dict, meta: dict) -> None:
+    """Old-style AllreduceRing<T> (allreduce_ring.h:20-125): per-rank outputs (they differ)."""
+    rows = []
+    rng = np.random.default_rng(77)
+    for name, code in (("f32", 6), ("i32", 2), ("f16", 8)):
+        for P in (1, 2, 3, 5, 8):
+            for n in (1, 100, 4099):
+                for nptr in (1, 2):
+                    if name == "f32":
+                        bufs = [[synth.stress_f32(P, r, n, seed=500 + i) for i in range(nptr)]
+                                for r in range(P)]
+                    elif name == "i32":
+                        bufs = [[synth.int32_bucket(P, r, n, seed=500 + i) for i in range(nptr)]
+                                for r in range(P)]
+                    else:
+                        bufs = [[np.array([O.f2h(float(v)) for v in rng.uniform(-8, 8, n)],
+                                          np.uint16) for _ in range(nptr)] for _ in range(P)]
+                    key = f"oldring_{name}_P{P}_n{n}_k{nptr}"
+                    out[key + "_in"] = np.stack([np.stack(b) for b in bufs])
+                    O.ref_allreduce_ring_old(bufs, dtype_code=code)
+                    out[key + "_out"] = np.stack([np.stack(b) for b in bufs])
+                    rows.append({"key": key, "P": P, "n": n, "nptr": nptr, "dtype": code})
+    meta["old_ring"] = rows
+
+
 def gen_new_test(meta: dict) -> None:
     """AllreduceNewTest.Default (test/allreduce_test.cc:302-362): confirm the reference meets the
     closed form k*stride^2 + stride(stride-1)/2 for uint64, every combination we test."""
@@ -163,6 +188,7 @@ def main() -> None:
                                "oracle/Makefile (g++ -O3 -DNDEBUG)"}
     gen_ops(out, meta)
     gen_ring(out, meta)
+    gen_old_ring(out, meta)
     gen_new_test(meta)
     import ctypes
     buf = ctypes.create_string_buffer(512)

@@ -371,3 +371,33 @@ void orc_sum_f32(void* c, const void* a, const void* b, size_t n) { orc_op(OP_SU
 void orc_sum_i32(void* c, const void* a, const void* b, size_t n) { orc_op(OP_SUM, D_INT32, c, a, b, n); }
 void orc_sum_u64(void* c, const void* a, const void* b, size_t n) { orc_op(OP_SUM, D_UINT64, c, a, b, n); }
 void orc_sum_f16(void* c, const void* a, const void* b, size_t n) { orc_op(OP_SUM, D_FLOAT16, c, a, b, n); }
+
+/* ---- old-style AllreduceRing<T> (gloo/gloo/allreduce_ring.h:71-106) ----
+ * bufs: P*nptr pointers [rank][ptr], in place.  Per rank: ptrs[0] = op(ptrs[0], ptrs[i]) for
+ * i >= 1 (in place); then P-1 rounds each folding the raw local value of the next rank to the
+ * LEFT: acc = op(acc, x_{r-k}) for k = 1..P-1 (c == a == acc); then ptrs[i] = ptrs[0].
+ * Unlike the new-style ring, every rank ends with its own fold order. */
+int orc_allreduce_ring_old(int P, int nptr, int op, int dtype, size_t n, void** bufs) {
+  size_t es = orc_esize(dtype);
+  if (!es || P < 1 || nptr < 1) return 1;
+  size_t bytes = n * es;
+  unsigned char* x = (unsigned char*)malloc(bytes * (size_t)P + 1);
+  if (!x) return 2;
+  for (int r = 0; r < P; r++) {
+    void* p0 = bufs[r * nptr];
+    for (int i = 1; i < nptr; i++) orc_op(op, dtype, p0, p0, bufs[r * nptr + i], n);
+    memcpy(x + (size_t)r * bytes, p0, bytes);
+  }
+  for (int r = 0; r < P; r++) {
+    void* p0 = bufs[r * nptr];
+    for (int k = 1; k < P; k++)
+      orc_op(op, dtype, p0, p0, x + (size_t)((r - k + P) % P) * bytes, n);
+    for (int i = 1; i < nptr; i++) memcpy(bufs[r * nptr + i], p0, bytes);
+  }
+  free(x);
+  return 0;
+}
+/* ReductionFunction<T>::Function-shaped (x = x op y) entry points for host-runtime tests. */
+void orc_isum_f32(void* x, const void* y, size_t n) { orc_op(OP_SUM, D_FLOAT32, x, x, y, n); }
+void orc_isum_i32(void* x, const void* y, size_t n) { orc_op(OP_SUM, D_INT32, x, x, y, n); }
+void orc_isum_f16(void* x, const void* y, size_t n) { orc_op(OP_SUM, D_FLOAT16, x, x, y, n); }

@@ -64,6 +64,8 @@ def orc():
         _orc.orc_h2f.argtypes = [ctypes.c_uint16]
         _orc.orc_h2f.restype = ctypes.c_float
         _orc.orc_acc_bf16_f32.argtypes = [_vp, _vp, _c]
+        _orc.orc_allreduce_ring_old.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                ctypes.c_int, _c, _vp]
     return _orc
 
 
@@ -87,6 +89,8 @@ def ref():
                                         ctypes.c_char_p, _c]
         _ref.ref_float2half.argtypes = [ctypes.c_float]
         _ref.ref_float2half.restype = ctypes.c_uint16
+        _ref.ref_allreduce_ring_old.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, _c,
+                                                _vp, ctypes.c_char_p, _c]
     return _ref
 
 
@@ -165,6 +169,33 @@ def ring_result(xs: list[np.ndarray], max_segment: int = 1 << 20, kind: str = "s
     outs = [[x.copy()] for x in xs]
     allreduce(len(xs), outs, None, kind, dtype_code, max_segment)
     return outs[0][0]
+
+
+def _old_ring(fn_is_ref, bufs, kind, dtype_code):
+    """bufs: [rank][ptr] arrays, in place."""
+    P, nptr = len(bufs), len(bufs[0])
+    n = bufs[0][0].size
+    code = _dt(bufs[0][0], dtype_code)
+    ptrs = (_vp * (P * nptr))(*[_ptr(b) for r in bufs for b in r])
+    if fn_is_ref:
+        err = ctypes.create_string_buffer(512)
+        rc = ref().ref_allreduce_ring_old(P, nptr, code, n, ctypes.cast(ptrs, _vp), err, 512)
+        if rc:
+            raise RuntimeError(f"reference AllreduceRing failed: {err.value.decode()}")
+    else:
+        if orc().orc_allreduce_ring_old(P, nptr, OPS[kind], code, n, ctypes.cast(ptrs, _vp)):
+            raise RuntimeError("oracle AllreduceRing failed")
+    return bufs
+
+
+def allreduce_ring_old(bufs, kind="sum", dtype_code=None):
+    """C restatement of the old-style gloo::AllreduceRing<T>::run() over len(bufs) ranks."""
+    return _old_ring(False, bufs, kind, dtype_code)
+
+
+def ref_allreduce_ring_old(bufs, dtype_code=None):
+    """The reference's own AllreduceRing<T> (ReductionFunction<T>::sum) on thread-ranks."""
+    return _old_ring(True, bufs, "sum", dtype_code)
 
 
 def split_aa(P: int, n: int):

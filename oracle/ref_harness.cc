@@ -13,6 +13,7 @@
 // bench.py's cpu_baseline leg (kind "reference").
 
 #include <chrono>
+#include <condition_variable>
 #include <cstring>
 #include <exception>
 #include <memory>
@@ -113,17 +114,25 @@ int spawn(int P, const std::function<void(int, std::shared_ptr<gloo::Context>)>&
   auto dev = loopback_device();
   std::vector<std::thread> threads;
   std::mutex mu;
+  std::condition_variable cv;
+  int arrived = 0;
   std::string first_err;
   for (int r = 0; r < P; r++) {
     threads.emplace_back([&, r]() {
+      std::shared_ptr<gloo::rendezvous::Context> ctx;
       try {
-        auto ctx = std::make_shared<gloo::rendezvous::Context>(r, P);
+        ctx = std::make_shared<gloo::rendezvous::Context>(r, P);
         ctx->connectFullMesh(store, dev);
         fn(r, ctx);
       } catch (const std::exception& e) {
         std::lock_guard<std::mutex> g(mu);
         if (first_err.empty()) first_err = e.what();
       }
+      // every rank finishes before any connection closes (base_test.h:142-155)
+      std::unique_lock<std::mutex> l(mu);
+      arrived++;
+      cv.notify_all();
+      cv.wait(l, [&] { return arrived == P; });
     });
   }
   for (auto& t : threads) t.join();
@@ -245,4 +254,31 @@ int ref_bench_ring(int P, size_t n, int warmup, int iters, double* samples_ns, c
 // so the host runtime's bench can use the reference reduction as its CPU baseline reducer.
 extern "C" void ref_sum_f32(void* c, const void* a, const void* b, size_t n) {
   gloo::sum<float>(c, a, b, n);
+}
+
+// ---- old-style AllreduceRing<T> (gloo/gloo/allreduce_ring.h:20-125), §8f row 3 ------------
+#include "gloo/allreduce_ring.h"
+
+namespace {
+template <typename T>
+int run_old_ring(int P, int nptr, size_t n, void** bufs, char* err, size_t errlen) {
+  return spawn(P, [&](int r, std::shared_ptr<gloo::Context> ctx) {
+    std::vector<T*> ptrs;
+    for (int i = 0; i < nptr; i++) ptrs.push_back(static_cast<T*>(bufs[r * nptr + i]));
+    gloo::AllreduceRing<T> algo(ctx, ptrs, (int)n, gloo::ReductionFunction<T>::sum);
+    algo.run();
+  }, err, errlen);
+}
+}  // namespace
+
+// In place on bufs ([rank][ptr]), ReductionFunction<T>::sum; dtype: float32, int32, float16.
+extern "C" int ref_allreduce_ring_old(int P, int nptr, int dtype, size_t n, void** bufs,
+                                      char* err, size_t errlen) {
+  switch (dtype) {
+    case D_FLOAT32: return run_old_ring<float>(P, nptr, n, bufs, err, errlen);
+    case D_INT32: return run_old_ring<int32_t>(P, nptr, n, bufs, err, errlen);
+    case D_FLOAT16: return run_old_ring<gloo::float16>(P, nptr, n, bufs, err, errlen);
+    case D_FLOAT64: return run_old_ring<double>(P, nptr, n, bufs, err, errlen);
+  }
+  return 2;
 }

@@ -109,7 +109,12 @@ def _worker(rank, world, port, algo, n, ms, ch, q):
         wall = ring.timed_steps(lambda: None, 3, 1, lambda: None, dist.barrier)
         assert wall >= 0
         xs = [synth.stress_f32(world, r, n) for r in range(world)]
-        exp = O.ring_result(xs, ms or (1 << 20))
+        if algo == "ring_old":  # per-rank left fold (allreduce_ring.h:71-106)
+            olds = [[x.copy()] for x in xs]
+            O.allreduce_ring_old(olds)
+            exp = olds[rank][0]
+        else:
+            exp = O.ring_result(xs, ms or (1 << 20))
         q.put((rank, bool(np.array_equal(got.view(np.uint32), exp.view(np.uint32)))))
     except Exception as e:  # report instead of hanging the parent
         q.put((rank, repr(e)))
@@ -118,7 +123,7 @@ def _worker(rank, world, port, algo, n, ms, ch, q):
 
 
 @pytest.mark.parametrize("world", [2, 3])
-@pytest.mark.parametrize("algo", ["ring", "direct", "a2a"])
+@pytest.mark.parametrize("algo", ["ring", "direct", "a2a", "ring_old"])
 def test_gloo_multiprocess_plan(algo, world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

@@ -49,3 +49,19 @@ def test_apipe_gpu_reducer(gpu, O, n):
         exp[e1:] = O.ring_result([x[e1:].copy() for x in ins])
     for r in range(P):
         assert np.array_equal(outs[r].view(np.uint32), exp.view(np.uint32))
+
+
+def test_old_style_allreduce_ring_gpu_reducer_vs_reference(gpu, golden, golden_meta):
+    """hydra::AllreduceRing<T> with the GPU in-place sum (gpuReductionFunction) reproduces the
+    reference's own old-style AllreduceRing<T> outputs (tests/golden old_ring) for f32/i32;
+    f16 is exercised by the CPU test with the custom reducer."""
+    for row in golden_meta["old_ring"]:
+        if row["dtype"] not in (6, 2):  # FLOAT32, INT32
+            continue
+        key = row["key"]
+        ins = golden[key + "_in"]
+        bufs = [[ins[r, i].copy() for i in range(row["nptr"])] for r in range(row["P"])]
+        host.allreduce_ring_old_threads(bufs, dtype_code=row["dtype"])
+        got = np.stack([np.stack(b) for b in bufs])
+        exp = golden[key + "_out"]
+        assert np.array_equal(got.view(np.uint32), exp.view(np.uint32)), key

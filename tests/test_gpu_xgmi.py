@@ -195,3 +195,45 @@ def test_fold_abi_reference_order(gpu, O, P, variant):
         for j in range(P - 2, -1, -1):
             acc = O.op(xs[j], acc, "sum", 6)
         assert np.array_equal(dst.cpu().numpy()[1:n + 1].view(np.uint32), acc.view(np.uint32))
+
+
+def test_simulated_ring_old_vs_reference_fixtures(gpu, golden, golden_meta):
+    """Device RING_OLD plan == the reference's own old-style AllreduceRing<T> outputs
+    (tests/golden old_ring fixtures, built from allreduce_ring.h), every rank, f32/i32/f16.
+    Several pointers per rank: the local pre-reduce ptrs[0] op= ptrs[i] and the closing
+    broadcast (allreduce_ring.h:60-66,108-112) are hydra_reduce + copies around the plan."""
+    import torch
+
+    from hydra_amd import reduce as R
+
+    views = {_lib.FLOAT32: np.uint32, _lib.INT32: np.int32, _lib.FLOAT16: np.int16}
+    for row in golden_meta["old_ring"]:
+        key, P, k, code = row["key"], row["P"], row["nptr"], row["dtype"]
+        ins = golden[key + "_in"]
+        exp = golden[key + "_out"]
+        v = views[code]
+        bufs = [[torch.from_numpy(ins[r, i].view(v).copy()).to(gpu) for i in range(k)]
+                for r in range(P)]
+        for r in range(P):
+            for i in range(1, k):
+                R.reduce_("sum", bufs[r][0], bufs[r][0], bufs[r][i], dtype_code=code)
+        ring.simulate([b[0] for b in bufs], algo="ring_old", dtype_code=code, chunk_bytes=1024)
+        for r in range(P):
+            for i in range(1, k):
+                bufs[r][i].copy_(bufs[r][0])
+        torch.cuda.synchronize()
+        for r in range(P):
+            for i in range(k):
+                got = bufs[r][i].cpu().numpy()
+                assert np.array_equal(got, exp[r, i].view(v)), (key, r, i)
+
+
+@pytest.mark.parametrize("P,n", [(2, 1 << 20), (8, 3000001)])
+def test_simulated_ring_old_large(gpu, O, P, n):
+    xs = [synth.stress_f32(P, r, n) for r in range(P)]
+    bufs = dev_bufs(gpu, xs)
+    ring.simulate(bufs, algo="ring_old")
+    olds = [[x.copy()] for x in xs]
+    O.allreduce_ring_old(olds)
+    for r in range(P):
+        assert np.array_equal(bufs[r].cpu().numpy().view(np.uint32), olds[r][0].view(np.uint32))

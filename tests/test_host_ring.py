@@ -98,3 +98,18 @@ def test_bench_bodies_run(O):
     assert s.shape == (3,) and np.all(s > 0)
     s = host.bench(3, 2, 1 << 16, 1, 3, reducer_fn=fnptr(O, "orc_sum_f32"))
     assert np.all(s > 0)
+
+
+def test_old_style_allreduce_ring_vs_golden(O, golden, golden_meta):
+    """hydra::AllreduceRing<T> (old Algorithm API, allreduce_ring.h:20-125) reproduces the
+    reference's per-rank results -- the oracle's in-place reduction stands in for the GPU."""
+    names = {6: "orc_isum_f32", 2: "orc_isum_i32", 8: "orc_isum_f16"}
+    for row in golden_meta["old_ring"]:
+        key = row["key"]
+        ins = golden[key + "_in"]
+        bufs = [[ins[r, i].copy() for i in range(row["nptr"])] for r in range(row["P"])]
+        host.allreduce_ring_old_threads(bufs, dtype_code=row["dtype"],
+                                        reducer_fn=fnptr(O, names[row["dtype"]]))
+        got = np.stack([np.stack(b) for b in bufs])
+        exp = golden[key + "_out"]
+        assert np.array_equal(got.view(f"u{got.itemsize}"), exp.view(f"u{exp.itemsize}")), key

@@ -291,3 +291,17 @@ def test_plan_geometry_matches_ring_plan():
         lo = min(o["off"] for o in folds)
         hi = max(o["off"] + o["bytes"] for o in folds)
         assert lo == min(4 * n, r * S * sb) and hi == min(4 * n, (r + 1) * S * sb)
+
+
+@pytest.mark.parametrize("P,n,ch", [(2, 1, 0), (3, 1000, 256), (5, 4099, 1024), (8, 100003, 4096),
+                                    (4, 262145, 0)])
+def test_ring_old_plan(O, P, n, ch):
+    """Old-style AllreduceRing<T> on device (plan RING_OLD): per-rank left folds, bit-exact vs
+    the oracle restatement (pinned to the reference by tests/test_oracle.py), and race-free."""
+    xs = [synth.stress_f32(P, r, n) for r in range(P)]
+    outs = run_plan_numpy(O, "ring_old", xs, 0, ch)
+    bufs = [[x.copy()] for x in xs]
+    O.allreduce_ring_old(bufs)
+    for r in range(P):
+        assert np.array_equal(outs[r].view(np.uint32), bufs[r][0].view(np.uint32)), r
+        race_check(ring.plan("ring_old", P, r, n, 4, 0, ch)[0])
