@@ -33,9 +33,10 @@ EXPORTS = [  # every symbol include/hydra_hip.h declares
     "hydra_plan", "hydra_allreduce_simulate", "hydra_fold",
 ]
 
-ALGO_AUTO, ALGO_RING, ALGO_DIRECT, ALGO_RCCL, ALGO_A2A, ALGO_RING_OLD = range(6)
+ALGO_AUTO, ALGO_RING, ALGO_DIRECT, ALGO_RCCL, ALGO_A2A, ALGO_RING_OLD, ALGO_RING_CHUNKED = range(7)
 ALGOS = {"auto": ALGO_AUTO, "ring": ALGO_RING, "direct": ALGO_DIRECT, "rccl": ALGO_RCCL,
-         "a2a": ALGO_A2A, "ring_old": ALGO_RING_OLD}
+         "a2a": ALGO_A2A, "ring_old": ALGO_RING_OLD,
+         "ring_chunked": ALGO_RING_CHUNKED}
 ACC_F32 = 1
 UNIQUE_ID_BYTES = 128
 

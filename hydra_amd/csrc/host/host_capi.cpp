@@ -1,6 +1,7 @@
 // host_capi.cpp -- extern "C" drivers of the host runtime (include/hydra_host.h).
 #include <chrono>
 #include <condition_variable>
+#include <cstdint>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -74,8 +75,8 @@ int spawn(int P, int rails, char* err, size_t errlen,
 
 namespace {
 template <typename T>
-int old_ring(int P, int nptr, size_t n, void** bufs, int reducer, hydra_inplace_fn fn, char* err,
-             size_t errlen) {
+int old_ring(bool chunked, int P, int nptr, size_t n, void** bufs, int reducer, hydra_inplace_fn fn,
+             char* err, size_t errlen) {
   using RF = hydra::ReductionFunction<T>;
   const RF* rf = nullptr;
   std::unique_ptr<RF> custom;
@@ -92,8 +93,13 @@ int old_ring(int P, int nptr, size_t n, void** bufs, int reducer, hydra_inplace_
   return spawn(P, 1, err, errlen, [&](int r, std::vector<std::shared_ptr<hydra::Context>>& c) {
     std::vector<T*> ptrs;
     for (int i = 0; i < nptr; i++) ptrs.push_back(static_cast<T*>(bufs[r * nptr + i]));
-    hydra::AllreduceRing<T> algo(c[0], ptrs, (int)n, rf);
-    algo.run();
+    if (chunked) {
+      hydra::AllreduceRingChunked<T> algo(c[0], ptrs, (int)n, rf);
+      algo.run();
+    } else {
+      hydra::AllreduceRing<T> algo(c[0], ptrs, (int)n, rf);
+      algo.run();
+    }
   });
 }
 }  // namespace
@@ -176,23 +182,34 @@ int hydra_host_bench(int config, int P, size_t n, int warmup, int iters, int red
   });
 }
 
-int hydra_host_allreduce_ring_old_threads(int P, int nptr, int dtype, size_t n, void** bufs,
-                                          int reducer, hydra_inplace_fn fn, char* err,
-                                          size_t errlen) {
-  if (P < 1 || nptr < 1 || !bufs) {
+static int algorithm_ring(bool chunked, int P, int nptr, int dtype, size_t n, void** bufs,
+                          int reducer, hydra_inplace_fn fn, char* err, size_t errlen) {
+  if (P < 1 || nptr < 1 || !bufs || n > (size_t)INT32_MAX) {
     set_err(err, errlen, "invalid arguments");
     return 2;
   }
   switch (dtype) {
-    case HYDRA_FLOAT32: return old_ring<float>(P, nptr, n, bufs, reducer, fn, err, errlen);
-    case HYDRA_INT32: return old_ring<int32_t>(P, nptr, n, bufs, reducer, fn, err, errlen);
-    case HYDRA_FLOAT64: return old_ring<double>(P, nptr, n, bufs, reducer, fn, err, errlen);
+    case HYDRA_FLOAT32: return old_ring<float>(chunked, P, nptr, n, bufs, reducer, fn, err, errlen);
+    case HYDRA_INT32: return old_ring<int32_t>(chunked, P, nptr, n, bufs, reducer, fn, err, errlen);
+    case HYDRA_FLOAT64: return old_ring<double>(chunked, P, nptr, n, bufs, reducer, fn, err, errlen);
     case HYDRA_FLOAT16:
       if (reducer != HYDRA_REDUCER_FN) break;
-      return old_ring<uint16_t>(P, nptr, n, bufs, reducer, fn, err, errlen);
+      return old_ring<uint16_t>(chunked, P, nptr, n, bufs, reducer, fn, err, errlen);
   }
   set_err(err, errlen, "unsupported dtype for AllreduceRing");
   return 3;
+}
+
+int hydra_host_allreduce_ring_old_threads(int P, int nptr, int dtype, size_t n, void** bufs,
+                                          int reducer, hydra_inplace_fn fn, char* err,
+                                          size_t errlen) {
+  return algorithm_ring(false, P, nptr, dtype, n, bufs, reducer, fn, err, errlen);
+}
+
+int hydra_host_allreduce_ring_chunked_threads(int P, int nptr, int dtype, size_t n, void** bufs,
+                                              int reducer, hydra_inplace_fn fn, char* err,
+                                              size_t errlen) {
+  return algorithm_ring(true, P, nptr, dtype, n, bufs, reducer, fn, err, errlen);
 }
 
 void hydra_host_calculate_elements(int table, int P, size_t n, size_t* e1, size_t* e2) {

@@ -42,8 +42,16 @@ enum PlanKind : int32_t {
 };
 enum PlanBuf : int32_t { kBufUser = 0, kBufScratch = 1 };
 enum Algo : int32_t {
-  kAlgoAuto = 0, kAlgoRing = 1, kAlgoDirect = 2, kAlgoRccl = 3, kAlgoA2A = 4, kAlgoRingOld = 5
+  kAlgoAuto = 0, kAlgoRing = 1, kAlgoDirect = 2, kAlgoRccl = 3, kAlgoA2A = 4, kAlgoRingOld = 5,
+  kAlgoRingChunked = 6
 };
+
+// AllreduceRingChunked<T> geometry (allreduce_ring_chunked.h:32-36): 2P chunks of
+// max(256, ceil(n / 2P)) elements; trailing chunks may be short or empty.
+inline size_t chunked_ring_elems(int P, size_t n) {
+  const size_t chunks = 2 * (size_t)P;
+  return std::max<size_t>(256, (n + chunks - 1) / chunks);
+}
 
 // Mirrored by hydra_plan_op_t in include/hydra_xgmi.h (same layout).
 struct PlanOp {
@@ -140,6 +148,7 @@ inline size_t plan_scratch_bytes(int algo, const PlanGeom& g) {
   if (algo == kAlgoDirect) return 2 * (size_t)(g.P - 1) * g.chunk;
   if (algo == kAlgoA2A) return g.total;
   if (algo == kAlgoRingOld) return 2 * round_up_sz(g.total, 16);
+  if (algo == kAlgoRingChunked) return 2 * round_up_sz(chunked_ring_elems(g.P, g.n) * g.esize, 16);
   return 0;
 }
 
@@ -306,7 +315,65 @@ inline std::vector<PlanOp> plan_ring_old(const PlanGeom& g, int r) {
   return pb.ops;
 }
 
+// ---- RING_CHUNKED: gloo::AllreduceRingChunked<T> (allreduce_ring_chunked.h:77-200) ---------
+// 2P chunks; rank r starts chunks 2r and 2r+1 and each later round i (a uniform index over the
+// reduce pass, rounds 2..2P-1, then the broadcast pass, rounds 0..2P-3) receives chunk
+// co(i) from rank-1, folds it (x = x op inbox) or -- in the broadcast pass -- takes it, and
+// forwards it to rank+1.  Send i and receive i form group i; rank r's send i is rank r+1's
+// receive i, so every group is one ring step.  Chunk c, started by s = c/2, ends as
+// x_{s-1} op (x_{s-2} op (... op (x_{s+1} op x_s))) on every rank, as in the reference.
+// Empty chunks move nothing on either side (the reference's 1-element placeholder send,
+// :218-225, carries no data the receiver uses).
+inline int chunked_ring_chunk(int r, int P, int i) {
+  const int C = 2 * P;
+  const int round = i < C - 2 ? i + 2 : i - (C - 2);
+  return ((2 * r) - (round & ~1) + (round & 1) + C) % C;
+}
+
+inline std::vector<PlanOp> plan_ring_chunked(const PlanGeom& g, int r) {
+  PlanBuilder pb;
+  const int P = g.P;
+  if (P <= 1 || g.total == 0) return pb.ops;
+  const int C = 2 * P, right = (r + 1) % P, left = (r + P - 1) % P;
+  const size_t ce = chunked_ring_elems(P, g.n);
+  const int64_t slot_bytes = (int64_t)round_up_sz(ce * g.esize, 16);
+  auto span = [&](int co, int64_t* off, int64_t* len) {
+    const size_t o = (size_t)co * ce;
+    const size_t l = o >= g.n ? 0 : std::min(ce, g.n - o);
+    *off = (int64_t)(o * g.esize);
+    *len = (int64_t)(l * g.esize);
+  };
+  const int nsteps = 2 * C - 4;              // sends == receives == 4P-4
+  std::vector<int> compute(nsteps, -1);      // REDUCE issued at step i (reduce pass only)
+  std::vector<int> wrote(C, -1);             // last REDUCE that wrote user chunk c
+  for (int i = 0; i < nsteps; i++) {
+    // send i: the prelude chunks 2r, 2r+1, then what step i-2 produced
+    const int sco = i < 2 ? 2 * r + i : chunked_ring_chunk(r, P, i - 2);
+    const int rco = chunked_ring_chunk(r, P, i);
+    const bool reduce_pass = i < C - 2;
+    int64_t so, sl, ro, rl;
+    span(sco, &so, &sl);
+    span(rco, &ro, &rl);
+    const int w0 = i >= 2 ? compute[i - 2] : -1;  // produced the sent chunk / read this slot
+    const int w1 = reduce_pass ? -1 : wrote[rco];  // broadcast receives land in the user chunk
+    if (sl == 0 && rl == 0) continue;
+    if (sl) pb.add(kOpSend, right, kBufUser, so, sl);
+    const int64_t slot_off = (int64_t)(i & 1) * slot_bytes;
+    if (rl) {
+      if (reduce_pass) pb.add(kOpRecv, left, kBufScratch, slot_off, rl);
+      else pb.add(kOpRecv, left, kBufUser, ro, rl);
+    }
+    const int grp = pb.add(kOpGroup, -1, 0, 0, 0, 0, 0, 0, w0, w1);
+    if (reduce_pass && rl) {
+      compute[i] = pb.add(kOpReduce, -1, kBufUser, ro, rl, slot_off, 0, 2, grp);
+      wrote[rco] = compute[i];
+    }
+  }
+  return pb.ops;
+}
+
 inline std::vector<PlanOp> make_plan(int algo, const PlanGeom& g, int r) {
+  if (algo == kAlgoRingChunked) return plan_ring_chunked(g, r);
   if (algo == kAlgoRingOld) return plan_ring_old(g, r);
   if (algo == kAlgoRing) return plan_ring(g, r);
   if (algo == kAlgoA2A) return plan_a2a(g, r);

@@ -36,6 +36,8 @@ def lib():
         L.hydra_host_timeout_probe.argtypes = [ctypes.c_long, ctypes.c_char_p, sz]
         L.hydra_host_allreduce_ring_old_threads.argtypes = [i, i, i, sz, vp, i, vp,
                                                             ctypes.c_char_p, sz]
+        L.hydra_host_allreduce_ring_chunked_threads.argtypes = \
+            L.hydra_host_allreduce_ring_old_threads.argtypes
         _h = L
     return _h
 
@@ -82,15 +84,18 @@ def apipe_threads(ins, outs, table=SPLIT_AA, reducer_fn=None, dtype_code=_lib.FL
     return outs
 
 
-def allreduce_ring_old_threads(bufs, dtype_code=None, reducer_fn=None):
+def allreduce_ring_old_threads(bufs, dtype_code=None, reducer_fn=None, chunked=False):
     """Old-style AllreduceRing<T>::run() on len(bufs) thread-ranks; bufs: [rank][ptr], in place.
-    reducer_fn: None -> GPU sum; else address of a void(T* x, const T* y, size_t n)."""
+    reducer_fn: None -> GPU sum; else address of a void(T* x, const T* y, size_t n).
+    chunked: AllreduceRingChunked<T> instead."""
     P, nptr = len(bufs), len(bufs[0])
     n = bufs[0][0].size
     code = dtype_code if dtype_code is not None else _np_code(bufs[0][0].dtype)
     red, fp = _fn(reducer_fn)
     err = ctypes.create_string_buffer(512)
-    rc = lib().hydra_host_allreduce_ring_old_threads(
+    f = (lib().hydra_host_allreduce_ring_chunked_threads if chunked
+         else lib().hydra_host_allreduce_ring_old_threads)
+    rc = f(
         P, nptr, code, n, ctypes.cast(_ptrs([b for r in bufs for b in r]), ctypes.c_void_p), red,
         fp, err, 512)
     if rc:

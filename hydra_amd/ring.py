@@ -174,6 +174,24 @@ def expected_old_ring_f32(xs: list[np.ndarray], rank: int) -> np.ndarray:
     return acc
 
 
+def expected_chunked_ring_f32(xs: list[np.ndarray]) -> np.ndarray:
+    """Self-check for the bench: AllreduceRingChunked<T>'s result -- chunk c (2P chunks of
+    max(256, ceil(n/2P))) seeded by s = c/2 and folded x_{s+1} + x_s, x_{s+2} + (...), ..."""
+    P, n = len(xs), xs[0].size
+    ce = max(256, -(-n // (2 * P)))
+    out = np.empty(n, np.float32)
+    for c in range(2 * P):
+        lo, hi = min(n, c * ce), min(n, (c + 1) * ce)
+        if lo >= hi:
+            continue
+        s = c // 2
+        acc = xs[s][lo:hi].astype(np.float32)
+        for d in range(1, P):
+            acc = xs[(s + d) % P][lo:hi] + acc
+        out[lo:hi] = acc
+    return out
+
+
 def bench_allreduce(args, dev) -> dict:
     """bench.py --gpus N (N > 1): BASELINE config 4 (fp32 64 Mi per rank) on this rank."""
     import torch
@@ -223,6 +241,13 @@ def bench_allreduce(args, dev) -> dict:
                                  expected_old_ring_f32(xs, rank).view(np.uint32)))
         parity["ring_old"] = ("bit-exact" if max_over_ranks(0.0 if ok else 1.0, dev) == 0.0
                               else "MISMATCH")
+        t = torch.from_numpy(xs[rank].copy()).to(dev)
+        comm.allreduce_(t, algo="ring_chunked")
+        torch.cuda.synchronize(dev)
+        ok = bool(np.array_equal(t.cpu().numpy().view(np.uint32),
+                                 expected_chunked_ring_f32(xs).view(np.uint32)))
+        parity["ring_chunked"] = ("bit-exact" if max_over_ranks(0.0 if ok else 1.0, dev) == 0.0
+                                  else "MISMATCH")
         # 2) exactness at full size: integer-valued inputs whose sums are exact in fp32
         j = np.arange(n, dtype=np.int64)
         x = torch.from_numpy(((j % 1024) * (rank + 1)).astype(np.float32)).to(dev)
@@ -269,7 +294,7 @@ def bench_allreduce(args, dev) -> dict:
         # 4) context: the other algorithms on the same bucket (fewer steps)
         others = {}
         k = max(5, args.steps // 4)
-        for a in ("ring", "direct", "a2a", "rccl", "ring_old"):
+        for a in ("ring", "direct", "a2a", "rccl", "ring_old", "ring_chunked"):
             if a == chosen:
                 continue
 

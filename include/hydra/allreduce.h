@@ -279,4 +279,97 @@ class AllreduceRing {
   std::vector<char> boxes_[2];
 };
 
+// gloo::AllreduceRingChunked<T> (allreduce_ring_chunked.h:20-248): 2P chunks of
+// max(256, ceil(count/2P)) elements.  Rank r seeds chunks 2r and 2r+1; each later step i
+// (reduce pass rounds 2..2P-1, then broadcast pass rounds 0..2P-3) receives chunk co(i) from
+// rank-1 into inbox[i&1], folds it into ptrs[0] (x = x op inbox) or, in the broadcast pass,
+// copies it, and forwards that chunk to rank+1.  Every rank ends with the same bits: chunk c,
+// seeded by s = c/2, is x_{s-1} op (x_{s-2} op (... op x_s)).  The reference's notification
+// handshake is implicit (a receive is posted only once its inbox is free; the transport holds
+// early bytes), and empty chunks move nothing instead of the reference's 1-element
+// placeholder (:218-225), which its receiver ignores.
+template <typename T>
+class AllreduceRingChunked {
+ public:
+  AllreduceRingChunked(const std::shared_ptr<Context>& context, const std::vector<T*>& ptrs,
+                       int count, const ReductionFunction<T>* fn)
+      : ctx_(context), ptrs_(ptrs), count_(count), fn_(fn) {
+    if (!fn_) throw EnforceNotMet("AllreduceRingChunked: null reduction function");
+    if (ptrs_.empty()) throw EnforceNotMet("AllreduceRingChunked: no pointers");
+    if (count_ < 0) throw EnforceNotMet("AllreduceRingChunked: negative count");
+    chunks_ = 2 * (size_t)ctx_->size;
+    chunk_ = std::max<size_t>(256, ((size_t)count_ + chunks_ - 1) / chunks_);
+    for (auto& b : inbox_) b.resize(chunk_ * sizeof(T));
+  }
+
+  void run() {
+    const size_t bytes = (size_t)count_ * sizeof(T);
+    for (size_t i = 1; i < ptrs_.size(); i++) fn_->call(ptrs_[0], ptrs_[i], count_);
+    const int P = ctx_->size, r = ctx_->rank;
+    if (P > 1 && count_ > 0) {
+      const int right = (r + 1) % P, left = (r + P - 1) % P;
+      const int C = (int)chunks_, steps = 2 * C - 4;
+      const auto tmo = ctx_->getTimeout();
+      auto out = ctx_->createUnboundBuffer(ptrs_[0], bytes);
+      std::unique_ptr<UnboundBuffer> in[2] = {
+          ctx_->createUnboundBuffer(inbox_[0].data(), inbox_[0].size()),
+          ctx_->createUnboundBuffer(inbox_[1].data(), inbox_[1].size())};
+      std::vector<char> sent(steps, 0);
+      auto chunk_of = [&](int i) {  // chunk received at step i
+        const int round = i < C - 2 ? i + 2 : i - (C - 2);
+        return ((2 * r) - (round & ~1) + (round & 1) + C) % C;
+      };
+      auto len_of = [&](int co) {
+        const size_t off = (size_t)co * chunk_;
+        return off >= (size_t)count_ ? (size_t)0 : std::min(chunk_, (size_t)count_ - off);
+      };
+      auto post_recv = [&](int i) {
+        const size_t l = len_of(chunk_of(i));
+        if (l) in[i & 1]->recv(left, kSlot, 0, l * sizeof(T));
+      };
+      auto post_send = [&](int i, int co) {
+        const size_t l = len_of(co);
+        if (l) out->send(right, kSlot, (size_t)co * chunk_ * sizeof(T), l * sizeof(T));
+        sent[i] = l != 0;
+      };
+      int waited = 0;  // sends completed in order (waitSend pops the oldest)
+      auto wait_sends_through = [&](int i) {
+        for (; waited <= i && waited < steps; waited++)
+          if (sent[waited]) out->waitSend(tmo);
+      };
+      post_recv(0);
+      post_recv(1);
+      post_send(0, 2 * r);
+      post_send(1, 2 * r + 1);
+      for (int i = 0; i < steps; i++) {
+        const int co = chunk_of(i);
+        const size_t l = len_of(co);
+        T* dst = ptrs_[0] + (size_t)co * chunk_;
+        const T* box = reinterpret_cast<const T*>(inbox_[i & 1].data());
+        if (l) {
+          in[i & 1]->waitRecv(tmo);
+          wait_sends_through(i);  // a still-queued send of this chunk must not see the update
+          if (i < C - 2) fn_->call(dst, box, l);
+          else std::memcpy(dst, box, l * sizeof(T));
+        }
+        if (i + 2 < steps) {
+          post_recv(i + 2);  // inbox[i&1] is free again
+          post_send(i + 2, co);
+        }
+      }
+      wait_sends_through(steps - 1);
+    }
+    for (size_t i = 1; i < ptrs_.size(); i++) std::memcpy(ptrs_[i], ptrs_[0], bytes);
+  }
+
+ private:
+  static constexpr uint64_t kSlot = uint64_t(0x11) << 56;
+  std::shared_ptr<Context> ctx_;
+  std::vector<T*> ptrs_;
+  int count_;
+  const ReductionFunction<T>* fn_;
+  size_t chunks_ = 0, chunk_ = 0;
+  std::vector<char> inbox_[2];
+};
+
 }  // namespace hydra

@@ -139,6 +139,10 @@ void hydra_ring_plan(int P, size_t n, size_t esize, size_t max_segment, size_t* 
  *   HYDRA_ALGO_RING_OLD  the old-style gloo::AllreduceRing<T> (allreduce_ring.h:20-125) on
  *                      device: P-1 whole-bucket rounds, each rank left-folds x_r op x_{r-1} op
  *                      ... (ranks differ, exactly as the reference; max_segment unused)
+ *   HYDRA_ALGO_RING_CHUNKED  gloo::AllreduceRingChunked<T> (allreduce_ring_chunked.h:20-248):
+ *                      2P chunks of max(256, ceil(n/2P)) elements, pipelined reduce pass +
+ *                      broadcast pass; identical bits on every rank (max_segment, chunk_bytes
+ *                      unused)
  *   HYDRA_ALGO_AUTO    DIRECT
  * max_segment: the reference's maxSegmentSize (0 = 1 MiB, allreduce.h:78) -- it fixes block
  * ownership; chunk_bytes: pipelining granularity (0 = 4 MiB), does not change results.
@@ -151,7 +155,8 @@ typedef enum {
   HYDRA_ALGO_DIRECT = 2,
   HYDRA_ALGO_RCCL = 3,
   HYDRA_ALGO_A2A = 4,
-  HYDRA_ALGO_RING_OLD = 5
+  HYDRA_ALGO_RING_OLD = 5,
+  HYDRA_ALGO_RING_CHUNKED = 6
 } hydra_algo_t;
 typedef struct hydra_comm* hydra_comm_t;
 

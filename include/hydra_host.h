@@ -52,6 +52,11 @@ int hydra_host_allreduce_ring_old_threads(int P, int nptr, int dtype, size_t n, 
                                           int reducer, hydra_inplace_fn fn, char* err,
                                           size_t errlen);
 
+/* gloo::AllreduceRingChunked<T>::run() (allreduce_ring_chunked.h:20-248), same arguments. */
+int hydra_host_allreduce_ring_chunked_threads(int P, int nptr, int dtype, size_t n, void** bufs,
+                                              int reducer, hydra_inplace_fn fn, char* err,
+                                              size_t errlen);
+
 /* AllreduceNewTest.TestTimeout (allreduce_test.cc:381-397): rank 0 of 2 times out; returns 0 and
  * the IoException text if it was raised. */
 int hydra_host_timeout_probe(long timeout_ms, char* what, size_t len);

@@ -151,6 +151,35 @@ def gen_old_ring(out: dict, meta: dict) -> None:
     meta["old_ring"] = rows
 
 
+def gen_chunked_ring(out: dict, meta: dict) -> None:
+    """AllreduceRingChunked<T> (allreduce_ring_chunked.h:20-248): 2P chunks of
+    max(256, ceil(n/2P)); sizes cover one chunk, partial and empty trailing chunks."""
+    rows = []
+    rng = np.random.default_rng(78)
+    for name, code in (("f32", 6), ("i32", 2), ("f16", 8)):
+        for P in (1, 2, 3, 5, 8):
+            for n in (1, 100, 1000, 4099):
+                for nptr in (1, 2):
+                    if name == "f32":
+                        bufs = [[synth.stress_f32(P, r, n, seed=600 + i) for i in range(nptr)]
+                                for r in range(P)]
+                    elif name == "i32":
+                        bufs = [[synth.int32_bucket(P, r, n, seed=600 + i) for i in range(nptr)]
+                                for r in range(P)]
+                    else:
+                        bufs = [[np.array([O.f2h(float(v)) for v in rng.uniform(-8, 8, n)],
+                                          np.uint16) for _ in range(nptr)] for _ in range(P)]
+                    key = f"chunkring_{name}_P{P}_n{n}_k{nptr}"
+                    out[key + "_in"] = np.stack([np.stack(b) for b in bufs])
+                    O.ref_allreduce_ring_chunked(bufs, dtype_code=code)
+                    res = np.stack([np.stack(b) for b in bufs])
+                    assert all(np.array_equal(res[0].view(np.uint8), res[r].view(np.uint8))
+                               for r in range(P)), key  # every rank holds the same bits
+                    out[key + "_out"] = res[0, 0]
+                    rows.append({"key": key, "P": P, "n": n, "nptr": nptr, "dtype": code})
+    meta["chunked_ring"] = rows
+
+
 def gen_new_test(meta: dict) -> None:
     """AllreduceNewTest.Default (test/allreduce_test.cc:302-362): confirm the reference meets the
     closed form k*stride^2 + stride(stride-1)/2 for uint64, every combination we test."""
@@ -189,6 +218,7 @@ def main() -> None:
     gen_ops(out, meta)
     gen_ring(out, meta)
     gen_old_ring(out, meta)
+    gen_chunked_ring(out, meta)
     gen_new_test(meta)
     import ctypes
     buf = ctypes.create_string_buffer(512)

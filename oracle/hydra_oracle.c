@@ -397,6 +397,47 @@ int orc_allreduce_ring_old(int P, int nptr, int op, int dtype, size_t n, void** 
   free(x);
   return 0;
 }
+/* ---- AllreduceRingChunked<T> (gloo/gloo/allreduce_ring_chunked.h:77-200) ----
+ * 2P chunks of max(256, ceil(n/2P)) elements (:32-36).  Rank s seeds chunks 2s and 2s+1
+ * (:88-89); each of the next P-1 ranks folds its own value in place, local op inbox (:138-139),
+ * so chunk c (s = c/2) ends as x_{s-1} op (x_{s-2} op (... op (x_{s+1} op x_s))), which the
+ * broadcast pass then copies to every rank (:146-186). */
+int orc_allreduce_ring_chunked(int P, int nptr, int op, int dtype, size_t n, void** bufs) {
+  size_t es = orc_esize(dtype);
+  if (!es || P < 1 || nptr < 1) return 1;
+  for (int r = 0; r < P; r++) {
+    void* p0 = bufs[r * nptr];
+    for (int i = 1; i < nptr; i++) orc_op(op, dtype, p0, p0, bufs[r * nptr + i], n);
+  }
+  if (P > 1) {
+    size_t chunks = 2 * (size_t)P;
+    size_t ce = (n + chunks - 1) / chunks;
+    if (ce < 256) ce = 256;
+    unsigned char* acc = (unsigned char*)malloc(ce * es + 1);
+    unsigned char* loc = (unsigned char*)malloc(ce * es + 1);
+    if (!acc || !loc) { free(acc); free(loc); return 2; }
+    for (size_t c = 0; c < chunks; c++) {
+      size_t off = c * ce;
+      if (off >= n) break;
+      size_t len = n - off < ce ? n - off : ce;
+      int s = (int)(c / 2);
+      memcpy(acc, (unsigned char*)bufs[s * nptr] + off * es, len * es);
+      for (int d = 1; d < P; d++) {
+        int q = (s + d) % P;
+        memcpy(loc, (unsigned char*)bufs[q * nptr] + off * es, len * es);
+        orc_op(op, dtype, loc, loc, acc, len); /* the ring hop: local = local op inbox */
+        memcpy(acc, loc, len * es);
+      }
+      for (int r = 0; r < P; r++) memcpy((unsigned char*)bufs[r * nptr] + off * es, acc, len * es);
+    }
+    free(acc);
+    free(loc);
+  }
+  for (int r = 0; r < P; r++)
+    for (int i = 1; i < nptr; i++) memcpy(bufs[r * nptr + i], bufs[r * nptr], n * es);
+  return 0;
+}
+
 /* ReductionFunction<T>::Function-shaped (x = x op y) entry points for host-runtime tests. */
 void orc_isum_f32(void* x, const void* y, size_t n) { orc_op(OP_SUM, D_FLOAT32, x, x, y, n); }
 void orc_isum_i32(void* x, const void* y, size_t n) { orc_op(OP_SUM, D_INT32, x, x, y, n); }

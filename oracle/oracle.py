@@ -66,6 +66,7 @@ def orc():
         _orc.orc_acc_bf16_f32.argtypes = [_vp, _vp, _c]
         _orc.orc_allreduce_ring_old.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                 ctypes.c_int, _c, _vp]
+        _orc.orc_allreduce_ring_chunked.argtypes = _orc.orc_allreduce_ring_old.argtypes
     return _orc
 
 
@@ -91,6 +92,7 @@ def ref():
         _ref.ref_float2half.restype = ctypes.c_uint16
         _ref.ref_allreduce_ring_old.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, _c,
                                                 _vp, ctypes.c_char_p, _c]
+        _ref.ref_allreduce_ring_chunked.argtypes = _ref.ref_allreduce_ring_old.argtypes
     return _ref
 
 
@@ -171,19 +173,21 @@ def ring_result(xs: list[np.ndarray], max_segment: int = 1 << 20, kind: str = "s
     return outs[0][0]
 
 
-def _old_ring(fn_is_ref, bufs, kind, dtype_code):
-    """bufs: [rank][ptr] arrays, in place."""
+def _old_ring(fn_is_ref, bufs, kind, dtype_code, chunked=False):
+    """bufs: [rank][ptr] arrays, in place.  chunked: AllreduceRingChunked<T> instead."""
     P, nptr = len(bufs), len(bufs[0])
     n = bufs[0][0].size
     code = _dt(bufs[0][0], dtype_code)
     ptrs = (_vp * (P * nptr))(*[_ptr(b) for r in bufs for b in r])
     if fn_is_ref:
         err = ctypes.create_string_buffer(512)
-        rc = ref().ref_allreduce_ring_old(P, nptr, code, n, ctypes.cast(ptrs, _vp), err, 512)
+        f = ref().ref_allreduce_ring_chunked if chunked else ref().ref_allreduce_ring_old
+        rc = f(P, nptr, code, n, ctypes.cast(ptrs, _vp), err, 512)
         if rc:
             raise RuntimeError(f"reference AllreduceRing failed: {err.value.decode()}")
     else:
-        if orc().orc_allreduce_ring_old(P, nptr, OPS[kind], code, n, ctypes.cast(ptrs, _vp)):
+        f = orc().orc_allreduce_ring_chunked if chunked else orc().orc_allreduce_ring_old
+        if f(P, nptr, OPS[kind], code, n, ctypes.cast(ptrs, _vp)):
             raise RuntimeError("oracle AllreduceRing failed")
     return bufs
 
@@ -196,6 +200,16 @@ def allreduce_ring_old(bufs, kind="sum", dtype_code=None):
 def ref_allreduce_ring_old(bufs, dtype_code=None):
     """The reference's own AllreduceRing<T> (ReductionFunction<T>::sum) on thread-ranks."""
     return _old_ring(True, bufs, "sum", dtype_code)
+
+
+def allreduce_ring_chunked(bufs, kind="sum", dtype_code=None):
+    """C restatement of gloo::AllreduceRingChunked<T>::run() over len(bufs) ranks."""
+    return _old_ring(False, bufs, kind, dtype_code, chunked=True)
+
+
+def ref_allreduce_ring_chunked(bufs, dtype_code=None):
+    """The reference's own AllreduceRingChunked<T> (ReductionFunction<T>::sum) on thread-ranks."""
+    return _old_ring(True, bufs, "sum", dtype_code, chunked=True)
 
 
 def split_aa(P: int, n: int):

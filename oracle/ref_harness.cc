@@ -271,6 +271,32 @@ int run_old_ring(int P, int nptr, size_t n, void** bufs, char* err, size_t errle
 }
 }  // namespace
 
+// ---- AllreduceRingChunked<T> (gloo/gloo/allreduce_ring_chunked.h:20-248) -----------------
+#include "gloo/allreduce_ring_chunked.h"
+
+namespace {
+template <typename T>
+int run_chunked_ring(int P, int nptr, size_t n, void** bufs, char* err, size_t errlen) {
+  return spawn(P, [&](int r, std::shared_ptr<gloo::Context> ctx) {
+    std::vector<T*> ptrs;
+    for (int i = 0; i < nptr; i++) ptrs.push_back(static_cast<T*>(bufs[r * nptr + i]));
+    gloo::AllreduceRingChunked<T> algo(ctx, ptrs, (int)n, gloo::ReductionFunction<T>::sum);
+    algo.run();
+  }, err, errlen);
+}
+}  // namespace
+
+extern "C" int ref_allreduce_ring_chunked(int P, int nptr, int dtype, size_t n, void** bufs,
+                                          char* err, size_t errlen) {
+  switch (dtype) {
+    case D_FLOAT32: return run_chunked_ring<float>(P, nptr, n, bufs, err, errlen);
+    case D_INT32: return run_chunked_ring<int32_t>(P, nptr, n, bufs, err, errlen);
+    case D_FLOAT16: return run_chunked_ring<gloo::float16>(P, nptr, n, bufs, err, errlen);
+    case D_FLOAT64: return run_chunked_ring<double>(P, nptr, n, bufs, err, errlen);
+  }
+  return 2;
+}
+
 // In place on bufs ([rank][ptr]), ReductionFunction<T>::sum; dtype: float32, int32, float16.
 extern "C" int ref_allreduce_ring_old(int P, int nptr, int dtype, size_t n, void** bufs,
                                       char* err, size_t errlen) {

@@ -75,6 +75,56 @@ static int run(int P, int nptr, size_t n, bool inplace, bool apipe) {
   return 0;
 }
 
+static void isum_u64(uint64_t* x, const uint64_t* y, size_t n) {
+  for (size_t i = 0; i < n; i++) x[i] += y[i];
+}
+
+// Old-style Algorithm API: AllreduceRing<T> / AllreduceRingChunked<T> (allreduce_ring.h,
+// allreduce_ring_chunked.h) with several pointers per rank.
+static int run_algorithm(int P, int nptr, int n, bool chunked) {
+  hydra::HashStore store;
+  std::vector<std::thread> th;
+  std::vector<int> bad(P, 0);
+  static const hydra::ReductionFunction<uint64_t> fn(hydra::SUM, &isum_u64);
+  for (int r = 0; r < P; r++) {
+    th.emplace_back([&, r] {
+      try {
+        auto c = std::make_shared<hydra::Context>(r, P);
+        c->connectFullMesh(store, "127.0.0.1", "alg");
+        const size_t stride = (size_t)P * nptr;
+        std::vector<std::vector<uint64_t>> buf(nptr, std::vector<uint64_t>(n));
+        std::vector<uint64_t*> ptrs;
+        for (int i = 0; i < nptr; i++) {
+          for (int k = 0; k < n; k++) buf[i][k] = k * stride + (size_t)r * nptr + i;
+          ptrs.push_back(buf[i].data());
+        }
+        for (int it = 0; it < 2; it++) {  // the algorithm object is reusable across runs
+          if (chunked) {
+            hydra::AllreduceRingChunked<uint64_t> a(c, ptrs, n, &fn);
+            a.run();
+          } else {
+            hydra::AllreduceRing<uint64_t> a(c, ptrs, n, &fn);
+            a.run();
+          }
+          const uint64_t mul = it == 0 ? 1 : stride;  // 2nd run sums the 1st run's outputs
+          for (int i = 0; i < nptr; i++)
+            for (int k = 0; k < n; k++) {
+              const uint64_t first = k * stride * stride + stride * (stride - 1) / 2;
+              if (buf[i][k] != first * mul) bad[r] = 1;
+            }
+        }
+      } catch (const std::exception& e) {
+        std::fprintf(stderr, "rank %d: %s\n", r, e.what());
+        bad[r] = 1;
+      }
+    });
+  }
+  for (auto& t : th) t.join();
+  for (int b : bad)
+    if (b) return 1;
+  return 0;
+}
+
 int main() {
   int fails = 0;
   for (int P : {1, 2, 3, 4})
@@ -93,6 +143,15 @@ int main() {
         std::fprintf(stderr, "FAIL apipe P=%d n=%zu\n", P, n);
         fails++;
       }
+  for (bool chunked : {false, true})
+    for (int P : {1, 2, 3, 5})
+      for (int nptr : {1, 2})
+        for (int n : {1, 1000, 20011})
+          if (run_algorithm(P, nptr, n, chunked)) {
+            std::fprintf(stderr, "FAIL %s P=%d nptr=%d n=%d\n",
+                         chunked ? "AllreduceRingChunked" : "AllreduceRing", P, nptr, n);
+            fails++;
+          }
   std::printf("%s\n", fails ? "FAILED" : "OK");
   return fails ? 1 : 0;
 }

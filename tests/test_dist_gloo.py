@@ -109,9 +109,9 @@ def _worker(rank, world, port, algo, n, ms, ch, q):
         wall = ring.timed_steps(lambda: None, 3, 1, lambda: None, dist.barrier)
         assert wall >= 0
         xs = [synth.stress_f32(world, r, n) for r in range(world)]
-        if algo == "ring_old":  # per-rank left fold (allreduce_ring.h:71-106)
+        if algo in ("ring_old", "ring_chunked"):  # allreduce_ring.h / allreduce_ring_chunked.h
             olds = [[x.copy()] for x in xs]
-            O.allreduce_ring_old(olds)
+            (O.allreduce_ring_old if algo == "ring_old" else O.allreduce_ring_chunked)(olds)
             exp = olds[rank][0]
         else:
             exp = O.ring_result(xs, ms or (1 << 20))
@@ -123,7 +123,7 @@ def _worker(rank, world, port, algo, n, ms, ch, q):
 
 
 @pytest.mark.parametrize("world", [2, 3])
-@pytest.mark.parametrize("algo", ["ring", "direct", "a2a", "ring_old"])
+@pytest.mark.parametrize("algo", ["ring", "direct", "a2a", "ring_old", "ring_chunked"])
 def test_gloo_multiprocess_plan(algo, world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

@@ -65,3 +65,19 @@ def test_old_style_allreduce_ring_gpu_reducer_vs_reference(gpu, golden, golden_m
         got = np.stack([np.stack(b) for b in bufs])
         exp = golden[key + "_out"]
         assert np.array_equal(got.view(np.uint32), exp.view(np.uint32)), key
+
+
+def test_chunked_allreduce_ring_gpu_reducer_vs_reference(gpu, golden, golden_meta):
+    """hydra::AllreduceRingChunked<T> with the GPU in-place sum == the reference's own
+    AllreduceRingChunked<T> outputs (f32/i32), every rank and pointer."""
+    for row in golden_meta["chunked_ring"]:
+        if row["dtype"] not in (6, 2):
+            continue
+        key, P, k = row["key"], row["P"], row["nptr"]
+        ins = golden[key + "_in"]
+        bufs = [[ins[r, i].copy() for i in range(k)] for r in range(P)]
+        host.allreduce_ring_old_threads(bufs, dtype_code=row["dtype"], chunked=True)
+        exp = golden[key + "_out"]
+        for r in range(P):
+            for i in range(k):
+                assert np.array_equal(bufs[r][i].view(np.uint32), exp.view(np.uint32)), key

@@ -237,3 +237,42 @@ def test_simulated_ring_old_large(gpu, O, P, n):
     O.allreduce_ring_old(olds)
     for r in range(P):
         assert np.array_equal(bufs[r].cpu().numpy().view(np.uint32), olds[r][0].view(np.uint32))
+
+
+def test_simulated_ring_chunked_vs_reference_fixtures(gpu, golden, golden_meta):
+    """Device RING_CHUNKED plan == the reference's own AllreduceRingChunked<T> on every rank
+    (tests/golden chunked_ring, f32/i32/f16, 1-2 pointers per rank)."""
+    import torch
+
+    from hydra_amd import reduce as R
+
+    views = {_lib.FLOAT32: np.uint32, _lib.INT32: np.int32, _lib.FLOAT16: np.int16}
+    for row in golden_meta["chunked_ring"]:
+        key, P, k, code = row["key"], row["P"], row["nptr"], row["dtype"]
+        ins = golden[key + "_in"]
+        v = views[code]
+        exp = golden[key + "_out"].view(v)
+        bufs = [[torch.from_numpy(ins[r, i].view(v).copy()).to(gpu) for i in range(k)]
+                for r in range(P)]
+        for r in range(P):
+            for i in range(1, k):
+                R.reduce_("sum", bufs[r][0], bufs[r][0], bufs[r][i], dtype_code=code)
+        ring.simulate([b[0] for b in bufs], algo="ring_chunked", dtype_code=code)
+        for r in range(P):
+            for i in range(1, k):
+                bufs[r][i].copy_(bufs[r][0])
+        torch.cuda.synchronize()
+        for r in range(P):
+            for i in range(k):
+                assert np.array_equal(bufs[r][i].cpu().numpy(), exp), (key, r, i)
+
+
+@pytest.mark.parametrize("P,n", [(2, 1 << 20), (8, 3000001)])
+def test_simulated_ring_chunked_large(gpu, O, P, n):
+    xs = [synth.stress_f32(P, r, n) for r in range(P)]
+    bufs = dev_bufs(gpu, xs)
+    ring.simulate(bufs, algo="ring_chunked")
+    exp = [[x.copy()] for x in xs]
+    O.allreduce_ring_chunked(exp)
+    for r in range(P):
+        assert np.array_equal(bufs[r].cpu().numpy().view(np.uint32), exp[r][0].view(np.uint32))

@@ -305,3 +305,46 @@ def test_ring_old_plan(O, P, n, ch):
     for r in range(P):
         assert np.array_equal(outs[r].view(np.uint32), bufs[r][0].view(np.uint32)), r
         race_check(ring.plan("ring_old", P, r, n, 4, 0, ch)[0])
+
+
+@pytest.mark.parametrize("P,n", [(2, 1), (2, 100), (3, 1000), (5, 4099), (8, 4099), (8, 100003),
+                                 (4, 262145), (7, 1 << 16)])
+def test_ring_chunked_plan(O, P, n):
+    """AllreduceRingChunked<T> on device (plan RING_CHUNKED): every rank bit-exact vs the oracle
+    restatement (pinned to the reference by tests/test_oracle.py), and race-free."""
+    xs = [synth.stress_f32(P, r, n) for r in range(P)]
+    outs = run_plan_numpy(O, "ring_chunked", xs, 0, 0)
+    bufs = [[x.copy()] for x in xs]
+    O.allreduce_ring_chunked(bufs)
+    for r in range(P):
+        assert np.array_equal(outs[r].view(np.uint32), bufs[r][0].view(np.uint32)), r
+        race_check(ring.plan("ring_chunked", P, r, n, 4, 0, 0)[0])
+
+
+def test_ring_chunked_plan_traffic():
+    """Each rank sends and receives 4P-4 chunks (2P-2 folds), as allreduce_ring_chunked.h does."""
+    P, n = 8, 1 << 20
+    for r in range(P):
+        ops, scr = ring.plan("ring_chunked", P, r, n, 4, 0, 0)
+        kinds = [o["kind"] for o in ops]
+        assert kinds.count(SEND) == kinds.count(RECV) == 4 * P - 4
+        assert kinds.count(REDUCE) == 2 * P - 2
+        assert scr == 2 * (n // (2 * P)) * 4
+
+
+def test_bench_self_check_helpers(O):
+    """bench.py's numpy self-checks agree with the oracle (they run on the GPU box, where the
+    oracle is not used by the product path)."""
+    P, n = 5, 4099
+    xs = [synth.stress_f32(P, r, n) for r in range(P)]
+    a = [[x.copy()] for x in xs]
+    O.allreduce_ring_chunked(a)
+    assert np.array_equal(ring.expected_chunked_ring_f32(xs).view(np.uint32),
+                          a[0][0].view(np.uint32))
+    b = [[x.copy()] for x in xs]
+    O.allreduce_ring_old(b)
+    for r in range(P):
+        assert np.array_equal(ring.expected_old_ring_f32(xs, r).view(np.uint32),
+                              b[r][0].view(np.uint32))
+    assert np.array_equal(ring.expected_fold_f32(xs).view(np.uint32),
+                          O.ring_result(xs).view(np.uint32))
