@@ -30,7 +30,8 @@ EXPORTS = [  # every symbol include/hydra_hip.h declares
     "hydra_stream_create", "hydra_stream_destroy", "hydra_stream_synchronize", "hydra_malloc",
     "hydra_free", "hydra_memcpy", "hydra_ring_plan",
     "hydra_comm_get_unique_id", "hydra_comm_init", "hydra_comm_destroy", "hydra_allreduce",
-    "hydra_plan", "hydra_allreduce_simulate", "hydra_fold",
+    "hydra_plan", "hydra_allreduce_simulate", "hydra_fold", "hydra_memcpy_async",
+    "hydra_malloc_host", "hydra_free_host", "hydra_pointer_device",
 ]
 
 ALGO_AUTO, ALGO_RING, ALGO_DIRECT, ALGO_RCCL, ALGO_A2A, ALGO_RING_OLD, ALGO_RING_CHUNKED = range(7)
@@ -95,6 +96,10 @@ def _declare(L) -> None:
     L.hydra_malloc.argtypes = [i, sz, ctypes.POINTER(vp)]
     L.hydra_free.argtypes = [vp]
     L.hydra_memcpy.argtypes = [vp, vp, sz]
+    L.hydra_memcpy_async.argtypes = [vp, vp, sz, vp]
+    L.hydra_malloc_host.argtypes = [sz, ctypes.POINTER(vp)]
+    L.hydra_free_host.argtypes = [vp]
+    L.hydra_pointer_device.argtypes = [vp, ctypes.POINTER(i)]
     L.hydra_ring_plan.argtypes = [i, sz, sz, sz] + [ctypes.POINTER(sz)] * 3
     L.hydra_ring_plan.restype = None
     L.hydra_comm_get_unique_id.argtypes = [vp]

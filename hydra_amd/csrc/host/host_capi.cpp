@@ -10,6 +10,7 @@
 
 #include "../../../include/hydra/allreduce.h"
 #include "../../../include/hydra/gloo_reduce.h"
+#include "../../../include/hydra/hip_allreduce_ring.h"
 #include "../../../include/hydra_host.h"
 
 namespace {
@@ -99,6 +100,32 @@ int old_ring(bool chunked, int P, int nptr, size_t n, void** bufs, int reducer, 
     } else {
       hydra::AllreduceRing<T> algo(c[0], ptrs, (int)n, rf);
       algo.run();
+    }
+  });
+}
+template <typename T>
+int hip_ring(int P, int nptr, size_t n, void** bufs, int workspace, int user_streams, char* err,
+             size_t errlen) {
+  return spawn(P, 1, err, errlen, [&](int r, std::vector<std::shared_ptr<hydra::Context>>& c) {
+    std::vector<T*> ptrs;
+    for (int i = 0; i < nptr; i++) ptrs.push_back(static_cast<T*>(bufs[r * nptr + i]));
+    std::vector<hydra_stream_t> streams;
+    if (user_streams) {
+      int dev = 0;  // an empty bucket may come with null pointers
+      if (n) hydra::gloo_compat::enforce(hydra_pointer_device(ptrs[0], &dev));
+      streams.resize(nptr);
+      for (auto& s : streams) hydra::gloo_compat::enforce(hydra_stream_create(dev, &s));
+    }
+    if (workspace == HYDRA_WORKSPACE_DEVICE) {
+      hydra::HipAllreduceRing<T, hydra::HipDeviceWorkspace<T>> algo(c[0], ptrs, (int)n, streams);
+      algo.run();
+    } else {
+      hydra::HipAllreduceRing<T, hydra::HipHostWorkspace<T>> algo(c[0], ptrs, (int)n, streams);
+      algo.run();
+    }
+    for (auto s : streams) {  // caller-provided streams: outputs are async until synchronized
+      hydra::gloo_compat::enforce(hydra_stream_synchronize(s));
+      hydra_stream_destroy(s);
     }
   });
 }
@@ -210,6 +237,22 @@ int hydra_host_allreduce_ring_chunked_threads(int P, int nptr, int dtype, size_t
                                               int reducer, hydra_inplace_fn fn, char* err,
                                               size_t errlen) {
   return algorithm_ring(true, P, nptr, dtype, n, bufs, reducer, fn, err, errlen);
+}
+
+int hydra_host_hip_ring_threads(int P, int nptr, int dtype, size_t n, void** dev_bufs,
+                                int workspace, int user_streams, char* err, size_t errlen) {
+  if (P < 1 || nptr < 1 || !dev_bufs || n > (size_t)INT32_MAX) {
+    set_err(err, errlen, "invalid arguments");
+    return 2;
+  }
+  switch (dtype) {
+    case HYDRA_FLOAT32: return hip_ring<float>(P, nptr, n, dev_bufs, workspace, user_streams, err, errlen);
+    case HYDRA_INT32: return hip_ring<int32_t>(P, nptr, n, dev_bufs, workspace, user_streams, err, errlen);
+    case HYDRA_FLOAT64: return hip_ring<double>(P, nptr, n, dev_bufs, workspace, user_streams, err, errlen);
+    case HYDRA_INT64: return hip_ring<int64_t>(P, nptr, n, dev_bufs, workspace, user_streams, err, errlen);
+  }
+  set_err(err, errlen, "unsupported dtype for HipAllreduceRing");
+  return 3;
 }
 
 void hydra_host_calculate_elements(int table, int P, size_t n, size_t* e1, size_t* e2) {

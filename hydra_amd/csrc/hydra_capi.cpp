@@ -314,6 +314,39 @@ int hydra_memcpy(void* dst, const void* src, size_t bytes) {
   return ok();
 }
 
+int hydra_memcpy_async(void* dst, const void* src, size_t bytes, hydra_stream_t stream) {
+  if (!bytes) return ok();
+  if (!dst || !src) return fail(HYDRA_ERR_INVALID, "null pointer");
+  HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, static_cast<hipStream_t>(stream)));
+  return ok();
+}
+
+int hydra_malloc_host(size_t bytes, void** out) {
+  if (!out) return fail(HYDRA_ERR_INVALID, "null out");
+  HIP_TRY(hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault));
+  return ok();
+}
+
+int hydra_free_host(void* p) {
+  if (p) HIP_TRY(hipHostFree(p));
+  return ok();
+}
+
+// CudaDevicePointer<T>::create's device lookup (cuda.cu:175-188): device of a device (or
+// managed) allocation; -1 for host memory, registered or not.
+int hydra_pointer_device(const void* p, int* device) {
+  if (!p || !device) return fail(HYDRA_ERR_INVALID, "null pointer");
+  hipPointerAttribute_t a{};
+  hipError_t e = hipPointerGetAttributes(&a, p);
+  if (e != hipSuccess) {  // plain pageable host memory is unknown to the runtime
+    (void)hipGetLastError();
+    *device = -1;
+    return ok();
+  }
+  *device = (a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged) ? a.device : -1;
+  return ok();
+}
+
 // allreduce.cc:199-221 -- identical integer arithmetic.
 void hydra_ring_plan(int P, size_t n, size_t esize, size_t max_segment, size_t* num_segments,
                      size_t* segment_bytes, size_t* segments_per_rank) {

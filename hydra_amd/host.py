@@ -36,6 +36,7 @@ def lib():
         L.hydra_host_timeout_probe.argtypes = [ctypes.c_long, ctypes.c_char_p, sz]
         L.hydra_host_allreduce_ring_old_threads.argtypes = [i, i, i, sz, vp, i, vp,
                                                             ctypes.c_char_p, sz]
+        L.hydra_host_hip_ring_threads.argtypes = [i, i, i, sz, vp, i, i, ctypes.c_char_p, sz]
         L.hydra_host_allreduce_ring_chunked_threads.argtypes = \
             L.hydra_host_allreduce_ring_old_threads.argtypes
         _h = L
@@ -44,6 +45,10 @@ def lib():
 
 def _ptrs(arrs):
     return (ctypes.c_void_p * len(arrs))(*[a.ctypes.data for a in arrs])
+
+
+def _ptrs_int(addrs):
+    return (ctypes.c_void_p * len(addrs))(*addrs)
 
 
 def _fn(reducer_fn):
@@ -101,6 +106,29 @@ def allreduce_ring_old_threads(bufs, dtype_code=None, reducer_fn=None, chunked=F
     if rc:
         raise _lib.HydraError(rc, err.value.decode())
     return bufs
+
+
+def hip_ring_threads(tensors, workspace: str = "host", user_streams: bool = False,
+                     dtype_code=None):
+    """hydra::HipAllreduceRing<T, W>::run() (gloo::CudaAllreduceRing) on len(tensors)
+    thread-ranks; tensors: [rank][ptr] contiguous device tensors, reduced in place."""
+    from .reduce import _torch_dtype_code
+
+    P, nptr = len(tensors), len(tensors[0])
+    n = tensors[0][0].numel()
+    code = dtype_code if dtype_code is not None else _torch_dtype_code(tensors[0][0])
+    for r in tensors:
+        for t in r:
+            if not (t.is_cuda and t.is_contiguous() and t.numel() == n):
+                raise _lib.HydraError(1, "contiguous, equally sized device tensors required")
+    ws = {"host": 0, "device": 1}[workspace]
+    err = ctypes.create_string_buffer(512)
+    rc = lib().hydra_host_hip_ring_threads(
+        P, nptr, code, n, ctypes.cast(_ptrs_int([t.data_ptr() for r in tensors for t in r]),
+                                      ctypes.c_void_p), ws, int(user_streams), err, 512)
+    if rc:
+        raise _lib.HydraError(rc, err.value.decode())
+    return tensors
 
 
 def bench(config: int, P: int, n: int, warmup: int, iters: int, reducer_fn=None) -> np.ndarray:

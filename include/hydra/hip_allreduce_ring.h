@@ -1,0 +1,207 @@
+// hydra::HipAllreduceRing<T, W> -- the HIP analog of gloo::CudaAllreduceRing<T, W>
+// (gloo/gloo/cuda_allreduce_ring.{h,cc}) for device-resident buffers on the host runtime's TCP
+// ring.  Same constructor (context, device ptrs, count, optional streams) and run(); same
+// result on rank r: x_r + x_{r-1} + ... + x_{r-P+1} (the AllreduceRing left fold,
+// cuda_allreduce_ring.cc:85-112), where x_r is the rank's locally reduced value.
+//
+//   HipHostWorkspace<T>   (CudaHostWorkspace, cuda_allreduce_ring.cc:122-142): the ring runs
+//       on pinned host boxes; the local pre-reduce is a left fold ptrs[0] op= ptrs[i] in
+//       pointer order (cuda_collectives_host.h:108-119), done on the device; each round's
+//       scratch += inbox is hydra_reduce_host (the gfx950 kernel behind a staged copy), where
+//       the reference runs its CPU sum<T>.
+//   HipDeviceWorkspace<T> (CudaDeviceWorkspace, :144-170): scratch is ptrs[0] itself; the local
+//       pre-reduce is the pairwise tree of CudaLocalNativeReduce (cuda_collectives_native.h:
+//       93-122) in pointer order (the reference shuffles the order at random, :53, so for
+//       floats with > 2 pointers it is itself nondeterministic; pointer order is one of its
+//       outcomes); each round's fold runs on the device on a copy of the received box.  TCP
+//       cannot read HBM, so the boxes the ring sends are pinned host memory: round 0 sends a
+//       D2H copy of scratch and round k forwards the box received in round k-1 (which holds
+//       exactly the bytes the reference's device outbox would).
+//
+// MI355X layout: one process per GPU, so every pointer must live on the same device (the
+// reference's multi-GPU-per-process peer-access tree is served here by the RCCL plans in
+// hydra_hip.h).  Only ReductionFunction SUM exists on this class, as in the reference
+// (fn_ = CudaReductionFunction<T>::sum, cuda_allreduce_ring.cc:26).
+#pragma once
+
+#include <cstring>
+#include <memory>
+#include <type_traits>
+#include <vector>
+
+#include "allreduce.h"
+#include "gloo_reduce.h"
+#include "../hydra_hip.h"
+
+namespace hydra {
+
+template <typename T>
+struct HipHostWorkspace {};
+template <typename T>
+struct HipDeviceWorkspace {};
+
+namespace detail {
+using gloo_compat::enforce;
+
+struct Pinned {  // CudaHostPointer<T>::alloc (cuda.cu:231-240)
+  void* p = nullptr;
+  Pinned() = default;
+  explicit Pinned(size_t bytes) { enforce(hydra_malloc_host(bytes, &p)); }
+  Pinned(const Pinned&) = delete;
+  Pinned& operator=(const Pinned&) = delete;
+  Pinned& operator=(Pinned&& o) noexcept {
+    std::swap(p, o.p);
+    return *this;
+  }
+  ~Pinned() {
+    if (p) hydra_free_host(p);
+  }
+};
+
+struct DeviceMem {
+  void* p = nullptr;
+  DeviceMem() = default;
+  DeviceMem(int device, size_t bytes) { enforce(hydra_malloc(device, bytes ? bytes : 1, &p)); }
+  DeviceMem(const DeviceMem&) = delete;
+  DeviceMem& operator=(const DeviceMem&) = delete;
+  DeviceMem& operator=(DeviceMem&& o) noexcept {
+    std::swap(p, o.p);
+    return *this;
+  }
+  ~DeviceMem() {
+    if (p) hydra_free(p);
+  }
+};
+}  // namespace detail
+
+template <typename T, typename W = HipHostWorkspace<T>>
+class HipAllreduceRing {
+  static constexpr bool kDeviceWorkspace = std::is_same<W, HipDeviceWorkspace<T>>::value;
+  static_assert(kDeviceWorkspace || std::is_same<W, HipHostWorkspace<T>>::value,
+                "W must be HipHostWorkspace<T> or HipDeviceWorkspace<T>");
+
+ public:
+  HipAllreduceRing(const std::shared_ptr<Context>& context, const std::vector<T*>& ptrs, int count,
+                   const std::vector<hydra_stream_t>& streams = std::vector<hydra_stream_t>())
+      : ctx_(context), ptrs_(ptrs), count_(count), bytes_((size_t)count * sizeof(T)),
+        synchronize_outputs_(streams.empty()) {
+    using detail::enforce;
+    if (ptrs_.empty()) throw EnforceNotMet("HipAllreduceRing: no pointers");
+    if (count_ < 0) throw EnforceNotMet("HipAllreduceRing: negative count");
+    if (!streams.empty() && streams.size() != ptrs_.size())
+      throw EnforceNotMet("HipAllreduceRing: streams.size() != ptrs.size()");  // :30-33
+    if (count_ == 0) return;  // nothing to move (pointers may be null)
+    enforce(hydra_pointer_device(ptrs_[0], &device_));
+    if (device_ < 0) throw EnforceNotMet("HipAllreduceRing: ptrs must be device memory");
+    for (T* p : ptrs_) {
+      int d = -1;
+      enforce(hydra_pointer_device(p, &d));
+      if (d != device_)
+        throw EnforceNotMet("HipAllreduceRing: all pointers must be on one device");
+    }
+    if (streams.empty()) {
+      owned_.resize(ptrs_.size());
+      for (auto& s : owned_) enforce(hydra_stream_create(device_, &s));
+      streams_ = owned_;
+    } else {
+      streams_ = streams;
+    }
+    boxes_[0] = detail::Pinned(bytes_ ? bytes_ : 1);
+    boxes_[1] = detail::Pinned(bytes_ ? bytes_ : 1);
+    if (kDeviceWorkspace) {
+      inbox_dev_ = detail::DeviceMem(device_, bytes_);
+    } else {
+      scratch_host_ = detail::Pinned(bytes_ ? bytes_ : 1);
+      if (ptrs_.size() > 1) local_dev_ = detail::DeviceMem(device_, bytes_);
+    }
+  }
+
+  ~HipAllreduceRing() {
+    for (auto s : owned_) hydra_stream_destroy(s);
+  }
+  HipAllreduceRing(const HipAllreduceRing&) = delete;
+  HipAllreduceRing& operator=(const HipAllreduceRing&) = delete;
+
+  void run() {
+    using detail::enforce;
+    if (count_ == 0) return;
+    const int dt = gloo_compat::dtype_of<T>();
+    hydra_stream_t s0 = streams_[0];
+    for (size_t i = 1; i < streams_.size(); i++) enforce(hydra_stream_synchronize(streams_[i]));
+    // ---- local reduce: scratch holds this rank's value x_r
+    void* scratch;
+    if (kDeviceWorkspace) {
+      for (size_t sz = 1; sz < ptrs_.size(); sz *= 2)  // CudaLocalNativeReduce tree
+        for (size_t j = 0; j + sz < ptrs_.size(); j += 2 * sz)
+          enforce(hydra_reduce(HYDRA_SUM, dt, ptrs_[j], ptrs_[j], ptrs_[j + sz], count_, s0));
+      scratch = ptrs_[0];
+    } else {
+      if (ptrs_.size() > 1) {  // ptrs[0] op= ptrs[i] in order, in place on a copy of ptrs[0]
+        enforce(hydra_memcpy_async(local_dev_.p, ptrs_[0], bytes_, s0));
+        for (size_t i = 1; i < ptrs_.size(); i++)
+          enforce(hydra_reduce(HYDRA_SUM, dt, local_dev_.p, local_dev_.p, ptrs_[i], count_, s0));
+        enforce(hydra_memcpy_async(scratch_host_.p, local_dev_.p, bytes_, s0));
+      } else {
+        enforce(hydra_memcpy_async(scratch_host_.p, ptrs_[0], bytes_, s0));
+      }
+      scratch = scratch_host_.p;
+    }
+    // ---- the ring (cuda_allreduce_ring.cc:79-112)
+    const int P = ctx_->size;
+    if (P > 1 && count_ > 0) {
+      const int right = (ctx_->rank + 1) % P, left = (ctx_->rank + P - 1) % P;
+      const auto tmo = ctx_->getTimeout();
+      enforce(hydra_memcpy_async(boxes_[0].p, scratch, bytes_, s0));  // outbox = scratch
+      enforce(hydra_stream_synchronize(s0));
+      int out = 0;
+      for (int round = 0; round < P - 1; round++) {
+        void* ob = boxes_[out].p;
+        void* ib = boxes_[out ^ 1].p;
+        auto send = ctx_->createUnboundBuffer(ob, bytes_);
+        auto recv = ctx_->createUnboundBuffer(ib, bytes_);
+        recv->recv(left, kSlot, 0, bytes_);
+        send->send(right, kSlot, 0, bytes_);
+        recv->waitRecv(tmo);
+        if (kDeviceWorkspace) {
+          enforce(hydra_memcpy_async(inbox_dev_.p, ib, bytes_, s0));
+          enforce(hydra_reduce(HYDRA_SUM, dt, scratch, scratch, inbox_dev_.p, count_, s0));
+          enforce(hydra_stream_synchronize(s0));  // ib is the next round's outbox
+        } else {
+          if (!lease_) lease_.reset(new gloo_compat::ContextPool::Lease(
+                           gloo_compat::ContextPool::instance(device_).acquire()));
+          enforce(hydra_reduce_host(lease_->get(), HYDRA_SUM, dt, scratch, scratch, ib, count_));
+        }
+        send->waitSend(tmo);
+        out ^= 1;  // forward what was just received (outbox <- inbox, :100-103)
+      }
+      lease_.reset();
+    }
+    // ---- broadcast the result to every device pointer (:114-120)
+    if (kDeviceWorkspace) {
+      enforce(hydra_stream_synchronize(s0));
+      for (size_t i = 1; i < ptrs_.size(); i++)
+        enforce(hydra_memcpy_async(ptrs_[i], scratch, bytes_, streams_[i]));
+    } else {
+      enforce(hydra_stream_synchronize(s0));
+      for (size_t i = 0; i < ptrs_.size(); i++)
+        enforce(hydra_memcpy_async(ptrs_[i], scratch, bytes_, streams_[i]));
+    }
+    if (synchronize_outputs_)
+      for (auto s : streams_) enforce(hydra_stream_synchronize(s));
+  }
+
+ private:
+  static constexpr uint64_t kSlot = uint64_t(0x12) << 56;
+  std::shared_ptr<Context> ctx_;
+  std::vector<T*> ptrs_;
+  int count_;
+  size_t bytes_;
+  bool synchronize_outputs_;
+  int device_ = -1;
+  std::vector<hydra_stream_t> streams_, owned_;
+  detail::Pinned boxes_[2], scratch_host_;
+  detail::DeviceMem inbox_dev_, local_dev_;
+  std::unique_ptr<gloo_compat::ContextPool::Lease> lease_;
+};
+
+}  // namespace hydra

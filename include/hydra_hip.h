@@ -120,6 +120,12 @@ int hydra_stream_synchronize(hydra_stream_t s);
 int hydra_malloc(int device, size_t bytes, void** out);
 int hydra_free(void* p);
 int hydra_memcpy(void* dst, const void* src, size_t bytes); /* hipMemcpyDefault, synchronous */
+int hydra_memcpy_async(void* dst, const void* src, size_t bytes, hydra_stream_t stream);
+/* Pinned host memory (CudaHostPointer<T>::alloc, cuda.cu:231-240). */
+int hydra_malloc_host(size_t bytes, void** out);
+int hydra_free_host(void* p);
+/* Device of a device allocation, -1 for host memory (CudaDevicePointer::create, cuda.cu:175-188). */
+int hydra_pointer_device(const void* p, int* device);
 
 /* ---- ring geometry (allreduce.cc:199-221), shared by the host ring and the xGMI ring ----- */
 void hydra_ring_plan(int P, size_t n, size_t esize, size_t max_segment, size_t* num_segments,

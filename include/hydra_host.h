@@ -52,6 +52,15 @@ int hydra_host_allreduce_ring_old_threads(int P, int nptr, int dtype, size_t n, 
                                           int reducer, hydra_inplace_fn fn, char* err,
                                           size_t errlen);
 
+/* hydra::HipAllreduceRing<T, W> (gloo::CudaAllreduceRing<T, W>, cuda_allreduce_ring.cc) on P
+ * thread-ranks over loopback TCP; dev_bufs ([rank][ptr]) are device pointers, in place.
+ * workspace: HYDRA_WORKSPACE_HOST / _DEVICE; user_streams: pass caller streams (outputs async).
+ * dtype: float32, int32, float64, int64. */
+#define HYDRA_WORKSPACE_HOST 0
+#define HYDRA_WORKSPACE_DEVICE 1
+int hydra_host_hip_ring_threads(int P, int nptr, int dtype, size_t n, void** dev_bufs,
+                                int workspace, int user_streams, char* err, size_t errlen);
+
 /* gloo::AllreduceRingChunked<T>::run() (allreduce_ring_chunked.h:20-248), same arguments. */
 int hydra_host_allreduce_ring_chunked_threads(int P, int nptr, int dtype, size_t n, void** bufs,
                                               int reducer, hydra_inplace_fn fn, char* err,

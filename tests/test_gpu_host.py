@@ -81,3 +81,63 @@ def test_chunked_allreduce_ring_gpu_reducer_vs_reference(gpu, golden, golden_met
         for r in range(P):
             for i in range(k):
                 assert np.array_equal(bufs[r][i].view(np.uint32), exp.view(np.uint32)), key
+
+
+def _tree(O, xs, code):
+    """CudaLocalNativeReduce's pairwise tree in pointer order (cuda_collectives_native.h:93-122)."""
+    xs = [x.copy() for x in xs]
+    sz = 1
+    while sz < len(xs):
+        for j in range(0, len(xs) - sz, 2 * sz):
+            xs[j] = O.op(xs[j], xs[j + sz], "sum", code)
+        sz *= 2
+    return xs[0]
+
+
+@pytest.mark.parametrize("workspace", ["host", "device"])
+@pytest.mark.parametrize("P,nptr,n,dt", [(1, 1, 1000, "f32"), (2, 1, 262145, "f32"),
+                                         (3, 2, 100003, "f32"), (4, 4, 4099, "f32"),
+                                         (5, 3, 7, "f32"), (3, 2, 70001, "i32"),
+                                         (2, 1, 0, "f32")])
+def test_hip_allreduce_ring(gpu, O, workspace, P, nptr, n, dt):
+    """hydra::HipAllreduceRing<T, W> (gloo::CudaAllreduceRing<T, W>): rank r ends with its own
+    left fold x_r + x_{r-1} + ... of the locally reduced values (the AllreduceRing result,
+    pinned to the reference by the old_ring fixtures); host workspace pre-reduces pointers as a
+    left fold, device workspace as the pairwise tree; every pointer gets the result."""
+    import torch
+
+    code = {"f32": 6, "i32": 2}[dt]
+    if dt == "f32":
+        xs = [[synth.stress_f32(P, r, n, seed=40 + i) for i in range(nptr)] for r in range(P)]
+    else:
+        xs = [[synth.int32_bucket(P, r, n, seed=40 + i) for i in range(nptr)] for r in range(P)]
+    local = []
+    for r in range(P):
+        if workspace == "device":
+            local.append(_tree(O, xs[r], code))
+        else:
+            acc = xs[r][0].copy()
+            for i in range(1, nptr):
+                acc = O.op(acc, xs[r][i], "sum", code)
+            local.append(acc)
+    exp = [[v.copy()] for v in local]
+    O.allreduce_ring_old(exp, dtype_code=code)
+    for user_streams in (False, True):
+        ts = [[torch.from_numpy(x.copy()).to(gpu) for x in xs[r]] for r in range(P)]
+        host.hip_ring_threads(ts, workspace=workspace, user_streams=user_streams)
+        for r in range(P):
+            for i in range(nptr):
+                got = ts[r][i].cpu().numpy()
+                assert np.array_equal(got.view(np.uint32), exp[r][0].view(np.uint32)), (r, i)
+
+
+def test_hip_allreduce_ring_rejects_host_pointers(gpu):
+    """CudaDevicePointer<T>::create needs device memory; so does the HIP ring's constructor."""
+    import ctypes
+
+    x = np.zeros(10, np.float32)
+    ptrs = (ctypes.c_void_p * 1)(x.ctypes.data)
+    err = ctypes.create_string_buffer(512)
+    rc = host.lib().hydra_host_hip_ring_threads(1, 1, 6, 10, ctypes.cast(ptrs, ctypes.c_void_p),
+                                                0, 0, err, 512)
+    assert rc != 0 and b"device memory" in err.value
