@@ -21,6 +21,7 @@
 #include "../../include/hydra_hip.h"
 #include "errors.h"
 #include "reduce_kernels.h"
+#include "split_table.h"
 #include "xgmi_plan.h"
 
 using hydra::fail;
@@ -143,13 +144,14 @@ void wait_on(hipStream_t st, const hydra::PlanOp& o, const std::vector<hipEvent_
   if (o.wait1 >= 0) (void)hipStreamWaitEvent(st, ev[o.wait1], 0);
 }
 
-int run_plan_rccl(hydra_comm* c, int op, int dtype, bool acc32, char* user, hipStream_t user_st) {
+// Enqueue the cached plan after `start` (recorded on the caller's stream); the caller joins
+// with join_streams().  Two communicators forked from one event run concurrently (apipe).
+int run_plan_rccl(hydra_comm* c, int op, int dtype, bool acc32, char* user, hipEvent_t start) {
   const auto& ops = c->plan;
   const size_t es = hydra::dtype_size(dtype);
   char* scratch = static_cast<char*>(c->scratch);
-  HIP_TRY(hipEventRecord(c->ev_start, user_st));
-  HIP_TRY(hipStreamWaitEvent(c->cs, c->ev_start, 0));
-  HIP_TRY(hipStreamWaitEvent(c->ks, c->ev_start, 0));
+  HIP_TRY(hipStreamWaitEvent(c->cs, start, 0));
+  HIP_TRY(hipStreamWaitEvent(c->ks, start, 0));
   size_t i = 0;
   while (i < ops.size()) {
     const hydra::PlanOp& o = ops[i];
@@ -192,6 +194,10 @@ int run_plan_rccl(hydra_comm* c, int op, int dtype, bool acc32, char* user, hipS
   }
   HIP_TRY(hipEventRecord(c->ev_cs, c->cs));
   HIP_TRY(hipEventRecord(c->ev_ks, c->ks));
+  return HYDRA_OK;
+}
+
+int join_streams(hydra_comm* c, hipStream_t user_st) {
   HIP_TRY(hipStreamWaitEvent(user_st, c->ev_cs, 0));
   HIP_TRY(hipStreamWaitEvent(user_st, c->ev_ks, 0));
   return HYDRA_OK;
@@ -255,32 +261,37 @@ int hydra_comm_destroy(hydra_comm_t c) {
   return ok();
 }
 
-int hydra_allreduce(hydra_comm_t c, int algo, int op, int dtype, int flags, void* buf, size_t n,
-                    size_t max_segment, size_t chunk_bytes, hydra_stream_t stream) {
+}  // extern "C"
+
+namespace {
+
+// Argument checks + plan cache + scratch for one allreduce on `c`.  *skip: nothing to do
+// (n == 0 or a single rank, allreduce.cc:129-133).
+int prepare(hydra_comm* c, int* algo, int op, int dtype, int flags, void* buf, size_t n,
+            size_t max_segment, size_t chunk_bytes, bool* skip) {
   if (!c) return fail(HYDRA_ERR_INVALID, "null comm");
   size_t es;
-  int rc = check_plan_args(algo, op, dtype, flags, &es);
+  int rc = check_plan_args(*algo, op, dtype, flags, &es);
   if (rc) return rc;
-  if (n == 0 || c->nranks == 1) return ok();  // allreduce.cc:129-133 (single process: no-op)
+  *skip = n == 0 || c->nranks == 1;
+  if (*skip) return HYDRA_OK;
   if (!buf) return fail(HYDRA_ERR_INVALID, "null buffer");
   if (reinterpret_cast<uintptr_t>(buf) % es)
     return fail(HYDRA_ERR_INVALID, "buffer not aligned to the element size");
-  hipStream_t st = static_cast<hipStream_t>(stream);
-  algo = resolve_algo(algo);
-  if (algo == HYDRA_ALGO_RCCL) {
+  *algo = resolve_algo(*algo);
+  if (*algo == HYDRA_ALGO_RCCL) {
     if (flags & HYDRA_ACC_F32) return fail(HYDRA_ERR_UNSUPPORTED, "ACC_F32 with RCCL");
-    NCCL_TRY(ncclAllReduce(buf, buf, n, nccl_type(dtype), nccl_op(op), c->nccl, st));
-    return ok();
+    return HYDRA_OK;
   }
   const size_t ms = max_segment ? max_segment : (1u << 20);
-  if (c->key_algo != algo || c->key_n != n || c->key_es != es || c->key_ms != ms ||
+  if (c->key_algo != *algo || c->key_n != n || c->key_es != es || c->key_ms != ms ||
       c->key_chunk != chunk_bytes) {
     const hydra::PlanGeom g = hydra::make_geom(c->nranks, n, es, ms, chunk_bytes);
-    rc = check_geometry(algo, g);
+    rc = check_geometry(*algo, g);
     if (rc) return rc;
-    c->plan = hydra::make_plan(algo, g, c->rank);
+    c->plan = hydra::make_plan(*algo, g, c->rank);
     c->waited = waited_set(c->plan);
-    const size_t need = hydra::plan_scratch_bytes(algo, g);
+    const size_t need = hydra::plan_scratch_bytes(*algo, g);
     if (need > c->scratch_bytes) {
       // (re)allocation happens outside any capture: first call with a new geometry
       HIP_TRY(hipDeviceSynchronize());
@@ -292,15 +303,88 @@ int hydra_allreduce(hydra_comm_t c, int algo, int op, int dtype, int flags, void
     }
     rc = ensure_events(c, c->plan.size());
     if (rc) return rc;
-    c->key_algo = algo;
+    c->key_algo = *algo;
     c->key_n = n;
     c->key_es = es;
     c->key_ms = ms;
     c->key_chunk = chunk_bytes;
   }
-  rc = run_plan_rccl(c, op, dtype, (flags & HYDRA_ACC_F32) != 0, static_cast<char*>(buf), st);
+  return HYDRA_OK;
+}
+
+// Enqueue a prepared allreduce after `start`; ends recorded in c->ev_cs / c->ev_ks.
+int enqueue(hydra_comm* c, int algo, int op, int dtype, int flags, void* buf, size_t n,
+            hipEvent_t start) {
+  if (algo == HYDRA_ALGO_RCCL) {
+    HIP_TRY(hipStreamWaitEvent(c->cs, start, 0));
+    NCCL_TRY(ncclAllReduce(buf, buf, n, nccl_type(dtype), nccl_op(op), c->nccl, c->cs));
+    HIP_TRY(hipEventRecord(c->ev_cs, c->cs));
+    HIP_TRY(hipEventRecord(c->ev_ks, c->ks));
+    return HYDRA_OK;
+  }
+  return run_plan_rccl(c, op, dtype, (flags & HYDRA_ACC_F32) != 0, static_cast<char*>(buf), start);
+}
+
+}  // namespace
+
+extern "C" {
+
+int hydra_allreduce(hydra_comm_t c, int algo, int op, int dtype, int flags, void* buf, size_t n,
+                    size_t max_segment, size_t chunk_bytes, hydra_stream_t stream) {
+  bool skip = false;
+  int rc = prepare(c, &algo, op, dtype, flags, buf, n, max_segment, chunk_bytes, &skip);
+  if (rc || skip) return rc ? rc : ok();
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  HIP_TRY(hipEventRecord(c->ev_start, st));
+  rc = enqueue(c, algo, op, dtype, flags, buf, n, c->ev_start);
   if (rc) return rc;
-  return ok();
+  rc = join_streams(c, st);
+  return rc ? rc : ok();
+}
+
+void hydra_split_elements(int table, int P, size_t n, size_t* e1, size_t* e2) {
+  size_t a = 0, b = 0;
+  hydra::split_elements(table, P, n, &a, &b);
+  if (e1) *e1 = a;
+  if (e2) *e2 = b;
+}
+
+int hydra_apipe_allreduce(hydra_comm_t rail1, hydra_comm_t rail2, int table, int algo, int op,
+                          int dtype, int flags, void* buf, size_t n, size_t max_segment,
+                          size_t chunk_bytes, hydra_stream_t stream) {
+  if (!rail1 || !rail2 || rail1 == rail2)
+    return fail(HYDRA_ERR_INVALID, "apipe needs two distinct communicators");
+  if (rail1->rank != rail2->rank || rail1->nranks != rail2->nranks ||
+      rail1->device != rail2->device)
+    return fail(HYDRA_ERR_INVALID, "rails disagree on rank/nranks/device");
+  if (table != HYDRA_SPLIT_AA && table != HYDRA_SPLIT_AG)
+    return fail(HYDRA_ERR_INVALID, "invalid split table");
+  const size_t es = hydra::dtype_size(dtype);
+  if (!es) return fail(HYDRA_ERR_INVALID, "invalid dtype");
+  size_t e1 = 0, e2 = 0;
+  hydra::split_elements(table, rail1->nranks, n, &e1, &e2);
+  char* p2 = static_cast<char*>(buf) + e1 * es;
+  // one part empty: a single allreduce, as apipe_allreduce does (pipeallreduce-a.cc:51-57)
+  if (e1 == 0 && e2 != 0)
+    return hydra_allreduce(rail2, algo, op, dtype, flags, p2, e2, max_segment, chunk_bytes, stream);
+  if (e2 == 0)
+    return hydra_allreduce(rail1, algo, op, dtype, flags, buf, e1, max_segment, chunk_bytes,
+                           stream);
+  int a1 = algo, a2 = algo;
+  bool s1 = false, s2 = false;
+  int rc = prepare(rail1, &a1, op, dtype, flags, buf, e1, max_segment, chunk_bytes, &s1);
+  if (!rc) rc = prepare(rail2, &a2, op, dtype, flags, p2, e2, max_segment, chunk_bytes, &s2);
+  if (rc) return rc;
+  if (s1 && s2) return ok();  // single rank
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  // both rails fork from one event on the caller's stream and run concurrently on their own
+  // streams (the two std::threads of pipeallreduce-a.cc:32-50); the caller's stream joins both
+  HIP_TRY(hipEventRecord(rail1->ev_start, st));
+  rc = enqueue(rail1, a1, op, dtype, flags, buf, e1, rail1->ev_start);
+  if (!rc) rc = enqueue(rail2, a2, op, dtype, flags, p2, e2, rail1->ev_start);
+  if (!rc) rc = join_streams(rail1, st);
+  if (!rc) rc = join_streams(rail2, st);
+  return rc ? rc : ok();
 }
 
 int hydra_plan(int algo, int P, int rank, size_t n, size_t esize, size_t max_segment,
@@ -538,6 +622,31 @@ int hydra_allreduce_simulate(int algo, int op, int dtype, int flags, int P, void
   SIM_TRY(hipDeviceSynchronize());
   cleanup();
 #undef SIM_TRY
+  return ok();
+}
+
+// apipe on one GPU: the split, then each non-empty part through the P-rank simulator.
+int hydra_apipe_allreduce_simulate(int table, int algo, int op, int dtype, int flags, int P,
+                                   void** bufs, size_t n, size_t max_segment, size_t chunk_bytes) {
+  if (table != HYDRA_SPLIT_AA && table != HYDRA_SPLIT_AG)
+    return fail(HYDRA_ERR_INVALID, "invalid split table");
+  const size_t es = hydra::dtype_size(dtype);
+  if (!es) return fail(HYDRA_ERR_INVALID, "invalid dtype");
+  if (P < 1 || P > hydra::kMaxRanks || !bufs) return fail(HYDRA_ERR_INVALID, "bad P/bufs");
+  size_t e1 = 0, e2 = 0;
+  hydra::split_elements(table, P, n, &e1, &e2);
+  if (e1) {
+    int rc = hydra_allreduce_simulate(algo, op, dtype, flags, P, bufs, e1, max_segment,
+                                      chunk_bytes);
+    if (rc) return rc;
+  }
+  if (e2) {
+    std::vector<void*> b2(P);
+    for (int r = 0; r < P; r++) b2[r] = static_cast<char*>(bufs[r]) + e1 * es;
+    int rc = hydra_allreduce_simulate(algo, op, dtype, flags, P, b2.data(), e2, max_segment,
+                                      chunk_bytes);
+    if (rc) return rc;
+  }
   return ok();
 }
 

@@ -46,6 +46,30 @@ def simulate(bufs, algo: str = "auto", op: str = "sum", dtype_code: int | None =
                                               max_segment, chunk_bytes))
 
 
+def split_elements(table: int, P: int, n: int) -> tuple[int, int]:
+    """calculateElements_AA (table 0) / _AG (1): (e1 for rail 1, e2 for rail 2)."""
+    e1, e2 = ctypes.c_size_t(), ctypes.c_size_t()
+    _lib.lib().hydra_split_elements(table, P, n, ctypes.byref(e1), ctypes.byref(e2))
+    return e1.value, e2.value
+
+
+def simulate_apipe(bufs, table: int = 0, algo: str = "auto", op: str = "sum",
+                   dtype_code: int | None = None, flags: int = 0, max_segment: int = 0,
+                   chunk_bytes: int = 0) -> None:
+    """hydra_apipe_allreduce on len(bufs) simulated ranks of one GPU (in place)."""
+    from .reduce import _torch_dtype_code
+
+    P = len(bufs)
+    code = dtype_code if dtype_code is not None else _torch_dtype_code(bufs[0])
+    n = _count(bufs[0], code)
+    for b in bufs:
+        if _count(b, code) != n or not b.is_contiguous():
+            raise HydraError(1, "simulate_apipe: buckets must be contiguous and equally sized")
+    ptrs = (ctypes.c_void_p * P)(*[b.data_ptr() for b in bufs])
+    check(_lib.lib().hydra_apipe_allreduce_simulate(table, ALGOS[algo], OPS[op], code, flags, P,
+                                                    ptrs, n, max_segment, chunk_bytes))
+
+
 def _count(t, code: int) -> int:
     """elements of dtype `code` in tensor t (t may hold the bits in another dtype)."""
     if code not in _lib.ESIZE:
@@ -103,6 +127,24 @@ class XgmiComm:
         check(_lib.lib().hydra_allreduce(self._h, ALGOS[algo], OPS[op], code, flags,
                                          t.data_ptr(), _count(t, code), max_segment,
                                          chunk_bytes, s))
+
+    def apipe_allreduce_(self, rail2: "XgmiComm", t, table: int = 0, algo: str = "auto",
+                         op: str = "sum", dtype_code: int | None = None, flags: int = 0,
+                         max_segment: int = 0, chunk_bytes: int = 0,
+                         stream: int | None = None) -> None:
+        """bew_allreduce_a on device: split t per calculateElements (table 0 = _AA, 1 = _AG),
+        [0, e1) on this communicator and [e1, n) on rail2, concurrently."""
+        import torch
+
+        from .reduce import _torch_dtype_code
+
+        code = dtype_code if dtype_code is not None else _torch_dtype_code(t)
+        if not t.is_contiguous():
+            raise HydraError(1, "apipe_allreduce_: contiguous tensor required")
+        s = stream if stream is not None else torch.cuda.current_stream(t.device).cuda_stream
+        check(_lib.lib().hydra_apipe_allreduce(self._h, rail2._h, table, ALGOS[algo], OPS[op],
+                                               code, flags, t.data_ptr(), _count(t, code),
+                                               max_segment, chunk_bytes, s))
 
     def close(self) -> None:
         if self._h:
@@ -215,6 +257,7 @@ def bench_allreduce(args, dev) -> dict:
     dog.start()
     uid = exchange_unique_id(rank, dev)
     comm = XgmiComm(rank, world, dev.index, uid)
+    rail2 = XgmiComm(rank, world, dev.index, exchange_unique_id(rank, dev))  # apipe's 2nd rail
     n = args.elements
     algo = getattr(args, "algo", "auto")
     try:
@@ -248,6 +291,18 @@ def bench_allreduce(args, dev) -> dict:
                                  expected_chunked_ring_f32(xs).view(np.uint32)))
         parity["ring_chunked"] = ("bit-exact" if max_over_ranks(0.0 if ok else 1.0, dev) == 0.0
                                   else "MISMATCH")
+        # two rails (bew_allreduce_a): each part is the reference ring on its slice
+        t = torch.from_numpy(xs[rank].copy()).to(dev)
+        comm.apipe_allreduce_(rail2, t, algo="direct")
+        torch.cuda.synchronize(dev)
+        e1, _ = split_elements(0, world, pn)
+        exp2 = np.concatenate([expected_fold_f32([x[:e1] for x in xs]) if e1 else
+                               np.empty(0, np.float32),
+                               expected_fold_f32([x[e1:] for x in xs]) if e1 < pn else
+                               np.empty(0, np.float32)])
+        ok = bool(np.array_equal(t.cpu().numpy().view(np.uint32), exp2.view(np.uint32)))
+        parity["apipe"] = ("bit-exact" if max_over_ranks(0.0 if ok else 1.0, dev) == 0.0
+                           else "MISMATCH")
         # 2) exactness at full size: integer-valued inputs whose sums are exact in fp32
         j = np.arange(n, dtype=np.int64)
         x = torch.from_numpy(((j % 1024) * (rank + 1)).astype(np.float32)).to(dev)
@@ -306,6 +361,15 @@ def bench_allreduce(args, dev) -> dict:
                 others[a] = round(ow / k * 1e3, 4)
             except _lib.HydraError as e:
                 others[a] = f"n/a: {e}"
+
+        def astep():
+            comm.apipe_allreduce_(rail2, x, algo="direct")
+
+        try:  # two rails split by calculateElements_AA, DIRECT on each
+            ow = max_over_ranks(timed_steps(astep, k, 3, sync, dist.barrier), dev)
+            others["apipe_direct"] = round(ow / k * 1e3, 4)
+        except _lib.HydraError as e:
+            others["apipe_direct"] = f"n/a: {e}"
         # 5) BASELINE config 5: bf16 bucket of 256 Mi elements, fp32 accumulation
         c5 = None
         if not getattr(args, "no_config5", False):
@@ -329,6 +393,7 @@ def bench_allreduce(args, dev) -> dict:
             del xb
     finally:
         comm.close()
+        rail2.close()
         dog.cancel()
     bucket = 4.0 * n
     algbw = bucket / (ms * 1e-3) / 1e9

@@ -183,6 +183,25 @@ int hydra_comm_destroy(hydra_comm_t comm);
 int hydra_allreduce(hydra_comm_t comm, int algo, int op, int dtype, int flags, void* buf,
                     size_t n, size_t max_segment, size_t chunk_bytes, hydra_stream_t stream);
 
+/* ---- bew_allreduce_a on device: two rails (pipeallreduce-a.cc:27-61) ---------------------- */
+#ifndef HYDRA_SPLIT_AA
+#define HYDRA_SPLIT_AA 0 /* calculateElements_AA, pipeallreduce-a.h:296-376 (default) */
+#define HYDRA_SPLIT_AG 1 /* calculateElements_AG, pipeallreduce-a.h:137-294 (ALLREDUCE_GLEX) */
+#endif
+/* e1 elements for rail 1 (opts3), e2 = n - e1 for rail 2 (opts2). */
+void hydra_split_elements(int table, int P, size_t n, size_t* e1, size_t* e2);
+/* [0, e1) allreduced on rail1 and [e1, n) on rail2, concurrently on the rails' own streams
+ * forked from and joined back into `stream` (the reference spawns two threads per call).  Each
+ * part equals gloo::allreduce RING on that slice with its own geometry (bit-exact for the
+ * plan algorithms).  One part empty: one allreduce on the other rail, as the reference does.
+ * The rails are two communicators over the same ranks (e.g. two hydra_comm_init calls). */
+int hydra_apipe_allreduce(hydra_comm_t rail1, hydra_comm_t rail2, int table, int algo, int op,
+                          int dtype, int flags, void* buf, size_t n, size_t max_segment,
+                          size_t chunk_bytes, hydra_stream_t stream);
+/* The same split on P simulated ranks of one GPU (see hydra_allreduce_simulate). */
+int hydra_apipe_allreduce_simulate(int table, int algo, int op, int dtype, int flags, int P,
+                                   void** bufs, size_t n, size_t max_segment, size_t chunk_bytes);
+
 /* The schedule rank `rank` of P executes (for inspection / host-side tests). */
 int hydra_plan(int algo, int P, int rank, size_t n, size_t esize, size_t max_segment,
                size_t chunk_bytes, hydra_plan_op_t* ops, size_t cap, size_t* count,

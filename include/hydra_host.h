@@ -21,8 +21,10 @@ extern "C" {
 typedef void (*hydra_reduce_fn)(void* c, const void* a, const void* b, size_t n);
 #define HYDRA_REDUCER_GPU 0
 #define HYDRA_REDUCER_FN 1
+#ifndef HYDRA_SPLIT_AA
 #define HYDRA_SPLIT_AA 0 /* calculateElements_AA, pipeallreduce-a.h:296-376 (default) */
 #define HYDRA_SPLIT_AG 1 /* calculateElements_AG, pipeallreduce-a.h:137-294 (ALLREDUCE_GLEX) */
+#endif
 
 /* gloo::allreduce (RING) on P thread-ranks.  in/out: P*nptr pointers [rank][ptr]; in == NULL is
  * in place (allreduce_test.cc:302-350).  timeout_ms <= 0: context default (30 s). */

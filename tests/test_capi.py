@@ -74,3 +74,15 @@ def test_missing_library_fails_loudly(monkeypatch, tmp_path):
     monkeypatch.setattr(_lib, "_lib", None)
     with pytest.raises(_lib.HydraError):
         _lib.lib()
+
+
+def test_split_elements_shared_with_host_runtime():
+    """The device library's split (hydra_split_elements) and the host runtime's
+    calculateElements are the same table (split_table.h), incl. the band edges."""
+    from hydra_amd import host, ring
+
+    for table in (0, 1):
+        for P in (2, 3, 4, 5, 6, 8):
+            for n in (0, 1, 6144, 6145, 65535, 65536, 65537, 131072, 524288, 524289, 828344,
+                      1048577, 1500000, 2097152, 4000001, 16777217, 67108864, 67108865):
+                assert ring.split_elements(table, P, n) == host.calculate_elements(table, P, n)

@@ -276,3 +276,51 @@ def test_simulated_ring_chunked_large(gpu, O, P, n):
     O.allreduce_ring_chunked(exp)
     for r in range(P):
         assert np.array_equal(bufs[r].cpu().numpy().view(np.uint32), exp[r][0].view(np.uint32))
+
+
+@pytest.mark.parametrize("table", [0, 1])
+@pytest.mark.parametrize("algo", ["direct", "ring", "ring_chunked"])
+@pytest.mark.parametrize("P,n", [(2, 1000), (2, 1500000), (3, 600000), (4, 1048577),
+                                 (6, 2000000), (8, 200000)])
+def test_simulated_apipe(gpu, O, table, algo, P, n):
+    """bew_allreduce_a on device: the split of calculateElements_AA/_AG, then each rail's part is
+    exactly the reference ring (or AllreduceRingChunked) on that slice, as apipe_allreduce
+    runs gloo::allreduce per rail (pipeallreduce-a.cc:27-61)."""
+    xs = [synth.stress_f32(P, r, n) for r in range(P)]
+    bufs = dev_bufs(gpu, xs)
+    ring.simulate_apipe(bufs, table=table, algo=algo)
+    e1, e2 = ring.split_elements(table, P, n)
+    assert e1 + e2 == n
+    exp = np.empty(n, np.float32)
+    for lo, hi in ((0, e1), (e1, n)):
+        if hi > lo:
+            part = [x[lo:hi].copy() for x in xs]
+            if algo == "ring_chunked":
+                b = [[p] for p in part]
+                O.allreduce_ring_chunked(b)
+                exp[lo:hi] = b[0][0]
+            else:
+                exp[lo:hi] = O.ring_result(part)
+    for r in range(P):
+        assert np.array_equal(bufs[r].cpu().numpy().view(np.uint32), exp.view(np.uint32)), r
+
+
+def test_apipe_single_rank_rails(gpu):
+    """Two 1-rank communicators as rails: argument checks and the P = 1 short circuit."""
+    import torch
+
+    r1 = ring.XgmiComm(0, 1, gpu.index or 0, ring._rccl_unique_id())
+    r2 = ring.XgmiComm(0, 1, gpu.index or 0, ring._rccl_unique_id())
+    try:
+        t = torch.arange(1 << 20, dtype=torch.float32, device=gpu)
+        r1.apipe_allreduce_(r2, t)
+        r1.apipe_allreduce_(r2, t, table=1, algo="rccl")
+        torch.cuda.synchronize()
+        assert torch.equal(t, torch.arange(1 << 20, dtype=torch.float32, device=gpu))
+        with pytest.raises(_lib.HydraError):
+            r1.apipe_allreduce_(r1, t)  # the two rails must be distinct communicators
+        with pytest.raises(_lib.HydraError):
+            r1.apipe_allreduce_(r2, t, table=7)
+    finally:
+        r1.close()
+        r2.close()
