@@ -83,9 +83,8 @@ void ring(const AllreduceOptions& o, const RangeFn& reduceInputs,
   const size_t S = numSegments / P;
   const size_t segBytes = round_up((total + numSegments - 1) / numSegments, o.elementSize);
 
-  // two segments in flight: scratch holds both
-  std::unique_ptr<char[]> tmpAlloc(new char[segBytes * 2]);
-  auto tmp = ctx.createUnboundBuffer(tmpAlloc.get(), segBytes * 2);
+  // two segments in flight: scratch holds both (the context's cached, optionally pinned, slots)
+  auto tmp = ctx.createUnboundBuffer(ctx.scratch(segBytes * 2), segBytes * 2);
   const size_t slotOff[2] = {0, segBytes};
 
   auto rs = [&](size_t i) {

@@ -146,7 +146,12 @@ int hydra_host_allreduce_threads(int P, int nptr, int op, int dtype, size_t n, v
     o.setAlgorithm(hydra::AllreduceOptions::RING);
     o.setOutputsRaw(out + r * nptr, nptr, n, es);
     if (in) o.setInputsRaw(in + r * nptr, nptr, n, es);
-    o.setReduceFunction(make_reducer(reducer, op, dtype, fn));
+    int red = reducer;
+    if (red == HYDRA_REDUCER_GPU_PINNED) {  // pinned receive slots (zero-copy GPU reduces)
+      c[0]->setScratchAllocator({&hydra::gloo_compat::pinnedAlloc, &hydra::gloo_compat::pinnedFree});
+      red = HYDRA_REDUCER_GPU;
+    }
+    o.setReduceFunction(make_reducer(red, op, dtype, fn));
     if (max_segment) o.setMaxSegmentSize(max_segment);
     if (timeout_ms > 0) o.setTimeout(std::chrono::milliseconds(timeout_ms));
     hydra::allreduce(o);
@@ -171,7 +176,7 @@ int hydra_host_apipe_threads(int P, int dtype, size_t n, void** in, void** out, 
   });
 }
 
-int hydra_host_bench(int config, int P, size_t n, int warmup, int iters, int reducer,
+int hydra_host_bench(int config, int P, size_t n, int warmup, int iters, int reducer_mode,
                      hydra_reduce_fn fn, double* samples_ns, char* err, size_t errlen) {
   if ((config != 1 && config != 3) || P < 1 || !samples_ns) {
     set_err(err, errlen, "invalid arguments");
@@ -179,7 +184,23 @@ int hydra_host_bench(int config, int P, size_t n, int warmup, int iters, int red
   }
   return spawn(P, config == 3 ? 2 : 1, err, errlen,
                [&](int r, std::vector<std::shared_ptr<hydra::Context>>& c) {
+    int reducer = reducer_mode;
     std::vector<float> in(n), out(n);
+    // GPU_PINNED: the receive slots are pinned and the output registered, so every segment
+    // reduce is the zero-copy kernel over PCIe
+    const bool pinned = reducer == HYDRA_REDUCER_GPU_PINNED;
+    if (pinned) {
+      for (auto& ctx : c)
+        ctx->setScratchAllocator({&hydra::gloo_compat::pinnedAlloc, &hydra::gloo_compat::pinnedFree});
+      if (n) hydra::gloo_compat::enforce(hydra_host_register(out.data(), n * sizeof(float)));
+      reducer = HYDRA_REDUCER_GPU;
+    }
+    struct Unreg {
+      void* p;
+      ~Unreg() {
+        if (p) hydra_host_unregister(p);
+      }
+    } unreg{pinned && n ? out.data() : nullptr};
     auto time_it = [&](const std::function<void()>& run) {
       for (int i = 0; i < warmup; i++) run();
       for (int i = 0; i < iters; i++) {

@@ -16,6 +16,7 @@
 
 #include <cerrno>
 #include <condition_variable>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <fstream>
@@ -258,7 +259,38 @@ Context::Context(int rank, int size) : rank(rank), size(size) {
   pairs_.resize(size);
 }
 
-Context::~Context() { closeConnections(); }
+Context::~Context() {
+  closeConnections();
+  releaseScratch();
+}
+
+void Context::releaseScratch() {
+  if (!scratch_) return;
+  if (scratch_alloc_.release && !scratch_heap_) scratch_alloc_.release(scratch_);
+  else std::free(scratch_);
+  scratch_ = nullptr;
+  scratch_bytes_ = 0;
+}
+
+void Context::setScratchAllocator(ScratchAllocator a) {
+  if ((a.alloc == nullptr) != (a.release == nullptr))
+    throw EnforceNotMet("scratch allocator needs both alloc and release");
+  releaseScratch();
+  scratch_alloc_ = a;
+}
+
+char* Context::scratch(size_t bytes) {
+  if (bytes > scratch_bytes_ || !scratch_) {
+    releaseScratch();
+    const size_t b = bytes ? bytes : 1;
+    scratch_ = scratch_alloc_.alloc ? scratch_alloc_.alloc(b) : nullptr;
+    scratch_heap_ = scratch_ == nullptr;  // no allocator, or it declined (e.g. no GPU)
+    if (!scratch_) scratch_ = std::malloc(b);
+    if (!scratch_) throw EnforceNotMet("scratch allocation of " + std::to_string(b) + " bytes failed");
+    scratch_bytes_ = b;
+  }
+  return static_cast<char*>(scratch_);
+}
 
 transport::Pair* Context::getPair(int peer) {
   if (peer < 0 || peer >= size || !pairs_[peer])

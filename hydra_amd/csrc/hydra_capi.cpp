@@ -83,6 +83,7 @@ struct hydra_ctx {
 
 namespace {
 constexpr size_t kChunkBytes = 8u << 20;
+constexpr int kVariantForceStaging = 1000;  // hydra_set_variant value: host path always stages
 
 void ctx_release(hydra_ctx* x) {
   for (int i = 0; i < 2; i++) {
@@ -217,6 +218,23 @@ int hydra_ctx_destroy(hydra_ctx_t ctx) {
   return ok();
 }
 
+namespace {
+// Device address of a pinned (hipHostMalloc) or registered (hipHostRegister) host byte, or null
+// for pageable memory.  The runtime reports the mapping of the allocation's base; interior
+// pointers keep their offset.
+void* mapped_device_ptr(const void* p) {
+  hipPointerAttribute_t at{};
+  if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  if (at.type != hipMemoryTypeHost || !at.devicePointer) return nullptr;
+  if (!at.hostPointer) return at.devicePointer;
+  return static_cast<char*>(at.devicePointer) +
+         (static_cast<const char*>(p) - static_cast<const char*>(at.hostPointer));
+}
+}  // namespace
+
 int hydra_reduce_host(hydra_ctx_t ctx, int op, int dtype, void* c, const void* a, const void* b,
                       size_t n) {
   if (!ctx) return fail(HYDRA_ERR_INVALID, "null context");
@@ -227,6 +245,20 @@ int hydra_reduce_host(hydra_ctx_t ctx, int op, int dtype, void* c, const void* a
   const size_t es = hydra::dtype_size(dtype);
   const size_t per = ctx->chunk_bytes / es;
   const int variant = g_variant.load(std::memory_order_relaxed);
+  // Zero-copy: when all three ranges are pinned/registered host memory (the ring's receive
+  // slots and output after hydra_host_register), the kernel streams them over PCIe directly --
+  // one pass, no staging copies.  kVariantForceStaging keeps the staged path for A/B.
+  if (variant != kVariantForceStaging) {
+    void* mc = mapped_device_ptr(c);
+    void* ma = mc ? (a == c ? mc : mapped_device_ptr(a)) : nullptr;
+    void* mb = ma ? (b == c ? mc : mapped_device_ptr(b)) : nullptr;
+    if (mb) {
+      hipError_t e = hydra::launch_reduce(0, op, dtype, mc, ma, mb, n, ctx->stream[0]);
+      if (e != hipSuccess) return hip_fail(e, "reduce kernel launch (zero-copy)");
+      HIP_TRY(hipStreamSynchronize(ctx->stream[0]));
+      return ok();
+    }
+  }
   size_t k = 0;
   for (size_t off = 0; off < n; off += per, k++) {
     const size_t cnt = std::min(per, n - off);

@@ -59,12 +59,17 @@ def _fn(reducer_fn):
 
 
 def allreduce_threads(outs, ins=None, dtype_code=None, op="sum", max_segment=0, reducer_fn=None,
-                      timeout_ms=0):
-    """gloo::allreduce(RING) on len(outs) thread-ranks; outs/ins: [rank][ptr] numpy arrays."""
+                      timeout_ms=0, pinned_scratch=False):
+    """gloo::allreduce(RING) on len(outs) thread-ranks; outs/ins: [rank][ptr] numpy arrays.
+    pinned_scratch (GPU reducer): the ring's receive slots come from pinned memory."""
     P, nptr = len(outs), len(outs[0])
     n = outs[0][0].size
     code = dtype_code if dtype_code is not None else _np_code(outs[0][0].dtype)
     red, fp = _fn(reducer_fn)
+    if pinned_scratch:
+        if reducer_fn is not None:
+            raise _lib.HydraError(1, "pinned_scratch applies to the GPU reducer")
+        red = 2
     err = ctypes.create_string_buffer(512)
     rc = lib().hydra_host_allreduce_threads(
         P, nptr, _lib.OPS[op], code, n,
@@ -131,9 +136,16 @@ def hip_ring_threads(tensors, workspace: str = "host", user_streams: bool = Fals
     return tensors
 
 
-def bench(config: int, P: int, n: int, warmup: int, iters: int, reducer_fn=None) -> np.ndarray:
+def bench(config: int, P: int, n: int, warmup: int, iters: int, reducer_fn=None,
+          pinned: bool = False) -> np.ndarray:
+    """Per-iteration ns of rank 0.  pinned (GPU reducer only): pinned receive slots and a
+    registered output, so each segment reduce is the zero-copy kernel."""
     s = np.zeros(iters, np.float64)
     red, fp = _fn(reducer_fn)
+    if pinned:
+        if reducer_fn is not None:
+            raise _lib.HydraError(1, "pinned applies to the GPU reducer")
+        red = 2
     err = ctypes.create_string_buffer(512)
     rc = lib().hydra_host_bench(config, P, n, warmup, iters, red, fp, s.ctypes.data, err, 512)
     if rc:

@@ -12,12 +12,15 @@ through ``hydra_reduce_host`` (synchronous, staged).  Every call lands in libhyd
 from __future__ import annotations
 
 import ctypes
+import sys
 import threading
 
 import numpy as np
 
 from . import _lib
 from ._lib import HydraError, OPS, check
+
+_is_finalizing = sys.is_finalizing
 
 _TORCH_DTYPES = None
 
@@ -112,10 +115,9 @@ class HostContext:
             self._h = ctypes.c_void_p()
 
     def __del__(self):
-        # never call into HIP/RCCL while the interpreter is finalizing (the runtime may be gone)
-        import sys
-
-        if sys.is_finalizing():
+        # never call into HIP/RCCL while the interpreter is finalizing (the runtime may be gone);
+        # `sys` is bound at import time: an import here fails during shutdown
+        if _is_finalizing():
             return
         try:
             self.close()

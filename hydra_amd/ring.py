@@ -8,12 +8,15 @@ module exchanges the RCCL unique id over torch.distributed and hands tensors ove
 from __future__ import annotations
 
 import ctypes
+import sys
 import time
 
 import numpy as np
 
 from . import _lib
 from ._lib import ALGOS, HydraError, OPS, check
+
+_is_finalizing = sys.is_finalizing
 
 
 def plan(algo: str, P: int, rank: int, n: int, esize: int, max_segment: int = 0,
@@ -152,10 +155,9 @@ class XgmiComm:
             self._h = ctypes.c_void_p()
 
     def __del__(self):
-        # never call into HIP/RCCL while the interpreter is finalizing (the runtime may be gone)
-        import sys
-
-        if sys.is_finalizing():
+        # never call into HIP/RCCL while the interpreter is finalizing (the runtime may be gone);
+        # `sys` is bound at import time: an import here fails during shutdown
+        if _is_finalizing():
             return
         try:
             self.close()

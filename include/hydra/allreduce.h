@@ -105,6 +105,17 @@ class Context {
   std::unique_ptr<UnboundBuffer> createUnboundBuffer(void* ptr, size_t size) {
     return std::unique_ptr<UnboundBuffer>(new UnboundBuffer(this, ptr, size));
   }
+  // Where the ring's receive slots live (the reference news them per call, allreduce.cc:
+  // 225-229).  Default: the heap.  With a pinned allocator (gloo_compat::pinnedAlloc/Free) the
+  // TCP receives land in page-locked memory that the GPU reducer reads in place over PCIe
+  // (hydra_reduce_host's zero-copy path) instead of staging it -- SURVEY §8f row 1.  The buffer
+  // is cached per context and reused by later collectives on it.
+  struct ScratchAllocator {
+    void* (*alloc)(size_t) = nullptr;
+    void (*release)(void*) = nullptr;
+  };
+  void setScratchAllocator(ScratchAllocator a);
+  char* scratch(size_t bytes);
   void setTimeout(std::chrono::milliseconds t) { timeout_ = t; }
   std::chrono::milliseconds getTimeout() const { return timeout_; }
   transport::Pair* getPair(int peer);
@@ -116,6 +127,11 @@ class Context {
  private:
   std::chrono::milliseconds timeout_{30000};  // gloo/gloo/context.cc:18
   std::vector<std::unique_ptr<transport::Pair>> pairs_;
+  ScratchAllocator scratch_alloc_;
+  void* scratch_ = nullptr;
+  size_t scratch_bytes_ = 0;
+  bool scratch_heap_ = true;
+  void releaseScratch();
 };
 
 class AllreduceOptions {

@@ -118,6 +118,14 @@ class ContextPool {
   std::vector<hydra_ctx_t> free_;
 };
 
+// Pinned host allocations (hipHostMalloc) for receive slots the GPU reducer reads in place;
+// pinnedAlloc returns null when no GPU is present (the caller then falls back to the heap).
+inline void* pinnedAlloc(size_t bytes) {
+  void* p = nullptr;
+  return hydra_malloc_host(bytes, &p) == HYDRA_OK ? p : nullptr;
+}
+inline void pinnedFree(void* p) { hydra_free_host(p); }
+
 using Func = std::function<void(void*, const void*, const void*, size_t)>;
 
 // --- AllreduceOptions::Func ------------------------------------------------------------------

@@ -8,6 +8,9 @@
  *
  * reducer: HYDRA_REDUCER_GPU  -> hydra_reduce_host (H2D -> gfx950 kernel -> D2H, synchronous)
  *          HYDRA_REDUCER_FN   -> the caller's function (CPU-side tests plug the oracle in here)
+ *          HYDRA_REDUCER_GPU_PINNED -> GPU with pinned receive slots (Context scratch allocator);
+ *                               with a registered output every segment reduce is zero-copy
+ *                               (hydra_host_bench registers its output itself)
  */
 #ifndef HYDRA_HOST_H_
 #define HYDRA_HOST_H_
@@ -21,6 +24,7 @@ extern "C" {
 typedef void (*hydra_reduce_fn)(void* c, const void* a, const void* b, size_t n);
 #define HYDRA_REDUCER_GPU 0
 #define HYDRA_REDUCER_FN 1
+#define HYDRA_REDUCER_GPU_PINNED 2
 #ifndef HYDRA_SPLIT_AA
 #define HYDRA_SPLIT_AA 0 /* calculateElements_AA, pipeallreduce-a.h:296-376 (default) */
 #define HYDRA_SPLIT_AG 1 /* calculateElements_AG, pipeallreduce-a.h:137-294 (ALLREDUCE_GLEX) */

@@ -40,8 +40,12 @@ ctx = HostContext(0)
 for n in (1 << 18, 1 << 22, 1 << 24):
     a = np.arange(n, dtype=np.float32)
     b = np.ones(n, dtype=np.float32)
-    for mode in ("pageable", "registered"):
-        if mode == "registered":
+    for mode in ("pageable", "registered", "registered_zero_copy"):
+        # "registered": staged copies on registered memory; "_zero_copy": the kernel reads and
+        # writes the registered host ranges over PCIe directly (hydra_reduce_host's default
+        # whenever all three ranges are pinned/registered)
+        prev = L.hydra_set_variant(1000 if mode == "registered" else 0)
+        if mode != "pageable":
             _lib.check(L.hydra_host_register(a.ctypes.data, a.nbytes))
             _lib.check(L.hydra_host_register(b.ctypes.data, b.nbytes))
         reps = max(3, int(2e8 / (12 * n)))
@@ -52,7 +56,8 @@ for n in (1 << 18, 1 << 22, 1 << 24):
             _lib.check(L.hydra_reduce_host(ctx.handle, 0, 6, a.ctypes.data, a.ctypes.data,
                                            b.ctypes.data, n))
         dt = (time.perf_counter() - t0) / reps
-        if mode == "registered":
+        L.hydra_set_variant(prev)
+        if mode != "pageable":
             L.hydra_host_unregister(a.ctypes.data)
             L.hydra_host_unregister(b.ctypes.data)
         iso.append({"elements": n, "mode": mode, "us": round(dt * 1e6, 1),
@@ -82,10 +87,14 @@ for n in sizes:
     if O.ref_available():
         c1.append({"impl": "reference (gloo, CPU sum)", **dist(O.ref_bench_ring(2, n, 3, iters), n)})
     c1.append({"impl": "hydra host runtime, GPU sum", **dist(host.bench(1, 2, n, 3, iters), n)})
+    c1.append({"impl": "hydra host runtime, GPU sum zero-copy (pinned slots, registered out)",
+               **dist(host.bench(1, 2, n, 3, iters, pinned=True), n)})
     if ref_fn:
         c3.append({"impl": "hydra split + reference gloo::sum (CPU)",
                    **dist(host.bench(3, 2, n, 3, iters, reducer_fn=ref_fn), n)})
     c3.append({"impl": "hydra split, GPU sum (H2D+sum+D2H)", **dist(host.bench(3, 2, n, 3, iters), n)})
+    c3.append({"impl": "hydra split, GPU sum zero-copy (pinned slots, registered out)",
+               **dist(host.bench(3, 2, n, 3, iters, pinned=True), n)})
 out["config1_new_allreduce_ring_P2"] = c1
 out["config3_bew_allreduce_a_P2"] = c3
 print(json.dumps(out))

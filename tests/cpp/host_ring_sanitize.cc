@@ -3,7 +3,9 @@
 // Mirrors AllreduceNewTest.Default (gloo/gloo/test/allreduce_test.cc:302-362) and the
 // bew_allreduce_a split on thread-ranks over loopback TCP, with a plain CPU sum as the reducer
 // (the product's GPU reducer is exercised by the GPU tests).  Exit 0 = all results correct.
+#include <atomic>
 #include <cstdint>
+#include <cstdlib>
 #include <cstdio>
 #include <string>
 #include <thread>
@@ -17,7 +19,19 @@ static void sum_u64(void* c, const void* a, const void* b, size_t n) {
                                    static_cast<const uint64_t*>(b)[i];
 }
 
-static int run(int P, int nptr, size_t n, bool inplace, bool apipe) {
+// Context::setScratchAllocator: counted allocations (the GPU users install pinned memory here)
+static std::atomic<int> g_allocs{0}, g_frees{0};
+static void* count_alloc(size_t b) {
+  g_allocs++;
+  return std::malloc(b);
+}
+static void count_free(void* p) {
+  g_frees++;
+  std::free(p);
+}
+static void* decline_alloc(size_t) { return nullptr; }  // e.g. pinned memory without a GPU
+
+static int run(int P, int nptr, size_t n, bool inplace, bool apipe, int alloc_mode = 0) {
   hydra::HashStore store;
   std::vector<std::thread> th;
   std::vector<int> bad(P, 0);
@@ -26,6 +40,8 @@ static int run(int P, int nptr, size_t n, bool inplace, bool apipe) {
       try {
         auto c1 = std::make_shared<hydra::Context>(r, P);
         c1->connectFullMesh(store, "127.0.0.1", "a");
+        if (alloc_mode == 1) c1->setScratchAllocator({&count_alloc, &count_free});
+        if (alloc_mode == 2) c1->setScratchAllocator({&decline_alloc, &count_free});
         std::shared_ptr<hydra::Context> c2;
         if (apipe) {
           c2 = std::make_shared<hydra::Context>(r, P);
@@ -143,6 +159,17 @@ int main() {
         std::fprintf(stderr, "FAIL apipe P=%d n=%zu\n", P, n);
         fails++;
       }
+  // scratch allocator: used once per context (cached across the ring's segments), released
+  // with the context; a declining allocator falls back to the heap (never handed to release)
+  if (run(3, 1, 10000, true, false, 1) || g_allocs.load() != 3 || g_frees.load() != 3) {
+    std::fprintf(stderr, "FAIL scratch allocator allocs=%d frees=%d\n", g_allocs.load(),
+                 g_frees.load());
+    fails++;
+  }
+  if (run(2, 1, 10000, true, false, 2) || g_frees.load() != 3) {
+    std::fprintf(stderr, "FAIL declining scratch allocator\n");
+    fails++;
+  }
   for (bool chunked : {false, true})
     for (int P : {1, 2, 3, 5})
       for (int nptr : {1, 2})

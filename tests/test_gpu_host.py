@@ -141,3 +141,33 @@ def test_hip_allreduce_ring_rejects_host_pointers(gpu):
     rc = host.lib().hydra_host_hip_ring_threads(1, 1, 6, 10, ctypes.cast(ptrs, ctypes.c_void_p),
                                                 0, 0, err, 512)
     assert rc != 0 and b"device memory" in err.value
+
+
+@pytest.mark.parametrize("config", [1, 3])
+def test_host_bench_pinned_zero_copy(gpu, config):
+    """Config 1 / 3 with pinned receive slots + registered output (zero-copy reduces) runs."""
+    s = host.bench(config, 2, 1 << 18, 1, 3, pinned=True)
+    assert s.shape == (3,) and np.all(s > 0)
+
+
+def test_host_ring_pinned_scratch_zero_copy(gpu, O):
+    """The ring over pinned receive slots and a registered output (zero-copy GPU reduces) is
+    bit-exact vs the reference ring: the default GPU reducer path picks zero-copy by itself."""
+    import ctypes
+
+    from hydra_amd import _lib
+
+    L = _lib.lib()
+    P, n = 3, 100003
+    xs = [synth.stress_f32(P, r, n) for r in range(P)]
+    outs = [[x.copy()] for x in xs]
+    for o in outs:
+        _lib.check(L.hydra_host_register(o[0].ctypes.data, o[0].nbytes))
+    try:
+        host.allreduce_threads(outs, None, max_segment=4096, pinned_scratch=True)
+    finally:
+        for o in outs:
+            L.hydra_host_unregister(o[0].ctypes.data)
+    exp = O.ring_result(xs, 4096)
+    for r in range(P):
+        assert np.array_equal(outs[r][0].view(np.uint32), exp.view(np.uint32)), r

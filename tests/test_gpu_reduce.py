@@ -233,6 +233,47 @@ def test_host_path(gpu, O, n):
         ctx.close()
 
 
+@pytest.mark.parametrize("n", [1, 1000, 262144, 3 * (1 << 20) + 7])
+def test_host_path_zero_copy(gpu, O, n):
+    """hydra_reduce_host on registered / pinned host memory takes the zero-copy path (the kernel
+    streams the host ranges over PCIe): same bits as the oracle, interior pointers included,
+    mixed pinned + pageable falls back to staging."""
+    L = _lib.lib()
+    pad = 3  # interior pointers: the ranges start 3 elements into the registered allocations
+    a = synth.stress_f32(2, 0, n + pad)
+    b = synth.stress_f32(2, 1, n + pad)
+    exp = O.op(a[pad:], b[pad:], "sum", 6)
+    ctx = HostContext(0)
+    _lib.check(L.hydra_host_register(a.ctypes.data, a.nbytes))
+    _lib.check(L.hydra_host_register(b.ctypes.data, b.nbytes))
+    try:
+        c = a[pad:]  # in place, the ring's form
+        _lib.check(L.hydra_reduce_host(ctx.handle, 0, 6, c.ctypes.data, c.ctypes.data,
+                                       b[pad:].ctypes.data, n))
+        assert np.array_equal(bits(c), bits(exp))
+        # pinned output, out of place
+        p = ctypes.c_void_p()
+        _lib.check(L.hydra_malloc_host(4 * n, ctypes.byref(p)))
+        try:
+            out = np.ctypeslib.as_array((ctypes.c_float * n).from_address(p.value))
+            out[:] = 7
+            a2 = synth.stress_f32(2, 0, n + pad)  # a restored (registered range re-filled)
+            a[:] = a2
+            _lib.check(L.hydra_reduce_host(ctx.handle, 0, 6, out.ctypes.data,
+                                           a[pad:].ctypes.data, b[pad:].ctypes.data, n))
+            assert np.array_equal(bits(out), bits(exp))
+            pg = np.full(n, 9, np.float32)  # pageable c: staged path
+            _lib.check(L.hydra_reduce_host(ctx.handle, 0, 6, pg.ctypes.data,
+                                           a[pad:].ctypes.data, b[pad:].ctypes.data, n))
+            assert np.array_equal(bits(pg), bits(exp))
+        finally:
+            L.hydra_free_host(p)
+    finally:
+        L.hydra_host_unregister(a.ctypes.data)
+        L.hydra_host_unregister(b.ctypes.data)
+        ctx.close()
+
+
 def test_host_path_f16_quirk(gpu, O):
     rng = np.random.default_rng(1)
     n = 20000
