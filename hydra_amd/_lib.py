@@ -35,10 +35,11 @@ EXPORTS = [  # every symbol include/hydra_hip.h declares
     "hydra_apipe_allreduce", "hydra_apipe_allreduce_simulate",
 ]
 
-ALGO_AUTO, ALGO_RING, ALGO_DIRECT, ALGO_RCCL, ALGO_A2A, ALGO_RING_OLD, ALGO_RING_CHUNKED = range(7)
+(ALGO_AUTO, ALGO_RING, ALGO_DIRECT, ALGO_RCCL, ALGO_A2A, ALGO_RING_OLD, ALGO_RING_CHUNKED,
+ ALGO_BCUBE) = range(8)
 ALGOS = {"auto": ALGO_AUTO, "ring": ALGO_RING, "direct": ALGO_DIRECT, "rccl": ALGO_RCCL,
          "a2a": ALGO_A2A, "ring_old": ALGO_RING_OLD,
-         "ring_chunked": ALGO_RING_CHUNKED}
+         "ring_chunked": ALGO_RING_CHUNKED, "bcube": ALGO_BCUBE}
 ACC_F32 = 1
 UNIQUE_ID_BYTES = 128
 

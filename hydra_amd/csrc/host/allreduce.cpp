@@ -10,6 +10,7 @@
 #include <thread>
 
 #include "../../../include/hydra/allreduce.h"
+#include "../bcube_geometry.h"
 #include "../split_table.h"
 
 namespace hydra {
@@ -146,6 +147,74 @@ void ring(const AllreduceOptions& o, const RangeFn& reduceInputs,
   }
 }
 
+// ---- BCUBE (allreduce.cc:423-700), geometry in bcube_geometry.h ------------------------------
+void bcube(const AllreduceOptions& o, const RangeFn& reduceInputs,
+           const RangeFn& broadcastOutputs) {
+  Context& ctx = *o.context;
+  const BufVec& out = o.out;
+  const uint64_t slot = make_slot(o.tag);
+  const size_t es = o.elementSize;
+  const std::vector<BcubeStep> steps = bcube_steps(ctx.size, ctx.rank, o.elements);
+  size_t scratchElems = o.elements;  // chunk lengths round up (:540-547)
+  for (const auto& s : steps) scratchElems = std::max(scratchElems, s.g * s.chunk);
+  auto tmp = ctx.createUnboundBuffer(ctx.scratch(scratchElems * es), scratchElems * es);
+  char* const obase = static_cast<char*>(out[0]->ptr);
+  const char* const tbase = static_cast<const char*>(tmp->ptr);
+
+  for (size_t k = 0; k < steps.size(); k++) {  // reduce-scatter
+    const BcubeStep& s = steps[k];
+    int nrecv = 0, nsend = 0;
+    for (size_t i = 0; i < s.g; i++) {
+      const int peer = (int)(s.base + i * s.dist);
+      if (peer == ctx.rank || s.mlen == 0) continue;
+      tmp->recv(peer, slot, i * s.chunk * es, s.mlen * es);
+      nrecv++;
+    }
+    for (size_t i = 0; i < s.g; i++) {
+      const int peer = (int)(s.base + i * s.dist);
+      if (peer == ctx.rank) continue;
+      const size_t coff = s.off + i * s.chunk, clen = s.chunk_len(i);
+      if (k == 0) reduceInputs(coff * es, clen * es);
+      if (clen == 0) continue;
+      out[0]->send(peer, slot, coff * es, clen * es);
+      nsend++;
+    }
+    for (int i = 0; i < nrecv; i++) tmp->waitRecv(o.timeout);
+    for (int i = 0; i < nsend; i++) out[0]->waitSend(o.timeout);
+    if (k == 0) reduceInputs(s.moff * es, s.mlen * es);
+    for (size_t i = 0; i < s.g && s.mlen; i++) {
+      if ((int)(s.base + i * s.dist) == ctx.rank) continue;
+      char* mine = obase + s.moff * es;
+      o.reduce(mine, mine, tbase + i * s.chunk * es, s.mlen);
+    }
+  }
+  broadcastOutputs(steps.back().moff * es, steps.back().mlen * es);
+
+  for (auto it = steps.rbegin(); it != steps.rend(); ++it) {  // all-gather
+    const BcubeStep& s = *it;
+    int nrecv = 0, nsend = 0;
+    for (size_t i = 0; i < s.g; i++) {
+      const int peer = (int)(s.base + i * s.dist);
+      const size_t clen = s.chunk_len(i);
+      if (peer == ctx.rank || clen == 0) continue;
+      out[0]->recv(peer, slot, (s.off + i * s.chunk) * es, clen * es);
+      nrecv++;
+    }
+    for (size_t i = 0; i < s.g; i++) {
+      const int peer = (int)(s.base + i * s.dist);
+      if (peer == ctx.rank || s.mlen == 0) continue;
+      out[0]->send(peer, slot, s.moff * es, s.mlen * es);
+      nsend++;
+    }
+    for (int i = 0; i < nrecv; i++) out[0]->waitRecv(o.timeout);
+    for (int i = 0; i < nsend; i++) out[0]->waitSend(o.timeout);
+    for (size_t i = 0; i < s.g; i++) {
+      if ((int)(s.base + i * s.dist) == ctx.rank) continue;
+      broadcastOutputs((s.off + i * s.chunk) * es, s.chunk_len(i) * es);
+    }
+  }
+}
+
 }  // namespace
 
 void allreduce(const AllreduceOptions& o) {
@@ -169,6 +238,9 @@ void allreduce(const AllreduceOptions& o) {
     case AllreduceOptions::UNSPECIFIED:
     case AllreduceOptions::RING:
       ring(o, reduceInputs, broadcastOutputs);
+      break;
+    case AllreduceOptions::BCUBE:
+      bcube(o, reduceInputs, broadcastOutputs);
       break;
     default:
       throw EnforceNotMet("Algorithm not handled.");

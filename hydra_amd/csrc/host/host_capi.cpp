@@ -134,8 +134,8 @@ int hip_ring(int P, int nptr, size_t n, void** bufs, int workspace, int user_str
 extern "C" {
 
 int hydra_host_allreduce_threads(int P, int nptr, int op, int dtype, size_t n, void** in,
-                                 void** out, size_t max_segment, int reducer, hydra_reduce_fn fn,
-                                 long timeout_ms, char* err, size_t errlen) {
+                                 void** out, size_t max_segment, int algorithm, int reducer,
+                                 hydra_reduce_fn fn, long timeout_ms, char* err, size_t errlen) {
   const size_t es = esize_of(dtype);
   if (!es || P < 1 || nptr < 1 || !out) {
     set_err(err, errlen, "invalid arguments");
@@ -143,7 +143,7 @@ int hydra_host_allreduce_threads(int P, int nptr, int op, int dtype, size_t n, v
   }
   return spawn(P, 1, err, errlen, [&](int r, std::vector<std::shared_ptr<hydra::Context>>& c) {
     hydra::AllreduceOptions o(c[0]);
-    o.setAlgorithm(hydra::AllreduceOptions::RING);
+    o.setAlgorithm(static_cast<hydra::AllreduceOptions::Algorithm>(algorithm));
     o.setOutputsRaw(out + r * nptr, nptr, n, es);
     if (in) o.setInputsRaw(in + r * nptr, nptr, n, es);
     int red = reducer;

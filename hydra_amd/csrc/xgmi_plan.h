@@ -29,6 +29,8 @@
 #include <algorithm>
 #include <vector>
 
+#include "bcube_geometry.h"
+
 namespace hydra {
 
 enum PlanKind : int32_t {
@@ -43,7 +45,7 @@ enum PlanKind : int32_t {
 enum PlanBuf : int32_t { kBufUser = 0, kBufScratch = 1 };
 enum Algo : int32_t {
   kAlgoAuto = 0, kAlgoRing = 1, kAlgoDirect = 2, kAlgoRccl = 3, kAlgoA2A = 4, kAlgoRingOld = 5,
-  kAlgoRingChunked = 6
+  kAlgoRingChunked = 6, kAlgoBcube = 7
 };
 
 // AllreduceRingChunked<T> geometry (allreduce_ring_chunked.h:32-36): 2P chunks of
@@ -149,6 +151,11 @@ inline size_t plan_scratch_bytes(int algo, const PlanGeom& g) {
   if (algo == kAlgoA2A) return g.total;
   if (algo == kAlgoRingOld) return 2 * round_up_sz(g.total, 16);
   if (algo == kAlgoRingChunked) return 2 * round_up_sz(chunked_ring_elems(g.P, g.n) * g.esize, 16);
+  if (algo == kAlgoBcube) {  // allreduce.cc:540-547: chunk lengths round up
+    size_t e = g.n;
+    for (const auto& s : bcube_steps(g.P, 0, g.n)) e = std::max(e, s.g * s.chunk);
+    return round_up_sz(e * g.esize, 16);
+  }
   return 0;
 }
 
@@ -372,7 +379,54 @@ inline std::vector<PlanOp> plan_ring_chunked(const PlanGeom& g, int r) {
   return pb.ops;
 }
 
+// ---- BCUBE: gloo's hypercube allreduce (allreduce.cc:423-700) on device ----------------------
+// Per step one p2p group with every group peer (its chunk out of the user bucket, their
+// partials of this rank's chunk into scratch slot i), then REDUCEs folding the partials into
+// the chunk in group order, own value first -- the reference's order, so results are its bits.
+// The all-gather walks the steps backwards, receiving straight into the user bucket.
+inline std::vector<PlanOp> plan_bcube(const PlanGeom& g, int r) {
+  PlanBuilder pb;
+  if (g.P <= 1 || g.n == 0) return pb.ops;
+  const int64_t es = (int64_t)g.esize;
+  const std::vector<BcubeStep> steps = bcube_steps(g.P, r, g.n);
+  int last = -1;  // last REDUCE: wrote this rank's chunk, read scratch
+  for (const BcubeStep& s : steps) {
+    const size_t first = pb.ops.size();
+    for (size_t i = 0; i < s.g; i++) {
+      const int peer = (int)(s.base + i * s.dist);
+      if (peer == r) continue;
+      const size_t cl = s.chunk_len(i);
+      if (cl) pb.add(kOpSend, peer, kBufUser, (int64_t)(s.off + i * s.chunk) * es, (int64_t)cl * es);
+      if (s.mlen) pb.add(kOpRecv, peer, kBufScratch, (int64_t)(i * s.chunk) * es, (int64_t)s.mlen * es);
+    }
+    if (pb.ops.size() == first) continue;
+    const int grp = pb.add(kOpGroup, -1, 0, 0, 0, 0, 0, 0, last);
+    for (size_t i = 0; i < s.g && s.mlen; i++) {
+      if ((int)(s.base + i * s.dist) == r) continue;
+      last = pb.add(kOpReduce, -1, kBufUser, (int64_t)s.moff * es, (int64_t)s.mlen * es,
+                    (int64_t)(i * s.chunk) * es, 0, 2, grp);
+    }
+  }
+  bool first_ag = true;
+  for (auto it = steps.rbegin(); it != steps.rend(); ++it) {
+    const BcubeStep& s = *it;
+    const size_t first = pb.ops.size();
+    for (size_t i = 0; i < s.g; i++) {
+      const int peer = (int)(s.base + i * s.dist);
+      if (peer == r) continue;
+      if (s.mlen) pb.add(kOpSend, peer, kBufUser, (int64_t)s.moff * es, (int64_t)s.mlen * es);
+      const size_t cl = s.chunk_len(i);
+      if (cl) pb.add(kOpRecv, peer, kBufUser, (int64_t)(s.off + i * s.chunk) * es, (int64_t)cl * es);
+    }
+    if (pb.ops.size() == first) continue;
+    pb.add(kOpGroup, -1, 0, 0, 0, 0, 0, 0, first_ag ? last : -1);
+    first_ag = false;
+  }
+  return pb.ops;
+}
+
 inline std::vector<PlanOp> make_plan(int algo, const PlanGeom& g, int r) {
+  if (algo == kAlgoBcube) return plan_bcube(g, r);
   if (algo == kAlgoRingChunked) return plan_ring_chunked(g, r);
   if (algo == kAlgoRingOld) return plan_ring_old(g, r);
   if (algo == kAlgoRing) return plan_ring(g, r);

@@ -26,7 +26,7 @@ def lib():
             raise _lib.HydraError(-1, f"{LIB_PATH} is not built")
         L = ctypes.CDLL(LIB_PATH)
         vp, sz, i = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
-        L.hydra_host_allreduce_threads.argtypes = [i, i, i, i, sz, vp, vp, sz, i, vp,
+        L.hydra_host_allreduce_threads.argtypes = [i, i, i, i, sz, vp, vp, sz, i, i, vp,
                                                    ctypes.c_long, ctypes.c_char_p, sz]
         L.hydra_host_apipe_threads.argtypes = [i, i, sz, vp, vp, i, i, vp, ctypes.c_char_p, sz]
         L.hydra_host_bench.argtypes = [i, i, sz, i, i, i, vp, vp, ctypes.c_char_p, sz]
@@ -59,7 +59,7 @@ def _fn(reducer_fn):
 
 
 def allreduce_threads(outs, ins=None, dtype_code=None, op="sum", max_segment=0, reducer_fn=None,
-                      timeout_ms=0, pinned_scratch=False):
+                      timeout_ms=0, pinned_scratch=False, algorithm="ring"):
     """gloo::allreduce(RING) on len(outs) thread-ranks; outs/ins: [rank][ptr] numpy arrays.
     pinned_scratch (GPU reducer): the ring's receive slots come from pinned memory."""
     P, nptr = len(outs), len(outs[0])
@@ -74,8 +74,8 @@ def allreduce_threads(outs, ins=None, dtype_code=None, op="sum", max_segment=0, 
     rc = lib().hydra_host_allreduce_threads(
         P, nptr, _lib.OPS[op], code, n,
         ctypes.cast(_ptrs([a for r in ins for a in r]), ctypes.c_void_p) if ins else None,
-        ctypes.cast(_ptrs([a for r in outs for a in r]), ctypes.c_void_p), max_segment, red, fp,
-        timeout_ms, err, 512)
+        ctypes.cast(_ptrs([a for r in outs for a in r]), ctypes.c_void_p), max_segment,
+        {"ring": 1, "bcube": 2}[algorithm], red, fp, timeout_ms, err, 512)
     if rc:
         raise _lib.HydraError(rc, err.value.decode())
     return outs

@@ -236,6 +236,42 @@ def expected_chunked_ring_f32(xs: list[np.ndarray]) -> np.ndarray:
     return out
 
 
+def expected_bcube_f32(xs: list[np.ndarray]) -> np.ndarray:
+    """Self-check for the bench: gloo's BCUBE result (allreduce.cc:423-700) -- per step, each
+    rank folds its group's partials into its chunk, own value first, peers in group order."""
+    P, n = len(xs), xs[0].size
+    part = [x.astype(np.float32).copy() for x in xs]
+    sizes, left = [], P
+    while left % 2 == 0:
+        sizes.append(2)
+        left //= 2
+    if left > 1:
+        sizes.append(left)
+    rng = [(0, n)] * P
+    dist = 1
+    for g in sizes:
+        snap = [p.copy() for p in part]
+        new = []
+        for r in range(P):
+            grank = (r // dist) % g
+            base = r - grank * dist
+            off, ln = rng[r]
+            ch = -(-ln // g)
+            mo, ml = off + grank * ch, max(0, min(ch, ln - grank * ch))
+            for i in range(g):
+                peer = base + i * dist
+                if peer != r and ml:
+                    part[r][mo:mo + ml] = part[r][mo:mo + ml] + snap[peer][mo:mo + ml]
+            new.append((mo, ml))
+        rng = new
+        dist *= g
+    out = np.empty(n, np.float32)
+    for r in range(P):
+        mo, ml = rng[r]
+        out[mo:mo + ml] = part[r][mo:mo + ml]
+    return out
+
+
 def bench_allreduce(args, dev) -> dict:
     """bench.py --gpus N (N > 1): BASELINE config 4 (fp32 64 Mi per rank) on this rank."""
     import torch
@@ -293,6 +329,13 @@ def bench_allreduce(args, dev) -> dict:
                                  expected_chunked_ring_f32(xs).view(np.uint32)))
         parity["ring_chunked"] = ("bit-exact" if max_over_ranks(0.0 if ok else 1.0, dev) == 0.0
                                   else "MISMATCH")
+        t = torch.from_numpy(xs[rank].copy()).to(dev)
+        comm.allreduce_(t, algo="bcube")
+        torch.cuda.synchronize(dev)
+        ok = bool(np.array_equal(t.cpu().numpy().view(np.uint32),
+                                 expected_bcube_f32(xs).view(np.uint32)))
+        parity["bcube"] = ("bit-exact" if max_over_ranks(0.0 if ok else 1.0, dev) == 0.0
+                           else "MISMATCH")
         # two rails (bew_allreduce_a): each part is the reference ring on its slice
         t = torch.from_numpy(xs[rank].copy()).to(dev)
         comm.apipe_allreduce_(rail2, t, algo="direct")
@@ -351,7 +394,7 @@ def bench_allreduce(args, dev) -> dict:
         # 4) context: the other algorithms on the same bucket (fewer steps)
         others = {}
         k = max(5, args.steps // 4)
-        for a in ("ring", "direct", "a2a", "rccl", "ring_old", "ring_chunked"):
+        for a in ("ring", "direct", "a2a", "rccl", "ring_old", "ring_chunked", "bcube"):
             if a == chosen:
                 continue
 

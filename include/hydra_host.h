@@ -30,11 +30,12 @@ typedef void (*hydra_reduce_fn)(void* c, const void* a, const void* b, size_t n)
 #define HYDRA_SPLIT_AG 1 /* calculateElements_AG, pipeallreduce-a.h:137-294 (ALLREDUCE_GLEX) */
 #endif
 
-/* gloo::allreduce (RING) on P thread-ranks.  in/out: P*nptr pointers [rank][ptr]; in == NULL is
- * in place (allreduce_test.cc:302-350).  timeout_ms <= 0: context default (30 s). */
+/* gloo::allreduce on P thread-ranks.  in/out: P*nptr pointers [rank][ptr]; in == NULL is in
+ * place (allreduce_test.cc:302-350).  algorithm: 0/1 RING, 2 BCUBE (AllreduceOptions::Algorithm).
+ * timeout_ms <= 0: context default (30 s). */
 int hydra_host_allreduce_threads(int P, int nptr, int op, int dtype, size_t n, void** in,
-                                 void** out, size_t max_segment, int reducer, hydra_reduce_fn fn,
-                                 long timeout_ms, char* err, size_t errlen);
+                                 void** out, size_t max_segment, int algorithm, int reducer,
+                                 hydra_reduce_fn fn, long timeout_ms, char* err, size_t errlen);
 
 /* gloo::apipe_allreduce (bew_allreduce_a) on P thread-ranks with two loopback rails each.
  * in/out: P pointers each. */

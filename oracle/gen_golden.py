@@ -126,6 +126,49 @@ def gen_ring(out: dict, meta: dict) -> None:
     meta["ring"] = rows
 
 
+def gen_bcube(out: dict, meta: dict) -> None:
+    """gloo::allreduce BCUBE (allreduce.cc:423-700): power-of-two and factor-3/5/7 group sizes,
+    fp32 stress inputs (regenerated from synth, sha-pinned), int32, and f16 (stored inputs);
+    multi-pointer in/out-of-place on a few cases."""
+    rows = []
+    rng = np.random.default_rng(79)
+    for P in (1, 2, 3, 4, 6, 8, 12):
+        for n in (1, 7, 100, 1000, 4099, 100003):
+            xs = [synth.stress_f32(P, r, n) for r in range(P)]
+            outs = [[x.copy()] for x in xs]
+            O.ref_allreduce(P, outs, None, algorithm=2)
+            res = outs[0][0]
+            for r in range(1, P):
+                assert np.array_equal(outs[r][0].view(np.uint32), res.view(np.uint32))
+            key = f"bcube_f32_P{P}_n{n}"
+            row = {"P": P, "n": n, "dtype": 6, "key": key, "inputs_sha256": sha(np.stack(xs)),
+                   "output_sha256": sha(res)}
+            if n <= 4099:
+                out[key] = res
+            else:
+                out[key + "_head"] = res[:1024]
+                out[key + "_tail"] = res[-1024:]
+            rows.append(row)
+    for P, n in ((2, 1000), (6, 4099), (8, 1000)):
+        xs = [synth.int32_bucket(P, r, n) for r in range(P)]
+        outs = [[x.copy()] for x in xs]
+        O.ref_allreduce(P, outs, None, algorithm=2)
+        key = f"bcube_i32_P{P}_n{n}"
+        out[key] = outs[0][0]
+        rows.append({"P": P, "n": n, "dtype": 2, "key": key, "inputs_sha256": sha(np.stack(xs)),
+                     "output_sha256": sha(outs[0][0])})
+    for P, n in ((2, 1000), (3, 4099), (8, 1000)):
+        xs = [np.array([O.f2h(float(v)) for v in rng.uniform(-8, 8, n)], np.uint16)
+              for _ in range(P)]
+        outs = [[x.copy()] for x in xs]
+        O.ref_allreduce(P, outs, None, dtype_code=8, algorithm=2)
+        key = f"bcube_f16_P{P}_n{n}"
+        out[key + "_in"] = np.stack(xs)
+        out[key] = outs[0][0]
+        rows.append({"P": P, "n": n, "dtype": 8, "key": key, "stored_inputs": True})
+    meta["bcube"] = rows
+
+
 def gen_old_ring(out: dict, meta: dict) -> None:
     """Old-style AllreduceRing<T> (allreduce_ring.h:20-125): per-rank outputs (they differ)."""
     rows = []
@@ -218,6 +261,7 @@ def main() -> None:
     gen_ops(out, meta)
     gen_ring(out, meta)
     gen_old_ring(out, meta)
+    gen_bcube(out, meta)
     gen_chunked_ring(out, meta)
     gen_new_test(meta)
     import ctypes

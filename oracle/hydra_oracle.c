@@ -226,14 +226,10 @@ void orc_ring_plan(int P, size_t n, size_t esize, size_t max_segment, size_t* nu
  *   op(x_q, op(x_{q+1}, ... op(x_{q-2}, x_{q-1})))   (indices mod P)
  * All-gather + genLocalBroadcastFunction then copy that into every output of every rank.
  * P == 1 short-circuits to local reduce + broadcast (:129-133).                           */
-int orc_allreduce(int P, int nptr, int op, int dtype, size_t n, void** in, void** out,
-                  size_t max_segment) {
-  size_t es = orc_esize(dtype);
-  if (!es || P < 1 || nptr < 1) return 1;
-  size_t bytes = n * es;
-  unsigned char* x = (unsigned char*)malloc(bytes * (size_t)P + 1);
-  unsigned char* acc = (unsigned char*)malloc(bytes + 1);
-  if (!x || !acc) { free(x); free(acc); return 2; }
+/* Each rank's locally reduced value x_r (allreduce.cc:46-97): out[0] op= the other inputs. */
+static void local_values(int P, int nptr, int op, int dtype, size_t n, void** in, void** out,
+                         unsigned char* x) {
+  size_t bytes = n * orc_esize(dtype);
   for (int r = 0; r < P; r++) {
     unsigned char* xr = x + (size_t)r * bytes;
     void** src = in ? in + r * nptr : out + r * nptr;
@@ -251,6 +247,17 @@ int orc_allreduce(int P, int nptr, int op, int dtype, size_t n, void** in, void*
       }
     }
   }
+}
+
+int orc_allreduce(int P, int nptr, int op, int dtype, size_t n, void** in, void** out,
+                  size_t max_segment) {
+  size_t es = orc_esize(dtype);
+  if (!es || P < 1 || nptr < 1) return 1;
+  size_t bytes = n * es;
+  unsigned char* x = (unsigned char*)malloc(bytes * (size_t)P + 1);
+  unsigned char* acc = (unsigned char*)malloc(bytes + 1);
+  if (!x || !acc) { free(x); free(acc); return 2; }
+  local_values(P, nptr, op, dtype, n, in, out, x);
   if (P == 1) {
     memcpy(acc, x, bytes);
   } else {
@@ -280,6 +287,71 @@ int orc_allreduce(int P, int nptr, int op, int dtype, size_t n, void** in, void*
     for (int i = 0; i < nptr; i++) memcpy(out[r * nptr + i], acc, bytes);
   free(x);
   free(acc);
+  return 0;
+}
+
+/* ---- BCUBE (allreduce.cc:423-700) ----
+ * Group sizes: factors of 2 while P divides, then the remainder (computeGroupSizePerStep,
+ * :426-437).  Step s: rank r's group is the ranks base + i*dist (i < g); the current buffer
+ * range splits into g chunks of ceil(len/g); r keeps chunk (r/dist) % g and folds the group's
+ * partials into it in place, own value first, then peers in group order (:592-603).  After the
+ * last step every element has one owner; the all-gather copies the owner's bits everywhere. */
+int orc_allreduce_bcube(int P, int nptr, int op, int dtype, size_t n, void** in, void** out) {
+  size_t es = orc_esize(dtype);
+  if (!es || P < 1 || nptr < 1) return 1;
+  size_t bytes = n * es;
+  unsigned char* x = (unsigned char*)malloc(bytes * (size_t)P + 1);   /* partials */
+  unsigned char* snap = (unsigned char*)malloc(bytes * (size_t)P + 1);
+  size_t* boff = (size_t*)calloc((size_t)P, sizeof(size_t));          /* buffer range per rank */
+  size_t* blen = (size_t*)calloc((size_t)P, sizeof(size_t));
+  if (!x || !snap || !boff || !blen) { free(x); free(snap); free(boff); free(blen); return 2; }
+  local_values(P, nptr, op, dtype, n, in, out, x);
+  size_t sizes[64];
+  int steps = 0;
+  {
+    size_t sz = (size_t)P;
+    while (sz % 2 == 0) { sizes[steps++] = 2; sz /= 2; }
+    if (sz > 1) sizes[steps++] = sz;
+  }
+  for (int r = 0; r < P; r++) { boff[r] = 0; blen[r] = n; }
+  size_t dist = 1;
+  for (int s = 0; s < steps; s++) {
+    size_t g = sizes[s];
+    memcpy(snap, x, bytes * (size_t)P);
+    size_t* noff = (size_t*)malloc((size_t)P * sizeof(size_t));
+    size_t* nlen = (size_t*)malloc((size_t)P * sizeof(size_t));
+    for (int r = 0; r < P; r++) {
+      size_t grank = ((size_t)r / dist) % g, base = (size_t)r - grank * dist;
+      size_t chunk = (blen[r] + g - 1) / g;
+      size_t moff = boff[r] + grank * chunk;
+      size_t mlen = blen[r] > grank * chunk ? blen[r] - grank * chunk : 0;
+      if (mlen > chunk) mlen = chunk;
+      unsigned char* mine = x + (size_t)r * bytes + moff * es;
+      for (size_t i = 0; i < g; i++) {
+        size_t peer = base + i * dist;
+        if (peer == (size_t)r || mlen == 0) continue;
+        orc_op(op, dtype, mine, mine, snap + peer * bytes + moff * es, mlen);
+      }
+      noff[r] = moff;
+      nlen[r] = mlen;
+    }
+    memcpy(boff, noff, (size_t)P * sizeof(size_t));
+    memcpy(blen, nlen, (size_t)P * sizeof(size_t));
+    free(noff);
+    free(nlen);
+    dist *= g;
+  }
+  /* all-gather: every element's owner (the rank whose final range holds it) supplies the bits */
+  unsigned char* res = snap;
+  if (P == 1) memcpy(res, x, bytes);
+  for (int r = 0; r < P && P > 1; r++)
+    if (blen[r]) memcpy(res + boff[r] * es, x + (size_t)r * bytes + boff[r] * es, blen[r] * es);
+  for (int r = 0; r < P; r++)
+    for (int i = 0; i < nptr; i++) memcpy(out[r * nptr + i], res, bytes);
+  free(x);
+  free(snap);
+  free(boff);
+  free(blen);
   return 0;
 }
 

@@ -67,6 +67,8 @@ def orc():
         _orc.orc_allreduce_ring_old.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                 ctypes.c_int, _c, _vp]
         _orc.orc_allreduce_ring_chunked.argtypes = _orc.orc_allreduce_ring_old.argtypes
+        _orc.orc_allreduce_bcube.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                             ctypes.c_int, _c, _vp, _vp]
     return _orc
 
 
@@ -145,6 +147,12 @@ def _allreduce(fn_is_ref, P, outs, ins, kind, dtype_code, max_segment, algorithm
                                  ctypes.cast(optrs, _vp), max_segment, algorithm, 0, err, 512)
         if rc:
             raise RuntimeError(f"reference allreduce failed: {err.value.decode()}")
+    elif algorithm == 2:  # BCUBE
+        rc = orc().orc_allreduce_bcube(P, nptr, OPS[kind], code, n,
+                                       ctypes.cast(iptrs, _vp) if iptrs is not None else None,
+                                       ctypes.cast(optrs, _vp))
+        if rc:
+            raise RuntimeError("oracle bcube failed")
     else:
         rc = orc().orc_allreduce(P, nptr, OPS[kind], code, n,
                                  ctypes.cast(iptrs, _vp) if iptrs is not None else None,
@@ -154,9 +162,17 @@ def _allreduce(fn_is_ref, P, outs, ins, kind, dtype_code, max_segment, algorithm
     return outs
 
 
-def allreduce(P, outs, ins=None, kind="sum", dtype_code=None, max_segment=1 << 20):
-    """C restatement of gloo::allreduce(RING) over P ranks; returns outs (in place)."""
-    return _allreduce(False, P, outs, ins, kind, dtype_code, max_segment)
+def allreduce(P, outs, ins=None, kind="sum", dtype_code=None, max_segment=1 << 20, algorithm=1):
+    """C restatement of gloo::allreduce (1 RING, 2 BCUBE) over P ranks; returns outs (in place)."""
+    return _allreduce(False, P, outs, ins, kind, dtype_code, max_segment, algorithm)
+
+
+def bcube_result(xs: list[np.ndarray], kind: str = "sum",
+                 dtype_code: int | None = None) -> np.ndarray:
+    """Convenience: BCUBE-reduced bucket of in-place single-pointer ranks xs (not modified)."""
+    outs = [[x.copy()] for x in xs]
+    allreduce(len(xs), outs, None, kind, dtype_code, algorithm=2)
+    return outs[0][0]
 
 
 def ref_allreduce(P, outs, ins=None, kind="sum", dtype_code=None, max_segment=1 << 20,

@@ -113,6 +113,8 @@ def _worker(rank, world, port, algo, n, ms, ch, q):
             olds = [[x.copy()] for x in xs]
             (O.allreduce_ring_old if algo == "ring_old" else O.allreduce_ring_chunked)(olds)
             exp = olds[rank][0]
+        elif algo == "bcube":
+            exp = O.bcube_result(xs)
         else:
             exp = O.ring_result(xs, ms or (1 << 20))
         q.put((rank, bool(np.array_equal(got.view(np.uint32), exp.view(np.uint32)))))
@@ -123,7 +125,8 @@ def _worker(rank, world, port, algo, n, ms, ch, q):
 
 
 @pytest.mark.parametrize("world", [2, 3])
-@pytest.mark.parametrize("algo", ["ring", "direct", "a2a", "ring_old", "ring_chunked"])
+@pytest.mark.parametrize("algo", ["ring", "direct", "a2a", "ring_old", "ring_chunked",
+                                  "bcube"])
 def test_gloo_multiprocess_plan(algo, world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

@@ -14,11 +14,13 @@ def fnptr(O, name):
     return ctypes.cast(getattr(O.orc(), name), ctypes.c_void_p).value
 
 
+@pytest.mark.parametrize("algorithm", ["ring", "bcube"])
 @pytest.mark.parametrize("P", [1, 2, 4, 7])
 @pytest.mark.parametrize("nptr", [1, 2, 3])
 @pytest.mark.parametrize("inplace", [True, False])
-def test_allreduce_new_test_default(O, P, nptr, inplace):
-    """AllreduceNewTest.Default (test/allreduce_test.cc:302-362): uint64, maxSegmentSize=128."""
+def test_allreduce_new_test_default(O, P, nptr, inplace, algorithm):
+    """AllreduceNewTest.Default (test/allreduce_test.cc:302-362): uint64, maxSegmentSize=128;
+    the reference test is parametrized over RING and BCUBE (allreduce_test.cc:355-362)."""
     for n in (1, 10, 100, 1000):
         stride = P * nptr
         vals = [[np.arange(n, dtype=np.uint64) * stride + r * nptr + i for i in range(nptr)]
@@ -28,7 +30,8 @@ def test_allreduce_new_test_default(O, P, nptr, inplace):
         else:
             outs = [[np.zeros(n, np.uint64) for _ in range(nptr)] for _ in range(P)]
             ins = vals
-        host.allreduce_threads(outs, ins, max_segment=128, reducer_fn=fnptr(O, "orc_sum_u64"))
+        host.allreduce_threads(outs, ins, max_segment=128, reducer_fn=fnptr(O, "orc_sum_u64"),
+                               algorithm=algorithm)
         exp = np.arange(n, dtype=np.uint64) * stride * stride + np.uint64(stride * (stride - 1) // 2)
         for r in range(P):
             for i in range(nptr):
@@ -143,3 +146,45 @@ def test_chunked_allreduce_ring_large(O):
     O.allreduce_ring_chunked(exp)
     for r in range(P):
         assert np.array_equal(bufs[r][0].view(np.uint32), exp[r][0].view(np.uint32))
+
+
+def test_bcube_vs_golden(O, golden, golden_meta):
+    """BCUBE (allreduce.cc:423-700) on the host runtime == the reference's own BCUBE output
+    (fixtures: P in 1,2,3,4,6,8,12, ragged n, fp32 stress / int32 / f16)."""
+    import hashlib
+
+    names = {6: "orc_sum_f32", 2: "orc_sum_i32", 8: "orc_sum_f16"}
+    for row in golden_meta["bcube"]:
+        P, n, key, code = row["P"], row["n"], row["key"], row["dtype"]
+        if row.get("stored_inputs"):
+            xs = list(golden[key + "_in"])
+        elif code == 2:
+            xs = [synth.int32_bucket(P, r, n) for r in range(P)]
+        else:
+            xs = [synth.stress_f32(P, r, n) for r in range(P)]
+        if "inputs_sha256" in row:
+            assert hashlib.sha256(np.stack(xs).tobytes()).hexdigest() == row["inputs_sha256"]
+        outs = [[x.copy()] for x in xs]
+        host.allreduce_threads(outs, None, dtype_code=code, reducer_fn=fnptr(O, names[code]),
+                               algorithm="bcube")
+        for r in range(P):
+            got = outs[r][0]
+            if key in golden:
+                assert np.array_equal(got.view(np.uint8), golden[key].view(np.uint8)), (key, r)
+            else:
+                assert hashlib.sha256(got.tobytes()).hexdigest() == row["output_sha256"], key
+
+
+def test_bcube_multi_pointer_out_of_place(O):
+    """BCUBE's local reduce (step 0, per chunk) and local broadcast (per received chunk) with
+    several inputs and outputs, vs the C restatement (pinned to the reference in test_oracle)."""
+    P, n, nptr = 6, 10007, 3
+    xs = [[synth.stress_f32(P, r, n, seed=90 + i) for i in range(nptr)] for r in range(P)]
+    outs = [[np.full(n, 5, np.float32) for _ in range(nptr)] for _ in range(P)]
+    exp = [[np.full(n, 5, np.float32) for _ in range(nptr)] for _ in range(P)]
+    host.allreduce_threads(outs, [[x.copy() for x in r] for r in xs],
+                           reducer_fn=fnptr(O, "orc_sum_f32"), algorithm="bcube")
+    O.allreduce(P, exp, [[x.copy() for x in r] for r in xs], algorithm=2)
+    for r in range(P):
+        for i in range(nptr):
+            assert np.array_equal(outs[r][i].view(np.uint32), exp[r][i].view(np.uint32))

@@ -348,3 +348,20 @@ def test_bench_self_check_helpers(O):
                               b[r][0].view(np.uint32))
     assert np.array_equal(ring.expected_fold_f32(xs).view(np.uint32),
                           O.ring_result(xs).view(np.uint32))
+    for P2 in (1, 2, 6, 8, 12):
+        ys = [synth.stress_f32(P2, r, n) for r in range(P2)]
+        assert np.array_equal(ring.expected_bcube_f32(ys).view(np.uint32),
+                              O.bcube_result(ys).view(np.uint32)), P2
+
+
+@pytest.mark.parametrize("P,n", [(2, 1), (2, 1000), (3, 7), (4, 4099), (6, 100003), (8, 262145),
+                                 (12, 30011), (5, 100)])
+def test_bcube_plan(O, P, n):
+    """BCUBE on device (plan BCUBE): bit-exact vs the oracle's BCUBE (pinned to the reference by
+    tests/test_oracle.py) on every rank, and race-free."""
+    xs = [synth.stress_f32(P, r, n) for r in range(P)]
+    outs = run_plan_numpy(O, "bcube", xs, 0, 0)
+    exp = O.bcube_result(xs)
+    for r in range(P):
+        assert np.array_equal(outs[r].view(np.uint32), exp.view(np.uint32)), r
+        race_check(ring.plan("bcube", P, r, n, 4, 0, 0)[0])
