@@ -44,7 +44,7 @@ def parse():
                    help="bounded CPU-baseline sample (seconds of reference gloo::sum work)")
     p.add_argument("--sweep", action="store_true", help="add the 4 Ki..64 Mi size sweep")
     p.add_argument("--algo", default="auto", help="ring algorithm for N>1 (see hydra_amd.ring)")
-    p.add_argument("--watchdog-s", type=float, default=900.0,
+    p.add_argument("--watchdog-s", type=float, default=420.0,
                    help="N>1: abort (exit 3) if the run exceeds this many seconds")
     p.add_argument("--no-config5", action="store_true", help="N>1: skip the bf16 config-5 leg")
     p.add_argument("--force-dist", action="store_true",

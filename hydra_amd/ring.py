@@ -290,7 +290,7 @@ def bench_allreduce(args, dev) -> dict:
         sys.stderr.flush()
         os._exit(3)
 
-    dog = threading.Timer(float(getattr(args, "watchdog_s", 900)), _expire)
+    dog = threading.Timer(float(getattr(args, "watchdog_s", 420)), _expire)
     dog.daemon = True
     dog.start()
     uid = exchange_unique_id(rank, dev)
