@@ -208,7 +208,11 @@ __device__ __forceinline__ u32x4 vapply(u32x4 ra, u32x4 rb, u32x4 rc) {
 //   head/tail : scalar elements before (at c - head) / after the body, each < Vec<E>::N
 //   C_OLD     : load c's old bits (float16 store quirk when c is not a)
 // -------------------------------------------------------------------------------------------
-template <typename E, int OP, int UNROLL, int LDP, int STP, bool C_OLD, int BS = kBlock>
+// MAP 1: XCD-contiguous tiles -- the dispatcher deals workgroups round-robin to the 8 XCDs, so
+// block b runs on XCD b % 8; remapping it to tile (b % 8) * (grid / 8) + b / 8 gives each XCD
+// one contiguous eighth of the stream instead of every eighth tile (measurement variant).
+template <typename E, int OP, int UNROLL, int LDP, int STP, bool C_OLD, int BS = kBlock,
+          int MAP = 0>
 __global__ __launch_bounds__(BS) void k_reduce(E* c_, const E* a_, const E* b_, size_t nvec,
                                                int head, int tail) {
   constexpr int N = Vec<E>::N;
@@ -234,7 +238,9 @@ __global__ __launch_bounds__(BS) void k_reduce(E* c_, const E* a_, const E* b_, 
   }
 
   const size_t ntiles = (nvec + TILE - 1) / TILE;
-  for (size_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+  size_t first = blockIdx.x;
+  if (MAP == 1 && (gridDim.x & 7) == 0) first = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+  for (size_t tile = first; tile < ntiles; tile += gridDim.x) {
     const size_t tbase = tile * TILE * 16;  // byte offset of this tile
     if ((tile + 1) * TILE <= nvec) {        // full tile: no predicates
       const char* at = a + tbase;
@@ -528,7 +534,7 @@ Split split_call(const void* c, size_t n) {
   return s;
 }
 
-template <typename E, int OP, int UNROLL, int LDP, int STP, int BS = kBlock>
+template <typename E, int OP, int UNROLL, int LDP, int STP, int BS = kBlock, int MAP = 0>
 hipError_t launch_t(void* c, const void* a, const void* b, size_t n, hipStream_t s,
                     int max_blocks) {
   const Split sp = split_call<E>(c, n);
@@ -542,10 +548,10 @@ hipError_t launch_t(void* c, const void* a, const void* b, size_t n, hipStream_t
   if (max_blocks > 0 && grid > (size_t)max_blocks) grid = (size_t)max_blocks;
   const bool c_old = Elem<E, OP>::kNeedsOld && c != a;
   if (c_old)
-    hipLaunchKernelGGL((k_reduce<E, OP, UNROLL, LDP, STP, true, BS>), dim3((unsigned)grid),
+    hipLaunchKernelGGL((k_reduce<E, OP, UNROLL, LDP, STP, true, BS, MAP>), dim3((unsigned)grid),
                        dim3(BS), 0, s, cb, ab, bb, sp.nvec, sp.head, sp.tail);
   else
-    hipLaunchKernelGGL((k_reduce<E, OP, UNROLL, LDP, STP, false, BS>), dim3((unsigned)grid),
+    hipLaunchKernelGGL((k_reduce<E, OP, UNROLL, LDP, STP, false, BS, MAP>), dim3((unsigned)grid),
                        dim3(BS), 0, s, cb, ab, bb, sp.nvec, sp.head, sp.tail);
   return hipGetLastError();
 }
@@ -572,12 +578,13 @@ hipError_t launch_lds(void* c, const void* a, const void* b, size_t n, hipStream
   return hipGetLastError();
 }
 
-// The tuned default (profiles/r01_tune.json): one 16-B vector per lane per
-// operand, nontemporal loads, write-through (sc1) stores -- 109.7 us for 64 Mi fp32 in place
-// back to back (7.34 TB/s), 6.2-6.3 TB/s once the working set is past the Infinity Cache.
+// The tuned default (profiles/r01_tune_variants.json, r01_tune_xcd.json): one
+// 16-B vector per lane per operand, nontemporal loads, write-through (sc1) stores, tiles mapped
+// XCD-contiguously -- 108.2 us for 64 Mi fp32 in place back to back (7.44 TB/s), 6.3-6.4 TB/s
+// once the working set is past the Infinity Cache.
 template <typename E, int OP>
 hipError_t launch_default(void* c, const void* a, const void* b, size_t n, hipStream_t s) {
-  return launch_t<E, OP, 1, kNT, kBuf | 16>(c, a, b, n, s, 0);
+  return launch_t<E, OP, 1, kNT, kBuf | 16, kBlock, 1>(c, a, b, n, s, 0);
 }
 
 template <typename E, int OP>
@@ -625,6 +632,10 @@ hipError_t launch_tuning(int variant, void* c, const void* a, const void* b, siz
     case 37: return launch_t<E, OP, 4, kNT, B | 18>(c, a, b, n, s, 0);
     case 38: return launch_t<E, OP, 4, B | 18, B | 16>(c, a, b, n, s, 0);
     case 39: return launch_t<E, OP, 2, kNT, B | 16, 512>(c, a, b, n, s, 0);
+    case 40: return launch_t<E, OP, 1, kNT, B | 16, kBlock, 1>(c, a, b, n, s, 0);  // 33, XCD map
+    case 41: return launch_t<E, OP, 1, kNT, B | 18, kBlock, 1>(c, a, b, n, s, 0);  // 36, XCD map
+    case 42: return launch_t<E, OP, 1, kNT, kNT, kBlock, 1>(c, a, b, n, s, 0);     // 17, XCD map
+    case 43: return launch_t<E, OP, 2, kNT, B | 16, kBlock, 1>(c, a, b, n, s, 0);  // 34, XCD map
     default: return launch_default<E, OP>(c, a, b, n, s);
   }
 }
