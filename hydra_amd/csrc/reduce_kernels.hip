@@ -474,7 +474,7 @@ __device__ __forceinline__ E fold_elem(const FoldSrcs& S, int nsrc, ptrdiff_t i)
 }
 
 // S.p[*] and dst already advanced by `head` elements (dst 16-B aligned at the body).
-template <typename E, int OP, bool ACC32, bool NT>
+template <typename E, int OP, bool ACC32, bool NT, int MAP = 0>
 __global__ __launch_bounds__(kBlock) void k_fold(E* dst, FoldSrcs S, int nsrc, size_t nvec,
                                                  int head, int tail) {
   constexpr int N = Vec<E>::N;
@@ -489,7 +489,9 @@ __global__ __launch_bounds__(kBlock) void k_fold(E* dst, FoldSrcs S, int nsrc, s
   }
   char* d = reinterpret_cast<char*>(dst);
   const size_t stride = (size_t)gridDim.x * kBlock;
-  for (size_t vb = (size_t)blockIdx.x * kBlock; vb < nvec; vb += stride) {  // wave-uniform
+  size_t first = blockIdx.x;  // MAP 1: XCD-contiguous blocks within each grid stride (k_reduce)
+  if (MAP == 1 && (gridDim.x & 7) == 0) first = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+  for (size_t vb = first * kBlock; vb < nvec; vb += stride) {  // wave-uniform
     const size_t v = vb + t;
     // write-through (sc1) store through a block-uniform descriptor, as the chunk-sum default
     const auto w = __builtin_amdgcn_make_buffer_rsrc(d + vb * 16, 0, kBlock * 16, 0x00020000);
@@ -685,7 +687,7 @@ hipError_t launch_reduce(int variant, int op, int dtype, void* c, const void* a,
 }
 
 namespace {
-template <typename E, int OP, bool ACC32, bool NT>
+template <typename E, int OP, bool ACC32, bool NT, int MAP = 0>
 hipError_t launch_fold_v(void* dst, const void* const* srcs, int nsrc, size_t n, hipStream_t s,
                          size_t cap_per_cu) {
   const Split sp = split_call<E>(dst, n);
@@ -698,22 +700,28 @@ hipError_t launch_fold_v(void* dst, const void* const* srcs, int nsrc, size_t n,
   const size_t cap = (size_t)cu_count() * cap_per_cu;
   if (cap_per_cu && blocks > cap) blocks = cap;
   if (blocks == 0) blocks = 1;
-  hipLaunchKernelGGL((k_fold<E, OP, ACC32, NT>), dim3((unsigned)blocks), dim3(kBlock), 0, s, d,
+  hipLaunchKernelGGL((k_fold<E, OP, ACC32, NT, MAP>), dim3((unsigned)blocks), dim3(kBlock), 0, s, d,
                      S, nsrc, sp.nvec, sp.head, sp.tail);
   return hipGetLastError();
 }
 
 // Fold variants (hydra_set_variant, measurement only; 0 = default): 1 plain loads, grid capped
-// at 8 blocks/CU; 2 nontemporal loads, capped; 3 nontemporal, one block per 256 vectors.
+// at 8 blocks/CU; 2 nontemporal loads, capped; 3 nontemporal, one block per 256 vectors;
+// 4-7 = 1, plain full grid, 3, 2 with XCD-contiguous blocks.
 template <typename E, int OP, bool ACC32>
 hipError_t launch_fold_t(void* dst, const void* const* srcs, int nsrc, size_t n, hipStream_t s) {
   switch (current_variant()) {
     case 1: return launch_fold_v<E, OP, ACC32, false>(dst, srcs, nsrc, n, s, 8);
     case 2: return launch_fold_v<E, OP, ACC32, true>(dst, srcs, nsrc, n, s, 8);
     case 3: return launch_fold_v<E, OP, ACC32, true>(dst, srcs, nsrc, n, s, 0);
-    default:  // tuned (profiles/r01_tune_fold.json): fp32 6.6 TB/s plain; bf16->fp32 6.3 nt
+    case 4: return launch_fold_v<E, OP, ACC32, false, 1>(dst, srcs, nsrc, n, s, 8);  // 1, XCD map
+    case 5: return launch_fold_v<E, OP, ACC32, false, 1>(dst, srcs, nsrc, n, s, 0);  // full grid
+    case 6: return launch_fold_v<E, OP, ACC32, true, 1>(dst, srcs, nsrc, n, s, 0);   // 3, XCD map
+    case 7: return launch_fold_v<E, OP, ACC32, true, 1>(dst, srcs, nsrc, n, s, 8);   // 2, XCD map
+    default:  // tuned (profiles/r01_tune_fold_xcd.json): same-type folds plain loads, full grid,
+              // XCD-contiguous (P=8 fp32 6.75 TB/s); bf16->fp32 nontemporal, full grid (6.4)
       if constexpr (ACC32) return launch_fold_v<E, OP, ACC32, true>(dst, srcs, nsrc, n, s, 0);
-      else return launch_fold_v<E, OP, ACC32, false>(dst, srcs, nsrc, n, s, 8);
+      else return launch_fold_v<E, OP, ACC32, false, 1>(dst, srcs, nsrc, n, s, 0);
   }
 }
 

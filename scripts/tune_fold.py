@@ -24,7 +24,7 @@ for (P, n, code, flags) in [(8, 8 << 20, 6, 0), (8, 32 << 20, 9, 1), (4, 16 << 2
     ptrs = (ctypes.c_void_p * P)(*[t.data_ptr() for t in srcs])
     key = f"P{P}/n{n}/{'bf16acc32' if flags else 'f32'}"
     for rnd in range(5):
-        for v in (0, 1, 2, 3):
+        for v in [int(x) for x in os.environ.get("VARIANTS", "0,1,2,3,4,5,6,7").split(",")]:
             L.hydra_set_variant(v)
             ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                   for _ in range(15)]

@@ -169,7 +169,7 @@ def test_a2a_rejects_unequal_blocks(gpu):
         ring.simulate(bufs, algo="a2a")
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7])
 @pytest.mark.parametrize("P", [1, 2, 5, 8, 16])
 def test_fold_abi_reference_order(gpu, O, P, variant):
     """hydra_fold == the owner's P-1 in-place ring hops, every fold variant, ragged sizes and
