@@ -174,15 +174,17 @@ int run_plan_rccl(hydra_comm* c, int op, int dtype, bool acc32, char* user, hipE
       if (g == ops.size()) return fail(HYDRA_ERR_INVALID, "plan: unterminated p2p group");
       wait_on(c->cs, ops[g], c->events);
       NCCL_TRY(ncclGroupStart());
-      for (size_t j = i; j < g; j++) {
+      ncclResult_t r = ncclSuccess;
+      for (size_t j = i; j < g && r == ncclSuccess; j++) {
         const hydra::PlanOp& p = ops[j];
         char* base = (p.buf == hydra::kBufUser ? user : scratch) + p.off;
-        if (p.kind == hydra::kOpSend)
-          NCCL_TRY(ncclSend(base, (size_t)p.bytes, ncclUint8, p.peer, c->nccl, c->cs));
-        else
-          NCCL_TRY(ncclRecv(base, (size_t)p.bytes, ncclUint8, p.peer, c->nccl, c->cs));
+        r = p.kind == hydra::kOpSend
+                ? ncclSend(base, (size_t)p.bytes, ncclUint8, p.peer, c->nccl, c->cs)
+                : ncclRecv(base, (size_t)p.bytes, ncclUint8, p.peer, c->nccl, c->cs);
       }
-      NCCL_TRY(ncclGroupEnd());
+      const ncclResult_t e = ncclGroupEnd();  // always close the group, even after a failure
+      if (r != ncclSuccess) return nccl_fail(r, "ncclSend/ncclRecv");
+      if (e != ncclSuccess) return nccl_fail(e, "ncclGroupEnd");
       if (c->waited[g]) HIP_TRY(hipEventRecord(c->events[g], c->cs));
       i = g + 1;
     } else {
