@@ -32,7 +32,7 @@ EXPORTS = [  # every symbol include/hydra_hip.h declares
     "hydra_comm_get_unique_id", "hydra_comm_init", "hydra_comm_destroy", "hydra_allreduce",
     "hydra_plan", "hydra_allreduce_simulate", "hydra_fold", "hydra_memcpy_async",
     "hydra_malloc_host", "hydra_free_host", "hydra_pointer_device", "hydra_split_elements",
-    "hydra_apipe_allreduce", "hydra_apipe_allreduce_simulate",
+    "hydra_apipe_allreduce", "hydra_apipe_allreduce_simulate", "hydra_comm_run_plan",
 ]
 
 (ALGO_AUTO, ALGO_RING, ALGO_DIRECT, ALGO_RCCL, ALGO_A2A, ALGO_RING_OLD, ALGO_RING_CHUNKED,
@@ -105,6 +105,7 @@ def _declare(L) -> None:
     L.hydra_split_elements.argtypes = [i, i, sz, ctypes.POINTER(sz), ctypes.POINTER(sz)]
     L.hydra_split_elements.restype = None
     L.hydra_apipe_allreduce.argtypes = [vp, vp, i, i, i, i, i, vp, sz, sz, sz, vp]
+    L.hydra_comm_run_plan.argtypes = [vp, ctypes.POINTER(PlanOp), sz, i, i, i, vp, sz, sz, vp]
     L.hydra_apipe_allreduce_simulate.argtypes = [i, i, i, i, i, i, ctypes.POINTER(vp), sz, sz,
                                                  sz]
     L.hydra_ring_plan.argtypes = [i, sz, sz, sz] + [ctypes.POINTER(sz)] * 3

@@ -628,6 +628,90 @@ int hydra_allreduce_simulate(int algo, int op, int dtype, int flags, int P, void
   return ok();
 }
 
+// Executor test hook: run an arbitrary (validated) plan through the RCCL executor.  With a
+// 1-rank communicator and every peer remapped to 0, RCCL's send/recv-to-self exercises the real
+// executor -- groups, both streams, the event edges -- on one GPU.
+int hydra_comm_run_plan(hydra_comm_t c, const hydra_plan_op_t* ops, size_t nops, int op, int dtype,
+                        int flags, void* buf, size_t buf_bytes, size_t scratch_bytes,
+                        hydra_stream_t stream) {
+  if (!c || (!ops && nops)) return fail(HYDRA_ERR_INVALID, "null argument");
+  size_t es;
+  int rc = check_plan_args(HYDRA_ALGO_RING, op, dtype, flags, &es);
+  if (rc) return rc;
+  std::vector<hydra::PlanOp> plan(nops);
+  if (nops) std::memcpy(plan.data(), ops, nops * sizeof(hydra::PlanOp));
+  // every access must stay inside buf / scratch: a bad plan must fail here, not fault the GPU
+  auto inside = [](int64_t off, int64_t len, size_t cap) {
+    return off >= 0 && len >= 0 && (size_t)off <= cap && (size_t)len <= cap - (size_t)off;
+  };
+  for (size_t i = 0; i < nops; i++) {
+    const hydra::PlanOp& o = plan[i];
+    const size_t cap = o.buf == hydra::kBufUser ? buf_bytes : scratch_bytes;
+    if ((o.wait0 >= (int)i) || (o.wait1 >= (int)i))
+      return fail(HYDRA_ERR_INVALID, "plan: wait on a later op");
+    switch (o.kind) {
+      case hydra::kOpSend:
+      case hydra::kOpRecv:
+        if (o.peer < 0 || o.peer >= c->nranks || !inside(o.off, o.bytes, cap))
+          return fail(HYDRA_ERR_INVALID, "plan: bad p2p op");
+        break;
+      case hydra::kOpGroup:
+        break;
+      case hydra::kOpReduce:
+        if (o.bytes % (int64_t)es || !inside(o.off, o.bytes, buf_bytes) ||
+            !inside(o.src_off, o.bytes, scratch_bytes))
+          return fail(HYDRA_ERR_INVALID, "plan: bad reduce");
+        break;
+      case hydra::kOpFold:
+        if (o.nsrc < 1 || o.nsrc > hydra::kMaxRanks || o.bytes % (int64_t)es ||
+            !inside(o.off, o.bytes, buf_bytes))
+          return fail(HYDRA_ERR_INVALID, "plan: bad fold");
+        for (int j = 1; j < o.nsrc; j++)
+          if (!inside(hydra::fold_slot(o, j), o.bytes, scratch_bytes))
+            return fail(HYDRA_ERR_INVALID, "plan: fold slot outside scratch");
+        break;
+      case hydra::kOpAllToAll:
+        if (o.bytes < 0 || !inside(o.off, o.bytes * c->nranks, buf_bytes) ||
+            !inside(o.src_off, o.bytes * c->nranks, scratch_bytes))
+          return fail(HYDRA_ERR_INVALID, "plan: bad all-to-all");
+        break;
+      case hydra::kOpAllGather:
+        if (o.bytes < 0 || !inside(o.off, o.bytes * c->nranks, buf_bytes))
+          return fail(HYDRA_ERR_INVALID, "plan: bad all-gather");
+        break;
+      default:
+        return fail(HYDRA_ERR_INVALID, "plan: unknown op kind");
+    }
+  }
+  if (nops && plan.back().kind != hydra::kOpGroup) {
+    bool open = false;
+    for (const auto& o : plan) open = (o.kind == hydra::kOpSend || o.kind == hydra::kOpRecv) ? true
+                                      : (o.kind == hydra::kOpGroup ? false : open);
+    if (open) return fail(HYDRA_ERR_INVALID, "plan: unterminated p2p group");
+  }
+  if (scratch_bytes > c->scratch_bytes) {
+    HIP_TRY(hipDeviceSynchronize());
+    if (c->scratch) HIP_TRY(hipFree(c->scratch));
+    c->scratch = nullptr;
+    c->scratch_bytes = 0;
+    HIP_TRY(hipMalloc(&c->scratch, scratch_bytes));
+    c->scratch_bytes = scratch_bytes;
+  }
+  c->plan = std::move(plan);
+  c->waited = waited_set(c->plan);
+  c->key_algo = -1;  // the plan cache no longer holds a library plan
+  rc = ensure_events(c, c->plan.size());
+  if (rc) return rc;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  // deterministic scratch for the hook (slots a 1-rank collective leaves untouched read as 0)
+  if (scratch_bytes) HIP_TRY(hipMemsetAsync(c->scratch, 0, scratch_bytes, st));
+  HIP_TRY(hipEventRecord(c->ev_start, st));
+  rc = run_plan_rccl(c, op, dtype, (flags & HYDRA_ACC_F32) != 0, static_cast<char*>(buf),
+                     c->ev_start);
+  if (!rc) rc = join_streams(c, st);
+  return rc ? rc : ok();
+}
+
 // apipe on one GPU: the split, then each non-empty part through the P-rank simulator.
 int hydra_apipe_allreduce_simulate(int table, int algo, int op, int dtype, int flags, int P,
                                    void** bufs, size_t n, size_t max_segment, size_t chunk_bytes) {

@@ -149,6 +149,24 @@ class XgmiComm:
                                                code, flags, t.data_ptr(), _count(t, code),
                                                max_segment, chunk_bytes, s))
 
+    def run_plan_(self, ops, t, scratch_bytes: int, op: str = "sum",
+                  dtype_code: int | None = None, flags: int = 0,
+                  stream: int | None = None) -> None:
+        """Executor test hook (hydra_comm_run_plan): run op dicts (as ring.plan returns) on t."""
+        import torch
+
+        from .reduce import _torch_dtype_code
+
+        code = dtype_code if dtype_code is not None else _torch_dtype_code(t)
+        arr = (_lib.PlanOp * max(1, len(ops)))()
+        for i, o in enumerate(ops):
+            for f, _ in _lib.PlanOp._fields_:
+                setattr(arr[i], f, int(o[f]))
+        s = stream if stream is not None else torch.cuda.current_stream(t.device).cuda_stream
+        check(_lib.lib().hydra_comm_run_plan(self._h, arr, len(ops), OPS[op], code, flags,
+                                             t.data_ptr(), t.numel() * t.element_size(),
+                                             scratch_bytes, s))
+
     def close(self) -> None:
         if self._h:
             _lib.lib().hydra_comm_destroy(self._h)

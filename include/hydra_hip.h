@@ -202,6 +202,13 @@ void hydra_split_elements(int table, int P, size_t n, size_t* e1, size_t* e2);
 int hydra_apipe_allreduce(hydra_comm_t rail1, hydra_comm_t rail2, int table, int algo, int op,
                           int dtype, int flags, void* buf, size_t n, size_t max_segment,
                           size_t chunk_bytes, hydra_stream_t stream);
+/* Executor test hook: run `ops` (e.g. a hydra_plan with peers remapped) through the RCCL
+ * executor of `comm`.  Every op is validated against buf_bytes / scratch_bytes (collectives:
+ * against the communicator size) first.  On a 1-rank communicator, RCCL's send/recv-to-self runs the real
+ * executor (groups, both streams, event edges) on one GPU. */
+int hydra_comm_run_plan(hydra_comm_t comm, const hydra_plan_op_t* ops, size_t nops, int op,
+                        int dtype, int flags, void* buf, size_t buf_bytes, size_t scratch_bytes,
+                        hydra_stream_t stream);
 /* The same split on P simulated ranks of one GPU (see hydra_allreduce_simulate). */
 int hydra_apipe_allreduce_simulate(int table, int algo, int op, int dtype, int flags, int P,
                                    void** bufs, size_t n, size_t max_segment, size_t chunk_bytes);

@@ -351,3 +351,40 @@ def test_simulated_bcube_vs_reference_fixtures(gpu, golden, golden_meta):
                 assert np.array_equal(got, golden[key].view(v)), (key, r)
             else:
                 assert hashlib.sha256(got.tobytes()).hexdigest() == row["output_sha256"], key
+
+
+@pytest.mark.parametrize("algo,P,n,ch", [("ring", 2, 1 << 20, 1 << 18), ("ring", 4, 1 << 20, 0),
+                                         ("direct", 4, 1 << 20, 1 << 18),
+                                         ("direct", 8, 1 << 21, 1 << 19),
+                                         ("ring_old", 3, 300000, 1 << 18),
+                                         ("ring_chunked", 4, 1 << 20, 0),
+                                         ("bcube", 8, 1 << 20, 0), ("bcube", 6, 6 << 12, 0),
+                                         ("a2a", 2, 1 << 20, 0), ("a2a", 8, 1 << 20, 0)])
+def test_rccl_executor_self_loop(gpu, O, algo, P, n, ch):
+    """The real RCCL executor on one GPU: rank 0's plan with every peer remapped to itself runs
+    on a 1-rank communicator (RCCL send/recv-to-self), through the same groups, streams and
+    event edges as on 8 GPUs (A2A: ncclAllToAll / ncclAllGather on the 1-rank communicator).
+    Expected bytes: the numpy interpreter on the same remapped plan."""
+    import torch
+
+    from plan_interp import RECV, SEND, run_plan_numpy
+
+    ops, scr = ring.plan(algo, P, 0, n, 4, 0, ch)
+    for o in ops:
+        if o["kind"] in (SEND, RECV):
+            o["peer"] = 0
+    x = synth.stress_f32(P, 0, n)
+    exp = run_plan_numpy(O, algo, [x], 0, ch, plans=[ops], scr=scr)[0]
+    comm = ring.XgmiComm(0, 1, gpu.index or 0, ring._rccl_unique_id())
+    try:
+        t = torch.from_numpy(x.copy()).to(gpu)
+        comm.run_plan_(ops, t, scr)
+        torch.cuda.synchronize()
+        assert np.array_equal(t.cpu().numpy().view(np.uint32), exp.view(np.uint32))
+        # a plan reaching outside the buffers is refused before anything is launched
+        bad = [dict(o) for o in ops]
+        bad[0]["off"] = 4 * n
+        with pytest.raises(_lib.HydraError):
+            comm.run_plan_(bad, t, scr)
+    finally:
+        comm.close()
