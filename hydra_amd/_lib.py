@@ -33,6 +33,9 @@ EXPORTS = [  # every symbol include/hydra_hip.h declares
     "hydra_plan", "hydra_allreduce_simulate", "hydra_fold", "hydra_memcpy_async",
     "hydra_malloc_host", "hydra_free_host", "hydra_pointer_device", "hydra_split_elements",
     "hydra_apipe_allreduce", "hydra_apipe_allreduce_simulate", "hydra_comm_run_plan",
+    "hydra_peer_create", "hydra_peer_connect", "hydra_peer_register", "hydra_peer_open",
+    "hydra_peer_close", "hydra_peer_set_option", "hydra_peer_error", "hydra_peer_allreduce",
+    "hydra_peer_destroy",
 ]
 
 (ALGO_AUTO, ALGO_RING, ALGO_DIRECT, ALGO_RCCL, ALGO_A2A, ALGO_RING_OLD, ALGO_RING_CHUNKED,
@@ -42,6 +45,10 @@ ALGOS = {"auto": ALGO_AUTO, "ring": ALGO_RING, "direct": ALGO_DIRECT, "rccl": AL
          "ring_chunked": ALGO_RING_CHUNKED, "bcube": ALGO_BCUBE}
 ACC_F32 = 1
 UNIQUE_ID_BYTES = 128
+# peer-access allreduce (hydra_peer_*)
+PEER_HANDLE_BYTES = 128
+PEER_ALGOS = {"peer": 0, "peer2": 1, "peer1": 2}  # AUTO, TWO_SHOT, ONE_SHOT
+PEER_OPT_TIMEOUT_MS, PEER_OPT_BLOCKS, PEER_OPT_ONE_SHOT_MAX = 1, 2, 3
 
 
 class PlanOp(ctypes.Structure):
@@ -118,6 +125,15 @@ def _declare(L) -> None:
                              ctypes.POINTER(sz), ctypes.POINTER(sz)]
     L.hydra_allreduce_simulate.argtypes = [i, i, i, i, i, ctypes.POINTER(vp), sz, sz, sz]
     L.hydra_fold.argtypes = [i, i, i, vp, ctypes.POINTER(vp), i, sz, vp]
+    L.hydra_peer_create.argtypes = [i, i, i, ctypes.POINTER(vp), vp]
+    L.hydra_peer_connect.argtypes = [vp, vp]
+    L.hydra_peer_register.argtypes = [vp, vp, sz, vp]
+    L.hydra_peer_open.argtypes = [vp, vp, sz, vp]
+    L.hydra_peer_close.argtypes = [vp, vp]
+    L.hydra_peer_set_option.argtypes = [vp, i, ctypes.c_longlong]
+    L.hydra_peer_error.argtypes = [vp, ctypes.POINTER(i)]
+    L.hydra_peer_allreduce.argtypes = [vp, i, i, i, i, vp, sz, sz, vp]
+    L.hydra_peer_destroy.argtypes = [vp]
 
 
 def lib():

@@ -1,0 +1,340 @@
+// peer_allreduce.cpp -- host side of the peer-access bucket allreduce (peer_kernels.hip).
+//
+// One process per GPU.  Buckets and the per-rank signal area are shared by hipIpc handles;
+// the handles travel through whatever channel the caller has (the reference's rendezvous store,
+// torch.distributed, a pipe): this file only produces and consumes opaque byte blobs.  After
+// that, hydra_peer_allreduce is ONE kernel launch on the caller's stream -- no host
+// synchronisation, no RCCL, graph-capturable -- whose reads of the peers' blocks travel over
+// xGMI.  Geometry and fold order are the reference ring's (xgmi_plan.h make_geom), so results
+// equal gloo::allreduce RING (allreduce.cc:147-422) bit for bit.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/hydra_hip.h"
+#include "errors.h"
+#include "peer_kernels.h"
+#include "reduce_kernels.h"
+#include "xgmi_plan.h"
+
+using hydra::fail;
+using hydra::ok;
+
+namespace {
+
+constexpr uint64_t kMagic = 0x3152505241445948ull;  // "HYDRAPR1"
+constexpr size_t kIpcBytes = sizeof(hipIpcMemHandle_t);
+static_assert(kIpcBytes <= 64, "hipIpcMemHandle_t larger than the blob slot");
+
+// Blob layout (HYDRA_PEER_HANDLE_BYTES): [0,64) hipIpcMemHandle_t of the allocation base,
+// [64,72) offset of the buffer in it, [72,80) buffer bytes, [80,88) magic, [88,92) rank.
+struct Blob {
+  unsigned char ipc[64];
+  uint64_t offset, bytes, magic;
+  int32_t rank, pad;
+};
+static_assert(sizeof(Blob) <= HYDRA_PEER_HANDLE_BYTES, "blob too large");
+
+struct Mapping {
+  void* base = nullptr;
+  int refs = 0;
+};
+
+}  // namespace
+
+struct hydra_peer {
+  int P = 1, rank = 0, device = 0;
+  hydra::PeerSignals* sig = nullptr;  // own signal area (uncached device memory)
+  hydra::PeerSigPtrs sigs{};          // every rank's, mapped
+  uint32_t* err_host = nullptr;       // host-mapped error word the kernels write
+  uint32_t* err_dev = nullptr;
+  uint32_t epoch = 1;
+  uint64_t timeout_ticks = 20ull * 100000000ull;  // 20 s at 100 MHz
+  int blocks = 0;                                 // 0 = derived from the bucket
+  size_t one_shot_max = 256u << 10;               // AUTO: ONE_SHOT up to this many bytes
+  char* scratch = nullptr;
+  size_t scratch_bytes = 0;
+  struct Reg {
+    char* base;
+    size_t bytes;
+    char* peer[hydra::kPeerMaxRanks];
+    std::string key[hydra::kPeerMaxRanks];
+  };
+  std::vector<Reg> regs;
+  std::map<std::string, Mapping> opened;  // ipc handle bytes -> mapping (one per allocation)
+};
+
+namespace {
+
+int export_blob(hydra_peer* p, void* ptr, size_t bytes, void* out) {
+  void* base = nullptr;
+  size_t size = 0;
+  HIP_TRY(hipMemGetAddressRange(&base, &size, ptr));
+  const char* b = static_cast<const char*>(base);
+  const char* q = static_cast<const char*>(ptr);
+  if (q < b || q + bytes > b + size)
+    return fail(HYDRA_ERR_INVALID, "buffer is not inside one device allocation");
+  hipIpcMemHandle_t h;
+  HIP_TRY(hipIpcGetMemHandle(&h, base));
+  Blob blob{};
+  std::memcpy(blob.ipc, &h, kIpcBytes);
+  blob.offset = (uint64_t)(q - b);
+  blob.bytes = bytes;
+  blob.magic = kMagic;
+  blob.rank = p->rank;
+  std::memset(out, 0, HYDRA_PEER_HANDLE_BYTES);
+  std::memcpy(out, &blob, sizeof(blob));
+  return HYDRA_OK;
+}
+
+int parse_blob(const void* in, int expect_rank, Blob* blob) {
+  std::memcpy(blob, in, sizeof(Blob));
+  if (blob->magic != kMagic) return fail(HYDRA_ERR_INVALID, "not a hydra peer handle");
+  if (blob->rank != expect_rank)
+    return fail(HYDRA_ERR_INVALID, "peer handles out of rank order");
+  return HYDRA_OK;
+}
+
+// Map a peer allocation (cached: several buffers may share one allocation).
+int open_mapping(hydra_peer* p, const Blob& b, std::string* key, char** base) {
+  *key = std::string(reinterpret_cast<const char*>(b.ipc), kIpcBytes);
+  auto it = p->opened.find(*key);
+  if (it == p->opened.end()) {
+    hipIpcMemHandle_t h;
+    std::memcpy(&h, b.ipc, kIpcBytes);
+    void* m = nullptr;
+    HIP_TRY(hipIpcOpenMemHandle(&m, h, hipIpcMemLazyEnablePeerAccess));
+    it = p->opened.emplace(*key, Mapping{m, 0}).first;
+  }
+  it->second.refs++;
+  *base = static_cast<char*>(it->second.base);
+  return HYDRA_OK;
+}
+
+void close_mapping(hydra_peer* p, const std::string& key) {
+  auto it = p->opened.find(key);
+  if (it == p->opened.end()) return;
+  if (--it->second.refs <= 0) {
+    (void)hipIpcCloseMemHandle(it->second.base);
+    p->opened.erase(it);
+  }
+}
+
+const hydra_peer::Reg* find_reg(const hydra_peer* p, const void* buf, size_t bytes) {
+  const char* b = static_cast<const char*>(buf);
+  for (const auto& r : p->regs)
+    if (b >= r.base && b + bytes <= r.base + r.bytes) return &r;
+  return nullptr;
+}
+
+}  // namespace
+
+extern "C" {
+
+int hydra_peer_create(int nranks, int rank, int device, hydra_peer_t* out, void* sig_handle) {
+  if (!out || !sig_handle) return fail(HYDRA_ERR_INVALID, "null argument");
+  *out = nullptr;
+  if (nranks < 1 || nranks > hydra::kPeerMaxRanks || rank < 0 || rank >= nranks)
+    return fail(HYDRA_ERR_INVALID, "bad rank/nranks (peer allreduce: 1..8 ranks)");
+  HIP_TRY(hipSetDevice(device));
+  auto* p = new hydra_peer();
+  p->P = nranks;
+  p->rank = rank;
+  p->device = device;
+  hipError_t e = hipExtMallocWithFlags(reinterpret_cast<void**>(&p->sig),
+                                       sizeof(hydra::PeerSignals), hipDeviceMallocUncached);
+  if (e == hipSuccess) e = hipMemset(p->sig, 0, sizeof(hydra::PeerSignals));
+  if (e == hipSuccess)
+    e = hipHostMalloc(reinterpret_cast<void**>(&p->err_host), sizeof(uint32_t),
+                      hipHostMallocMapped | hipHostMallocCoherent);
+  if (e == hipSuccess) {
+    *p->err_host = 0;
+    e = hipHostGetDevicePointer(reinterpret_cast<void**>(&p->err_dev), p->err_host, 0);
+  }
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  if (e != hipSuccess) {
+    hydra_peer_destroy(p);
+    return hydra::hip_fail(e, "hydra_peer_create");
+  }
+  p->sigs.p[rank] = p->sig;
+  int rc = export_blob(p, p->sig, sizeof(hydra::PeerSignals), sig_handle);
+  if (rc) {
+    hydra_peer_destroy(p);
+    return rc;
+  }
+  *out = p;
+  return ok();
+}
+
+int hydra_peer_connect(hydra_peer_t p, const void* sig_handles) {
+  if (!p || !sig_handles) return fail(HYDRA_ERR_INVALID, "null argument");
+  const char* h = static_cast<const char*>(sig_handles);
+  for (int q = 0; q < p->P; q++) {
+    Blob b;
+    int rc = parse_blob(h + (size_t)q * HYDRA_PEER_HANDLE_BYTES, q, &b);
+    if (rc) return rc;
+    if (q == p->rank || p->sigs.p[q]) continue;
+    std::string key;
+    char* base = nullptr;
+    rc = open_mapping(p, b, &key, &base);
+    if (rc) return rc;
+    p->sigs.p[q] = reinterpret_cast<hydra::PeerSignals*>(base + b.offset);
+  }
+  return ok();
+}
+
+int hydra_peer_register(hydra_peer_t p, void* buf, size_t bytes, void* handle) {
+  if (!p || !buf || !handle) return fail(HYDRA_ERR_INVALID, "null argument");
+  const int rc = export_blob(p, buf, bytes, handle);
+  return rc ? rc : ok();
+}
+
+int hydra_peer_open(hydra_peer_t p, void* buf, size_t bytes, const void* handles) {
+  if (!p || !buf || !handles) return fail(HYDRA_ERR_INVALID, "null argument");
+  const char* h = static_cast<const char*>(handles);
+  hydra_peer::Reg reg{};
+  reg.base = static_cast<char*>(buf);
+  reg.bytes = bytes;
+  reg.peer[p->rank] = reg.base;
+  for (int q = 0; q < p->P; q++) {
+    Blob b;
+    int rc = parse_blob(h + (size_t)q * HYDRA_PEER_HANDLE_BYTES, q, &b);
+    if (!rc && b.bytes != bytes) rc = fail(HYDRA_ERR_INVALID, "ranks registered different sizes");
+    if (!rc && q != p->rank) {
+      char* base = nullptr;
+      rc = open_mapping(p, b, &reg.key[q], &base);
+      if (!rc) reg.peer[q] = base + b.offset;
+    }
+    if (rc) {
+      for (int j = 0; j < q; j++)
+        if (j != p->rank && !reg.key[j].empty()) close_mapping(p, reg.key[j]);
+      return rc;
+    }
+  }
+  p->regs.push_back(reg);
+  return ok();
+}
+
+int hydra_peer_close(hydra_peer_t p, void* buf) {
+  if (!p) return fail(HYDRA_ERR_INVALID, "null peer");
+  for (size_t i = 0; i < p->regs.size(); i++) {
+    if (p->regs[i].base != buf) continue;
+    (void)hipSetDevice(p->device);
+    (void)hipDeviceSynchronize();  // no kernel may still read through the mappings
+    for (int q = 0; q < p->P; q++)
+      if (q != p->rank) close_mapping(p, p->regs[i].key[q]);
+    p->regs.erase(p->regs.begin() + (long)i);
+    return ok();
+  }
+  return fail(HYDRA_ERR_INVALID, "buffer was not opened on this peer group");
+}
+
+int hydra_peer_set_option(hydra_peer_t p, int key, long long value) {
+  if (!p) return fail(HYDRA_ERR_INVALID, "null peer");
+  switch (key) {
+    case HYDRA_PEER_OPT_TIMEOUT_MS:
+      if (value <= 0) return fail(HYDRA_ERR_INVALID, "timeout must be positive");
+      p->timeout_ticks = (uint64_t)value * 100000ull;
+      return ok();
+    case HYDRA_PEER_OPT_BLOCKS:
+      if (value < 0 || value > hydra::kPeerMaxBlocks)
+        return fail(HYDRA_ERR_INVALID, "blocks out of range");
+      p->blocks = (int)value;
+      return ok();
+    case HYDRA_PEER_OPT_ONE_SHOT_MAX:
+      if (value < 0) return fail(HYDRA_ERR_INVALID, "negative size");
+      p->one_shot_max = (size_t)value;
+      return ok();
+  }
+  return fail(HYDRA_ERR_INVALID, "unknown option");
+}
+
+int hydra_peer_error(hydra_peer_t p, int* code) {
+  if (!p || !code) return fail(HYDRA_ERR_INVALID, "null argument");
+  *code = (int)__atomic_load_n(p->err_host, __ATOMIC_ACQUIRE);
+  return ok();
+}
+
+int hydra_peer_allreduce(hydra_peer_t p, int algo, int op, int dtype, int flags, void* buf,
+                         size_t n, size_t max_segment, hydra_stream_t stream) {
+  if (!p) return fail(HYDRA_ERR_INVALID, "null peer");
+  const size_t es = hydra::dtype_size(dtype);
+  if (!es) return fail(HYDRA_ERR_INVALID, "invalid dtype");
+  if (op < HYDRA_SUM || op > HYDRA_MIN) return fail(HYDRA_ERR_INVALID, "invalid op");
+  if (algo < HYDRA_PEER_AUTO || algo > HYDRA_PEER_ONE_SHOT)
+    return fail(HYDRA_ERR_INVALID, "invalid peer algorithm");
+  const bool acc32 = (flags & HYDRA_ACC_F32) != 0;
+  if (acc32 && dtype != HYDRA_BFLOAT16)
+    return fail(HYDRA_ERR_UNSUPPORTED, "HYDRA_ACC_F32 needs a bf16 bucket");
+  if (*p->err_host)
+    return fail(HYDRA_ERR_HIP, "peer group is broken: an earlier barrier timed out (code " +
+                                   std::to_string(*p->err_host) + ")");
+  if (n == 0 || p->P == 1) return ok();  // allreduce.cc:129-133
+  if (!buf) return fail(HYDRA_ERR_INVALID, "null buffer");
+  if (reinterpret_cast<uintptr_t>(buf) % es)
+    return fail(HYDRA_ERR_INVALID, "buffer not aligned to the element size");
+  for (int q = 0; q < p->P; q++)
+    if (!p->sigs.p[q]) return fail(HYDRA_ERR_INVALID, "hydra_peer_connect has not run");
+  const hydra_peer::Reg* reg = find_reg(p, buf, n * es);
+  if (!reg) return fail(HYDRA_ERR_INVALID, "bucket is not inside a buffer opened by hydra_peer_open");
+  if (algo == HYDRA_PEER_AUTO)
+    algo = n * es <= p->one_shot_max ? HYDRA_PEER_ONE_SHOT : HYDRA_PEER_TWO_SHOT;
+
+  const hydra::PlanGeom g =
+      hydra::make_geom(p->P, n, es, max_segment ? max_segment : (1u << 20), 0);
+  hydra::PeerLaunch A{};
+  const size_t off = static_cast<const char*>(buf) - reg->base;
+  for (int q = 0; q < p->P; q++) {
+    A.x[q] = reg->peer[q] + off;
+    A.sig.p[q] = p->sigs.p[q];
+    A.lo[q] = g.block_begin(q) / es;
+  }
+  A.lo[p->P] = n;
+  A.err = p->err_dev;
+  A.timeout_ticks = p->timeout_ticks;
+  A.epoch = p->epoch;
+  A.P = p->P;
+  A.rank = p->rank;
+  // grid: one workgroup per slab of the largest block (two-shot) / of the bucket (one-shot),
+  // at most 512 (2 per CU); identical on every rank since it depends on (P, n, dtype) only
+  const size_t slab = hydra::kPeerSlabBytes;
+  size_t work = algo == HYDRA_PEER_ONE_SHOT ? 0 : (g.max_block() + slab - 1) / slab;
+  if (algo == HYDRA_PEER_ONE_SHOT)
+    for (int q = 0; q < p->P; q++) work += (g.block_bytes(q) + slab - 1) / slab;
+  size_t grid = p->blocks > 0 ? (size_t)p->blocks : std::min<size_t>(std::max<size_t>(work, 1), 512);
+  if (algo == HYDRA_PEER_ONE_SHOT) {
+    if (p->scratch_bytes < n * es) {
+      HIP_TRY(hipDeviceSynchronize());  // first call at a new size: outside any capture
+      if (p->scratch) HIP_TRY(hipFree(p->scratch));
+      p->scratch = nullptr;
+      p->scratch_bytes = 0;
+      HIP_TRY(hipMalloc(reinterpret_cast<void**>(&p->scratch), n * es));
+      p->scratch_bytes = n * es;
+    }
+    A.scratch = p->scratch;
+  }
+  const hipError_t e = hydra::launch_peer(
+      algo == HYDRA_PEER_ONE_SHOT ? hydra::kPeerOneShot : hydra::kPeerTwoShot, op, dtype, acc32,
+      A, (unsigned)grid, static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return hydra::hip_fail(e, "peer allreduce kernel launch");
+  p->epoch += algo == HYDRA_PEER_ONE_SHOT ? 2 : 3;
+  return ok();
+}
+
+int hydra_peer_destroy(hydra_peer_t p) {
+  if (!p) return ok();
+  (void)hipSetDevice(p->device);
+  (void)hipDeviceSynchronize();
+  for (auto& kv : p->opened) (void)hipIpcCloseMemHandle(kv.second.base);
+  p->opened.clear();
+  if (p->scratch) (void)hipFree(p->scratch);
+  if (p->sig) (void)hipFree(p->sig);
+  if (p->err_host) (void)hipHostFree(p->err_host);
+  delete p;
+  return ok();
+}
+
+}  // extern "C"

@@ -1,0 +1,298 @@
+// peer_kernels.hip -- gfx950 peer-access bucket allreduce: the reduction reads the peers'
+// buckets straight over xGMI (IPC-mapped HBM), so the sum IS the hop -- no RCCL proxy, no
+// scratch landing zone, one kernel per allreduce.
+//
+// Ownership and fold order are the reference ring's (gloo/gloo/allreduce.cc:199-221, :253-258,
+// :301-305): owner block q = segments [qS, (q+1)S) of the bucket, reduced as
+// x_q + (x_{q+1} + (... + (x_{q-2} + x_{q-1}))), so every result is bit-identical to RING /
+// DIRECT (xgmi_plan.h) and to the reference.
+//
+//   TWO_SHOT  phase 1: rank r folds ITS block r, pulling slab k of block r from all P buckets
+//             (P-1 of them remote) and writing the result in place; phase 2: rank r pulls the
+//             finished slabs of every other block q from their owners into its own bucket.
+//             Link bytes per rank 2(P-1)/P * n * E, the same as the ring, spread over P-1 links.
+//   ONE_SHOT  every rank folds the WHOLE bucket (each block in its owner's order) into local
+//             scratch, then copies it back; (P-1) * n * E link bytes, 2 barriers -- for small
+//             buckets, where the ring's 2(P-1) latencies dominate.
+//
+// Work unit: a slab of 64 KiB of one owner block.  Slab k of block q is always handled by
+// workgroup k mod G (G identical on every rank), so workgroup b on rank r only ever depends on
+// workgroup b's / the slab's producer on other ranks:
+//   start barrier (per workgroup, peer_sync.h): every rank's inputs are ready;
+//   phase 1 -> 2: each workgroup publishes "my phase-1 slabs are final" (flag[b][r] = e+1 on
+//   every rank); a phase-2 slab (q, k) waits for flag[k mod G][q] only -- no global barrier;
+//   end barrier: nobody leaves while a peer may still read its bucket.
+// Every wait is bounded (timeout -> host-mapped error word), so the grid always drains.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "errors.h"
+#include "peer_kernels.h"
+#include "peer_sync.h"
+#include "reduce_kernels.h"
+#include "reduce_ops.h"
+
+namespace hydra {
+namespace {
+
+constexpr int kPU = 2;  // 16-B vectors per lane per source in flight
+
+// dst = fold of nsrc 16-B sources in the reference order (nsrc == 1: a raw copy)
+template <typename E, int OP, bool ACC32>
+__device__ __forceinline__ u32x4 fold_regs(const u32x4 (&v)[kPeerMaxRanks], int nsrc) {
+  if constexpr (ACC32) {
+    float a[8];
+#pragma unroll
+    for (int j = kPeerMaxRanks - 1; j >= 0; j--) {
+      if (j < nsrc) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const float lo = bitsf(v[j][k] << 16), hi = bitsf(v[j][k] & 0xffff0000u);
+          if (j == nsrc - 1) {
+            a[2 * k] = lo;
+            a[2 * k + 1] = hi;
+          } else {
+            a[2 * k] = fop<OP>(lo, a[2 * k]);
+            a[2 * k + 1] = fop<OP>(hi, a[2 * k + 1]);
+          }
+        }
+      }
+    }
+    u32x4 o;
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+      o[k] = (uint32_t)f2bf(a[2 * k]) | ((uint32_t)f2bf(a[2 * k + 1]) << 16);
+    return o;
+  } else {
+    u32x4 acc = v[0];
+#pragma unroll
+    for (int j = kPeerMaxRanks - 1; j >= 0; j--) {
+      if (j < nsrc) {
+        if (j == nsrc - 1) acc = v[j];
+        else acc = vapply<E, OP>(v[j], acc, v[j]);  // c = local + received, in place on local
+      }
+    }
+    return acc;
+  }
+}
+
+struct PeerSrcs {
+  const char* p[kPeerMaxRanks];
+};
+
+// one element, same order as fold_regs (static source indices: no scratch spills)
+template <typename E, int OP, bool ACC32>
+__device__ __forceinline__ E fold_one(const PeerSrcs& S, int nsrc, size_t i) {
+  if constexpr (ACC32) {
+    float a = 0.f;
+#pragma unroll
+    for (int j = kPeerMaxRanks - 1; j >= 0; j--) {
+      if (j < nsrc) {
+        const float x = bf2f(reinterpret_cast<const uint16_t*>(S.p[j])[i]);
+        a = (j == nsrc - 1) ? x : fop<OP>(x, a);
+      }
+    }
+    E r;
+    const uint16_t h = f2bf(a);
+    __builtin_memcpy(&r, &h, 2);
+    return r;
+  } else {
+    E acc = reinterpret_cast<const E*>(S.p[0])[i];
+#pragma unroll
+    for (int j = kPeerMaxRanks - 1; j >= 0; j--) {
+      if (j < nsrc) {
+        const E x = reinterpret_cast<const E*>(S.p[j])[i];
+        acc = (j == nsrc - 1) ? x : Elem<E, OP>::apply(x, acc, x);
+      }
+    }
+    return acc;
+  }
+}
+
+// One workgroup folds `count` elements: dst[i] = fold(S.p[0][i], ..., S.p[nsrc-1][i]).
+// Aligned on dst (16 B); sources may sit at any element alignment (gfx950 unaligned mode).
+template <typename E, int OP, bool ACC32>
+__device__ __forceinline__ void slab_fold(char* dst, const PeerSrcs& S, int nsrc, size_t count) {
+  constexpr int N = Vec<E>::N;
+  const int t = threadIdx.x;
+  size_t head = ((16 - (reinterpret_cast<uintptr_t>(dst) & 15)) & 15) / sizeof(E);
+  if (head > count) head = count;
+  const size_t nvec = (count - head) / N;
+  const size_t tail = count - head - nvec * N;
+  E* de = reinterpret_cast<E*>(dst);
+  if ((size_t)t < head) de[t] = fold_one<E, OP, ACC32>(S, nsrc, t);
+  if ((size_t)t < tail) {
+    const size_t i = head + nvec * N + t;
+    de[i] = fold_one<E, OP, ACC32>(S, nsrc, i);
+  }
+  const size_t base = head * sizeof(E);
+  for (size_t v0 = 0; v0 < nvec; v0 += (size_t)kBlock * kPU) {
+    u32x4 r[kPU][kPeerMaxRanks];
+#pragma unroll
+    for (int u = 0; u < kPU; u++) {
+      const size_t v = v0 + (size_t)u * kBlock + t;
+      if (v < nvec) {
+#pragma unroll
+        for (int j = 0; j < kPeerMaxRanks; j++)
+          if (j < nsrc) r[u][j] = ld_u(S.p[j] + base + v * 16);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kPU; u++) {
+      const size_t v = v0 + (size_t)u * kBlock + t;
+      if (v < nvec) st_a(dst + base + v * 16, fold_regs<E, OP, ACC32>(r[u], nsrc));
+    }
+  }
+}
+
+// Wait until rank q's workgroup `wg` has published epoch `e` into OUR signal area.
+__device__ __forceinline__ bool wait_flag(const PeerLaunch& A, int wg, int q, uint32_t e) {
+  int ok = 1;
+  if (threadIdx.x == 0) {
+    uint32_t* f = &A.sig.p[A.rank]->flag[wg][q];
+    const uint64_t t0 = peer_clock();
+    while ((int32_t)(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - e) < 0) {
+      __builtin_amdgcn_s_sleep(1);
+      if (peer_clock() - t0 > A.timeout_ticks) {
+        __hip_atomic_store(A.err, 4u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        ok = 0;
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  }
+  return __syncthreads_and(ok) != 0;
+}
+
+// Publish "this workgroup reached epoch e" to every rank without waiting.
+__device__ __forceinline__ void signal_all(const PeerLaunch& A, uint32_t e) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if ((int)threadIdx.x < A.P)
+    __hip_atomic_store(&A.sig.p[threadIdx.x]->flag[blockIdx.x][A.rank], e, __ATOMIC_RELEASE,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+template <typename E, int OP, bool ACC32>
+__global__ __launch_bounds__(kBlock) void k_peer_two_shot(PeerLaunch A) {
+  constexpr size_t SL = kPeerSlabBytes / sizeof(E);
+  const int P = A.P, r = A.rank;
+  const uint32_t G = gridDim.x;
+  if (!peer_barrier(A.sig, P, r, A.epoch, A.timeout_ticks, A.err, 1)) return;
+  PeerSrcs S;
+  // phase 1: own block, all P sources, in place
+  {
+    const size_t lo = A.lo[r], hi = A.lo[r + 1];
+    for (size_t k = blockIdx.x; lo + k * SL < hi; k += G) {
+      const size_t s = lo + k * SL;
+#pragma unroll
+      for (int j = 0; j < kPeerMaxRanks; j++)
+        if (j < P) S.p[j] = A.x[(r + j) % P] + s * sizeof(E);
+      slab_fold<E, OP, ACC32>(A.x[r] + s * sizeof(E), S, P, hi - s < SL ? hi - s : SL);
+    }
+  }
+  signal_all(A, A.epoch + 1);
+  // phase 2: every other block from its owner; slabs interleaved over the peers so all P-1
+  // links stream at once
+  size_t nslab = 0;
+  for (int d = 1; d < P; d++) {
+    const int q = (r + d) % P;
+    const size_t sl = (A.lo[q + 1] - A.lo[q] + SL - 1) / SL;
+    nslab = sl > nslab ? sl : nslab;
+  }
+  for (size_t w = blockIdx.x; w < nslab * (size_t)(P - 1); w += G) {
+    const size_t k = w / (size_t)(P - 1);
+    const int q = (r + 1 + (int)(w % (size_t)(P - 1))) % P;
+    const size_t lo = A.lo[q], hi = A.lo[q + 1];
+    if (lo + k * SL >= hi) continue;  // block-uniform
+    if (!wait_flag(A, (int)(k % G), q, A.epoch + 1)) return;
+    const size_t s = lo + k * SL;
+    S.p[0] = A.x[q] + s * sizeof(E);
+    slab_fold<E, OP, false>(A.x[r] + s * sizeof(E), S, 1, hi - s < SL ? hi - s : SL);
+  }
+  peer_barrier(A.sig, P, r, A.epoch + 2, A.timeout_ticks, A.err, 3);
+}
+
+template <typename E, int OP, bool ACC32>
+__global__ __launch_bounds__(kBlock) void k_peer_one_shot(PeerLaunch A) {
+  constexpr size_t SL = kPeerSlabBytes / sizeof(E);
+  const int P = A.P, r = A.rank;
+  const uint32_t G = gridDim.x;
+  if (!peer_barrier(A.sig, P, r, A.epoch, A.timeout_ticks, A.err, 1)) return;
+  PeerSrcs S;
+  // slab list over all owner blocks: (q, k) enumerated block by block
+  size_t w = 0;
+  for (int q = 0; q < P; q++) {
+    const size_t lo = A.lo[q], hi = A.lo[q + 1];
+    const size_t nsl = (hi - lo + SL - 1) / SL;
+    for (size_t k = 0; k < nsl; k++, w++) {
+      if (w % G != blockIdx.x) continue;
+      const size_t s = lo + k * SL;
+#pragma unroll
+      for (int j = 0; j < kPeerMaxRanks; j++)
+        if (j < P) S.p[j] = A.x[(q + j) % P] + s * sizeof(E);
+      slab_fold<E, OP, ACC32>(A.scratch + s * sizeof(E), S, P, hi - s < SL ? hi - s : SL);
+    }
+  }
+  // every rank's workgroup b has read its slabs of every bucket -> safe to overwrite ours
+  if (!peer_barrier(A.sig, P, r, A.epoch + 1, A.timeout_ticks, A.err, 2)) return;
+  w = 0;
+  for (int q = 0; q < P; q++) {
+    const size_t lo = A.lo[q], hi = A.lo[q + 1];
+    const size_t nsl = (hi - lo + SL - 1) / SL;
+    for (size_t k = 0; k < nsl; k++, w++) {
+      if (w % G != blockIdx.x) continue;
+      const size_t s = lo + k * SL;
+      S.p[0] = A.scratch + s * sizeof(E);
+      slab_fold<E, OP, false>(A.x[r] + s * sizeof(E), S, 1, hi - s < SL ? hi - s : SL);
+    }
+  }
+}
+
+template <typename E, int OP, bool ACC32>
+hipError_t launch_t(int algo, const PeerLaunch& A, unsigned grid, hipStream_t s) {
+  if (algo == kPeerOneShot)
+    hipLaunchKernelGGL((k_peer_one_shot<E, OP, ACC32>), dim3(grid), dim3(kBlock), 0, s, A);
+  else
+    hipLaunchKernelGGL((k_peer_two_shot<E, OP, ACC32>), dim3(grid), dim3(kBlock), 0, s, A);
+  return hipGetLastError();
+}
+
+template <int OP>
+hipError_t dispatch(int algo, int dtype, bool acc32, const PeerLaunch& A, unsigned grid,
+                    hipStream_t s) {
+  if (acc32) {
+    if (dtype != kBF16) return hipErrorInvalidValue;
+    return launch_t<bf16_t, OP, true>(algo, A, grid, s);
+  }
+  switch (dtype) {
+    case kI8: return launch_t<int8_t, OP, false>(algo, A, grid, s);
+    case kU8: return launch_t<uint8_t, OP, false>(algo, A, grid, s);
+    case kI32: return launch_t<int32_t, OP, false>(algo, A, grid, s);
+    case kU32: return launch_t<uint32_t, OP, false>(algo, A, grid, s);
+    case kI64: return launch_t<int64_t, OP, false>(algo, A, grid, s);
+    case kU64: return launch_t<uint64_t, OP, false>(algo, A, grid, s);
+    case kF32: return launch_t<float, OP, false>(algo, A, grid, s);
+    case kF64: return launch_t<double, OP, false>(algo, A, grid, s);
+    case kF16: return launch_t<f16_t, OP, false>(algo, A, grid, s);
+    case kBF16: return launch_t<bf16_t, OP, false>(algo, A, grid, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+}  // namespace
+
+hipError_t launch_peer(int algo, int op, int dtype, bool acc32, const PeerLaunch& A,
+                       unsigned grid, hipStream_t s) {
+  if (A.P < 1 || A.P > kPeerMaxRanks || grid < 1 || grid > (unsigned)kPeerMaxBlocks)
+    return hipErrorInvalidValue;
+  switch (op) {
+    case kSum: return dispatch<kSum>(algo, dtype, acc32, A, grid, s);
+    case kProduct: return dispatch<kProduct>(algo, dtype, acc32, A, grid, s);
+    case kMax: return dispatch<kMax>(algo, dtype, acc32, A, grid, s);
+    case kMin: return dispatch<kMin>(algo, dtype, acc32, A, grid, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+}  // namespace hydra

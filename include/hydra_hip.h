@@ -224,6 +224,45 @@ int hydra_plan(int algo, int P, int rank, size_t n, size_t esize, size_t max_seg
 int hydra_allreduce_simulate(int algo, int op, int dtype, int flags, int P, void** bufs,
                              size_t n, size_t max_segment, size_t chunk_bytes);
 
+/* ---- peer-access bucket allreduce over xGMI (no RCCL) --------------------------------------
+ * The MI355X-first form of gloo::allreduce RING (allreduce.cc:147-422) for device-resident
+ * buckets on one fully connected node: the peers' buckets are mapped into every rank by hipIpc
+ * handles and ONE kernel per allreduce reads the other ranks' data over xGMI, folding it in the
+ * reference's order (owner block q = x_q + (x_{q+1} + (... + x_{q-1})), blocks from
+ * allreduce.cc:199-221) -- so results are bit-identical to RING/DIRECT and to the reference.
+ *   HYDRA_PEER_TWO_SHOT  each rank folds its own block pulling from all P buckets (in place),
+ *                        then pulls the other finished blocks (2(P-1)/P * n * E link bytes)
+ *   HYDRA_PEER_ONE_SHOT  each rank folds the whole bucket into scratch, then copies it back
+ *                        ((P-1) * n * E link bytes, 2 barriers: small buckets)
+ *   HYDRA_PEER_AUTO      ONE_SHOT up to HYDRA_PEER_OPT_ONE_SHOT_MAX bytes (256 KiB), else TWO_SHOT
+ * Setup (every rank, same order; the byte blobs travel over any channel the caller has, e.g.
+ * the rendezvous store): hydra_peer_create -> exchange sig handles -> hydra_peer_connect; for
+ * each bucket: hydra_peer_register -> exchange -> hydra_peer_open.  Every rank must then issue
+ * the same sequence of hydra_peer_allreduce calls (like any collective).  A peer that never
+ * arrives ends the kernel after the timeout (default 20 s) and leaves an error code readable
+ * with hydra_peer_error; later calls on the group fail with HYDRA_ERR_HIP. 1 <= nranks <= 8. */
+#define HYDRA_PEER_HANDLE_BYTES 128
+typedef enum { HYDRA_PEER_AUTO = 0, HYDRA_PEER_TWO_SHOT = 1, HYDRA_PEER_ONE_SHOT = 2 } hydra_peer_algo_t;
+typedef enum {
+  HYDRA_PEER_OPT_TIMEOUT_MS = 1,  /* barrier timeout (default 20000) */
+  HYDRA_PEER_OPT_BLOCKS = 2,      /* workgroups per launch (0 = derived from the bucket, <= 1024) */
+  HYDRA_PEER_OPT_ONE_SHOT_MAX = 3 /* AUTO threshold in bytes */
+} hydra_peer_opt_t;
+typedef struct hydra_peer* hydra_peer_t;
+/* sig_handle: HYDRA_PEER_HANDLE_BYTES out, to be gathered in rank order for hydra_peer_connect */
+int hydra_peer_create(int nranks, int rank, int device, hydra_peer_t* out, void* sig_handle);
+int hydra_peer_connect(hydra_peer_t peer, const void* sig_handles /* nranks * HANDLE_BYTES */);
+/* buf: device memory (any sub-range of one allocation, e.g. a torch tensor) */
+int hydra_peer_register(hydra_peer_t peer, void* buf, size_t bytes, void* handle);
+int hydra_peer_open(hydra_peer_t peer, void* buf, size_t bytes, const void* handles);
+int hydra_peer_close(hydra_peer_t peer, void* buf);
+int hydra_peer_set_option(hydra_peer_t peer, int key, long long value);
+int hydra_peer_error(hydra_peer_t peer, int* code); /* 0 = healthy */
+/* buf must lie inside a buffer opened with hydra_peer_open, at the same offset on every rank */
+int hydra_peer_allreduce(hydra_peer_t peer, int algo, int op, int dtype, int flags, void* buf,
+                         size_t n, size_t max_segment, hydra_stream_t stream);
+int hydra_peer_destroy(hydra_peer_t peer);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,106 @@
+"""One rank of the peer-access allreduce test (tests/test_gpu_peer.py).
+
+Launched by the test as a child process per rank, all ranks on cuda:0 of the one-GPU box (IPC
+between processes on one device exercises the same handles, barriers and fences as xGMI peers).
+Rendezvous over gloo on 127.0.0.1 (handle exchange only).  Runs the case list in order, writes
+every rank's result bytes to <out>/rank<r>.npz; the parent compares them with the oracle.
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def inputs(case, P, r):
+    from hydra_amd import synth
+
+    n, kind = case["n"], case["data"]
+    if kind == "stress_f32":
+        return synth.stress_f32(P, r, n)
+    if kind == "int32":
+        return synth.int32_bucket(P, r, n)
+    if kind == "f16":
+        rng = np.random.default_rng(1000 + r)
+        v = rng.uniform(-4, 4, n).astype(np.float16)
+        return v.view(np.uint16).copy()
+    if kind == "bf16":
+        return synth.bf16_bits(synth.uniform_f32(n, 100 + r) * 4)
+    raise ValueError(kind)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rank", type=int, required=True)
+    ap.add_argument("--world", type=int, required=True)
+    ap.add_argument("--port", type=int, required=True)
+    ap.add_argument("--out", required=True)
+    ap.add_argument("--cases", required=True)
+    ap.add_argument("--blocks", type=int, default=64)
+    a = ap.parse_args()
+    import torch
+    import torch.distributed as dist
+
+    from hydra_amd import _lib
+    from hydra_amd.peer import PeerComm
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(a.port)
+    dist.init_process_group("gloo", rank=a.rank, world_size=a.world)
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    with open(a.cases) as f:
+        cases = json.load(f)
+    peer = PeerComm(a.rank, a.world, 0, timeout_ms=30000, blocks=a.blocks)
+    results, status = {}, {}
+    try:
+        # one large registered arena; buckets are views at a per-case element offset (same on
+        # every rank), so sub-allocation offsets and 16-B misalignment are exercised
+        arena = torch.zeros(64 << 20, dtype=torch.uint8, device=dev)
+        peer.register(arena)
+        for c in cases:
+            name = c["name"]
+            if c.get("skip_rank") == a.rank:  # timeout case: this rank never arrives
+                dist.barrier()
+                dist.barrier()
+                continue
+            if c.get("timeout_ms"):
+                peer.set_option(_lib.PEER_OPT_TIMEOUT_MS, c["timeout_ms"])
+            x = inputs(c, a.world, a.rank)
+            nbytes = x.nbytes
+            off = c.get("offset_bytes", 0)
+            view = arena[off:off + nbytes]
+            view.copy_(torch.from_numpy(x.view(np.uint8)))
+            code = c["dtype"]
+            for _ in range(c.get("repeat", 1)):
+                view.copy_(torch.from_numpy(x.view(np.uint8)))
+                peer.allreduce_(view, algo=c["algo"], op=c.get("op", "sum"), dtype_code=code,
+                                flags=c.get("flags", 0), max_segment=c.get("ms", 0))
+            torch.cuda.synchronize(dev)
+            if c.get("skip_rank") is not None:
+                status[name] = peer.error()
+                try:
+                    peer.allreduce_(view, algo=c["algo"], dtype_code=code)
+                    status[name + "/next"] = "accepted"
+                except _lib.HydraError as e:
+                    status[name + "/next"] = str(e)
+                dist.barrier()
+                dist.barrier()
+                continue
+            results[name] = view.cpu().numpy().copy()
+            status[name] = peer.error()
+        dist.barrier()
+    finally:
+        peer.close()
+    np.savez(os.path.join(a.out, f"rank{a.rank}.npz"), **results)
+    with open(os.path.join(a.out, f"status{a.rank}.json"), "w") as f:
+        json.dump(status, f)
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

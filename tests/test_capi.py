@@ -86,3 +86,19 @@ def test_split_elements_shared_with_host_runtime():
             for n in (0, 1, 6144, 6145, 65535, 65536, 65537, 131072, 524288, 524289, 828344,
                       1048577, 1500000, 2097152, 4000001, 16777217, 67108864, 67108865):
                 assert ring.split_elements(table, P, n) == host.calculate_elements(table, P, n)
+
+
+def test_peer_args_rejected_before_hip():
+    """hydra_peer_*: bad arguments fail with HYDRA_ERR_INVALID before any HIP call (no GPU)."""
+    import ctypes
+
+    L = _lib.lib()
+    h = ctypes.c_void_p()
+    sig = ctypes.create_string_buffer(_lib.PEER_HANDLE_BYTES)
+    assert L.hydra_peer_create(9, 0, 0, ctypes.byref(h), sig) == 1  # > 8 ranks
+    assert L.hydra_peer_create(2, 2, 0, ctypes.byref(h), sig) == 1  # rank out of range
+    assert L.hydra_peer_create(2, 0, 0, None, sig) == 1
+    assert L.hydra_peer_allreduce(None, 1, 0, _lib.FLOAT32, 0, None, 4, 0, None) == 1
+    assert L.hydra_peer_connect(None, sig) == 1
+    assert L.hydra_peer_set_option(None, 1, 5) == 1
+    assert L.hydra_peer_destroy(None) == 0

@@ -1,0 +1,142 @@
+"""Peer-access allreduce (hydra_peer_*): P real processes, each mapping the others' buckets by
+hipIpc handles, one kernel per allreduce reading the peers' data directly.  On the one-GPU box
+all ranks share cuda:0 (IPC across processes on one device: the same handles, signal flags,
+system-scope fences and per-workgroup barriers the xGMI node uses).  Bar: bit-exact vs the
+reference ring (oracle) for fp32 (fold-order-sensitive inputs), int32 and float16; bf16 with
+fp32 accumulation within one bf16 rounding of the fp64 sum, identical on every rank."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from hydra_amd import _lib, synth
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+WORKER = os.path.join(ROOT, "tests", "peer_worker.py")
+
+
+def free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def run_ranks(tmp_path, P, cases, blocks=64, timeout=150):
+    cpath = tmp_path / "cases.json"
+    cpath.write_text(json.dumps(cases))
+    port = free_port()
+    procs = []
+    for r in range(P):
+        cmd = [sys.executable, "-u", WORKER, "--rank", str(r), "--world", str(P), "--port",
+               str(port), "--out", str(tmp_path), "--cases", str(cpath), "--blocks", str(blocks)]
+        procs.append(subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                                      start_new_session=True))
+    outs = []
+    try:
+        for p in procs:
+            out, _ = p.communicate(timeout=timeout)
+            outs.append(out.decode(errors="replace"))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                os.killpg(p.pid, 9)
+                p.wait()
+    for r, (p, o) in enumerate(zip(procs, outs)):
+        assert p.returncode == 0, f"rank {r} rc={p.returncode}\n{o[-3000:]}"
+    res = [np.load(tmp_path / f"rank{r}.npz") for r in range(P)]
+    st = [json.loads((tmp_path / f"status{r}.json").read_text()) for r in range(P)]
+    return res, st
+
+
+def f16_inputs(P, n):
+    rng = [np.random.default_rng(1000 + r) for r in range(P)]
+    return [g.uniform(-4, 4, n).astype(np.float16).view(np.uint16).copy() for g in rng]
+
+
+def expected(O, c, P):
+    n = c["n"]
+    if c["data"] == "stress_f32":
+        xs = [synth.stress_f32(P, r, n) for r in range(P)]
+        return O.ring_result(xs, c.get("ms") or (1 << 20), kind=c.get("op", "sum")).view(np.uint8)
+    if c["data"] == "int32":
+        xs = [synth.int32_bucket(P, r, n) for r in range(P)]
+        return O.ring_result(xs, c.get("ms") or (1 << 20), kind=c.get("op", "sum")).view(np.uint8)
+    if c["data"] == "f16":
+        return O.ring_result(f16_inputs(P, n), c.get("ms") or (1 << 20),
+                             dtype_code=_lib.FLOAT16).view(np.uint8)
+    raise ValueError(c["data"])
+
+
+def cases_for(P):
+    F32, I32, F16, BF16 = _lib.FLOAT32, _lib.INT32, _lib.FLOAT16, _lib.BFLOAT16
+    cs = []
+    for algo in ("peer2", "peer1"):
+        for n, ms, off in ((1, 0, 0), (7, 0, 4), (1000, 128, 0), (4099, 128, 12),
+                           (262145, 0, 0), (1 << 20, 0, 4), (3000001, 0, 0)):
+            if algo == "peer1" and n > (1 << 20):
+                continue
+            cs.append(dict(name=f"{algo}_f32_{n}_{ms}_{off}", algo=algo, data="stress_f32",
+                           dtype=F32, n=n, ms=ms, offset_bytes=off))
+    cs.append(dict(name="peer2_i32", algo="peer2", data="int32", dtype=I32, n=100003, ms=4096,
+                   offset_bytes=8))
+    cs.append(dict(name="peer1_i32", algo="peer1", data="int32", dtype=I32, n=100003, ms=4096))
+    cs.append(dict(name="peer2_f16", algo="peer2", data="f16", dtype=F16, n=20011, ms=1024,
+                   offset_bytes=2))
+    cs.append(dict(name="peer1_f16", algo="peer1", data="f16", dtype=F16, n=20011, ms=1024))
+    for op in ("max", "min", "product"):
+        cs.append(dict(name=f"peer2_{op}", algo="peer2", data="stress_f32", dtype=F32, n=70001,
+                       ms=4096, op=op))
+    cs.append(dict(name="auto_small", algo="peer", data="stress_f32", dtype=F32, n=5000))
+    cs.append(dict(name="repeat", algo="peer2", data="stress_f32", dtype=F32, n=262147,
+                   repeat=25))
+    cs.append(dict(name="bf16_acc32", algo="peer2", data="bf16", dtype=BF16, n=1 << 20,
+                   flags=_lib.ACC_F32))
+    return cs
+
+
+@pytest.mark.parametrize("P", [2, 3, 4])
+def test_peer_allreduce_bit_exact(gpu, O, tmp_path, P):
+    cases = cases_for(P)
+    res, st = run_ranks(tmp_path, P, cases)
+    for c in cases:
+        name = c["name"]
+        assert all(s[name] == 0 for s in st), (name, st)
+        if c["data"] == "bf16":
+            n = c["n"]
+            xs = [synth.bf16_bits(synth.uniform_f32(n, 100 + r) * 4) for r in range(P)]
+            vals = np.stack([synth.bf16_to_f32(x).astype(np.float64) for x in xs])
+            exact = vals.sum(0)
+            tol = np.abs(exact) * 2.0 ** -8 + P * 2.0 ** -24 * np.abs(vals).sum(0) + 1e-30
+            got = synth.bf16_to_f32(res[0][name].view(np.uint16)).astype(np.float64)
+            assert np.all(np.abs(got - exact) <= tol), name
+            assert all(np.array_equal(r[name], res[0][name]) for r in res), name
+            continue
+        exp = expected(O, c, P)
+        for r in range(P):
+            assert np.array_equal(res[r][name], exp), (name, r)
+
+
+def test_peer_default_grid(gpu, O, tmp_path):
+    """The derived grid (one workgroup per 64 KiB slab, up to 512) at P = 2."""
+    P = 2
+    cases = [dict(name="big", algo="peer2", data="stress_f32", dtype=_lib.FLOAT32,
+                  n=(8 << 20) + 5, ms=0, offset_bytes=4)]
+    res, st = run_ranks(tmp_path, P, cases, blocks=0)
+    exp = expected(O, cases[0], P)
+    assert all(np.array_equal(r["big"], exp) for r in res)
+
+
+def test_peer_timeout_reports_and_poisons(gpu, tmp_path):
+    """A rank that never arrives: the kernel leaves after the timeout (every wave drains), the
+    error word is set, and the group refuses further allreduces."""
+    cases = [dict(name="lonely", algo="peer2", data="stress_f32", dtype=_lib.FLOAT32, n=4096,
+                  skip_rank=1, timeout_ms=300)]
+    _, st = run_ranks(tmp_path, 2, cases)
+    assert st[0]["lonely"] != 0
+    assert "timed out" in st[0]["lonely/next"]
