@@ -9,6 +9,7 @@
 // equal gloo::allreduce RING (allreduce.cc:147-422) bit for bit.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstring>
 #include <map>
 #include <string>
@@ -289,22 +290,29 @@ int hydra_peer_allreduce(hydra_peer_t p, int algo, int op, int dtype, int flags,
   const size_t off = static_cast<const char*>(buf) - reg->base;
   for (int q = 0; q < p->P; q++) {
     A.x[q] = reg->peer[q] + off;
-    A.sig.p[q] = p->sigs.p[q];
+    A.sync.sig.p[q] = p->sigs.p[q];
     A.lo[q] = g.block_begin(q) / es;
   }
   A.lo[p->P] = n;
-  A.err = p->err_dev;
-  A.timeout_ticks = p->timeout_ticks;
+  A.sync.err = p->err_dev;
+  A.sync.timeout_ticks = p->timeout_ticks;
+  A.sync.P = p->P;
+  A.sync.rank = p->rank;
   A.epoch = p->epoch;
-  A.P = p->P;
-  A.rank = p->rank;
-  // grid: one workgroup per slab of the largest block (two-shot) / of the bucket (one-shot),
-  // at most 512 (2 per CU); identical on every rank since it depends on (P, n, dtype) only
-  const size_t slab = hydra::kPeerSlabBytes;
-  size_t work = algo == HYDRA_PEER_ONE_SHOT ? 0 : (g.max_block() + slab - 1) / slab;
+  // work unit: 64 KiB slabs for big buckets; smaller (down to 4 KiB) so that a small bucket
+  // still spreads over ~256 workgroups.  Depends on (P, n, dtype) only: identical on all ranks.
+  const size_t span = algo == HYDRA_PEER_ONE_SHOT ? n * es : g.max_block();
+  size_t slab = hydra::kPeerSlabBytes;
+  while (slab > hydra::kPeerMinSlabBytes && span / slab < 256) slab >>= 1;
+  A.slab_bytes = slab;
+  size_t work = 0;  // slabs of the largest block (two-shot) / of the bucket (one-shot)
   if (algo == HYDRA_PEER_ONE_SHOT)
     for (int q = 0; q < p->P; q++) work += (g.block_bytes(q) + slab - 1) / slab;
-  size_t grid = p->blocks > 0 ? (size_t)p->blocks : std::min<size_t>(std::max<size_t>(work, 1), 512);
+  else
+    work = (g.max_block() + slab - 1) / slab;
+  // grid: one workgroup per slab, at most 512 (2 per CU: every workgroup resident)
+  const size_t grid =
+      p->blocks > 0 ? (size_t)p->blocks : std::min<size_t>(std::max<size_t>(work, 1), 512);
   if (algo == HYDRA_PEER_ONE_SHOT) {
     if (p->scratch_bytes < n * es) {
       HIP_TRY(hipDeviceSynchronize());  // first call at a new size: outside any capture

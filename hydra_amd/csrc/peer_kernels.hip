@@ -15,14 +15,13 @@
 //             scratch, then copies it back; (P-1) * n * E link bytes, 2 barriers -- for small
 //             buckets, where the ring's 2(P-1) latencies dominate.
 //
-// Work unit: a slab of 64 KiB of one owner block.  Slab k of block q is always handled by
-// workgroup k mod G (G identical on every rank), so workgroup b on rank r only ever depends on
-// workgroup b's / the slab's producer on other ranks:
-//   start barrier (per workgroup, peer_sync.h): every rank's inputs are ready;
-//   phase 1 -> 2: each workgroup publishes "my phase-1 slabs are final" (flag[b][r] = e+1 on
-//   every rank); a phase-2 slab (q, k) waits for flag[k mod G][q] only -- no global barrier;
-//   end barrier: nobody leaves while a peer may still read its bucket.
-// Every wait is bounded (timeout -> host-mapped error word), so the grid always drains.
+// Work unit: a slab (4-64 KiB, fixed per call from (P, n, dtype)) of one owner block.  Slab k of
+// every block is handled by workgroup k mod G on every rank (G identical on every rank), so
+// workgroup b only ever synchronises with workgroup b of the other ranks (peer_sync.h):
+//   start barrier: every rank's bucket is ready;
+//   phase 1 -> 2 barrier: workgroup b's phase-1 slabs are final on every rank;
+//   end barrier (two-shot): nobody leaves while a peer may still read its bucket.
+// Every wait is bounded (timeout -> error word + abort broadcast), so the grid always drains.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -37,7 +36,7 @@ namespace {
 
 constexpr int kPU = 2;  // 16-B vectors per lane per source in flight
 
-// dst = fold of nsrc 16-B sources in the reference order (nsrc == 1: a raw copy)
+// dst = fold of nsrc 16-B sources in the reference order
 template <typename E, int OP, bool ACC32>
 __device__ __forceinline__ u32x4 fold_regs(const u32x4 (&v)[kPeerMaxRanks], int nsrc) {
   if constexpr (ACC32) {
@@ -145,42 +144,57 @@ __device__ __forceinline__ void slab_fold(char* dst, const PeerSrcs& S, int nsrc
   }
 }
 
-// Wait until rank q's workgroup `wg` has published epoch `e` into OUR signal area.
-__device__ __forceinline__ bool wait_flag(const PeerLaunch& A, int wg, int q, uint32_t e) {
-  int ok = 1;
-  if (threadIdx.x == 0) {
-    uint32_t* f = &A.sig.p[A.rank]->flag[wg][q];
-    const uint64_t t0 = peer_clock();
-    while ((int32_t)(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - e) < 0) {
-      __builtin_amdgcn_s_sleep(1);
-      if (peer_clock() - t0 > A.timeout_ticks) {
-        __hip_atomic_store(A.err, 4u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        ok = 0;
-        break;
-      }
+// One workgroup copies `count` elements src -> dst (phase 2 / copy-back): raw 16-B vectors,
+// kCU of them per lane in flight (one source only, so deeper than the fold's kPU).
+constexpr int kCU = 8;
+template <typename E>
+__device__ __forceinline__ void slab_copy(char* dst, const char* src, size_t count) {
+  constexpr int N = Vec<E>::N;
+  const int t = threadIdx.x;
+  size_t head = ((16 - (reinterpret_cast<uintptr_t>(dst) & 15)) & 15) / sizeof(E);
+  if (head > count) head = count;
+  const size_t nvec = (count - head) / N;
+  const size_t tail = count - head - nvec * N;
+  E* de = reinterpret_cast<E*>(dst);
+  const E* se = reinterpret_cast<const E*>(src);
+  if ((size_t)t < head) de[t] = se[t];
+  if ((size_t)t < tail) de[head + nvec * N + t] = se[head + nvec * N + t];
+  const size_t base = head * sizeof(E);
+  for (size_t v0 = 0; v0 < nvec; v0 += (size_t)kBlock * kCU) {
+    u32x4 r[kCU];
+#pragma unroll
+    for (int u = 0; u < kCU; u++) {
+      const size_t v = v0 + (size_t)u * kBlock + t;
+      if (v < nvec) r[u] = ld_u(src + base + v * 16);
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+#pragma unroll
+    for (int u = 0; u < kCU; u++) {
+      const size_t v = v0 + (size_t)u * kBlock + t;
+      if (v < nvec) st_a(dst + base + v * 16, r[u]);
+    }
   }
-  return __syncthreads_and(ok) != 0;
 }
 
-// Publish "this workgroup reached epoch e" to every rank without waiting.
-__device__ __forceinline__ void signal_all(const PeerLaunch& A, uint32_t e) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if ((int)threadIdx.x < A.P)
-    __hip_atomic_store(&A.sig.p[threadIdx.x]->flag[blockIdx.x][A.rank], e, __ATOMIC_RELEASE,
-                       __HIP_MEMORY_SCOPE_SYSTEM);
+// The group already failed (an earlier timeout here or on a peer): leave at once.
+__device__ __forceinline__ bool group_broken(const PeerSync& S) {
+  int bad = 0;
+  if (threadIdx.x == 0 && peer_aborted(S)) {
+    if (peer_ld(S.err) == 0) peer_st(S.err, kPeerErrAborted);
+    bad = 1;
+  }
+  return __syncthreads_or(bad) != 0;
 }
 
 template <typename E, int OP, bool ACC32>
 __global__ __launch_bounds__(kBlock) void k_peer_two_shot(PeerLaunch A) {
-  constexpr size_t SL = kPeerSlabBytes / sizeof(E);
-  const int P = A.P, r = A.rank;
+  const size_t SL = A.slab_bytes / sizeof(E);
+  const PeerSync& Y = A.sync;
+  const int P = Y.P, r = Y.rank;
   const uint32_t G = gridDim.x;
-  if (!peer_barrier(A.sig, P, r, A.epoch, A.timeout_ticks, A.err, 1)) return;
+  if (group_broken(Y)) return;
+  if (!peer_barrier(Y, A.epoch, 1)) return;  // every rank's bucket is ready
   PeerSrcs S;
-  // phase 1: own block, all P sources, in place
+  // phase 1: own block r, slabs k = b, b+G, ...; all P sources, in place
   {
     const size_t lo = A.lo[r], hi = A.lo[r + 1];
     for (size_t k = blockIdx.x; lo + k * SL < hi; k += G) {
@@ -191,36 +205,32 @@ __global__ __launch_bounds__(kBlock) void k_peer_two_shot(PeerLaunch A) {
       slab_fold<E, OP, ACC32>(A.x[r] + s * sizeof(E), S, P, hi - s < SL ? hi - s : SL);
     }
   }
-  signal_all(A, A.epoch + 1);
-  // phase 2: every other block from its owner; slabs interleaved over the peers so all P-1
-  // links stream at once
-  size_t nslab = 0;
-  for (int d = 1; d < P; d++) {
-    const int q = (r + d) % P;
-    const size_t sl = (A.lo[q + 1] - A.lo[q] + SL - 1) / SL;
-    nslab = sl > nslab ? sl : nslab;
-  }
-  for (size_t w = blockIdx.x; w < nslab * (size_t)(P - 1); w += G) {
-    const size_t k = w / (size_t)(P - 1);
-    const int q = (r + 1 + (int)(w % (size_t)(P - 1))) % P;
+  // workgroup b of every rank has finished ITS slabs (k = b mod G) of its own block
+  if (!peer_barrier(Y, A.epoch + 1, 2)) return;
+  // phase 2: the same slab indices of every other block, pulled from their owners; the start
+  // peer rotates with b so the workgroups of one rank read from all P-1 links at once
+  for (int i = 0; i < P - 1; i++) {
+    const int q = (r + 1 + (int)((blockIdx.x + i) % (uint32_t)(P - 1))) % P;
     const size_t lo = A.lo[q], hi = A.lo[q + 1];
-    if (lo + k * SL >= hi) continue;  // block-uniform
-    if (!wait_flag(A, (int)(k % G), q, A.epoch + 1)) return;
-    const size_t s = lo + k * SL;
-    S.p[0] = A.x[q] + s * sizeof(E);
-    slab_fold<E, OP, false>(A.x[r] + s * sizeof(E), S, 1, hi - s < SL ? hi - s : SL);
+    for (size_t k = blockIdx.x; lo + k * SL < hi; k += G) {
+      const size_t s = lo + k * SL;
+      slab_copy<E>(A.x[r] + s * sizeof(E), A.x[q] + s * sizeof(E), hi - s < SL ? hi - s : SL);
+    }
   }
-  peer_barrier(A.sig, P, r, A.epoch + 2, A.timeout_ticks, A.err, 3);
+  // nobody leaves (and lets its caller overwrite the bucket) while a peer may still read it
+  peer_barrier(Y, A.epoch + 2, 3);
 }
 
 template <typename E, int OP, bool ACC32>
 __global__ __launch_bounds__(kBlock) void k_peer_one_shot(PeerLaunch A) {
-  constexpr size_t SL = kPeerSlabBytes / sizeof(E);
-  const int P = A.P, r = A.rank;
+  const size_t SL = A.slab_bytes / sizeof(E);
+  const PeerSync& Y = A.sync;
+  const int P = Y.P, r = Y.rank;
   const uint32_t G = gridDim.x;
-  if (!peer_barrier(A.sig, P, r, A.epoch, A.timeout_ticks, A.err, 1)) return;
+  if (group_broken(Y)) return;
+  if (!peer_barrier(Y, A.epoch, 1)) return;
   PeerSrcs S;
-  // slab list over all owner blocks: (q, k) enumerated block by block
+  // slab list over all owner blocks: (q, k) enumerated block by block; slab w -> workgroup w%G
   size_t w = 0;
   for (int q = 0; q < P; q++) {
     const size_t lo = A.lo[q], hi = A.lo[q + 1];
@@ -235,7 +245,7 @@ __global__ __launch_bounds__(kBlock) void k_peer_one_shot(PeerLaunch A) {
     }
   }
   // every rank's workgroup b has read its slabs of every bucket -> safe to overwrite ours
-  if (!peer_barrier(A.sig, P, r, A.epoch + 1, A.timeout_ticks, A.err, 2)) return;
+  if (!peer_barrier(Y, A.epoch + 1, 2)) return;
   w = 0;
   for (int q = 0; q < P; q++) {
     const size_t lo = A.lo[q], hi = A.lo[q + 1];
@@ -243,8 +253,7 @@ __global__ __launch_bounds__(kBlock) void k_peer_one_shot(PeerLaunch A) {
     for (size_t k = 0; k < nsl; k++, w++) {
       if (w % G != blockIdx.x) continue;
       const size_t s = lo + k * SL;
-      S.p[0] = A.scratch + s * sizeof(E);
-      slab_fold<E, OP, false>(A.x[r] + s * sizeof(E), S, 1, hi - s < SL ? hi - s : SL);
+      slab_copy<E>(A.x[r] + s * sizeof(E), A.scratch + s * sizeof(E), hi - s < SL ? hi - s : SL);
     }
   }
 }
@@ -284,7 +293,8 @@ hipError_t dispatch(int algo, int dtype, bool acc32, const PeerLaunch& A, unsign
 
 hipError_t launch_peer(int algo, int op, int dtype, bool acc32, const PeerLaunch& A,
                        unsigned grid, hipStream_t s) {
-  if (A.P < 1 || A.P > kPeerMaxRanks || grid < 1 || grid > (unsigned)kPeerMaxBlocks)
+  if (A.sync.P < 1 || A.sync.P > kPeerMaxRanks || grid < 1 || grid > (unsigned)kPeerMaxBlocks ||
+      A.slab_bytes < 16 || A.slab_bytes % 16)
     return hipErrorInvalidValue;
   switch (op) {
     case kSum: return dispatch<kSum>(algo, dtype, acc32, A, grid, s);

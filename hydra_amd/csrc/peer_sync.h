@@ -2,13 +2,20 @@
 //
 // Used by the peer-access allreduce (peer_kernels.hip): every rank's kernel has the same grid,
 // and workgroup b of each rank synchronises only with workgroup b of every other rank, so no
-// grid-wide barrier (and no co-residency requirement beyond one workgroup per rank) is needed.
+// grid-wide barrier (and no co-residency requirement across workgroups) is needed.
 //
-// Memory model (LLVM AMDGPU, gfx950): the flag store is a system-scope release (buffer_wbl2 sc0
-// sc1 + wait: this XCD's dirty L2 lines -- the block's phase results -- reach memory before the
-// flag does); the waiter's system-scope acquire (buffer_inv sc0 sc1) drops stale copies of
-// remote lines (peer HBM is cached non-coherently in the local L2) before the next phase reads
-// them.  The flags live in uncached device memory shared by IPC.
+// Memory model (LLVM AMDGPU, gfx950; MI355X_MICROARCH.md "inter-workgroup visibility"):
+//   producer: every storing wave `s_waitcnt vmcnt(0)` -> workgroup barrier -> one wave:
+//             system-scope release fence (buffer_wbl2 sc0 sc1: this XCD's dirty L2 lines --
+//             the workgroup's results -- reach memory) -> explicit `s_waitcnt vmcnt(0)` (the
+//             compiler may drop the wait after buffer_wbl2, letting the flag overtake the
+//             write-back) -> relaxed system-scope flag stores into every rank's signal area;
+//   consumer: relaxed polls of its own (uncached) signal area -> system-scope acquire fence
+//             (buffer_inv sc0 sc1: drops stale L1 / non-coherent L2 copies of peer lines) ->
+//             `s_waitcnt vmcnt(0)` -> workgroup barrier -> plain loads.
+// Failure: a wait that exceeds its timeout records a code in the rank's host-mapped error
+// word and in every peer's `abort` word; every spin loop watches its own `abort`, so the whole
+// group drains within one timeout and every later kernel on the group exits at once.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -17,47 +24,95 @@ namespace hydra {
 
 constexpr int kPeerMaxRanks = 8;  // one xGMI-connected node
 constexpr int kPeerMaxBlocks = 1024;
+// error codes in the host-mapped word: 1-3 = timeout at barrier 1-3 of a call on this rank,
+// kPeerErrAborted = another rank gave up first
+constexpr uint32_t kPeerErrAborted = 5;
 
 struct PeerSignals {
   uint32_t flag[kPeerMaxBlocks][kPeerMaxRanks];  // flag[block][source rank] = last epoch seen
+  uint32_t abort;                                // non-zero: some rank gave up (its code)
 };
 
 struct PeerSigPtrs {
   PeerSignals* p[kPeerMaxRanks];  // rank q's signal area, mapped into this process
 };
 
+struct PeerSync {
+  PeerSigPtrs sig;
+  uint32_t* err;           // this rank's host-mapped error word
+  uint64_t timeout_ticks;  // s_memrealtime ticks (100 MHz)
+  int P, rank;
+};
+
 // s_memrealtime runs at a constant 100 MHz on gfx9
 __device__ __forceinline__ uint64_t peer_clock() { return __builtin_amdgcn_s_memrealtime(); }
 
-// Workgroup-level barrier with the same workgroup index on every rank.  Returns false (and
-// records `code` in *err, a host-mapped word) if a peer did not arrive within timeout_ticks;
-// every wave still leaves the barrier, so the grid always drains.
-__device__ __forceinline__ bool peer_barrier(const PeerSigPtrs& sig, int P, int rank,
-                                             uint32_t epoch, uint64_t timeout_ticks,
-                                             uint32_t* err, uint32_t code) {
-  // Every wave waits for its own stores to be acknowledged by L2 (hipcc's __syncthreads does
-  // not wait on vmcnt), so wave 0's buffer_wbl2 below writes back the whole block's results.
+__device__ __forceinline__ uint32_t peer_ld(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void peer_st(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Is the group already broken?  (one lane; cheap: own uncached area + host word)
+__device__ __forceinline__ bool peer_aborted(const PeerSync& S) {
+  return peer_ld(&S.sig.p[S.rank]->abort) != 0 || peer_ld(S.err) != 0;
+}
+
+// Give up: record `code` here and tell every peer.
+__device__ __forceinline__ void peer_fail(const PeerSync& S, uint32_t code) {
+  peer_st(S.err, code);
+  for (int q = 0; q < S.P; q++) peer_st(&S.sig.p[q]->abort, code);
+}
+
+// Release this workgroup's finished stores and publish `epoch` as flag[blockIdx.x][rank] in
+// every rank's signal area.  Call from all threads.
+__device__ __forceinline__ void peer_signal(const PeerSync& S, uint32_t epoch) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  const int t = threadIdx.x;
+  if (threadIdx.x < 64) {  // wave 0
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if ((int)threadIdx.x < S.P) peer_st(&S.sig.p[threadIdx.x]->flag[blockIdx.x][S.rank], epoch);
+  }
+}
+
+// Wait until every rank's workgroup blockIdx.x has published `epoch`, then acquire.  Returns
+// false (group broken) on timeout or abort; every wave still leaves, so the grid drains.
+__device__ __forceinline__ bool peer_wait(const PeerSync& S, uint32_t epoch, uint32_t code) {
   int ok = 1;
-  if (t < P) {
-    __hip_atomic_store(&sig.p[t]->flag[blockIdx.x][rank], epoch, __ATOMIC_RELEASE,
-                       __HIP_MEMORY_SCOPE_SYSTEM);
-    uint32_t* mine = &sig.p[rank]->flag[blockIdx.x][t];
+  if (threadIdx.x < 64) {  // wave 0: lane q polls rank q's arrival
+    const int q = threadIdx.x;
     const uint64_t t0 = peer_clock();
-    while ((int32_t)(__hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) -
-                     epoch) < 0) {
-      __builtin_amdgcn_s_sleep(1);
-      if (peer_clock() - t0 > timeout_ticks) {
-        __hip_atomic_store(err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        ok = 0;
-        break;
+    uint32_t spins = 0;
+    if (q < S.P) {
+      const uint32_t* mine = &S.sig.p[S.rank]->flag[blockIdx.x][q];
+      while ((int32_t)(peer_ld(mine) - epoch) < 0) {
+        __builtin_amdgcn_s_sleep(2);
+        if ((++spins & 63) == 0) {
+          if (peer_aborted(S)) {
+            if (peer_ld(S.err) == 0) peer_st(S.err, kPeerErrAborted);
+            ok = 0;
+            break;
+          }
+          if (peer_clock() - t0 > S.timeout_ticks) {
+            peer_fail(S, code);
+            ok = 0;
+            break;
+          }
+        }
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   return __syncthreads_and(ok) != 0;
+}
+
+// Workgroup-level barrier with the same workgroup index on every rank.
+__device__ __forceinline__ bool peer_barrier(const PeerSync& S, uint32_t epoch, uint32_t code) {
+  peer_signal(S, epoch);
+  return peer_wait(S, epoch, code);
 }
 
 }  // namespace hydra

@@ -314,24 +314,51 @@ def bench_allreduce(args, dev) -> dict:
     uid = exchange_unique_id(rank, dev)
     comm = XgmiComm(rank, world, dev.index, uid)
     rail2 = XgmiComm(rank, world, dev.index, exchange_unique_id(rank, dev))  # apipe's 2nd rail
+    from .peer import PeerComm
+
+    try:  # IPC-mapped buckets, one kernel per allreduce (hydra_amd.peer)
+        peer, peer_err = PeerComm(rank, world, dev.index), None
+    except HydraError as e:
+        peer, peer_err = None, str(e)
     n = args.elements
     algo = getattr(args, "algo", "auto")
+
+    def run(a, t, ch=0, **kw):
+        if a in _lib.PEER_ALGOS:
+            if peer is None:
+                raise HydraError(3, f"peer group unavailable: {peer_err}")
+            peer.allreduce_(t, algo=a, **kw)
+        else:
+            comm.allreduce_(t, algo=a, chunk_bytes=ch, **kw)
+
+    def peer_register(t):
+        if peer is not None:
+            peer.register(t)
+
+    def peer_ok():  # collective; a barrier timeout poisons the group: report, never hang
+        return max_over_ranks(float(peer.error()) if peer is not None else 1.0, dev) == 0.0
+
     try:
         # 1) parity self-check on fold-order-sensitive inputs (small bucket), every algorithm
         pn = 1 << 20  # equal blocks at P = 2..8, so A2A is checked too
         xs = [synth.stress_f32(world, r, pn) for r in range(world)]
         exp = expected_fold_f32(xs)
         parity = {}
-        for a in ("direct", "ring", "a2a"):
-            t = torch.from_numpy(xs[rank].copy()).to(dev)
+        tp = torch.empty(pn, dtype=torch.float32, device=dev)
+        peer_register(tp)
+        for a in ("direct", "ring", "a2a", "peer2", "peer1"):
+            tp.copy_(torch.from_numpy(xs[rank]))
             try:
-                comm.allreduce_(t, algo=a)
+                run(a, tp)
             except HydraError as e:  # e.g. A2A with unequal blocks at this P
                 parity[a] = f"n/a: {e}"
                 continue
             torch.cuda.synchronize(dev)
-            ok = bool(np.array_equal(t.cpu().numpy().view(np.uint32), exp.view(np.uint32)))
+            ok = bool(np.array_equal(tp.cpu().numpy().view(np.uint32), exp.view(np.uint32)))
             ok_all = max_over_ranks(0.0 if ok else 1.0, dev) == 0.0
+            if a.startswith("peer") and not peer_ok():
+                parity[a] = "barrier timeout"
+                continue
             parity[a] = "bit-exact" if ok_all else "MISMATCH"
         t = torch.from_numpy(xs[rank].copy()).to(dev)
         comm.allreduce_(t, algo="ring_old")
@@ -368,42 +395,49 @@ def bench_allreduce(args, dev) -> dict:
                            else "MISMATCH")
         # 2) exactness at full size: integer-valued inputs whose sums are exact in fp32
         j = np.arange(n, dtype=np.int64)
-        x = torch.from_numpy(((j % 1024) * (rank + 1)).astype(np.float32)).to(dev)
-
-        def step():
-            comm.allreduce_(x, algo=algo)
-
+        x0 = torch.from_numpy(((j % 1024) * (rank + 1)).astype(np.float32)).to(dev)
+        x = x0.clone()
+        peer_register(x)
+        full_exp = torch.from_numpy(((j % 1024) * (world * (world + 1) // 2))
+                                    .astype(np.float32)).to(dev)
         sync = lambda: torch.cuda.synchronize(dev)  # noqa: E731
-        step()
-        sync()
-        full_ok = torch.equal(
-            x, torch.from_numpy(((j % 1024) * (world * (world + 1) // 2)).astype(np.float32))
-            .to(dev))
-        full_ok = max_over_ranks(0.0 if full_ok else 1.0, dev) == 0.0
+
+        def full_exact(a, ch=0):
+            x.copy_(x0)
+            run(a, x, ch)
+            sync()
+            good = bool(torch.equal(x, full_exp))
+            return max_over_ranks(0.0 if good else 1.0, dev) == 0.0
+
+        full_ok = {"direct": full_exact("direct")}
         # 3) pick the algorithm: "auto" = the fastest bit-exact schedule on this node
-        #    (DIRECT / A2A / RING, chunk 4 or 16 MiB), chosen on a few untimed steps
+        #    (DIRECT / A2A / RING / PEER two-shot), chosen on a few untimed steps
         chosen, chunk = algo, 0
         tuning = {}
         if algo == "auto":
             best = None
             for a, ch in (("direct", 4 << 20), ("direct", 16 << 20), ("a2a", 0),
-                          ("ring", 4 << 20)):
-                if parity.get(a) not in (None, "bit-exact"):
+                          ("ring", 4 << 20), ("peer2", 0)):
+                if parity.get(a) != "bit-exact":
                     continue  # only schedules that reproduced the reference are eligible
                 try:
                     def tstep(a=a, ch=ch):
-                        comm.allreduce_(x, algo=a, chunk_bytes=ch)
+                        run(a, x, ch)
 
                     tw = max_over_ranks(timed_steps(tstep, 5, 2, sync, dist.barrier), dev) / 5
                 except _lib.HydraError:
+                    continue
+                if a.startswith("peer") and not peer_ok():
                     continue
                 tuning[f"{a}/{ch >> 20}MiB"] = round(tw * 1e3, 4)
                 if best is None or tw < best[0]:
                     best = (tw, a, ch)
             chosen, chunk = best[1], best[2]
+        if chosen not in full_ok:
+            full_ok[chosen] = full_exact(chosen, chunk)
 
         def step():
-            comm.allreduce_(x, algo=chosen, chunk_bytes=chunk)
+            run(chosen, x, chunk)
 
         # timed region: exactly `steps` allreduces, barrier + sync on both sides, max over ranks
         wall = timed_steps(step, args.steps, args.warmup, sync, dist.barrier)
@@ -412,12 +446,13 @@ def bench_allreduce(args, dev) -> dict:
         # 4) context: the other algorithms on the same bucket (fewer steps)
         others = {}
         k = max(5, args.steps // 4)
-        for a in ("ring", "direct", "a2a", "rccl", "ring_old", "ring_chunked", "bcube"):
+        for a in ("ring", "direct", "a2a", "rccl", "ring_old", "ring_chunked", "bcube", "peer2",
+                  "peer1"):
             if a == chosen:
                 continue
 
             def ostep(a=a):
-                comm.allreduce_(x, algo=a)
+                run(a, x)
 
             try:
                 ow = max_over_ranks(timed_steps(ostep, k, 3, sync, dist.barrier), dev)
@@ -440,11 +475,16 @@ def bench_allreduce(args, dev) -> dict:
             xb = torch.from_numpy(synth.bf16_bits((j[: 1 << 20] % 7 - 3).astype(np.float32))
                                   .view(np.int16)).to(dev).repeat(n5 >> 20)
 
-            c5_algo = chosen if chosen in ("direct", "a2a") else "direct"
+            c5_algo = chosen if chosen in ("direct", "a2a", "peer2") else "direct"
+            if c5_algo == "peer2":
+                if peer_ok():
+                    peer_register(xb)
+                else:
+                    c5_algo = "direct"
 
             def bstep():
-                comm.allreduce_(xb, algo=c5_algo, dtype_code=_lib.BFLOAT16, flags=_lib.ACC_F32,
-                                chunk_bytes=chunk if c5_algo == "direct" else 0)
+                run(c5_algo, xb, chunk if c5_algo == "direct" else 0, dtype_code=_lib.BFLOAT16,
+                    flags=_lib.ACC_F32)
 
             k5 = max(5, args.steps // 10)
             bw = max_over_ranks(timed_steps(bstep, k5, 2, sync, dist.barrier), dev)
@@ -455,6 +495,8 @@ def bench_allreduce(args, dev) -> dict:
                   "busbw_GBps": round(b_alg * 2 * (world - 1) / world, 2)}
             del xb
     finally:
+        if peer is not None:
+            peer.close()
         comm.close()
         rail2.close()
         dog.cancel()
@@ -467,9 +509,12 @@ def bench_allreduce(args, dev) -> dict:
         "value": round(world * algbw, 2), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-        "config": {"workload": f"in-place allreduce of a {n}-element fp32 bucket per rank, "
-                               "RCCL p2p over xGMI with the HIP sum fused per hop "
-                               "(BASELINE config 4)", "elements": n, "algo": chosen,
+        "config": {"workload": f"in-place allreduce of a {n}-element fp32 bucket per rank over "
+                               "xGMI, reference ring block ownership and fold order, "
+                               + ("ONE gfx950 kernel reading the peers' IPC-mapped blocks"
+                                  if chosen.startswith("peer") else
+                                  "RCCL p2p with the HIP sum fused per hop")
+                               + " (BASELINE config 4)", "elements": n, "algo": chosen,
                    "chunk_bytes": chunk, "autotune_ms": tuning,
                    "parallelism": f"dp{world}"},
         "algbw_GBps": round(algbw, 2), "busbw_GBps": round(busbw, 2),
@@ -480,5 +525,5 @@ def bench_allreduce(args, dev) -> dict:
                              "1 link (153 GB/s)"},
         "other_algos_ms": others,
         "config5_bf16": c5,
-        "parity": {"fold_order_1M": parity, "full_size_exact": bool(full_ok)},
+        "parity": {"fold_order_1M": parity, "full_size_exact": full_ok},
     }
