@@ -4,8 +4,8 @@
 // the handles travel through whatever channel the caller has (the reference's rendezvous store,
 // torch.distributed, a pipe): this file only produces and consumes opaque byte blobs.  After
 // that, hydra_peer_allreduce is ONE kernel launch on the caller's stream -- no host
-// synchronisation, no RCCL, graph-capturable -- whose reads of the peers' blocks travel over
-// xGMI.  Geometry and fold order are the reference ring's (xgmi_plan.h make_geom), so results
+// synchronisation, no RCCL, graph-capturable (barrier epochs are kept on the device) -- whose
+// reads of the peers' blocks travel over xGMI.  Geometry and fold order are the reference ring's (xgmi_plan.h make_geom), so results
 // equal gloo::allreduce RING (allreduce.cc:147-422) bit for bit.
 #include <hip/hip_runtime.h>
 
@@ -52,7 +52,6 @@ struct hydra_peer {
   hydra::PeerSigPtrs sigs{};          // every rank's, mapped
   uint32_t* err_host = nullptr;       // host-mapped error word the kernels write
   uint32_t* err_dev = nullptr;
-  uint32_t epoch = 1;
   uint64_t timeout_ticks = 20ull * 100000000ull;  // 20 s at 100 MHz
   int blocks = 0;                                 // 0 = derived from the bucket
   size_t one_shot_max = 256u << 10;               // AUTO: ONE_SHOT up to this many bytes
@@ -298,7 +297,6 @@ int hydra_peer_allreduce(hydra_peer_t p, int algo, int op, int dtype, int flags,
   A.sync.timeout_ticks = p->timeout_ticks;
   A.sync.P = p->P;
   A.sync.rank = p->rank;
-  A.epoch = p->epoch;
   // work unit: 64 KiB slabs for big buckets; smaller (down to 4 KiB) so that a small bucket
   // still spreads over ~256 workgroups.  Depends on (P, n, dtype) only: identical on all ranks.
   const size_t span = algo == HYDRA_PEER_ONE_SHOT ? n * es : g.max_block();
@@ -328,7 +326,6 @@ int hydra_peer_allreduce(hydra_peer_t p, int algo, int op, int dtype, int flags,
       algo == HYDRA_PEER_ONE_SHOT ? hydra::kPeerOneShot : hydra::kPeerTwoShot, op, dtype, acc32,
       A, (unsigned)grid, static_cast<hipStream_t>(stream));
   if (e != hipSuccess) return hydra::hip_fail(e, "peer allreduce kernel launch");
-  p->epoch += algo == HYDRA_PEER_ONE_SHOT ? 2 : 3;
   return ok();
 }
 

@@ -18,7 +18,6 @@ struct PeerLaunch {
   size_t lo[kPeerMaxRanks + 1];  // owner block q = elements [lo[q], lo[q+1])
   size_t slab_bytes;             // work unit (multiple of 16 and of the element size)
   char* scratch;                 // ONE_SHOT: n elements of local staging
-  uint32_t epoch;                // first epoch of this call (TWO_SHOT uses 3, ONE_SHOT 2)
 };
 
 hipError_t launch_peer(int algo, int op, int dtype, bool acc32, const PeerLaunch& A,

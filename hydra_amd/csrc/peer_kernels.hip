@@ -192,7 +192,7 @@ __global__ __launch_bounds__(kBlock) void k_peer_two_shot(PeerLaunch A) {
   const int P = Y.P, r = Y.rank;
   const uint32_t G = gridDim.x;
   if (group_broken(Y)) return;
-  if (!peer_barrier(Y, A.epoch, 1)) return;  // every rank's bucket is ready
+  if (!peer_barrier(Y, 1)) return;  // every rank's bucket is ready
   PeerSrcs S;
   // phase 1: own block r, slabs k = b, b+G, ...; all P sources, in place
   {
@@ -206,7 +206,7 @@ __global__ __launch_bounds__(kBlock) void k_peer_two_shot(PeerLaunch A) {
     }
   }
   // workgroup b of every rank has finished ITS slabs (k = b mod G) of its own block
-  if (!peer_barrier(Y, A.epoch + 1, 2)) return;
+  if (!peer_barrier(Y, 2)) return;
   // phase 2: the same slab indices of every other block, pulled from their owners; the start
   // peer rotates with b so the workgroups of one rank read from all P-1 links at once
   for (int i = 0; i < P - 1; i++) {
@@ -218,7 +218,7 @@ __global__ __launch_bounds__(kBlock) void k_peer_two_shot(PeerLaunch A) {
     }
   }
   // nobody leaves (and lets its caller overwrite the bucket) while a peer may still read it
-  peer_barrier(Y, A.epoch + 2, 3);
+  peer_barrier(Y, 3);
 }
 
 template <typename E, int OP, bool ACC32>
@@ -228,7 +228,7 @@ __global__ __launch_bounds__(kBlock) void k_peer_one_shot(PeerLaunch A) {
   const int P = Y.P, r = Y.rank;
   const uint32_t G = gridDim.x;
   if (group_broken(Y)) return;
-  if (!peer_barrier(Y, A.epoch, 1)) return;
+  if (!peer_barrier(Y, 1)) return;
   PeerSrcs S;
   // slab list over all owner blocks: (q, k) enumerated block by block; slab w -> workgroup w%G
   size_t w = 0;
@@ -245,7 +245,7 @@ __global__ __launch_bounds__(kBlock) void k_peer_one_shot(PeerLaunch A) {
     }
   }
   // every rank's workgroup b has read its slabs of every bucket -> safe to overwrite ours
-  if (!peer_barrier(Y, A.epoch + 1, 2)) return;
+  if (!peer_barrier(Y, 2)) return;
   w = 0;
   for (int q = 0; q < P; q++) {
     const size_t lo = A.lo[q], hi = A.lo[q + 1];

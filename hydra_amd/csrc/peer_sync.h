@@ -65,6 +65,14 @@ __device__ __forceinline__ void peer_fail(const PeerSync& S, uint32_t code) {
   for (int q = 0; q < S.P; q++) peer_st(&S.sig.p[q]->abort, code);
 }
 
+// Epochs live on the device: workgroup b's next epoch is one past the value it last published
+// for itself (flag[b][rank] of its own area, written only by it).  Workgroup b of every rank
+// runs the same sequence of barriers, so the counters agree without any host bookkeeping --
+// which is what makes a captured hipGraph replayable (kernel arguments never change).
+__device__ __forceinline__ uint32_t peer_next_epoch(const PeerSync& S) {
+  return peer_ld(&S.sig.p[S.rank]->flag[blockIdx.x][S.rank]) + 1u;
+}
+
 // Release this workgroup's finished stores and publish `epoch` as flag[blockIdx.x][rank] in
 // every rank's signal area.  Call from all threads.
 __device__ __forceinline__ void peer_signal(const PeerSync& S, uint32_t epoch) {
@@ -110,7 +118,11 @@ __device__ __forceinline__ bool peer_wait(const PeerSync& S, uint32_t epoch, uin
 }
 
 // Workgroup-level barrier with the same workgroup index on every rank.
-__device__ __forceinline__ bool peer_barrier(const PeerSync& S, uint32_t epoch, uint32_t code) {
+__device__ __forceinline__ bool peer_barrier(const PeerSync& S, uint32_t code) {
+  __shared__ uint32_t epoch_s;
+  if (threadIdx.x == 0) epoch_s = peer_next_epoch(S);
+  __syncthreads();
+  const uint32_t epoch = epoch_s;
   peer_signal(S, epoch);
   return peer_wait(S, epoch, code);
 }

@@ -1,5 +1,5 @@
 set -u
-O=gpurun_out/peerb3
+O=gpurun_out/peerb4
 mkdir -p $O
 timeout -k 10 400 python -u -m pytest tests/test_gpu_peer.py -x -v --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1 || { echo "pytest rc=$?"; exit 1; }
 timeout -k 10 200 python -u scripts/peer_bench.py --P 2 --blocks 256 > $O/p2.log 2>&1 || { echo "p2 rc=$?"; exit 1; }

@@ -76,10 +76,22 @@ def main():
             view = arena[off:off + nbytes]
             view.copy_(torch.from_numpy(x.view(np.uint8)))
             code = c["dtype"]
+            kw = dict(algo=c["algo"], op=c.get("op", "sum"), dtype_code=code,
+                      flags=c.get("flags", 0), max_segment=c.get("ms", 0))
             for _ in range(c.get("repeat", 1)):
                 view.copy_(torch.from_numpy(x.view(np.uint8)))
-                peer.allreduce_(view, algo=c["algo"], op=c.get("op", "sum"), dtype_code=code,
-                                flags=c.get("flags", 0), max_segment=c.get("ms", 0))
+                peer.allreduce_(view, **kw)
+            if c.get("graph"):  # capture once, replay: the kernel arguments never change
+                xin = torch.from_numpy(x.view(np.uint8)).to(dev)
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    peer.allreduce_(view, **kw)
+                for _ in range(3):
+                    view.copy_(xin)
+                    g.replay()
+                # and eager calls still line up with the replays' barriers afterwards
+                view.copy_(xin)
+                peer.allreduce_(view, **kw)
             torch.cuda.synchronize(dev)
             if c.get("skip_rank") is not None:
                 status[name] = peer.error()

@@ -95,6 +95,10 @@ def cases_for(P):
     cs.append(dict(name="auto_small", algo="peer", data="stress_f32", dtype=F32, n=5000))
     cs.append(dict(name="repeat", algo="peer2", data="stress_f32", dtype=F32, n=262147,
                    repeat=25))
+    cs.append(dict(name="graph2", algo="peer2", data="stress_f32", dtype=F32, n=300007,
+                   graph=True))
+    cs.append(dict(name="graph1", algo="peer1", data="int32", dtype=I32, n=30011, ms=4096,
+                   graph=True))
     cs.append(dict(name="bf16_acc32", algo="peer2", data="bf16", dtype=BF16, n=1 << 20,
                    flags=_lib.ACC_F32))
     return cs
