@@ -238,10 +238,11 @@ int hydra_allreduce_simulate(int algo, int op, int dtype, int flags, int P, void
  * Setup (every rank, same order; the byte blobs travel over any channel the caller has, e.g.
  * the rendezvous store): hydra_peer_create -> exchange sig handles -> hydra_peer_connect; for
  * each bucket: hydra_peer_register -> exchange -> hydra_peer_open.  Every rank must then issue
- * the same sequence of hydra_peer_allreduce calls (like any collective); a call is one kernel
- * launch, graph-capturable (barrier epochs live on the device, so replays need no new args).  A peer that never
- * arrives ends the kernel after the timeout (default 20 s) and leaves an error code readable
- * with hydra_peer_error; later calls on the group fail with HYDRA_ERR_HIP. 1 <= nranks <= 8. */
+ * the same sequence of hydra_peer_allreduce calls (like any collective).  A call is one kernel
+ * launch and is graph-capturable: barrier epochs live on the device, so replays need no new
+ * arguments.  A peer that never arrives ends the kernel after the timeout (default 20 s) and
+ * leaves an error code readable with hydra_peer_error; later calls on the group fail with
+ * HYDRA_ERR_HIP.  1 <= nranks <= 8. */
 #define HYDRA_PEER_HANDLE_BYTES 128
 typedef enum { HYDRA_PEER_AUTO = 0, HYDRA_PEER_TWO_SHOT = 1, HYDRA_PEER_ONE_SHOT = 2 } hydra_peer_algo_t;
 typedef enum {
