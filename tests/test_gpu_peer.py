@@ -144,3 +144,15 @@ def test_peer_timeout_reports_and_poisons(gpu, tmp_path):
     _, st = run_ranks(tmp_path, 2, cases)
     assert st[0]["lonely"] != 0
     assert "timed out" in st[0]["lonely/next"]
+
+
+@pytest.mark.parametrize("P,n", [(2, 1000003), (3, 4099)])
+def test_peer_from_c(gpu, P, n):
+    """The C-ABI alone (tests/cpp/peer_capi.c: fork, pipes for the handle blobs, hydra_malloc /
+    hydra_peer_* / hydra_stream_*), as a C caller such as the reference's benchmark wires it."""
+    exe = os.path.join(ROOT, "tests", "cpp", "peer_capi")
+    assert os.path.exists(exe), "built by hydra_amd/csrc/Makefile (hydra_amd._lib.build())"
+    r = subprocess.run([exe, str(P), str(n)], capture_output=True, timeout=120)
+    out = r.stdout.decode() + r.stderr.decode()
+    assert r.returncode == 0, out
+    assert f"peer_capi P={P} n={n}: ok" in out
