@@ -432,9 +432,11 @@ def bench_allreduce(args, dev) -> dict:
                 tuning[f"{a}/{ch >> 20}MiB"] = round(tw * 1e3, 4)
                 if best is None or tw < best[0]:
                     best = (tw, a, ch)
-            chosen, chunk = best[1], best[2]
+            chosen, chunk = (best[1], best[2]) if best is not None else ("direct", 0)
         if chosen not in full_ok:
             full_ok[chosen] = full_exact(chosen, chunk)
+            if not full_ok[chosen]:  # never time a schedule that missed the reference bits
+                chosen, chunk = "direct", 0
 
         def step():
             run(chosen, x, chunk)
