@@ -23,35 +23,56 @@ from ._lib import HydraError, OPS, PEER_ALGOS, check
 _is_finalizing = sys.is_finalizing
 
 
-def _all_gather_bytes(blob: bytes, group=None) -> bytes:
+def _all_gather_bytes(blob: bytes, group=None) -> list:
     import torch.distributed as dist
 
     out = [None] * dist.get_world_size(group)
     dist.all_gather_object(out, blob, group=group)
-    return b"".join(out)
+    return out
+
+
+def _agree(ok: bool, group=None) -> bool:
+    """Collective AND: every rank learns whether every rank succeeded."""
+    return all(_all_gather_bytes(b"1" if ok else b"0", group)[i] == b"1"
+               for i in range(_world(group)))
+
+
+def _world(group=None) -> int:
+    import torch.distributed as dist
+
+    return dist.get_world_size(group)
 
 
 class PeerComm:
-    """hydra_peer_t: signal area + IPC mappings of the registered buckets of all ranks."""
+    """hydra_peer_t: signal area + IPC mappings of the registered buckets of all ranks.
+
+    Setup steps are collective and fail collectively: a rank whose HIP call fails still joins
+    every exchange, so its peers raise HydraError too instead of waiting for it forever."""
 
     def __init__(self, rank: int, world: int, device_index: int, group=None,
                  timeout_ms: int | None = None, blocks: int | None = None):
-        h = ctypes.c_void_p()
-        sig = ctypes.create_string_buffer(_lib.PEER_HANDLE_BYTES)
-        check(_lib.lib().hydra_peer_create(world, rank, device_index, ctypes.byref(h), sig))
-        self._h = h
+        self._h = ctypes.c_void_p()
         self.rank, self.world, self.group = rank, world, group
         self._registered: dict[int, int] = {}  # data_ptr -> bytes
-        try:
-            allsig = _all_gather_bytes(sig.raw, group)
-            check(_lib.lib().hydra_peer_connect(self._h, allsig))
-            if timeout_ms is not None:
-                self.set_option(_lib.PEER_OPT_TIMEOUT_MS, timeout_ms)
-            if blocks is not None:
-                self.set_option(_lib.PEER_OPT_BLOCKS, blocks)
-        except Exception:
+        sig = ctypes.create_string_buffer(_lib.PEER_HANDLE_BYTES)
+        err = None
+        rc = _lib.lib().hydra_peer_create(world, rank, device_index, ctypes.byref(self._h), sig)
+        if rc:
+            err = HydraError(rc, _lib.lib().hydra_last_error().decode(errors="replace"))
+        allsig = _all_gather_bytes(sig.raw if err is None else b"", group)
+        if err is None and any(len(b) != _lib.PEER_HANDLE_BYTES for b in allsig):
+            err = HydraError(3, "a peer failed to create its signal area")
+        if err is None:
+            rc = _lib.lib().hydra_peer_connect(self._h, b"".join(allsig))
+            if rc:
+                err = HydraError(rc, _lib.lib().hydra_last_error().decode(errors="replace"))
+        if not _agree(err is None, group):
             self.close()
-            raise
+            raise err or HydraError(3, "a peer failed to map the signal areas")
+        if timeout_ms is not None:
+            self.set_option(_lib.PEER_OPT_TIMEOUT_MS, timeout_ms)
+        if blocks is not None:
+            self.set_option(_lib.PEER_OPT_BLOCKS, blocks)
 
     def set_option(self, key: int, value: int) -> None:
         check(_lib.lib().hydra_peer_set_option(self._h, key, int(value)))
@@ -59,13 +80,26 @@ class PeerComm:
     def register(self, t) -> None:
         """Collective: share device tensor t's memory with every rank (same call order on all
         ranks).  t must stay alive while registered; allreduce_ accepts t or any view of it."""
-        if not t.is_cuda or not t.is_contiguous():
-            raise HydraError(1, "register: contiguous device tensor required")
         nbytes = t.numel() * t.element_size()
         blob = ctypes.create_string_buffer(_lib.PEER_HANDLE_BYTES)
-        check(_lib.lib().hydra_peer_register(self._h, t.data_ptr(), nbytes, blob))
-        allh = _all_gather_bytes(blob.raw, self.group)
-        check(_lib.lib().hydra_peer_open(self._h, t.data_ptr(), nbytes, allh))
+        err = None
+        if not t.is_cuda or not t.is_contiguous():
+            err = HydraError(1, "register: contiguous device tensor required")
+        else:
+            rc = _lib.lib().hydra_peer_register(self._h, t.data_ptr(), nbytes, blob)
+            if rc:
+                err = HydraError(rc, _lib.lib().hydra_last_error().decode(errors="replace"))
+        allh = _all_gather_bytes(blob.raw if err is None else b"", self.group)
+        if err is None and any(len(b) != _lib.PEER_HANDLE_BYTES for b in allh):
+            err = HydraError(3, "a peer failed to export its buffer")
+        if err is None:
+            rc = _lib.lib().hydra_peer_open(self._h, t.data_ptr(), nbytes, b"".join(allh))
+            if rc:
+                err = HydraError(rc, _lib.lib().hydra_last_error().decode(errors="replace"))
+        if not _agree(err is None, self.group):
+            if err is None:  # mapped here, failed elsewhere: undo so every rank agrees
+                _lib.lib().hydra_peer_close(self._h, t.data_ptr())
+            raise err or HydraError(3, "a peer failed to map the buffer")
         self._registered[t.data_ptr()] = nbytes
 
     def unregister(self, t) -> None:

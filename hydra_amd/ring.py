@@ -316,27 +316,35 @@ def bench_allreduce(args, dev) -> dict:
     rail2 = XgmiComm(rank, world, dev.index, exchange_unique_id(rank, dev))  # apipe's 2nd rail
     from .peer import PeerComm
 
-    try:  # IPC-mapped buckets, one kernel per allreduce (hydra_amd.peer)
-        peer, peer_err = PeerComm(rank, world, dev.index), None
+    pg = {"peer": None, "err": None}  # IPC-mapped buckets, one kernel per allreduce
+    try:  # (hydra_amd.peer; setup fails collectively, so every rank takes the same branch)
+        pg["peer"] = PeerComm(rank, world, dev.index)
     except HydraError as e:
-        peer, peer_err = None, str(e)
+        pg["err"] = str(e)
     n = args.elements
     algo = getattr(args, "algo", "auto")
 
     def run(a, t, ch=0, **kw):
+        """ch: RCCL plans' pipelining chunk in bytes; peer algorithms' workgroup count."""
         if a in _lib.PEER_ALGOS:
-            if peer is None:
-                raise HydraError(3, f"peer group unavailable: {peer_err}")
-            peer.allreduce_(t, algo=a, **kw)
+            if pg["peer"] is None:
+                raise HydraError(3, f"peer group unavailable: {pg['err']}")
+            pg["peer"].set_option(_lib.PEER_OPT_BLOCKS, ch)
+            pg["peer"].allreduce_(t, algo=a, **kw)
         else:
             comm.allreduce_(t, algo=a, chunk_bytes=ch, **kw)
 
     def peer_register(t):
-        if peer is not None:
-            peer.register(t)
+        if pg["peer"] is not None:
+            try:
+                pg["peer"].register(t)
+            except HydraError as e:  # collective failure: drop the peer algorithms
+                pg["peer"].close()
+                pg["peer"], pg["err"] = None, str(e)
 
     def peer_ok():  # collective; a barrier timeout poisons the group: report, never hang
-        return max_over_ranks(float(peer.error()) if peer is not None else 1.0, dev) == 0.0
+        p = pg["peer"]
+        return max_over_ranks(float(p.error()) if p is not None else 1.0, dev) == 0.0
 
     try:
         # 1) parity self-check on fold-order-sensitive inputs (small bucket), every algorithm
@@ -417,7 +425,7 @@ def bench_allreduce(args, dev) -> dict:
         if algo == "auto":
             best = None
             for a, ch in (("direct", 4 << 20), ("direct", 16 << 20), ("a2a", 0),
-                          ("ring", 4 << 20), ("peer2", 0)):
+                          ("ring", 4 << 20), ("peer2", 0), ("peer2", 256)):
                 if parity.get(a) != "bit-exact":
                     continue  # only schedules that reproduced the reference are eligible
                 try:
@@ -429,7 +437,8 @@ def bench_allreduce(args, dev) -> dict:
                     continue
                 if a.startswith("peer") and not peer_ok():
                     continue
-                tuning[f"{a}/{ch >> 20}MiB"] = round(tw * 1e3, 4)
+                tuning[f"{a}/{ch}wg" if a in _lib.PEER_ALGOS else f"{a}/{ch >> 20}MiB"] = \
+                    round(tw * 1e3, 4)
                 if best is None or tw < best[0]:
                     best = (tw, a, ch)
             chosen, chunk = (best[1], best[2]) if best is not None else ("direct", 0)
@@ -481,12 +490,12 @@ def bench_allreduce(args, dev) -> dict:
             if c5_algo == "peer2":
                 if peer_ok():
                     peer_register(xb)
-                else:
+                if pg["peer"] is None or not peer_ok():
                     c5_algo = "direct"
 
             def bstep():
-                run(c5_algo, xb, chunk if c5_algo == "direct" else 0, dtype_code=_lib.BFLOAT16,
-                    flags=_lib.ACC_F32)
+                run(c5_algo, xb, chunk if c5_algo in ("direct", "peer2") else 0,
+                    dtype_code=_lib.BFLOAT16, flags=_lib.ACC_F32)
 
             k5 = max(5, args.steps // 10)
             bw = max_over_ranks(timed_steps(bstep, k5, 2, sync, dist.barrier), dev)
@@ -497,8 +506,8 @@ def bench_allreduce(args, dev) -> dict:
                   "busbw_GBps": round(b_alg * 2 * (world - 1) / world, 2)}
             del xb
     finally:
-        if peer is not None:
-            peer.close()
+        if pg["peer"] is not None:
+            pg["peer"].close()
         comm.close()
         rail2.close()
         dog.cancel()
@@ -517,7 +526,8 @@ def bench_allreduce(args, dev) -> dict:
                                   if chosen.startswith("peer") else
                                   "RCCL p2p with the HIP sum fused per hop")
                                + " (BASELINE config 4)", "elements": n, "algo": chosen,
-                   "chunk_bytes": chunk, "autotune_ms": tuning,
+                   ("peer_workgroups" if chosen in _lib.PEER_ALGOS else "chunk_bytes"): chunk,
+                   "autotune_ms": tuning,
                    "parallelism": f"dp{world}"},
         "algbw_GBps": round(algbw, 2), "busbw_GBps": round(busbw, 2),
         "roofline": {"bound": "xgmi", "achieved": round(busbw, 2),
