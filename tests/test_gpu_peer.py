@@ -104,7 +104,7 @@ def cases_for(P):
     return cs
 
 
-@pytest.mark.parametrize("P", [2, 3, 4])
+@pytest.mark.parametrize("P", [2, 3, 4, 8])
 def test_peer_allreduce_bit_exact(gpu, O, tmp_path, P):
     cases = cases_for(P)
     res, st = run_ranks(tmp_path, P, cases)
