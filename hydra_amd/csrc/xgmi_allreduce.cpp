@@ -3,9 +3,11 @@
 // The schedule is data (xgmi_plan.h).  This file interprets it:
 //   * run_plan_rccl   one rank: SEND/RECV groups -> ncclGroupStart/ncclSend/ncclRecv/ncclGroupEnd
 //                     on the comm stream; REDUCE/FOLD -> HIP kernels on the compute stream; the
-//                     plan's wait0/wait1 edges -> hipEventRecord / hipStreamWaitEvent.  No host
-//                     synchronisation: the whole allreduce is enqueued asynchronously on the
-//                     caller's stream (graph-capturable).
+//                     plan's cross-stream wait0/wait1 edges -> hipEventRecord /
+//                     hipStreamWaitEvent.  No host synchronisation: the whole allreduce is
+//                     enqueued asynchronously on the caller's stream.  The fork/join, events,
+//                     kernels and RCCL collectives capture into hipGraphs (tested); RCCL p2p
+//                     capture is untested (RCCL faults on send-to-self under capture).
 //   * simulate        every rank's plan on one GPU in lock-step, device copies on a "fabric"
 //                     stream standing in for xGMI -- the multi-GPU path's test bench.
 
@@ -140,9 +142,20 @@ int ensure_events(hydra_comm* c, size_t n) {
   return HYDRA_OK;
 }
 
-void wait_on(hipStream_t st, const hydra::PlanOp& o, const std::vector<hipEvent_t>& ev) {
-  if (o.wait0 >= 0) (void)hipStreamWaitEvent(st, ev[o.wait0], 0);
-  if (o.wait1 >= 0) (void)hipStreamWaitEvent(st, ev[o.wait1], 0);
+// Which executor stream an op runs on: p2p groups and collectives on the comm stream, the
+// fused reductions on the compute stream.
+bool on_comm_stream(int32_t kind) {
+  return kind != hydra::kOpReduce && kind != hydra::kOpFold;
+}
+
+// Cross-stream edges only: an op waiting on an earlier op of its OWN stream is already
+// ordered behind it, and HIP graph capture faults on a wait for an event recorded on the
+// capturing stream itself (scripts/probe_graph.py "fold_wait").
+void wait_on(hipStream_t st, const hydra::PlanOp& o, const std::vector<hydra::PlanOp>& ops,
+             const std::vector<hipEvent_t>& ev) {
+  const bool comm = on_comm_stream(o.kind);
+  for (int32_t w : {o.wait0, o.wait1})
+    if (w >= 0 && on_comm_stream(ops[w].kind) != comm) (void)hipStreamWaitEvent(st, ev[w], 0);
 }
 
 // Enqueue the cached plan after `start` (recorded on the caller's stream); the caller joins
@@ -157,7 +170,7 @@ int run_plan_rccl(hydra_comm* c, int op, int dtype, bool acc32, char* user, hipE
   while (i < ops.size()) {
     const hydra::PlanOp& o = ops[i];
     if (o.kind == hydra::kOpAllToAll || o.kind == hydra::kOpAllGather) {
-      wait_on(c->cs, o, c->events);
+      wait_on(c->cs, o, ops, c->events);
       if (o.kind == hydra::kOpAllToAll)
         NCCL_TRY(ncclAllToAll(user + o.off, scratch + o.src_off, (size_t)o.bytes, ncclUint8,
                               c->nccl, c->cs));
@@ -172,7 +185,7 @@ int run_plan_rccl(hydra_comm* c, int op, int dtype, bool acc32, char* user, hipE
       size_t g = i;
       while (g < ops.size() && ops[g].kind != hydra::kOpGroup) g++;
       if (g == ops.size()) return fail(HYDRA_ERR_INVALID, "plan: unterminated p2p group");
-      wait_on(c->cs, ops[g], c->events);
+      wait_on(c->cs, ops[g], ops, c->events);
       NCCL_TRY(ncclGroupStart());
       ncclResult_t r = ncclSuccess;
       for (size_t j = i; j < g && r == ncclSuccess; j++) {
@@ -188,7 +201,7 @@ int run_plan_rccl(hydra_comm* c, int op, int dtype, bool acc32, char* user, hipE
       if (c->waited[g]) HIP_TRY(hipEventRecord(c->events[g], c->cs));
       i = g + 1;
     } else {
-      wait_on(c->ks, o, c->events);
+      wait_on(c->ks, o, ops, c->events);
       hipError_t e = launch_compute(o, op, dtype, acc32, user, scratch, es, c->ks);
       if (e != hipSuccess) return hydra::hip_fail(e, "fused reduction kernel");
       if (c->waited[i]) HIP_TRY(hipEventRecord(c->events[i], c->ks));

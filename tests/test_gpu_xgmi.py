@@ -388,3 +388,45 @@ def test_rccl_executor_self_loop(gpu, O, algo, P, n, ch):
             comm.run_plan_(bad, t, scr)
     finally:
         comm.close()
+
+
+def test_executor_graph_replay(gpu, O):
+    """The executor's stream fork/join, events, scratch reset and kernels capture into a
+    hipGraph and replay: a compute-only plan (REDUCE then FOLD on the compute stream, waiting
+    on each other and joined into the caller's stream; op = max against the zeroed scratch,
+    i.e. max(x, 0)) plus RCCL's own collective (HYDRA_ALGO_RCCL) on a 1-rank communicator,
+    captured once and replayed three times.  (RCCL send/recv-to-self and ncclAllToAll on a
+    1-rank communicator crash inside RCCL under capture -- scripts/probe_graph.py -- so p2p
+    plans are not captured here)"""
+    import torch
+
+    n = 1 << 18
+    B = n * 4
+    x = synth.stress_f32(4, 1, n)
+    ops = [dict(kind=4, peer=0, buf=0, nsrc=0, off=0, bytes=B, src_off=0, slot_stride=0,
+                wait0=-1, wait1=-1),
+           dict(kind=5, peer=-1, buf=0, nsrc=2, off=0, bytes=B, src_off=B, slot_stride=B,
+                wait0=0, wait1=-1)]
+    zero = np.zeros(n, np.float32)
+    exp = O.op(O.op(x, zero, "max", 6), zero, "max", 6)
+    comm = ring.XgmiComm(0, 1, gpu.index or 0, ring._rccl_unique_id())
+    try:
+        xin = torch.from_numpy(x).to(gpu)
+        t = xin.clone()
+        u = xin.clone()
+        comm.run_plan_(ops, t, 2 * B, op="max")  # warm-up outside capture (scratch, events)
+        comm.allreduce_(u, algo="rccl")
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            comm.run_plan_(ops, t, 2 * B, op="max")
+            comm.allreduce_(u, algo="rccl")  # 1 rank: a captured identity collective
+        for _ in range(3):
+            t.copy_(xin)
+            u.copy_(xin)
+            g.replay()
+        torch.cuda.synchronize()
+        assert np.array_equal(t.cpu().numpy().view(np.uint32), exp.view(np.uint32))
+        assert np.array_equal(u.cpu().numpy().view(np.uint32), x.view(np.uint32))
+    finally:
+        comm.close()
