@@ -33,6 +33,29 @@ def inputs(case, P, r):
     raise ValueError(kind)
 
 
+def stress(peer, arena, c, rank, world, dev):
+    """`iters` allreduces of integer-valued fp32 buckets that change every iteration (a stale
+    read of the previous call's data cannot go unnoticed), each rank delayed by a random spin
+    before every call (uneven arrival), every word of every result checked exactly.  Returns
+    the number of wrong words (sums of small integers are exact in any order)."""
+    import torch
+
+    n, off = c["n"], c.get("offset_bytes", 0)
+    view = arena[off:off + 4 * n].view(torch.float32)
+    base = torch.arange(n, device=dev, dtype=torch.int64) % 1000
+    g = np.random.default_rng(99 + rank)
+    bad = 0
+    spin = getattr(torch.cuda, "_sleep", None)
+    for it in range(c["iters"]):
+        view.copy_((base * (rank + 1) + it * (rank + 2)).to(torch.float32))
+        if spin is not None:
+            spin(int(g.integers(0, 200000)))
+        peer.allreduce_(view, algo=c["algo"], dtype_code=c["dtype"])
+        exp = base * (world * (world + 1) // 2) + it * (world * (world + 3) // 2)
+        bad += int((view != exp.to(torch.float32)).sum().item())
+    return bad
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rank", type=int, required=True)
@@ -67,6 +90,9 @@ def main():
             if c.get("skip_rank") == a.rank:  # timeout case: this rank never arrives
                 dist.barrier()
                 dist.barrier()
+                continue
+            if c["data"] == "stress":  # varying inputs, uneven arrival, every word checked
+                status[name] = stress(peer, arena, c, a.rank, a.world, dev)
                 continue
             if c.get("timeout_ms"):
                 peer.set_option(_lib.PEER_OPT_TIMEOUT_MS, c["timeout_ms"])
