@@ -6,10 +6,13 @@ Metric (BASELINE.json): chunk-sum GB/s (fp32) vs HBM peak; ring-allreduce GB/s a
   N = 1  (BASELINE config 2): one step = one device-resident, in-place fp32 chunk-sum
          c = a + b over 64 Mi elements (gloo::sum<float>, math.h:15-23, in the ring's c == a
          form).  value = 12 B/element x elements x steps / wall time of the timed region.
+         --sweep adds config 2's 4 Ki..64 Mi size sweep to the line.
   N > 1  (BASELINE config 4): one step = one allreduce of a 64 Mi-element fp32 bucket per rank
-         over RCCL/xGMI with the HIP sum fused into every reduce-scatter hop (hydra_amd.ring).
-         value = N x bucket bytes / time (whole-job bucket bytes reduced per second); algbw and
-         busbw = algbw x 2(N-1)/N are reported beside it.
+         over xGMI in the reference's block ownership and fold order -- the fastest bit-exact
+         schedule of RCCL p2p with the HIP sum fused per hop (DIRECT / A2A / RING) and the
+         peer-access kernel (hydra_amd.ring, hydra_amd.peer).  value = N x bucket bytes / time
+         (whole-job bucket bytes reduced per second); algbw and busbw = algbw x 2(N-1)/N are
+         reported beside it.
 
 Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under torch.distributed.run.
 Prints ONE JSON line on rank 0.
@@ -42,7 +45,9 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0,
                    help="bounded CPU-baseline sample (seconds of reference gloo::sum work)")
-    p.add_argument("--sweep", action="store_true", help="add the 4 Ki..64 Mi size sweep")
+    p.add_argument("--sweep", action="store_true",
+                   help="add the 4 Ki..64 Mi size sweep (BASELINE config 2's range); off by "
+                        "default so a kernel trace of the default command holds one size only")
     p.add_argument("--algo", default="auto", help="ring algorithm for N>1 (see hydra_amd.ring)")
     p.add_argument("--watchdog-s", type=float, default=420.0,
                    help="N>1: abort (exit 3) if the run exceeds this many seconds")
@@ -117,8 +122,9 @@ def time_chunk_sum(torch, L, dev, n, code, steps, warmup, variant=None, cold_rep
 
 def pmc_traffic():
     """HBM bytes per launch of the 64 Mi chunk-sum from the committed rocprofv3 PMC summary
-    (profiles/pmc_chunk_sum.json, written by profiles/collect.sh: FETCH_SIZE x2 gfx950
-    correction + WRITE_SIZE, MI355X_MICROARCH.md §HBM).  None if absent."""
+    (profiles/pmc_chunk_sum.json, written by scripts/pmc_summary.py from scripts/gpu_check.sh's
+    --pmc passes: FETCH_SIZE x2 gfx950 correction + WRITE_SIZE, MI355X_MICROARCH.md §HBM).
+    None if absent."""
     p = os.path.join(ROOT, "profiles", "pmc_chunk_sum.json")
     if not os.path.exists(p):
         return None
@@ -194,12 +200,17 @@ def run_single(args):
                                   "evicts the 256 MiB Infinity Cache"},
     }
     if args.sweep:
+        # config 2's size range: back-to-back launches, wall time per launch (what a caller
+        # issuing one segment after another sees: dispatch-bound below ~1 Mi elements; per-launch
+        # HIP events would bottom out at their own ~6 us floor instead)
         sweep = []
         for k in range(12, 27, 2):
             nn = 1 << k
-            w, m, _ = time_chunk_sum(torch, L, dev, nn, code, 200, 20)
-            sweep.append({"elements": nn, "kernel_us": round(float(np.median(m)) * 1e3, 2),
-                          "GBps": round(12.0 * nn / (float(np.median(m)) * 1e-3) / 1e9, 1)})
+            reps = 400 if nn <= (1 << 22) else 100
+            w, _, _ = time_chunk_sum(torch, L, dev, nn, code, reps, 20)
+            us = w / reps * 1e6
+            sweep.append({"elements": nn, "us_per_launch": round(us, 2),
+                          "GBps": round(12.0 * nn / (us * 1e-6) / 1e9, 1)})
         out["sweep"] = sweep
     if not args.no_cpu_baseline:
         try:
