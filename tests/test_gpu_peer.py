@@ -161,3 +161,16 @@ def test_peer_from_c(gpu, P, n):
     out = r.stdout.decode() + r.stderr.decode()
     assert r.returncode == 0, out
     assert f"peer_capi P={P} n={n}: ok" in out
+
+
+@pytest.mark.parametrize("P,n", [(2, 1000003), (4, 262147)])
+def test_peer_algorithm_class_cpp(gpu, tmp_path, P, n):
+    """hydra::PeerAllreduce<T> (include/hydra/peer_allreduce.h) from C++ over the host runtime's
+    FileStore + TCP rendezvous (tests/cpp/peer_algo.cc): fp32 and int32, changing inputs every
+    run, every word exact on every rank."""
+    exe = os.path.join(ROOT, "tests", "cpp", "peer_algo")
+    assert os.path.exists(exe), "built by hydra_amd/csrc/Makefile (hydra_amd._lib.build())"
+    r = subprocess.run([exe, str(P), str(n), str(tmp_path)], capture_output=True, timeout=150)
+    out = r.stdout.decode() + r.stderr.decode()
+    assert r.returncode == 0, out
+    assert f"peer_algo P={P} n={n}: ok" in out
