@@ -35,7 +35,7 @@ EXPORTS = [  # every symbol include/hydra_hip.h declares
     "hydra_apipe_allreduce", "hydra_apipe_allreduce_simulate", "hydra_comm_run_plan",
     "hydra_peer_create", "hydra_peer_connect", "hydra_peer_register", "hydra_peer_open",
     "hydra_peer_close", "hydra_peer_set_option", "hydra_peer_error", "hydra_peer_allreduce",
-    "hydra_peer_destroy",
+    "hydra_peer_destroy", "hydra_comm_wait",
 ]
 
 (ALGO_AUTO, ALGO_RING, ALGO_DIRECT, ALGO_RCCL, ALGO_A2A, ALGO_RING_OLD, ALGO_RING_CHUNKED,
@@ -44,6 +44,7 @@ ALGOS = {"auto": ALGO_AUTO, "ring": ALGO_RING, "direct": ALGO_DIRECT, "rccl": AL
          "a2a": ALGO_A2A, "ring_old": ALGO_RING_OLD,
          "ring_chunked": ALGO_RING_CHUNKED, "bcube": ALGO_BCUBE}
 ACC_F32 = 1
+ERR_TIMEOUT = 5
 UNIQUE_ID_BYTES = 128
 # peer-access allreduce (hydra_peer_*)
 PEER_HANDLE_BYTES = 128
@@ -134,6 +135,7 @@ def _declare(L) -> None:
     L.hydra_peer_error.argtypes = [vp, ctypes.POINTER(i)]
     L.hydra_peer_allreduce.argtypes = [vp, i, i, i, i, vp, sz, sz, vp]
     L.hydra_peer_destroy.argtypes = [vp]
+    L.hydra_comm_wait.argtypes = [vp, vp, ctypes.c_int64]
 
 
 def lib():

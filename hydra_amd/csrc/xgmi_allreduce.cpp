@@ -14,8 +14,10 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <chrono>
 #include <cstring>
 #include <deque>
+#include <thread>
 #include <map>
 #include <string>
 #include <vector>
@@ -118,6 +120,7 @@ hipError_t launch_compute(const hydra::PlanOp& o, int op, int dtype, bool acc32,
 // ---- communicator ----------------------------------------------------------------------------
 struct hydra_comm {
   int rank = 0, nranks = 1, device = 0;
+  bool aborted = false;  // hydra_comm_wait timed out: nccl was aborted
   ncclComm_t nccl = nullptr;
   hipStream_t cs = nullptr, ks = nullptr;  // comm stream, compute stream
   void* scratch = nullptr;
@@ -261,6 +264,31 @@ int hydra_comm_init(hydra_comm_t* out, int nranks, int rank, const void* id, int
   return ok();
 }
 
+int hydra_comm_wait(hydra_comm_t c, hydra_stream_t stream, int64_t timeout_ms) {
+  if (!c) return fail(HYDRA_ERR_INVALID, "null comm");
+  if (c->aborted) return fail(HYDRA_ERR_TIMEOUT, "communicator was aborted by an earlier timeout");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int spin = 0;; spin++) {
+    const hipError_t q = hipStreamQuery(st);
+    if (q == hipSuccess) return ok();
+    if (q != hipErrorNotReady) return hydra::hip_fail(q, "hipStreamQuery");
+    ncclResult_t ae = ncclSuccess;
+    NCCL_TRY(ncclCommGetAsyncError(c->nccl, &ae));
+    const auto waited = std::chrono::duration_cast<std::chrono::milliseconds>(
+                            std::chrono::steady_clock::now() - t0).count();
+    if (ae != ncclSuccess || waited > timeout_ms) {
+      (void)ncclCommAbort(c->nccl);  // unblocks this rank's RCCL kernels
+      c->nccl = nullptr;
+      c->aborted = true;
+      if (ae != ncclSuccess) return nccl_fail(ae, "RCCL asynchronous error");
+      return fail(HYDRA_ERR_TIMEOUT, "Timed out waiting " + std::to_string(timeout_ms) +
+                                         "ms for allreduce to complete");
+    }
+    if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(50));
+  }
+}
+
 int hydra_comm_destroy(hydra_comm_t c) {
   if (!c) return ok();
   (void)hipSetDevice(c->device);
@@ -286,6 +314,7 @@ namespace {
 int prepare(hydra_comm* c, int* algo, int op, int dtype, int flags, void* buf, size_t n,
             size_t max_segment, size_t chunk_bytes, bool* skip) {
   if (!c) return fail(HYDRA_ERR_INVALID, "null comm");
+  if (c->aborted) return fail(HYDRA_ERR_TIMEOUT, "communicator was aborted by an earlier timeout");
   size_t es;
   int rc = check_plan_args(*algo, op, dtype, flags, &es);
   if (rc) return rc;
@@ -648,6 +677,7 @@ int hydra_comm_run_plan(hydra_comm_t c, const hydra_plan_op_t* ops, size_t nops,
                         int flags, void* buf, size_t buf_bytes, size_t scratch_bytes,
                         hydra_stream_t stream) {
   if (!c || (!ops && nops)) return fail(HYDRA_ERR_INVALID, "null argument");
+  if (c->aborted) return fail(HYDRA_ERR_TIMEOUT, "communicator was aborted by an earlier timeout");
   size_t es;
   int rc = check_plan_args(HYDRA_ALGO_RING, op, dtype, flags, &es);
   if (rc) return rc;

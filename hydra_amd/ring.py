@@ -149,6 +149,15 @@ class XgmiComm:
                                                code, flags, t.data_ptr(), _count(t, code),
                                                max_segment, chunk_bytes, s))
 
+    def wait(self, timeout_ms: int, stream: int | None = None) -> None:
+        """Block until the work enqueued on `stream` (default: current) is done; past timeout_ms
+        the communicator is aborted and HydraError(ERR_TIMEOUT, "Timed out waiting ...") is
+        raised -- the reference's per-op timeout (tcp/unbound_buffer.cc:60-85)."""
+        import torch
+
+        s = stream if stream is not None else torch.cuda.current_stream().cuda_stream
+        check(_lib.lib().hydra_comm_wait(self._h, s, int(timeout_ms)))
+
     def run_plan_(self, ops, t, scratch_bytes: int, op: str = "sum",
                   dtype_code: int | None = None, flags: int = 0,
                   stream: int | None = None) -> None:
@@ -454,6 +463,20 @@ def bench_allreduce(args, dev) -> dict:
         wall = timed_steps(step, args.steps, args.warmup, sync, dist.barrier)
         wall = max_over_ranks(wall, dev)
         ms = wall / args.steps * 1e3
+        # per-iteration latency as the reference's benchmark reports it (runner.cc:693-697:
+        # wall time around each run(), p50/p99 over the samples), outside the timed region
+        lat = []
+        for _ in range(max(5, min(50, args.steps))):
+            sync()
+            dist.barrier()
+            sync()
+            t0 = time.perf_counter()
+            step()
+            sync()
+            lat.append(time.perf_counter() - t0)
+        lat_ms = {"p50": round(max_over_ranks(float(np.percentile(lat, 50)), dev) * 1e3, 4),
+                  "p99": round(max_over_ranks(float(np.percentile(lat, 99)), dev) * 1e3, 4),
+                  "samples": len(lat), "note": "per step, synchronised, max over ranks"}
         # 4) context: the other algorithms on the same bucket (fewer steps)
         others = {}
         k = max(5, args.steps // 4)
@@ -535,6 +558,7 @@ def bench_allreduce(args, dev) -> dict:
                      "frac": round(busbw / (link * max(1, world - 1)), 4), "traffic": None,
                      "note": "busbw vs (P-1) xGMI links x 153 GB/s; a single ring is bound by "
                              "1 link (153 GB/s)"},
+        "latency_ms": lat_ms,
         "other_algos_ms": others,
         "config5_bf16": c5,
         "parity": {"fold_order_1M": parity, "full_size_exact": full_ok},

@@ -60,7 +60,8 @@ typedef enum {
   HYDRA_ERR_INVALID = 1,     /* bad argument (dtype, op, misaligned pointer, partial overlap) */
   HYDRA_ERR_HIP = 2,         /* HIP runtime error (message carries hipGetErrorString) */
   HYDRA_ERR_UNSUPPORTED = 3, /* op/dtype combination not provided */
-  HYDRA_ERR_NO_DEVICE = 4    /* no gfx950 device visible */
+  HYDRA_ERR_NO_DEVICE = 4,   /* no gfx950 device visible */
+  HYDRA_ERR_TIMEOUT = 5      /* hydra_comm_wait: the enqueued work did not finish in time */
 } hydra_status_t;
 
 typedef void* hydra_stream_t; /* hipStream_t; NULL = the legacy default stream */
@@ -186,6 +187,13 @@ int hydra_comm_init(hydra_comm_t* out, int nranks, int rank, const void* id, int
 int hydra_comm_destroy(hydra_comm_t comm);
 int hydra_allreduce(hydra_comm_t comm, int algo, int op, int dtype, int flags, void* buf,
                     size_t n, size_t max_segment, size_t chunk_bytes, hydra_stream_t stream);
+/* The reference's per-op timeout (AllreduceOptions::setTimeout, allreduce.h:52; waitRecv /
+ * waitSend(opts.timeout) -> IoException "Timed out waiting ...", tcp/unbound_buffer.cc:60-85)
+ * for the asynchronous device path: wait until everything enqueued on `stream` so far is done.
+ * Past `timeout_ms` the communicator is aborted (ncclCommAbort: no rank stays stuck in RCCL)
+ * and HYDRA_ERR_TIMEOUT is returned with "Timed out waiting <ms>ms for ..."; the communicator
+ * is then unusable (destroy it).  RCCL's asynchronous errors are reported the same way. */
+int hydra_comm_wait(hydra_comm_t comm, hydra_stream_t stream, int64_t timeout_ms);
 
 /* ---- bew_allreduce_a on device: two rails (pipeallreduce-a.cc:27-61) ---------------------- */
 #ifndef HYDRA_SPLIT_AA

@@ -430,3 +430,25 @@ def test_executor_graph_replay(gpu, O):
         assert np.array_equal(u.cpu().numpy().view(np.uint32), x.view(np.uint32))
     finally:
         comm.close()
+
+
+def test_comm_wait_timeout_aborts(gpu):
+    """hydra_comm_wait: the reference's per-op timeout for the asynchronous device path.  Work
+    that finishes in time returns; a stream held by a long spin kernel times out with
+    "Timed out waiting ...", the communicator is aborted and refuses further allreduces."""
+    import torch
+
+    comm = ring.XgmiComm(0, 1, gpu.index or 0, ring._rccl_unique_id())
+    try:
+        t = torch.ones(1 << 16, device=gpu)
+        comm.allreduce_(t, algo="rccl")
+        comm.wait(5000)
+        torch.cuda._sleep(500_000_000)  # 0.2-5 s of spinning (GPU clock or 100 MHz)
+        with pytest.raises(_lib.HydraError, match="Timed out waiting 50ms") as e:
+            comm.wait(50)
+        assert e.value.code == _lib.ERR_TIMEOUT
+        with pytest.raises(_lib.HydraError, match="aborted"):
+            comm.allreduce_(t, algo="direct")
+        torch.cuda.synchronize()
+    finally:
+        comm.close()
