@@ -433,8 +433,9 @@ def bench_allreduce(args, dev) -> dict:
         tuning = {}
         if algo == "auto":
             best = None
-            for a, ch in (("direct", 4 << 20), ("direct", 16 << 20), ("a2a", 0),
-                          ("ring", 4 << 20), ("peer2", 0), ("peer2", 256)):
+            for a, ch in (("direct", 1 << 20), ("direct", 4 << 20), ("direct", 16 << 20),
+                          ("direct", 64 << 20), ("a2a", 0), ("ring", 4 << 20), ("peer2", 0),
+                          ("peer2", 256), ("peer2", 128)):
                 if parity.get(a) != "bit-exact":
                     continue  # only schedules that reproduced the reference are eligible
                 try:
