@@ -15,6 +15,7 @@
 #include "../../include/hydra_hip.h"
 #include "errors.h"
 #include "reduce_kernels.h"
+#include "trace.h"
 
 namespace {
 thread_local std::string g_err;
@@ -237,6 +238,7 @@ void* mapped_device_ptr(const void* p) {
 
 int hydra_reduce_host(hydra_ctx_t ctx, int op, int dtype, void* c, const void* a, const void* b,
                       size_t n) {
+  hydra::TraceRange trace_("hydra_reduce_host");
   if (!ctx) return fail(HYDRA_ERR_INVALID, "null context");
   int rc = check_args(op, dtype, c, a, b, n);
   if (rc) return rc;

@@ -19,6 +19,7 @@
 #include "errors.h"
 #include "peer_kernels.h"
 #include "reduce_kernels.h"
+#include "trace.h"
 #include "xgmi_plan.h"
 
 using hydra::fail;
@@ -260,6 +261,7 @@ int hydra_peer_error(hydra_peer_t p, int* code) {
 
 int hydra_peer_allreduce(hydra_peer_t p, int algo, int op, int dtype, int flags, void* buf,
                          size_t n, size_t max_segment, hydra_stream_t stream) {
+  hydra::TraceRange trace_("hydra_peer_allreduce");
   if (!p) return fail(HYDRA_ERR_INVALID, "null peer");
   const size_t es = hydra::dtype_size(dtype);
   if (!es) return fail(HYDRA_ERR_INVALID, "invalid dtype");

@@ -26,6 +26,7 @@
 #include "errors.h"
 #include "reduce_kernels.h"
 #include "split_table.h"
+#include "trace.h"
 #include "xgmi_plan.h"
 
 using hydra::fail;
@@ -376,6 +377,7 @@ extern "C" {
 
 int hydra_allreduce(hydra_comm_t c, int algo, int op, int dtype, int flags, void* buf, size_t n,
                     size_t max_segment, size_t chunk_bytes, hydra_stream_t stream) {
+  hydra::TraceRange trace_("hydra_allreduce");
   bool skip = false;
   int rc = prepare(c, &algo, op, dtype, flags, buf, n, max_segment, chunk_bytes, &skip);
   if (rc || skip) return rc ? rc : ok();
@@ -397,6 +399,7 @@ void hydra_split_elements(int table, int P, size_t n, size_t* e1, size_t* e2) {
 int hydra_apipe_allreduce(hydra_comm_t rail1, hydra_comm_t rail2, int table, int algo, int op,
                           int dtype, int flags, void* buf, size_t n, size_t max_segment,
                           size_t chunk_bytes, hydra_stream_t stream) {
+  hydra::TraceRange trace_("hydra_apipe_allreduce");
   if (!rail1 || !rail2 || rail1 == rail2)
     return fail(HYDRA_ERR_INVALID, "apipe needs two distinct communicators");
   if (rail1->rank != rail2->rank || rail1->nranks != rail2->nranks ||

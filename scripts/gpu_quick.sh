@@ -1,4 +1,6 @@
 set -u
-mkdir -p gpurun_out/wait
-timeout -k 10 300 python -u -m pytest tests/test_gpu_xgmi.py -x -v -k "comm_wait or graph_replay" --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/wait/pytest.log 2>&1 || exit 1
-timeout -k 10 300 python -u bench.py --force-dist --steps 10 --warmup 2 --elements 16777216 > gpurun_out/wait/forcedist.log 2>&1 || exit 1
+O=gpurun_out/quick
+mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1 || { echo "pytest rc=$?"; exit 1; }
+timeout -k 10 300 rocprofv3 --marker-trace --kernel-trace --stats --output-format csv -d $O/mt -o run -- python3 bench.py --force-dist --steps 5 --warmup 1 --elements 4194304 --no-config5 > $O/mt.log 2>&1 || { echo "mt rc=$?"; exit 1; }
