@@ -561,6 +561,8 @@ def bench_allreduce(args, dev) -> dict:
                              "1 link (153 GB/s)"},
         "latency_ms": lat_ms,
         "other_algos_ms": others,
+        "other_algos_busbw_GBps": {a: round(bucket / (v * 1e-3) / 1e9 * 2 * (world - 1) / world, 2)
+                                   for a, v in others.items() if isinstance(v, float)},
         "config5_bf16": c5,
         "parity": {"fold_order_1M": parity, "full_size_exact": full_ok},
     }
