@@ -190,6 +190,99 @@ __global__ __launch_bounds__(kBlock) void k_reduce_lds(E* c_, const E* a_, const
 }
 
 // -------------------------------------------------------------------------------------------
+// Wavefront-shuffle realignment (the north star's "wavefront-shuffle" on gfx950).
+// An operand whose address is not co-aligned with c mod 16 B (the ring's tmp slot 1 sits at
+// +segmentBytes, a multiple of E only: allreduce.cc:236; user sub-buffers) is read with ALIGNED
+// 16-B loads only: lane i loads the aligned slot under the start of its window, receives slot
+// i+1 from lane i+1 through a DPP wave_shl:1 (one v_mov_dpp per dword, VALU, no LDS), and cuts
+// its window out of the 32-byte pair with v_alignbyte.  Lane 63's window reaches into the next
+// wave's first slot, so lane 63 alone reads its window directly (unaligned, within bounds).
+// -------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t wave_shl1(uint32_t x) {
+  // DPP_WF_SL1 (0x130, GFX9 family): lane i reads lane i+1; lane 63 keeps `old` (ignored)
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x130, 0xf, 0xf, false);
+}
+
+// bytes [k, k+16) of the 32-byte pair (x, y); k = 4q + r, 1 <= k <= 15, q and r wave-uniform
+__device__ __forceinline__ u32x4 realign(u32x4 x, u32x4 y, int q, uint32_t r) {
+  const uint32_t d[8] = {x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
+  auto cut = [&](auto Q) {  // constant dword offset: four v_alignbyte, no per-lane select
+    constexpr int s = decltype(Q)::value;
+    return u32x4{__builtin_amdgcn_alignbyte(d[s + 1], d[s], r),
+                 __builtin_amdgcn_alignbyte(d[s + 2], d[s + 1], r),
+                 __builtin_amdgcn_alignbyte(d[s + 3], d[s + 2], r),
+                 __builtin_amdgcn_alignbyte(d[s + 4], d[s + 3], r)};
+  };
+  switch (q) {  // wave-uniform: one scalar branch
+    case 0: return cut(std::integral_constant<int, 0>{});
+    case 1: return cut(std::integral_constant<int, 1>{});
+    case 2: return cut(std::integral_constant<int, 2>{});
+    default: return cut(std::integral_constant<int, 3>{});
+  }
+}
+
+// x = the aligned slot under this lane's window, u = lane 63's own window (unaligned load);
+// k = the operand's misalignment (wave-uniform).  Returns this lane's window.
+__device__ __forceinline__ u32x4 shfl_window(u32x4 x, u32x4 u, uint32_t k, int lane) {
+  if (k == 0) return x;
+  u32x4 y;
+#pragma unroll
+  for (int j = 0; j < 4; j++) y[j] = wave_shl1(x[j]);
+  const u32x4 o = realign(x, y, (int)(k >> 2), k & 3);
+  return lane == 63 ? u : o;
+}
+
+template <typename E, int OP, bool C_OLD>
+__global__ __launch_bounds__(kBlock) void k_reduce_shfl(E* c_, const E* a_, const E* b_,
+                                                        size_t nvec, int head, int tail) {
+  constexpr int N = Vec<E>::N;
+  constexpr size_t TILE = kBlock;  // one 16-B vector per lane per operand (the tuned default)
+  char* c = reinterpret_cast<char*>(c_);
+  const char* a = reinterpret_cast<const char*>(a_);
+  const char* b = reinterpret_cast<const char*>(b_);
+  const int t = threadIdx.x, lane = t & 63;
+  const uint32_t ka = __builtin_amdgcn_readfirstlane((uint32_t)((uintptr_t)a & 15));
+  const uint32_t kb = __builtin_amdgcn_readfirstlane((uint32_t)((uintptr_t)b & 15));
+
+  if (blockIdx.x == 0) {
+    if (t < head) {
+      const int i = t - head;
+      E ea = a_[i], eb = b_[i];
+      c_[i] = Elem<E, OP>::apply(ea, eb, C_OLD ? c_[i] : ea);
+    } else if (t >= 64 && t - 64 < tail) {
+      const size_t i = nvec * N + (size_t)(t - 64);
+      E ea = a_[i], eb = b_[i];
+      c_[i] = Elem<E, OP>::apply(ea, eb, C_OLD ? c_[i] : ea);
+    }
+  }
+
+  const size_t ntiles = (nvec + TILE - 1) / TILE;
+  size_t first = blockIdx.x;  // XCD-contiguous tiles, as the default
+  if ((gridDim.x & 7) == 0) first = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+  for (size_t tile = first; tile < ntiles; tile += gridDim.x) {
+    const size_t off = (tile * TILE + t) * 16;
+    if ((tile + 1) * TILE <= nvec) {  // full tile: every lane of every wave is live
+      // every load issued before the first use: aligned slots, then lane 63's own windows
+      u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a - ka + off));
+      u32x4 y = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(b - kb + off));
+      u32x4 ux = {0, 0, 0, 0}, uy = {0, 0, 0, 0};  // (not x/y: no wait on their loads)
+      if (lane == 63 && ka) ux = ld_u(a + off);
+      if (lane == 63 && kb) uy = ld_u(b + off);
+      u32x4 z;
+      if (C_OLD) z = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(c + off));
+      x = shfl_window(x, ux, ka, lane);
+      y = shfl_window(y, uy, kb, lane);
+      if (!C_OLD) z = x;  // the f16 store quirk's old bits are a's in the in-place form
+      const auto w = rsrc<kBuf | 16>(c + tile * TILE * 16, TILE * 16);
+      st<kBuf | 16>(c, w, (uint32_t)t * 16, vapply<E, OP>(x, y, z));
+    } else if (tile * TILE + t < nvec) {
+      u32x4 x = ld_u(a + off), y = ld_u(b + off);
+      st_a(c + off, vapply<E, OP>(x, y, C_OLD ? ld_u(c + off) : x));
+    }
+  }
+}
+
+// -------------------------------------------------------------------------------------------
 // bf16 bucket, fp32 accumulate (BASELINE config 5): acc[i] += float(b[i]); 10 B / element.
 // acc 16-B aligned (we own it), b element-aligned.  8 elements per lane per step.
 // -------------------------------------------------------------------------------------------
@@ -335,6 +428,24 @@ hipError_t launch_lds(void* c, const void* a, const void* b, size_t n, hipStream
   return hipGetLastError();
 }
 
+template <typename E, int OP>
+hipError_t launch_shfl(void* c, const void* a, const void* b, size_t n, hipStream_t s) {
+  const Split sp = split_call<E>(c, n);
+  E* cb = reinterpret_cast<E*>(c) + sp.head;
+  const E* ab = reinterpret_cast<const E*>(a) + sp.head;
+  const E* bb = reinterpret_cast<const E*>(b) + sp.head;
+  size_t grid = (sp.nvec + kBlock - 1) / kBlock;
+  if (grid == 0) grid = 1;
+  const bool c_old = Elem<E, OP>::kNeedsOld && c != a;
+  if (c_old)
+    hipLaunchKernelGGL((k_reduce_shfl<E, OP, true>), dim3((unsigned)grid), dim3(kBlock), 0, s, cb,
+                       ab, bb, sp.nvec, sp.head, sp.tail);
+  else
+    hipLaunchKernelGGL((k_reduce_shfl<E, OP, false>), dim3((unsigned)grid), dim3(kBlock), 0, s,
+                       cb, ab, bb, sp.nvec, sp.head, sp.tail);
+  return hipGetLastError();
+}
+
 // The tuned default (profiles/r01_tune_variants.json, r01_tune_xcd.json): one
 // 16-B vector per lane per operand, nontemporal loads, write-through (sc1) stores, tiles mapped
 // XCD-contiguously -- 108.2 us for 64 Mi fp32 in place back to back (7.44 TB/s), 6.3-6.4 TB/s
@@ -393,6 +504,7 @@ hipError_t launch_tuning(int variant, void* c, const void* a, const void* b, siz
     case 41: return launch_t<E, OP, 1, kNT, B | 18, kBlock, 1>(c, a, b, n, s, 0);  // 36, XCD map
     case 42: return launch_t<E, OP, 1, kNT, kNT, kBlock, 1>(c, a, b, n, s, 0);     // 17, XCD map
     case 43: return launch_t<E, OP, 2, kNT, B | 16, kBlock, 1>(c, a, b, n, s, 0);  // 34, XCD map
+    case 44: return launch_shfl<E, OP>(c, a, b, n, s);  // 40 + aligned loads, DPP realignment
     default: return launch_default<E, OP>(c, a, b, n, s);
   }
 }

@@ -21,23 +21,26 @@ res = {}
 s = torch.cuda.current_stream(dev)
 for n in sizes:
     a = torch.rand(n, device=dev)
-    b = torch.rand(n, device=dev)
+    b = torch.rand(n + 4, device=dev)
     c = torch.empty(n, device=dev)
     flush = torch.empty(1 << 28, dtype=torch.float32, device=dev)  # 1 GiB: evicts the 256 MiB MALL
     for mode in os.environ.get("MODES", "inplace,outofplace").split(","):
         pc = c.data_ptr() if mode == "outofplace" else a.data_ptr()
+        # misalign: in place, b one element past 16-B alignment (the ring's tmp slot 1 at
+        # +segmentBytes, allreduce.cc:236, when segmentBytes is not a multiple of 16)
+        pb = b.data_ptr() + (4 if mode == "misalign" else 0)
         for r in range(rounds):
             for v in variants:
                 L.hydra_set_variant(v)
                 for _ in range(3):
-                    _lib.check(L.hydra_chunk_sum(6, pc, a.data_ptr(), b.data_ptr(), n, s.cuda_stream))
+                    _lib.check(L.hydra_chunk_sum(6, pc, a.data_ptr(), pb, n, s.cuda_stream))
                 ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                       for _ in range(reps)]
                 for e0, e1 in ev:
                     if mode == "cold":
                         flush.fill_(1.0)
                     e0.record(s)
-                    _lib.check(L.hydra_chunk_sum(6, pc, a.data_ptr(), b.data_ptr(), n, s.cuda_stream))
+                    _lib.check(L.hydra_chunk_sum(6, pc, a.data_ptr(), pb, n, s.cuda_stream))
                     e1.record(s)
                 torch.cuda.synchronize()
                 t = float(np.median([e0.elapsed_time(e1) for e0, e1 in ev])) * 1e3

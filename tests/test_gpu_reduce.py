@@ -152,7 +152,7 @@ def test_f16_out_of_place_old_bits(dev, O):
     assert np.array_equal(c, exp)
 
 
-@pytest.mark.parametrize("variant", list(range(44)))
+@pytest.mark.parametrize("variant", list(range(45)))
 def test_variants_equal(dev, O, variant):
     rng = np.random.default_rng(variant)
     for n in (1, 77, 4096 + 3, 1 << 20, (1 << 21) + 5):
@@ -160,6 +160,28 @@ def test_variants_equal(dev, O, variant):
         b = rng.standard_normal(n).astype(np.float32)
         c = dev_reduce(dev, "sum", 6, a, b, offs=(4, 4, 8), variant=variant)
         assert np.array_equal(bits(c), bits(O.op(a, b, "sum", 6)))
+
+
+@pytest.mark.parametrize("code,dt", [(6, np.float32), (2, np.int32)])
+def test_shuffle_realign_every_offset(dev, O, code, dt):
+    """Variant 44 (aligned loads + DPP wave_shl realignment) at every relative misalignment of
+    a and b against c, in and out of place, over sizes spanning many full 256-vector tiles."""
+    rng = np.random.default_rng(44)
+    for n in (5, 1025, 4 * 1024 + 3, (1 << 20) + 7):
+        if code == 6:
+            a = rng.standard_normal(n).astype(dt)
+            b = rng.standard_normal(n).astype(dt)
+        else:
+            a = rng.integers(-(1 << 30), 1 << 30, n).astype(dt)
+            b = rng.integers(-(1 << 30), 1 << 30, n).astype(dt)
+        exp = O.op(a, b, "sum", code)
+        for oa in (0, 4, 8, 12):
+            for ob in (0, 4, 8, 12):
+                c = dev_reduce(dev, "sum", code, a, b, offs=(0, oa, ob), variant=44)
+                assert np.array_equal(bits(c), bits(exp)), (n, oa, ob, "inplace")
+                c = dev_reduce(dev, "sum", code, a, b, c0=a.copy(), offs=(8, oa, ob),
+                               inplace=False, variant=44)
+                assert np.array_equal(bits(c), bits(exp)), (n, oa, ob, "out of place")
 
 
 @pytest.mark.parametrize("name,code,dt", [("f32", 6, np.float32), ("i32", 2, np.int32)])
