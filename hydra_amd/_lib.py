@@ -35,7 +35,7 @@ EXPORTS = [  # every symbol include/hydra_hip.h declares
     "hydra_apipe_allreduce", "hydra_apipe_allreduce_simulate", "hydra_comm_run_plan",
     "hydra_peer_create", "hydra_peer_connect", "hydra_peer_register", "hydra_peer_open",
     "hydra_peer_close", "hydra_peer_set_option", "hydra_peer_error", "hydra_peer_allreduce",
-    "hydra_peer_destroy", "hydra_comm_wait",
+    "hydra_peer_detach", "hydra_peer_destroy", "hydra_comm_wait",
 ]
 
 (ALGO_AUTO, ALGO_RING, ALGO_DIRECT, ALGO_RCCL, ALGO_A2A, ALGO_RING_OLD, ALGO_RING_CHUNKED,
@@ -134,6 +134,7 @@ def _declare(L) -> None:
     L.hydra_peer_set_option.argtypes = [vp, i, ctypes.c_longlong]
     L.hydra_peer_error.argtypes = [vp, ctypes.POINTER(i)]
     L.hydra_peer_allreduce.argtypes = [vp, i, i, i, i, vp, sz, sz, vp]
+    L.hydra_peer_detach.argtypes = [vp]
     L.hydra_peer_destroy.argtypes = [vp]
     L.hydra_comm_wait.argtypes = [vp, vp, ctypes.c_int64]
 

@@ -10,6 +10,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <string>
@@ -66,6 +68,7 @@ struct hydra_peer {
   };
   std::vector<Reg> regs;
   std::map<std::string, Mapping> opened;  // ipc handle bytes -> mapping (one per allocation)
+  bool detached = false;                  // hydra_peer_detach ran: no mappings left
 };
 
 namespace {
@@ -78,6 +81,9 @@ int export_blob(hydra_peer* p, void* ptr, size_t bytes, void* out) {
   const char* q = static_cast<const char*>(ptr);
   if (q < b || q + bytes > b + size)
     return fail(HYDRA_ERR_INVALID, "buffer is not inside one device allocation");
+  if (std::getenv("HYDRA_PEER_DEBUG"))
+    std::fprintf(stderr, "[hydra_peer] rank %d export %p (+%zu) in allocation [%p, +%zu)\n",
+                 p->rank, ptr, bytes, base, size);
   hipIpcMemHandle_t h;
   HIP_TRY(hipIpcGetMemHandle(&h, base));
   Blob blob{};
@@ -108,6 +114,9 @@ int open_mapping(hydra_peer* p, const Blob& b, std::string* key, char** base) {
     std::memcpy(&h, b.ipc, kIpcBytes);
     void* m = nullptr;
     HIP_TRY(hipIpcOpenMemHandle(&m, h, hipIpcMemLazyEnablePeerAccess));
+    if (std::getenv("HYDRA_PEER_DEBUG"))
+      std::fprintf(stderr, "[hydra_peer] rank %d mapped rank %d's allocation (+%llu B) at %p\n",
+                   p->rank, b.rank, (unsigned long long)b.bytes, m);
     it = p->opened.emplace(*key, Mapping{m, 0}).first;
   }
   it->second.refs++;
@@ -263,6 +272,7 @@ int hydra_peer_allreduce(hydra_peer_t p, int algo, int op, int dtype, int flags,
                          size_t n, size_t max_segment, hydra_stream_t stream) {
   hydra::TraceRange trace_("hydra_peer_allreduce");
   if (!p) return fail(HYDRA_ERR_INVALID, "null peer");
+  if (p->detached) return fail(HYDRA_ERR_INVALID, "peer group detached");
   const size_t es = hydra::dtype_size(dtype);
   if (!es) return fail(HYDRA_ERR_INVALID, "invalid dtype");
   if (op < HYDRA_SUM || op > HYDRA_MIN) return fail(HYDRA_ERR_INVALID, "invalid op");
@@ -331,12 +341,23 @@ int hydra_peer_allreduce(hydra_peer_t p, int algo, int op, int dtype, int flags,
   return ok();
 }
 
-int hydra_peer_destroy(hydra_peer_t p) {
-  if (!p) return ok();
+int hydra_peer_detach(hydra_peer_t p) {
+  if (!p) return fail(HYDRA_ERR_INVALID, "null peer");
+  if (p->detached) return ok();
   (void)hipSetDevice(p->device);
-  (void)hipDeviceSynchronize();
+  (void)hipDeviceSynchronize();  // no kernel of ours may still read through the mappings
   for (auto& kv : p->opened) (void)hipIpcCloseMemHandle(kv.second.base);
   p->opened.clear();
+  p->regs.clear();
+  for (int q = 0; q < p->P; q++)
+    if (q != p->rank) p->sigs.p[q] = nullptr;
+  p->detached = true;
+  return ok();
+}
+
+int hydra_peer_destroy(hydra_peer_t p) {
+  if (!p) return ok();
+  (void)hydra_peer_detach(p);  // local; callers detach + barrier first (hydra_hip.h)
   if (p->scratch) (void)hipFree(p->scratch);
   if (p->sig) (void)hipFree(p->sig);
   if (p->err_host) (void)hipHostFree(p->err_host);

@@ -103,8 +103,12 @@ class PeerComm:
         self._registered[t.data_ptr()] = nbytes
 
     def unregister(self, t) -> None:
-        check(_lib.lib().hydra_peer_close(self._h, t.data_ptr()))
+        """Collective: every rank closes its mappings of t's peers, then all meet, so t (on
+        any rank) may be freed once this returns (teardown rule in include/hydra_hip.h)."""
+        rc = _lib.lib().hydra_peer_close(self._h, t.data_ptr())
         self._registered.pop(t.data_ptr(), None)
+        _agree(rc == 0, self.group)
+        check(rc)
 
     def allreduce_(self, t, algo: str = "peer2", op: str = "sum", dtype_code: int | None = None,
                    flags: int = 0, max_segment: int = 0, stream: int | None = None) -> None:
@@ -128,8 +132,17 @@ class PeerComm:
         check(_lib.lib().hydra_peer_error(self._h, ctypes.byref(c)))
         return c.value
 
-    def close(self) -> None:
+    def close(self, collective: bool = True) -> None:
+        """Collective teardown (include/hydra_hip.h): detach every mapping of the other ranks'
+        memory, meet them, then free this rank's signal area -- no rank ever frees memory a
+        peer still maps.  collective=False (garbage collection) skips the meeting."""
         if self._h:
+            _lib.lib().hydra_peer_detach(self._h)
+            if collective:
+                try:
+                    _agree(True, self.group)
+                except Exception:  # the process group is gone: nobody left to wait for
+                    pass
             _lib.lib().hydra_peer_destroy(self._h)
             self._h = ctypes.c_void_p()
 
@@ -137,6 +150,6 @@ class PeerComm:
         if _is_finalizing():  # no HIP calls while the interpreter is finalizing
             return
         try:
-            self.close()
+            self.close(collective=False)
         except Exception:
             pass

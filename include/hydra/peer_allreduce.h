@@ -68,8 +68,20 @@ class PeerAllreduce {
     enforce(hydra_peer_open(peer_, ptr_, bytes(), hs.data()));
   }
 
+  // Collective, like the constructor: every rank closes its mappings of the others' memory,
+  // meets the others, and only then frees its own signal area -- so once the destructor
+  // returns on any rank, no rank maps that rank's bucket any more and the caller may free it
+  // (hydra_hip.h, teardown rule).
   ~PeerAllreduce() {
-    if (peer_) hydra_peer_destroy(peer_);
+    if (peer_) {
+      hydra_peer_detach(peer_);
+      try {
+        const char c = 0;
+        (void)detail::allgather_blob(*ctx_, &c, 1, slot(2));
+      } catch (...) {  // a dead peer: nothing left to wait for
+      }
+      hydra_peer_destroy(peer_);
+    }
     if (synchronous_ && stream_) hydra_stream_destroy(stream_);
   }
   PeerAllreduce(const PeerAllreduce&) = delete;

@@ -271,6 +271,16 @@ int hydra_peer_error(hydra_peer_t peer, int* code); /* 0 = healthy */
 /* buf must lie inside a buffer opened with hydra_peer_open, at the same offset on every rank */
 int hydra_peer_allreduce(hydra_peer_t peer, int algo, int op, int dtype, int flags, void* buf,
                          size_t n, size_t max_segment, hydra_stream_t stream);
+/* Teardown is collective, in this order on every rank:
+ *   hydra_peer_detach  (closes every mapping this rank holds of the other ranks' memory)
+ *   -> a barrier on the caller's channel
+ *   -> hydra_peer_destroy (frees this rank's signal area), and only then free the buckets.
+ * A rank never frees memory another rank still has mapped.  detach is local and idempotent;
+ * allreduce calls fail once it ran.  hydra_peer_close(buf) has the same rule per buffer: close
+ * on every rank, barrier, then free.  Register long-lived buckets: freeing a registered
+ * allocation and registering a new one in the same process intermittently gave a peer a
+ * mapping of the wrong memory on ROCm 7.2. */
+int hydra_peer_detach(hydra_peer_t peer);
 int hydra_peer_destroy(hydra_peer_t peer);
 
 #ifdef __cplusplus

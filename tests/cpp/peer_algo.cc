@@ -18,11 +18,15 @@
 
 namespace {
 
+// `dev` outlives every group that registers it: freeing a registered allocation and
+// registering a new one in the same process intermittently gave a peer a mapping of the wrong
+// memory on ROCm 7.2, so buckets are allocated once per process, as a
+// framework's caching allocator keeps them.
 template <typename T>
-int check_type(const std::shared_ptr<hydra::Context>& ctx, size_t n, int algo, size_t ms) {
+int check_type(const std::shared_ptr<hydra::Context>& ctx, void* dev, size_t n, int algo,
+               size_t ms) {
   const int P = ctx->size, r = ctx->rank;
-  void* dev = nullptr;
-  hydra::gloo_compat::enforce(hydra_malloc(0, n * sizeof(T), &dev));
+
   int bad = 0;
   {
     hydra::PeerAllreduce<T> ar(ctx, static_cast<T*>(dev), n, nullptr, algo, ms);
@@ -32,14 +36,23 @@ int check_type(const std::shared_ptr<hydra::Context>& ctx, size_t n, int algo, s
       hydra::gloo_compat::enforce(hydra_memcpy(dev, h.data(), n * sizeof(T)));
       ar.run();
       hydra::gloo_compat::enforce(hydra_memcpy(h.data(), dev, n * sizeof(T)));
-      for (size_t i = 0; i < n; i++)
-        bad += h[i] != (T)((i % 1000) * (size_t)(P * (P + 1) / 2) + it * (P * (P + 3) / 2));
+      int b0 = 0;
+      size_t first = n;
+      for (size_t i = 0; i < n; i++) {
+        const T want = (T)((i % 1000) * (size_t)(P * (P + 1) / 2) + it * (P * (P + 3) / 2));
+        if (h[i] != want) {
+          if (!b0) first = i;
+          b0++;
+        }
+      }
+      if (b0)
+        std::printf("rank %d: %s n=%zu algo=%d it=%d: %d wrong, first at %zu (got %g want %g)\n",
+                    r, sizeof(T) == 4 && (T)0.5 ? "f32" : "i32", n, algo, it, b0, first,
+                    (double)h[first],
+                    (double)(T)((first % 1000) * (size_t)(P * (P + 1) / 2) + it * (P * (P + 3) / 2)));
+      bad += b0;
     }
-    // every rank is done reading every mapping before anyone's bucket goes away
-    char c = 0;
-    (void)hydra::detail::allgather_blob(*ctx, &c, 1, (uint64_t(0x14) << 56) | (uint64_t)algo);
   }
-  hydra_free(dev);
   return bad;
 }
 
@@ -48,9 +61,18 @@ int run(int rank, int P, size_t n, const std::string& dir) {
     hydra::FileStore store(dir);
     auto ctx = std::make_shared<hydra::Context>(rank, P);
     ctx->connectFullMesh(store, "127.0.0.1");
-    int bad = check_type<float>(ctx, n, HYDRA_PEER_AUTO, 0);
-    bad += check_type<int32_t>(ctx, n / 3 + 7, HYDRA_PEER_TWO_SHOT, 4096);
-    bad += check_type<int32_t>(ctx, 5003, HYDRA_PEER_ONE_SHOT, 4096);
+    const size_t n2 = n / 3 + 7, n3 = 5003;
+    void *d1 = nullptr, *d2 = nullptr, *d3 = nullptr;
+    hydra::gloo_compat::enforce(hydra_malloc(0, n * sizeof(float), &d1));
+    hydra::gloo_compat::enforce(hydra_malloc(0, n2 * sizeof(int32_t), &d2));
+    hydra::gloo_compat::enforce(hydra_malloc(0, n3 * sizeof(int32_t), &d3));
+    int bad = check_type<float>(ctx, d1, n, HYDRA_PEER_AUTO, 0);
+    bad += check_type<int32_t>(ctx, d2, n2, HYDRA_PEER_TWO_SHOT, 4096);
+    bad += check_type<int32_t>(ctx, d3, n3, HYDRA_PEER_ONE_SHOT, 4096);
+    // ~PeerAllreduce was collective: no rank maps these any more
+    hydra_free(d1);
+    hydra_free(d2);
+    hydra_free(d3);
     std::printf("rank %d: mismatches=%d\n", rank, bad);
     std::fflush(stdout);
     return bad ? 1 : 0;

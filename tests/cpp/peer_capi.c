@@ -71,7 +71,8 @@ static int run(int rank, int P, size_t n) {
   CK(hydra_peer_error(peer, &err));
   for (i = 0; i < n; i++)
     bad += host[i] != (float)((i % 1000) * (size_t)(P * (P + 1) / 2));
-  /* everyone done with every mapping before anyone frees */
+  /* collective teardown (hydra_hip.h): detach, barrier, then destroy and free */
+  CK(hydra_peer_detach(peer));
   if (gather(rank, h, all)) return 3;
   CK(hydra_peer_destroy(peer));
   CK(hydra_free(buf));

@@ -54,6 +54,10 @@ class FakeLib:
     def hydra_peer_set_option(self, h, k, v):
         return 0
 
+    def hydra_peer_detach(self, h):
+        self.calls.append("detach")
+        return 0
+
     def hydra_peer_destroy(self, h):
         return 0
 
