@@ -452,3 +452,37 @@ def test_comm_wait_timeout_aborts(gpu):
         torch.cuda.synchronize()
     finally:
         comm.close()
+
+
+@pytest.mark.parametrize("algo", ["direct", "ring", "a2a"])
+def test_simulated_config4_full_size(gpu, algo):
+    """BASELINE config 4 at its full size (8 ranks x 64 Mi fp32) through a size-independent
+    property: integer-valued inputs whose sums are exact in fp32 in any order, so every rank
+    must hold exactly sum_r x_r -- the full-size companion of the bit-exact fold-order tests."""
+    import torch
+
+    P, n = 8, 64 << 20
+    j = torch.arange(n, device=gpu, dtype=torch.int64) % 1024
+    bufs = [(j * (r + 1)).to(torch.float32) for r in range(P)]
+    exp = (j * (P * (P + 1) // 2)).to(torch.float32)
+    del j
+    ring.simulate(bufs, algo=algo)
+    for r, b in enumerate(bufs):
+        assert torch.equal(b, exp), (algo, r)
+
+
+def test_simulated_config5_full_size(gpu):
+    """BASELINE config 5 at its full size (8 ranks x 256 Mi bf16, fp32 accumulation): small
+    integer inputs make every partial sum exact, so the one final rounding to bf16 is exact
+    and every rank must hold sum_r x_r bit for bit."""
+    import torch
+
+    P, n = 8, 256 << 20
+    base = (torch.arange(n, device=gpu, dtype=torch.int32) % 7 - 3)
+    m = [1, 2, -1, 3, -2, 1, 0, 2]  # |partial sums| <= 88: exact in fp32 and in bf16
+    bufs = [(base * m[r] + r % 3).to(torch.bfloat16).view(torch.int16) for r in range(P)]
+    exp = sum(base * m[r] + r % 3 for r in range(P)).to(torch.bfloat16)
+    del base
+    ring.simulate(bufs, algo="direct", dtype_code=_lib.BFLOAT16, flags=_lib.ACC_F32)
+    for r, b in enumerate(bufs):
+        assert torch.equal(b.view(torch.bfloat16), exp), r
