@@ -164,7 +164,15 @@ def cpu_baseline(n_total, seconds):
             k += 1
         per = (time.perf_counter() - t0) / k
     gbs = 12.0 * sample_n / per / 1e9
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")),
+                         None)
+    except OSError:
+        pass
     return {"value": round(gbs, 3), "unit": "GB/s", "cores": 1, "kind": kind,
+            "host_cpu": model, "host_logical_cpus": os.cpu_count(),
             "sample": f"gloo::sum<float> in place over 16 Mi fp32 (12 B/element), "
                       f"single thread, ~{seconds:.0f} s of repetitions, best-of-3 mean",
             "per_call_ms_at_64Mi": round(per * 4 * 1e3, 2)}
