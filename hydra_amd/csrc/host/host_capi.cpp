@@ -281,6 +281,55 @@ void hydra_host_calculate_elements(int table, int P, size_t n, size_t* e1, size_
                            P, n, e1, e2);
 }
 
+int hydra_host_reduce_threads(int P, int op, int dtype, size_t n, void** in, void** out,
+                              int root, size_t max_segment, int reducer, hydra_reduce_fn fn,
+                              long timeout_ms, char* err, size_t errlen) {
+  const size_t es = esize_of(dtype);
+  if (!es || P < 1 || !out) {
+    set_err(err, errlen, "invalid arguments");
+    return 2;
+  }
+  return spawn(P, 1, err, errlen, [&](int r, std::vector<std::shared_ptr<hydra::Context>>& c) {
+    hydra::ReduceOptions o(c[0]);
+    if (in) o.setInputRaw(in[r], n, es);
+    o.setOutputRaw(out[r], n, es);
+    o.setRoot(root);
+    int red = reducer;
+    if (red == HYDRA_REDUCER_GPU_PINNED) {
+      c[0]->setScratchAllocator({&hydra::gloo_compat::pinnedAlloc, &hydra::gloo_compat::pinnedFree});
+      red = HYDRA_REDUCER_GPU;
+    }
+    o.setReduceFunction(make_reducer(red, op, dtype, fn));
+    if (max_segment) o.setMaxSegmentSize(max_segment);
+    if (timeout_ms > 0) o.setTimeout(std::chrono::milliseconds(timeout_ms));
+    hydra::reduce(o);
+  });
+}
+
+int hydra_host_reduce_timeout_probe(long timeout_ms, char* what, size_t len) {
+  int rc = 3;
+  spawn(2, 1, nullptr, 0, [&](int r, std::vector<std::shared_ptr<hydra::Context>>& c) {
+    if (r != 0) return;  // ReduceTest.TestTimeout (reduce_test.cc:91-108): rank 1 never joins
+    uint64_t buf = 0;
+    hydra::ReduceOptions o(c[0]);
+    o.setOutput(&buf, 1);
+    o.setRoot(0);
+    o.setReduceFunction([](void* x, const void* a, const void* b, size_t n) {
+      for (size_t i = 0; i < n; i++)
+        static_cast<uint64_t*>(x)[i] =
+            static_cast<const uint64_t*>(a)[i] + static_cast<const uint64_t*>(b)[i];
+    });
+    o.setTimeout(std::chrono::milliseconds(timeout_ms));
+    try {
+      hydra::reduce(o);
+    } catch (const hydra::IoException& e) {
+      set_err(what, len, e.what());
+      rc = 0;
+    }
+  });
+  return rc;
+}
+
 int hydra_host_timeout_probe(long timeout_ms, char* what, size_t len) {
   int rc = 3;
   spawn(2, 1, nullptr, 0, [&](int r, std::vector<std::shared_ptr<hydra::Context>>& c) {

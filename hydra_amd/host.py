@@ -39,6 +39,9 @@ def lib():
         L.hydra_host_hip_ring_threads.argtypes = [i, i, i, sz, vp, i, i, ctypes.c_char_p, sz]
         L.hydra_host_allreduce_ring_chunked_threads.argtypes = \
             L.hydra_host_allreduce_ring_old_threads.argtypes
+        L.hydra_host_reduce_threads.argtypes = [i, i, i, sz, vp, vp, i, sz, i, vp,
+                                                ctypes.c_long, ctypes.c_char_p, sz]
+        L.hydra_host_reduce_timeout_probe.argtypes = [ctypes.c_long, ctypes.c_char_p, sz]
         _h = L
     return _h
 
@@ -79,6 +82,34 @@ def allreduce_threads(outs, ins=None, dtype_code=None, op="sum", max_segment=0, 
     if rc:
         raise _lib.HydraError(rc, err.value.decode())
     return outs
+
+
+def reduce_threads(outs, ins=None, root=0, dtype_code=None, op="sum", max_segment=0,
+                   reducer_fn=None, timeout_ms=0, pinned_scratch=False):
+    """gloo::reduce (reduce.cc:21-262) to `root` on len(outs) thread-ranks; outs/ins: one numpy
+    array per rank (ins None: in place).  Only outs[root] is the reduction."""
+    P, n = len(outs), outs[0].size
+    code = dtype_code if dtype_code is not None else _np_code(outs[0].dtype)
+    red, fp = _fn(reducer_fn)
+    if pinned_scratch:
+        if reducer_fn is not None:
+            raise _lib.HydraError(1, "pinned_scratch applies to the GPU reducer")
+        red = 2
+    err = ctypes.create_string_buffer(512)
+    rc = lib().hydra_host_reduce_threads(
+        P, _lib.OPS[op], code, n,
+        ctypes.cast(_ptrs(ins), ctypes.c_void_p) if ins is not None else None,
+        ctypes.cast(_ptrs(outs), ctypes.c_void_p), root, max_segment, red, fp, timeout_ms,
+        err, 512)
+    if rc:
+        raise _lib.HydraError(rc, err.value.decode())
+    return outs
+
+
+def reduce_timeout_probe(ms: int):
+    what = ctypes.create_string_buffer(512)
+    rc = lib().hydra_host_reduce_timeout_probe(ms, what, 512)
+    return rc, what.value.decode()
 
 
 def apipe_threads(ins, outs, table=SPLIT_AA, reducer_fn=None, dtype_code=_lib.FLOAT32):

@@ -193,6 +193,51 @@ class AllreduceOptions {
 
 void allreduce(const AllreduceOptions& opts);
 
+// ---- new-style reduce to a root (gloo/gloo/reduce.h:20-110, reduce.cc:21-262) -------------
+// The other new-style caller of the reduce function (reduce.cc:195): a ring reduce-scatter
+// with reduce(out + off, in + off, tmp, n), then every rank sends its chunk to the root.  Only
+// the root's output is defined; the other ranks' outputs hold what the reference's schedule
+// leaves there (reproduced too).
+class ReduceOptions {
+ public:
+  using Func = AllreduceOptions::Func;
+  static constexpr size_t kMaxSegmentSize = 1024 * 1024;  // reduce.h:92
+
+  explicit ReduceOptions(const std::shared_ptr<Context>& context)
+      : context(context), timeout(context->getTimeout()) {}
+
+  template <typename T>
+  void setInput(T* ptr, size_t n) { setInputRaw(ptr, n, sizeof(T)); }
+  template <typename T>
+  void setOutput(T* ptr, size_t n) { setOutputRaw(ptr, n, sizeof(T)); }
+  void setInputRaw(void* ptr, size_t n, size_t esize) {
+    elements = n;
+    elementSize = esize;
+    in = context->createUnboundBuffer(ptr, n * esize);
+  }
+  void setOutputRaw(void* ptr, size_t n, size_t esize) {
+    elements = n;
+    elementSize = esize;
+    out = context->createUnboundBuffer(ptr, n * esize);
+  }
+  void setRoot(int r) { root = r; }
+  void setReduceFunction(Func fn) { reduce = std::move(fn); }
+  void setTag(uint32_t t) { tag = t; }
+  void setMaxSegmentSize(size_t s) { maxSegmentSize = s; }
+  void setTimeout(std::chrono::milliseconds t) { timeout = t; }
+
+  std::shared_ptr<Context> context;
+  std::chrono::milliseconds timeout;
+  std::unique_ptr<UnboundBuffer> in, out;
+  size_t elements = 0, elementSize = 0;
+  int root = -1;
+  Func reduce;
+  uint32_t tag = 0;
+  size_t maxSegmentSize = kMaxSegmentSize;
+};
+
+void reduce(ReduceOptions& opts);
+
 // ---- bew_allreduce_a: the buffer split over two rails, two concurrent rings ----------------
 enum class SplitTable { AA, AG };  // calculateElements_AA (default) / _AG (env ALLREDUCE_GLEX)
 void calculateElements(SplitTable t, int P, size_t n, size_t* e1, size_t* e2);

@@ -73,6 +73,16 @@ int hydra_host_allreduce_ring_chunked_threads(int P, int nptr, int dtype, size_t
                                               int reducer, hydra_inplace_fn fn, char* err,
                                               size_t errlen);
 
+/* gloo::reduce (reduce.cc:21-262) to `root` on P thread-ranks.  in/out: P pointers each
+ * (in == NULL: in place on out, reduce_test.cc:27-33).  Every rank's out is left as the
+ * reference's schedule leaves it; only the root's is the reduction. */
+int hydra_host_reduce_threads(int P, int op, int dtype, size_t n, void** in, void** out,
+                              int root, size_t max_segment, int reducer, hydra_reduce_fn fn,
+                              long timeout_ms, char* err, size_t errlen);
+
+/* ReduceTest.TestTimeout (reduce_test.cc:91-108): root 0 of 2 alone, IoException text. */
+int hydra_host_reduce_timeout_probe(long timeout_ms, char* what, size_t len);
+
 /* AllreduceNewTest.TestTimeout (allreduce_test.cc:381-397): rank 0 of 2 times out; returns 0 and
  * the IoException text if it was raised. */
 int hydra_host_timeout_probe(long timeout_ms, char* what, size_t len);

@@ -250,6 +250,69 @@ def gen_new_test(meta: dict) -> None:
     meta["allreduce_new_test_closed_form_cases"] = checked
 
 
+REDUCE_CASES = [(P, n, ms) for P in (1, 2, 3, 4, 7) for n in (1, 10, 100, 1000, 4099)
+                for ms in (128, 1 << 20)]
+
+
+def gen_reduce(out: dict, meta: dict) -> None:
+    """gloo::reduce (reduce.cc:21-262) to a root: fp32 stress inputs, in place and out of
+    place (outputs start zeroed, as ReduceTest clears them: reduce_test.cc:50-56).  Every
+    rank's output is stored for n <= 1000 (non-root outputs are whatever the reference's
+    schedule leaves there); the root's only for n = 4099.  Plus int32 and in-place float16."""
+    rows = []
+    for (P, n, ms) in REDUCE_CASES:
+        for inplace in (True, False):
+            root = (n + P) % P  # varies with the case
+            xs = [synth.stress_f32(P, r, n) for r in range(P)]
+            if inplace:
+                outs, ins = [x.copy() for x in xs], None
+            else:
+                outs, ins = [np.zeros(n, np.float32) for _ in xs], [x.copy() for x in xs]
+            O.ref_reduce(outs, ins, root, max_segment=ms)
+            key = f"reduce_f32_P{P}_n{n}_ms{ms}_{'in' if inplace else 'out'}"
+            if n <= 1000:
+                out[key] = np.stack(outs)
+            else:
+                out[key + "_root"] = outs[root]
+            rows.append({"P": P, "n": n, "max_segment": ms, "inplace": inplace, "root": root,
+                         "key": key, "inputs_sha256": sha(np.stack(xs)),
+                         "root_sha256": sha(outs[root])})
+    for (P, n, dt, code) in [(3, 1000, np.int32, 2), (4, 4099, np.int32, 2),
+                             (3, 1000, np.uint16, 8), (7, 999, np.uint16, 8)]:
+        if code == 2:
+            xs = [synth.int32_bucket(P, r, n) for r in range(P)]
+        else:
+            rng = np.random.default_rng(P * 1000 + n)
+            xs = [np.array([O.f2h(float(v)) for v in rng.uniform(-8, 8, n)], np.uint16)
+                  for _ in range(P)]
+        outs = [x.copy() for x in xs]
+        root = 1
+        O.ref_reduce(outs, None, root, dtype_code=code, max_segment=128)
+        key = f"reduce_{'i32' if code == 2 else 'f16'}_P{P}_n{n}_in"
+        out[key + "_inputs"] = np.stack(xs)
+        out[key] = np.stack(outs)
+        rows.append({"P": P, "n": n, "max_segment": 128, "inplace": True, "root": root,
+                     "dtype": code, "key": key})
+    meta["reduce"] = rows
+    # ReduceTest.Default's closed form (reduce_test.cc:22-86) on the reference, uint64
+    checked = 0
+    for P in (1, 2, 4, 7):
+        for n in (1, 10, 100, 1000):
+            for inplace in (True, False):
+                for root in range(P):
+                    vals = [np.arange(n, dtype=np.uint64) * P + r for r in range(P)]
+                    if inplace:
+                        outs, ins = [v.copy() for v in vals], None
+                    else:
+                        outs, ins = [np.zeros(n, np.uint64) for _ in range(P)], vals
+                    O.ref_reduce(outs, ins, root, max_segment=128)
+                    exp = np.arange(n, dtype=np.uint64) * P * P + np.uint64(P * (P - 1) // 2)
+                    assert np.array_equal(outs[root], exp), (P, n, inplace, root)
+                    checked += 1
+    meta["reduce_test_closed_form_cases"] = checked
+    meta["reduce_timeout_probe"] = O.ref_reduce_timeout(10)
+
+
 def main() -> None:
     if not O.ref_available():
         raise SystemExit("oracle/_ref/libgloo_ref.so missing: make -C oracle ref")
@@ -264,6 +327,7 @@ def main() -> None:
     gen_bcube(out, meta)
     gen_chunked_ring(out, meta)
     gen_new_test(meta)
+    gen_reduce(out, meta)
     import ctypes
     buf = ctypes.create_string_buffer(512)
     rc = O.ref().ref_allreduce_timeout(10, buf, 512)

@@ -15,6 +15,7 @@
  *   orc_ring_plan     segment geometry of ring()        gloo/gloo/allreduce.cc:199-221
  *   orc_allreduce     local reduce + ring RS/AG result  gloo/gloo/allreduce.cc:46-146, 147-422
  *   orc_split_aa/_ag  bew_allreduce_a rail split        gloo/gloo/pipeallreduce-a.h:137-376
+ *   orc_reduce        gloo::reduce root result         gloo/gloo/reduce.cc:21-262
  * bf16 (dtype 9) has no reference counterpart: c = bf16_rne(float(a) + float(b)) (our spec).
  */
 #include <math.h>
@@ -514,3 +515,62 @@ int orc_allreduce_ring_chunked(int P, int nptr, int op, int dtype, size_t n, voi
 void orc_isum_f32(void* x, const void* y, size_t n) { orc_op(OP_SUM, D_FLOAT32, x, x, y, n); }
 void orc_isum_i32(void* x, const void* y, size_t n) { orc_op(OP_SUM, D_INT32, x, x, y, n); }
 void orc_isum_f16(void* x, const void* y, size_t n) { orc_op(OP_SUM, D_FLOAT16, x, x, y, n); }
+
+/* ---- new-style gloo::reduce (reduce.cc:21-262) ----
+ * Segment geometry (reduce.cc:87-135) differs from the allreduce ring's: segmentBytes =
+ * roundUp(min(ceil(B / 2P), maxSegmentSize rounded down to E), E), then numSegments =
+ * roundUp(max(ceil(B / segmentBytes), 2P), P).  The reduce-scatter is the ring's (send to
+ * rank-1, receive from rank+1, reduce(out + off, in + off, tmp)), so segment k's owner q = k / S
+ * ends with x_q + (x_{q+1} + (... + x_{q-1})); rank q then sends its chunk to the root
+ * (reduce.cc:229-261).  Only the root's output is defined; this restatement writes out[root]. */
+void orc_reduce_plan(int P, size_t n, size_t esize, size_t max_segment, size_t* num_segments,
+                     size_t* segment_bytes, size_t* segments_per_rank) {
+  size_t total = n * esize;
+  size_t max_seg_bytes = esize * (max_segment / esize);
+  size_t half = (total + (size_t)P * 2 - 1) / ((size_t)P * 2);
+  size_t sb = half < max_seg_bytes ? half : max_seg_bytes;
+  if (sb % esize) sb += esize - sb % esize;
+  size_t want = sb ? (total + sb - 1) / sb : 0;
+  size_t ns = want > (size_t)P * 2 ? want : (size_t)P * 2;
+  if (ns % (size_t)P) ns += (size_t)P - ns % (size_t)P;
+  *num_segments = ns;
+  *segment_bytes = sb;
+  *segments_per_rank = ns / (size_t)P;
+}
+
+int orc_reduce(int P, int op, int dtype, size_t n, void** in, void** out, int root,
+               size_t max_segment) {
+  size_t es = orc_esize(dtype);
+  if (!es || P < 1 || root < 0 || root >= P) return 1;
+  if (n == 0) return 0;
+  size_t bytes = n * es;
+  if (P == 1) {
+    if (in && in[0] != out[0]) memcpy(out[0], in[0], bytes);
+    return 0;
+  }
+  size_t ns, sb, S;
+  orc_reduce_plan(P, n, es, max_segment ? max_segment : (1u << 20), &ns, &sb, &S);
+  if (!sb) return 1;
+  unsigned char* acc = (unsigned char*)malloc(bytes + 1);
+  unsigned char* tmp = (unsigned char*)malloc(sb + 1);
+  if (!acc || !tmp) { free(acc); free(tmp); return 2; }
+  for (size_t k = 0; k < ns; k++) {
+    size_t off = k * sb;
+    if (off >= bytes) break;
+    size_t len = (bytes - off < sb) ? bytes - off : sb;
+    size_t cnt = len / es;
+    int q = (int)(k / S);
+    const unsigned char* src = (const unsigned char*)(in ? in : out)[(q + P - 1) % P];
+    memcpy(acc + off, src + off, len);
+    for (int d = P - 2; d >= 0; d--) {
+      int j = (q + d) % P;
+      memcpy(tmp, (const unsigned char*)(in ? in : out)[j] + off, len);
+      orc_op(op, dtype, tmp, tmp, acc + off, cnt);
+      memcpy(acc + off, tmp, len);
+    }
+  }
+  memcpy(out[root], acc, bytes);
+  free(acc);
+  free(tmp);
+  return 0;
+}

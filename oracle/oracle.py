@@ -69,6 +69,9 @@ def orc():
         _orc.orc_allreduce_ring_chunked.argtypes = _orc.orc_allreduce_ring_old.argtypes
         _orc.orc_allreduce_bcube.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                              ctypes.c_int, _c, _vp, _vp]
+        _orc.orc_reduce.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, _c, _vp, _vp,
+                                    ctypes.c_int, _c]
+        _orc.orc_reduce_plan.argtypes = _orc.orc_ring_plan.argtypes
     return _orc
 
 
@@ -95,6 +98,9 @@ def ref():
         _ref.ref_allreduce_ring_old.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, _c,
                                                 _vp, ctypes.c_char_p, _c]
         _ref.ref_allreduce_ring_chunked.argtypes = _ref.ref_allreduce_ring_old.argtypes
+        _ref.ref_reduce.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, _c, _vp, _vp,
+                                    ctypes.c_int, _c, ctypes.c_long, ctypes.c_char_p, _c]
+        _ref.ref_reduce_timeout.argtypes = [ctypes.c_long, ctypes.c_char_p, _c]
     return _ref
 
 
@@ -269,3 +275,52 @@ def ref_bench_ring(P: int, n: int, warmup: int, iters: int) -> np.ndarray:
     if rc:
         raise RuntimeError(err.value.decode())
     return s
+
+
+# ---------------------------------------------------------------- gloo::reduce (reduce.cc)
+def reduce_plan(P: int, n: int, esize: int, max_segment: int = 1 << 20):
+    """(numSegments, segmentBytes, segments per rank) of gloo::reduce (reduce.cc:87-135)."""
+    ns, sb, S = _c(), _c(), _c()
+    orc().orc_reduce_plan(P, n, esize, max_segment, ctypes.byref(ns), ctypes.byref(sb),
+                          ctypes.byref(S))
+    return ns.value, sb.value, S.value
+
+
+def _reduce(fn_is_ref, outs, ins, root, kind, dtype_code, max_segment, timeout_ms=0):
+    P = len(outs)
+    n = outs[0].size
+    code = _dt(outs[0], dtype_code)
+    optrs = (_vp * P)(*[_ptr(o) for o in outs])
+    iptrs = (_vp * P)(*[_ptr(i) for i in ins]) if ins is not None else None
+    ip = ctypes.cast(iptrs, _vp) if iptrs is not None else None
+    if fn_is_ref:
+        err = ctypes.create_string_buffer(512)
+        rc = ref().ref_reduce(P, OPS[kind], code, n, ip, ctypes.cast(optrs, _vp), root,
+                              max_segment, timeout_ms, err, 512)
+        if rc:
+            raise RuntimeError(f"reference reduce failed: {err.value.decode()}")
+    else:
+        rc = orc().orc_reduce(P, OPS[kind], code, n, ip, ctypes.cast(optrs, _vp), root,
+                              max_segment)
+        if rc:
+            raise RuntimeError("oracle reduce failed")
+    return outs
+
+
+def reduce(outs, ins=None, root=0, kind="sum", dtype_code=None, max_segment=1 << 20):
+    """C restatement of gloo::reduce: writes the root's output (outs[root]) only.  float16
+    only in place (out of place, its stores depend on the output's old bits)."""
+    return _reduce(False, outs, ins, root, kind, dtype_code, max_segment)
+
+
+def ref_reduce(outs, ins=None, root=0, kind="sum", dtype_code=None, max_segment=1 << 20):
+    """The reference's own gloo::reduce over len(outs) loopback thread-ranks; every rank's
+    output is left as the reference leaves it."""
+    return _reduce(True, outs, ins, root, kind, dtype_code, max_segment)
+
+
+def ref_reduce_timeout(timeout_ms: int = 10) -> str:
+    what = ctypes.create_string_buffer(512)
+    if ref().ref_reduce_timeout(timeout_ms, what, 512):
+        raise RuntimeError("reference reduce did not time out")
+    return what.value.decode()

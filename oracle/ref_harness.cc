@@ -5,6 +5,7 @@
 // Nothing here re-implements the reference: every result comes from the reference's functions
 //   gloo::sum/product/max/min<T>   gloo/gloo/math.h:15-73
 //   gloo::allreduce (ring, bcube)  gloo/gloo/allreduce.cc:99-422
+//   gloo::reduce (ring + gather)   gloo/gloo/reduce.cc:21-262
 //   rendezvous + TCP loopback      gloo/gloo/rendezvous/context.cc:32-69, transport/tcp/*
 // driven the way the reference's own tests drive them (thread per rank, in-process HashStore,
 // one shared TCP device on the loopback interface: gloo/gloo/test/base_test.h:73-156).
@@ -307,4 +308,65 @@ extern "C" int ref_allreduce_ring_old(int P, int nptr, int dtype, size_t n, void
     case D_FLOAT64: return run_old_ring<double>(P, nptr, n, bufs, err, errlen);
   }
   return 2;
+}
+
+// ---- new-style gloo::reduce (gloo/gloo/reduce.cc:21-262): the other caller of the Func ---
+#include "gloo/reduce.h"
+
+namespace {
+template <typename T>
+void set_reduce_bufs(gloo::ReduceOptions& o, void* in, void* out, size_t n) {
+  if (in) o.setInput(static_cast<T*>(in), n);
+  o.setOutput(static_cast<T*>(out), n);
+}
+}  // namespace
+
+// One gloo::reduce to `root` over P thread-ranks.  in/out are P pointers (in == NULL: in
+// place on out, reduce_test.cc:27-33).  Every rank's out is left as the reference leaves it.
+extern "C" int ref_reduce(int P, int op, int dtype, size_t n, void** in, void** out, int root,
+                          size_t max_segment, long timeout_ms, char* err, size_t errlen) {
+  size_t es = 0;
+  Fn f = lookup(op, dtype, &es);
+  if (!f) return 2;
+  return spawn(P, [&](int r, std::shared_ptr<gloo::Context> ctx) {
+    gloo::ReduceOptions o(ctx);
+    void* ip = in ? in[r] : nullptr;
+    switch (dtype) {
+      case D_INT8: set_reduce_bufs<int8_t>(o, ip, out[r], n); break;
+      case D_UINT8: set_reduce_bufs<uint8_t>(o, ip, out[r], n); break;
+      case D_INT32: set_reduce_bufs<int32_t>(o, ip, out[r], n); break;
+      case D_UINT32: set_reduce_bufs<uint32_t>(o, ip, out[r], n); break;
+      case D_INT64: set_reduce_bufs<int64_t>(o, ip, out[r], n); break;
+      case D_UINT64: set_reduce_bufs<uint64_t>(o, ip, out[r], n); break;
+      case D_FLOAT32: set_reduce_bufs<float>(o, ip, out[r], n); break;
+      case D_FLOAT64: set_reduce_bufs<double>(o, ip, out[r], n); break;
+      case D_FLOAT16: set_reduce_bufs<gloo::float16>(o, ip, out[r], n); break;
+    }
+    o.setRoot(root);
+    o.setReduceFunction(f);
+    if (max_segment) o.setMaxSegmentSize(max_segment);
+    if (timeout_ms > 0) o.setTimeout(std::chrono::milliseconds(timeout_ms));
+    gloo::reduce(o);
+  }, err, errlen);
+}
+
+// ReduceTest.TestTimeout (reduce_test.cc:91-108): root 0 alone with a 10 ms timeout.
+extern "C" int ref_reduce_timeout(long timeout_ms, char* what, size_t len) {
+  int rc = 3;
+  spawn(2, [&](int r, std::shared_ptr<gloo::Context> ctx) {
+    if (r != 0) return;
+    uint64_t buf = 0;
+    gloo::ReduceOptions o(ctx);
+    o.setOutput(&buf, 1);
+    o.setRoot(0);
+    o.setReduceFunction(Fn(&gloo::sum<uint64_t>));
+    o.setTimeout(std::chrono::milliseconds(timeout_ms));
+    try {
+      gloo::reduce(o);
+    } catch (const gloo::IoException& e) {
+      set_err(what, len, e.what());
+      rc = 0;
+    }
+  }, nullptr, 0);
+  return rc;
 }

@@ -1,8 +1,9 @@
-// Sanitizer driver for the host runtime (transport + ring + rail split), built by
+// Sanitizer driver for the host runtime (transport + ring + rail split + reduce), built by
 // tests/test_sanitizers.py with -fsanitize=thread and with -fsanitize=address,undefined.
 // Mirrors AllreduceNewTest.Default (gloo/gloo/test/allreduce_test.cc:302-362) and the
 // bew_allreduce_a split on thread-ranks over loopback TCP, with a plain CPU sum as the reducer
 // (the product's GPU reducer is exercised by the GPU tests).  Exit 0 = all results correct.
+#include <algorithm>
 #include <atomic>
 #include <cstdint>
 #include <cstdlib>
@@ -141,8 +142,56 @@ static int run_algorithm(int P, int nptr, int n, bool chunked) {
   return 0;
 }
 
+// ReduceTest.Default (gloo/gloo/test/reduce_test.cc:22-86): every rank takes a turn as root.
+static int run_reduce(int P, size_t n, bool inplace) {
+  hydra::HashStore store;
+  std::vector<std::thread> th;
+  std::vector<int> bad(P, 0);
+  for (int r = 0; r < P; r++) {
+    th.emplace_back([&, r] {
+      try {
+        auto c = std::make_shared<hydra::Context>(r, P);
+        c->connectFullMesh(store, "127.0.0.1", "r");
+        std::vector<uint64_t> in(n), out(n);
+        for (int root = 0; root < P; root++) {
+          for (size_t k = 0; k < n; k++) in[k] = k * P + r;
+          hydra::ReduceOptions o(c);
+          if (inplace) {
+            out = in;
+          } else {
+            std::fill(out.begin(), out.end(), 0);
+            o.setInput(in.data(), n);
+          }
+          o.setOutput(out.data(), n);
+          o.setRoot(root);
+          o.setReduceFunction(&sum_u64);
+          o.setMaxSegmentSize(128);
+          hydra::reduce(o);
+          if (r == root)
+            for (size_t k = 0; k < n; k++)
+              if (out[k] != k * P * P + (size_t)P * (P - 1) / 2) bad[r]++;
+        }
+      } catch (const std::exception& e) {
+        std::fprintf(stderr, "rank %d: %s\n", r, e.what());
+        bad[r]++;
+      }
+    });
+  }
+  for (auto& t : th) t.join();
+  for (int b : bad)
+    if (b) return 1;
+  return 0;
+}
+
 int main() {
   int fails = 0;
+  for (int P : {1, 2, 3, 4})
+    for (bool inplace : {true, false})
+      for (size_t n : {(size_t)1, (size_t)1000, (size_t)20011})
+        if (run_reduce(P, n, inplace)) {
+          std::fprintf(stderr, "FAIL reduce P=%d n=%zu inplace=%d\n", P, n, (int)inplace);
+          fails++;
+        }
   for (int P : {1, 2, 3, 4})
     for (int nptr : {1, 2})
       for (bool inplace : {true, false})

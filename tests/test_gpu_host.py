@@ -171,3 +171,44 @@ def test_host_ring_pinned_scratch_zero_copy(gpu, O):
     exp = O.ring_result(xs, 4096)
     for r in range(P):
         assert np.array_equal(outs[r][0].view(np.uint32), exp.view(np.uint32)), r
+
+
+def test_reduce_gpu_reducer_vs_golden(gpu, golden, golden_meta):
+    """gloo::reduce (reduce.cc:21-262) with every segment reduced on the MI355X (out of place:
+    reduce(out + off, in + off, tmp)) against the reference's own outputs on every rank."""
+    for row in golden_meta["reduce"]:
+        if "dtype" in row and row["dtype"] != 2:
+            continue  # the GPU sum covers int32/fp32 here (float16: tests/test_gpu_reduce.py)
+        if "dtype" in row:
+            xs = list(golden[row["key"] + "_inputs"])
+            outs = [x.copy() for x in xs]
+            host.reduce_threads(outs, None, row["root"], dtype_code=2,
+                                max_segment=row["max_segment"])
+            assert np.array_equal(np.stack(outs), golden[row["key"]]), row["key"]
+            continue
+        P, n = row["P"], row["n"]
+        xs = [synth.stress_f32(P, r, n) for r in range(P)]
+        if row["inplace"]:
+            outs, ins = [x.copy() for x in xs], None
+        else:
+            outs, ins = [np.zeros(n, np.float32) for _ in xs], [x.copy() for x in xs]
+        host.reduce_threads(outs, ins, row["root"], max_segment=row["max_segment"])
+        if row["key"] in golden.files:
+            assert np.array_equal(np.stack(outs).view(np.uint32),
+                                  golden[row["key"]].view(np.uint32)), row["key"]
+        else:
+            assert np.array_equal(outs[row["root"]].view(np.uint32),
+                                  golden[row["key"] + "_root"].view(np.uint32)), row["key"]
+
+
+@pytest.mark.parametrize("pinned", [False, True])
+def test_reduce_gpu_reducer_large(gpu, O, pinned):
+    """Past the 1 MiB segment cap, out of place, GPU reducer (staged, or zero-copy from pinned
+    receive slots): the root equals the C restatement bit for bit."""
+    P, n, root = 4, 3_000_001, 1
+    xs = [synth.stress_f32(P, r, n) for r in range(P)]
+    outs = [np.zeros(n, np.float32) for _ in range(P)]
+    host.reduce_threads(outs, [x.copy() for x in xs], root, pinned_scratch=pinned)
+    exp = [np.zeros(n, np.float32) for _ in range(P)]
+    O.reduce(exp, [x.copy() for x in xs], root)
+    assert np.array_equal(outs[root].view(np.uint32), exp[root].view(np.uint32))

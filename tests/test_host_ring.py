@@ -188,3 +188,99 @@ def test_bcube_multi_pointer_out_of_place(O):
     for r in range(P):
         for i in range(nptr):
             assert np.array_equal(outs[r][i].view(np.uint32), exp[r][i].view(np.uint32))
+
+
+# ---- gloo::reduce (reduce.cc:21-262): the other new-style caller of the reduce function ----
+def _reduce_case_inputs(row):
+    P, n = row["P"], row["n"]
+    xs = [synth.stress_f32(P, r, n) for r in range(P)]
+    if row["inplace"]:
+        return [x.copy() for x in xs], None
+    return [np.zeros(n, np.float32) for _ in xs], [x.copy() for x in xs]
+
+
+def test_reduce_every_rank_vs_golden(golden, golden_meta, O):
+    """Host runtime reduce() against the reference's own outputs on EVERY rank: the root holds
+    the reduction, the other ranks what the reference's schedule leaves (its extra ring
+    iterations, reduce.cc:182-223) -- so the schedule itself is pinned, not just the result."""
+    for row in golden_meta["reduce"]:
+        if "dtype" in row:
+            code = row["dtype"]
+            xs = list(golden[row["key"] + "_inputs"])
+            outs = [x.copy() for x in xs]
+            fn = fnptr(O, "orc_sum_i32" if code == 2 else "orc_sum_f16")
+            host.reduce_threads(outs, None, row["root"], dtype_code=code,
+                                max_segment=row["max_segment"], reducer_fn=fn)
+            assert np.array_equal(np.stack(outs), golden[row["key"]]), row["key"]
+            continue
+        outs, ins = _reduce_case_inputs(row)
+        host.reduce_threads(outs, ins, row["root"], max_segment=row["max_segment"],
+                            reducer_fn=fnptr(O, "orc_sum_f32"))
+        if row["key"] in golden.files:
+            exp = golden[row["key"]]
+            assert np.array_equal(np.stack(outs).view(np.uint32), exp.view(np.uint32)), row["key"]
+        else:
+            exp = golden[row["key"] + "_root"]
+            got = outs[row["root"]]
+            assert np.array_equal(got.view(np.uint32), exp.view(np.uint32)), row["key"]
+
+
+def test_reduce_oracle_vs_golden(golden, golden_meta, O):
+    """The C restatement's root result against the reference's, every fp32 case (fold order
+    under reduce's own segment geometry) and the in-place int32/float16 cases."""
+    for row in golden_meta["reduce"]:
+        root = row["root"]
+        if "dtype" in row:
+            xs = list(golden[row["key"] + "_inputs"])
+            outs = [x.copy() for x in xs]
+            O.reduce(outs, None, root, dtype_code=row["dtype"], max_segment=row["max_segment"])
+            assert np.array_equal(outs[root], golden[row["key"]][root]), row["key"]
+            continue
+        outs, ins = _reduce_case_inputs(row)
+        O.reduce(outs, ins, root, max_segment=row["max_segment"])
+        exp = golden[row["key"]][root] if row["key"] in golden.files else \
+            golden[row["key"] + "_root"]
+        assert np.array_equal(outs[root].view(np.uint32), exp.view(np.uint32)), row["key"]
+
+
+@pytest.mark.parametrize("P", [1, 2, 4, 7])
+@pytest.mark.parametrize("inplace", [True, False])
+def test_reduce_test_default(O, P, inplace):
+    """ReduceTest.Default (test/reduce_test.cc:22-86): uint64, maxSegmentSize 128, every rank
+    takes a turn as root, closed form j*P^2 + P(P-1)/2 on the root."""
+    for n in (1, 10, 100, 1000, 10000):
+        for root in range(P):
+            vals = [np.arange(n, dtype=np.uint64) * P + r for r in range(P)]
+            if inplace:
+                outs, ins = [v.copy() for v in vals], None
+            else:
+                outs, ins = [np.zeros(n, np.uint64) for _ in range(P)], vals
+            host.reduce_threads(outs, ins, root, max_segment=128,
+                                reducer_fn=fnptr(O, "orc_sum_u64"))
+            exp = np.arange(n, dtype=np.uint64) * P * P + np.uint64(P * (P - 1) // 2)
+            assert np.array_equal(outs[root], exp), (P, n, root, inplace)
+
+
+def test_reduce_timeout_raises_io_exception(golden_meta):
+    """ReduceTest.TestTimeout (reduce_test.cc:91-108): same text as the reference's."""
+    rc, what = host.reduce_timeout_probe(10)
+    assert rc == 0 and "Timed out waiting 10ms for recv operation to complete" in what
+    assert "Timed out waiting 10ms for recv operation to complete" in \
+        golden_meta["reduce_timeout_probe"]
+
+
+def test_reduce_large_vs_reference(O):
+    """Past the 1 MiB segment cap (many segments per rank), fp32 stress inputs: root bit-exact
+    against the live reference when it is built, else the C restatement."""
+    P, n = 3, 1_000_003
+    xs = [synth.stress_f32(P, r, n) for r in range(P)]
+    outs = [np.zeros(n, np.float32) for _ in range(P)]
+    host.reduce_threads(outs, [x.copy() for x in xs], 2, reducer_fn=fnptr(O, "orc_sum_f32"))
+    exp = [np.zeros(n, np.float32) for _ in range(P)]
+    if O.ref_available():
+        O.ref_reduce(exp, [x.copy() for x in xs], 2)
+        for r in range(P):
+            assert np.array_equal(outs[r].view(np.uint32), exp[r].view(np.uint32)), r
+    else:
+        O.reduce(exp, [x.copy() for x in xs], 2)
+        assert np.array_equal(outs[2].view(np.uint32), exp[2].view(np.uint32))

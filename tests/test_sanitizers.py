@@ -1,6 +1,6 @@
 """Host-runtime race and memory checks (the reference's SANITIZE=thread CI job,
 gloo/CMakeLists.txt:66-71, .circleci/config.yml:117-121): tests/cpp/host_ring_sanitize.cc
-built against hydra_amd/csrc/host/{transport,allreduce}.cpp with ThreadSanitizer and with
+built against hydra_amd/csrc/host/{transport,allreduce,reduce}.cpp with ThreadSanitizer and with
 AddressSanitizer + UBSan, run on loopback TCP thread-ranks."""
 import os
 import subprocess
@@ -10,7 +10,8 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRCS = [os.path.join(ROOT, "tests", "cpp", "host_ring_sanitize.cc"),
         os.path.join(ROOT, "hydra_amd", "csrc", "host", "transport.cpp"),
-        os.path.join(ROOT, "hydra_amd", "csrc", "host", "allreduce.cpp")]
+        os.path.join(ROOT, "hydra_amd", "csrc", "host", "allreduce.cpp"),
+        os.path.join(ROOT, "hydra_amd", "csrc", "host", "reduce.cpp")]
 
 
 @pytest.mark.parametrize("san", ["thread", "address,undefined"])
