@@ -36,6 +36,7 @@ EXPORTS = [  # every symbol include/hydra_hip.h declares
     "hydra_peer_create", "hydra_peer_connect", "hydra_peer_register", "hydra_peer_open",
     "hydra_peer_close", "hydra_peer_set_option", "hydra_peer_error", "hydra_peer_allreduce",
     "hydra_peer_detach", "hydra_peer_destroy", "hydra_comm_wait",
+    "hydra_reduce_root", "hydra_reduce_root_plan", "hydra_reduce_root_simulate",
 ]
 
 (ALGO_AUTO, ALGO_RING, ALGO_DIRECT, ALGO_RCCL, ALGO_A2A, ALGO_RING_OLD, ALGO_RING_CHUNKED,
@@ -125,6 +126,9 @@ def _declare(L) -> None:
     L.hydra_plan.argtypes = [i, i, i, sz, sz, sz, sz, ctypes.POINTER(PlanOp), sz,
                              ctypes.POINTER(sz), ctypes.POINTER(sz)]
     L.hydra_allreduce_simulate.argtypes = [i, i, i, i, i, ctypes.POINTER(vp), sz, sz, sz]
+    L.hydra_reduce_root.argtypes = [vp, i, i, i, i, vp, sz, sz, sz, vp]
+    L.hydra_reduce_root_plan.argtypes = L.hydra_plan.argtypes
+    L.hydra_reduce_root_simulate.argtypes = L.hydra_allreduce_simulate.argtypes
     L.hydra_fold.argtypes = [i, i, i, vp, ctypes.POINTER(vp), i, sz, vp]
     L.hydra_peer_create.argtypes = [i, i, i, ctypes.POINTER(vp), vp]
     L.hydra_peer_connect.argtypes = [vp, vp]

@@ -131,6 +131,7 @@ struct hydra_comm {
   // plan cache
   int key_algo = -1;
   size_t key_n = 0, key_es = 0, key_ms = 0, key_chunk = 0;
+  int key_root = -1;
   std::vector<hydra::PlanOp> plan;
   std::vector<char> waited;
 };
@@ -313,7 +314,7 @@ namespace {
 // Argument checks + plan cache + scratch for one allreduce on `c`.  *skip: nothing to do
 // (n == 0 or a single rank, allreduce.cc:129-133).
 int prepare(hydra_comm* c, int* algo, int op, int dtype, int flags, void* buf, size_t n,
-            size_t max_segment, size_t chunk_bytes, bool* skip) {
+            size_t max_segment, size_t chunk_bytes, bool* skip, int root = -1) {
   if (!c) return fail(HYDRA_ERR_INVALID, "null comm");
   if (c->aborted) return fail(HYDRA_ERR_TIMEOUT, "communicator was aborted by an earlier timeout");
   size_t es;
@@ -330,9 +331,16 @@ int prepare(hydra_comm* c, int* algo, int op, int dtype, int flags, void* buf, s
     return HYDRA_OK;
   }
   const size_t ms = max_segment ? max_segment : (1u << 20);
+  if (root >= 0) {  // hydra_reduce_root: DIRECT's arguments, gloo::reduce's plan
+    if (root >= c->nranks) return fail(HYDRA_ERR_INVALID, "root out of range");
+    *algo = hydra::kAlgoReduce;
+  }
   if (c->key_algo != *algo || c->key_n != n || c->key_es != es || c->key_ms != ms ||
-      c->key_chunk != chunk_bytes) {
-    const hydra::PlanGeom g = hydra::make_geom(c->nranks, n, es, ms, chunk_bytes);
+      c->key_chunk != chunk_bytes || c->key_root != root) {
+    if (root >= 0 && ms < es) return fail(HYDRA_ERR_INVALID, "max_segment below the element size");
+    const hydra::PlanGeom g = root >= 0
+                                  ? hydra::make_geom_reduce(c->nranks, n, es, ms, chunk_bytes, root)
+                                  : hydra::make_geom(c->nranks, n, es, ms, chunk_bytes);
     rc = check_geometry(*algo, g);
     if (rc) return rc;
     c->plan = hydra::make_plan(*algo, g, c->rank);
@@ -354,6 +362,7 @@ int prepare(hydra_comm* c, int* algo, int op, int dtype, int flags, void* buf, s
     c->key_es = es;
     c->key_ms = ms;
     c->key_chunk = chunk_bytes;
+    c->key_root = root;
   }
   return HYDRA_OK;
 }
@@ -380,6 +389,24 @@ int hydra_allreduce(hydra_comm_t c, int algo, int op, int dtype, int flags, void
   hydra::TraceRange trace_("hydra_allreduce");
   bool skip = false;
   int rc = prepare(c, &algo, op, dtype, flags, buf, n, max_segment, chunk_bytes, &skip);
+  if (rc || skip) return rc ? rc : ok();
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  HIP_TRY(hipEventRecord(c->ev_start, st));
+  rc = enqueue(c, algo, op, dtype, flags, buf, n, c->ev_start);
+  if (rc) return rc;
+  rc = join_streams(c, st);
+  return rc ? rc : ok();
+}
+
+// gloo::reduce (reduce.cc:21-262) of a device bucket to `root`, in place: plan_reduce.
+int hydra_reduce_root(hydra_comm_t c, int root, int op, int dtype, int flags, void* buf,
+                      size_t n, size_t max_segment, size_t chunk_bytes, hydra_stream_t stream) {
+  hydra::TraceRange trace_("hydra_reduce_root");
+  // checked before the single-rank / empty short cuts, as the reference does (reduce.cc:31)
+  if (root < 0 || (c && root >= c->nranks)) return fail(HYDRA_ERR_INVALID, "root out of range");
+  int algo = HYDRA_ALGO_DIRECT;
+  bool skip = false;
+  int rc = prepare(c, &algo, op, dtype, flags, buf, n, max_segment, chunk_bytes, &skip, root);
   if (rc || skip) return rc ? rc : ok();
   hipStream_t st = static_cast<hipStream_t>(stream);
   HIP_TRY(hipEventRecord(c->ev_start, st));
@@ -435,17 +462,21 @@ int hydra_apipe_allreduce(hydra_comm_t rail1, hydra_comm_t rail2, int table, int
   return rc ? rc : ok();
 }
 
-int hydra_plan(int algo, int P, int rank, size_t n, size_t esize, size_t max_segment,
-               size_t chunk_bytes, hydra_plan_op_t* ops, size_t cap, size_t* count,
-               size_t* scratch_bytes) {
+namespace {
+int plan_impl(int algo, int root, int P, int rank, size_t n, size_t esize, size_t max_segment,
+              size_t chunk_bytes, hydra_plan_op_t* ops, size_t cap, size_t* count,
+              size_t* scratch_bytes) {
   if (P < 1 || P > hydra::kMaxRanks || rank < 0 || rank >= P)
     return fail(HYDRA_ERR_INVALID, "bad rank/P");
   if (esize != 1 && esize != 2 && esize != 4 && esize != 8)
     return fail(HYDRA_ERR_INVALID, "bad element size");
-  algo = resolve_algo(algo);
+  if (root >= P) return fail(HYDRA_ERR_INVALID, "root out of range");
+  algo = root >= 0 ? hydra::kAlgoReduce : resolve_algo(algo);
   if (algo == HYDRA_ALGO_RCCL) return fail(HYDRA_ERR_UNSUPPORTED, "RCCL has no plan");
-  const hydra::PlanGeom g =
-      hydra::make_geom(P, n, esize, max_segment ? max_segment : (1u << 20), chunk_bytes);
+  const size_t ms = max_segment ? max_segment : (1u << 20);
+  if (root >= 0 && ms < esize) return fail(HYDRA_ERR_INVALID, "max_segment below the element size");
+  const hydra::PlanGeom g = root >= 0 ? hydra::make_geom_reduce(P, n, esize, ms, chunk_bytes, root)
+                                      : hydra::make_geom(P, n, esize, ms, chunk_bytes);
   if (int rc = check_geometry(algo, g)) return rc;
   const auto plan = hydra::make_plan(algo, g, rank);
   if (count) *count = plan.size();
@@ -457,20 +488,40 @@ int hydra_plan(int algo, int P, int rank, size_t n, size_t esize, size_t max_seg
   }
   return ok();
 }
+}  // namespace
+
+int hydra_plan(int algo, int P, int rank, size_t n, size_t esize, size_t max_segment,
+               size_t chunk_bytes, hydra_plan_op_t* ops, size_t cap, size_t* count,
+               size_t* scratch_bytes) {
+  return plan_impl(algo, -1, P, rank, n, esize, max_segment, chunk_bytes, ops, cap, count,
+                   scratch_bytes);
+}
+
+int hydra_reduce_root_plan(int root, int P, int rank, size_t n, size_t esize, size_t max_segment,
+                           size_t chunk_bytes, hydra_plan_op_t* ops, size_t cap, size_t* count,
+                           size_t* scratch_bytes) {
+  if (root < 0) return fail(HYDRA_ERR_INVALID, "root out of range");
+  return plan_impl(HYDRA_ALGO_DIRECT, root, P, rank, n, esize, max_segment, chunk_bytes, ops, cap,
+                   count, scratch_bytes);
+}
 
 // ---- one-GPU simulation of P ranks ---------------------------------------------------------
-int hydra_allreduce_simulate(int algo, int op, int dtype, int flags, int P, void** bufs, size_t n,
-                             size_t max_segment, size_t chunk_bytes) {
+namespace {
+int simulate_impl(int algo, int root, int op, int dtype, int flags, int P, void** bufs, size_t n,
+                  size_t max_segment, size_t chunk_bytes) {
   size_t es;
   int rc = check_plan_args(algo, op, dtype, flags, &es);
   if (rc) return rc;
   if (P < 1 || P > hydra::kMaxRanks || !bufs) return fail(HYDRA_ERR_INVALID, "bad P/bufs");
-  algo = resolve_algo(algo);
+  if (root >= P) return fail(HYDRA_ERR_INVALID, "root out of range");
+  algo = root >= 0 ? hydra::kAlgoReduce : resolve_algo(algo);
   if (algo == HYDRA_ALGO_RCCL) return fail(HYDRA_ERR_UNSUPPORTED, "no RCCL in the simulator");
   if (n == 0 || P == 1) return ok();
   const bool acc32 = (flags & HYDRA_ACC_F32) != 0;
-  const hydra::PlanGeom g =
-      hydra::make_geom(P, n, es, max_segment ? max_segment : (1u << 20), chunk_bytes);
+  const size_t ms = max_segment ? max_segment : (1u << 20);
+  if (root >= 0 && ms < es) return fail(HYDRA_ERR_INVALID, "max_segment below the element size");
+  const hydra::PlanGeom g = root >= 0 ? hydra::make_geom_reduce(P, n, es, ms, chunk_bytes, root)
+                                      : hydra::make_geom(P, n, es, ms, chunk_bytes);
   rc = check_geometry(algo, g);
   if (rc) return rc;
   const size_t sbytes = hydra::plan_scratch_bytes(algo, g);
@@ -671,6 +722,19 @@ int hydra_allreduce_simulate(int algo, int op, int dtype, int flags, int P, void
   cleanup();
 #undef SIM_TRY
   return ok();
+}
+}  // namespace
+
+int hydra_allreduce_simulate(int algo, int op, int dtype, int flags, int P, void** bufs, size_t n,
+                             size_t max_segment, size_t chunk_bytes) {
+  return simulate_impl(algo, -1, op, dtype, flags, P, bufs, n, max_segment, chunk_bytes);
+}
+
+int hydra_reduce_root_simulate(int root, int op, int dtype, int flags, int P, void** bufs,
+                               size_t n, size_t max_segment, size_t chunk_bytes) {
+  if (root < 0) return fail(HYDRA_ERR_INVALID, "root out of range");
+  return simulate_impl(HYDRA_ALGO_DIRECT, root, op, dtype, flags, P, bufs, n, max_segment,
+                       chunk_bytes);
 }
 
 // Executor test hook: run an arbitrary (validated) plan through the RCCL executor.  With a

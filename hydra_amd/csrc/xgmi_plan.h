@@ -45,7 +45,8 @@ enum PlanKind : int32_t {
 enum PlanBuf : int32_t { kBufUser = 0, kBufScratch = 1 };
 enum Algo : int32_t {
   kAlgoAuto = 0, kAlgoRing = 1, kAlgoDirect = 2, kAlgoRccl = 3, kAlgoA2A = 4, kAlgoRingOld = 5,
-  kAlgoRingChunked = 6, kAlgoBcube = 7
+  kAlgoRingChunked = 6, kAlgoBcube = 7,
+  kAlgoReduce = 8  // internal: gloo::reduce to PlanGeom::root (hydra_reduce_root), not an allreduce
 };
 
 // AllreduceRingChunked<T> geometry (allreduce_ring_chunked.h:32-36): 2P chunks of
@@ -75,6 +76,7 @@ struct PlanGeom {
   size_t n = 0, esize = 4, total = 0;
   size_t num_segments = 0, segment_bytes = 0, S = 0;
   size_t chunk = 0;  // pipelining chunk (bytes, multiple of esize and 16)
+  int root = -1;     // kAlgoReduce: the rank that ends with the reduction
   size_t block_begin(int q) const { return std::min(total, (size_t)q * S * segment_bytes); }
   size_t block_end(int q) const { return std::min(total, (size_t)(q + 1) * S * segment_bytes); }
   size_t block_bytes(int q) const { return block_end(q) - block_begin(q); }
@@ -112,6 +114,18 @@ inline void ring_geometry(int P, size_t n, size_t esize, size_t max_segment, siz
   *sb = round_up_sz((total + *ns - 1) / *ns, esize);
 }
 
+// gloo::reduce's own geometry (reduce.cc:87-135): segmentBytes = roundUp(min(ceil(B / 2P),
+// maxSegmentSize rounded down to E), E); numSegments = roundUp(max(ceil(B / segmentBytes), 2P), P).
+// *sb == 0 when max_segment < esize (the reference would divide by zero).
+inline void reduce_geometry(int P, size_t n, size_t esize, size_t max_segment, size_t* ns,
+                            size_t* sb, size_t* S) {
+  const size_t total = n * esize;
+  const size_t max_seg_bytes = esize * (max_segment / esize);
+  *sb = round_up_sz(std::min((total + (size_t)P * 2 - 1) / ((size_t)P * 2), max_seg_bytes), esize);
+  *ns = *sb ? round_up_sz(std::max((total + *sb - 1) / *sb, (size_t)P * 2), (size_t)P) : 0;
+  *S = *ns / (size_t)P;
+}
+
 inline PlanGeom make_geom(int P, size_t n, size_t esize, size_t max_segment, size_t chunk) {
   PlanGeom g;
   g.P = P;
@@ -124,6 +138,18 @@ inline PlanGeom make_geom(int P, size_t n, size_t esize, size_t max_segment, siz
   g.chunk = round_up_sz(std::max<size_t>(chunk ? chunk : (4u << 20), unit), unit);
   // never pipeline in chunks larger than a block (small buckets keep a small scratch)
   g.chunk = std::min(g.chunk, round_up_sz(std::max<size_t>(g.max_block(), 1), unit));
+  return g;
+}
+
+inline PlanGeom make_geom_reduce(int P, size_t n, size_t esize, size_t max_segment,
+                                 size_t chunk, int root) {
+  PlanGeom g = make_geom(P, n, esize, max_segment, chunk);
+  reduce_geometry(P, n, esize, max_segment ? max_segment : (1u << 20), &g.num_segments,
+                  &g.segment_bytes, &g.S);
+  const size_t unit = 16;
+  g.chunk = round_up_sz(std::max<size_t>(chunk ? chunk : (4u << 20), unit), unit);
+  g.chunk = std::min(g.chunk, round_up_sz(std::max<size_t>(g.max_block(), 1), unit));
+  g.root = root;
   return g;
 }
 
@@ -147,7 +173,7 @@ inline bool blocks_equal(const PlanGeom& g) {
 inline size_t plan_scratch_bytes(int algo, const PlanGeom& g) {
   if (g.P <= 1) return 0;
   if (algo == kAlgoRing) return 2 * g.chunk;
-  if (algo == kAlgoDirect) return 2 * (size_t)(g.P - 1) * g.chunk;
+  if (algo == kAlgoDirect || algo == kAlgoReduce) return 2 * (size_t)(g.P - 1) * g.chunk;
   if (algo == kAlgoA2A) return g.total;
   if (algo == kAlgoRingOld) return 2 * round_up_sz(g.total, 16);
   if (algo == kAlgoRingChunked) return 2 * round_up_sz(chunked_ring_elems(g.P, g.n) * g.esize, 16);
@@ -425,7 +451,69 @@ inline std::vector<PlanOp> plan_bcube(const PlanGeom& g, int r) {
   return pb.ops;
 }
 
+// ---- REDUCE to a root: gloo::reduce (reduce.cc:21-262) on device ---------------------------
+// The reduce-scatter is DIRECT's (every rank sends each owner its block chunk in one p2p group,
+// the owner folds the P contributions in the reference's order) over gloo::reduce's own block
+// geometry, so owner q's block is x_q + (x_{q+1} + (... + x_{q-1})) exactly as the reference's
+// ring leaves it; then every owner sends its block to the root (reduce.cc:229-261) chunk by
+// chunk, as soon as that chunk is folded.  The root's bucket ends with the reduction; another
+// rank's bucket holds its own folded block and its input elsewhere (only the root is defined).
+inline std::vector<PlanOp> plan_reduce(const PlanGeom& g, int r) {
+  PlanBuilder pb;
+  const int P = g.P;
+  if (P <= 1 || g.total == 0 || g.root < 0) return pb.ops;
+  const size_t C = g.nchunks();
+  int reader[2] = {-1, -1};
+  std::vector<int> folded(C, -1);
+  for (size_t c = 0; c < C; c++) {  // reduce-scatter: plan_direct's first half
+    const int par = (int)(c & 1);
+    const int64_t base = (int64_t)par * (P - 1) * (int64_t)g.chunk;
+    bool any = false;
+    for (int d = 1; d < P; d++) {
+      const int q = (r + d) % P;
+      size_t b, l;
+      g.chunk_of(q, c, &b, &l);
+      if (l) { pb.add(kOpSend, q, kBufUser, b, l); any = true; }
+    }
+    size_t mb, ml;
+    g.chunk_of(r, c, &mb, &ml);
+    if (ml)
+      for (int j = 1; j < P; j++) {
+        pb.add(kOpRecv, (r + j) % P, kBufScratch, base + (int64_t)(j - 1) * (int64_t)g.chunk, ml);
+        any = true;
+      }
+    if (!any) continue;
+    const int grp = pb.add(kOpGroup, -1, 0, 0, 0, 0, 0, 0, reader[par]);
+    if (ml) {
+      const int f = pb.add(kOpFold, -1, kBufUser, mb, ml, base, (int64_t)g.chunk, P, grp);
+      reader[par] = f;
+      folded[c] = f;
+    }
+  }
+  for (size_t c = 0; c < C; c++) {  // gather the owners' blocks to the root
+    bool any = false;
+    if (r == g.root) {
+      for (int d = 1; d < P; d++) {
+        const int q = (r + d) % P;
+        size_t b, l;
+        g.chunk_of(q, c, &b, &l);
+        if (l) { pb.add(kOpRecv, q, kBufUser, b, l); any = true; }
+      }
+      if (any) pb.add(kOpGroup, -1, 0, 0, 0, 0, 0, 0, -1);
+    } else {
+      size_t mb, ml;
+      g.chunk_of(r, c, &mb, &ml);
+      if (ml) {
+        pb.add(kOpSend, g.root, kBufUser, mb, ml);
+        pb.add(kOpGroup, -1, 0, 0, 0, 0, 0, 0, folded[c]);
+      }
+    }
+  }
+  return pb.ops;
+}
+
 inline std::vector<PlanOp> make_plan(int algo, const PlanGeom& g, int r) {
+  if (algo == kAlgoReduce) return plan_reduce(g, r);
   if (algo == kAlgoBcube) return plan_bcube(g, r);
   if (algo == kAlgoRingChunked) return plan_ring_chunked(g, r);
   if (algo == kAlgoRingOld) return plan_ring_old(g, r);

@@ -33,6 +33,36 @@ def plan(algo: str, P: int, rank: int, n: int, esize: int, max_segment: int = 0,
     return ops, scr.value
 
 
+def plan_reduce(root: int, P: int, rank: int, n: int, esize: int, max_segment: int = 0,
+                chunk_bytes: int = 0):
+    """hydra_reduce_root's op list for `rank` (gloo::reduce to `root`), plus its scratch bytes."""
+    L = _lib.lib()
+    cnt, scr = ctypes.c_size_t(), ctypes.c_size_t()
+    check(L.hydra_reduce_root_plan(root, P, rank, n, esize, max_segment, chunk_bytes, None, 0,
+                                   ctypes.byref(cnt), ctypes.byref(scr)))
+    arr = (_lib.PlanOp * max(1, cnt.value))()
+    check(L.hydra_reduce_root_plan(root, P, rank, n, esize, max_segment, chunk_bytes, arr,
+                                   cnt.value, ctypes.byref(cnt), ctypes.byref(scr)))
+    ops = [{f: getattr(arr[i], f) for f, _ in _lib.PlanOp._fields_} for i in range(cnt.value)]
+    return ops, scr.value
+
+
+def simulate_reduce(bufs, root: int, op: str = "sum", dtype_code: int | None = None,
+                    flags: int = 0, max_segment: int = 0, chunk_bytes: int = 0) -> None:
+    """hydra_reduce_root for len(bufs) ranks on ONE GPU; bufs[root] ends with the reduction."""
+    from .reduce import _torch_dtype_code
+
+    P = len(bufs)
+    code = dtype_code if dtype_code is not None else _torch_dtype_code(bufs[0])
+    n = _count(bufs[0], code)
+    for b in bufs:
+        if _count(b, code) != n or not b.is_contiguous():
+            raise HydraError(1, "simulate_reduce: buckets must be contiguous and equally sized")
+    ptrs = (ctypes.c_void_p * P)(*[b.data_ptr() for b in bufs])
+    check(_lib.lib().hydra_reduce_root_simulate(root, OPS[op], code, flags, P, ptrs, n,
+                                                max_segment, chunk_bytes))
+
+
 def simulate(bufs, algo: str = "auto", op: str = "sum", dtype_code: int | None = None,
              flags: int = 0, max_segment: int = 0, chunk_bytes: int = 0) -> None:
     """Run all len(bufs) ranks' plans on ONE GPU (device tensors, modified in place)."""
@@ -131,6 +161,21 @@ class XgmiComm:
                                          t.data_ptr(), _count(t, code), max_segment,
                                          chunk_bytes, s))
 
+    def reduce_(self, t, root: int, op: str = "sum", dtype_code: int | None = None,
+                flags: int = 0, max_segment: int = 0, chunk_bytes: int = 0,
+                stream: int | None = None) -> None:
+        """gloo::reduce of device tensor t to `root`, in place (only the root's t is defined)."""
+        import torch
+
+        from .reduce import _torch_dtype_code
+
+        code = dtype_code if dtype_code is not None else _torch_dtype_code(t)
+        if not t.is_contiguous():
+            raise HydraError(1, "reduce_: contiguous tensor required")
+        s = stream if stream is not None else torch.cuda.current_stream(t.device).cuda_stream
+        check(_lib.lib().hydra_reduce_root(self._h, root, OPS[op], code, flags, t.data_ptr(),
+                                           _count(t, code), max_segment, chunk_bytes, s))
+
     def apipe_allreduce_(self, rail2: "XgmiComm", t, table: int = 0, algo: str = "auto",
                          op: str = "sum", dtype_code: int | None = None, flags: int = 0,
                          max_segment: int = 0, chunk_bytes: int = 0,
@@ -223,6 +268,34 @@ def expected_fold_f32(xs: list[np.ndarray], max_segment: int = 1 << 20) -> np.nd
     fp32 buckets -- block q = [qS*sb, (q+1)S*sb) folded x_q + (x_{q+1} + (... + x_{q-1}))."""
     P, n = len(xs), xs[0].size
     ns, sb, S = _lib.ring_plan(P, n, 4, max_segment)
+    out = np.empty(n, np.float32)
+    for q in range(P):
+        lo, hi = min(n, q * S * sb // 4), min(n, (q + 1) * S * sb // 4)
+        if lo >= hi:
+            continue
+        acc = xs[(q + P - 1) % P][lo:hi].astype(np.float32)
+        for d in range(P - 2, -1, -1):
+            acc = xs[(q + d) % P][lo:hi] + acc
+        out[lo:hi] = acc
+    return out
+
+
+def reduce_geometry(P: int, n: int, esize: int, max_segment: int = 1 << 20):
+    """gloo::reduce's segment geometry (reduce.cc:87-135) -> (numSegments, segmentBytes, S)."""
+    total = n * esize
+    msb = esize * (max_segment // esize)
+    sb = min((total + 2 * P - 1) // (2 * P), msb)
+    sb = -(-sb // esize) * esize
+    ns = max(-(-total // sb), 2 * P)
+    ns = -(-ns // P) * P
+    return ns, sb, ns // P
+
+
+def expected_reduce_f32(xs: list[np.ndarray], max_segment: int = 1 << 20) -> np.ndarray:
+    """Self-check for the bench: gloo::reduce's root result for fp32 buckets -- the ring fold
+    over gloo::reduce's own blocks."""
+    P, n = len(xs), xs[0].size
+    ns, sb, S = reduce_geometry(P, n, 4, max_segment)
     out = np.empty(n, np.float32)
     for q in range(P):
         lo, hi = min(n, q * S * sb // 4), min(n, (q + 1) * S * sb // 4)
@@ -398,6 +471,14 @@ def bench_allreduce(args, dev) -> dict:
                                  expected_bcube_f32(xs).view(np.uint32)))
         parity["bcube"] = ("bit-exact" if max_over_ranks(0.0 if ok else 1.0, dev) == 0.0
                            else "MISMATCH")
+        # gloo::reduce to the last rank (hydra_reduce_root): only the root's bucket is defined
+        t = torch.from_numpy(xs[rank].copy()).to(dev)
+        comm.reduce_(t, world - 1)
+        torch.cuda.synchronize(dev)
+        ok = rank != world - 1 or bool(np.array_equal(
+            t.cpu().numpy().view(np.uint32), expected_reduce_f32(xs).view(np.uint32)))
+        parity["reduce_root"] = ("bit-exact" if max_over_ranks(0.0 if ok else 1.0, dev) == 0.0
+                                 else "MISMATCH")
         # two rails (bew_allreduce_a): each part is the reference ring on its slice
         t = torch.from_numpy(xs[rank].copy()).to(dev)
         comm.apipe_allreduce_(rail2, t, algo="direct")
@@ -495,6 +576,15 @@ def bench_allreduce(args, dev) -> dict:
             except _lib.HydraError as e:
                 others[a] = f"n/a: {e}"
 
+        def rstep():
+            comm.reduce_(x, 0)
+
+        try:  # gloo::reduce of the same bucket to rank 0 (context: no all-gather half)
+            ow = max_over_ranks(timed_steps(rstep, k, 3, sync, dist.barrier), dev)
+            others["reduce_root0"] = round(ow / k * 1e3, 4)
+        except _lib.HydraError as e:
+            others["reduce_root0"] = f"n/a: {e}"
+
         def astep():
             comm.apipe_allreduce_(rail2, x, algo="direct")
 
@@ -562,7 +652,8 @@ def bench_allreduce(args, dev) -> dict:
         "latency_ms": lat_ms,
         "other_algos_ms": others,
         "other_algos_busbw_GBps": {a: round(bucket / (v * 1e-3) / 1e9 * 2 * (world - 1) / world, 2)
-                                   for a, v in others.items() if isinstance(v, float)},
+                                   for a, v in others.items()
+                                   if isinstance(v, float) and a != "reduce_root0"},
         "config5_bf16": c5,
         "parity": {"fold_order_1M": parity, "full_size_exact": full_ok},
     }

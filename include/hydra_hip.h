@@ -187,6 +187,14 @@ int hydra_comm_init(hydra_comm_t* out, int nranks, int rank, const void* id, int
 int hydra_comm_destroy(hydra_comm_t comm);
 int hydra_allreduce(hydra_comm_t comm, int algo, int op, int dtype, int flags, void* buf,
                     size_t n, size_t max_segment, size_t chunk_bytes, hydra_stream_t stream);
+
+/* gloo::reduce (gloo/gloo/reduce.cc:21-262) of a device bucket to `root`, in place, on
+ * `stream`: gloo::reduce's own block geometry (reduce.cc:87-135), a DIRECT-style reduce-scatter
+ * whose owner folds are the reference's order, then every owner sends its block to the root.
+ * Only the root's bucket is defined afterwards (as in the reference).  flags: HYDRA_ACC_F32
+ * for bf16 buckets, as DIRECT. */
+int hydra_reduce_root(hydra_comm_t comm, int root, int op, int dtype, int flags, void* buf,
+                      size_t n, size_t max_segment, size_t chunk_bytes, hydra_stream_t stream);
 /* The reference's per-op timeout (AllreduceOptions::setTimeout, allreduce.h:52; waitRecv /
  * waitSend(opts.timeout) -> IoException "Timed out waiting ...", tcp/unbound_buffer.cc:60-85)
  * for the asynchronous device path: wait until everything enqueued on `stream` so far is done.
@@ -231,6 +239,13 @@ int hydra_plan(int algo, int P, int rank, size_t n, size_t esize, size_t max_seg
  * multi-GPU path on a single-GPU machine. */
 int hydra_allreduce_simulate(int algo, int op, int dtype, int flags, int P, void** bufs,
                              size_t n, size_t max_segment, size_t chunk_bytes);
+/* hydra_reduce_root's schedule: the op list of `rank`, and all P ranks simulated on one GPU
+ * (bufs: P device buckets, in place; bufs[root] ends with the reduction). */
+int hydra_reduce_root_plan(int root, int P, int rank, size_t n, size_t esize, size_t max_segment,
+                           size_t chunk_bytes, hydra_plan_op_t* ops, size_t cap, size_t* count,
+                           size_t* scratch_bytes);
+int hydra_reduce_root_simulate(int root, int op, int dtype, int flags, int P, void** bufs,
+                               size_t n, size_t max_segment, size_t chunk_bytes);
 
 /* ---- peer-access bucket allreduce over xGMI (no RCCL) --------------------------------------
  * The MI355X-first form of gloo::allreduce RING (allreduce.cc:147-422) for device-resident

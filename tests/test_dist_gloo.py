@@ -41,7 +41,11 @@ def _worker(rank, world, port, algo, n, ms, ch, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         x = synth.stress_f32(world, rank, n)
-        ops, scr = ring.plan(algo, world, rank, n, 4, ms, ch)
+        root = world - 1  # algo "reduce": hydra_reduce_root's plan (gloo::reduce to a root)
+        if algo == "reduce":
+            ops, scr = ring.plan_reduce(root, world, rank, n, 4, ms, ch)
+        else:
+            ops, scr = ring.plan(algo, world, rank, n, 4, ms, ch)
         user = torch.from_numpy(x.copy().view(np.uint8))
         scratch = torch.zeros(scr + 16, dtype=torch.uint8)
         i = 0
@@ -115,6 +119,10 @@ def _worker(rank, world, port, algo, n, ms, ch, q):
             exp = olds[rank][0]
         elif algo == "bcube":
             exp = O.bcube_result(xs)
+        elif algo == "reduce":  # only the root's bucket is defined
+            outs = [x.copy() for x in xs]
+            O.reduce(outs, None, root, max_segment=ms or (1 << 20))
+            exp = outs[root] if rank == root else got
         else:
             exp = O.ring_result(xs, ms or (1 << 20))
         q.put((rank, bool(np.array_equal(got.view(np.uint32), exp.view(np.uint32)))))
@@ -126,7 +134,7 @@ def _worker(rank, world, port, algo, n, ms, ch, q):
 
 @pytest.mark.parametrize("world", [2, 3])
 @pytest.mark.parametrize("algo", ["ring", "direct", "a2a", "ring_old", "ring_chunked",
-                                  "bcube"])
+                                  "bcube", "reduce"])
 def test_gloo_multiprocess_plan(algo, world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

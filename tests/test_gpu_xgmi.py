@@ -486,3 +486,59 @@ def test_simulated_config5_full_size(gpu):
     ring.simulate(bufs, algo="direct", dtype_code=_lib.BFLOAT16, flags=_lib.ACC_F32)
     for r, b in enumerate(bufs):
         assert torch.equal(b.view(torch.bfloat16), exp), r
+
+
+@pytest.mark.parametrize("P,n,ms,ch", [(2, 1, 0, 0), (2, 1000, 128, 256), (3, 4099, 128, 1024),
+                                       (4, 262145, 0, 0), (5, 1 << 20, 0, 1 << 18),
+                                       (8, 3000001, 0, 0), (8, 5003, 64, 128)])
+def test_simulated_reduce_root_f32(gpu, O, P, n, ms, ch):
+    """hydra_reduce_root (gloo::reduce to a root on device): with the real HIP fold kernel and
+    event edges, the root's bucket equals the reference's root output bit for bit."""
+    xs = [synth.stress_f32(P, r, n) for r in range(P)]
+    for root in sorted({0, P - 1, P // 2}):
+        bufs = dev_bufs(gpu, xs)
+        ring.simulate_reduce(bufs, root, max_segment=ms, chunk_bytes=ch)
+        exp = [x.copy() for x in xs]
+        O.reduce(exp, None, root, max_segment=ms or (1 << 20))
+        got = bufs[root].cpu().numpy()
+        assert np.array_equal(got.view(np.uint32), exp[root].view(np.uint32)), (P, n, root)
+
+
+def test_simulated_reduce_root_int32_bf16(gpu, O):
+    import torch
+
+    P, n = 4, 100003
+    xs = [synth.int32_bucket(P, r, n) for r in range(P)]
+    bufs = dev_bufs(gpu, xs)
+    ring.simulate_reduce(bufs, 2, max_segment=4096, chunk_bytes=8192)
+    exp = [x.copy() for x in xs]
+    O.reduce(exp, None, 2, max_segment=4096)
+    assert np.array_equal(bufs[2].cpu().numpy(), exp[2])
+    # bf16 bucket, fp32 accumulation (config 5's arithmetic), integer-valued: exact
+    base = torch.arange(n, device=gpu, dtype=torch.int32) % 7 - 3
+    m = [1, 2, -1, 3]
+    bb = [(base * m[r] + r).to(torch.bfloat16).view(torch.int16) for r in range(P)]
+    ring.simulate_reduce(bb, 1, dtype_code=_lib.BFLOAT16, flags=_lib.ACC_F32)
+    want = sum(base * m[r] + r for r in range(P)).to(torch.bfloat16)
+    assert torch.equal(bb[1].view(torch.bfloat16), want)
+
+
+def test_reduce_root_public_entry(gpu):
+    """hydra_reduce_root through a live 1-rank RCCL communicator: P = 1 is the identity
+    (reduce.cc:52-58), and bad roots are refused before anything is enqueued.  (A remapped
+    self-loop of the multi-rank plan, as for the allreduces, cannot run: the gather half only
+    sends on non-roots and only receives on the root.)"""
+    import torch
+
+    x = synth.stress_f32(2, 0, 100003)
+    comm = ring.XgmiComm(0, 1, gpu.index or 0, ring._rccl_unique_id())
+    try:
+        y = torch.from_numpy(x.copy()).to(gpu)
+        comm.reduce_(y, 0)
+        torch.cuda.synchronize()
+        assert np.array_equal(y.cpu().numpy().view(np.uint32), x.view(np.uint32))
+        for bad in (-1, 1):
+            with pytest.raises(_lib.HydraError):
+                comm.reduce_(y, bad)
+    finally:
+        comm.close()

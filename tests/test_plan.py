@@ -258,3 +258,73 @@ def test_bcube_plan(O, P, n):
     for r in range(P):
         assert np.array_equal(outs[r].view(np.uint32), exp.view(np.uint32)), r
         race_check(ring.plan("bcube", P, r, n, 4, 0, 0)[0])
+
+
+def _reduce_plans(root, P, n, es, ms, ch):
+    plans, scr = [], 0
+    for r in range(P):
+        ops, s = ring.plan_reduce(root, P, r, n, es, ms, ch)
+        plans.append(ops)
+        scr = max(scr, s)
+    return plans, scr
+
+
+@pytest.mark.parametrize("P,n,ms,ch", [(2, 1, 0, 0), (2, 1000, 128, 256), (3, 4099, 128, 1024),
+                                       (4, 262145, 0, 0), (7, 10007, 4096, 2048),
+                                       (8, 300001, 0, 1 << 16)])
+def test_reduce_root_plan_matches_reference(O, P, n, ms, ch):
+    """hydra_reduce_root (gloo::reduce to a root on device): the root's bucket equals the
+    reference's root output bit for bit (gloo::reduce's own geometry, reference fold order),
+    for every root; every rank's plan is race-free."""
+    xs = [synth.stress_f32(P, r, n) for r in range(P)]
+    for root in range(P):
+        plans, scr = _reduce_plans(root, P, n, 4, ms, ch)
+        outs = run_plan_numpy(O, None, xs, ms, ch, plans=plans, scr=scr)
+        exp = [x.copy() for x in xs]
+        O.reduce(exp, None, root, max_segment=ms or (1 << 20))
+        assert np.array_equal(outs[root].view(np.uint32), exp[root].view(np.uint32)), root
+        for ops in plans:
+            race_check(ops)
+
+
+def test_reduce_root_geometry_is_gloo_reduce():
+    """The plan's blocks follow gloo::reduce's segment geometry (reduce.cc:87-135), which is
+    not the allreduce ring's: e.g. 5 MiB of fp32 at P = 2 gives 6 segments of 1 MiB
+    (the ring: 6 segments of 873 816 B)."""
+    from oracle import oracle as Oc
+
+    assert Oc.reduce_plan(2, 1310720, 4, 1 << 20) == (6, 1 << 20, 3)
+    assert Oc.ring_plan(2, 1310720, 4, 1 << 20) == (6, 873816, 3)
+    for P, n, ms in [(3, 4099, 128), (8, 1 << 24, 1 << 20), (7, 1, 128), (2, 1310720, 1 << 20)]:
+        ns, sb, S = Oc.reduce_plan(P, n, 4, ms)
+        ops, _ = ring.plan_reduce(0, P, 0, n, 4, ms, 0)
+        # the root receives exactly the other owners' blocks
+        got = sorted((o["off"], o["off"] + o["bytes"]) for o in ops
+                     if o["kind"] == RECV and o["buf"] == 0)
+        blocks = []
+        for q in range(1, P):
+            lo, hi = min(n * 4, q * S * sb), min(n * 4, (q + 1) * S * sb)
+            if hi > lo:
+                blocks.append((lo, hi))
+        def merge(spans):
+            out = []
+            for lo, hi in sorted(spans):
+                if out and out[-1][1] == lo:
+                    out[-1] = (out[-1][0], hi)
+                else:
+                    out.append((lo, hi))
+            return out
+
+        assert merge(got) == merge(blocks), (P, n, ms)
+
+
+def test_bench_reduce_self_check_helper(O):
+    """bench.py's gloo::reduce self-check (ring.expected_reduce_f32, not the oracle) equals the
+    oracle's root result, and its geometry helper equals the oracle's."""
+    for P, n in [(1, 100), (2, 1 << 20), (3, 1_000_003), (8, 1 << 20), (5, 77)]:
+        assert ring.reduce_geometry(P, n, 4) == O.reduce_plan(P, n, 4, 1 << 20)
+        xs = [synth.stress_f32(P, r, n) for r in range(P)]
+        exp = [x.copy() for x in xs]
+        O.reduce(exp, None, P - 1)
+        assert np.array_equal(ring.expected_reduce_f32(xs).view(np.uint32),
+                              exp[P - 1].view(np.uint32)), (P, n)
