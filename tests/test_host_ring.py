@@ -284,3 +284,17 @@ def test_reduce_large_vs_reference(O):
     else:
         O.reduce(exp, [x.copy() for x in xs], 2)
         assert np.array_equal(outs[2].view(np.uint32), exp[2].view(np.uint32))
+
+
+@pytest.mark.parametrize("chunked", [False, True])
+def test_allreduce_test_single_pointer_p1_to_15(O, chunked):
+    """AllreduceTest SinglePointer (test/allreduce_test.cc:138-164, 236-244) on the host
+    runtime's old-style AllreduceRing<float> / AllreduceRingChunked<float>: P = 1..15 ranks
+    each holding `rank`, n in {4, 100, 1000, 10000}; every rank must hold P(P-1)/2."""
+    fn = fnptr(O, "orc_isum_f32")
+    for P in range(1, 16):
+        for n in (4, 100, 1000, 10000):
+            bufs = [[np.full(n, float(r), np.float32)] for r in range(P)]
+            host.allreduce_ring_old_threads(bufs, dtype_code=6, reducer_fn=fn, chunked=chunked)
+            for r in range(P):
+                assert np.all(bufs[r][0] == P * (P - 1) / 2), (P, n, r)
