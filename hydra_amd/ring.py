@@ -385,7 +385,21 @@ def bench_allreduce(args, dev) -> dict:
     import sys
     import threading
 
+    state = {}  # "result": builds the JSON line once the headline measurement is complete
+
     def _expire():
+        done = state.get("result")
+        if done is not None:  # headline measured: report it, flag the context as cut short
+            sys.stderr.write(f"[hydra bench] rank {rank}: watchdog expired in the context "
+                             "phase; reporting the headline\n")
+            sys.stderr.flush()
+            if rank == 0:
+                import json
+
+                r = done()
+                r["watchdog"] = "context measurements (other algorithms, config 5) cut short"
+                print(json.dumps(r), flush=True)
+            os._exit(0)
         sys.stderr.write(f"[hydra bench] rank {rank}: watchdog expired, aborting\n")
         sys.stderr.flush()
         os._exit(3)
@@ -561,6 +575,16 @@ def bench_allreduce(args, dev) -> dict:
                   "samples": len(lat), "note": "per step, synchronised, max over ranks"}
         # 4) context: the other algorithms on the same bucket (fewer steps)
         others = {}
+        c5 = None
+
+        def _result(ms_, lat_, others_, c5_):
+            return _bench_result(n, world, args, chosen, chunk, tuning, parity, full_ok, ms_,
+                                 lat_, dict(others_), c5_)
+
+        state["result"] = lambda: _result(ms, lat_ms, others, c5)
+        stall = float(os.environ.get("HYDRA_BENCH_STALL_CONTEXT", "0"))
+        if stall > 0:  # test hook: a context phase that hangs (tests the watchdog's report)
+            time.sleep(stall)
         k = max(5, args.steps // 4)
         for a in ("ring", "direct", "a2a", "rccl", "ring_old", "ring_chunked", "bcube", "peer2",
                   "peer1"):
@@ -594,7 +618,6 @@ def bench_allreduce(args, dev) -> dict:
         except _lib.HydraError as e:
             others["apipe_direct"] = f"n/a: {e}"
         # 5) BASELINE config 5: bf16 bucket of 256 Mi elements, fp32 accumulation
-        c5 = None
         if not getattr(args, "no_config5", False):
             n5 = 256 << 20
             xb = torch.from_numpy(synth.bf16_bits((j[: 1 << 20] % 7 - 3).astype(np.float32))
@@ -618,6 +641,7 @@ def bench_allreduce(args, dev) -> dict:
             c5 = {"elements": n5, "dtype": "bf16 (fp32 accumulate, one rounding)", "algo": c5_algo,
                   "ms": round(bms, 4), "algbw_GBps": round(b_alg, 2),
                   "busbw_GBps": round(b_alg * 2 * (world - 1) / world, 2)}
+            state["result"] = lambda: _result(ms, lat_ms, others, c5)
             del xb
     finally:
         if pg["peer"] is not None:
@@ -625,6 +649,13 @@ def bench_allreduce(args, dev) -> dict:
         comm.close()
         rail2.close()
         dog.cancel()
+    return _result(ms, lat_ms, others, c5)
+
+
+def _bench_result(n, world, args, chosen, chunk, tuning, parity, full_ok, ms, lat_ms, others,
+                  c5) -> dict:
+    """The N>1 bench JSON line (bench_allreduce; also printed by its watchdog once the headline
+    is measured)."""
     bucket = 4.0 * n
     algbw = bucket / (ms * 1e-3) / 1e9
     busbw = algbw * 2 * (world - 1) / world
