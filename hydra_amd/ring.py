@@ -465,47 +465,6 @@ def bench_allreduce(args, dev) -> dict:
                 parity[a] = "barrier timeout"
                 continue
             parity[a] = "bit-exact" if ok_all else "MISMATCH"
-        t = torch.from_numpy(xs[rank].copy()).to(dev)
-        comm.allreduce_(t, algo="ring_old")
-        torch.cuda.synchronize(dev)
-        ok = bool(np.array_equal(t.cpu().numpy().view(np.uint32),
-                                 expected_old_ring_f32(xs, rank).view(np.uint32)))
-        parity["ring_old"] = ("bit-exact" if max_over_ranks(0.0 if ok else 1.0, dev) == 0.0
-                              else "MISMATCH")
-        t = torch.from_numpy(xs[rank].copy()).to(dev)
-        comm.allreduce_(t, algo="ring_chunked")
-        torch.cuda.synchronize(dev)
-        ok = bool(np.array_equal(t.cpu().numpy().view(np.uint32),
-                                 expected_chunked_ring_f32(xs).view(np.uint32)))
-        parity["ring_chunked"] = ("bit-exact" if max_over_ranks(0.0 if ok else 1.0, dev) == 0.0
-                                  else "MISMATCH")
-        t = torch.from_numpy(xs[rank].copy()).to(dev)
-        comm.allreduce_(t, algo="bcube")
-        torch.cuda.synchronize(dev)
-        ok = bool(np.array_equal(t.cpu().numpy().view(np.uint32),
-                                 expected_bcube_f32(xs).view(np.uint32)))
-        parity["bcube"] = ("bit-exact" if max_over_ranks(0.0 if ok else 1.0, dev) == 0.0
-                           else "MISMATCH")
-        # gloo::reduce to the last rank (hydra_reduce_root): only the root's bucket is defined
-        t = torch.from_numpy(xs[rank].copy()).to(dev)
-        comm.reduce_(t, world - 1)
-        torch.cuda.synchronize(dev)
-        ok = rank != world - 1 or bool(np.array_equal(
-            t.cpu().numpy().view(np.uint32), expected_reduce_f32(xs).view(np.uint32)))
-        parity["reduce_root"] = ("bit-exact" if max_over_ranks(0.0 if ok else 1.0, dev) == 0.0
-                                 else "MISMATCH")
-        # two rails (bew_allreduce_a): each part is the reference ring on its slice
-        t = torch.from_numpy(xs[rank].copy()).to(dev)
-        comm.apipe_allreduce_(rail2, t, algo="direct")
-        torch.cuda.synchronize(dev)
-        e1, _ = split_elements(0, world, pn)
-        exp2 = np.concatenate([expected_fold_f32([x[:e1] for x in xs]) if e1 else
-                               np.empty(0, np.float32),
-                               expected_fold_f32([x[e1:] for x in xs]) if e1 < pn else
-                               np.empty(0, np.float32)])
-        ok = bool(np.array_equal(t.cpu().numpy().view(np.uint32), exp2.view(np.uint32)))
-        parity["apipe"] = ("bit-exact" if max_over_ranks(0.0 if ok else 1.0, dev) == 0.0
-                           else "MISMATCH")
         # 2) exactness at full size: integer-valued inputs whose sums are exact in fp32
         j = np.arange(n, dtype=np.int64)
         x0 = torch.from_numpy(((j % 1024) * (rank + 1)).astype(np.float32)).to(dev)
@@ -598,6 +557,49 @@ def bench_allreduce(args, dev) -> dict:
         stall = float(os.environ.get("HYDRA_BENCH_STALL_CONTEXT", "0"))
         if stall > 0:  # test hook: a context phase that hangs (tests the watchdog's report)
             time.sleep(stall)
+        # parity of the schedules the headline does not use (after it: a hang here cannot lose
+        # the measured line)
+        t = torch.from_numpy(xs[rank].copy()).to(dev)
+        comm.allreduce_(t, algo="ring_old")
+        torch.cuda.synchronize(dev)
+        ok = bool(np.array_equal(t.cpu().numpy().view(np.uint32),
+                                 expected_old_ring_f32(xs, rank).view(np.uint32)))
+        parity["ring_old"] = ("bit-exact" if max_over_ranks(0.0 if ok else 1.0, dev) == 0.0
+                              else "MISMATCH")
+        t = torch.from_numpy(xs[rank].copy()).to(dev)
+        comm.allreduce_(t, algo="ring_chunked")
+        torch.cuda.synchronize(dev)
+        ok = bool(np.array_equal(t.cpu().numpy().view(np.uint32),
+                                 expected_chunked_ring_f32(xs).view(np.uint32)))
+        parity["ring_chunked"] = ("bit-exact" if max_over_ranks(0.0 if ok else 1.0, dev) == 0.0
+                                  else "MISMATCH")
+        t = torch.from_numpy(xs[rank].copy()).to(dev)
+        comm.allreduce_(t, algo="bcube")
+        torch.cuda.synchronize(dev)
+        ok = bool(np.array_equal(t.cpu().numpy().view(np.uint32),
+                                 expected_bcube_f32(xs).view(np.uint32)))
+        parity["bcube"] = ("bit-exact" if max_over_ranks(0.0 if ok else 1.0, dev) == 0.0
+                           else "MISMATCH")
+        # gloo::reduce to the last rank (hydra_reduce_root): only the root's bucket is defined
+        t = torch.from_numpy(xs[rank].copy()).to(dev)
+        comm.reduce_(t, world - 1)
+        torch.cuda.synchronize(dev)
+        ok = rank != world - 1 or bool(np.array_equal(
+            t.cpu().numpy().view(np.uint32), expected_reduce_f32(xs).view(np.uint32)))
+        parity["reduce_root"] = ("bit-exact" if max_over_ranks(0.0 if ok else 1.0, dev) == 0.0
+                                 else "MISMATCH")
+        # two rails (bew_allreduce_a): each part is the reference ring on its slice
+        t = torch.from_numpy(xs[rank].copy()).to(dev)
+        comm.apipe_allreduce_(rail2, t, algo="direct")
+        torch.cuda.synchronize(dev)
+        e1, _ = split_elements(0, world, pn)
+        exp2 = np.concatenate([expected_fold_f32([x[:e1] for x in xs]) if e1 else
+                               np.empty(0, np.float32),
+                               expected_fold_f32([x[e1:] for x in xs]) if e1 < pn else
+                               np.empty(0, np.float32)])
+        ok = bool(np.array_equal(t.cpu().numpy().view(np.uint32), exp2.view(np.uint32)))
+        parity["apipe"] = ("bit-exact" if max_over_ranks(0.0 if ok else 1.0, dev) == 0.0
+                           else "MISMATCH")
         k = max(5, args.steps // 4)
         for a in ("ring", "direct", "a2a", "rccl", "ring_old", "ring_chunked", "bcube", "peer2",
                   "peer1"):
