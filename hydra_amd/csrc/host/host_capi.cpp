@@ -105,7 +105,7 @@ int old_ring(bool chunked, int P, int nptr, size_t n, void** bufs, int reducer, 
 }
 template <typename T>
 int hip_ring(int P, int nptr, size_t n, void** bufs, int workspace, int user_streams, char* err,
-             size_t errlen) {
+             size_t errlen, bool chunked = false) {
   return spawn(P, 1, err, errlen, [&](int r, std::vector<std::shared_ptr<hydra::Context>>& c) {
     std::vector<T*> ptrs;
     for (int i = 0; i < nptr; i++) ptrs.push_back(static_cast<T*>(bufs[r * nptr + i]));
@@ -116,7 +116,15 @@ int hip_ring(int P, int nptr, size_t n, void** bufs, int workspace, int user_str
       streams.resize(nptr);
       for (auto& s : streams) hydra::gloo_compat::enforce(hydra_stream_create(dev, &s));
     }
-    if (workspace == HYDRA_WORKSPACE_DEVICE) {
+    if (chunked && workspace == HYDRA_WORKSPACE_DEVICE) {
+      hydra::HipAllreduceRingChunked<T, hydra::HipDeviceWorkspace<T>> algo(c[0], ptrs, (int)n,
+                                                                           streams);
+      algo.run();
+    } else if (chunked) {
+      hydra::HipAllreduceRingChunked<T, hydra::HipHostWorkspace<T>> algo(c[0], ptrs, (int)n,
+                                                                         streams);
+      algo.run();
+    } else if (workspace == HYDRA_WORKSPACE_DEVICE) {
       hydra::HipAllreduceRing<T, hydra::HipDeviceWorkspace<T>> algo(c[0], ptrs, (int)n, streams);
       algo.run();
     } else {
@@ -273,6 +281,27 @@ int hydra_host_hip_ring_threads(int P, int nptr, int dtype, size_t n, void** dev
     case HYDRA_INT64: return hip_ring<int64_t>(P, nptr, n, dev_bufs, workspace, user_streams, err, errlen);
   }
   set_err(err, errlen, "unsupported dtype for HipAllreduceRing");
+  return 3;
+}
+
+int hydra_host_hip_ring_chunked_threads(int P, int nptr, int dtype, size_t n, void** dev_bufs,
+                                        int workspace, int user_streams, char* err,
+                                        size_t errlen) {
+  if (P < 1 || nptr < 1 || !dev_bufs || n > (size_t)INT32_MAX) {
+    set_err(err, errlen, "invalid arguments");
+    return 2;
+  }
+  switch (dtype) {
+    case HYDRA_FLOAT32:
+      return hip_ring<float>(P, nptr, n, dev_bufs, workspace, user_streams, err, errlen, true);
+    case HYDRA_INT32:
+      return hip_ring<int32_t>(P, nptr, n, dev_bufs, workspace, user_streams, err, errlen, true);
+    case HYDRA_FLOAT64:
+      return hip_ring<double>(P, nptr, n, dev_bufs, workspace, user_streams, err, errlen, true);
+    case HYDRA_INT64:
+      return hip_ring<int64_t>(P, nptr, n, dev_bufs, workspace, user_streams, err, errlen, true);
+  }
+  set_err(err, errlen, "unsupported dtype for HipAllreduceRingChunked");
   return 3;
 }
 

@@ -37,6 +37,7 @@ def lib():
         L.hydra_host_allreduce_ring_old_threads.argtypes = [i, i, i, sz, vp, i, vp,
                                                             ctypes.c_char_p, sz]
         L.hydra_host_hip_ring_threads.argtypes = [i, i, i, sz, vp, i, i, ctypes.c_char_p, sz]
+        L.hydra_host_hip_ring_chunked_threads.argtypes = L.hydra_host_hip_ring_threads.argtypes
         L.hydra_host_allreduce_ring_chunked_threads.argtypes = \
             L.hydra_host_allreduce_ring_old_threads.argtypes
         L.hydra_host_reduce_threads.argtypes = [i, i, i, sz, vp, vp, i, sz, i, vp,
@@ -145,9 +146,10 @@ def allreduce_ring_old_threads(bufs, dtype_code=None, reducer_fn=None, chunked=F
 
 
 def hip_ring_threads(tensors, workspace: str = "host", user_streams: bool = False,
-                     dtype_code=None):
+                     dtype_code=None, chunked: bool = False):
     """hydra::HipAllreduceRing<T, W>::run() (gloo::CudaAllreduceRing) on len(tensors)
-    thread-ranks; tensors: [rank][ptr] contiguous device tensors, reduced in place."""
+    thread-ranks; tensors: [rank][ptr] contiguous device tensors, reduced in place.
+    chunked: HipAllreduceRingChunked<T, W> (gloo::CudaAllreduceRingChunked) instead."""
     from .reduce import _torch_dtype_code
 
     P, nptr = len(tensors), len(tensors[0])
@@ -159,7 +161,9 @@ def hip_ring_threads(tensors, workspace: str = "host", user_streams: bool = Fals
                 raise _lib.HydraError(1, "contiguous, equally sized device tensors required")
     ws = {"host": 0, "device": 1}[workspace]
     err = ctypes.create_string_buffer(512)
-    rc = lib().hydra_host_hip_ring_threads(
+    fn = (lib().hydra_host_hip_ring_chunked_threads if chunked
+          else lib().hydra_host_hip_ring_threads)
+    rc = fn(
         P, nptr, code, n, ctypes.cast(_ptrs_int([t.data_ptr() for r in tensors for t in r]),
                                       ctypes.c_void_p), ws, int(user_streams), err, 512)
     if rc:

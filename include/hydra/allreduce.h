@@ -349,6 +349,71 @@ class AllreduceRing {
 // handshake is implicit (a receive is posted only once its inbox is free; the transport holds
 // early bytes), and empty chunks move nothing instead of the reference's 1-element
 // placeholder (:218-225), which its receiver ignores.
+namespace detail {
+// AllreduceRingChunked's schedule (allreduce_ring_chunked.h:77-200) over `count` elements of
+// `es` bytes at `base` (host memory the transport sends from): 2P chunks of `chunk` elements,
+// two inboxes of `chunk` elements, a reduce pass whose steps call fold(dst, box, n) (dst op=
+// box) and a broadcast pass whose steps call copy(dst, box, n).  Shared by the host class
+// and HipAllreduceRingChunked<T, W> (cuda_allreduce_ring_chunked.cc), which differ only in
+// where the fold runs.
+template <typename Fold, typename Copy>
+void chunked_ring(Context& ctx, char* base, size_t count, size_t es, size_t chunk, char* inbox0,
+                  char* inbox1, uint64_t slot, Fold fold, Copy copy) {
+  const int P = ctx.size, r = ctx.rank;
+  if (P <= 1 || count == 0) return;
+  const int right = (r + 1) % P, left = (r + P - 1) % P;
+  const int C = 2 * P, steps = 2 * C - 4;
+  const auto tmo = ctx.getTimeout();
+  auto out = ctx.createUnboundBuffer(base, count * es);
+  char* inbox[2] = {inbox0, inbox1};
+  std::unique_ptr<UnboundBuffer> in[2] = {ctx.createUnboundBuffer(inbox0, chunk * es),
+                                          ctx.createUnboundBuffer(inbox1, chunk * es)};
+  std::vector<char> sent(steps, 0);
+  auto chunk_of = [&](int i) {  // chunk received at step i
+    const int round = i < C - 2 ? i + 2 : i - (C - 2);
+    return ((2 * r) - (round & ~1) + (round & 1) + C) % C;
+  };
+  auto len_of = [&](int co) {
+    const size_t off = (size_t)co * chunk;
+    return off >= count ? (size_t)0 : std::min(chunk, count - off);
+  };
+  auto post_recv = [&](int i) {
+    const size_t l = len_of(chunk_of(i));
+    if (l) in[i & 1]->recv(left, slot, 0, l * es);
+  };
+  auto post_send = [&](int i, int co) {
+    const size_t l = len_of(co);
+    if (l) out->send(right, slot, (size_t)co * chunk * es, l * es);
+    sent[i] = l != 0;
+  };
+  int waited = 0;  // sends completed in order (waitSend pops the oldest)
+  auto wait_sends_through = [&](int i) {
+    for (; waited <= i && waited < steps; waited++)
+      if (sent[waited]) out->waitSend(tmo);
+  };
+  post_recv(0);
+  post_recv(1);
+  post_send(0, 2 * r);
+  post_send(1, 2 * r + 1);
+  for (int i = 0; i < steps; i++) {
+    const int co = chunk_of(i);
+    const size_t l = len_of(co);
+    char* dst = base + (size_t)co * chunk * es;
+    if (l) {
+      in[i & 1]->waitRecv(tmo);
+      wait_sends_through(i);  // a still-queued send of this chunk must not see the update
+      if (i < C - 2) fold(dst, inbox[i & 1], l);
+      else copy(dst, inbox[i & 1], l);
+    }
+    if (i + 2 < steps) {
+      post_recv(i + 2);  // inbox[i&1] is free again
+      post_send(i + 2, co);
+    }
+  }
+  wait_sends_through(steps - 1);
+}
+}  // namespace detail
+
 template <typename T>
 class AllreduceRingChunked {
  public:
@@ -366,60 +431,13 @@ class AllreduceRingChunked {
   void run() {
     const size_t bytes = (size_t)count_ * sizeof(T);
     for (size_t i = 1; i < ptrs_.size(); i++) fn_->call(ptrs_[0], ptrs_[i], count_);
-    const int P = ctx_->size, r = ctx_->rank;
-    if (P > 1 && count_ > 0) {
-      const int right = (r + 1) % P, left = (r + P - 1) % P;
-      const int C = (int)chunks_, steps = 2 * C - 4;
-      const auto tmo = ctx_->getTimeout();
-      auto out = ctx_->createUnboundBuffer(ptrs_[0], bytes);
-      std::unique_ptr<UnboundBuffer> in[2] = {
-          ctx_->createUnboundBuffer(inbox_[0].data(), inbox_[0].size()),
-          ctx_->createUnboundBuffer(inbox_[1].data(), inbox_[1].size())};
-      std::vector<char> sent(steps, 0);
-      auto chunk_of = [&](int i) {  // chunk received at step i
-        const int round = i < C - 2 ? i + 2 : i - (C - 2);
-        return ((2 * r) - (round & ~1) + (round & 1) + C) % C;
-      };
-      auto len_of = [&](int co) {
-        const size_t off = (size_t)co * chunk_;
-        return off >= (size_t)count_ ? (size_t)0 : std::min(chunk_, (size_t)count_ - off);
-      };
-      auto post_recv = [&](int i) {
-        const size_t l = len_of(chunk_of(i));
-        if (l) in[i & 1]->recv(left, kSlot, 0, l * sizeof(T));
-      };
-      auto post_send = [&](int i, int co) {
-        const size_t l = len_of(co);
-        if (l) out->send(right, kSlot, (size_t)co * chunk_ * sizeof(T), l * sizeof(T));
-        sent[i] = l != 0;
-      };
-      int waited = 0;  // sends completed in order (waitSend pops the oldest)
-      auto wait_sends_through = [&](int i) {
-        for (; waited <= i && waited < steps; waited++)
-          if (sent[waited]) out->waitSend(tmo);
-      };
-      post_recv(0);
-      post_recv(1);
-      post_send(0, 2 * r);
-      post_send(1, 2 * r + 1);
-      for (int i = 0; i < steps; i++) {
-        const int co = chunk_of(i);
-        const size_t l = len_of(co);
-        T* dst = ptrs_[0] + (size_t)co * chunk_;
-        const T* box = reinterpret_cast<const T*>(inbox_[i & 1].data());
-        if (l) {
-          in[i & 1]->waitRecv(tmo);
-          wait_sends_through(i);  // a still-queued send of this chunk must not see the update
-          if (i < C - 2) fn_->call(dst, box, l);
-          else std::memcpy(dst, box, l * sizeof(T));
-        }
-        if (i + 2 < steps) {
-          post_recv(i + 2);  // inbox[i&1] is free again
-          post_send(i + 2, co);
-        }
-      }
-      wait_sends_through(steps - 1);
-    }
+    detail::chunked_ring(
+        *ctx_, reinterpret_cast<char*>(ptrs_[0]), (size_t)count_, sizeof(T), chunk_,
+        inbox_[0].data(), inbox_[1].data(), kSlot,
+        [this](char* dst, const char* box, size_t l) {
+          fn_->call(reinterpret_cast<T*>(dst), reinterpret_cast<const T*>(box), l);
+        },
+        [](char* dst, const char* box, size_t l) { std::memcpy(dst, box, l * sizeof(T)); });
     for (size_t i = 1; i < ptrs_.size(); i++) std::memcpy(ptrs_[i], ptrs_[0], bytes);
   }
 

@@ -24,6 +24,7 @@
 // (fn_ = CudaReductionFunction<T>::sum, cuda_allreduce_ring.cc:26).
 #pragma once
 
+#include <algorithm>
 #include <cstring>
 #include <memory>
 #include <type_traits>
@@ -201,6 +202,132 @@ class HipAllreduceRing {
   std::vector<hydra_stream_t> streams_, owned_;
   detail::Pinned boxes_[2], scratch_host_;
   detail::DeviceMem inbox_dev_, local_dev_;
+  std::unique_ptr<gloo_compat::ContextPool::Lease> lease_;
+};
+
+// hydra::HipAllreduceRingChunked<T, W> -- the HIP analog of gloo::CudaAllreduceRingChunked<T, W>
+// (gloo/gloo/cuda_allreduce_ring_chunked.{h,cc}): same constructor and run(), same result on
+// every rank -- AllreduceRingChunked's (allreduce_ring_chunked.h) over each rank's locally
+// reduced value.  The local reduce is CudaLocalNativeReduce's pairwise tree in pointer order
+// for both workspaces (cudaDeviceReduce, cuda_collectives_device.h:29-56; memcpy for one
+// pointer), the ring is the shared chunked schedule (allreduce.h detail::chunked_ring, 2P
+// chunks of max(256, ceil(n / 2P))), and the broadcast copies the result to every pointer.
+//   HipHostWorkspace<T>:   scratch and inboxes are pinned host memory; each fold is
+//       hydra_reduce_host, i.e. the gfx950 kernel streaming the pinned chunks (zero-copy).
+//   HipDeviceWorkspace<T>: scratch is ptrs[0] on the device; each fold copies the received
+//       chunk to a device inbox, runs the kernel on the device chunk and refreshes the pinned
+//       mirror the transport sends from (TCP cannot read HBM).
+template <typename T, typename W = HipHostWorkspace<T>>
+class HipAllreduceRingChunked {
+  static constexpr bool kDeviceWorkspace = std::is_same<W, HipDeviceWorkspace<T>>::value;
+  static_assert(kDeviceWorkspace || std::is_same<W, HipHostWorkspace<T>>::value,
+                "W must be HipHostWorkspace<T> or HipDeviceWorkspace<T>");
+
+ public:
+  HipAllreduceRingChunked(const std::shared_ptr<Context>& context, const std::vector<T*>& ptrs,
+                          int count,
+                          const std::vector<hydra_stream_t>& streams = std::vector<hydra_stream_t>())
+      : ctx_(context), ptrs_(ptrs), count_(count), bytes_((size_t)count * sizeof(T)),
+        synchronize_outputs_(streams.empty()) {
+    using detail::enforce;
+    if (ptrs_.empty()) throw EnforceNotMet("HipAllreduceRingChunked: no pointers");
+    if (count_ < 0) throw EnforceNotMet("HipAllreduceRingChunked: negative count");
+    if (!streams.empty() && streams.size() != ptrs_.size())
+      throw EnforceNotMet("HipAllreduceRingChunked: streams.size() != ptrs.size()");
+    const size_t chunks = 2 * (size_t)ctx_->size;  // cuda_allreduce_ring_chunked.cc:57-60
+    chunk_ = std::max<size_t>(256, ((size_t)count_ + chunks - 1) / chunks);
+    if (count_ == 0) return;
+    enforce(hydra_pointer_device(ptrs_[0], &device_));
+    if (device_ < 0) throw EnforceNotMet("HipAllreduceRingChunked: ptrs must be device memory");
+    for (T* p : ptrs_) {
+      int d = -1;
+      enforce(hydra_pointer_device(p, &d));
+      if (d != device_)
+        throw EnforceNotMet("HipAllreduceRingChunked: all pointers must be on one device");
+    }
+    if (streams.empty()) {
+      owned_.resize(ptrs_.size());
+      for (auto& s : owned_) enforce(hydra_stream_create(device_, &s));
+      streams_ = owned_;
+    } else {
+      streams_ = streams;
+    }
+    scratch_host_ = detail::Pinned(bytes_);
+    inbox_[0] = detail::Pinned(chunk_ * sizeof(T));
+    inbox_[1] = detail::Pinned(chunk_ * sizeof(T));
+    if (kDeviceWorkspace) inbox_dev_ = detail::DeviceMem(device_, chunk_ * sizeof(T));
+  }
+
+  ~HipAllreduceRingChunked() {
+    for (auto s : owned_) hydra_stream_destroy(s);
+  }
+  HipAllreduceRingChunked(const HipAllreduceRingChunked&) = delete;
+  HipAllreduceRingChunked& operator=(const HipAllreduceRingChunked&) = delete;
+
+  void run() {
+    using detail::enforce;
+    if (count_ == 0) return;
+    const int dt = gloo_compat::dtype_of<T>();
+    hydra_stream_t s0 = streams_[0];
+    for (size_t i = 1; i < streams_.size(); i++) enforce(hydra_stream_synchronize(streams_[i]));
+    for (size_t sz = 1; sz < ptrs_.size(); sz *= 2)  // CudaLocalNativeReduce tree, in place
+      for (size_t j = 0; j + sz < ptrs_.size(); j += 2 * sz)
+        enforce(hydra_reduce(HYDRA_SUM, dt, ptrs_[j], ptrs_[j], ptrs_[j + sz], count_, s0));
+    char* const dscratch = reinterpret_cast<char*>(ptrs_[0]);
+    char* const hscratch = static_cast<char*>(scratch_host_.p);
+    enforce(hydra_memcpy_async(hscratch, dscratch, bytes_, s0));
+    enforce(hydra_stream_synchronize(s0));
+    if (ctx_->size > 1) {
+      if (!kDeviceWorkspace)
+        lease_.reset(new gloo_compat::ContextPool::Lease(
+            gloo_compat::ContextPool::instance(device_).acquire()));
+      auto fold = [&](char* dst, const char* box, size_t n) {
+        if (!kDeviceWorkspace) {
+          enforce(hydra_reduce_host(lease_->get(), HYDRA_SUM, dt, dst, dst, box, n));
+          return;
+        }
+        char* dev = dscratch + (dst - hscratch);
+        enforce(hydra_memcpy_async(inbox_dev_.p, box, n * sizeof(T), s0));
+        enforce(hydra_reduce(HYDRA_SUM, dt, dev, dev, inbox_dev_.p, n, s0));
+        enforce(hydra_memcpy_async(dst, dev, n * sizeof(T), s0));  // what the next send reads
+        enforce(hydra_stream_synchronize(s0));
+      };
+      auto copy = [&](char* dst, const char* box, size_t n) {
+        std::memcpy(dst, box, n * sizeof(T));
+        if (kDeviceWorkspace) {
+          enforce(hydra_memcpy_async(dscratch + (dst - hscratch), box, n * sizeof(T), s0));
+          enforce(hydra_stream_synchronize(s0));  // the inbox is reused two steps later
+        }
+      };
+      detail::chunked_ring(*ctx_, hscratch, (size_t)count_, sizeof(T), chunk_,
+                           static_cast<char*>(inbox_[0].p), static_cast<char*>(inbox_[1].p),
+                           kSlot, fold, copy);
+      lease_.reset();
+    }
+    // broadcast (cudaDeviceBroadcast): every pointer gets the result
+    if (kDeviceWorkspace) {
+      enforce(hydra_stream_synchronize(s0));
+      for (size_t i = 1; i < ptrs_.size(); i++)
+        enforce(hydra_memcpy_async(ptrs_[i], dscratch, bytes_, streams_[i]));
+    } else {
+      for (size_t i = 0; i < ptrs_.size(); i++)
+        enforce(hydra_memcpy_async(ptrs_[i], hscratch, bytes_, streams_[i]));
+    }
+    if (synchronize_outputs_)
+      for (auto s : streams_) enforce(hydra_stream_synchronize(s));
+  }
+
+ private:
+  static constexpr uint64_t kSlot = uint64_t(0x14) << 56;
+  std::shared_ptr<Context> ctx_;
+  std::vector<T*> ptrs_;
+  int count_;
+  size_t bytes_, chunk_ = 0;
+  bool synchronize_outputs_;
+  int device_ = -1;
+  std::vector<hydra_stream_t> streams_, owned_;
+  detail::Pinned scratch_host_, inbox_[2];
+  detail::DeviceMem inbox_dev_;
   std::unique_ptr<gloo_compat::ContextPool::Lease> lease_;
 };
 

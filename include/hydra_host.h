@@ -68,6 +68,12 @@ int hydra_host_allreduce_ring_old_threads(int P, int nptr, int dtype, size_t n, 
 int hydra_host_hip_ring_threads(int P, int nptr, int dtype, size_t n, void** dev_bufs,
                                 int workspace, int user_streams, char* err, size_t errlen);
 
+/* hydra::HipAllreduceRingChunked<T, W> (gloo::CudaAllreduceRingChunked<T, W>,
+ * cuda_allreduce_ring_chunked.cc), same arguments as hydra_host_hip_ring_threads. */
+int hydra_host_hip_ring_chunked_threads(int P, int nptr, int dtype, size_t n, void** dev_bufs,
+                                        int workspace, int user_streams, char* err,
+                                        size_t errlen);
+
 /* gloo::AllreduceRingChunked<T>::run() (allreduce_ring_chunked.h:20-248), same arguments. */
 int hydra_host_allreduce_ring_chunked_threads(int P, int nptr, int dtype, size_t n, void** bufs,
                                               int reducer, hydra_inplace_fn fn, char* err,

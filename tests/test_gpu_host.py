@@ -212,3 +212,32 @@ def test_reduce_gpu_reducer_large(gpu, O, pinned):
     exp = [np.zeros(n, np.float32) for _ in range(P)]
     O.reduce(exp, [x.copy() for x in xs], root)
     assert np.array_equal(outs[root].view(np.uint32), exp[root].view(np.uint32))
+
+
+@pytest.mark.parametrize("workspace", ["host", "device"])
+@pytest.mark.parametrize("P,nptr,n,dt", [(1, 1, 1000, "f32"), (2, 1, 262145, "f32"),
+                                         (3, 2, 100003, "f32"), (4, 4, 4099, "f32"),
+                                         (5, 3, 7, "f32"), (3, 2, 70001, "i32"),
+                                         (2, 1, 0, "f32")])
+def test_hip_allreduce_ring_chunked(gpu, O, workspace, P, nptr, n, dt):
+    """hydra::HipAllreduceRingChunked<T, W> (gloo::CudaAllreduceRingChunked<T, W>): every rank
+    ends with AllreduceRingChunked's result (pinned to the reference by the chunked_ring
+    fixtures) over the locally reduced values -- CudaLocalNativeReduce's pairwise tree for both
+    workspaces (cuda_collectives_device.h:29-56); every pointer gets the result."""
+    import torch
+
+    code = {"f32": 6, "i32": 2}[dt]
+    if dt == "f32":
+        xs = [[synth.stress_f32(P, r, n, seed=50 + i) for i in range(nptr)] for r in range(P)]
+    else:
+        xs = [[synth.int32_bucket(P, r, n, seed=50 + i) for i in range(nptr)] for r in range(P)]
+    exp = [[_tree(O, xs[r], code)] for r in range(P)]
+    if n:
+        O.allreduce_ring_chunked(exp, dtype_code=code)
+    for user_streams in (False, True):
+        ts = [[torch.from_numpy(x.copy()).to(gpu) for x in xs[r]] for r in range(P)]
+        host.hip_ring_threads(ts, workspace=workspace, user_streams=user_streams, chunked=True)
+        for r in range(P):
+            for i in range(nptr):
+                got = ts[r][i].cpu().numpy()
+                assert np.array_equal(got.view(np.uint32), exp[r][0].view(np.uint32)), (r, i)
