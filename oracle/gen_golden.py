@@ -223,6 +223,49 @@ def gen_chunked_ring(out: dict, meta: dict) -> None:
     meta["chunked_ring"] = rows
 
 
+def gen_halving_doubling(out: dict, meta: dict) -> None:
+    """AllreduceHalvingDoubling<T> (allreduce_halving_doubling.h:37-358): P covers one binary
+    block (1, 2, 4, 8), two (3, 5, 6, 12) and three (7, 11); n covers fewer elements than
+    chunks, ragged last chunks and empty steps."""
+    rows = []
+    rng = np.random.default_rng(79)
+    for name, code in (("f32", 6), ("i32", 2), ("f16", 8)):
+        for P in (1, 2, 3, 4, 5, 6, 7, 8, 11, 12):
+            for n in ((1, 7, 100, 1001, 4099) if P in (3, 7, 8) else (1, 7, 100, 1001)):
+                for nptr in ((1, 2) if n <= 100 else (1,)):
+                    if name == "f32":
+                        bufs = [[synth.stress_f32(P, r, n, seed=700 + i) for i in range(nptr)]
+                                for r in range(P)]
+                    elif name == "i32":
+                        bufs = [[synth.int32_bucket(P, r, n, seed=700 + i) for i in range(nptr)]
+                                for r in range(P)]
+                    else:
+                        bufs = [[np.array([O.f2h(float(v)) for v in rng.uniform(-8, 8, n)],
+                                          np.uint16) for _ in range(nptr)] for _ in range(P)]
+                    key = f"hd_{name}_P{P}_n{n}_k{nptr}"
+                    out[key + "_in"] = np.stack([np.stack(b) for b in bufs])
+                    O.ref_allreduce_halving_doubling(bufs, dtype_code=code)
+                    res = np.stack([np.stack(b) for b in bufs])
+                    assert all(np.array_equal(res[0].view(np.uint8), res[r].view(np.uint8))
+                               for r in range(P)), key  # every rank holds the same bits
+                    out[key + "_out"] = res[0, 0]
+                    rows.append({"key": key, "P": P, "n": n, "nptr": nptr, "dtype": code})
+    meta["halving_doubling"] = rows
+
+
+def main_hd() -> None:
+    """Fixtures added after golden.npz was frozen go to their own file (golden_hd.*)."""
+    out: dict = {}
+    meta: dict = {"generator": "oracle/gen_golden.py --hd",
+                  "reference": "hydra-ppopp2024/hydra snapshot 2025-02-12, gloo core built by "
+                               "oracle/Makefile (g++ -O3 -DNDEBUG)"}
+    gen_halving_doubling(out, meta)
+    np.savez_compressed(os.path.join(GOLD, "golden_hd.npz"), **out)
+    with open(os.path.join(GOLD, "golden_hd.json"), "w") as f:
+        json.dump(meta, f, indent=1)
+    print(f"wrote {len(out)} arrays to golden_hd.npz")
+
+
 def gen_new_test(meta: dict) -> None:
     """AllreduceNewTest.Default (test/allreduce_test.cc:302-362): confirm the reference meets the
     closed form k*stride^2 + stride(stride-1)/2 for uint64, every combination we test."""
@@ -340,4 +383,6 @@ def main() -> None:
 
 
 if __name__ == "__main__":
-    main()
+    if not O.ref_available():
+        raise SystemExit("oracle/_ref/libgloo_ref.so missing: make -C oracle ref")
+    main_hd() if "--hd" in sys.argv[1:] else main()

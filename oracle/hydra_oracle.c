@@ -511,6 +511,164 @@ int orc_allreduce_ring_chunked(int P, int nptr, int op, int dtype, size_t n, voi
   return 0;
 }
 
+/* ---- AllreduceHalvingDoubling<T> (gloo/gloo/allreduce_halving_doubling.h:37-358) ----
+ * steps = floor(log2 P), 2^steps chunks of ceil(n / 2^steps) elements (:76-78).  Ranks form
+ * binary blocks, the largest first (:39-64).  Inside a block: recursive-halving reduce-scatter
+ * (step i exchanges with rank ^ 2^i, local op= received, :241-256), then recursive-doubling
+ * allgather (:316-338).  Between blocks: each rank folds the piece its smaller-block partner
+ * sends (:263-269), scatters its reduced chunk to the next larger block in bit-reversed order
+ * (:273-287), takes the larger block's finished pieces back (:293-301) and forwards its chunk to
+ * the smaller block (:306-313).  Restated as a phase-ordered simulation: the schedule's only
+ * cross-rank dependencies are those messages, so applying them block by block in that order
+ * yields the reference's bits. */
+typedef struct {
+  uint32_t off, size, steps, rib, smaller, larger;
+  size_t send_off[32], recv_off[32], send_cnt[32], recv_cnt[32];
+  size_t sc_larger; /* sendCountToLargerBlock_ (:195-196) */
+} hd_rank;
+
+static uint32_t hd_log2(uint64_t x) { uint32_t l = 0; while (x >>= 1) l++; return l; }
+
+static uint32_t hd_rev(uint32_t ctr, uint32_t nbits) { /* reverseLastNBits (:23-34) */
+  uint32_t r = 0;
+  for (uint32_t b = 0; b < nbits; b++) r = (r << 1) | ((ctr >> b) & 1u);
+  return r;
+}
+
+static void hd_geometry(int P, int rank, size_t n, hd_rank* g) {
+  const uint32_t steps = hd_log2((uint64_t)P);
+  const size_t chunk = (n + ((size_t)1 << steps) - 1) >> steps;
+  memset(g, 0, sizeof *g);
+  uint32_t off = (uint32_t)P, bs = 1, cur = 0, prev = 0;
+  do { /* initBinaryBlocks (:39-64) */
+    if ((uint32_t)P & bs) {
+      prev = cur;
+      cur = bs;
+      off -= bs;
+      if (g->size) { g->larger = cur; break; }
+      if (off <= (uint32_t)rank) { g->off = off; g->size = cur; g->smaller = prev; }
+    }
+    bs <<= 1;
+  } while (off != 0);
+  g->steps = hd_log2(g->size);
+  g->rib = (uint32_t)rank % g->size;
+  size_t step_chunk = steps ? chunk << (steps - 1) : 0, base = 0;
+  for (uint32_t i = 0; i < g->steps; i++) { /* :113-157 */
+    const uint32_t bit = 1u << i, dest = (uint32_t)rank ^ bit;
+    g->send_off[i] = base + ((dest & bit) ? step_chunk : 0);
+    g->recv_off[i] = base + (((uint32_t)rank & bit) ? step_chunk : 0);
+    if (g->send_off[i] < n) g->send_cnt[i] = n - g->send_off[i] < step_chunk ? n - g->send_off[i] : step_chunk;
+    if (g->recv_off[i] < n) g->recv_cnt[i] = n - g->recv_off[i] < step_chunk ? n - g->recv_off[i] : step_chunk;
+    if ((uint32_t)rank & bit) base += step_chunk;
+    step_chunk >>= 1;
+  }
+  if (g->larger) g->sc_larger = step_chunk >> (hd_log2(g->larger / g->size) - 1);
+}
+
+int orc_allreduce_halving_doubling(int P, int nptr, int op, int dtype, size_t n, void** bufs) {
+  size_t es = orc_esize(dtype);
+  if (!es || P < 1 || nptr < 1) return 1;
+  for (int r = 0; r < P; r++) {
+    void* p0 = bufs[r * nptr];
+    for (int i = 1; i < nptr; i++) orc_op(op, dtype, p0, p0, bufs[r * nptr + i], n);
+  }
+  int rc = 0;
+  if (P > 1 && n > 0) {
+    hd_rank* g = (hd_rank*)calloc((size_t)P, sizeof(hd_rank));
+    unsigned char* snap = (unsigned char*)malloc((size_t)P * n * es);
+    if (!g || !snap) { free(g); free(snap); return 2; }
+#define B(r) ((unsigned char*)bufs[(r) * nptr])
+#define SNAP(r) (snap + (size_t)(r) * n * es)
+    uint32_t max_steps = 0;
+    for (int r = 0; r < P; r++) {
+      hd_geometry(P, r, n, &g[r]);
+      if (g[r].steps > max_steps) max_steps = g[r].steps;
+    }
+    /* 1. reduce-scatter inside every block */
+    for (uint32_t i = 0; i < max_steps; i++) {
+      for (int r = 0; r < P; r++) memcpy(SNAP(r), B(r), n * es);
+      for (int r = 0; r < P; r++) {
+        if (g[r].steps <= i || !g[r].recv_cnt[i]) continue;
+        const int q = r ^ (1 << i);
+        if (g[q].send_cnt[i] != g[r].recv_cnt[i]) { rc = 3; goto out; }
+        orc_op(op, dtype, B(r) + g[r].recv_off[i] * es, B(r) + g[r].recv_off[i] * es,
+               SNAP(q) + g[q].send_off[i] * es, g[r].recv_cnt[i]);
+      }
+    }
+    /* 2. up the chain of blocks, smallest first: fold the smaller block's scattered pieces.
+     * Blocks sit at decreasing rank offsets as they grow, so walk block offsets downwards. */
+    for (int r = P - 1; r >= 0; r = (int)g[r].off - 1) {
+      const uint32_t bo = g[r].off, bsz = g[r].size;
+      if (!g[r].smaller) continue;
+      for (uint32_t l = bo; l < bo + bsz; l++) {
+        const hd_rank* L = &g[l];
+        const size_t want = L->recv_cnt[L->steps - 1];
+        if (!want) continue;
+        const int s = (int)(bo + bsz + L->rib % L->smaller);
+        const hd_rank* S = &g[s];
+        const size_t total = S->steps ? S->recv_cnt[S->steps - 1] : n;
+        const size_t soff = S->steps ? S->recv_off[S->steps - 1] : 0;
+        const uint32_t k = L->size / S->size, ord = hd_rev(S->rib, S->steps) * k;
+        int found = 0;
+        for (uint32_t i = 0; i < k; i++) {
+          if (S->sc_larger * i >= total) break;
+          if (S->off - L->size + hd_rev(ord + i, L->steps) != l) continue;
+          const size_t len = total - S->sc_larger * i < S->sc_larger ? total - S->sc_larger * i
+                                                                      : S->sc_larger;
+          if (len != want) { rc = 4; goto out; }
+          unsigned char* dst = B(l) + L->recv_off[L->steps - 1] * es;
+          orc_op(op, dtype, dst, dst, B(s) + (soff + i * S->sc_larger) * es, want);
+          found = 1;
+        }
+        if (!found) { rc = 5; goto out; }
+      }
+    }
+    /* 3. down the chain, largest first: the smaller block copies the finished pieces. */
+    for (int r = 0; r < P; r += (int)g[r].size) {
+      if (!g[r].larger) continue;
+      const uint32_t bo = g[r].off, bsz = g[r].size;
+      for (uint32_t s = bo; s < bo + bsz; s++) {
+        const hd_rank* S = &g[s];
+        const size_t total = S->steps ? S->recv_cnt[S->steps - 1] : n;
+        const size_t soff = S->steps ? S->recv_off[S->steps - 1] : 0;
+        if (!total) continue;
+        const uint32_t k = S->larger / S->size, ord = hd_rev(S->rib, S->steps) * k;
+        for (uint32_t i = 0; i < k; i++) {
+          if (S->sc_larger * i >= total) break;
+          const int l = (int)(S->off - S->larger + hd_rev(ord + i, hd_log2(S->larger)));
+          const hd_rank* L = &g[l];
+          const size_t len = total - S->sc_larger * i < S->sc_larger ? total - S->sc_larger * i
+                                                                      : S->sc_larger;
+          if (L->off + L->size + L->rib % L->smaller != s || L->recv_cnt[L->steps - 1] != len) {
+            rc = 6;
+            goto out;
+          }
+          memcpy(B(s) + (soff + i * S->sc_larger) * es, B(l) + L->recv_off[L->steps - 1] * es,
+                 len * es);
+        }
+      }
+    }
+    /* 4. allgather inside every block, last step first */
+    for (int i = (int)max_steps - 1; i >= 0; i--) {
+      for (int r = 0; r < P; r++) memcpy(SNAP(r), B(r), n * es);
+      for (int r = 0; r < P; r++) {
+        if (g[r].steps <= (uint32_t)i || !g[r].send_cnt[i]) continue;
+        const int q = r ^ (1 << i);
+        memcpy(B(r) + g[r].send_off[i] * es, SNAP(q) + g[q].recv_off[i] * es, g[r].send_cnt[i] * es);
+      }
+    }
+  out:
+#undef B
+#undef SNAP
+    free(g);
+    free(snap);
+  }
+  if (!rc)
+    for (int r = 0; r < P; r++)
+      for (int i = 1; i < nptr; i++) memcpy(bufs[r * nptr + i], bufs[r * nptr], n * es);
+  return rc;
+}
+
 /* ReductionFunction<T>::Function-shaped (x = x op y) entry points for host-runtime tests. */
 void orc_isum_f32(void* x, const void* y, size_t n) { orc_op(OP_SUM, D_FLOAT32, x, x, y, n); }
 void orc_isum_i32(void* x, const void* y, size_t n) { orc_op(OP_SUM, D_INT32, x, x, y, n); }

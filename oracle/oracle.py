@@ -67,6 +67,7 @@ def orc():
         _orc.orc_allreduce_ring_old.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                 ctypes.c_int, _c, _vp]
         _orc.orc_allreduce_ring_chunked.argtypes = _orc.orc_allreduce_ring_old.argtypes
+        _orc.orc_allreduce_halving_doubling.argtypes = _orc.orc_allreduce_ring_old.argtypes
         _orc.orc_allreduce_bcube.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                              ctypes.c_int, _c, _vp, _vp]
         _orc.orc_reduce.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, _c, _vp, _vp,
@@ -98,6 +99,7 @@ def ref():
         _ref.ref_allreduce_ring_old.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, _c,
                                                 _vp, ctypes.c_char_p, _c]
         _ref.ref_allreduce_ring_chunked.argtypes = _ref.ref_allreduce_ring_old.argtypes
+        _ref.ref_allreduce_halving_doubling.argtypes = _ref.ref_allreduce_ring_old.argtypes
         _ref.ref_reduce.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, _c, _vp, _vp,
                                     ctypes.c_int, _c, ctypes.c_long, ctypes.c_char_p, _c]
         _ref.ref_reduce_timeout.argtypes = [ctypes.c_long, ctypes.c_char_p, _c]
@@ -195,8 +197,9 @@ def ring_result(xs: list[np.ndarray], max_segment: int = 1 << 20, kind: str = "s
     return outs[0][0]
 
 
-def _old_ring(fn_is_ref, bufs, kind, dtype_code, chunked=False):
-    """bufs: [rank][ptr] arrays, in place.  chunked: AllreduceRingChunked<T> instead."""
+def _old_ring(fn_is_ref, bufs, kind, dtype_code, chunked=False, hd=False):
+    """bufs: [rank][ptr] arrays, in place.  chunked: AllreduceRingChunked<T> instead;
+    hd: AllreduceHalvingDoubling<T> instead."""
     P, nptr = len(bufs), len(bufs[0])
     n = bufs[0][0].size
     code = _dt(bufs[0][0], dtype_code)
@@ -204,13 +207,16 @@ def _old_ring(fn_is_ref, bufs, kind, dtype_code, chunked=False):
     if fn_is_ref:
         err = ctypes.create_string_buffer(512)
         f = ref().ref_allreduce_ring_chunked if chunked else ref().ref_allreduce_ring_old
+        f = ref().ref_allreduce_halving_doubling if hd else f
         rc = f(P, nptr, code, n, ctypes.cast(ptrs, _vp), err, 512)
         if rc:
             raise RuntimeError(f"reference AllreduceRing failed: {err.value.decode()}")
     else:
         f = orc().orc_allreduce_ring_chunked if chunked else orc().orc_allreduce_ring_old
-        if f(P, nptr, OPS[kind], code, n, ctypes.cast(ptrs, _vp)):
-            raise RuntimeError("oracle AllreduceRing failed")
+        f = orc().orc_allreduce_halving_doubling if hd else f
+        rc = f(P, nptr, OPS[kind], code, n, ctypes.cast(ptrs, _vp))
+        if rc:
+            raise RuntimeError(f"oracle AllreduceRing failed (rc {rc})")
     return bufs
 
 
@@ -232,6 +238,17 @@ def allreduce_ring_chunked(bufs, kind="sum", dtype_code=None):
 def ref_allreduce_ring_chunked(bufs, dtype_code=None):
     """The reference's own AllreduceRingChunked<T> (ReductionFunction<T>::sum) on thread-ranks."""
     return _old_ring(True, bufs, "sum", dtype_code, chunked=True)
+
+
+def allreduce_halving_doubling(bufs, kind="sum", dtype_code=None):
+    """C restatement of gloo::AllreduceHalvingDoubling<T>::run() over len(bufs) ranks
+    (allreduce_halving_doubling.h:37-358)."""
+    return _old_ring(False, bufs, kind, dtype_code, hd=True)
+
+
+def ref_allreduce_halving_doubling(bufs, dtype_code=None):
+    """The reference's own AllreduceHalvingDoubling<T> (ReductionFunction<T>::sum)."""
+    return _old_ring(True, bufs, "sum", dtype_code, hd=True)
 
 
 def split_aa(P: int, n: int):

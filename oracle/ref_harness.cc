@@ -298,6 +298,32 @@ extern "C" int ref_allreduce_ring_chunked(int P, int nptr, int dtype, size_t n, 
   return 2;
 }
 
+// ---- AllreduceHalvingDoubling<T> (gloo/gloo/allreduce_halving_doubling.h:37-411) ----------
+#include "gloo/allreduce_halving_doubling.h"
+
+namespace {
+template <typename T>
+int run_halving_doubling(int P, int nptr, size_t n, void** bufs, char* err, size_t errlen) {
+  return spawn(P, [&](int r, std::shared_ptr<gloo::Context> ctx) {
+    std::vector<T*> ptrs;
+    for (int i = 0; i < nptr; i++) ptrs.push_back(static_cast<T*>(bufs[r * nptr + i]));
+    gloo::AllreduceHalvingDoubling<T> algo(ctx, ptrs, (int)n, gloo::ReductionFunction<T>::sum);
+    algo.run();
+  }, err, errlen);
+}
+}  // namespace
+
+extern "C" int ref_allreduce_halving_doubling(int P, int nptr, int dtype, size_t n, void** bufs,
+                                              char* err, size_t errlen) {
+  switch (dtype) {
+    case D_FLOAT32: return run_halving_doubling<float>(P, nptr, n, bufs, err, errlen);
+    case D_INT32: return run_halving_doubling<int32_t>(P, nptr, n, bufs, err, errlen);
+    case D_FLOAT16: return run_halving_doubling<gloo::float16>(P, nptr, n, bufs, err, errlen);
+    case D_FLOAT64: return run_halving_doubling<double>(P, nptr, n, bufs, err, errlen);
+  }
+  return 2;
+}
+
 // In place on bufs ([rank][ptr]), ReductionFunction<T>::sum; dtype: float32, int32, float16.
 extern "C" int ref_allreduce_ring_old(int P, int nptr, int dtype, size_t n, void** bufs,
                                       char* err, size_t errlen) {

@@ -31,6 +31,16 @@ def golden_meta():
 
 
 @pytest.fixture(scope="session")
+def golden_hd():
+    """AllreduceHalvingDoubling<T> fixtures (oracle/gen_golden.py --hd): inputs, result, meta."""
+    import json
+
+    with open(os.path.join(GOLDEN, "golden_hd.json")) as f:
+        meta = json.load(f)
+    return np.load(os.path.join(GOLDEN, "golden_hd.npz"), allow_pickle=False), meta
+
+
+@pytest.fixture(scope="session")
 def O():
     """The oracle (test infrastructure): C restatement + (when built) the reference itself."""
     from oracle import oracle
