@@ -40,10 +40,11 @@ EXPORTS = [  # every symbol include/hydra_hip.h declares
 ]
 
 (ALGO_AUTO, ALGO_RING, ALGO_DIRECT, ALGO_RCCL, ALGO_A2A, ALGO_RING_OLD, ALGO_RING_CHUNKED,
- ALGO_BCUBE) = range(8)
+ ALGO_BCUBE, ALGO_HALVING_DOUBLING) = range(9)
 ALGOS = {"auto": ALGO_AUTO, "ring": ALGO_RING, "direct": ALGO_DIRECT, "rccl": ALGO_RCCL,
          "a2a": ALGO_A2A, "ring_old": ALGO_RING_OLD,
-         "ring_chunked": ALGO_RING_CHUNKED, "bcube": ALGO_BCUBE}
+         "ring_chunked": ALGO_RING_CHUNKED, "bcube": ALGO_BCUBE,
+         "halving_doubling": ALGO_HALVING_DOUBLING}
 ACC_F32 = 1
 ERR_TIMEOUT = 5
 UNIQUE_ID_BYTES = 128

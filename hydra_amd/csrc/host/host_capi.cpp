@@ -76,8 +76,8 @@ int spawn(int P, int rails, char* err, size_t errlen,
 
 namespace {
 template <typename T>
-int old_ring(bool chunked, int P, int nptr, size_t n, void** bufs, int reducer, hydra_inplace_fn fn,
-             char* err, size_t errlen) {
+int old_ring(int kind, int P, int nptr, size_t n, void** bufs, int reducer, hydra_inplace_fn fn,
+             char* err, size_t errlen) {  // kind: 0 AllreduceRing, 1 chunked, 2 halving-doubling
   using RF = hydra::ReductionFunction<T>;
   const RF* rf = nullptr;
   std::unique_ptr<RF> custom;
@@ -94,7 +94,10 @@ int old_ring(bool chunked, int P, int nptr, size_t n, void** bufs, int reducer, 
   return spawn(P, 1, err, errlen, [&](int r, std::vector<std::shared_ptr<hydra::Context>>& c) {
     std::vector<T*> ptrs;
     for (int i = 0; i < nptr; i++) ptrs.push_back(static_cast<T*>(bufs[r * nptr + i]));
-    if (chunked) {
+    if (kind == 2) {
+      hydra::AllreduceHalvingDoubling<T> algo(c[0], ptrs, (int)n, rf);
+      algo.run();
+    } else if (kind == 1) {
       hydra::AllreduceRingChunked<T> algo(c[0], ptrs, (int)n, rf);
       algo.run();
     } else {
@@ -238,19 +241,19 @@ int hydra_host_bench(int config, int P, size_t n, int warmup, int iters, int red
   });
 }
 
-static int algorithm_ring(bool chunked, int P, int nptr, int dtype, size_t n, void** bufs,
+static int algorithm_ring(int kind, int P, int nptr, int dtype, size_t n, void** bufs,
                           int reducer, hydra_inplace_fn fn, char* err, size_t errlen) {
   if (P < 1 || nptr < 1 || !bufs || n > (size_t)INT32_MAX) {
     set_err(err, errlen, "invalid arguments");
     return 2;
   }
   switch (dtype) {
-    case HYDRA_FLOAT32: return old_ring<float>(chunked, P, nptr, n, bufs, reducer, fn, err, errlen);
-    case HYDRA_INT32: return old_ring<int32_t>(chunked, P, nptr, n, bufs, reducer, fn, err, errlen);
-    case HYDRA_FLOAT64: return old_ring<double>(chunked, P, nptr, n, bufs, reducer, fn, err, errlen);
+    case HYDRA_FLOAT32: return old_ring<float>(kind, P, nptr, n, bufs, reducer, fn, err, errlen);
+    case HYDRA_INT32: return old_ring<int32_t>(kind, P, nptr, n, bufs, reducer, fn, err, errlen);
+    case HYDRA_FLOAT64: return old_ring<double>(kind, P, nptr, n, bufs, reducer, fn, err, errlen);
     case HYDRA_FLOAT16:
       if (reducer != HYDRA_REDUCER_FN) break;
-      return old_ring<uint16_t>(chunked, P, nptr, n, bufs, reducer, fn, err, errlen);
+      return old_ring<uint16_t>(kind, P, nptr, n, bufs, reducer, fn, err, errlen);
   }
   set_err(err, errlen, "unsupported dtype for AllreduceRing");
   return 3;
@@ -259,13 +262,19 @@ static int algorithm_ring(bool chunked, int P, int nptr, int dtype, size_t n, vo
 int hydra_host_allreduce_ring_old_threads(int P, int nptr, int dtype, size_t n, void** bufs,
                                           int reducer, hydra_inplace_fn fn, char* err,
                                           size_t errlen) {
-  return algorithm_ring(false, P, nptr, dtype, n, bufs, reducer, fn, err, errlen);
+  return algorithm_ring(0, P, nptr, dtype, n, bufs, reducer, fn, err, errlen);
 }
 
 int hydra_host_allreduce_ring_chunked_threads(int P, int nptr, int dtype, size_t n, void** bufs,
                                               int reducer, hydra_inplace_fn fn, char* err,
                                               size_t errlen) {
-  return algorithm_ring(true, P, nptr, dtype, n, bufs, reducer, fn, err, errlen);
+  return algorithm_ring(1, P, nptr, dtype, n, bufs, reducer, fn, err, errlen);
+}
+
+int hydra_host_allreduce_halving_doubling_threads(int P, int nptr, int dtype, size_t n,
+                                                  void** bufs, int reducer, hydra_inplace_fn fn,
+                                                  char* err, size_t errlen) {
+  return algorithm_ring(2, P, nptr, dtype, n, bufs, reducer, fn, err, errlen);
 }
 
 int hydra_host_hip_ring_threads(int P, int nptr, int dtype, size_t n, void** dev_bufs,

@@ -73,13 +73,14 @@ int check_plan_args(int algo, int op, int dtype, int flags, size_t* esize) {
   *esize = hydra::dtype_size(dtype);
   if (!*esize) return fail(HYDRA_ERR_INVALID, "invalid dtype");
   if (op < HYDRA_SUM || op > HYDRA_MIN) return fail(HYDRA_ERR_INVALID, "invalid op");
-  if (algo < HYDRA_ALGO_AUTO || algo > HYDRA_ALGO_BCUBE)
+  if (algo < HYDRA_ALGO_AUTO || algo > HYDRA_ALGO_HALVING_DOUBLING)
     return fail(HYDRA_ERR_INVALID, "invalid algorithm");
   if (flags & HYDRA_ACC_F32) {
     if (dtype != HYDRA_BFLOAT16)
       return fail(HYDRA_ERR_UNSUPPORTED, "HYDRA_ACC_F32 needs a bf16 bucket");
     if (algo == HYDRA_ALGO_RING || algo == HYDRA_ALGO_RING_OLD ||
-        algo == HYDRA_ALGO_RING_CHUNKED || algo == HYDRA_ALGO_BCUBE)
+        algo == HYDRA_ALGO_RING_CHUNKED || algo == HYDRA_ALGO_BCUBE ||
+        algo == HYDRA_ALGO_HALVING_DOUBLING)
       return fail(HYDRA_ERR_UNSUPPORTED, "HYDRA_ACC_F32 runs on the DIRECT/A2A algorithms");
   }
   return HYDRA_OK;

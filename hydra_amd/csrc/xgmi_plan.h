@@ -30,6 +30,7 @@
 #include <vector>
 
 #include "bcube_geometry.h"
+#include "hydra/halving_doubling_geometry.h"
 
 namespace hydra {
 
@@ -45,8 +46,8 @@ enum PlanKind : int32_t {
 enum PlanBuf : int32_t { kBufUser = 0, kBufScratch = 1 };
 enum Algo : int32_t {
   kAlgoAuto = 0, kAlgoRing = 1, kAlgoDirect = 2, kAlgoRccl = 3, kAlgoA2A = 4, kAlgoRingOld = 5,
-  kAlgoRingChunked = 6, kAlgoBcube = 7,
-  kAlgoReduce = 8  // internal: gloo::reduce to PlanGeom::root (hydra_reduce_root), not an allreduce
+  kAlgoRingChunked = 6, kAlgoBcube = 7, kAlgoHalvingDoubling = 8,
+  kAlgoReduce = 64  // internal: gloo::reduce to PlanGeom::root (hydra_reduce_root), not an allreduce
 };
 
 // AllreduceRingChunked<T> geometry (allreduce_ring_chunked.h:32-36): 2P chunks of
@@ -177,6 +178,11 @@ inline size_t plan_scratch_bytes(int algo, const PlanGeom& g) {
   if (algo == kAlgoA2A) return g.total;
   if (algo == kAlgoRingOld) return 2 * round_up_sz(g.total, 16);
   if (algo == kAlgoRingChunked) return 2 * round_up_sz(chunked_ring_elems(g.P, g.n) * g.esize, 16);
+  if (algo == kAlgoHalvingDoubling) {  // the largest halving receive: step 0's half
+    const int steps = detail::HalvingDoublingGeometry::ilog2((uint64_t)g.P);
+    const size_t chunk = (g.n + (size_t(1) << steps) - 1) >> steps;
+    return round_up_sz((chunk << (steps - 1)) * g.esize, 16);
+  }
   if (algo == kAlgoBcube) {  // allreduce.cc:540-547: chunk lengths round up
     size_t e = g.n;
     for (const auto& s : bcube_steps(g.P, 0, g.n)) e = std::max(e, s.g * s.chunk);
@@ -512,7 +518,67 @@ inline std::vector<PlanOp> plan_reduce(const PlanGeom& g, int r) {
   return pb.ops;
 }
 
+// ---- HALVING_DOUBLING: gloo::AllreduceHalvingDoubling<T> (allreduce_halving_doubling.h) ----
+// One p2p group per step of the reference's schedule (shared geometry, halving_doubling_
+// geometry.h): recursive halving inside the binary block (send the other half out of the
+// bucket, receive the partner's half into scratch, REDUCE x = x op scratch), the smaller
+// block's piece folded into the kept chunk, the kept chunk scattered to the next larger block
+// and its finished pieces received back in place, the finished chunk forwarded to the smaller
+// block, then recursive doubling straight into the bucket.  Same operands in the same order as
+// the reference, so every rank ends with its bits.
+inline std::vector<PlanOp> plan_halving_doubling(const PlanGeom& g, int r) {
+  PlanBuilder pb;
+  if (g.P <= 1 || g.n == 0) return pb.ops;
+  const detail::HalvingDoublingGeometry h(g.P, r, g.n);
+  const int64_t es = (int64_t)g.esize;
+  int last = -1;  // last REDUCE: wrote the bucket, read scratch
+  for (size_t i = 0; i < h.steps.size(); i++) {
+    const auto& s = h.steps[i];
+    const int peer = r ^ (1 << i);
+    if (!s.send_cnt && !s.recv_cnt) continue;
+    if (s.send_cnt) pb.add(kOpSend, peer, kBufUser, (int64_t)s.send_off * es, (int64_t)s.send_cnt * es);
+    if (s.recv_cnt) pb.add(kOpRecv, peer, kBufScratch, 0, (int64_t)s.recv_cnt * es);
+    const int grp = pb.add(kOpGroup, -1, 0, 0, 0, 0, 0, 0, last);
+    if (s.recv_cnt)
+      last = pb.add(kOpReduce, -1, kBufUser, (int64_t)s.recv_off * es, (int64_t)s.recv_cnt * es, 0,
+                    0, 2, grp);
+  }
+  const int64_t kept_off = (int64_t)h.kept_off * es, kept = (int64_t)h.kept * es;
+  if (h.smaller && kept) {  // :263-269
+    pb.add(kOpRecv, h.smaller_peer(), kBufScratch, 0, kept);
+    const int grp = pb.add(kOpGroup, -1, 0, 0, 0, 0, 0, 0, last);
+    last = pb.add(kOpReduce, -1, kBufUser, kept_off, kept, 0, 0, 2, grp);
+  }
+  if (h.larger && kept) {  // :273-301
+    const int k = h.larger / h.block;
+    for (int i = 0; i < k; i++)
+      if (const size_t l = h.piece_len(i))
+        pb.add(kOpSend, h.larger_peer(i), kBufUser, kept_off + (int64_t)(h.piece_to_larger * i) * es,
+               (int64_t)l * es);
+    pb.add(kOpGroup, -1, 0, 0, 0, 0, 0, 0, last);
+    for (int i = 0; i < k; i++)
+      if (const size_t l = h.piece_len(i))
+        pb.add(kOpRecv, h.larger_peer(i), kBufUser, kept_off + (int64_t)(h.piece_to_larger * i) * es,
+               (int64_t)l * es);
+    pb.add(kOpGroup, -1, 0, 0, 0, 0, 0, 0, -1);
+  }
+  if (h.smaller && kept) {  // :306-313
+    pb.add(kOpSend, h.smaller_peer(), kBufUser, kept_off, kept);
+    pb.add(kOpGroup, -1, 0, 0, 0, 0, 0, 0, last);
+  }
+  for (size_t i = h.steps.size(); i-- > 0;) {  // :316-338
+    const auto& s = h.steps[i];
+    const int peer = r ^ (1 << i);
+    if (!s.send_cnt && !s.recv_cnt) continue;
+    if (s.recv_cnt) pb.add(kOpSend, peer, kBufUser, (int64_t)s.recv_off * es, (int64_t)s.recv_cnt * es);
+    if (s.send_cnt) pb.add(kOpRecv, peer, kBufUser, (int64_t)s.send_off * es, (int64_t)s.send_cnt * es);
+    pb.add(kOpGroup, -1, 0, 0, 0, 0, 0, 0, last);
+  }
+  return pb.ops;
+}
+
 inline std::vector<PlanOp> make_plan(int algo, const PlanGeom& g, int r) {
+  if (algo == kAlgoHalvingDoubling) return plan_halving_doubling(g, r);
   if (algo == kAlgoReduce) return plan_reduce(g, r);
   if (algo == kAlgoBcube) return plan_bcube(g, r);
   if (algo == kAlgoRingChunked) return plan_ring_chunked(g, r);

@@ -40,6 +40,8 @@ def lib():
         L.hydra_host_hip_ring_chunked_threads.argtypes = L.hydra_host_hip_ring_threads.argtypes
         L.hydra_host_allreduce_ring_chunked_threads.argtypes = \
             L.hydra_host_allreduce_ring_old_threads.argtypes
+        L.hydra_host_allreduce_halving_doubling_threads.argtypes = \
+            L.hydra_host_allreduce_ring_old_threads.argtypes
         L.hydra_host_reduce_threads.argtypes = [i, i, i, sz, vp, vp, i, sz, i, vp,
                                                 ctypes.c_long, ctypes.c_char_p, sz]
         L.hydra_host_reduce_timeout_probe.argtypes = [ctypes.c_long, ctypes.c_char_p, sz]
@@ -126,10 +128,11 @@ def apipe_threads(ins, outs, table=SPLIT_AA, reducer_fn=None, dtype_code=_lib.FL
     return outs
 
 
-def allreduce_ring_old_threads(bufs, dtype_code=None, reducer_fn=None, chunked=False):
+def allreduce_ring_old_threads(bufs, dtype_code=None, reducer_fn=None, chunked=False,
+                               halving_doubling=False):
     """Old-style AllreduceRing<T>::run() on len(bufs) thread-ranks; bufs: [rank][ptr], in place.
     reducer_fn: None -> GPU sum; else address of a void(T* x, const T* y, size_t n).
-    chunked: AllreduceRingChunked<T> instead."""
+    chunked: AllreduceRingChunked<T> instead; halving_doubling: AllreduceHalvingDoubling<T>."""
     P, nptr = len(bufs), len(bufs[0])
     n = bufs[0][0].size
     code = dtype_code if dtype_code is not None else _np_code(bufs[0][0].dtype)
@@ -137,12 +140,20 @@ def allreduce_ring_old_threads(bufs, dtype_code=None, reducer_fn=None, chunked=F
     err = ctypes.create_string_buffer(512)
     f = (lib().hydra_host_allreduce_ring_chunked_threads if chunked
          else lib().hydra_host_allreduce_ring_old_threads)
+    if halving_doubling:
+        f = lib().hydra_host_allreduce_halving_doubling_threads
     rc = f(
         P, nptr, code, n, ctypes.cast(_ptrs([b for r in bufs for b in r]), ctypes.c_void_p), red,
         fp, err, 512)
     if rc:
         raise _lib.HydraError(rc, err.value.decode())
     return bufs
+
+
+def allreduce_halving_doubling_threads(bufs, dtype_code=None, reducer_fn=None):
+    """hydra::AllreduceHalvingDoubling<T>::run() (allreduce_halving_doubling.h:37-358) on
+    len(bufs) thread-ranks over loopback TCP; same arguments as allreduce_ring_old_threads."""
+    return allreduce_ring_old_threads(bufs, dtype_code, reducer_fn, halving_doubling=True)
 
 
 def hip_ring_threads(tensors, workspace: str = "host", user_streams: bool = False,

@@ -601,8 +601,8 @@ def bench_allreduce(args, dev) -> dict:
         parity["apipe"] = ("bit-exact" if max_over_ranks(0.0 if ok else 1.0, dev) == 0.0
                            else "MISMATCH")
         k = max(5, args.steps // 4)
-        for a in ("ring", "direct", "a2a", "rccl", "ring_old", "ring_chunked", "bcube", "peer2",
-                  "peer1"):
+        for a in ("ring", "direct", "a2a", "rccl", "ring_old", "ring_chunked", "bcube",
+                  "halving_doubling", "peer2", "peer1"):
             if a == chosen:
                 continue
 

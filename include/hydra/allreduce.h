@@ -27,6 +27,8 @@
 #include <string>
 #include <vector>
 
+#include "halving_doubling_geometry.h"
+
 namespace hydra {
 
 class EnforceNotMet : public std::runtime_error {
@@ -338,6 +340,130 @@ class AllreduceRing {
   size_t bytes_;
   const ReductionFunction<T>* fn_;
   std::vector<char> boxes_[2];
+};
+
+// gloo::AllreduceHalvingDoubling<T> (allreduce_halving_doubling.h:37-358).  P splits into
+// binary blocks (largest at rank 0, :39-64).  Inside a block, step i exchanges with
+// rank ^ 2^i: recursive halving folds the kept half (x = x op received, :241-256), then
+// recursive doubling copies the other half back (:316-338).  Between blocks, a rank folds the
+// piece from its smaller-block partner (:263-269), scatters its chunk to the next larger block
+// in bit-reversed order (:273-287), copies the larger block's finished pieces back (:293-301),
+// and forwards its finished chunk to the smaller block (:306-313).  Receives land straight in
+// the bucket where the reference copies from its recvBuf_ (same bits); the notification
+// handshake is implicit in the FIFO transport, as for the rings above.
+
+template <typename T>
+class AllreduceHalvingDoubling {
+ public:
+  AllreduceHalvingDoubling(const std::shared_ptr<Context>& context, const std::vector<T*>& ptrs,
+                           int count, const ReductionFunction<T>* fn)
+      : ctx_(context), ptrs_(ptrs), count_(count), fn_(fn),
+        geo_(context->size, context->rank, count < 0 ? 0 : (size_t)count) {
+    if (!fn_) throw EnforceNotMet("AllreduceHalvingDoubling: null reduction function");
+    if (ptrs_.empty()) throw EnforceNotMet("AllreduceHalvingDoubling: no pointers");
+    if (count_ < 0) throw EnforceNotMet("AllreduceHalvingDoubling: negative count");
+    size_t box = geo_.smaller ? geo_.kept : 0;  // the fold of the smaller block's piece
+    for (const auto& s : geo_.steps) box = std::max(box, s.recv_cnt);
+    inbox_.resize(box);
+  }
+
+  void run() {
+    const size_t n = (size_t)count_, E = sizeof(T);
+    for (size_t i = 1; i < ptrs_.size(); i++) fn_->call(ptrs_[0], ptrs_[i], count_);
+    if (ctx_->size > 1 && n > 0) exchange(n, E);
+    for (size_t i = 1; i < ptrs_.size(); i++) std::memcpy(ptrs_[i], ptrs_[0], n * E);
+  }
+
+ private:
+  // Sends read the bucket asynchronously (the pair's writer thread), so every region a later
+  // receive writes is first released by waiting on the send that read it.  Each phase sends
+  // through its own view of the bucket, so one wait never blocks on an unrelated send.
+  void exchange(size_t n, size_t E) {
+    const auto tmo = ctx_->getTimeout();
+    const auto& g = geo_;
+    const int r = ctx_->rank;
+    T* x = ptrs_[0];
+    const size_t S = g.steps.size();
+    std::vector<std::unique_ptr<UnboundBuffer>> halve;  // one per step: its send is waited
+    std::vector<char> halve_sent(S, 0);                 // before doubling writes that region
+    for (size_t i = 0; i < S; i++) halve.push_back(ctx_->createUnboundBuffer(x, n * E));
+    auto up = ctx_->createUnboundBuffer(x, n * E);    // scatter to the larger block
+    auto down = ctx_->createUnboundBuffer(x, n * E);  // larger block's pieces, chunk to smaller
+    auto dbl = ctx_->createUnboundBuffer(x, n * E);   // recursive doubling
+    auto box = ctx_->createUnboundBuffer(inbox_.data(), inbox_.size() * E);
+    size_t up_sent = 0, down_sent = 0, dbl_sent = 0;
+    // 1. recursive halving inside the block
+    for (size_t i = 0; i < S; i++) {
+      const auto& s = g.steps[i];
+      const int peer = r ^ (1 << i);
+      if (s.send_cnt) {
+        halve[i]->send(peer, kSlot + i, s.send_off * E, s.send_cnt * E);
+        halve_sent[i] = 1;
+      }
+      if (s.recv_cnt) {
+        box->recv(peer, kSlot + i, 0, s.recv_cnt * E);
+        box->waitRecv(tmo);
+        fn_->call(x + s.recv_off, inbox_.data(), s.recv_cnt);
+      }
+    }
+    // 2. fold the smaller block's piece of my chunk
+    if (g.smaller && g.kept) {
+      box->recv(g.smaller_peer(), kSlotUp, 0, g.kept * E);
+      box->waitRecv(tmo);
+      fn_->call(x + g.kept_off, inbox_.data(), g.kept);
+    }
+    // 3. scatter my chunk to the larger block, then take the finished pieces back in place
+    if (g.larger && g.kept) {
+      const int k = g.larger / g.block;
+      for (int i = 0; i < k; i++)
+        if (const size_t l = g.piece_len(i)) {
+          up->send(g.larger_peer(i), kSlotUp, (g.kept_off + g.piece_to_larger * i) * E, l * E);
+          up_sent++;
+        }
+      for (; up_sent; up_sent--) up->waitSend(tmo);
+      int posted = 0;
+      for (int i = 0; i < k; i++)
+        if (const size_t l = g.piece_len(i)) {
+          down->recv(g.larger_peer(i), kSlotDown, (g.kept_off + g.piece_to_larger * i) * E,
+                     l * E);
+          posted++;
+        }
+      for (int i = 0; i < posted; i++) down->waitRecv(tmo);
+    }
+    // 4. my finished chunk to the smaller block
+    if (g.smaller && g.kept) {
+      down->send(g.smaller_peer(), kSlotDown, g.kept_off * E, g.kept * E);
+      down_sent++;
+    }
+    // 5. recursive doubling inside the block
+    for (size_t i = S; i-- > 0;) {
+      const auto& s = g.steps[i];
+      const int peer = r ^ (1 << i);
+      if (s.recv_cnt) {
+        dbl->send(peer, kSlotGather + i, s.recv_off * E, s.recv_cnt * E);
+        dbl_sent++;
+      }
+      if (s.send_cnt) {
+        if (halve_sent[i]) halve[i]->waitSend(tmo), halve_sent[i] = 0;
+        dbl->recv(peer, kSlotGather + i, s.send_off * E, s.send_cnt * E);
+        dbl->waitRecv(tmo);
+      }
+    }
+    for (size_t i = 0; i < S; i++)
+      if (halve_sent[i]) halve[i]->waitSend(tmo);
+    for (; down_sent; down_sent--) down->waitSend(tmo);
+    for (; dbl_sent; dbl_sent--) dbl->waitSend(tmo);
+  }
+
+  static constexpr uint64_t kSlot = uint64_t(0x12) << 56;
+  static constexpr uint64_t kSlotUp = kSlot + 0x40, kSlotDown = kSlot + 0x41;
+  static constexpr uint64_t kSlotGather = kSlot + 0x80;
+  std::shared_ptr<Context> ctx_;
+  std::vector<T*> ptrs_;
+  int count_;
+  const ReductionFunction<T>* fn_;
+  detail::HalvingDoublingGeometry geo_;
+  std::vector<T> inbox_;
 };
 
 // gloo::AllreduceRingChunked<T> (allreduce_ring_chunked.h:20-248): 2P chunks of

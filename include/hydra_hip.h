@@ -153,6 +153,10 @@ void hydra_ring_plan(int P, size_t n, size_t esize, size_t max_segment, size_t* 
  *   HYDRA_ALGO_BCUBE   gloo::allreduce BCUBE (allreduce.cc:423-700): hypercube reduce-scatter
  *                      over the factors of P, then the reverse all-gather; the reference's
  *                      BCUBE bits (max_segment, chunk_bytes unused)
+ *   HYDRA_ALGO_HALVING_DOUBLING  gloo::AllreduceHalvingDoubling<T>
+ *                      (allreduce_halving_doubling.h:37-358): recursive halving / doubling in
+ *                      binary blocks of P, bit-reversed exchange between blocks; identical
+ *                      bits on every rank (max_segment, chunk_bytes unused)
  *   HYDRA_ALGO_AUTO    DIRECT
  * max_segment: the reference's maxSegmentSize (0 = 1 MiB, allreduce.h:78) -- it fixes block
  * ownership; chunk_bytes: pipelining granularity (0 = 4 MiB), does not change results.
@@ -167,7 +171,8 @@ typedef enum {
   HYDRA_ALGO_A2A = 4,
   HYDRA_ALGO_RING_OLD = 5,
   HYDRA_ALGO_RING_CHUNKED = 6,
-  HYDRA_ALGO_BCUBE = 7
+  HYDRA_ALGO_BCUBE = 7,
+  HYDRA_ALGO_HALVING_DOUBLING = 8
 } hydra_algo_t;
 typedef struct hydra_comm* hydra_comm_t;
 

@@ -79,6 +79,12 @@ int hydra_host_allreduce_ring_chunked_threads(int P, int nptr, int dtype, size_t
                                               int reducer, hydra_inplace_fn fn, char* err,
                                               size_t errlen);
 
+/* gloo::AllreduceHalvingDoubling<T>::run() (allreduce_halving_doubling.h:37-358), same
+ * arguments as hydra_host_allreduce_ring_old_threads. */
+int hydra_host_allreduce_halving_doubling_threads(int P, int nptr, int dtype, size_t n,
+                                                  void** bufs, int reducer, hydra_inplace_fn fn,
+                                                  char* err, size_t errlen);
+
 /* gloo::reduce (reduce.cc:21-262) to `root` on P thread-ranks.  in/out: P pointers each
  * (in == NULL: in place on out, reduce_test.cc:27-33).  Every rank's out is left as the
  * reference's schedule leaves it; only the root's is the reduction. */

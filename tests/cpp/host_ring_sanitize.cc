@@ -96,9 +96,10 @@ static void isum_u64(uint64_t* x, const uint64_t* y, size_t n) {
   for (size_t i = 0; i < n; i++) x[i] += y[i];
 }
 
-// Old-style Algorithm API: AllreduceRing<T> / AllreduceRingChunked<T> (allreduce_ring.h,
-// allreduce_ring_chunked.h) with several pointers per rank.
-static int run_algorithm(int P, int nptr, int n, bool chunked) {
+// Old-style Algorithm API: AllreduceRing<T> / AllreduceRingChunked<T> /
+// AllreduceHalvingDoubling<T> (allreduce_ring.h, allreduce_ring_chunked.h,
+// allreduce_halving_doubling.h) with several pointers per rank.  kind: 0 ring, 1 chunked, 2 HD.
+static int run_algorithm(int P, int nptr, int n, int kind) {
   hydra::HashStore store;
   std::vector<std::thread> th;
   std::vector<int> bad(P, 0);
@@ -116,7 +117,10 @@ static int run_algorithm(int P, int nptr, int n, bool chunked) {
           ptrs.push_back(buf[i].data());
         }
         for (int it = 0; it < 2; it++) {  // the algorithm object is reusable across runs
-          if (chunked) {
+          if (kind == 2) {
+            hydra::AllreduceHalvingDoubling<uint64_t> a(c, ptrs, n, &fn);
+            a.run();
+          } else if (kind == 1) {
             hydra::AllreduceRingChunked<uint64_t> a(c, ptrs, n, &fn);
             a.run();
           } else {
@@ -219,13 +223,14 @@ int main() {
     std::fprintf(stderr, "FAIL declining scratch allocator\n");
     fails++;
   }
-  for (bool chunked : {false, true})
-    for (int P : {1, 2, 3, 5})
+  static const char* kNames[] = {"AllreduceRing", "AllreduceRingChunked",
+                                 "AllreduceHalvingDoubling"};
+  for (int kind : {0, 1, 2})
+    for (int P : {1, 2, 3, 5, 7})
       for (int nptr : {1, 2})
         for (int n : {1, 1000, 20011})
-          if (run_algorithm(P, nptr, n, chunked)) {
-            std::fprintf(stderr, "FAIL %s P=%d nptr=%d n=%d\n",
-                         chunked ? "AllreduceRingChunked" : "AllreduceRing", P, nptr, n);
+          if (run_algorithm(P, nptr, n, kind)) {
+            std::fprintf(stderr, "FAIL %s P=%d nptr=%d n=%d\n", kNames[kind], P, nptr, n);
             fails++;
           }
   std::printf("%s\n", fails ? "FAILED" : "OK");

@@ -113,9 +113,10 @@ def _worker(rank, world, port, algo, n, ms, ch, q):
         wall = ring.timed_steps(lambda: None, 3, 1, lambda: None, dist.barrier)
         assert wall >= 0
         xs = [synth.stress_f32(world, r, n) for r in range(world)]
-        if algo in ("ring_old", "ring_chunked"):  # allreduce_ring.h / allreduce_ring_chunked.h
+        if algo in ("ring_old", "ring_chunked", "halving_doubling"):  # the Algorithm classes
             olds = [[x.copy()] for x in xs]
-            (O.allreduce_ring_old if algo == "ring_old" else O.allreduce_ring_chunked)(olds)
+            {"ring_old": O.allreduce_ring_old, "ring_chunked": O.allreduce_ring_chunked,
+             "halving_doubling": O.allreduce_halving_doubling}[algo](olds)
             exp = olds[rank][0]
         elif algo == "bcube":
             exp = O.bcube_result(xs)
@@ -134,7 +135,7 @@ def _worker(rank, world, port, algo, n, ms, ch, q):
 
 @pytest.mark.parametrize("world", [2, 3])
 @pytest.mark.parametrize("algo", ["ring", "direct", "a2a", "ring_old", "ring_chunked",
-                                  "bcube", "reduce"])
+                                  "bcube", "reduce", "halving_doubling"])
 def test_gloo_multiprocess_plan(algo, world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

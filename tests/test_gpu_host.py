@@ -83,6 +83,24 @@ def test_chunked_allreduce_ring_gpu_reducer_vs_reference(gpu, golden, golden_met
                 assert np.array_equal(bufs[r][i].view(np.uint32), exp.view(np.uint32)), key
 
 
+def test_halving_doubling_gpu_reducer_vs_reference(gpu, golden_hd):
+    """hydra::AllreduceHalvingDoubling<T> with the GPU in-place sum (gpuReductionFunction) ==
+    the reference's own AllreduceHalvingDoubling<T> outputs (f32/i32), every rank and pointer,
+    P = 1..12 (one to three binary blocks)."""
+    golden, meta = golden_hd
+    for row in meta["halving_doubling"]:
+        if row["dtype"] not in (6, 2):
+            continue
+        key, P, k = row["key"], row["P"], row["nptr"]
+        ins = golden[key + "_in"]
+        bufs = [[ins[r, i].copy() for i in range(k)] for r in range(P)]
+        host.allreduce_halving_doubling_threads(bufs, dtype_code=row["dtype"])
+        exp = golden[key + "_out"]
+        for r in range(P):
+            for i in range(k):
+                assert np.array_equal(bufs[r][i].view(np.uint32), exp.view(np.uint32)), (key, r)
+
+
 def _tree(O, xs, code):
     """CudaLocalNativeReduce's pairwise tree in pointer order (cuda_collectives_native.h:93-122)."""
     xs = [x.copy() for x in xs]

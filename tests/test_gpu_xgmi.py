@@ -353,12 +353,48 @@ def test_simulated_bcube_vs_reference_fixtures(gpu, golden, golden_meta):
                 assert hashlib.sha256(got.tobytes()).hexdigest() == row["output_sha256"], key
 
 
+def test_simulated_halving_doubling_vs_reference_fixtures(gpu, golden_hd):
+    """Device HALVING_DOUBLING plan == the reference's own AllreduceHalvingDoubling<T> on every
+    rank (tests/golden/golden_hd: P = 1..12, one to three binary blocks, fp32 stress / int32 /
+    f16, single-pointer cases)."""
+    import torch
+
+    golden, meta = golden_hd
+    views = {6: np.uint32, 2: np.int32, 8: np.int16}
+    for row in meta["halving_doubling"]:
+        if row["nptr"] != 1:
+            continue
+        P, key, code = row["P"], row["key"], row["dtype"]
+        v = views[code]
+        ins = golden[key + "_in"]
+        bufs = [torch.from_numpy(ins[r, 0].view(v).copy()).to(gpu) for r in range(P)]
+        ring.simulate(bufs, algo="halving_doubling", dtype_code=code)
+        exp = golden[key + "_out"].view(v)
+        for r in range(P):
+            assert np.array_equal(bufs[r].cpu().numpy(), exp), (key, r)
+
+
+@pytest.mark.parametrize("P,n", [(8, 1 << 22), (6, 3000017), (7, 1 << 20)])
+def test_simulated_halving_doubling_large(gpu, O, P, n):
+    """Multi-MiB buckets through the simulator: bit-exact vs the oracle on every rank."""
+    import torch
+
+    xs = [synth.stress_f32(P, r, n) for r in range(P)]
+    bufs = [torch.from_numpy(x.copy()).to(gpu) for x in xs]
+    ring.simulate(bufs, algo="halving_doubling")
+    exp = [[x.copy()] for x in xs]
+    O.allreduce_halving_doubling(exp)
+    for r in range(P):
+        assert np.array_equal(bufs[r].cpu().numpy().view(np.uint32), exp[r][0].view(np.uint32)), r
+
+
 @pytest.mark.parametrize("algo,P,n,ch", [("ring", 2, 1 << 20, 1 << 18), ("ring", 4, 1 << 20, 0),
                                          ("direct", 4, 1 << 20, 1 << 18),
                                          ("direct", 8, 1 << 21, 1 << 19),
                                          ("ring_old", 3, 300000, 1 << 18),
                                          ("ring_chunked", 4, 1 << 20, 0),
                                          ("bcube", 8, 1 << 20, 0), ("bcube", 6, 6 << 12, 0),
+                                         ("halving_doubling", 8, 1 << 20, 0),
                                          ("a2a", 2, 1 << 20, 0), ("a2a", 8, 1 << 20, 0)])
 def test_rccl_executor_self_loop(gpu, O, algo, P, n, ch):
     """The real RCCL executor on one GPU: rank 0's plan with every peer remapped to itself runs

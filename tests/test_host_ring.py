@@ -298,3 +298,36 @@ def test_allreduce_test_single_pointer_p1_to_15(O, chunked):
             host.allreduce_ring_old_threads(bufs, dtype_code=6, reducer_fn=fn, chunked=chunked)
             for r in range(P):
                 assert np.all(bufs[r][0] == P * (P - 1) / 2), (P, n, r)
+
+
+def test_halving_doubling_vs_golden(O, golden_hd):
+    """hydra::AllreduceHalvingDoubling<T> (allreduce_halving_doubling.h:37-358) reproduces the
+    reference's result on every rank and pointer: one, two and three binary blocks (P = 1..12),
+    tiny and ragged n (oracle in-place sum as the reducer)."""
+    golden, meta = golden_hd
+    names = {6: "orc_isum_f32", 2: "orc_isum_i32", 8: "orc_isum_f16"}
+    for row in meta["halving_doubling"]:
+        key, P, k = row["key"], row["P"], row["nptr"]
+        ins = golden[key + "_in"]
+        bufs = [[ins[r, i].copy() for i in range(k)] for r in range(P)]
+        host.allreduce_halving_doubling_threads(bufs, dtype_code=row["dtype"],
+                                                reducer_fn=fnptr(O, names[row["dtype"]]))
+        exp = golden[key + "_out"]
+        for r in range(P):
+            for i in range(k):
+                got = bufs[r][i]
+                assert np.array_equal(got.view(f"u{got.itemsize}"),
+                                      exp.view(f"u{exp.itemsize}")), (key, r, i)
+
+
+@pytest.mark.parametrize("P,n", [(4, (1 << 20) + 7), (6, 300001), (7, 1 << 18), (13, 70001)])
+def test_halving_doubling_large(O, P, n):
+    """Messages far beyond the socket buffers (the FIFO transport must not deadlock) with
+    every cross-block leg active; bit-exact vs the oracle."""
+    xs = [synth.stress_f32(P, r, n) for r in range(P)]
+    bufs = [[x.copy()] for x in xs]
+    host.allreduce_halving_doubling_threads(bufs, reducer_fn=fnptr(O, "orc_isum_f32"))
+    exp = [[x.copy()] for x in xs]
+    O.allreduce_halving_doubling(exp)
+    for r in range(P):
+        assert np.array_equal(bufs[r][0].view(np.uint32), exp[r][0].view(np.uint32)), r

@@ -328,3 +328,18 @@ def test_bench_reduce_self_check_helper(O):
         O.reduce(exp, None, P - 1)
         assert np.array_equal(ring.expected_reduce_f32(xs).view(np.uint32),
                               exp[P - 1].view(np.uint32)), (P, n)
+
+
+@pytest.mark.parametrize("P,n", [(2, 1), (2, 1000), (3, 7), (4, 4099), (5, 100), (6, 100003),
+                                 (7, 262145), (8, 30011), (11, 5000), (12, 3), (13, 20011)])
+def test_halving_doubling_plan(O, P, n):
+    """AllreduceHalvingDoubling<T> on device (plan HALVING_DOUBLING): bit-exact vs the oracle's
+    restatement (pinned to the reference by tests/test_oracle.py) on every rank, one to three
+    binary blocks and fewer elements than chunks, and race-free."""
+    xs = [synth.stress_f32(P, r, n) for r in range(P)]
+    outs = run_plan_numpy(O, "halving_doubling", xs, 0, 0)
+    exp = [[x.copy()] for x in xs]
+    O.allreduce_halving_doubling(exp)
+    for r in range(P):
+        assert np.array_equal(outs[r].view(np.uint32), exp[r][0].view(np.uint32)), r
+        race_check(ring.plan("halving_doubling", P, r, n, 4, 0, 0)[0])
