@@ -108,7 +108,8 @@ int old_ring(int kind, int P, int nptr, size_t n, void** bufs, int reducer, hydr
 }
 template <typename T>
 int hip_ring(int P, int nptr, size_t n, void** bufs, int workspace, int user_streams, char* err,
-             size_t errlen, bool chunked = false) {
+             size_t errlen, int kind = 0) {  // kind: 0 ring, 1 chunked, 2 halving-doubling
+  const bool chunked = kind == 1;
   return spawn(P, 1, err, errlen, [&](int r, std::vector<std::shared_ptr<hydra::Context>>& c) {
     std::vector<T*> ptrs;
     for (int i = 0; i < nptr; i++) ptrs.push_back(static_cast<T*>(bufs[r * nptr + i]));
@@ -119,7 +120,15 @@ int hip_ring(int P, int nptr, size_t n, void** bufs, int workspace, int user_str
       streams.resize(nptr);
       for (auto& s : streams) hydra::gloo_compat::enforce(hydra_stream_create(dev, &s));
     }
-    if (chunked && workspace == HYDRA_WORKSPACE_DEVICE) {
+    if (kind == 2 && workspace == HYDRA_WORKSPACE_DEVICE) {
+      hydra::HipAllreduceHalvingDoubling<T, hydra::HipDeviceWorkspace<T>> algo(c[0], ptrs, (int)n,
+                                                                               streams);
+      algo.run();
+    } else if (kind == 2) {
+      hydra::HipAllreduceHalvingDoubling<T, hydra::HipHostWorkspace<T>> algo(c[0], ptrs, (int)n,
+                                                                             streams);
+      algo.run();
+    } else if (chunked && workspace == HYDRA_WORKSPACE_DEVICE) {
       hydra::HipAllreduceRingChunked<T, hydra::HipDeviceWorkspace<T>> algo(c[0], ptrs, (int)n,
                                                                            streams);
       algo.run();
@@ -302,15 +311,36 @@ int hydra_host_hip_ring_chunked_threads(int P, int nptr, int dtype, size_t n, vo
   }
   switch (dtype) {
     case HYDRA_FLOAT32:
-      return hip_ring<float>(P, nptr, n, dev_bufs, workspace, user_streams, err, errlen, true);
+      return hip_ring<float>(P, nptr, n, dev_bufs, workspace, user_streams, err, errlen, 1);
     case HYDRA_INT32:
-      return hip_ring<int32_t>(P, nptr, n, dev_bufs, workspace, user_streams, err, errlen, true);
+      return hip_ring<int32_t>(P, nptr, n, dev_bufs, workspace, user_streams, err, errlen, 1);
     case HYDRA_FLOAT64:
-      return hip_ring<double>(P, nptr, n, dev_bufs, workspace, user_streams, err, errlen, true);
+      return hip_ring<double>(P, nptr, n, dev_bufs, workspace, user_streams, err, errlen, 1);
     case HYDRA_INT64:
-      return hip_ring<int64_t>(P, nptr, n, dev_bufs, workspace, user_streams, err, errlen, true);
+      return hip_ring<int64_t>(P, nptr, n, dev_bufs, workspace, user_streams, err, errlen, 1);
   }
   set_err(err, errlen, "unsupported dtype for HipAllreduceRingChunked");
+  return 3;
+}
+
+int hydra_host_hip_halving_doubling_threads(int P, int nptr, int dtype, size_t n, void** dev_bufs,
+                                        int workspace, int user_streams, char* err,
+                                        size_t errlen) {
+  if (P < 1 || nptr < 1 || !dev_bufs || n > (size_t)INT32_MAX) {
+    set_err(err, errlen, "invalid arguments");
+    return 2;
+  }
+  switch (dtype) {
+    case HYDRA_FLOAT32:
+      return hip_ring<float>(P, nptr, n, dev_bufs, workspace, user_streams, err, errlen, 2);
+    case HYDRA_INT32:
+      return hip_ring<int32_t>(P, nptr, n, dev_bufs, workspace, user_streams, err, errlen, 2);
+    case HYDRA_FLOAT64:
+      return hip_ring<double>(P, nptr, n, dev_bufs, workspace, user_streams, err, errlen, 2);
+    case HYDRA_INT64:
+      return hip_ring<int64_t>(P, nptr, n, dev_bufs, workspace, user_streams, err, errlen, 2);
+  }
+  set_err(err, errlen, "unsupported dtype for HipAllreduceHalvingDoubling");
   return 3;
 }
 

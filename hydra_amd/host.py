@@ -38,6 +38,8 @@ def lib():
                                                             ctypes.c_char_p, sz]
         L.hydra_host_hip_ring_threads.argtypes = [i, i, i, sz, vp, i, i, ctypes.c_char_p, sz]
         L.hydra_host_hip_ring_chunked_threads.argtypes = L.hydra_host_hip_ring_threads.argtypes
+        L.hydra_host_hip_halving_doubling_threads.argtypes = \
+            L.hydra_host_hip_ring_threads.argtypes
         L.hydra_host_allreduce_ring_chunked_threads.argtypes = \
             L.hydra_host_allreduce_ring_old_threads.argtypes
         L.hydra_host_allreduce_halving_doubling_threads.argtypes = \
@@ -157,10 +159,11 @@ def allreduce_halving_doubling_threads(bufs, dtype_code=None, reducer_fn=None):
 
 
 def hip_ring_threads(tensors, workspace: str = "host", user_streams: bool = False,
-                     dtype_code=None, chunked: bool = False):
+                     dtype_code=None, chunked: bool = False, halving_doubling: bool = False):
     """hydra::HipAllreduceRing<T, W>::run() (gloo::CudaAllreduceRing) on len(tensors)
     thread-ranks; tensors: [rank][ptr] contiguous device tensors, reduced in place.
-    chunked: HipAllreduceRingChunked<T, W> (gloo::CudaAllreduceRingChunked) instead."""
+    chunked: HipAllreduceRingChunked<T, W> (gloo::CudaAllreduceRingChunked) instead;
+    halving_doubling: HipAllreduceHalvingDoubling<T, W> (gloo::CudaAllreduceHalvingDoubling)."""
     from .reduce import _torch_dtype_code
 
     P, nptr = len(tensors), len(tensors[0])
@@ -174,6 +177,8 @@ def hip_ring_threads(tensors, workspace: str = "host", user_streams: bool = Fals
     err = ctypes.create_string_buffer(512)
     fn = (lib().hydra_host_hip_ring_chunked_threads if chunked
           else lib().hydra_host_hip_ring_threads)
+    if halving_doubling:
+        fn = lib().hydra_host_hip_halving_doubling_threads
     rc = fn(
         P, nptr, code, n, ctypes.cast(_ptrs_int([t.data_ptr() for r in tensors for t in r]),
                                       ctypes.c_void_p), ws, int(user_streams), err, 512)

@@ -352,6 +352,96 @@ class AllreduceRing {
 // the bucket where the reference copies from its recvBuf_ (same bits); the notification
 // handshake is implicit in the FIFO transport, as for the rings above.
 
+namespace detail {
+// AllreduceHalvingDoubling's schedule (allreduce_halving_doubling.h:224-358) over `count`
+// elements of `es` bytes at `base` (host memory the transport sends from), for this rank's
+// geometry `g`.  fold(dst, box, n) applies dst op= box for n elements; `inbox` holds
+// g.inbox_elems() elements.  Shared by AllreduceHalvingDoubling<T> and
+// HipAllreduceHalvingDoubling<T, W> (cuda_allreduce_halving_doubling.cc), which differ only in
+// where the fold runs.
+//
+// Sends read the bucket asynchronously (the pair's writer thread), so every region a later
+// receive writes is first released by waiting on the send that read it.  Each phase sends
+// through its own view of the bucket, so one wait never blocks on an unrelated send.
+template <typename Fold>
+void halving_doubling(Context& ctx, const HalvingDoublingGeometry& g, char* base, size_t count,
+                      size_t es, char* inbox, uint64_t slot, Fold fold) {
+  const auto tmo = ctx.getTimeout();
+  const int r = ctx.rank;
+  const size_t E = es, n = count;
+  const uint64_t slot_up = slot + 0x40, slot_down = slot + 0x41, slot_gather = slot + 0x80;
+  const size_t S = g.steps.size();
+  std::vector<std::unique_ptr<UnboundBuffer>> halve;  // one per step: its send is waited
+  std::vector<char> halve_sent(S, 0);                 // before doubling writes that region
+  for (size_t i = 0; i < S; i++) halve.push_back(ctx.createUnboundBuffer(base, n * E));
+  auto up = ctx.createUnboundBuffer(base, n * E);    // scatter to the larger block
+  auto down = ctx.createUnboundBuffer(base, n * E);  // larger block's pieces, chunk to smaller
+  auto dbl = ctx.createUnboundBuffer(base, n * E);   // recursive doubling
+  auto box = ctx.createUnboundBuffer(inbox, g.inbox_elems() * E);
+  size_t up_sent = 0, down_sent = 0, dbl_sent = 0;
+  // 1. recursive halving inside the block
+  for (size_t i = 0; i < S; i++) {
+    const auto& s = g.steps[i];
+    const int peer = r ^ (1 << i);
+    if (s.send_cnt) {
+      halve[i]->send(peer, slot + i, s.send_off * E, s.send_cnt * E);
+      halve_sent[i] = 1;
+    }
+    if (s.recv_cnt) {
+      box->recv(peer, slot + i, 0, s.recv_cnt * E);
+      box->waitRecv(tmo);
+      fold(base + s.recv_off * E, inbox, s.recv_cnt);
+    }
+  }
+  // 2. fold the smaller block's piece of my chunk
+  if (g.smaller && g.kept) {
+    box->recv(g.smaller_peer(), slot_up, 0, g.kept * E);
+    box->waitRecv(tmo);
+    fold(base + g.kept_off * E, inbox, g.kept);
+  }
+  // 3. scatter my chunk to the larger block, then take the finished pieces back in place
+  if (g.larger && g.kept) {
+    const int k = g.larger / g.block;
+    for (int i = 0; i < k; i++)
+      if (const size_t l = g.piece_len(i)) {
+        up->send(g.larger_peer(i), slot_up, (g.kept_off + g.piece_to_larger * i) * E, l * E);
+        up_sent++;
+      }
+    for (; up_sent; up_sent--) up->waitSend(tmo);
+    int posted = 0;
+    for (int i = 0; i < k; i++)
+      if (const size_t l = g.piece_len(i)) {
+        down->recv(g.larger_peer(i), slot_down, (g.kept_off + g.piece_to_larger * i) * E, l * E);
+        posted++;
+      }
+    for (int i = 0; i < posted; i++) down->waitRecv(tmo);
+  }
+  // 4. my finished chunk to the smaller block
+  if (g.smaller && g.kept) {
+    down->send(g.smaller_peer(), slot_down, g.kept_off * E, g.kept * E);
+    down_sent++;
+  }
+  // 5. recursive doubling inside the block
+  for (size_t i = S; i-- > 0;) {
+    const auto& s = g.steps[i];
+    const int peer = r ^ (1 << i);
+    if (s.recv_cnt) {
+      dbl->send(peer, slot_gather + i, s.recv_off * E, s.recv_cnt * E);
+      dbl_sent++;
+    }
+    if (s.send_cnt) {
+      if (halve_sent[i]) halve[i]->waitSend(tmo), halve_sent[i] = 0;
+      dbl->recv(peer, slot_gather + i, s.send_off * E, s.send_cnt * E);
+      dbl->waitRecv(tmo);
+    }
+  }
+  for (size_t i = 0; i < S; i++)
+    if (halve_sent[i]) halve[i]->waitSend(tmo);
+  for (; down_sent; down_sent--) down->waitSend(tmo);
+  for (; dbl_sent; dbl_sent--) dbl->waitSend(tmo);
+}
+}  // namespace detail
+
 template <typename T>
 class AllreduceHalvingDoubling {
  public:
@@ -362,102 +452,24 @@ class AllreduceHalvingDoubling {
     if (!fn_) throw EnforceNotMet("AllreduceHalvingDoubling: null reduction function");
     if (ptrs_.empty()) throw EnforceNotMet("AllreduceHalvingDoubling: no pointers");
     if (count_ < 0) throw EnforceNotMet("AllreduceHalvingDoubling: negative count");
-    size_t box = geo_.smaller ? geo_.kept : 0;  // the fold of the smaller block's piece
-    for (const auto& s : geo_.steps) box = std::max(box, s.recv_cnt);
-    inbox_.resize(box);
+    inbox_.resize(geo_.inbox_elems());
   }
 
   void run() {
     const size_t n = (size_t)count_, E = sizeof(T);
     for (size_t i = 1; i < ptrs_.size(); i++) fn_->call(ptrs_[0], ptrs_[i], count_);
-    if (ctx_->size > 1 && n > 0) exchange(n, E);
+    if (ctx_->size > 1 && n > 0)
+      detail::halving_doubling(*ctx_, geo_, reinterpret_cast<char*>(ptrs_[0]), n, E,
+                               reinterpret_cast<char*>(inbox_.data()), kSlot,
+                               [this](char* dst, const char* box, size_t l) {
+                                 fn_->call(reinterpret_cast<T*>(dst),
+                                           reinterpret_cast<const T*>(box), l);
+                               });
     for (size_t i = 1; i < ptrs_.size(); i++) std::memcpy(ptrs_[i], ptrs_[0], n * E);
   }
 
  private:
-  // Sends read the bucket asynchronously (the pair's writer thread), so every region a later
-  // receive writes is first released by waiting on the send that read it.  Each phase sends
-  // through its own view of the bucket, so one wait never blocks on an unrelated send.
-  void exchange(size_t n, size_t E) {
-    const auto tmo = ctx_->getTimeout();
-    const auto& g = geo_;
-    const int r = ctx_->rank;
-    T* x = ptrs_[0];
-    const size_t S = g.steps.size();
-    std::vector<std::unique_ptr<UnboundBuffer>> halve;  // one per step: its send is waited
-    std::vector<char> halve_sent(S, 0);                 // before doubling writes that region
-    for (size_t i = 0; i < S; i++) halve.push_back(ctx_->createUnboundBuffer(x, n * E));
-    auto up = ctx_->createUnboundBuffer(x, n * E);    // scatter to the larger block
-    auto down = ctx_->createUnboundBuffer(x, n * E);  // larger block's pieces, chunk to smaller
-    auto dbl = ctx_->createUnboundBuffer(x, n * E);   // recursive doubling
-    auto box = ctx_->createUnboundBuffer(inbox_.data(), inbox_.size() * E);
-    size_t up_sent = 0, down_sent = 0, dbl_sent = 0;
-    // 1. recursive halving inside the block
-    for (size_t i = 0; i < S; i++) {
-      const auto& s = g.steps[i];
-      const int peer = r ^ (1 << i);
-      if (s.send_cnt) {
-        halve[i]->send(peer, kSlot + i, s.send_off * E, s.send_cnt * E);
-        halve_sent[i] = 1;
-      }
-      if (s.recv_cnt) {
-        box->recv(peer, kSlot + i, 0, s.recv_cnt * E);
-        box->waitRecv(tmo);
-        fn_->call(x + s.recv_off, inbox_.data(), s.recv_cnt);
-      }
-    }
-    // 2. fold the smaller block's piece of my chunk
-    if (g.smaller && g.kept) {
-      box->recv(g.smaller_peer(), kSlotUp, 0, g.kept * E);
-      box->waitRecv(tmo);
-      fn_->call(x + g.kept_off, inbox_.data(), g.kept);
-    }
-    // 3. scatter my chunk to the larger block, then take the finished pieces back in place
-    if (g.larger && g.kept) {
-      const int k = g.larger / g.block;
-      for (int i = 0; i < k; i++)
-        if (const size_t l = g.piece_len(i)) {
-          up->send(g.larger_peer(i), kSlotUp, (g.kept_off + g.piece_to_larger * i) * E, l * E);
-          up_sent++;
-        }
-      for (; up_sent; up_sent--) up->waitSend(tmo);
-      int posted = 0;
-      for (int i = 0; i < k; i++)
-        if (const size_t l = g.piece_len(i)) {
-          down->recv(g.larger_peer(i), kSlotDown, (g.kept_off + g.piece_to_larger * i) * E,
-                     l * E);
-          posted++;
-        }
-      for (int i = 0; i < posted; i++) down->waitRecv(tmo);
-    }
-    // 4. my finished chunk to the smaller block
-    if (g.smaller && g.kept) {
-      down->send(g.smaller_peer(), kSlotDown, g.kept_off * E, g.kept * E);
-      down_sent++;
-    }
-    // 5. recursive doubling inside the block
-    for (size_t i = S; i-- > 0;) {
-      const auto& s = g.steps[i];
-      const int peer = r ^ (1 << i);
-      if (s.recv_cnt) {
-        dbl->send(peer, kSlotGather + i, s.recv_off * E, s.recv_cnt * E);
-        dbl_sent++;
-      }
-      if (s.send_cnt) {
-        if (halve_sent[i]) halve[i]->waitSend(tmo), halve_sent[i] = 0;
-        dbl->recv(peer, kSlotGather + i, s.send_off * E, s.send_cnt * E);
-        dbl->waitRecv(tmo);
-      }
-    }
-    for (size_t i = 0; i < S; i++)
-      if (halve_sent[i]) halve[i]->waitSend(tmo);
-    for (; down_sent; down_sent--) down->waitSend(tmo);
-    for (; dbl_sent; dbl_sent--) dbl->waitSend(tmo);
-  }
-
   static constexpr uint64_t kSlot = uint64_t(0x12) << 56;
-  static constexpr uint64_t kSlotUp = kSlot + 0x40, kSlotDown = kSlot + 0x41;
-  static constexpr uint64_t kSlotGather = kSlot + 0x80;
   std::shared_ptr<Context> ctx_;
   std::vector<T*> ptrs_;
   int count_;

@@ -67,6 +67,12 @@ struct HalvingDoublingGeometry {
     return at < kept ? std::min(piece_to_larger, kept - at) : 0;
   }
   int smaller_peer() const { return block_off + block + rank_in_block % smaller; }
+  // Receive box for the halving steps and the smaller block's piece (elements).
+  size_t inbox_elems() const {
+    size_t m = smaller ? kept : 0;
+    for (const auto& s : steps) m = std::max(m, s.recv_cnt);
+    return m;
+  }
 };
 
 }  // namespace detail

@@ -331,4 +331,116 @@ class HipAllreduceRingChunked {
   std::unique_ptr<gloo_compat::ContextPool::Lease> lease_;
 };
 
+// hydra::HipAllreduceHalvingDoubling<T, W> -- the analog of gloo::CudaAllreduceHalvingDoubling
+// <T, W> (gloo/gloo/cuda_allreduce_halving_doubling.cc:246-408, non-pipelined): the pairwise-tree
+// local reduce on the device, then AllreduceHalvingDoubling's schedule
+// (detail::halving_doubling, shared with the host class) on a pinned host copy of the bucket,
+// every fold (scratch op= received, :282-285, :299-302) on the gfx950 kernel -- zero-copy on
+// the pinned box (host workspace) or on the device copy after an H2D of the box (device
+// workspace).  Received finished pieces are copies (:340-341, :370-373).  Every pointer ends
+// with the pinned copy's bits, identical on every rank.
+template <typename T, typename W>
+class HipAllreduceHalvingDoubling {
+  static constexpr bool kDeviceWorkspace = std::is_same<W, HipDeviceWorkspace<T>>::value;
+  static_assert(kDeviceWorkspace || std::is_same<W, HipHostWorkspace<T>>::value,
+                "W must be HipHostWorkspace<T> or HipDeviceWorkspace<T>");
+
+ public:
+  HipAllreduceHalvingDoubling(const std::shared_ptr<Context>& context,
+                              const std::vector<T*>& ptrs, int count,
+                              const std::vector<hydra_stream_t>& streams =
+                                  std::vector<hydra_stream_t>())
+      : ctx_(context), ptrs_(ptrs), count_(count), bytes_((size_t)count * sizeof(T)),
+        synchronize_outputs_(streams.empty()),
+        geo_(context->size, context->rank, count < 0 ? 0 : (size_t)count) {
+    using detail::enforce;
+    if (ptrs_.empty()) throw EnforceNotMet("HipAllreduceHalvingDoubling: no pointers");
+    if (count_ < 0) throw EnforceNotMet("HipAllreduceHalvingDoubling: negative count");
+    if (!streams.empty() && streams.size() != ptrs_.size())
+      throw EnforceNotMet("HipAllreduceHalvingDoubling: streams.size() != ptrs.size()");
+    if (count_ == 0) return;
+    enforce(hydra_pointer_device(ptrs_[0], &device_));
+    if (device_ < 0)
+      throw EnforceNotMet("HipAllreduceHalvingDoubling: ptrs must be device memory");
+    for (T* p : ptrs_) {
+      int d = -1;
+      enforce(hydra_pointer_device(p, &d));
+      if (d != device_)
+        throw EnforceNotMet("HipAllreduceHalvingDoubling: all pointers must be on one device");
+    }
+    if (streams.empty()) {
+      owned_.resize(ptrs_.size());
+      for (auto& s : owned_) enforce(hydra_stream_create(device_, &s));
+      streams_ = owned_;
+    } else {
+      streams_ = streams;
+    }
+    scratch_host_ = detail::Pinned(bytes_);
+    const size_t box = std::max<size_t>(geo_.inbox_elems(), 1) * sizeof(T);
+    inbox_ = detail::Pinned(box);
+    if (kDeviceWorkspace) inbox_dev_ = detail::DeviceMem(device_, box);
+  }
+
+  ~HipAllreduceHalvingDoubling() {
+    for (auto s : owned_) hydra_stream_destroy(s);
+  }
+  HipAllreduceHalvingDoubling(const HipAllreduceHalvingDoubling&) = delete;
+  HipAllreduceHalvingDoubling& operator=(const HipAllreduceHalvingDoubling&) = delete;
+
+  void run() {
+    using detail::enforce;
+    if (count_ == 0) return;
+    const int dt = gloo_compat::dtype_of<T>();
+    hydra_stream_t s0 = streams_[0];
+    for (size_t i = 1; i < streams_.size(); i++) enforce(hydra_stream_synchronize(streams_[i]));
+    for (size_t sz = 1; sz < ptrs_.size(); sz *= 2)  // CudaLocalNativeReduce tree, in place
+      for (size_t j = 0; j + sz < ptrs_.size(); j += 2 * sz)
+        enforce(hydra_reduce(HYDRA_SUM, dt, ptrs_[j], ptrs_[j], ptrs_[j + sz], count_, s0));
+    char* const dscratch = reinterpret_cast<char*>(ptrs_[0]);
+    char* const hscratch = static_cast<char*>(scratch_host_.p);
+    enforce(hydra_memcpy_async(hscratch, dscratch, bytes_, s0));
+    enforce(hydra_stream_synchronize(s0));
+    if (ctx_->size > 1) {
+      if (!kDeviceWorkspace)
+        lease_.reset(new gloo_compat::ContextPool::Lease(
+            gloo_compat::ContextPool::instance(device_).acquire()));
+      // Folds only ever touch regions no copy has written yet, so the device copy is current
+      // wherever the device workspace folds.
+      auto fold = [&](char* dst, const char* box, size_t n) {
+        if (!kDeviceWorkspace) {
+          enforce(hydra_reduce_host(lease_->get(), HYDRA_SUM, dt, dst, dst, box, n));
+          return;
+        }
+        char* dev = dscratch + (dst - hscratch);
+        enforce(hydra_memcpy_async(inbox_dev_.p, box, n * sizeof(T), s0));
+        enforce(hydra_reduce(HYDRA_SUM, dt, dev, dev, inbox_dev_.p, n, s0));
+        enforce(hydra_memcpy_async(dst, dev, n * sizeof(T), s0));  // what later sends read
+        enforce(hydra_stream_synchronize(s0));
+      };
+      detail::halving_doubling(*ctx_, geo_, hscratch, (size_t)count_, sizeof(T),
+                               static_cast<char*>(inbox_.p), kSlot, fold);
+      lease_.reset();
+    }
+    // broadcast (localBroadcastOp_): every pointer gets the pinned copy's result
+    for (size_t i = 0; i < ptrs_.size(); i++)
+      enforce(hydra_memcpy_async(ptrs_[i], hscratch, bytes_, streams_[i]));
+    if (synchronize_outputs_)
+      for (auto s : streams_) enforce(hydra_stream_synchronize(s));
+  }
+
+ private:
+  static constexpr uint64_t kSlot = uint64_t(0x15) << 56;
+  std::shared_ptr<Context> ctx_;
+  std::vector<T*> ptrs_;
+  int count_;
+  size_t bytes_;
+  bool synchronize_outputs_;
+  detail::HalvingDoublingGeometry geo_;
+  int device_ = -1;
+  std::vector<hydra_stream_t> streams_, owned_;
+  detail::Pinned scratch_host_, inbox_;
+  detail::DeviceMem inbox_dev_;
+  std::unique_ptr<gloo_compat::ContextPool::Lease> lease_;
+};
+
 }  // namespace hydra

@@ -74,6 +74,12 @@ int hydra_host_hip_ring_chunked_threads(int P, int nptr, int dtype, size_t n, vo
                                         int workspace, int user_streams, char* err,
                                         size_t errlen);
 
+/* hydra::HipAllreduceHalvingDoubling<T, W> (gloo::CudaAllreduceHalvingDoubling<T, W>,
+ * cuda_allreduce_halving_doubling.cc), same arguments as hydra_host_hip_ring_threads. */
+int hydra_host_hip_halving_doubling_threads(int P, int nptr, int dtype, size_t n,
+                                            void** dev_bufs, int workspace, int user_streams,
+                                            char* err, size_t errlen);
+
 /* gloo::AllreduceRingChunked<T>::run() (allreduce_ring_chunked.h:20-248), same arguments. */
 int hydra_host_allreduce_ring_chunked_threads(int P, int nptr, int dtype, size_t n, void** bufs,
                                               int reducer, hydra_inplace_fn fn, char* err,

@@ -259,3 +259,33 @@ def test_hip_allreduce_ring_chunked(gpu, O, workspace, P, nptr, n, dt):
             for i in range(nptr):
                 got = ts[r][i].cpu().numpy()
                 assert np.array_equal(got.view(np.uint32), exp[r][0].view(np.uint32)), (r, i)
+
+
+@pytest.mark.parametrize("workspace", ["host", "device"])
+@pytest.mark.parametrize("P,nptr,n,dt", [(1, 2, 1000, "f32"), (2, 1, 262145, "f32"),
+                                         (3, 2, 100003, "f32"), (4, 4, 4099, "f32"),
+                                         (5, 3, 7, "f32"), (6, 1, 300001, "f32"),
+                                         (7, 2, 70001, "i32"), (2, 1, 0, "f32")])
+def test_hip_allreduce_halving_doubling(gpu, O, workspace, P, nptr, n, dt):
+    """hydra::HipAllreduceHalvingDoubling<T, W> (gloo::CudaAllreduceHalvingDoubling<T, W>):
+    every rank ends with AllreduceHalvingDoubling's result (pinned to the reference by the
+    golden_hd fixtures) over the pairwise-tree local values, both workspaces, caller or own
+    streams; every pointer gets the result."""
+    import torch
+
+    code = {"f32": 6, "i32": 2}[dt]
+    if dt == "f32":
+        xs = [[synth.stress_f32(P, r, n, seed=60 + i) for i in range(nptr)] for r in range(P)]
+    else:
+        xs = [[synth.int32_bucket(P, r, n, seed=60 + i) for i in range(nptr)] for r in range(P)]
+    exp = [[_tree(O, xs[r], code)] for r in range(P)]
+    if n:
+        O.allreduce_halving_doubling(exp, dtype_code=code)
+    for user_streams in (False, True):
+        ts = [[torch.from_numpy(x.copy()).to(gpu) for x in xs[r]] for r in range(P)]
+        host.hip_ring_threads(ts, workspace=workspace, user_streams=user_streams,
+                              halving_doubling=True)
+        for r in range(P):
+            for i in range(nptr):
+                got = ts[r][i].cpu().numpy()
+                assert np.array_equal(got.view(np.uint32), exp[r][0].view(np.uint32)), (r, i)
