@@ -77,7 +77,7 @@ int spawn(int P, int rails, char* err, size_t errlen,
 namespace {
 template <typename T>
 int old_ring(int kind, int P, int nptr, size_t n, void** bufs, int reducer, hydra_inplace_fn fn,
-             char* err, size_t errlen) {  // kind: 0 AllreduceRing, 1 chunked, 2 halving-doubling
+             char* err, size_t errlen) {  // kind: 0 AllreduceRing, 1 chunked, 2 halving-doubling, 3 bcube
   using RF = hydra::ReductionFunction<T>;
   const RF* rf = nullptr;
   std::unique_ptr<RF> custom;
@@ -94,7 +94,10 @@ int old_ring(int kind, int P, int nptr, size_t n, void** bufs, int reducer, hydr
   return spawn(P, 1, err, errlen, [&](int r, std::vector<std::shared_ptr<hydra::Context>>& c) {
     std::vector<T*> ptrs;
     for (int i = 0; i < nptr; i++) ptrs.push_back(static_cast<T*>(bufs[r * nptr + i]));
-    if (kind == 2) {
+    if (kind == 3) {
+      hydra::AllreduceBcube<T> algo(c[0], ptrs, (int)n, rf);
+      algo.run();
+    } else if (kind == 2) {
       hydra::AllreduceHalvingDoubling<T> algo(c[0], ptrs, (int)n, rf);
       algo.run();
     } else if (kind == 1) {
@@ -284,6 +287,12 @@ int hydra_host_allreduce_halving_doubling_threads(int P, int nptr, int dtype, si
                                                   void** bufs, int reducer, hydra_inplace_fn fn,
                                                   char* err, size_t errlen) {
   return algorithm_ring(2, P, nptr, dtype, n, bufs, reducer, fn, err, errlen);
+}
+
+int hydra_host_allreduce_bcube_old_threads(int P, int nptr, int dtype, size_t n, void** bufs,
+                                           int reducer, hydra_inplace_fn fn, char* err,
+                                           size_t errlen) {
+  return algorithm_ring(3, P, nptr, dtype, n, bufs, reducer, fn, err, errlen);
 }
 
 int hydra_host_hip_ring_threads(int P, int nptr, int dtype, size_t n, void** dev_bufs,

@@ -44,6 +44,8 @@ def lib():
             L.hydra_host_allreduce_ring_old_threads.argtypes
         L.hydra_host_allreduce_halving_doubling_threads.argtypes = \
             L.hydra_host_allreduce_ring_old_threads.argtypes
+        L.hydra_host_allreduce_bcube_old_threads.argtypes = \
+            L.hydra_host_allreduce_ring_old_threads.argtypes
         L.hydra_host_reduce_threads.argtypes = [i, i, i, sz, vp, vp, i, sz, i, vp,
                                                 ctypes.c_long, ctypes.c_char_p, sz]
         L.hydra_host_reduce_timeout_probe.argtypes = [ctypes.c_long, ctypes.c_char_p, sz]
@@ -131,7 +133,7 @@ def apipe_threads(ins, outs, table=SPLIT_AA, reducer_fn=None, dtype_code=_lib.FL
 
 
 def allreduce_ring_old_threads(bufs, dtype_code=None, reducer_fn=None, chunked=False,
-                               halving_doubling=False):
+                               halving_doubling=False, bcube=False):
     """Old-style AllreduceRing<T>::run() on len(bufs) thread-ranks; bufs: [rank][ptr], in place.
     reducer_fn: None -> GPU sum; else address of a void(T* x, const T* y, size_t n).
     chunked: AllreduceRingChunked<T> instead; halving_doubling: AllreduceHalvingDoubling<T>."""
@@ -144,6 +146,8 @@ def allreduce_ring_old_threads(bufs, dtype_code=None, reducer_fn=None, chunked=F
          else lib().hydra_host_allreduce_ring_old_threads)
     if halving_doubling:
         f = lib().hydra_host_allreduce_halving_doubling_threads
+    if bcube:
+        f = lib().hydra_host_allreduce_bcube_old_threads
     rc = f(
         P, nptr, code, n, ctypes.cast(_ptrs([b for r in bufs for b in r]), ctypes.c_void_p), red,
         fp, err, 512)
@@ -156,6 +160,12 @@ def allreduce_halving_doubling_threads(bufs, dtype_code=None, reducer_fn=None):
     """hydra::AllreduceHalvingDoubling<T>::run() (allreduce_halving_doubling.h:37-358) on
     len(bufs) thread-ranks over loopback TCP; same arguments as allreduce_ring_old_threads."""
     return allreduce_ring_old_threads(bufs, dtype_code, reducer_fn, halving_doubling=True)
+
+
+def allreduce_bcube_old_threads(bufs, dtype_code=None, reducer_fn=None):
+    """Old-style hydra::AllreduceBcube<T>::run() (allreduce_bcube.h, base 2) on len(bufs)
+    thread-ranks (a power of two); same arguments as allreduce_ring_old_threads."""
+    return allreduce_ring_old_threads(bufs, dtype_code, reducer_fn, bcube=True)
 
 
 def hip_ring_threads(tensors, workspace: str = "host", user_streams: bool = False,

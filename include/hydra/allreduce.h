@@ -478,6 +478,49 @@ class AllreduceHalvingDoubling {
   std::vector<T> inbox_;
 };
 
+// Old-style gloo::AllreduceBcube<T> (allreduce_bcube.h:255-691) with the context's default base
+// 2: the left-fold local reduce (:339-341), then the hypercube reduce-scatter / all-gather.  For
+// P a power of two its result is the new-style BCUBE's bit for bit (checked against the
+// reference's own class, tests/test_oracle.py), so the bucket runs through allreduce(BCUBE)
+// with the ReductionFunction as the Func.  For other P the reference's ranks end with different
+// values; this class refuses them instead (EnforceNotMet).
+template <typename T>
+class AllreduceBcube {
+ public:
+  AllreduceBcube(const std::shared_ptr<Context>& context, const std::vector<T*>& ptrs, int count,
+                 const ReductionFunction<T>* fn)
+      : ctx_(context), ptrs_(ptrs), count_(count), fn_(fn) {
+    if (!fn_) throw EnforceNotMet("AllreduceBcube: null reduction function");
+    if (ptrs_.empty()) throw EnforceNotMet("AllreduceBcube: no pointers");
+    if (count_ < 0) throw EnforceNotMet("AllreduceBcube: negative count");
+    if (ctx_->size & (ctx_->size - 1))
+      throw EnforceNotMet("AllreduceBcube: the number of ranks must be a power of the base (2)");
+  }
+
+  void run() {
+    const size_t n = (size_t)count_, bytes = n * sizeof(T);
+    for (size_t i = 1; i < ptrs_.size(); i++) fn_->call(ptrs_[0], ptrs_[i], count_);
+    if (ctx_->size > 1 && n > 0) {
+      AllreduceOptions opts(ctx_);
+      opts.setAlgorithm(AllreduceOptions::BCUBE);
+      opts.setOutput(ptrs_[0], n);
+      const ReductionFunction<T>* fn = fn_;
+      opts.setReduceFunction([fn](void* c, const void* a, const void* b, size_t l) {
+        if (c != a) std::memcpy(c, a, l * sizeof(T));
+        fn->call(static_cast<T*>(c), static_cast<const T*>(b), l);
+      });
+      allreduce(opts);
+    }
+    for (size_t i = 1; i < ptrs_.size(); i++) std::memcpy(ptrs_[i], ptrs_[0], bytes);
+  }
+
+ private:
+  std::shared_ptr<Context> ctx_;
+  std::vector<T*> ptrs_;
+  int count_;
+  const ReductionFunction<T>* fn_;
+};
+
 // gloo::AllreduceRingChunked<T> (allreduce_ring_chunked.h:20-248): 2P chunks of
 // max(256, ceil(count/2P)) elements.  Rank r seeds chunks 2r and 2r+1; each later step i
 // (reduce pass rounds 2..2P-1, then broadcast pass rounds 0..2P-3) receives chunk co(i) from

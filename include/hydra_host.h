@@ -91,6 +91,12 @@ int hydra_host_allreduce_halving_doubling_threads(int P, int nptr, int dtype, si
                                                   void** bufs, int reducer, hydra_inplace_fn fn,
                                                   char* err, size_t errlen);
 
+/* Old-style gloo::AllreduceBcube<T>::run() (allreduce_bcube.h:255-691, base 2; P must be a
+ * power of two), same arguments as hydra_host_allreduce_ring_old_threads. */
+int hydra_host_allreduce_bcube_old_threads(int P, int nptr, int dtype, size_t n, void** bufs,
+                                           int reducer, hydra_inplace_fn fn, char* err,
+                                           size_t errlen);
+
 /* gloo::reduce (reduce.cc:21-262) to `root` on P thread-ranks.  in/out: P pointers each
  * (in == NULL: in place on out, reduce_test.cc:27-33).  Every rank's out is left as the
  * reference's schedule leaves it; only the root's is the reduction. */

@@ -253,17 +253,47 @@ def gen_halving_doubling(out: dict, meta: dict) -> None:
     meta["halving_doubling"] = rows
 
 
-def main_hd() -> None:
-    """Fixtures added after golden.npz was frozen go to their own file (golden_hd.*)."""
+def gen_bcube_old(out: dict, meta: dict) -> None:
+    """Old-style AllreduceBcube<T> (allreduce_bcube.h:255-691, context base 2): P a power of
+    two (for other P its ranks disagree, see tests/test_oracle.py), 1-2 pointers."""
+    rows = []
+    rng = np.random.default_rng(80)
+    for name, code in (("f32", 6), ("i32", 2), ("f16", 8)):
+        for P in (1, 2, 4, 8):
+            for n in (1, 7, 100, 1001):
+                for nptr in (1, 2):
+                    if name == "f32":
+                        bufs = [[synth.stress_f32(P, r, n, seed=800 + i) for i in range(nptr)]
+                                for r in range(P)]
+                    elif name == "i32":
+                        bufs = [[synth.int32_bucket(P, r, n, seed=800 + i) for i in range(nptr)]
+                                for r in range(P)]
+                    else:
+                        bufs = [[np.array([O.f2h(float(v)) for v in rng.uniform(-8, 8, n)],
+                                          np.uint16) for _ in range(nptr)] for _ in range(P)]
+                    key = f"bcube_old_{name}_P{P}_n{n}_k{nptr}"
+                    out[key + "_in"] = np.stack([np.stack(b) for b in bufs])
+                    O.ref_allreduce_bcube_old(bufs, dtype_code=code)
+                    res = np.stack([np.stack(b) for b in bufs])
+                    assert all(np.array_equal(res[0].view(np.uint8), res[r].view(np.uint8))
+                               for r in range(P)), key
+                    out[key + "_out"] = res[0, 0]
+                    rows.append({"key": key, "P": P, "n": n, "nptr": nptr, "dtype": code})
+    meta["bcube_old"] = rows
+
+
+def main_algo() -> None:
+    """Fixtures added after golden.npz was frozen go to their own file (golden_algo.*)."""
     out: dict = {}
-    meta: dict = {"generator": "oracle/gen_golden.py --hd",
+    meta: dict = {"generator": "oracle/gen_golden.py --algo",
                   "reference": "hydra-ppopp2024/hydra snapshot 2025-02-12, gloo core built by "
                                "oracle/Makefile (g++ -O3 -DNDEBUG)"}
     gen_halving_doubling(out, meta)
-    np.savez_compressed(os.path.join(GOLD, "golden_hd.npz"), **out)
-    with open(os.path.join(GOLD, "golden_hd.json"), "w") as f:
+    gen_bcube_old(out, meta)
+    np.savez_compressed(os.path.join(GOLD, "golden_algo.npz"), **out)
+    with open(os.path.join(GOLD, "golden_algo.json"), "w") as f:
         json.dump(meta, f, indent=1)
-    print(f"wrote {len(out)} arrays to golden_hd.npz")
+    print(f"wrote {len(out)} arrays to golden_algo.npz")
 
 
 def gen_new_test(meta: dict) -> None:
@@ -385,4 +415,4 @@ def main() -> None:
 if __name__ == "__main__":
     if not O.ref_available():
         raise SystemExit("oracle/_ref/libgloo_ref.so missing: make -C oracle ref")
-    main_hd() if "--hd" in sys.argv[1:] else main()
+    main_algo() if "--algo" in sys.argv[1:] else main()

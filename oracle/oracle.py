@@ -100,6 +100,7 @@ def ref():
                                                 _vp, ctypes.c_char_p, _c]
         _ref.ref_allreduce_ring_chunked.argtypes = _ref.ref_allreduce_ring_old.argtypes
         _ref.ref_allreduce_halving_doubling.argtypes = _ref.ref_allreduce_ring_old.argtypes
+        _ref.ref_allreduce_bcube_old.argtypes = _ref.ref_allreduce_ring_old.argtypes
         _ref.ref_reduce.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, _c, _vp, _vp,
                                     ctypes.c_int, _c, ctypes.c_long, ctypes.c_char_p, _c]
         _ref.ref_reduce_timeout.argtypes = [ctypes.c_long, ctypes.c_char_p, _c]
@@ -249,6 +250,19 @@ def allreduce_halving_doubling(bufs, kind="sum", dtype_code=None):
 def ref_allreduce_halving_doubling(bufs, dtype_code=None):
     """The reference's own AllreduceHalvingDoubling<T> (ReductionFunction<T>::sum)."""
     return _old_ring(True, bufs, "sum", dtype_code, hd=True)
+
+
+def ref_allreduce_bcube_old(bufs, dtype_code=None):
+    """The reference's own old-style AllreduceBcube<T> (allreduce_bcube.h, context base 2) on
+    thread-ranks, in place on bufs ([rank][ptr])."""
+    P, nptr = len(bufs), len(bufs[0])
+    ptrs = (_vp * (P * nptr))(*[_ptr(b) for r in bufs for b in r])
+    err = ctypes.create_string_buffer(512)
+    rc = ref().ref_allreduce_bcube_old(P, nptr, _dt(bufs[0][0], dtype_code), bufs[0][0].size,
+                                      ctypes.cast(ptrs, _vp), err, 512)
+    if rc:
+        raise RuntimeError(f"reference AllreduceBcube failed: {err.value.decode()}")
+    return bufs
 
 
 def split_aa(P: int, n: int):

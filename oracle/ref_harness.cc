@@ -324,6 +324,32 @@ extern "C" int ref_allreduce_halving_doubling(int P, int nptr, int dtype, size_t
   return 2;
 }
 
+// ---- old-style AllreduceBcube<T> (gloo/gloo/allreduce_bcube.h) ---------------------------
+#include "gloo/allreduce_bcube.h"
+
+namespace {
+template <typename T>
+int run_bcube_old(int P, int nptr, size_t n, void** bufs, char* err, size_t errlen) {
+  return spawn(P, [&](int r, std::shared_ptr<gloo::Context> ctx) {
+    std::vector<T*> ptrs;
+    for (int i = 0; i < nptr; i++) ptrs.push_back(static_cast<T*>(bufs[r * nptr + i]));
+    gloo::AllreduceBcube<T> algo(ctx, ptrs, (int)n, gloo::ReductionFunction<T>::sum);
+    algo.run();
+  }, err, errlen);
+}
+}  // namespace
+
+extern "C" int ref_allreduce_bcube_old(int P, int nptr, int dtype, size_t n, void** bufs,
+                                       char* err, size_t errlen) {
+  switch (dtype) {
+    case D_FLOAT32: return run_bcube_old<float>(P, nptr, n, bufs, err, errlen);
+    case D_INT32: return run_bcube_old<int32_t>(P, nptr, n, bufs, err, errlen);
+    case D_FLOAT16: return run_bcube_old<gloo::float16>(P, nptr, n, bufs, err, errlen);
+    case D_FLOAT64: return run_bcube_old<double>(P, nptr, n, bufs, err, errlen);
+  }
+  return 2;
+}
+
 // In place on bufs ([rank][ptr]), ReductionFunction<T>::sum; dtype: float32, int32, float16.
 extern "C" int ref_allreduce_ring_old(int P, int nptr, int dtype, size_t n, void** bufs,
                                       char* err, size_t errlen) {

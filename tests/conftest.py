@@ -31,13 +31,14 @@ def golden_meta():
 
 
 @pytest.fixture(scope="session")
-def golden_hd():
-    """AllreduceHalvingDoubling<T> fixtures (oracle/gen_golden.py --hd): inputs, result, meta."""
+def golden_algo():
+    """Algorithm-API fixtures (oracle/gen_golden.py --algo): AllreduceHalvingDoubling<T> and
+    old-style AllreduceBcube<T> inputs and results, meta."""
     import json
 
-    with open(os.path.join(GOLDEN, "golden_hd.json")) as f:
+    with open(os.path.join(GOLDEN, "golden_algo.json")) as f:
         meta = json.load(f)
-    return np.load(os.path.join(GOLDEN, "golden_hd.npz"), allow_pickle=False), meta
+    return np.load(os.path.join(GOLDEN, "golden_algo.npz"), allow_pickle=False), meta
 
 
 @pytest.fixture(scope="session")

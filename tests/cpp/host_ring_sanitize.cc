@@ -98,7 +98,8 @@ static void isum_u64(uint64_t* x, const uint64_t* y, size_t n) {
 
 // Old-style Algorithm API: AllreduceRing<T> / AllreduceRingChunked<T> /
 // AllreduceHalvingDoubling<T> (allreduce_ring.h, allreduce_ring_chunked.h,
-// allreduce_halving_doubling.h) with several pointers per rank.  kind: 0 ring, 1 chunked, 2 HD.
+// allreduce_halving_doubling.h, allreduce_bcube.h) with several pointers per rank.  kind: 0 ring,
+// 1 chunked, 2 halving-doubling, 3 old-style bcube.
 static int run_algorithm(int P, int nptr, int n, int kind) {
   hydra::HashStore store;
   std::vector<std::thread> th;
@@ -117,7 +118,10 @@ static int run_algorithm(int P, int nptr, int n, int kind) {
           ptrs.push_back(buf[i].data());
         }
         for (int it = 0; it < 2; it++) {  // the algorithm object is reusable across runs
-          if (kind == 2) {
+          if (kind == 3) {
+            hydra::AllreduceBcube<uint64_t> a(c, ptrs, n, &fn);
+            a.run();
+          } else if (kind == 2) {
             hydra::AllreduceHalvingDoubling<uint64_t> a(c, ptrs, n, &fn);
             a.run();
           } else if (kind == 1) {
@@ -224,7 +228,7 @@ int main() {
     fails++;
   }
   static const char* kNames[] = {"AllreduceRing", "AllreduceRingChunked",
-                                 "AllreduceHalvingDoubling"};
+                                 "AllreduceHalvingDoubling", "AllreduceBcube"};
   for (int kind : {0, 1, 2})
     for (int P : {1, 2, 3, 5, 7})
       for (int nptr : {1, 2})
@@ -233,6 +237,13 @@ int main() {
             std::fprintf(stderr, "FAIL %s P=%d nptr=%d n=%d\n", kNames[kind], P, nptr, n);
             fails++;
           }
+  for (int P : {1, 2, 4})  // AllreduceBcube: powers of the base only
+    for (int nptr : {1, 2})
+      for (int n : {1, 1000, 20011})
+        if (run_algorithm(P, nptr, n, 3)) {
+          std::fprintf(stderr, "FAIL %s P=%d nptr=%d n=%d\n", kNames[3], P, nptr, n);
+          fails++;
+        }
   std::printf("%s\n", fails ? "FAILED" : "OK");
   return fails ? 1 : 0;
 }

@@ -83,11 +83,11 @@ def test_chunked_allreduce_ring_gpu_reducer_vs_reference(gpu, golden, golden_met
                 assert np.array_equal(bufs[r][i].view(np.uint32), exp.view(np.uint32)), key
 
 
-def test_halving_doubling_gpu_reducer_vs_reference(gpu, golden_hd):
+def test_halving_doubling_gpu_reducer_vs_reference(gpu, golden_algo):
     """hydra::AllreduceHalvingDoubling<T> with the GPU in-place sum (gpuReductionFunction) ==
     the reference's own AllreduceHalvingDoubling<T> outputs (f32/i32), every rank and pointer,
     P = 1..12 (one to three binary blocks)."""
-    golden, meta = golden_hd
+    golden, meta = golden_algo
     for row in meta["halving_doubling"]:
         if row["dtype"] not in (6, 2):
             continue
@@ -95,6 +95,23 @@ def test_halving_doubling_gpu_reducer_vs_reference(gpu, golden_hd):
         ins = golden[key + "_in"]
         bufs = [[ins[r, i].copy() for i in range(k)] for r in range(P)]
         host.allreduce_halving_doubling_threads(bufs, dtype_code=row["dtype"])
+        exp = golden[key + "_out"]
+        for r in range(P):
+            for i in range(k):
+                assert np.array_equal(bufs[r][i].view(np.uint32), exp.view(np.uint32)), (key, r)
+
+
+def test_bcube_old_gpu_reducer_vs_reference(gpu, golden_algo):
+    """Old-style hydra::AllreduceBcube<T> with the GPU in-place sum == the reference's own
+    AllreduceBcube<T> outputs (f32/i32), every rank and pointer."""
+    golden, meta = golden_algo
+    for row in meta["bcube_old"]:
+        if row["dtype"] not in (6, 2):
+            continue
+        key, P, k = row["key"], row["P"], row["nptr"]
+        ins = golden[key + "_in"]
+        bufs = [[ins[r, i].copy() for i in range(k)] for r in range(P)]
+        host.allreduce_bcube_old_threads(bufs, dtype_code=row["dtype"])
         exp = golden[key + "_out"]
         for r in range(P):
             for i in range(k):
@@ -269,7 +286,7 @@ def test_hip_allreduce_ring_chunked(gpu, O, workspace, P, nptr, n, dt):
 def test_hip_allreduce_halving_doubling(gpu, O, workspace, P, nptr, n, dt):
     """hydra::HipAllreduceHalvingDoubling<T, W> (gloo::CudaAllreduceHalvingDoubling<T, W>):
     every rank ends with AllreduceHalvingDoubling's result (pinned to the reference by the
-    golden_hd fixtures) over the pairwise-tree local values, both workspaces, caller or own
+    golden_algo fixtures) over the pairwise-tree local values, both workspaces, caller or own
     streams; every pointer gets the result."""
     import torch
 

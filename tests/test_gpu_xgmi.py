@@ -353,13 +353,13 @@ def test_simulated_bcube_vs_reference_fixtures(gpu, golden, golden_meta):
                 assert hashlib.sha256(got.tobytes()).hexdigest() == row["output_sha256"], key
 
 
-def test_simulated_halving_doubling_vs_reference_fixtures(gpu, golden_hd):
+def test_simulated_halving_doubling_vs_reference_fixtures(gpu, golden_algo):
     """Device HALVING_DOUBLING plan == the reference's own AllreduceHalvingDoubling<T> on every
-    rank (tests/golden/golden_hd: P = 1..12, one to three binary blocks, fp32 stress / int32 /
+    rank (tests/golden/golden_algo: P = 1..12, one to three binary blocks, fp32 stress / int32 /
     f16, single-pointer cases)."""
     import torch
 
-    golden, meta = golden_hd
+    golden, meta = golden_algo
     views = {6: np.uint32, 2: np.int32, 8: np.int16}
     for row in meta["halving_doubling"]:
         if row["nptr"] != 1:

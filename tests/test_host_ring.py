@@ -300,11 +300,11 @@ def test_allreduce_test_single_pointer_p1_to_15(O, chunked):
                 assert np.all(bufs[r][0] == P * (P - 1) / 2), (P, n, r)
 
 
-def test_halving_doubling_vs_golden(O, golden_hd):
+def test_halving_doubling_vs_golden(O, golden_algo):
     """hydra::AllreduceHalvingDoubling<T> (allreduce_halving_doubling.h:37-358) reproduces the
     reference's result on every rank and pointer: one, two and three binary blocks (P = 1..12),
     tiny and ragged n (oracle in-place sum as the reducer)."""
-    golden, meta = golden_hd
+    golden, meta = golden_algo
     names = {6: "orc_isum_f32", 2: "orc_isum_i32", 8: "orc_isum_f16"}
     for row in meta["halving_doubling"]:
         key, P, k = row["key"], row["P"], row["nptr"]
@@ -331,3 +331,30 @@ def test_halving_doubling_large(O, P, n):
     O.allreduce_halving_doubling(exp)
     for r in range(P):
         assert np.array_equal(bufs[r][0].view(np.uint32), exp[r][0].view(np.uint32)), r
+
+
+def test_bcube_old_vs_golden(O, golden_algo):
+    """Old-style hydra::AllreduceBcube<T> (allreduce_bcube.h:255-691) reproduces the
+    reference's own class on every rank and pointer (P = 1, 2, 4, 8; 1-2 pointers; f32 / i32
+    / f16), with the oracle in-place sum as the reducer."""
+    golden, meta = golden_algo
+    names = {6: "orc_isum_f32", 2: "orc_isum_i32", 8: "orc_isum_f16"}
+    for row in meta["bcube_old"]:
+        key, P, k = row["key"], row["P"], row["nptr"]
+        ins = golden[key + "_in"]
+        bufs = [[ins[r, i].copy() for i in range(k)] for r in range(P)]
+        host.allreduce_bcube_old_threads(bufs, dtype_code=row["dtype"],
+                                         reducer_fn=fnptr(O, names[row["dtype"]]))
+        exp = golden[key + "_out"]
+        for r in range(P):
+            for i in range(k):
+                got = bufs[r][i]
+                assert np.array_equal(got.view(f"u{got.itemsize}"),
+                                      exp.view(f"u{exp.itemsize}")), (key, r, i)
+
+
+def test_bcube_old_rejects_non_power_of_two(O):
+    """The reference's ranks disagree for such P; the drop-in refuses them."""
+    bufs = [[np.ones(10, np.float32)] for _ in range(3)]
+    with pytest.raises(Exception, match="power of the base"):
+        host.allreduce_bcube_old_threads(bufs, reducer_fn=fnptr(O, "orc_isum_f32"))
