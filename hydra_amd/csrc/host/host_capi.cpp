@@ -77,7 +77,7 @@ int spawn(int P, int rails, char* err, size_t errlen,
 namespace {
 template <typename T>
 int old_ring(int kind, int P, int nptr, size_t n, void** bufs, int reducer, hydra_inplace_fn fn,
-             char* err, size_t errlen) {  // kind: 0 AllreduceRing, 1 chunked, 2 halving-doubling, 3 bcube
+             char* err, size_t errlen) {  // kind: 0 AllreduceRing, 1 chunked, 2 halving-doubling, 3 bcube, 4 local
   using RF = hydra::ReductionFunction<T>;
   const RF* rf = nullptr;
   std::unique_ptr<RF> custom;
@@ -94,7 +94,10 @@ int old_ring(int kind, int P, int nptr, size_t n, void** bufs, int reducer, hydr
   return spawn(P, 1, err, errlen, [&](int r, std::vector<std::shared_ptr<hydra::Context>>& c) {
     std::vector<T*> ptrs;
     for (int i = 0; i < nptr; i++) ptrs.push_back(static_cast<T*>(bufs[r * nptr + i]));
-    if (kind == 3) {
+    if (kind == 4) {
+      hydra::AllreduceLocal<T> algo(c[0], ptrs, (int)n, rf);
+      algo.run();
+    } else if (kind == 3) {
       hydra::AllreduceBcube<T> algo(c[0], ptrs, (int)n, rf);
       algo.run();
     } else if (kind == 2) {
@@ -111,7 +114,7 @@ int old_ring(int kind, int P, int nptr, size_t n, void** bufs, int reducer, hydr
 }
 template <typename T>
 int hip_ring(int P, int nptr, size_t n, void** bufs, int workspace, int user_streams, char* err,
-             size_t errlen, int kind = 0) {  // kind: 0 ring, 1 chunked, 2 halving-doubling
+             size_t errlen, int kind = 0) {  // kind: 0 ring, 1 chunked, 2 halving-doubling, 3 local
   const bool chunked = kind == 1;
   return spawn(P, 1, err, errlen, [&](int r, std::vector<std::shared_ptr<hydra::Context>>& c) {
     std::vector<T*> ptrs;
@@ -123,7 +126,10 @@ int hip_ring(int P, int nptr, size_t n, void** bufs, int workspace, int user_str
       streams.resize(nptr);
       for (auto& s : streams) hydra::gloo_compat::enforce(hydra_stream_create(dev, &s));
     }
-    if (kind == 2 && workspace == HYDRA_WORKSPACE_DEVICE) {
+    if (kind == 3) {
+      hydra::HipAllreduceLocal<T> algo(c[0], ptrs, (int)n, streams);
+      algo.run();
+    } else if (kind == 2 && workspace == HYDRA_WORKSPACE_DEVICE) {
       hydra::HipAllreduceHalvingDoubling<T, hydra::HipDeviceWorkspace<T>> algo(c[0], ptrs, (int)n,
                                                                                streams);
       algo.run();
@@ -295,6 +301,12 @@ int hydra_host_allreduce_bcube_old_threads(int P, int nptr, int dtype, size_t n,
   return algorithm_ring(3, P, nptr, dtype, n, bufs, reducer, fn, err, errlen);
 }
 
+int hydra_host_allreduce_local_threads(int P, int nptr, int dtype, size_t n, void** bufs,
+                                       int reducer, hydra_inplace_fn fn, char* err,
+                                       size_t errlen) {
+  return algorithm_ring(4, P, nptr, dtype, n, bufs, reducer, fn, err, errlen);
+}
+
 int hydra_host_hip_ring_threads(int P, int nptr, int dtype, size_t n, void** dev_bufs,
                                 int workspace, int user_streams, char* err, size_t errlen) {
   if (P < 1 || nptr < 1 || !dev_bufs || n > (size_t)INT32_MAX) {
@@ -350,6 +362,27 @@ int hydra_host_hip_halving_doubling_threads(int P, int nptr, int dtype, size_t n
       return hip_ring<int64_t>(P, nptr, n, dev_bufs, workspace, user_streams, err, errlen, 2);
   }
   set_err(err, errlen, "unsupported dtype for HipAllreduceHalvingDoubling");
+  return 3;
+}
+
+int hydra_host_hip_local_threads(int P, int nptr, int dtype, size_t n, void** dev_bufs,
+                                        int workspace, int user_streams, char* err,
+                                        size_t errlen) {
+  if (P < 1 || nptr < 1 || !dev_bufs || n > (size_t)INT32_MAX) {
+    set_err(err, errlen, "invalid arguments");
+    return 2;
+  }
+  switch (dtype) {
+    case HYDRA_FLOAT32:
+      return hip_ring<float>(P, nptr, n, dev_bufs, workspace, user_streams, err, errlen, 3);
+    case HYDRA_INT32:
+      return hip_ring<int32_t>(P, nptr, n, dev_bufs, workspace, user_streams, err, errlen, 3);
+    case HYDRA_FLOAT64:
+      return hip_ring<double>(P, nptr, n, dev_bufs, workspace, user_streams, err, errlen, 3);
+    case HYDRA_INT64:
+      return hip_ring<int64_t>(P, nptr, n, dev_bufs, workspace, user_streams, err, errlen, 3);
+  }
+  set_err(err, errlen, "unsupported dtype for HipAllreduceLocal");
   return 3;
 }
 

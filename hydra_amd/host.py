@@ -46,6 +46,9 @@ def lib():
             L.hydra_host_allreduce_ring_old_threads.argtypes
         L.hydra_host_allreduce_bcube_old_threads.argtypes = \
             L.hydra_host_allreduce_ring_old_threads.argtypes
+        L.hydra_host_allreduce_local_threads.argtypes = \
+            L.hydra_host_allreduce_ring_old_threads.argtypes
+        L.hydra_host_hip_local_threads.argtypes = L.hydra_host_hip_ring_threads.argtypes
         L.hydra_host_reduce_threads.argtypes = [i, i, i, sz, vp, vp, i, sz, i, vp,
                                                 ctypes.c_long, ctypes.c_char_p, sz]
         L.hydra_host_reduce_timeout_probe.argtypes = [ctypes.c_long, ctypes.c_char_p, sz]
@@ -133,7 +136,7 @@ def apipe_threads(ins, outs, table=SPLIT_AA, reducer_fn=None, dtype_code=_lib.FL
 
 
 def allreduce_ring_old_threads(bufs, dtype_code=None, reducer_fn=None, chunked=False,
-                               halving_doubling=False, bcube=False):
+                               halving_doubling=False, bcube=False, local=False):
     """Old-style AllreduceRing<T>::run() on len(bufs) thread-ranks; bufs: [rank][ptr], in place.
     reducer_fn: None -> GPU sum; else address of a void(T* x, const T* y, size_t n).
     chunked: AllreduceRingChunked<T> instead; halving_doubling: AllreduceHalvingDoubling<T>."""
@@ -148,6 +151,8 @@ def allreduce_ring_old_threads(bufs, dtype_code=None, reducer_fn=None, chunked=F
         f = lib().hydra_host_allreduce_halving_doubling_threads
     if bcube:
         f = lib().hydra_host_allreduce_bcube_old_threads
+    if local:
+        f = lib().hydra_host_allreduce_local_threads
     rc = f(
         P, nptr, code, n, ctypes.cast(_ptrs([b for r in bufs for b in r]), ctypes.c_void_p), red,
         fp, err, 512)
@@ -169,7 +174,8 @@ def allreduce_bcube_old_threads(bufs, dtype_code=None, reducer_fn=None):
 
 
 def hip_ring_threads(tensors, workspace: str = "host", user_streams: bool = False,
-                     dtype_code=None, chunked: bool = False, halving_doubling: bool = False):
+                     dtype_code=None, chunked: bool = False, halving_doubling: bool = False,
+                     local: bool = False):
     """hydra::HipAllreduceRing<T, W>::run() (gloo::CudaAllreduceRing) on len(tensors)
     thread-ranks; tensors: [rank][ptr] contiguous device tensors, reduced in place.
     chunked: HipAllreduceRingChunked<T, W> (gloo::CudaAllreduceRingChunked) instead;
@@ -189,6 +195,8 @@ def hip_ring_threads(tensors, workspace: str = "host", user_streams: bool = Fals
           else lib().hydra_host_hip_ring_threads)
     if halving_doubling:
         fn = lib().hydra_host_hip_halving_doubling_threads
+    if local:  # HipAllreduceLocal<T> (gloo::CudaAllreduceLocal)
+        fn = lib().hydra_host_hip_local_threads
     rc = fn(
         P, nptr, code, n, ctypes.cast(_ptrs_int([t.data_ptr() for r in tensors for t in r]),
                                       ctypes.c_void_p), ws, int(user_streams), err, 512)

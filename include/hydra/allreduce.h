@@ -478,6 +478,31 @@ class AllreduceHalvingDoubling {
   std::vector<T> inbox_;
 };
 
+// gloo::AllreduceLocal<T> (allreduce_local.{h,cc}): no communication -- ptrs[0] op= ptrs[i] in
+// pointer order (allreduce_local.cc:30-33), then every pointer gets ptrs[0] (:35-37).
+template <typename T>
+class AllreduceLocal {
+ public:
+  AllreduceLocal(const std::shared_ptr<Context>& context, const std::vector<T*>& ptrs, int count,
+                 const ReductionFunction<T>* fn)
+      : ctx_(context), ptrs_(ptrs), count_(count), fn_(fn) {
+    if (!fn_) throw EnforceNotMet("AllreduceLocal: null reduction function");
+    if (count_ < 0) throw EnforceNotMet("AllreduceLocal: negative count");
+  }
+
+  void run() {
+    for (size_t i = 1; i < ptrs_.size(); i++) fn_->call(ptrs_[0], ptrs_[i], count_);
+    for (size_t i = 1; i < ptrs_.size(); i++)
+      std::memcpy(ptrs_[i], ptrs_[0], (size_t)count_ * sizeof(T));
+  }
+
+ private:
+  std::shared_ptr<Context> ctx_;
+  std::vector<T*> ptrs_;
+  int count_;
+  const ReductionFunction<T>* fn_;
+};
+
 // Old-style gloo::AllreduceBcube<T> (allreduce_bcube.h:255-691) with the context's default base
 // 2: the left-fold local reduce (:339-341), then the hypercube reduce-scatter / all-gather.  For
 // P a power of two its result is the new-style BCUBE's bit for bit (checked against the

@@ -331,6 +331,70 @@ class HipAllreduceRingChunked {
   std::unique_ptr<gloo_compat::ContextPool::Lease> lease_;
 };
 
+// hydra::HipAllreduceLocal<T> -- gloo::CudaAllreduceLocal<T> (cuda_allreduce_local.cc:17-66):
+// the device pointers of one process reduced into ptrs[0] by the pairwise tree of
+// cudaDeviceReduce (cuda_collectives_device.h:29-56) on the gfx950 kernel, then copied to every
+// pointer on its stream (cudaDeviceBroadcast).  No communication; outputs are synchronized
+// unless the caller passes streams.
+template <typename T>
+class HipAllreduceLocal {
+ public:
+  HipAllreduceLocal(const std::shared_ptr<Context>& context, const std::vector<T*>& ptrs,
+                    int count,
+                    const std::vector<hydra_stream_t>& streams = std::vector<hydra_stream_t>())
+      : ctx_(context), ptrs_(ptrs), count_(count), synchronize_outputs_(streams.empty()) {
+    using detail::enforce;
+    if (count_ < 0) throw EnforceNotMet("HipAllreduceLocal: negative count");
+    if (!streams.empty() && streams.size() != ptrs_.size())
+      throw EnforceNotMet("HipAllreduceLocal: streams.size() != ptrs.size()");
+    if (count_ == 0 || ptrs_.size() < 2) return;
+    int device = -1;
+    for (T* p : ptrs_) {
+      int d = -1;
+      enforce(hydra_pointer_device(p, &d));
+      if (d < 0) throw EnforceNotMet("HipAllreduceLocal: ptrs must be device memory");
+      if (device >= 0 && d != device)
+        throw EnforceNotMet("HipAllreduceLocal: all pointers must be on one device");
+      device = d;
+    }
+    if (streams.empty()) {
+      owned_.resize(ptrs_.size());
+      for (auto& s : owned_) enforce(hydra_stream_create(device, &s));
+      streams_ = owned_;
+    } else {
+      streams_ = streams;
+    }
+  }
+  ~HipAllreduceLocal() {
+    for (auto s : owned_) hydra_stream_destroy(s);
+  }
+  HipAllreduceLocal(const HipAllreduceLocal&) = delete;
+  HipAllreduceLocal& operator=(const HipAllreduceLocal&) = delete;
+
+  void run() {
+    using detail::enforce;
+    if (count_ == 0 || ptrs_.size() < 2) return;
+    const int dt = gloo_compat::dtype_of<T>();
+    hydra_stream_t s0 = streams_[0];
+    for (size_t i = 1; i < streams_.size(); i++) enforce(hydra_stream_synchronize(streams_[i]));
+    for (size_t sz = 1; sz < ptrs_.size(); sz *= 2)
+      for (size_t j = 0; j + sz < ptrs_.size(); j += 2 * sz)
+        enforce(hydra_reduce(HYDRA_SUM, dt, ptrs_[j], ptrs_[j], ptrs_[j + sz], count_, s0));
+    enforce(hydra_stream_synchronize(s0));
+    for (size_t i = 1; i < ptrs_.size(); i++)
+      enforce(hydra_memcpy_async(ptrs_[i], ptrs_[0], (size_t)count_ * sizeof(T), streams_[i]));
+    if (synchronize_outputs_)
+      for (auto s : streams_) enforce(hydra_stream_synchronize(s));
+  }
+
+ private:
+  std::shared_ptr<Context> ctx_;
+  std::vector<T*> ptrs_;
+  int count_;
+  bool synchronize_outputs_;
+  std::vector<hydra_stream_t> streams_, owned_;
+};
+
 // hydra::HipAllreduceHalvingDoubling<T, W> -- the analog of gloo::CudaAllreduceHalvingDoubling
 // <T, W> (gloo/gloo/cuda_allreduce_halving_doubling.cc:246-408, non-pipelined): the pairwise-tree
 // local reduce on the device, then AllreduceHalvingDoubling's schedule

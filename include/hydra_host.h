@@ -97,6 +97,17 @@ int hydra_host_allreduce_bcube_old_threads(int P, int nptr, int dtype, size_t n,
                                            int reducer, hydra_inplace_fn fn, char* err,
                                            size_t errlen);
 
+/* gloo::AllreduceLocal<T>::run() (allreduce_local.cc:28-38): each rank's pointers only, same
+ * arguments as hydra_host_allreduce_ring_old_threads. */
+int hydra_host_allreduce_local_threads(int P, int nptr, int dtype, size_t n, void** bufs,
+                                       int reducer, hydra_inplace_fn fn, char* err,
+                                       size_t errlen);
+
+/* hydra::HipAllreduceLocal<T> (gloo::CudaAllreduceLocal<T>, cuda_allreduce_local.cc), same
+ * arguments as hydra_host_hip_ring_threads (workspace unused). */
+int hydra_host_hip_local_threads(int P, int nptr, int dtype, size_t n, void** dev_bufs,
+                                 int workspace, int user_streams, char* err, size_t errlen);
+
 /* gloo::reduce (reduce.cc:21-262) to `root` on P thread-ranks.  in/out: P pointers each
  * (in == NULL: in place on out, reduce_test.cc:27-33).  Every rank's out is left as the
  * reference's schedule leaves it; only the root's is the reduction. */

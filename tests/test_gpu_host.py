@@ -306,3 +306,27 @@ def test_hip_allreduce_halving_doubling(gpu, O, workspace, P, nptr, n, dt):
             for i in range(nptr):
                 got = ts[r][i].cpu().numpy()
                 assert np.array_equal(got.view(np.uint32), exp[r][0].view(np.uint32)), (r, i)
+
+
+@pytest.mark.parametrize("P,nptr,n,dt", [(1, 1, 1000, "f32"), (1, 2, 262145, "f32"),
+                                         (2, 3, 100003, "f32"), (1, 5, 4099, "i32"),
+                                         (1, 8, 7, "f32"), (1, 2, 0, "f32")])
+def test_hip_allreduce_local(gpu, O, P, nptr, n, dt):
+    """hydra::HipAllreduceLocal<T> (gloo::CudaAllreduceLocal<T>): every pointer of a rank ends
+    with the pairwise tree of cudaDeviceReduce (cuda_collectives_device.h:29-56) over that
+    rank's pointers, on the gfx950 kernel; caller or own streams."""
+    import torch
+
+    code = {"f32": 6, "i32": 2}[dt]
+    if dt == "f32":
+        xs = [[synth.stress_f32(nptr, i, n, seed=70 + r) for i in range(nptr)] for r in range(P)]
+    else:
+        xs = [[synth.int32_bucket(nptr, i, n, seed=70 + r) for i in range(nptr)] for r in range(P)]
+    exp = [_tree(O, xs[r], code) for r in range(P)]
+    for user_streams in (False, True):
+        ts = [[torch.from_numpy(x.copy()).to(gpu) for x in xs[r]] for r in range(P)]
+        host.hip_ring_threads(ts, user_streams=user_streams, local=True)
+        for r in range(P):
+            for i in range(nptr):
+                got = ts[r][i].cpu().numpy()
+                assert np.array_equal(got.view(np.uint32), exp[r].view(np.uint32)), (r, i)

@@ -358,3 +358,19 @@ def test_bcube_old_rejects_non_power_of_two(O):
     bufs = [[np.ones(10, np.float32)] for _ in range(3)]
     with pytest.raises(Exception, match="power of the base"):
         host.allreduce_bcube_old_threads(bufs, reducer_fn=fnptr(O, "orc_isum_f32"))
+
+
+@pytest.mark.parametrize("P,nptr,n", [(1, 1, 100), (1, 3, 1000), (2, 4, 4099), (3, 2, 0)])
+def test_allreduce_local(O, P, nptr, n):
+    """gloo::AllreduceLocal<T> (allreduce_local.cc:28-38): each rank's pointers left-folded in
+    pointer order into ptrs[0] (x = x op ptrs[i]), then copied to every pointer; ranks do not
+    communicate."""
+    xs = [[synth.stress_f32(nptr, i, n, seed=90 + r) for i in range(nptr)] for r in range(P)]
+    bufs = [[x.copy() for x in r] for r in xs]
+    host.allreduce_ring_old_threads(bufs, reducer_fn=fnptr(O, "orc_isum_f32"), local=True)
+    for r in range(P):
+        exp = xs[r][0].copy()
+        for i in range(1, nptr):
+            exp = exp + xs[r][i]  # float32 numpy add == the in-place fp32 sum, RNE
+        for i in range(nptr):
+            assert np.array_equal(bufs[r][i].view(np.uint32), exp.view(np.uint32)), (r, i)
