@@ -114,7 +114,7 @@ int old_ring(int kind, int P, int nptr, size_t n, void** bufs, int reducer, hydr
 }
 template <typename T>
 int hip_ring(int P, int nptr, size_t n, void** bufs, int workspace, int user_streams, char* err,
-             size_t errlen, int kind = 0) {  // kind: 0 ring, 1 chunked, 2 halving-doubling, 3 local
+             size_t errlen, int kind = 0) {  // kind: 0 ring, 1 chunked, 2 halving-doubling, 3 local, 4 bcube
   const bool chunked = kind == 1;
   return spawn(P, 1, err, errlen, [&](int r, std::vector<std::shared_ptr<hydra::Context>>& c) {
     std::vector<T*> ptrs;
@@ -126,7 +126,13 @@ int hip_ring(int P, int nptr, size_t n, void** bufs, int workspace, int user_str
       streams.resize(nptr);
       for (auto& s : streams) hydra::gloo_compat::enforce(hydra_stream_create(dev, &s));
     }
-    if (kind == 3) {
+    if (kind == 4 && workspace == HYDRA_WORKSPACE_DEVICE) {
+      hydra::HipAllreduceBcube<T, hydra::HipDeviceWorkspace<T>> algo(c[0], ptrs, (int)n, streams);
+      algo.run();
+    } else if (kind == 4) {
+      hydra::HipAllreduceBcube<T, hydra::HipHostWorkspace<T>> algo(c[0], ptrs, (int)n, streams);
+      algo.run();
+    } else if (kind == 3) {
       hydra::HipAllreduceLocal<T> algo(c[0], ptrs, (int)n, streams);
       algo.run();
     } else if (kind == 2 && workspace == HYDRA_WORKSPACE_DEVICE) {
@@ -362,6 +368,27 @@ int hydra_host_hip_halving_doubling_threads(int P, int nptr, int dtype, size_t n
       return hip_ring<int64_t>(P, nptr, n, dev_bufs, workspace, user_streams, err, errlen, 2);
   }
   set_err(err, errlen, "unsupported dtype for HipAllreduceHalvingDoubling");
+  return 3;
+}
+
+int hydra_host_hip_bcube_threads(int P, int nptr, int dtype, size_t n, void** dev_bufs,
+                                        int workspace, int user_streams, char* err,
+                                        size_t errlen) {
+  if (P < 1 || nptr < 1 || !dev_bufs || n > (size_t)INT32_MAX) {
+    set_err(err, errlen, "invalid arguments");
+    return 2;
+  }
+  switch (dtype) {
+    case HYDRA_FLOAT32:
+      return hip_ring<float>(P, nptr, n, dev_bufs, workspace, user_streams, err, errlen, 4);
+    case HYDRA_INT32:
+      return hip_ring<int32_t>(P, nptr, n, dev_bufs, workspace, user_streams, err, errlen, 4);
+    case HYDRA_FLOAT64:
+      return hip_ring<double>(P, nptr, n, dev_bufs, workspace, user_streams, err, errlen, 4);
+    case HYDRA_INT64:
+      return hip_ring<int64_t>(P, nptr, n, dev_bufs, workspace, user_streams, err, errlen, 4);
+  }
+  set_err(err, errlen, "unsupported dtype for HipAllreduceBcube");
   return 3;
 }
 

@@ -49,6 +49,7 @@ def lib():
         L.hydra_host_allreduce_local_threads.argtypes = \
             L.hydra_host_allreduce_ring_old_threads.argtypes
         L.hydra_host_hip_local_threads.argtypes = L.hydra_host_hip_ring_threads.argtypes
+        L.hydra_host_hip_bcube_threads.argtypes = L.hydra_host_hip_ring_threads.argtypes
         L.hydra_host_reduce_threads.argtypes = [i, i, i, sz, vp, vp, i, sz, i, vp,
                                                 ctypes.c_long, ctypes.c_char_p, sz]
         L.hydra_host_reduce_timeout_probe.argtypes = [ctypes.c_long, ctypes.c_char_p, sz]
@@ -175,7 +176,7 @@ def allreduce_bcube_old_threads(bufs, dtype_code=None, reducer_fn=None):
 
 def hip_ring_threads(tensors, workspace: str = "host", user_streams: bool = False,
                      dtype_code=None, chunked: bool = False, halving_doubling: bool = False,
-                     local: bool = False):
+                     local: bool = False, bcube: bool = False):
     """hydra::HipAllreduceRing<T, W>::run() (gloo::CudaAllreduceRing) on len(tensors)
     thread-ranks; tensors: [rank][ptr] contiguous device tensors, reduced in place.
     chunked: HipAllreduceRingChunked<T, W> (gloo::CudaAllreduceRingChunked) instead;
@@ -197,6 +198,8 @@ def hip_ring_threads(tensors, workspace: str = "host", user_streams: bool = Fals
         fn = lib().hydra_host_hip_halving_doubling_threads
     if local:  # HipAllreduceLocal<T> (gloo::CudaAllreduceLocal)
         fn = lib().hydra_host_hip_local_threads
+    if bcube:  # HipAllreduceBcube<T, W> (gloo::CudaAllreduceBcube)
+        fn = lib().hydra_host_hip_bcube_threads
     rc = fn(
         P, nptr, code, n, ctypes.cast(_ptrs_int([t.data_ptr() for r in tensors for t in r]),
                                       ctypes.c_void_p), ws, int(user_streams), err, 512)

@@ -331,6 +331,133 @@ class HipAllreduceRingChunked {
   std::unique_ptr<gloo_compat::ContextPool::Lease> lease_;
 };
 
+// hydra::HipAllreduceBcube<T, W> -- gloo::CudaAllreduceBcube<T, W> (cuda_allreduce_bcube.cc:
+// 111-200, 358-410): the local reduce into a pinned scratch (host workspace: cudaHostReduce's
+// left fold in pointer order below kOnDeviceThreshold = 256 KiB, algorithm.cc:16, else
+// cudaDeviceReduce's pairwise tree; device workspace: the tree), then the old-style
+// AllreduceBcube schedule (the BCUBE schedule for P a power of two, row a17) on the scratch with
+// every fold (scratch op= received, :151) on the gfx950 kernel, then every pointer gets the
+// result.  Other P are refused as by hydra::AllreduceBcube<T>.
+template <typename T, typename W>
+class HipAllreduceBcube {
+  static constexpr bool kDeviceWorkspace = std::is_same<W, HipDeviceWorkspace<T>>::value;
+  static_assert(kDeviceWorkspace || std::is_same<W, HipHostWorkspace<T>>::value,
+                "W must be HipHostWorkspace<T> or HipDeviceWorkspace<T>");
+  static constexpr size_t kOnDeviceThreshold = 256 * 1024;  // algorithm.cc:16
+
+ public:
+  HipAllreduceBcube(const std::shared_ptr<Context>& context, const std::vector<T*>& ptrs,
+                    int count,
+                    const std::vector<hydra_stream_t>& streams = std::vector<hydra_stream_t>())
+      : ctx_(context), ptrs_(ptrs), count_(count), bytes_((size_t)count * sizeof(T)),
+        synchronize_outputs_(streams.empty()) {
+    using detail::enforce;
+    if (ptrs_.empty()) throw EnforceNotMet("HipAllreduceBcube: no pointers");
+    if (count_ < 0) throw EnforceNotMet("HipAllreduceBcube: negative count");
+    if (ctx_->size & (ctx_->size - 1))
+      throw EnforceNotMet("HipAllreduceBcube: the number of ranks must be a power of the base (2)");
+    if (!streams.empty() && streams.size() != ptrs_.size())
+      throw EnforceNotMet("HipAllreduceBcube: streams.size() != ptrs.size()");
+    if (count_ == 0) return;
+    enforce(hydra_pointer_device(ptrs_[0], &device_));
+    if (device_ < 0) throw EnforceNotMet("HipAllreduceBcube: ptrs must be device memory");
+    for (T* p : ptrs_) {
+      int d = -1;
+      enforce(hydra_pointer_device(p, &d));
+      if (d != device_)
+        throw EnforceNotMet("HipAllreduceBcube: all pointers must be on one device");
+    }
+    if (streams.empty()) {
+      owned_.resize(ptrs_.size());
+      for (auto& s : owned_) enforce(hydra_stream_create(device_, &s));
+      streams_ = owned_;
+    } else {
+      streams_ = streams;
+    }
+    scratch_host_ = detail::Pinned(bytes_);
+    local_dev_ = detail::DeviceMem(device_, bytes_);
+    if (kDeviceWorkspace) inbox_dev_ = detail::DeviceMem(device_, bytes_);
+  }
+
+  ~HipAllreduceBcube() {
+    for (auto s : owned_) hydra_stream_destroy(s);
+  }
+  HipAllreduceBcube(const HipAllreduceBcube&) = delete;
+  HipAllreduceBcube& operator=(const HipAllreduceBcube&) = delete;
+
+  void run() {
+    using detail::enforce;
+    if (count_ == 0) return;
+    const int dt = gloo_compat::dtype_of<T>();
+    hydra_stream_t s0 = streams_[0];
+    for (size_t i = 1; i < streams_.size(); i++) enforce(hydra_stream_synchronize(streams_[i]));
+    // ---- local reduce into a device copy (the inputs stay untouched until the broadcast)
+    char* const dscratch = static_cast<char*>(local_dev_.p);
+    enforce(hydra_memcpy_async(dscratch, ptrs_[0], bytes_, s0));
+    if (!kDeviceWorkspace && bytes_ < kOnDeviceThreshold) {  // cudaHostReduce: left fold
+      for (size_t i = 1; i < ptrs_.size(); i++)
+        enforce(hydra_reduce(HYDRA_SUM, dt, dscratch, dscratch, ptrs_[i], count_, s0));
+    } else {  // cudaDeviceReduce: pairwise tree; operand j is ptrs[j] (dscratch for j = 0)
+      std::vector<const void*> v(ptrs_.begin(), ptrs_.end());
+      std::vector<void*> out(ptrs_.size(), nullptr);
+      out[0] = dscratch;
+      v[0] = dscratch;
+      for (size_t sz = 1; sz < ptrs_.size(); sz *= 2)
+        for (size_t j = 0; j + sz < ptrs_.size(); j += 2 * sz) {
+          if (!out[j]) {  // never write the caller's inputs: fold into a device temporary
+            temps_.emplace_back(new detail::DeviceMem(device_, bytes_));
+            out[j] = temps_.back()->p;
+          }
+          enforce(hydra_reduce(HYDRA_SUM, dt, out[j], v[j], v[j + sz], count_, s0));
+          v[j] = out[j];
+        }
+    }
+    char* const hscratch = static_cast<char*>(scratch_host_.p);
+    enforce(hydra_memcpy_async(hscratch, dscratch, bytes_, s0));
+    enforce(hydra_stream_synchronize(s0));
+    temps_.clear();
+    if (ctx_->size > 1) {
+      if (!kDeviceWorkspace)
+        lease_.reset(new gloo_compat::ContextPool::Lease(
+            gloo_compat::ContextPool::instance(device_).acquire()));
+      AllreduceOptions opts(ctx_);
+      opts.setAlgorithm(AllreduceOptions::BCUBE);
+      opts.setOutput(reinterpret_cast<T*>(hscratch), (size_t)count_);
+      opts.setReduceFunction([&](void* c, const void* a, const void* b, size_t n) {
+        if (!kDeviceWorkspace) {
+          enforce(hydra_reduce_host(lease_->get(), HYDRA_SUM, dt, c, a, b, n));
+          return;
+        }
+        // folds only touch regions no all-gather copy has written: the device copy is current
+        char* dev = dscratch + (static_cast<const char*>(a) - hscratch);
+        enforce(hydra_memcpy_async(inbox_dev_.p, b, n * sizeof(T), s0));
+        enforce(hydra_reduce(HYDRA_SUM, dt, dev, dev, inbox_dev_.p, n, s0));
+        enforce(hydra_memcpy_async(c, dev, n * sizeof(T), s0));
+        enforce(hydra_stream_synchronize(s0));
+      });
+      allreduce(opts);
+      lease_.reset();
+    }
+    for (size_t i = 0; i < ptrs_.size(); i++)
+      enforce(hydra_memcpy_async(ptrs_[i], hscratch, bytes_, streams_[i]));
+    if (synchronize_outputs_)
+      for (auto s : streams_) enforce(hydra_stream_synchronize(s));
+  }
+
+ private:
+  std::shared_ptr<Context> ctx_;
+  std::vector<T*> ptrs_;
+  int count_;
+  size_t bytes_;
+  bool synchronize_outputs_;
+  int device_ = -1;
+  std::vector<hydra_stream_t> streams_, owned_;
+  detail::Pinned scratch_host_;
+  detail::DeviceMem local_dev_, inbox_dev_;
+  std::vector<std::unique_ptr<detail::DeviceMem>> temps_;
+  std::unique_ptr<gloo_compat::ContextPool::Lease> lease_;
+};
+
 // hydra::HipAllreduceLocal<T> -- gloo::CudaAllreduceLocal<T> (cuda_allreduce_local.cc:17-66):
 // the device pointers of one process reduced into ptrs[0] by the pairwise tree of
 // cudaDeviceReduce (cuda_collectives_device.h:29-56) on the gfx950 kernel, then copied to every

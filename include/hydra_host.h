@@ -108,6 +108,11 @@ int hydra_host_allreduce_local_threads(int P, int nptr, int dtype, size_t n, voi
 int hydra_host_hip_local_threads(int P, int nptr, int dtype, size_t n, void** dev_bufs,
                                  int workspace, int user_streams, char* err, size_t errlen);
 
+/* hydra::HipAllreduceBcube<T, W> (gloo::CudaAllreduceBcube<T, W>, cuda_allreduce_bcube.cc; P a
+ * power of two), same arguments as hydra_host_hip_ring_threads. */
+int hydra_host_hip_bcube_threads(int P, int nptr, int dtype, size_t n, void** dev_bufs,
+                                 int workspace, int user_streams, char* err, size_t errlen);
+
 /* gloo::reduce (reduce.cc:21-262) to `root` on P thread-ranks.  in/out: P pointers each
  * (in == NULL: in place on out, reduce_test.cc:27-33).  Every rank's out is left as the
  * reference's schedule leaves it; only the root's is the reduction. */

@@ -330,3 +330,41 @@ def test_hip_allreduce_local(gpu, O, P, nptr, n, dt):
             for i in range(nptr):
                 got = ts[r][i].cpu().numpy()
                 assert np.array_equal(got.view(np.uint32), exp[r].view(np.uint32)), (r, i)
+
+
+@pytest.mark.parametrize("workspace", ["host", "device"])
+@pytest.mark.parametrize("P,nptr,n,dt", [(1, 2, 1000, "f32"), (2, 1, 262145, "f32"),
+                                         (4, 3, 1000, "f32"), (4, 3, 100003, "f32"),
+                                         (8, 2, 4099, "f32"), (2, 2, 70001, "i32"),
+                                         (2, 1, 0, "f32")])
+def test_hip_allreduce_bcube(gpu, O, workspace, P, nptr, n, dt):
+    """hydra::HipAllreduceBcube<T, W> (gloo::CudaAllreduceBcube<T, W>): the local reduce
+    (host workspace below 256 KiB: left fold in pointer order, cudaHostReduce; otherwise the
+    pairwise tree) then the old-style AllreduceBcube result (= the BCUBE bits for P = 2^k,
+    pinned by the golden_algo fixtures); every pointer gets it, caller or own streams."""
+    import torch
+
+    code = {"f32": 6, "i32": 2}[dt]
+    if dt == "f32":
+        xs = [[synth.stress_f32(P, r, n, seed=40 + i) for i in range(nptr)] for r in range(P)]
+    else:
+        xs = [[synth.int32_bucket(P, r, n, seed=40 + i) for i in range(nptr)] for r in range(P)]
+    left = workspace == "host" and n * 4 < 256 * 1024
+    loc = []
+    for r in range(P):
+        if left:
+            acc = xs[r][0].copy()
+            for i in range(1, nptr):
+                acc = O.op(acc, xs[r][i], "sum", code)
+            loc.append(acc)
+        else:
+            loc.append(_tree(O, xs[r], code))
+    exp = O.bcube_result(loc, dtype_code=code) if n and P > 1 else None
+    for user_streams in (False, True):
+        ts = [[torch.from_numpy(x.copy()).to(gpu) for x in xs[r]] for r in range(P)]
+        host.hip_ring_threads(ts, workspace=workspace, user_streams=user_streams, bcube=True)
+        for r in range(P):
+            want = exp if exp is not None else loc[r]
+            for i in range(nptr):
+                got = ts[r][i].cpu().numpy()
+                assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), (r, i)
