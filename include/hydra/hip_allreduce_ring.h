@@ -523,8 +523,10 @@ class HipAllreduceLocal {
 };
 
 // hydra::HipAllreduceHalvingDoubling<T, W> -- the analog of gloo::CudaAllreduceHalvingDoubling
-// <T, W> (gloo/gloo/cuda_allreduce_halving_doubling.cc:246-408, non-pipelined): the pairwise-tree
-// local reduce on the device, then AllreduceHalvingDoubling's schedule
+// <T, W> (gloo/gloo/cuda_allreduce_halving_doubling.cc:246-408, non-pipelined): the local reduce
+// on the device as the reference picks it (host workspace below kOnDeviceThreshold = 256 KiB:
+// cudaHostReduce's left fold, :478-481; otherwise cudaDeviceReduce's pairwise tree), then
+// AllreduceHalvingDoubling's schedule
 // (detail::halving_doubling, shared with the host class) on a pinned host copy of the bucket,
 // every fold (scratch op= received, :282-285, :299-302) on the gfx950 kernel -- zero-copy on
 // the pinned box (host workspace) or on the device copy after an H2D of the box (device
@@ -535,6 +537,7 @@ class HipAllreduceHalvingDoubling {
   static constexpr bool kDeviceWorkspace = std::is_same<W, HipDeviceWorkspace<T>>::value;
   static_assert(kDeviceWorkspace || std::is_same<W, HipHostWorkspace<T>>::value,
                 "W must be HipHostWorkspace<T> or HipDeviceWorkspace<T>");
+  static constexpr size_t kOnDeviceThreshold = 256 * 1024;  // algorithm.cc:16
 
  public:
   HipAllreduceHalvingDoubling(const std::shared_ptr<Context>& context,
@@ -584,9 +587,14 @@ class HipAllreduceHalvingDoubling {
     const int dt = gloo_compat::dtype_of<T>();
     hydra_stream_t s0 = streams_[0];
     for (size_t i = 1; i < streams_.size(); i++) enforce(hydra_stream_synchronize(streams_[i]));
-    for (size_t sz = 1; sz < ptrs_.size(); sz *= 2)  // CudaLocalNativeReduce tree, in place
-      for (size_t j = 0; j + sz < ptrs_.size(); j += 2 * sz)
-        enforce(hydra_reduce(HYDRA_SUM, dt, ptrs_[j], ptrs_[j], ptrs_[j + sz], count_, s0));
+    if (!kDeviceWorkspace && bytes_ < kOnDeviceThreshold) {  // cudaHostReduce: left fold (:478-481)
+      for (size_t i = 1; i < ptrs_.size(); i++)
+        enforce(hydra_reduce(HYDRA_SUM, dt, ptrs_[0], ptrs_[0], ptrs_[i], count_, s0));
+    } else {  // cudaDeviceReduce's pairwise tree, in place (the outputs are overwritten anyway)
+      for (size_t sz = 1; sz < ptrs_.size(); sz *= 2)
+        for (size_t j = 0; j + sz < ptrs_.size(); j += 2 * sz)
+          enforce(hydra_reduce(HYDRA_SUM, dt, ptrs_[j], ptrs_[j], ptrs_[j + sz], count_, s0));
+    }
     char* const dscratch = reinterpret_cast<char*>(ptrs_[0]);
     char* const hscratch = static_cast<char*>(scratch_host_.p);
     enforce(hydra_memcpy_async(hscratch, dscratch, bytes_, s0));

@@ -118,6 +118,17 @@ def test_bcube_old_gpu_reducer_vs_reference(gpu, golden_algo):
                 assert np.array_equal(bufs[r][i].view(np.uint32), exp.view(np.uint32)), (key, r)
 
 
+def _local(O, xs, code, left_fold):
+    """The CUDA algorithms' local reduce: cudaHostReduce's left fold in pointer order
+    (host workspace below kOnDeviceThreshold = 256 KiB, algorithm.cc:16) or the pairwise tree."""
+    if not left_fold:
+        return _tree(O, xs, code)
+    acc = xs[0].copy()
+    for x in xs[1:]:
+        acc = O.op(acc, x, "sum", code)
+    return acc
+
+
 def _tree(O, xs, code):
     """CudaLocalNativeReduce's pairwise tree in pointer order (cuda_collectives_native.h:93-122)."""
     xs = [x.copy() for x in xs]
@@ -295,7 +306,8 @@ def test_hip_allreduce_halving_doubling(gpu, O, workspace, P, nptr, n, dt):
         xs = [[synth.stress_f32(P, r, n, seed=60 + i) for i in range(nptr)] for r in range(P)]
     else:
         xs = [[synth.int32_bucket(P, r, n, seed=60 + i) for i in range(nptr)] for r in range(P)]
-    exp = [[_tree(O, xs[r], code)] for r in range(P)]
+    exp = [[_local(O, xs[r], code, workspace == "host" and n * 4 < 256 * 1024)]
+           for r in range(P)]
     if n:
         O.allreduce_halving_doubling(exp, dtype_code=code)
     for user_streams in (False, True):
@@ -350,15 +362,7 @@ def test_hip_allreduce_bcube(gpu, O, workspace, P, nptr, n, dt):
     else:
         xs = [[synth.int32_bucket(P, r, n, seed=40 + i) for i in range(nptr)] for r in range(P)]
     left = workspace == "host" and n * 4 < 256 * 1024
-    loc = []
-    for r in range(P):
-        if left:
-            acc = xs[r][0].copy()
-            for i in range(1, nptr):
-                acc = O.op(acc, xs[r][i], "sum", code)
-            loc.append(acc)
-        else:
-            loc.append(_tree(O, xs[r], code))
+    loc = [_local(O, xs[r], code, left) for r in range(P)]
     exp = O.bcube_result(loc, dtype_code=code) if n and P > 1 else None
     for user_streams in (False, True):
         ts = [[torch.from_numpy(x.copy()).to(gpu) for x in xs[r]] for r in range(P)]
