@@ -118,6 +118,9 @@ class HipAllreduceRing {
   }
 
   ~HipAllreduceRing() {
+    // outputs may still be copying from pinned scratch on the caller's streams: drain them
+    // before the members (pinned / device buffers) are freed
+    for (auto s : streams_) hydra_stream_synchronize(s);
     for (auto s : owned_) hydra_stream_destroy(s);
   }
   HipAllreduceRing(const HipAllreduceRing&) = delete;
@@ -259,6 +262,9 @@ class HipAllreduceRingChunked {
   }
 
   ~HipAllreduceRingChunked() {
+    // outputs may still be copying from pinned scratch on the caller's streams: drain them
+    // before the members (pinned / device buffers) are freed
+    for (auto s : streams_) hydra_stream_synchronize(s);
     for (auto s : owned_) hydra_stream_destroy(s);
   }
   HipAllreduceRingChunked(const HipAllreduceRingChunked&) = delete;
@@ -380,6 +386,9 @@ class HipAllreduceBcube {
   }
 
   ~HipAllreduceBcube() {
+    // outputs may still be copying from pinned scratch on the caller's streams: drain them
+    // before the members (pinned / device buffers) are freed
+    for (auto s : streams_) hydra_stream_synchronize(s);
     for (auto s : owned_) hydra_stream_destroy(s);
   }
   HipAllreduceBcube(const HipAllreduceBcube&) = delete;
@@ -493,6 +502,9 @@ class HipAllreduceLocal {
     }
   }
   ~HipAllreduceLocal() {
+    // outputs may still be copying from pinned scratch on the caller's streams: drain them
+    // before the members (pinned / device buffers) are freed
+    for (auto s : streams_) hydra_stream_synchronize(s);
     for (auto s : owned_) hydra_stream_destroy(s);
   }
   HipAllreduceLocal(const HipAllreduceLocal&) = delete;
@@ -576,6 +588,9 @@ class HipAllreduceHalvingDoubling {
   }
 
   ~HipAllreduceHalvingDoubling() {
+    // outputs may still be copying from pinned scratch on the caller's streams: drain them
+    // before the members (pinned / device buffers) are freed
+    for (auto s : streams_) hydra_stream_synchronize(s);
     for (auto s : owned_) hydra_stream_destroy(s);
   }
   HipAllreduceHalvingDoubling(const HipAllreduceHalvingDoubling&) = delete;
