@@ -52,6 +52,9 @@ def parse():
     p.add_argument("--watchdog-s", type=float, default=420.0,
                    help="N>1: abort (exit 3) if the run exceeds this many seconds")
     p.add_argument("--no-config5", action="store_true", help="N>1: skip the bf16 config-5 leg")
+    p.add_argument("--peer", action="store_true",
+                   help="N>1: also check, autotune and time the peer-access (IPC) schedules; "
+                        "off by default -- the cross-GPU IPC path has not run on an xGMI node")
     p.add_argument("--force-dist", action="store_true",
                    help="run the N>1 (RCCL) path even at world size 1 (code-path check)")
     return p.parse_args()

@@ -24,6 +24,8 @@ ESIZE = {INT8: 1, UINT8: 1, INT32: 4, UINT32: 4, INT64: 8, UINT64: 8, FLOAT32: 4
 
 EXPORTS = [  # every symbol include/hydra_hip.h declares
     "hydra_abi_version", "hydra_last_error", "hydra_device_count", "hydra_device_arch",
+    "hydra_device_check", "hydra_event_create", "hydra_event_record", "hydra_event_synchronize",
+    "hydra_event_destroy",
     "hydra_reduce", "hydra_chunk_sum", "hydra_acc_bf16_f32", "hydra_f32_to_bf16",
     "hydra_set_variant", "hydra_ctx_create", "hydra_ctx_destroy", "hydra_reduce_host",
     "hydra_chunk_sum_host", "hydra_host_register", "hydra_host_unregister",
@@ -91,6 +93,11 @@ def _declare(L) -> None:
     L.hydra_last_error.restype = ctypes.c_char_p
     L.hydra_device_count.argtypes = [ctypes.POINTER(i)]
     L.hydra_device_arch.argtypes = [i, ctypes.c_char_p, sz]
+    L.hydra_device_check.argtypes = [i]
+    L.hydra_event_create.argtypes = [ctypes.POINTER(vp)]
+    L.hydra_event_record.argtypes = [vp, vp]
+    L.hydra_event_synchronize.argtypes = [vp]
+    L.hydra_event_destroy.argtypes = [vp]
     L.hydra_reduce.argtypes = [i, i, vp, vp, vp, sz, vp]
     L.hydra_chunk_sum.argtypes = [i, vp, vp, vp, sz, vp]
     L.hydra_acc_bf16_f32.argtypes = [vp, vp, sz, vp]

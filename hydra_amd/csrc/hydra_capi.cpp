@@ -124,6 +124,14 @@ int hydra_device_arch(int device, char* buf, size_t len) {
   return ok();
 }
 
+int hydra_device_check(int device) {
+  HIP_TRY(hipSetDevice(device));
+  HIP_TRY(hipDeviceSynchronize());  // surfaces an asynchronous fault of any enqueued work
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return hydra::hip_fail(e, "sticky device error");
+  return ok();
+}
+
 int hydra_set_variant(int variant) { return g_variant.exchange(variant); }
 
 int hydra_reduce(int op, int dtype, void* c, const void* a, const void* b, size_t n,
@@ -328,6 +336,31 @@ int hydra_stream_destroy(hydra_stream_t s) {
 
 int hydra_stream_synchronize(hydra_stream_t s) {
   HIP_TRY(hipStreamSynchronize(static_cast<hipStream_t>(s)));
+  return ok();
+}
+
+int hydra_event_create(hydra_event_t* out) {
+  if (!out) return fail(HYDRA_ERR_INVALID, "null out");
+  hipEvent_t e = nullptr;
+  HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  *out = e;
+  return ok();
+}
+
+int hydra_event_record(hydra_event_t e, hydra_stream_t s) {
+  if (!e) return fail(HYDRA_ERR_INVALID, "null event");
+  HIP_TRY(hipEventRecord(static_cast<hipEvent_t>(e), static_cast<hipStream_t>(s)));
+  return ok();
+}
+
+int hydra_event_synchronize(hydra_event_t e) {
+  if (!e) return fail(HYDRA_ERR_INVALID, "null event");
+  HIP_TRY(hipEventSynchronize(static_cast<hipEvent_t>(e)));
+  return ok();
+}
+
+int hydra_event_destroy(hydra_event_t e) {
+  if (e) HIP_TRY(hipEventDestroy(static_cast<hipEvent_t>(e)));
   return ok();
 }
 

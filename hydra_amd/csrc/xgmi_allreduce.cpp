@@ -117,6 +117,68 @@ hipError_t launch_compute(const hydra::PlanOp& o, int op, int dtype, bool acc32,
                             st);
 }
 
+// Every access of a plan must stay inside the rank's user bucket (buf_bytes) and scratch
+// (scratch_bytes): a bad plan fails here with HYDRA_ERR_INVALID instead of faulting the GPU.
+// One check for all three executors (RCCL, simulator, the run_plan test hook).
+int validate_plan(const std::vector<hydra::PlanOp>& plan, int nranks, size_t es, size_t buf_bytes,
+                  size_t scratch_bytes) {
+  auto inside = [](int64_t off, int64_t len, size_t cap) {
+    return off >= 0 && len >= 0 && (size_t)off <= cap && (size_t)len <= cap - (size_t)off;
+  };
+  bool open = false;  // a SEND/RECV not yet closed by a GROUP
+  for (size_t i = 0; i < plan.size(); i++) {
+    const hydra::PlanOp& o = plan[i];
+    if (o.wait0 >= (int)i || o.wait1 >= (int)i)
+      return fail(HYDRA_ERR_INVALID, "plan: wait on a later op");
+    if (o.wait0 < -1 || o.wait1 < -1) return fail(HYDRA_ERR_INVALID, "plan: bad wait index");
+    switch (o.kind) {
+      case hydra::kOpSend:
+      case hydra::kOpRecv: {
+        if (o.buf != hydra::kBufUser && o.buf != hydra::kBufScratch)
+          return fail(HYDRA_ERR_INVALID, "plan: bad p2p buffer");
+        const size_t cap = o.buf == hydra::kBufUser ? buf_bytes : scratch_bytes;
+        if (o.peer < 0 || o.peer >= nranks || !inside(o.off, o.bytes, cap))
+          return fail(HYDRA_ERR_INVALID, "plan: bad p2p op");
+        open = true;
+        break;
+      }
+      case hydra::kOpGroup:
+        open = false;
+        break;
+      case hydra::kOpReduce:
+        if (open) return fail(HYDRA_ERR_INVALID, "plan: compute op inside a p2p group");
+        if (o.bytes % (int64_t)es || !inside(o.off, o.bytes, buf_bytes) ||
+            !inside(o.src_off, o.bytes, scratch_bytes))
+          return fail(HYDRA_ERR_INVALID, "plan: bad reduce");
+        break;
+      case hydra::kOpFold:
+        if (open) return fail(HYDRA_ERR_INVALID, "plan: compute op inside a p2p group");
+        if (o.nsrc < 1 || o.nsrc > hydra::kMaxRanks || o.bytes % (int64_t)es ||
+            !inside(o.off, o.bytes, buf_bytes))
+          return fail(HYDRA_ERR_INVALID, "plan: bad fold");
+        for (int j = 1; j < o.nsrc; j++)
+          if (!inside(hydra::fold_slot(o, j), o.bytes, scratch_bytes))
+            return fail(HYDRA_ERR_INVALID, "plan: fold slot outside scratch");
+        break;
+      case hydra::kOpAllToAll:
+        if (open) return fail(HYDRA_ERR_INVALID, "plan: collective inside a p2p group");
+        if (o.bytes < 0 || !inside(o.off, o.bytes * nranks, buf_bytes) ||
+            !inside(o.src_off, o.bytes * nranks, scratch_bytes))
+          return fail(HYDRA_ERR_INVALID, "plan: bad all-to-all");
+        break;
+      case hydra::kOpAllGather:
+        if (open) return fail(HYDRA_ERR_INVALID, "plan: collective inside a p2p group");
+        if (o.bytes < 0 || !inside(o.off, o.bytes * nranks, buf_bytes))
+          return fail(HYDRA_ERR_INVALID, "plan: bad all-gather");
+        break;
+      default:
+        return fail(HYDRA_ERR_INVALID, "plan: unknown op kind");
+    }
+  }
+  if (open) return fail(HYDRA_ERR_INVALID, "plan: unterminated p2p group");
+  return HYDRA_OK;
+}
+
 }  // namespace
 
 // ---- communicator ----------------------------------------------------------------------------
@@ -295,8 +357,10 @@ int hydra_comm_wait(hydra_comm_t c, hydra_stream_t stream, int64_t timeout_ms) {
 int hydra_comm_destroy(hydra_comm_t c) {
   if (!c) return ok();
   (void)hipSetDevice(c->device);
-  if (c->cs) (void)hipStreamSynchronize(c->cs);
-  if (c->ks) (void)hipStreamSynchronize(c->ks);
+  // Drain the DEVICE, not only cs/ks: the caller's stream may still hold waits on ev_cs/ev_ks
+  // and on plan events (join_streams), and kernels of an earlier allreduce may still read the
+  // scratch freed below.  Destroy is rare; a full drain is the safe order.
+  (void)hipDeviceSynchronize();
   if (c->nccl) (void)ncclCommDestroy(c->nccl);
   for (auto e : c->events) (void)hipEventDestroy(e);
   for (auto e : {c->ev_start, c->ev_cs, c->ev_ks})
@@ -344,9 +408,13 @@ int prepare(hydra_comm* c, int* algo, int op, int dtype, int flags, void* buf, s
                                   : hydra::make_geom(c->nranks, n, es, ms, chunk_bytes);
     rc = check_geometry(*algo, g);
     if (rc) return rc;
-    c->plan = hydra::make_plan(*algo, g, c->rank);
-    c->waited = waited_set(c->plan);
+    std::vector<hydra::PlanOp> plan = hydra::make_plan(*algo, g, c->rank);
     const size_t need = hydra::plan_scratch_bytes(*algo, g);
+    rc = validate_plan(plan, c->nranks, es, n * es, need);
+    if (rc) return rc;
+    c->key_algo = -1;  // invalid until the new plan, its scratch and events are all in place
+    c->plan = std::move(plan);
+    c->waited = waited_set(c->plan);
     if (need > c->scratch_bytes) {
       // (re)allocation happens outside any capture: first call with a new geometry
       HIP_TRY(hipDeviceSynchronize());
@@ -480,8 +548,11 @@ int plan_impl(int algo, int root, int P, int rank, size_t n, size_t esize, size_
                                       : hydra::make_geom(P, n, esize, ms, chunk_bytes);
   if (int rc = check_geometry(algo, g)) return rc;
   const auto plan = hydra::make_plan(algo, g, rank);
+  const size_t sbytes = hydra::plan_scratch_bytes(algo, g);
+  // the library's own plans pass the executors' bounds check (CPU-testable, tests/test_plan.py)
+  if (int rc = validate_plan(plan, P, esize, n * esize, sbytes)) return rc;
   if (count) *count = plan.size();
-  if (scratch_bytes) *scratch_bytes = hydra::plan_scratch_bytes(algo, g);
+  if (scratch_bytes) *scratch_bytes = sbytes;
   if (ops) {
     static_assert(sizeof(hydra_plan_op_t) == sizeof(hydra::PlanOp), "layout");
     const size_t k = plan.size() < cap ? plan.size() : cap;
@@ -571,10 +642,14 @@ int simulate_impl(int algo, int root, int op, int dtype, int flags, int P, void*
     }                                               \
   } while (0)
 
+  for (int r = 0; r < P; r++) {  // validated before anything is enqueued
+    R[r].ops = hydra::make_plan(algo, g, r);
+    rc = validate_plan(R[r].ops, P, es, n * es, sbytes);
+    if (rc) return rc;
+  }
   SIM_TRY(hipDeviceSynchronize());
   SIM_TRY(hipStreamCreateWithFlags(&fabric, hipStreamNonBlocking));
   for (int r = 0; r < P; r++) {
-    R[r].ops = hydra::make_plan(algo, g, r);
     R[r].waited = waited_set(R[r].ops);
     R[r].ev.resize(R[r].ops.size(), nullptr);
     for (size_t i = 0; i < R[r].ops.size(); i++)
@@ -752,54 +827,8 @@ int hydra_comm_run_plan(hydra_comm_t c, const hydra_plan_op_t* ops, size_t nops,
   std::vector<hydra::PlanOp> plan(nops);
   if (nops) std::memcpy(plan.data(), ops, nops * sizeof(hydra::PlanOp));
   // every access must stay inside buf / scratch: a bad plan must fail here, not fault the GPU
-  auto inside = [](int64_t off, int64_t len, size_t cap) {
-    return off >= 0 && len >= 0 && (size_t)off <= cap && (size_t)len <= cap - (size_t)off;
-  };
-  for (size_t i = 0; i < nops; i++) {
-    const hydra::PlanOp& o = plan[i];
-    const size_t cap = o.buf == hydra::kBufUser ? buf_bytes : scratch_bytes;
-    if ((o.wait0 >= (int)i) || (o.wait1 >= (int)i))
-      return fail(HYDRA_ERR_INVALID, "plan: wait on a later op");
-    switch (o.kind) {
-      case hydra::kOpSend:
-      case hydra::kOpRecv:
-        if (o.peer < 0 || o.peer >= c->nranks || !inside(o.off, o.bytes, cap))
-          return fail(HYDRA_ERR_INVALID, "plan: bad p2p op");
-        break;
-      case hydra::kOpGroup:
-        break;
-      case hydra::kOpReduce:
-        if (o.bytes % (int64_t)es || !inside(o.off, o.bytes, buf_bytes) ||
-            !inside(o.src_off, o.bytes, scratch_bytes))
-          return fail(HYDRA_ERR_INVALID, "plan: bad reduce");
-        break;
-      case hydra::kOpFold:
-        if (o.nsrc < 1 || o.nsrc > hydra::kMaxRanks || o.bytes % (int64_t)es ||
-            !inside(o.off, o.bytes, buf_bytes))
-          return fail(HYDRA_ERR_INVALID, "plan: bad fold");
-        for (int j = 1; j < o.nsrc; j++)
-          if (!inside(hydra::fold_slot(o, j), o.bytes, scratch_bytes))
-            return fail(HYDRA_ERR_INVALID, "plan: fold slot outside scratch");
-        break;
-      case hydra::kOpAllToAll:
-        if (o.bytes < 0 || !inside(o.off, o.bytes * c->nranks, buf_bytes) ||
-            !inside(o.src_off, o.bytes * c->nranks, scratch_bytes))
-          return fail(HYDRA_ERR_INVALID, "plan: bad all-to-all");
-        break;
-      case hydra::kOpAllGather:
-        if (o.bytes < 0 || !inside(o.off, o.bytes * c->nranks, buf_bytes))
-          return fail(HYDRA_ERR_INVALID, "plan: bad all-gather");
-        break;
-      default:
-        return fail(HYDRA_ERR_INVALID, "plan: unknown op kind");
-    }
-  }
-  if (nops && plan.back().kind != hydra::kOpGroup) {
-    bool open = false;
-    for (const auto& o : plan) open = (o.kind == hydra::kOpSend || o.kind == hydra::kOpRecv) ? true
-                                      : (o.kind == hydra::kOpGroup ? false : open);
-    if (open) return fail(HYDRA_ERR_INVALID, "plan: unterminated p2p group");
-  }
+  rc = validate_plan(plan, c->nranks, es, buf_bytes, scratch_bytes);
+  if (rc) return rc;
   if (scratch_bytes > c->scratch_bytes) {
     HIP_TRY(hipDeviceSynchronize());
     if (c->scratch) HIP_TRY(hipFree(c->scratch));

@@ -380,44 +380,27 @@ def bench_allreduce(args, dev) -> dict:
     from . import synth
 
     rank, world = dist.get_rank(), dist.get_world_size()
-    # a hung collective must fail the run, not stall it: hard exit after `watchdog_s`
+    # a hung collective must fail the run, not stall it: hard exit (status 3) after `watchdog_s`,
+    # printing the measured headline flagged when there is one (hydra_amd/watchdog.py)
     import os
-    import sys
-    import threading
+
+    from . import watchdog
 
     state = {}  # "result": builds the JSON line once the headline measurement is complete
-
-    def _expire():
-        done = state.get("result")
-        if done is not None:  # headline measured: report it, flag the context as cut short
-            sys.stderr.write(f"[hydra bench] rank {rank}: watchdog expired in the context "
-                             "phase; reporting the headline\n")
-            sys.stderr.flush()
-            if rank == 0:
-                import json
-
-                r = done()
-                r["watchdog"] = ("measurements after this headline (autotune, other algorithms, "
-                                 "config 5) cut short")
-                print(json.dumps(r), flush=True)
-            os._exit(0)
-        sys.stderr.write(f"[hydra bench] rank {rank}: watchdog expired, aborting\n")
-        sys.stderr.flush()
-        os._exit(3)
-
-    dog = threading.Timer(float(getattr(args, "watchdog_s", 420)), _expire)
-    dog.daemon = True
-    dog.start()
+    dog = watchdog.start(rank, float(getattr(args, "watchdog_s", 420)), state)
     uid = exchange_unique_id(rank, dev)
     comm = XgmiComm(rank, world, dev.index, uid)
     rail2 = XgmiComm(rank, world, dev.index, exchange_unique_id(rank, dev))  # apipe's 2nd rail
     from .peer import PeerComm
 
     pg = {"peer": None, "err": None}  # IPC-mapped buckets, one kernel per allreduce
-    try:  # (hydra_amd.peer; setup fails collectively, so every rank takes the same branch)
-        pg["peer"] = PeerComm(rank, world, dev.index)
-    except HydraError as e:
-        pg["err"] = str(e)
+    if getattr(args, "peer", False):
+        try:  # (hydra_amd.peer; setup fails collectively, so every rank takes the same branch)
+            pg["peer"] = PeerComm(rank, world, dev.index)
+        except HydraError as e:
+            pg["err"] = str(e)
+    else:  # opt-in until the cross-GPU IPC path has run on an xGMI node
+        pg["err"] = "disabled (bench.py --peer enables the peer-access schedules)"
     n = args.elements
     algo = getattr(args, "algo", "auto")
 

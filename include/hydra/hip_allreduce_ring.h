@@ -73,6 +73,36 @@ struct DeviceMem {
     if (p) hydra_free(p);
   }
 };
+// Completion of run()'s last output copies, recorded on each caller stream as an event this
+// object owns.  The destructor waits on these events before the pinned / device scratch the
+// copies read is freed -- never on the caller's streams, which it does not own and which the
+// caller may already have destroyed.
+class OutputFence {
+ public:
+  OutputFence() = default;
+  OutputFence(const OutputFence&) = delete;
+  OutputFence& operator=(const OutputFence&) = delete;
+  ~OutputFence() {
+    wait_nothrow();
+    for (auto e : ev_) hydra_event_destroy(e);
+  }
+  void record(const std::vector<hydra_stream_t>& streams) {
+    while (ev_.size() < streams.size()) {
+      hydra_event_t e = nullptr;
+      enforce(hydra_event_create(&e));
+      ev_.push_back(e);
+    }
+    for (size_t i = 0; i < streams.size(); i++) enforce(hydra_event_record(ev_[i], streams[i]));
+    recorded_ = streams.size();
+  }
+  void wait_nothrow() {
+    for (size_t i = 0; i < recorded_; i++) hydra_event_synchronize(ev_[i]);
+  }
+
+ private:
+  std::vector<hydra_event_t> ev_;
+  size_t recorded_ = 0;
+};
 }  // namespace detail
 
 template <typename T, typename W = HipHostWorkspace<T>>
@@ -118,9 +148,9 @@ class HipAllreduceRing {
   }
 
   ~HipAllreduceRing() {
-    // outputs may still be copying from pinned scratch on the caller's streams: drain them
-    // before the members (pinned / device buffers) are freed
-    for (auto s : streams_) hydra_stream_synchronize(s);
+    // outputs may still be copying from pinned scratch on the caller's streams: wait for the
+    // fence events run() recorded (not the streams) before the pinned / device buffers are freed
+    fence_.wait_nothrow();
     for (auto s : owned_) hydra_stream_destroy(s);
   }
   HipAllreduceRing(const HipAllreduceRing&) = delete;
@@ -190,6 +220,7 @@ class HipAllreduceRing {
       for (size_t i = 0; i < ptrs_.size(); i++)
         enforce(hydra_memcpy_async(ptrs_[i], scratch, bytes_, streams_[i]));
     }
+    fence_.record(streams_);
     if (synchronize_outputs_)
       for (auto s : streams_) enforce(hydra_stream_synchronize(s));
   }
@@ -203,6 +234,7 @@ class HipAllreduceRing {
   bool synchronize_outputs_;
   int device_ = -1;
   std::vector<hydra_stream_t> streams_, owned_;
+  detail::OutputFence fence_;  // declared last: destroyed first, before any scratch
   detail::Pinned boxes_[2], scratch_host_;
   detail::DeviceMem inbox_dev_, local_dev_;
   std::unique_ptr<gloo_compat::ContextPool::Lease> lease_;
@@ -262,9 +294,9 @@ class HipAllreduceRingChunked {
   }
 
   ~HipAllreduceRingChunked() {
-    // outputs may still be copying from pinned scratch on the caller's streams: drain them
-    // before the members (pinned / device buffers) are freed
-    for (auto s : streams_) hydra_stream_synchronize(s);
+    // outputs may still be copying from pinned scratch on the caller's streams: wait for the
+    // fence events run() recorded (not the streams) before the pinned / device buffers are freed
+    fence_.wait_nothrow();
     for (auto s : owned_) hydra_stream_destroy(s);
   }
   HipAllreduceRingChunked(const HipAllreduceRingChunked&) = delete;
@@ -319,6 +351,7 @@ class HipAllreduceRingChunked {
       for (size_t i = 0; i < ptrs_.size(); i++)
         enforce(hydra_memcpy_async(ptrs_[i], hscratch, bytes_, streams_[i]));
     }
+    fence_.record(streams_);
     if (synchronize_outputs_)
       for (auto s : streams_) enforce(hydra_stream_synchronize(s));
   }
@@ -332,6 +365,7 @@ class HipAllreduceRingChunked {
   bool synchronize_outputs_;
   int device_ = -1;
   std::vector<hydra_stream_t> streams_, owned_;
+  detail::OutputFence fence_;  // declared last: destroyed first, before any scratch
   detail::Pinned scratch_host_, inbox_[2];
   detail::DeviceMem inbox_dev_;
   std::unique_ptr<gloo_compat::ContextPool::Lease> lease_;
@@ -386,9 +420,9 @@ class HipAllreduceBcube {
   }
 
   ~HipAllreduceBcube() {
-    // outputs may still be copying from pinned scratch on the caller's streams: drain them
-    // before the members (pinned / device buffers) are freed
-    for (auto s : streams_) hydra_stream_synchronize(s);
+    // outputs may still be copying from pinned scratch on the caller's streams: wait for the
+    // fence events run() recorded (not the streams) before the pinned / device buffers are freed
+    fence_.wait_nothrow();
     for (auto s : owned_) hydra_stream_destroy(s);
   }
   HipAllreduceBcube(const HipAllreduceBcube&) = delete;
@@ -449,6 +483,7 @@ class HipAllreduceBcube {
     }
     for (size_t i = 0; i < ptrs_.size(); i++)
       enforce(hydra_memcpy_async(ptrs_[i], hscratch, bytes_, streams_[i]));
+    fence_.record(streams_);
     if (synchronize_outputs_)
       for (auto s : streams_) enforce(hydra_stream_synchronize(s));
   }
@@ -461,6 +496,7 @@ class HipAllreduceBcube {
   bool synchronize_outputs_;
   int device_ = -1;
   std::vector<hydra_stream_t> streams_, owned_;
+  detail::OutputFence fence_;  // declared last: destroyed first, before any scratch
   detail::Pinned scratch_host_;
   detail::DeviceMem local_dev_, inbox_dev_;
   std::vector<std::unique_ptr<detail::DeviceMem>> temps_;
@@ -502,9 +538,9 @@ class HipAllreduceLocal {
     }
   }
   ~HipAllreduceLocal() {
-    // outputs may still be copying from pinned scratch on the caller's streams: drain them
-    // before the members (pinned / device buffers) are freed
-    for (auto s : streams_) hydra_stream_synchronize(s);
+    // outputs may still be copying from pinned scratch on the caller's streams: wait for the
+    // fence events run() recorded (not the streams) before the pinned / device buffers are freed
+    fence_.wait_nothrow();
     for (auto s : owned_) hydra_stream_destroy(s);
   }
   HipAllreduceLocal(const HipAllreduceLocal&) = delete;
@@ -522,6 +558,7 @@ class HipAllreduceLocal {
     enforce(hydra_stream_synchronize(s0));
     for (size_t i = 1; i < ptrs_.size(); i++)
       enforce(hydra_memcpy_async(ptrs_[i], ptrs_[0], (size_t)count_ * sizeof(T), streams_[i]));
+    fence_.record(streams_);
     if (synchronize_outputs_)
       for (auto s : streams_) enforce(hydra_stream_synchronize(s));
   }
@@ -532,6 +569,7 @@ class HipAllreduceLocal {
   int count_;
   bool synchronize_outputs_;
   std::vector<hydra_stream_t> streams_, owned_;
+  detail::OutputFence fence_;  // declared last: destroyed first, before any scratch
 };
 
 // hydra::HipAllreduceHalvingDoubling<T, W> -- the analog of gloo::CudaAllreduceHalvingDoubling
@@ -588,9 +626,9 @@ class HipAllreduceHalvingDoubling {
   }
 
   ~HipAllreduceHalvingDoubling() {
-    // outputs may still be copying from pinned scratch on the caller's streams: drain them
-    // before the members (pinned / device buffers) are freed
-    for (auto s : streams_) hydra_stream_synchronize(s);
+    // outputs may still be copying from pinned scratch on the caller's streams: wait for the
+    // fence events run() recorded (not the streams) before the pinned / device buffers are freed
+    fence_.wait_nothrow();
     for (auto s : owned_) hydra_stream_destroy(s);
   }
   HipAllreduceHalvingDoubling(const HipAllreduceHalvingDoubling&) = delete;
@@ -638,6 +676,7 @@ class HipAllreduceHalvingDoubling {
     // broadcast (localBroadcastOp_): every pointer gets the pinned copy's result
     for (size_t i = 0; i < ptrs_.size(); i++)
       enforce(hydra_memcpy_async(ptrs_[i], hscratch, bytes_, streams_[i]));
+    fence_.record(streams_);
     if (synchronize_outputs_)
       for (auto s : streams_) enforce(hydra_stream_synchronize(s));
   }
@@ -652,6 +691,7 @@ class HipAllreduceHalvingDoubling {
   detail::HalvingDoublingGeometry geo_;
   int device_ = -1;
   std::vector<hydra_stream_t> streams_, owned_;
+  detail::OutputFence fence_;  // declared last: destroyed first, before any scratch
   detail::Pinned scratch_host_, inbox_;
   detail::DeviceMem inbox_dev_;
   std::unique_ptr<gloo_compat::ContextPool::Lease> lease_;

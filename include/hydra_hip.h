@@ -72,6 +72,9 @@ int hydra_abi_version(void);
 const char* hydra_last_error(void);      /* thread-local; "" when the last call succeeded */
 int hydra_device_count(int* count);
 int hydra_device_arch(int device, char* buf, size_t len); /* e.g. "gfx950:sramecc+:xnack-" */
+/* Drain every stream of `device` and report a pending asynchronous error (a faulting kernel,
+ * an illegal address).  Test attribution: the GPU suite calls it after every test. */
+int hydra_device_check(int device);
 
 /* ---- device-resident reduction (the hot path) ---------------------------------------------
  * c[i] = op(a[i], b[i]) for i < n, enqueued on `stream` (asynchronous, graph-capturable: no
@@ -118,6 +121,13 @@ int hydra_host_unregister(void* ptr);
 int hydra_stream_create(int device, hydra_stream_t* out);
 int hydra_stream_destroy(hydra_stream_t s);
 int hydra_stream_synchronize(hydra_stream_t s);
+/* Events (hipEvent_t, timing disabled): completion markers an owner records on a caller's
+ * stream, so it can later wait for ITS work without touching a stream it does not own. */
+typedef void* hydra_event_t;
+int hydra_event_create(hydra_event_t* out);
+int hydra_event_record(hydra_event_t e, hydra_stream_t s);
+int hydra_event_synchronize(hydra_event_t e);
+int hydra_event_destroy(hydra_event_t e);
 int hydra_malloc(int device, size_t bytes, void** out);
 int hydra_free(void* p);
 int hydra_memcpy(void* dst, const void* src, size_t bytes); /* hipMemcpyDefault, synchronous */

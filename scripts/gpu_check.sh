@@ -26,7 +26,7 @@ rocminfo 2>/dev/null | grep -m2 -E "gfx|Marketing" > "$OUT/device.txt" || true
 nproc > "$OUT/host.txt"; grep -m1 "model name" /proc/cpuinfo >> "$OUT/host.txt" || true
 
 if [ "${SKIP_TESTS:-0}" != "1" ]; then
-  step pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider
+  step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -p no:cacheprovider
 fi
 step bench 600 python bench.py --steps 200 --warmup 20 ${BENCH_ARGS:-}
 cp "$OUT/bench.log" "$OUT/bench.json" 2>/dev/null

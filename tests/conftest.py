@@ -50,6 +50,23 @@ def O():
     return oracle
 
 
+@pytest.fixture(autouse=True)
+def _gpu_fault_attribution(request):
+    """After every GPU test: drain the device and fail THIS test if any work it enqueued faulted.
+    HIP reports faults asynchronously, so without this a fault surfaces at the next test's first
+    HIP call (round-1 r01f: hipErrorIllegalAddress at a later test's first tensor copy)."""
+    yield
+    if request.node.get_closest_marker("gpu") is None:
+        return
+    import torch
+
+    if not torch.cuda.is_available():
+        return
+    from hydra_amd import _lib
+
+    _lib.check(_lib.lib().hydra_device_check(0))
+
+
 @pytest.fixture(scope="session")
 def gpu():
     """cuda:0 with libhydra_hip.so loaded; the HIP path must be the one that runs."""

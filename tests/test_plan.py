@@ -343,3 +343,39 @@ def test_halving_doubling_plan(O, P, n):
     for r in range(P):
         assert np.array_equal(outs[r].view(np.uint32), exp[r][0].view(np.uint32)), r
         race_check(ring.plan("halving_doubling", P, r, n, 4, 0, 0)[0])
+
+
+BOUNDS_ALGOS = ["ring", "direct", "ring_old", "ring_chunked", "bcube", "halving_doubling"]
+
+
+@pytest.mark.parametrize("algo", BOUNDS_ALGOS)
+def test_every_plan_passes_the_executor_bounds_check(algo):
+    """Regression for the round-1 GPU fault hunt: hydra_plan now runs the same validate_plan the
+    RCCL executor, the simulator and the run_plan hook run before enqueueing anything (every
+    access inside n*E user bytes and plan_scratch_bytes, groups closed, waits backwards).  Sweep
+    every rank of ragged geometries, every element size and RING_OLD's small chunks (the
+    round-1 suspect); a plan that reaches outside its buffers raises here, on the CPU."""
+    sizes = [1, 2, 7, 100, 1000, 4099, 30011, 300000]
+    for P in (2, 3, 5, 8, 16):
+        for n in sizes:
+            for es in (1, 2, 4, 8):
+                for ms, ch in ((0, 0), (128, 1024), (64, 16), (1 << 20, 1 << 18)):
+                    if n * es // max(ch, 1 << 12) > 64 or (ms and n * es // ms > 256):
+                        continue  # keep plans small: the geometry, not the length, is under test
+                    for r in sorted({0, 1, P // 2, P - 1}):
+                        ops, scr = ring.plan(algo, P, r, n, es, ms, ch)
+                        for o in ops:  # belt and braces: the same bounds, restated
+                            if o["kind"] in (SEND, RECV):
+                                cap = n * es if o["buf"] == 0 else scr
+                                assert 0 <= o["off"] and o["off"] + o["bytes"] <= cap
+                            elif o["kind"] == REDUCE:
+                                assert o["off"] + o["bytes"] <= n * es
+                                assert o["src_off"] + o["bytes"] <= scr
+
+
+def test_plan_bounds_check_covers_reduce_root():
+    for P in (2, 3, 7):
+        for n in (1, 1000, 4099, 262145):
+            for root in range(P):
+                for r in range(P):
+                    ring.plan_reduce(root, P, r, n, 4, 128, 1024)
