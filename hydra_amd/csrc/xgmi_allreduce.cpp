@@ -578,6 +578,17 @@ int hydra_reduce_root_plan(int root, int P, int rank, size_t n, size_t esize, si
 }
 
 // ---- one-GPU simulation of P ranks ---------------------------------------------------------
+// Every rank's plan runs on ONE GPU with the real kernels: REDUCE/FOLD launch the gfx950 kernels,
+// a matched SEND/RECV pair is a device copy, a collective is the copies it implies.  The ranks
+// advance in lock-step (a rank stalls at a p2p group until every peer has posted its side) and
+// everything is enqueued on ONE stream in that discovery order, which is a sequentially
+// consistent execution of the schedule: a copy is enqueued only after both ranks enqueued every
+// op before their group, and a rank's later ops only after its group's copies.  No events and
+// no cross-stream waits: the simulator checks the kernels and the data movement; the plans'
+// cross-stream edges are checked by the RCCL executor (hydra_comm_run_plan) and the CPU race
+// checker (tests/test_plan.py).  (Round 1 ran 2P+1 streams with per-op events here; three
+// intermittent device faults surfaced only after syncs that had returned success -- DESIGN.md
+// 10.  One stream keeps the HIP runtime out of the picture.)
 namespace {
 int simulate_impl(int algo, int root, int op, int dtype, int flags, int P, void** bufs, size_t n,
                   size_t max_segment, size_t chunk_bytes) {
@@ -597,40 +608,31 @@ int simulate_impl(int algo, int root, int op, int dtype, int flags, int P, void*
   rc = check_geometry(algo, g);
   if (rc) return rc;
   const size_t sbytes = hydra::plan_scratch_bytes(algo, g);
+  for (int r = 0; r < P; r++)
+    if (!bufs[r]) return fail(HYDRA_ERR_INVALID, "null bucket");
 
   struct Rank {
     std::vector<hydra::PlanOp> ops;
-    std::vector<char> waited;
-    std::vector<hipEvent_t> ev;
-    hipStream_t cs = nullptr, ks = nullptr;
     char* scratch = nullptr;
     size_t pc = 0;
     bool posted = false;
     size_t group_end = 0;
     int outstanding = 0;
-    hipEvent_t start = nullptr;
-    std::vector<hipEvent_t> done;  // copy-completion events of the posted group
-    int coll_posted = 0;            // collectives posted so far (sequence number)
+    int coll_posted = 0;  // collectives posted so far (sequence number)
   };
-  int coll_done = 0;               // collectives completed (all ranks matched)
-  hipEvent_t coll_ev = nullptr;    // completion of the last completed collective
   std::vector<Rank> R(P);
-  std::vector<hipEvent_t> all_events;
-  hipStream_t fabric = nullptr;
+  for (int r = 0; r < P; r++) {  // validated before anything is allocated or enqueued
+    R[r].ops = hydra::make_plan(algo, g, r);
+    rc = validate_plan(R[r].ops, P, es, n * es, sbytes);
+    if (rc) return rc;
+  }
+  int coll_done = 0;  // collectives performed (every rank matched)
+  hipStream_t st = nullptr;
   auto cleanup = [&]() {
     (void)hipDeviceSynchronize();
-    for (auto& r : R) {
-      if (r.cs) (void)hipStreamDestroy(r.cs);
-      if (r.ks) (void)hipStreamDestroy(r.ks);
+    for (auto& r : R)
       if (r.scratch) (void)hipFree(r.scratch);
-    }
-    for (auto e : all_events) (void)hipEventDestroy(e);
-    if (fabric) (void)hipStreamDestroy(fabric);
-  };
-  auto new_event = [&](hipEvent_t* e) -> hipError_t {
-    hipError_t x = hipEventCreateWithFlags(e, hipEventDisableTiming);
-    if (x == hipSuccess) all_events.push_back(*e);
-    return x;
+    if (st) (void)hipStreamDestroy(st);
   };
 #define SIM_TRY(expr)                               \
   do {                                              \
@@ -642,31 +644,16 @@ int simulate_impl(int algo, int root, int op, int dtype, int flags, int P, void*
     }                                               \
   } while (0)
 
-  for (int r = 0; r < P; r++) {  // validated before anything is enqueued
-    R[r].ops = hydra::make_plan(algo, g, r);
-    rc = validate_plan(R[r].ops, P, es, n * es, sbytes);
-    if (rc) return rc;
-  }
   SIM_TRY(hipDeviceSynchronize());
-  SIM_TRY(hipStreamCreateWithFlags(&fabric, hipStreamNonBlocking));
-  for (int r = 0; r < P; r++) {
-    R[r].waited = waited_set(R[r].ops);
-    R[r].ev.resize(R[r].ops.size(), nullptr);
-    for (size_t i = 0; i < R[r].ops.size(); i++)
-      if (R[r].waited[i]) SIM_TRY(new_event(&R[r].ev[i]));
-    SIM_TRY(hipStreamCreateWithFlags(&R[r].cs, hipStreamNonBlocking));
-    SIM_TRY(hipStreamCreateWithFlags(&R[r].ks, hipStreamNonBlocking));
+  SIM_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  for (int r = 0; r < P; r++)
     if (sbytes) SIM_TRY(hipMalloc(&R[r].scratch, sbytes));
-  }
   struct Posted {
     int rank;
     size_t idx;
   };
   std::map<std::pair<int, int>, std::deque<Posted>> sends, recvs;  // key (src, dst)
-  auto wait_ev = [&](hipStream_t st, Rank& rk, const hydra::PlanOp& o) {
-    if (o.wait0 >= 0) (void)hipStreamWaitEvent(st, rk.ev[o.wait0], 0);
-    if (o.wait1 >= 0) (void)hipStreamWaitEvent(st, rk.ev[o.wait1], 0);
-  };
+  auto user = [&](int r) { return static_cast<char*>(bufs[r]); };
   for (;;) {
     bool progress = false, all_done = true;
     for (int r = 0; r < P; r++) {
@@ -674,47 +661,35 @@ int simulate_impl(int algo, int root, int op, int dtype, int flags, int P, void*
       while (rk.pc < rk.ops.size()) {
         const hydra::PlanOp& o = rk.ops[rk.pc];
         if (o.kind == hydra::kOpReduce || o.kind == hydra::kOpFold) {
-          wait_ev(rk.ks, rk, o);
-          SIM_TRY(launch_compute(o, op, dtype, acc32, static_cast<char*>(bufs[r]), rk.scratch,
-                                 es, rk.ks));
-          if (rk.waited[rk.pc]) SIM_TRY(hipEventRecord(rk.ev[rk.pc], rk.ks));
+          SIM_TRY(launch_compute(o, op, dtype, acc32, user(r), rk.scratch, es, st));
           rk.pc++;
           progress = true;
           continue;
         }
         if (o.kind == hydra::kOpAllToAll || o.kind == hydra::kOpAllGather) {
-          if (!rk.posted) {  // post this rank's participation
-            wait_ev(rk.cs, rk, o);
-            SIM_TRY(new_event(&rk.start));
-            SIM_TRY(hipEventRecord(rk.start, rk.cs));
+          if (!rk.posted) {  // this rank reached the collective
             rk.posted = true;
             rk.coll_posted++;
             progress = true;
           }
           bool all = true;
           for (int q = 0; q < P; q++) all = all && R[q].coll_posted == coll_done + 1;
-          if (all) {  // every rank reached it: perform the collective on the fabric stream
-            for (int q = 0; q < P; q++) SIM_TRY(hipStreamWaitEvent(fabric, R[q].start, 0));
+          if (all) {  // every rank reached it: perform it
             const int64_t B = o.bytes;
             for (int sr = 0; sr < P; sr++)
               for (int dr = 0; dr < P; dr++) {
-                char* su = static_cast<char*>(bufs[sr]);
-                char* du = static_cast<char*>(bufs[dr]);
                 if (o.kind == hydra::kOpAllToAll)
-                  SIM_TRY(hipMemcpyAsync(R[dr].scratch + o.src_off + sr * B, su + o.off + dr * B,
-                                         (size_t)B, hipMemcpyDeviceToDevice, fabric));
+                  SIM_TRY(hipMemcpyAsync(R[dr].scratch + o.src_off + sr * B,
+                                         user(sr) + o.off + dr * B, (size_t)B,
+                                         hipMemcpyDeviceToDevice, st));
                 else if (sr != dr)
-                  SIM_TRY(hipMemcpyAsync(du + o.off + sr * B, su + o.off + sr * B, (size_t)B,
-                                         hipMemcpyDeviceToDevice, fabric));
+                  SIM_TRY(hipMemcpyAsync(user(dr) + o.off + sr * B, user(sr) + o.off + sr * B,
+                                         (size_t)B, hipMemcpyDeviceToDevice, st));
               }
-            SIM_TRY(new_event(&coll_ev));
-            SIM_TRY(hipEventRecord(coll_ev, fabric));
             coll_done++;
             progress = true;
           }
-          if (rk.posted && rk.coll_posted == coll_done) {  // this rank's collective completed
-            SIM_TRY(hipStreamWaitEvent(rk.cs, coll_ev, 0));
-            if (rk.waited[rk.pc]) SIM_TRY(hipEventRecord(rk.ev[rk.pc], rk.cs));
+          if (rk.posted && rk.coll_posted == coll_done) {  // this rank's collective is done
             rk.posted = false;
             rk.pc++;
             progress = true;
@@ -725,16 +700,8 @@ int simulate_impl(int algo, int root, int op, int dtype, int flags, int P, void*
         if (!rk.posted) {  // post the whole group
           size_t gi = rk.pc;
           while (gi < rk.ops.size() && rk.ops[gi].kind != hydra::kOpGroup) gi++;
-          if (gi == rk.ops.size()) {
-            cleanup();
-            return fail(HYDRA_ERR_INVALID, "plan: unterminated group");
-          }
-          wait_ev(rk.cs, rk, rk.ops[gi]);
-          SIM_TRY(new_event(&rk.start));
-          SIM_TRY(hipEventRecord(rk.start, rk.cs));
-          rk.group_end = gi;
+          rk.group_end = gi;  // validate_plan guarantees the group is closed
           rk.outstanding = 0;
-          rk.done.clear();
           for (size_t j = rk.pc; j < gi; j++) {
             const hydra::PlanOp& p = rk.ops[j];
             if (p.kind == hydra::kOpSend) sends[{r, p.peer}].push_back({r, j});
@@ -743,8 +710,7 @@ int simulate_impl(int algo, int root, int op, int dtype, int flags, int P, void*
           }
           rk.posted = true;
           progress = true;
-          // match everything now matchable
-          for (auto& kv : sends) {
+          for (auto& kv : sends) {  // match everything now matchable, FIFO per (src, dst)
             auto& sq = kv.second;
             auto& rq = recvs[kv.first];
             while (!sq.empty() && !rq.empty()) {
@@ -759,26 +725,16 @@ int simulate_impl(int algo, int root, int op, int dtype, int flags, int P, void*
                 cleanup();
                 return fail(HYDRA_ERR_INVALID, "plan: send/recv size mismatch");
               }
-              const char* src = (so.buf == hydra::kBufUser ? static_cast<char*>(bufs[s.rank])
-                                                           : S.scratch) + so.off;
-              char* dst = (ro.buf == hydra::kBufUser ? static_cast<char*>(bufs[d.rank])
-                                                     : D.scratch) + ro.off;
-              SIM_TRY(hipStreamWaitEvent(fabric, S.start, 0));
-              SIM_TRY(hipStreamWaitEvent(fabric, D.start, 0));
-              SIM_TRY(hipMemcpyAsync(dst, src, (size_t)so.bytes, hipMemcpyDeviceToDevice, fabric));
-              hipEvent_t ce;
-              SIM_TRY(new_event(&ce));
-              SIM_TRY(hipEventRecord(ce, fabric));
-              S.done.push_back(ce);
-              D.done.push_back(ce);
+              const char* src = (so.buf == hydra::kBufUser ? user(s.rank) : S.scratch) + so.off;
+              char* dst = (ro.buf == hydra::kBufUser ? user(d.rank) : D.scratch) + ro.off;
+              if (so.bytes)
+                SIM_TRY(hipMemcpyAsync(dst, src, (size_t)so.bytes, hipMemcpyDeviceToDevice, st));
               S.outstanding--;
               D.outstanding--;
             }
           }
         }
         if (rk.outstanding == 0) {  // group complete
-          for (auto e : rk.done) SIM_TRY(hipStreamWaitEvent(rk.cs, e, 0));
-          if (rk.waited[rk.group_end]) SIM_TRY(hipEventRecord(rk.ev[rk.group_end], rk.cs));
           rk.pc = rk.group_end + 1;
           rk.posted = false;
           progress = true;
@@ -794,7 +750,8 @@ int simulate_impl(int algo, int root, int op, int dtype, int flags, int P, void*
       return fail(HYDRA_ERR_INVALID, "plan deadlock in simulation");
     }
   }
-  SIM_TRY(hipDeviceSynchronize());
+  SIM_TRY(hipStreamSynchronize(st));
+  SIM_TRY(hipGetLastError());
   cleanup();
 #undef SIM_TRY
   return ok();

@@ -35,8 +35,12 @@ def build(force: bool = False) -> None:
     the reference core.  Prebuilt files travel to the GPU box with the repo snapshot."""
     if force or not os.path.exists(LIBORACLE):
         subprocess.check_call(["make", "-s", "-C", HERE, "oracle"])
-    if os.path.isdir("/root/reference/gloo") and (force or not os.path.exists(LIBREF)):
-        subprocess.check_call(["make", "-s", "-j8", "-C", HERE, "ref"])
+    if os.path.isdir("/root/reference/gloo"):
+        if force or not os.path.exists(LIBREF):
+            subprocess.check_call(["make", "-s", "-j8", "-C", HERE, "ref"])
+        # the drop-in harness links libhydra_hip.so too: make rebuilds it when either changed
+        if os.path.exists(os.path.join(os.path.dirname(HERE), "hydra_amd", "libhydra_hip.so")):
+            subprocess.check_call(["make", "-s", "-C", HERE, "dropin"])
 
 
 def _load(path):

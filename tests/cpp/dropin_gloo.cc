@@ -1,0 +1,243 @@
+// tests/cpp/dropin_gloo.cc -- TEST HARNESS: the drop-in proven inside the reference itself.
+//
+// Runs the REFERENCE's own collectives -- gloo::allreduce's ring (gloo/gloo/allreduce.cc:147-422)
+// and the old-style gloo::AllreduceRing<T> (gloo/gloo/allreduce_ring.h:20-125) -- compiled from
+// /root/reference by oracle/Makefile into oracle/_ref/libgloo_ref.so, on thread-ranks with an
+// in-process HashStore and a loopback TCP device (the reference's own test setup,
+// gloo/gloo/test/base_test.h:73-156).  Each case runs twice on identical inputs:
+//   reducer "gloo"   the reference's gloo::sum<T> / ReductionFunction<T>::sum (math.h:15-23)
+//   reducer "hydra"  libhydra_hip.so through include/hydra/gloo_reduce.h, plugged in exactly
+//                    where a user would: AllreduceOptions::setReduceFunction(Func)
+//                    (allreduce.h:36,179-181; called at allreduce.cc:301-305) and the
+//                    ReductionFunction<T>* argument of AllreduceRing<T> (algorithm.h:59-96)
+// and reports whether every rank's bytes are identical, plus per-iteration timings of both
+// (rank 0 wall time around each collective, ranks released together, as runner.cc:683-702).
+//
+// Built by oracle/Makefile (it needs the reference headers, present only in the build
+// container); the binary travels to the GPU box, where tests/test_gpu_dropin.py runs it.
+//
+// usage: dropin_gloo <new_ring|old_ring> <P> <n> <f32|i32> [timed_iters] [max_segment]
+// prints one JSON object on stdout; exit 0 iff both runs finished (equality is in the JSON).
+
+#include <algorithm>
+#include <chrono>
+#include <condition_variable>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <random>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "gloo/algorithm.h"
+#include "gloo/allreduce.h"
+#include "gloo/allreduce_ring.h"
+#include "gloo/math.h"
+#include "gloo/rendezvous/context.h"
+#include "gloo/rendezvous/hash_store.h"
+#include "gloo/transport/tcp/device.h"
+
+#include "hydra/gloo_reduce.h"
+
+namespace {
+
+struct Barrier {  // reusable: all P threads leave wait() together
+  explicit Barrier(int n) : n_(n) {}
+  void wait() {
+    std::unique_lock<std::mutex> l(mu_);
+    const long gen = gen_;
+    if (++count_ == n_) {
+      count_ = 0;
+      gen_++;
+      cv_.notify_all();
+    } else {
+      cv_.wait(l, [&] { return gen_ != gen; });
+    }
+  }
+  int n_, count_ = 0;
+  long gen_ = 0;
+  std::mutex mu_;
+  std::condition_variable cv_;
+};
+
+template <typename T>
+std::vector<T> make_input(int P, int r, size_t n);
+
+// fold-order-sensitive fp32: uniform [-1, 1) scaled by 2^(3r mod 17), so a different
+// association changes the low bits (the oracle's stress pattern)
+template <>
+std::vector<float> make_input<float>(int P, int r, size_t n) {
+  std::mt19937 g(1234u + 97u * (unsigned)P + (unsigned)r);
+  std::uniform_real_distribution<float> u(-1.0f, 1.0f);
+  const float scale = std::ldexp(1.0f, (3 * r) % 17);
+  std::vector<float> x(n);
+  for (auto& v : x) v = u(g) * scale;
+  return x;
+}
+
+template <>
+std::vector<int32_t> make_input<int32_t>(int P, int r, size_t n) {
+  std::vector<int32_t> x(n);
+  for (size_t i = 0; i < n; i++) x[i] = (int32_t)((i * 2654435761u + (unsigned)r * 40503u) & 0xfffff) - 0x80000;
+  (void)P;
+  return x;
+}
+
+struct RunOut {
+  std::vector<std::vector<uint8_t>> bytes;  // [rank] output after the first collective
+  std::vector<double> iter_ms;              // rank 0, timed iterations
+  std::string error;
+};
+
+template <typename T>
+RunOut run_case(const std::string& mode, int P, size_t n, bool hydra, int iters, size_t ms) {
+  RunOut out;
+  out.bytes.resize(P);
+  gloo::rendezvous::HashStore store;
+  gloo::transport::tcp::attr attr;
+  attr.hostname = "127.0.0.1";
+  auto dev = gloo::transport::tcp::CreateDevice(attr);
+  Barrier bar(P);
+  std::mutex mu;
+  std::vector<std::thread> th;
+  for (int r = 0; r < P; r++) {
+    th.emplace_back([&, r]() {
+      try {
+        auto ctx = std::make_shared<gloo::rendezvous::Context>(r, P);
+        ctx->connectFullMesh(store, dev);
+        std::vector<T> x = make_input<T>(P, r, n);
+        std::function<void()> once;
+        std::unique_ptr<gloo::AllreduceRing<T>> old;
+        if (mode == "new_ring") {
+          once = [&]() {
+            gloo::AllreduceOptions o(ctx);
+            o.setAlgorithm(gloo::AllreduceOptions::Algorithm::RING);
+            o.setOutput(x.data(), n);
+            if (ms) o.setMaxSegmentSize(ms);
+            if (hydra)  // the drop-in: the gfx950 chunk-sum behind AllreduceOptions::Func
+              o.setReduceFunction(hydra::gloo_compat::hostSum<T>());
+            else
+              o.setReduceFunction(
+                  gloo::AllreduceOptions::Func(static_cast<void (*)(void*, const void*, const void*, size_t)>(&gloo::sum<T>)));
+            gloo::allreduce(o);
+          };
+        } else {
+          const gloo::ReductionFunction<T>* fn =
+              hydra ? hydra::gloo_compat::gpuReductionFunction<gloo::ReductionFunction<T>, T>(gloo::SUM)
+                    : gloo::ReductionFunction<T>::sum;
+          std::vector<T*> ptrs{x.data()};
+          old.reset(new gloo::AllreduceRing<T>(ctx, ptrs, (int)n, fn));
+          once = [&]() { old->run(); };
+        }
+        bar.wait();
+        once();
+        {
+          std::lock_guard<std::mutex> g(mu);
+          out.bytes[r].assign(reinterpret_cast<uint8_t*>(x.data()),
+                              reinterpret_cast<uint8_t*>(x.data()) + n * sizeof(T));
+        }
+        for (int it = 0; it < iters + 1; it++) {  // one untimed warm-up, then `iters`
+          bar.wait();
+          const auto t0 = std::chrono::steady_clock::now();
+          once();
+          const double msec =
+              std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+          if (r == 0 && it > 0) out.iter_ms.push_back(msec);
+        }
+        bar.wait();  // nobody closes its pairs while a peer still runs (base_test.h:142-155)
+        old.reset();
+      } catch (const std::exception& e) {
+        std::lock_guard<std::mutex> g(mu);
+        if (out.error.empty()) out.error = e.what();
+        // a failed rank cannot rejoin the barrier protocol: abort the process, loudly
+        std::fprintf(stderr, "rank %d: %s\n", r, e.what());
+        std::fflush(stderr);
+        std::_Exit(2);
+      }
+    });
+  }
+  for (auto& t : th) t.join();
+  return out;
+}
+
+uint64_t fnv1a(const std::vector<std::vector<uint8_t>>& v) {
+  uint64_t h = 1469598103934665603ull;
+  for (const auto& b : v)
+    for (uint8_t c : b) h = (h ^ c) * 1099511628211ull;
+  return h;
+}
+
+double pct(std::vector<double> v, double p) {
+  if (v.empty()) return 0;
+  std::sort(v.begin(), v.end());
+  return v[std::min(v.size() - 1, (size_t)(p / 100.0 * (v.size() - 1) + 0.5))];
+}
+
+template <typename T>
+int run_all(const std::string& mode, int P, size_t n, int iters, size_t ms, const char* dt) {
+  // HYDRA_DROPIN_REF_ONLY=1 (CPU self-test of the harness): the second run is the reference too
+  const char* ro = std::getenv("HYDRA_DROPIN_REF_ONLY");
+  const bool ref_only = ro && ro[0] == '1';
+  RunOut ref = run_case<T>(mode, P, n, false, iters, ms);
+  RunOut hyd = run_case<T>(mode, P, n, !ref_only, iters, ms);
+  size_t mism = 0, first = (size_t)-1;
+  int first_rank = -1;
+  for (int r = 0; r < P; r++)
+    for (size_t i = 0; i < ref.bytes[r].size(); i++)
+      if (ref.bytes[r][i] != hyd.bytes[r][i]) {
+        if (!mism) first = i, first_rank = r;
+        mism++;
+      }
+  bool ranks_equal = true;
+  for (int r = 1; r < P; r++) ranks_equal = ranks_equal && ref.bytes[r] == ref.bytes[0];
+  auto avg = [](const std::vector<double>& v) {
+    double s = 0;
+    for (double x : v) s += x;
+    return v.empty() ? 0.0 : s / v.size();
+  };
+  const double bytes = (double)n * sizeof(T);
+  auto gib = [&](double msec) { return msec > 0 ? bytes / (msec * 1e-3) / (1024.0 * 1024 * 1024) : 0; };
+  std::printf(
+      "{\"mode\": \"%s\", \"P\": %d, \"n\": %zu, \"dtype\": \"%s\", \"max_segment\": %zu, "
+      "\"mismatched_bytes\": %zu, \"first_mismatch\": [%d, %lld], \"ref_ranks_equal\": %s, "
+      "\"fnv_ref\": \"%016llx\", \"fnv_hydra\": \"%016llx\", \"iters\": %d, "
+      "\"ref_ms\": {\"p50\": %.4f, \"p99\": %.4f, \"avg\": %.4f, \"GiBps_avg\": %.4f}, "
+      "\"hydra_ms\": {\"p50\": %.4f, \"p99\": %.4f, \"avg\": %.4f, \"GiBps_avg\": %.4f}}\n",
+      mode.c_str(), P, n, dt, ms, mism, first_rank, mism ? (long long)first : -1LL,
+      ranks_equal ? "true" : "false", (unsigned long long)fnv1a(ref.bytes),
+      (unsigned long long)fnv1a(hyd.bytes), iters, pct(ref.iter_ms, 50), pct(ref.iter_ms, 99),
+      avg(ref.iter_ms), gib(avg(ref.iter_ms)), pct(hyd.iter_ms, 50), pct(hyd.iter_ms, 99),
+      avg(hyd.iter_ms), gib(avg(hyd.iter_ms)));
+  return 0;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  if (argc < 5) {
+    std::fprintf(stderr, "usage: %s <new_ring|old_ring> <P> <n> <f32|i32> [iters] [max_segment]\n",
+                 argv[0]);
+    return 64;
+  }
+  const std::string mode = argv[1], dt = argv[4];
+  const int P = std::atoi(argv[2]);
+  const size_t n = std::strtoull(argv[3], nullptr, 10);
+  const int iters = argc > 5 ? std::atoi(argv[5]) : 0;
+  const size_t ms = argc > 6 ? std::strtoull(argv[6], nullptr, 10) : 0;
+  if ((mode != "new_ring" && mode != "old_ring") || P < 1 || P > 16 || n < 1 ||
+      (dt != "f32" && dt != "i32")) {
+    std::fprintf(stderr, "bad arguments\n");
+    return 64;
+  }
+  if (mode == "old_ring" && ms) {
+    std::fprintf(stderr, "max_segment applies to new_ring only\n");
+    return 64;
+  }
+  return dt == "f32" ? run_all<float>(mode, P, n, iters, ms, "f32")
+                     : run_all<int32_t>(mode, P, n, iters, ms, "i32");
+}

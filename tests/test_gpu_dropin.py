@@ -1,0 +1,68 @@
+"""The drop-in proven inside the reference itself (tests/cpp/dropin_gloo.cc): the REFERENCE's own
+gloo::allreduce ring (allreduce.cc:147-422) and old-style gloo::AllreduceRing<T>
+(allreduce_ring.h:20-125), compiled from its sources into oracle/_ref, run twice on identical
+inputs -- once with gloo::sum<T> / ReductionFunction<T>::sum, once with libhydra_hip.so's gfx950
+chunk-sum plugged into AllreduceOptions::setReduceFunction (allreduce.h:36,179-181) and into
+AllreduceRing<T>'s ReductionFunction<T>* (algorithm.h:59-96) through include/hydra/gloo_reduce.h.
+Bar: every byte of every rank identical (fp32 on fold-order-sensitive inputs, int32).
+
+The new-style ring's scratch is the reference's own pageable `new uint8_t[]` (allreduce.cc:225),
+so the plug-in is the host-buffer Func (hostSum: staged H2D -> kernel -> D2H); a device-buffer
+Func (deviceSum) has no reference caller that hands it device memory -- the CUDA-workspace
+classes that would are CUDA sources, unbuildable here."""
+import json
+import os
+import subprocess
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EXE = os.path.join(ROOT, "tests", "cpp", "dropin_gloo")
+
+
+def dropin(mode, P, n, dt="f32", iters=0, ms=0, timeout=240):
+    assert os.path.exists(EXE), "built with the reference by oracle/Makefile (build())"
+    args = [EXE, mode, str(P), str(n), dt, str(iters)] + ([str(ms)] if ms else [])
+    r = subprocess.run(args, capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, r.stdout + r.stderr
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+NEW_CASES = [(P, n, ms) for P in (2, 3, 4, 8) for (n, ms) in
+             [(1, 0), (100, 128), (4099, 128), (262145, 0), (1 << 20, 0)]] + \
+            [(2, 4 << 20, 0), (4, 4 << 20, 0), (8, 4 << 20, 0), (3, 3000001, 0)]
+
+
+@pytest.mark.parametrize("P,n,ms", NEW_CASES)
+def test_reference_allreduce_ring_with_hydra_func(gpu, P, n, ms):
+    j = dropin("new_ring", P, n, ms=ms)
+    assert j["mismatched_bytes"] == 0, j
+    assert j["fnv_ref"] == j["fnv_hydra"]
+    assert j["ref_ranks_equal"]  # the reference ring leaves every rank with the same bits
+
+
+@pytest.mark.parametrize("P,n", [(2, 100003), (3, 1 << 20), (8, 262147)])
+def test_reference_allreduce_ring_with_hydra_func_int32(gpu, P, n):
+    j = dropin("new_ring", P, n, dt="i32")
+    assert j["mismatched_bytes"] == 0, j
+
+
+@pytest.mark.parametrize("P,n,dt", [(2, 1, "f32"), (3, 100, "f32"), (4, 4099, "f32"),
+                                    (8, 1000, "f32"), (5, 1 << 20, "f32"), (3, 4099, "i32"),
+                                    (8, 262147, "i32")])
+def test_reference_allreduce_ring_old_with_hydra_reduction_function(gpu, P, n, dt):
+    """old-style AllreduceRing<T>: every rank folds in its own order (ranks may differ in the
+    last bits), so the bar is rank-by-rank identity with the reference's own run."""
+    j = dropin("old_ring", P, n, dt=dt)
+    assert j["mismatched_bytes"] == 0, j
+
+
+@pytest.mark.parametrize("n", [16 << 20, 64 << 20])
+def test_config1_full_size_inside_the_reference(gpu, n):
+    """BASELINE config 1 at its top sizes (new_allreduce_ring, fp32, 2 ranks, loopback TCP):
+    the reference's ring with the hydra Func equals the reference's ring with gloo::sum<float>
+    byte for byte at 16 Mi and 64 Mi elements (the published row is README.md:86)."""
+    j = dropin("new_ring", 2, n, iters=1, timeout=600)
+    assert j["mismatched_bytes"] == 0, j

@@ -372,3 +372,29 @@ def test_hip_allreduce_bcube(gpu, O, workspace, P, nptr, n, dt):
             for i in range(nptr):
                 got = ts[r][i].cpu().numpy()
                 assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), (r, i)
+
+
+@pytest.mark.parametrize("n", [16 << 20, 64 << 20])
+def test_configs_1_and_3_full_size_gpu_reducer(gpu, O, n):
+    """BASELINE configs 1 and 3 at their top sizes, 2 ranks on loopback TCP with every segment
+    reduced on the MI355X: the host runtime's ring (new_allreduce_ring) and two-rail split
+    (bew_allreduce_a, calculateElements_AA) are bit-exact vs the oracle ring, full output.
+    (runner.cc:338-362 sweeps up to 2^26; the published rows are README.md:86,123.)"""
+    P = 2
+    xs = [synth.stress_f32(P, r, n) for r in range(P)]
+    exp = O.ring_result(xs)
+    outs = [[x.copy()] for x in xs]
+    host.allreduce_threads(outs, None)  # config 1
+    for r in range(P):
+        assert np.array_equal(outs[r][0].view(np.uint32), exp.view(np.uint32)), r
+    del outs
+    aout = [np.zeros(n, np.float32) for _ in range(P)]
+    host.apipe_threads(xs, aout)  # config 3
+    e1, e2 = O.split_aa(P, n)
+    exp3 = np.empty(n, np.float32)
+    if e1:
+        exp3[:e1] = O.ring_result([x[:e1].copy() for x in xs])
+    if e2:
+        exp3[e1:] = O.ring_result([x[e1:].copy() for x in xs])
+    for r in range(P):
+        assert np.array_equal(aout[r].view(np.uint32), exp3.view(np.uint32)), r
