@@ -5,7 +5,9 @@ Metric (BASELINE.json): chunk-sum GB/s (fp32) vs HBM peak; ring-allreduce GB/s a
 
   N = 1  (BASELINE config 2): one step = one device-resident, in-place fp32 chunk-sum
          c = a + b over 64 Mi elements (gloo::sum<float>, math.h:15-23, in the ring's c == a
-         form).  value = 12 B/element x elements x steps / wall time of the timed region.
+         form), HBM-resident: launch k works on buffer pair k mod 4 (2 GiB cycled, 8x the
+         Infinity Cache).  value = 12 B/element x elements x steps / wall time of the timed
+         region; roofline.mall_assisted reports one pair back to back beside it.
          --sweep adds config 2's 4 Ki..64 Mi size sweep to the line.
   N > 1  (BASELINE config 4): one step = one allreduce of a 64 Mi-element fp32 bucket per rank
          over xGMI in the reference's block ownership and fold order -- the fastest bit-exact
@@ -68,56 +70,88 @@ def dist_env():
 
 
 # ------------------------------------------------------------------------------- N = 1
-def time_chunk_sum(torch, L, dev, n, code, steps, warmup, variant=None, cold_reps=0):
-    """Returns (wall seconds for `steps` launches, average launch ms from HIP events over the
-    timed region, per-launch event ms (each launch bracketed alone), cold-cache ms)."""
+ROTATE = 4  # buffer pairs the headline cycles through: 4 x 512 MiB >> the 256 MiB Infinity Cache
+
+
+def kernel_src_hash():
+    """sha256 of the chunk-sum kernel's sources: ties a committed PMC profile to the kernel it
+    measured (roofline.traffic is reported only while they match)."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for f in ("reduce_kernels.hip", "reduce_ops.h", "reduce_kernels.h"):
+        with open(os.path.join(ROOT, "hydra_amd", "csrc", f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()
+
+
+def make_pairs(torch, dev, n, code, count):
     from hydra_amd import _lib
     from hydra_amd import synth
 
-    if code == _lib.FLOAT32:
-        a = torch.from_numpy(synth.bew_inputs(0, n)).to(dev)
-        b = torch.from_numpy(synth.uniform_f32(n, 42)).to(dev)
-    else:
-        a = torch.from_numpy(synth.int32_bucket(8, 0, n)).to(dev)
-        b = torch.from_numpy(synth.int32_bucket(8, 1, n)).to(dev)
+    pairs = []
+    for i in range(count):
+        if code == _lib.FLOAT32:
+            a = torch.from_numpy(synth.bew_inputs(i, n)).to(dev)
+            b = torch.from_numpy(synth.uniform_f32(n, 42 + i)).to(dev)
+        else:
+            a = torch.from_numpy(synth.int32_bucket(8, 2 * i, n)).to(dev)
+            b = torch.from_numpy(synth.int32_bucket(8, 2 * i + 1, n)).to(dev)
+        pairs.append((a, b))
+    return pairs
+
+
+def time_chunk_sum(torch, L, dev, pairs, code, steps, warmup, per_launch=0, cold_reps=0,
+                   variant=None):
+    """Launch k of every leg runs in place on pairs[k % len(pairs)].  Returns (wall seconds for
+    the `steps` launches of the timed region, average launch ms = HIP-event span over that region
+    / steps, per-launch event ms (each launch bracketed alone, `per_launch` of them), cold ms
+    (each launch after a 1 GiB fill, `cold_reps` of them))."""
+    from hydra_amd import _lib
+
+    n = pairs[0][0].numel()
     s = torch.cuda.current_stream(dev)
     sp = s.cuda_stream
-    pa, pb = a.data_ptr(), b.data_ptr()
+    ptrs = [(a.data_ptr(), b.data_ptr()) for a, b in pairs]
+    R = len(ptrs)
+
+    def launch(k):
+        pa, pb = ptrs[k % R]
+        _lib.check(L.hydra_chunk_sum(code, pa, pa, pb, n, sp))
+
     prev = L.hydra_set_variant(variant) if variant is not None else None
     try:
-        for _ in range(warmup):
-            _lib.check(L.hydra_chunk_sum(code, pa, pa, pb, n, sp))
+        for k in range(warmup):
+            launch(k)
         torch.cuda.synchronize(dev)
         # timed region: exactly `steps` launches, synchronised on both sides, bracketed by HIP
         # events on the launch stream (average launch duration = event span / steps)
         r0, r1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t0 = time.perf_counter()
         r0.record(s)
-        for _ in range(steps):
-            _lib.check(L.hydra_chunk_sum(code, pa, pa, pb, n, sp))
+        for k in range(steps):
+            launch(k)
         r1.record(s)
         torch.cuda.synchronize(dev)
         wall = time.perf_counter() - t0
         region_ms = r0.elapsed_time(r1) / steps
-        # per-launch device time with HIP events recorded on the launch stream
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-              for _ in range(steps)]
-        for e0, e1 in ev:
+              for _ in range(per_launch)]
+        for k, (e0, e1) in enumerate(ev):
             e0.record(s)
-            _lib.check(L.hydra_chunk_sum(code, pa, pa, pb, n, sp))
+            launch(k)
             e1.record(s)
         torch.cuda.synchronize(dev)
         ms = [e0.elapsed_time(e1) for e0, e1 in ev]
-        # cold: evict the 256 MiB Infinity Cache (1 GiB fill) before each timed launch
         cold = []
         if cold_reps:
             flush = torch.empty(1 << 28, dtype=torch.float32, device=dev)
             evc = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                    for _ in range(cold_reps)]
-            for e0, e1 in evc:
+            for k, (e0, e1) in enumerate(evc):
                 flush.fill_(1.0)
                 e0.record(s)
-                _lib.check(L.hydra_chunk_sum(code, pa, pa, pb, n, sp))
+                launch(k)
                 e1.record(s)
             torch.cuda.synchronize(dev)
             cold = [e0.elapsed_time(e1) for e0, e1 in evc]
@@ -125,48 +159,55 @@ def time_chunk_sum(torch, L, dev, n, code, steps, warmup, variant=None, cold_rep
     finally:
         if prev is not None:
             L.hydra_set_variant(prev)
-    del a, b
     return wall, region_ms, ms, cold
 
 
 def pmc_traffic():
     """HBM bytes per launch of the 64 Mi chunk-sum from the committed rocprofv3 PMC summary
-    (profiles/pmc_chunk_sum.json, written by scripts/pmc_summary.py from scripts/gpu_check.sh's
-    --pmc passes: FETCH_SIZE x2 gfx950 correction + WRITE_SIZE, MI355X_MICROARCH.md §HBM).
-    None if absent."""
+    (profiles/pmc_chunk_sum.json, written by scripts/pmc_summary.py from separate --pmc
+    FETCH_SIZE / WRITE_SIZE passes over this command: FETCH_SIZE x2 gfx950 correction +
+    WRITE_SIZE, MI355X_MICROARCH.md §HBM).  Returned only while the profile's kernel-source hash
+    equals the current sources, so a kernel change cannot inherit a stale figure."""
     p = os.path.join(ROOT, "profiles", "pmc_chunk_sum.json")
+    info = {"file": "profiles/pmc_chunk_sum.json"}
     if not os.path.exists(p):
-        return None
+        return None, dict(info, status="absent")
     try:
         with open(p) as f:
             d = json.load(f)
-        return d.get("hbm_bytes_per_launch")
-    except Exception:
-        return None
+    except Exception as e:
+        return None, dict(info, status=f"unreadable: {e}")
+    cur = kernel_src_hash()
+    info.update(round=d.get("round"), kernel_src_sha256=d.get("kernel_src_sha256"),
+                mode=d.get("mode"))
+    if d.get("kernel_src_sha256") != cur:
+        return None, dict(info, status="stale: profiled kernel sources differ from these")
+    return d.get("hbm_bytes_per_launch"), dict(info, status="matches these kernel sources")
 
 
-def cpu_baseline(n_total, seconds):
+def cpu_baseline(n, seconds):
     """The reference's own gloo::sum<float> (oracle/_ref, compiled from /root/reference) timed
-    single-threaded on this host; falls back to the C restatement (oracle/liboracle.so)."""
+    single-threaded on this host at the headline's size; falls back to the C restatement
+    (oracle/liboracle.so)."""
     from oracle import oracle as O
 
-    sample_n = 16 << 20  # bounded sample: 16 Mi fp32 in place (192 MB of traffic per call)
-    a = np.arange(sample_n, dtype=np.float32)
-    b = np.ones(sample_n, dtype=np.float32)
+    a = np.arange(n, dtype=np.float32)
+    b = np.ones(n, dtype=np.float32)
     kind = "reference" if O.ref_available() else "port"
-    # calibrate, then run ~`seconds` of work
+    # calibrate, then run ~`seconds` of work (3 repetitions, best mean)
     if kind == "reference":
-        per = O.ref_time_sum(6, a, a, b, 2, 1)
+        per = O.ref_time_sum(6, a, a, b, 1, 1)
         iters = max(1, int(seconds / max(per, 1e-6) / 3))
         per = O.ref_time_sum(6, a, a, b, iters, 3)
     else:
         t0 = time.perf_counter()
         k = 0
         while time.perf_counter() - t0 < seconds:
-            O.orc().orc_op(0, 6, a.ctypes.data, a.ctypes.data, b.ctypes.data, sample_n)
+            O.orc().orc_op(0, 6, a.ctypes.data, a.ctypes.data, b.ctypes.data, n)
             k += 1
+        iters = k
         per = (time.perf_counter() - t0) / k
-    gbs = 12.0 * sample_n / per / 1e9
+    gbs = 12.0 * n / per / 1e9
     model = None
     try:
         with open("/proc/cpuinfo") as f:
@@ -176,9 +217,10 @@ def cpu_baseline(n_total, seconds):
         pass
     return {"value": round(gbs, 3), "unit": "GB/s", "cores": 1, "kind": kind,
             "host_cpu": model, "host_logical_cpus": os.cpu_count(),
-            "sample": f"gloo::sum<float> in place over 16 Mi fp32 (12 B/element), "
-                      f"single thread, ~{seconds:.0f} s of repetitions, best-of-3 mean",
-            "per_call_ms_at_64Mi": round(per * 4 * 1e3, 2)}
+            "sample": f"gloo::sum<float> in place over {n} fp32 elements (the headline's size, "
+                      f"12 B/element), single thread, {iters} calls x 3 repetitions "
+                      f"(~{seconds:.0f} s), best-of-3 mean",
+            "per_call_ms": round(per * 1e3, 3)}
 
 
 def run_single(args):
@@ -191,13 +233,18 @@ def run_single(args):
     torch.cuda.set_device(dev)
     code = _lib.FLOAT32 if args.dtype == "f32" else _lib.INT32
     n = args.elements
-    wall, region_ms, ms, cold = time_chunk_sum(torch, L, dev, n, code, args.steps, args.warmup,
-                                               cold_reps=20)
     algo_bytes = 12.0 * n
+    pairs = make_pairs(torch, dev, n, code, ROTATE)
+    # headline: HBM-resident launches, each on the next of ROTATE buffer pairs, so no launch
+    # finds its operands in the 256 MiB Infinity Cache (2 GiB cycled between reuses)
+    wall, region_ms, ms, cold = time_chunk_sum(torch, L, dev, pairs, code, args.steps,
+                                               args.warmup, per_launch=min(100, args.steps),
+                                               cold_reps=20)
+    # context: one pair back to back -- part of its 512 MiB stays in the Infinity Cache
+    mwall, mregion, _, _ = time_chunk_sum(torch, L, dev, pairs[:1], code, 20, 2)
     value = algo_bytes * args.steps / wall / 1e9
-    avg_ms = region_ms
-    achieved = algo_bytes / (avg_ms * 1e-3) / 1e9
-    traffic = pmc_traffic()
+    achieved = algo_bytes / (region_ms * 1e-3) / 1e9
+    traffic, traffic_src = pmc_traffic()
     out = {
         "metric": "chunk-sum GB/s (fp32) vs HBM peak; ring-allreduce GB/s at 1/2/4/8 GPU",
         "value": round(value, 2), "unit": "GB/s", "n_gpus": 1, "steps": args.steps,
@@ -205,28 +252,42 @@ def run_single(args):
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "f32" if code == _lib.FLOAT32 else "i32", "data": "synthetic",
         "config": {"workload": "device-resident in-place chunk sum c=a+b (gloo::sum<float> "
-                               "ring form), BASELINE config 2", "elements": n,
-                   "bytes_per_element": 12, "parallelism": "single GPU"},
+                               "ring form), BASELINE config 2, HBM-resident: launch k runs on "
+                               f"buffer pair k mod {ROTATE} ({ROTATE} x 512 MiB cycled)",
+                   "elements": n, "bytes_per_element": 12, "buffer_pairs": ROTATE,
+                   "parallelism": "single GPU"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": traffic, "kernel_ms_avg": round(avg_ms, 5),
-                     "per_launch_event_ms_min": round(float(np.min(ms)), 5),
+                     "traffic": traffic, "traffic_source": traffic_src,
+                     "kernel_ms_avg": round(region_ms, 5),
                      "timing": "HIP events on the launch stream over the timed region "
-                               "(event span / steps)",
+                               "(event span / steps), HBM-resident rotation",
                      "per_launch_event_ms_median": round(float(np.median(ms)), 5),
+                     "frac_of_measured_copy_ceiling": round(achieved / 6290.0, 4),
+                     "copy_ceiling_note": "6.29 TB/s = best float4 HBM copy measured on MI355X "
+                                          "(MI355X_MICROARCH.md); spec peak 8 TB/s",
                      "cold_achieved": round(algo_bytes / (float(np.median(cold)) * 1e-3) / 1e9, 1),
                      "cold_note": "median over 20 launches, each after a 1 GiB fill that "
-                                  "evicts the 256 MiB Infinity Cache"},
+                                  "evicts the 256 MiB Infinity Cache",
+                     "mall_assisted": {
+                         "achieved": round(algo_bytes / (mregion * 1e-3) / 1e9, 1),
+                         "frac": round(algo_bytes / (mregion * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                         "kernel_ms_avg": round(mregion, 5),
+                         "note": "context only: ONE buffer pair launched back to back (20 "
+                                 "launches); part of its 512 MiB working set is served by the "
+                                 "256 MiB Infinity Cache, so this is not an HBM rate"}},
     }
+    del pairs
     if args.sweep:
         # config 2's size range: back-to-back launches, wall time per launch (what a caller
-        # issuing one segment after another sees: dispatch-bound below ~1 Mi elements; per-launch
-        # HIP events would bottom out at their own ~6 us floor instead)
+        # issuing one segment after another sees: dispatch-bound below ~1 Mi elements)
         sweep = []
         for k in range(12, 27, 2):
             nn = 1 << k
             reps = 400 if nn <= (1 << 22) else 100
-            w, _, _, _ = time_chunk_sum(torch, L, dev, nn, code, reps, 20)
+            pp = make_pairs(torch, dev, nn, code, 1)
+            w, _, _, _ = time_chunk_sum(torch, L, dev, pp, code, reps, 20)
+            del pp
             us = w / reps * 1e6
             sweep.append({"elements": nn, "us_per_launch": round(us, 2),
                           "GBps": round(12.0 * nn / (us * 1e-6) / 1e9, 1)})

@@ -9,6 +9,7 @@ profiles/pmc_chunk_sum.json (per-launch HBM bytes, read by bench.py as roofline.
 HBM bytes = (2 x FETCH_SIZE + WRITE_SIZE) x 1024: rocprofv3 reports KiB, and on gfx950 FETCH_SIZE
 counts exactly half of a wide coalesced streaming read (MI355X_MICROARCH.md §HBM)."""
 import csv
+import hashlib
 import json
 import os
 import shutil
@@ -20,6 +21,10 @@ root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 prof = os.path.join(root, "profiles")
 os.makedirs(prof, exist_ok=True)
 HOT = "k_reduce<float, 0"
+h = hashlib.sha256()  # the same hash bench.py's kernel_src_hash() computes
+for f in ("reduce_kernels.hip", "reduce_ops.h", "reduce_kernels.h"):
+    h.update(open(os.path.join(root, "hydra_amd", "csrc", f), "rb").read())
+src_hash = h.hexdigest()
 
 shutil.copy(os.path.join(src, "prof_kt", "run_kernel_stats.csv"),
             os.path.join(prof, f"{tag}_kernel_stats.csv"))
@@ -51,6 +56,8 @@ out = {"kernel": hot[0]["Name"] if hot else None, "round": tag,
        "fetch_size_kib_median": fm, "write_size_kib_median": wm,
        "hbm_bytes_per_launch": hbm, "traffic_over_algorithmic": hbm / (12 * (64 << 20)),
        "kernel_trace_avg_ns": avg_ns, "dispatches": len(fetch),
-       "correction": "FETCH_SIZE x2 (gfx950 wide-stream read counting), KiB x1024"}
+       "correction": "FETCH_SIZE x2 (gfx950 wide-stream read counting), KiB x1024",
+       "mode": "bench.py N=1 default command: HBM-resident rotation over 4 buffer pairs",
+       "kernel_src_sha256": src_hash}
 json.dump(out, open(os.path.join(prof, "pmc_chunk_sum.json"), "w"), indent=1)
 print(json.dumps(out, indent=1))
