@@ -1,4 +1,6 @@
 // host_capi.cpp -- extern "C" drivers of the host runtime (include/hydra_host.h).
+#include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <cstdint>
@@ -462,6 +464,55 @@ int hydra_host_reduce_timeout_probe(long timeout_ms, char* what, size_t len) {
     } catch (const hydra::IoException& e) {
       set_err(what, len, e.what());
       rc = 0;
+    }
+  });
+  return rc;
+}
+
+// A SLOW peer (not a dead one): rank 0 times out, rank 1 joins `delay_ms` later and sends its
+// data.  Rank 0's context must be poisoned by the timeout (every pair closed, as the reference's
+// signalException), so the late bytes land nowhere: rank 0 refills its bucket with a sentinel
+// right after the exception and checks it once rank 1 is done.  *intact = 1 when untouched.
+int hydra_host_slow_peer_probe(long timeout_ms, long delay_ms, size_t n, char* what, size_t len,
+                               int* intact) {
+  int rc = 3;
+  std::atomic<int> late_done{0};
+  *intact = 0;
+  spawn(2, 1, nullptr, 0, [&](int r, std::vector<std::shared_ptr<hydra::Context>>& c) {
+    std::vector<uint64_t> buf(n, (uint64_t)r + 1);
+    auto ub = c[0]->createUnboundBuffer(buf.data(), n * sizeof(uint64_t));
+    const uint64_t slot = 77;
+    if (r == 1) {  // the slow peer: its send arrives after rank 0 gave up
+      std::this_thread::sleep_for(std::chrono::milliseconds(delay_ms));
+      try {
+        ub->send(0, slot, 0, n * sizeof(uint64_t));
+        ub->waitSend(std::chrono::milliseconds(2000));
+      } catch (const std::exception&) {  // rank 0 closed the connection: fails, never hangs
+      }
+      late_done = 1;
+      return;
+    }
+    // the receive lands straight in the caller's bucket, as the ring's all-gather does
+    ub->recv(1, slot, 0, n * sizeof(uint64_t));
+    try {
+      ub->waitRecv(std::chrono::milliseconds(timeout_ms));
+    } catch (const hydra::IoException& e) {
+      set_err(what, len, e.what());
+      rc = 0;
+    }
+    std::fill(buf.begin(), buf.end(), 0x5a5a5a5a5a5a5a5aull);  // the caller reuses its memory
+    while (!late_done) std::this_thread::sleep_for(std::chrono::milliseconds(5));
+    std::this_thread::sleep_for(std::chrono::milliseconds(50));
+    *intact = std::all_of(buf.begin(), buf.end(),
+                          [](uint64_t v) { return v == 0x5a5a5a5a5a5a5a5aull; }) ? 1 : 0;
+    // later operations on the poisoned context fail at once instead of waiting
+    const auto t0 = std::chrono::steady_clock::now();
+    try {
+      ub->recv(1, slot + 1, 0, sizeof(uint64_t));
+      ub->waitRecv(std::chrono::milliseconds(5000));
+      rc = 4;
+    } catch (const hydra::IoException&) {
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(1000)) rc = 5;
     }
   });
   return rc;

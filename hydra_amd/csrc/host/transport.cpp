@@ -128,7 +128,11 @@ class Pair {
     recvq_.push_back(std::move(op));
     cv_.notify_all();
   }
-  void close() {
+  void close() { abort("Connection closed"); }
+  // Fail every pending operation with `e`, refuse new ones, shut the socket and join both
+  // threads: when this returns no transport thread touches any operation's memory again.
+  void abort(const std::string& e) {
+    fail(e);
     {
       std::lock_guard<std::mutex> g(mu_);
       if (closed_) return;
@@ -195,7 +199,7 @@ class Pair {
       {
         std::unique_lock<std::mutex> l(mu_);
         cv_.wait(l, [&] { return closed_ || !sendq_.empty(); });
-        if (closed_ && sendq_.empty()) return;
+        if (closed_) return;  // abort() already failed whatever was queued
         op = sendq_.front();
         sendq_.pop_front();
       }
@@ -304,6 +308,11 @@ void Context::closeConnections() {
     if (p) p->close();
 }
 
+void Context::signalException(const std::string& msg) {
+  for (auto& p : pairs_)
+    if (p) p->abort(msg);
+}
+
 namespace {
 int listen_on(const std::string& host, int* port) {
   int fd = ::socket(AF_INET, SOCK_STREAM, 0);
@@ -394,7 +403,7 @@ void UnboundBuffer::recv(int src, uint64_t slot, size_t offset, size_t nbytes) {
 }
 
 namespace {
-void wait_oldest(std::mutex& mu, std::vector<std::shared_ptr<UnboundBuffer::Op>>& q,
+void wait_oldest(Context* ctx, std::mutex& mu, std::vector<std::shared_ptr<UnboundBuffer::Op>>& q,
                  std::chrono::milliseconds timeout, const char* what) {
   std::shared_ptr<UnboundBuffer::Op> op;
   {
@@ -402,29 +411,40 @@ void wait_oldest(std::mutex& mu, std::vector<std::shared_ptr<UnboundBuffer::Op>>
     if (q.empty()) throw EnforceNotMet(std::string("no pending ") + what + " operation");
     op = q.front();
   }
+  std::string timed_out, failed;
   {
     std::unique_lock<std::mutex> l(op->mu);
     // system_clock deadline: lowers to pthread_cond_timedwait (steady_clock's
     // pthread_cond_clockwait is invisible to GCC 11's ThreadSanitizer)
     const auto deadline = std::chrono::system_clock::now() + timeout;
-    if (!op->cv.wait_until(l, deadline, [&] { return op->done; })) {
+    if (!op->cv.wait_until(l, deadline, [&] { return op->done; }))
       // the reference's message (gloo/gloo/transport/tcp/unbound_buffer.cc:80-84)
-      throw IoException("Timed out waiting " + std::to_string(timeout.count()) + "ms for " +
-                        what + " operation to complete");
-    }
-    if (!op->error.empty()) throw IoException(op->error);
+      timed_out = "Timed out waiting " + std::to_string(timeout.count()) + "ms for " + what +
+                  " operation to complete";
+    else if (!op->error.empty())
+      failed = op->error;
   }
-  std::lock_guard<std::mutex> g(mu);
-  q.erase(q.begin());
+  {
+    std::lock_guard<std::mutex> g(mu);
+    q.erase(q.begin());
+  }
+  if (!timed_out.empty()) {
+    // the op may still sit in a pair's queue, pointing into the caller's memory: poison the
+    // context (every pair fails and joins its threads) before the exception unwinds that
+    // memory, as the reference signals the context (tcp/unbound_buffer.cc:66-76)
+    ctx->signalException(timed_out);
+    throw IoException(timed_out);
+  }
+  if (!failed.empty()) throw IoException(failed);
 }
 }  // namespace
 
 void UnboundBuffer::waitSend(std::chrono::milliseconds timeout) {
-  wait_oldest(mu_, sends_, timeout, "send");
+  wait_oldest(ctx_, mu_, sends_, timeout, "send");
 }
 
 void UnboundBuffer::waitRecv(std::chrono::milliseconds timeout) {
-  wait_oldest(mu_, recvs_, timeout, "recv");
+  wait_oldest(ctx_, mu_, recvs_, timeout, "recv");
 }
 
 }  // namespace hydra

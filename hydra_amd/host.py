@@ -53,6 +53,8 @@ def lib():
         L.hydra_host_reduce_threads.argtypes = [i, i, i, sz, vp, vp, i, sz, i, vp,
                                                 ctypes.c_long, ctypes.c_char_p, sz]
         L.hydra_host_reduce_timeout_probe.argtypes = [ctypes.c_long, ctypes.c_char_p, sz]
+        L.hydra_host_slow_peer_probe.argtypes = [ctypes.c_long, ctypes.c_long, sz,
+                                                 ctypes.c_char_p, sz, ctypes.POINTER(ctypes.c_int)]
         _h = L
     return _h
 
@@ -115,6 +117,15 @@ def reduce_threads(outs, ins=None, root=0, dtype_code=None, op="sum", max_segmen
     if rc:
         raise _lib.HydraError(rc, err.value.decode())
     return outs
+
+
+def slow_peer_probe(timeout_ms: int, delay_ms: int, n: int = 1 << 16):
+    """(rc, message, intact): see hydra_host_slow_peer_probe (include/hydra_host.h)."""
+    what = ctypes.create_string_buffer(512)
+    intact = ctypes.c_int(0)
+    rc = lib().hydra_host_slow_peer_probe(timeout_ms, delay_ms, n, what, 512,
+                                          ctypes.byref(intact))
+    return rc, what.value.decode(), bool(intact.value)
 
 
 def reduce_timeout_probe(ms: int):

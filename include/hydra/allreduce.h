@@ -122,6 +122,12 @@ class Context {
   std::chrono::milliseconds getTimeout() const { return timeout_; }
   transport::Pair* getPair(int peer);
   void closeConnections();
+  // A timed-out or failed operation poisons the whole context, as the reference's
+  // context_->signalException does (gloo/gloo/transport/tcp/unbound_buffer.cc:66-76): every pair
+  // fails its pending operations with `msg`, closes its socket and joins its threads, so no
+  // late peer message can land in a buffer the caller is about to free; later operations on the
+  // context fail at once.
+  void signalException(const std::string& msg);
 
   const int rank;
   const int size;

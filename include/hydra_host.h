@@ -126,6 +126,10 @@ int hydra_host_reduce_timeout_probe(long timeout_ms, char* what, size_t len);
 /* AllreduceNewTest.TestTimeout (allreduce_test.cc:381-397): rank 0 of 2 times out; returns 0 and
  * the IoException text if it was raised. */
 int hydra_host_timeout_probe(long timeout_ms, char* what, size_t len);
+/* Slow-peer timeout probe: rank 0 times out, rank 1 sends `delay_ms` later; *intact = 1 when
+ * the late bytes did not land in rank 0's refilled bucket (its context was poisoned). */
+int hydra_host_slow_peer_probe(long timeout_ms, long delay_ms, size_t n, char* what, size_t len,
+                               int* intact);
 
 #ifdef __cplusplus
 }

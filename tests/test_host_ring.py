@@ -374,3 +374,14 @@ def test_allreduce_local(O, P, nptr, n):
             exp = exp + xs[r][i]  # float32 numpy add == the in-place fp32 sum, RNE
         for i in range(nptr):
             assert np.array_equal(bufs[r][i].view(np.uint32), exp.view(np.uint32)), (r, i)
+
+
+def test_slow_peer_after_timeout_lands_nowhere():
+    """a timeout must poison the context like the reference's signalException
+    (tcp/unbound_buffer.cc:66-76), not leave the op queued on its pair.  Rank 0 times out, rank 1
+    (slow, not dead) sends 300 ms later: rank 0 raises "Timed out waiting ...", its refilled
+    bucket stays untouched by the late bytes, and later collectives on the context fail."""
+    rc, what, intact = host.slow_peer_probe(50, 300)
+    assert rc == 0, (rc, what)
+    assert "Timed out waiting 50ms" in what
+    assert intact
