@@ -48,6 +48,7 @@ ALGOS = {"auto": ALGO_AUTO, "ring": ALGO_RING, "direct": ALGO_DIRECT, "rccl": AL
          "ring_chunked": ALGO_RING_CHUNKED, "bcube": ALGO_BCUBE,
          "halving_doubling": ALGO_HALVING_DOUBLING}
 ACC_F32 = 1
+ERR_INVALID = 1
 ERR_TIMEOUT = 5
 UNIQUE_ID_BYTES = 128
 # peer-access allreduce (hydra_peer_*)

@@ -34,11 +34,14 @@ constexpr size_t kIpcBytes = sizeof(hipIpcMemHandle_t);
 static_assert(kIpcBytes <= 64, "hipIpcMemHandle_t larger than the blob slot");
 
 // Blob layout (HYDRA_PEER_HANDLE_BYTES): [0,64) hipIpcMemHandle_t of the allocation base,
-// [64,72) offset of the buffer in it, [72,80) buffer bytes, [80,88) magic, [88,92) rank.
+// [64,72) offset of the buffer in it, [72,80) buffer bytes, [80,88) magic, [88,92) rank,
+// [96,104) the exporter's allocation id (HIP_POINTER_ATTRIBUTE_BUFFER_ID: unique per
+// allocation, so a freed-and-reallocated bucket whose IPC handle bytes repeat is a NEW mapping).
 struct Blob {
   unsigned char ipc[64];
   uint64_t offset, bytes, magic;
   int32_t rank, pad;
+  uint64_t alloc_id;
 };
 static_assert(sizeof(Blob) <= HYDRA_PEER_HANDLE_BYTES, "blob too large");
 
@@ -63,11 +66,13 @@ struct hydra_peer {
   struct Reg {
     char* base;
     size_t bytes;
+    const void* alloc_base;  // base of the device allocation holding it (its export record)
     char* peer[hydra::kPeerMaxRanks];
     std::string key[hydra::kPeerMaxRanks];
   };
   std::vector<Reg> regs;
-  std::map<std::string, Mapping> opened;  // ipc handle bytes -> mapping (one per allocation)
+  std::map<std::string, Mapping> opened;  // (rank, allocation id, ipc bytes) -> mapping
+  std::map<const void*, uint64_t> exported;  // own allocation base -> allocation id exported
   bool detached = false;                  // hydra_peer_detach ran: no mappings left
 };
 
@@ -84,14 +89,28 @@ int export_blob(hydra_peer* p, void* ptr, size_t bytes, void* out) {
   if (std::getenv("HYDRA_PEER_DEBUG"))
     std::fprintf(stderr, "[hydra_peer] rank %d export %p (+%zu) in allocation [%p, +%zu)\n",
                  p->rank, ptr, bytes, base, size);
+  unsigned long long id = 0;
+  HIP_TRY(hipPointerGetAttribute(&id, HIP_POINTER_ATTRIBUTE_BUFFER_ID,
+                                 reinterpret_cast<hipDeviceptr_t>(base)));
+  // Register once: an allocation base this group exported before must still be the SAME
+  // allocation.  Freeing a registered bucket and exporting a new allocation at that address
+  // while peers may still map the old one (round 1: peers read zeros/garbage after free +
+  // re-register) is refused; hydra_peer_close the old registration on every rank first.
+  auto ex = p->exported.find(base);
+  if (ex != p->exported.end() && ex->second != (uint64_t)id)
+    return fail(HYDRA_ERR_INVALID,
+                "allocation at this address changed since it was exported to the peer group "
+                "(register a bucket once; hydra_peer_close it on every rank before freeing it)");
   hipIpcMemHandle_t h;
   HIP_TRY(hipIpcGetMemHandle(&h, base));
+  p->exported[base] = (uint64_t)id;
   Blob blob{};
   std::memcpy(blob.ipc, &h, kIpcBytes);
   blob.offset = (uint64_t)(q - b);
   blob.bytes = bytes;
   blob.magic = kMagic;
   blob.rank = p->rank;
+  blob.alloc_id = (uint64_t)id;
   std::memset(out, 0, HYDRA_PEER_HANDLE_BYTES);
   std::memcpy(out, &blob, sizeof(blob));
   return HYDRA_OK;
@@ -107,7 +126,9 @@ int parse_blob(const void* in, int expect_rank, Blob* blob) {
 
 // Map a peer allocation (cached: several buffers may share one allocation).
 int open_mapping(hydra_peer* p, const Blob& b, std::string* key, char** base) {
-  *key = std::string(reinterpret_cast<const char*>(b.ipc), kIpcBytes);
+  // keyed by exporter rank + allocation id + handle bytes, never by the handle bytes alone
+  *key = std::to_string(b.rank) + ":" + std::to_string(b.alloc_id) + ":" +
+         std::string(reinterpret_cast<const char*>(b.ipc), kIpcBytes);
   auto it = p->opened.find(*key);
   if (it == p->opened.end()) {
     hipIpcMemHandle_t h;
@@ -208,6 +229,12 @@ int hydra_peer_open(hydra_peer_t p, void* buf, size_t bytes, const void* handles
   hydra_peer::Reg reg{};
   reg.base = static_cast<char*>(buf);
   reg.bytes = bytes;
+  {
+    void* ab = nullptr;
+    size_t asz = 0;
+    HIP_TRY(hipMemGetAddressRange(&ab, &asz, buf));
+    reg.alloc_base = ab;
+  }
   reg.peer[p->rank] = reg.base;
   for (int q = 0; q < p->P; q++) {
     Blob b;
@@ -236,6 +263,10 @@ int hydra_peer_close(hydra_peer_t p, void* buf) {
     (void)hipDeviceSynchronize();  // no kernel may still read through the mappings
     for (int q = 0; q < p->P; q++)
       if (q != p->rank) close_mapping(p, p->regs[i].key[q]);
+    bool shared = false;  // another open registration in the same allocation keeps its record
+    for (size_t j = 0; j < p->regs.size(); j++)
+      if (j != i && p->regs[j].alloc_base == p->regs[i].alloc_base) shared = true;
+    if (!shared) p->exported.erase(p->regs[i].alloc_base);
     p->regs.erase(p->regs.begin() + (long)i);
     return ok();
   }

@@ -309,7 +309,10 @@ int hydra_peer_allreduce(hydra_peer_t peer, int algo, int op, int dtype, int fla
  * allreduce calls fail once it ran.  hydra_peer_close(buf) has the same rule per buffer: close
  * on every rank, barrier, then free.  Register long-lived buckets: freeing a registered
  * allocation and registering a new one in the same process intermittently gave a peer a
- * mapping of the wrong memory on ROCm 7.2. */
+ * mapping of the wrong memory on ROCm 7.2.  Enforced: every handle carries the
+ * exporter's allocation id (HIP_POINTER_ATTRIBUTE_BUFFER_ID) and peers key their mappings by
+ * it, and hydra_peer_register refuses (HYDRA_ERR_INVALID) an address whose allocation changed
+ * since this group exported it, until hydra_peer_close released the old registration. */
 int hydra_peer_detach(hydra_peer_t peer);
 int hydra_peer_destroy(hydra_peer_t peer);
 

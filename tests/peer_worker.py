@@ -56,6 +56,29 @@ def stress(peer, arena, c, rank, world, dev):
     return bad
 
 
+def reregister(peer, c, rank, world, dev):
+    """`iters` rounds of: a FRESH allocation (the caching allocator emptied first), register,
+    allreduce with inputs that change every round, every word checked, collective unregister,
+    free.  Each round's mappings must be of that round's memory (round 1's symptom: a peer's
+    mapping of a re-registered bucket read zeros or garbage).  Returns wrong words."""
+    import torch
+
+    n = c["n"]
+    bad = 0
+    base = torch.arange(n, device=dev, dtype=torch.int64) % 1000
+    for it in range(c["iters"]):
+        torch.cuda.synchronize(dev)
+        torch.cuda.empty_cache()
+        t = ((base * (rank + 1)) + it * (rank + 2)).to(torch.float32)
+        peer.register(t)
+        peer.allreduce_(t, algo=c["algo"], dtype_code=c["dtype"])
+        exp = base * (world * (world + 1) // 2) + it * (world * (world + 3) // 2)
+        bad += int((t != exp.to(torch.float32)).sum().item())
+        peer.unregister(t)  # collective: every rank closed its mappings before anyone frees
+        del t
+    return bad
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rank", type=int, required=True)
@@ -93,6 +116,9 @@ def main():
                 continue
             if c["data"] == "stress":  # varying inputs, uneven arrival, every word checked
                 status[name] = stress(peer, arena, c, a.rank, a.world, dev)
+                continue
+            if c["data"] == "reregister":  # fresh allocations, register/unregister loop
+                status[name] = reregister(peer, c, a.rank, a.world, dev)
                 continue
             if c.get("timeout_ms"):
                 peer.set_option(_lib.PEER_OPT_TIMEOUT_MS, c["timeout_ms"])

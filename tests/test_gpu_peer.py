@@ -104,6 +104,8 @@ def cases_for(P):
     cs.append(dict(name="stress1", algo="peer1", data="stress", dtype=F32, n=50021, iters=40))
     cs.append(dict(name="bf16_acc32", algo="peer2", data="bf16", dtype=BF16, n=1 << 20,
                    flags=_lib.ACC_F32))
+    cs.append(dict(name="reregister", algo="peer2", data="reregister", dtype=F32,
+                   n=(1 << 20) + 3, iters=12))
     return cs
 
 
@@ -114,7 +116,7 @@ def test_peer_allreduce_bit_exact(gpu, O, tmp_path, P):
     for c in cases:
         name = c["name"]
         assert all(s[name] == 0 for s in st), (name, st)
-        if c["data"] == "stress":  # checked word by word inside every rank
+        if c["data"] in ("stress", "reregister"):  # checked word by word inside every rank
             continue
         if c["data"] == "bf16":
             n = c["n"]
@@ -174,3 +176,41 @@ def test_peer_algorithm_class_cpp(gpu, tmp_path, P, n):
     out = r.stdout.decode() + r.stderr.decode()
     assert r.returncode == 0, out
     assert f"peer_algo P={P} n={n}: ok" in out
+
+
+def test_register_refuses_a_changed_allocation(gpu):
+    """Register once: a peer group refuses to export an address whose allocation
+    changed since it was exported (freed and reallocated without hydra_peer_close), and accepts
+    it again once the old registration is closed.  A 1-rank group in this process; the check
+    needs the allocator to hand back the freed address, which a same-size hipMalloc does."""
+    import ctypes
+
+    L = _lib.lib()
+    h = ctypes.c_void_p()
+    sig = ctypes.create_string_buffer(_lib.PEER_HANDLE_BYTES)
+    _lib.check(L.hydra_peer_create(1, 0, 0, ctypes.byref(h), sig))
+    try:
+        _lib.check(L.hydra_peer_connect(h, sig))
+        nbytes = 64 << 20
+        a = ctypes.c_void_p()
+        _lib.check(L.hydra_malloc(0, nbytes, ctypes.byref(a)))
+        blob = ctypes.create_string_buffer(_lib.PEER_HANDLE_BYTES)
+        _lib.check(L.hydra_peer_register(h, a, nbytes, blob))
+        _lib.check(L.hydra_peer_open(h, a, nbytes, blob))
+        _lib.check(L.hydra_peer_register(h, a, nbytes, blob))  # same allocation again: fine
+        _lib.check(L.hydra_free(a))
+        b = ctypes.c_void_p()
+        _lib.check(L.hydra_malloc(0, nbytes, ctypes.byref(b)))
+        reused = b.value == a.value
+        rc = L.hydra_peer_register(h, b, nbytes, blob)
+        if reused:
+            assert rc == _lib.ERR_INVALID, "a changed allocation at a registered address"
+            assert b"changed" in L.hydra_last_error()
+        _lib.check(L.hydra_peer_close(h, a))  # the old registration released ...
+        _lib.check(L.hydra_peer_register(h, b, nbytes, blob))  # ... the new one is accepted
+        _lib.check(L.hydra_free(b))
+        if not reused:
+            pytest.skip("allocator did not reuse the address; refusal not exercised")
+    finally:
+        L.hydra_peer_detach(h)
+        L.hydra_peer_destroy(h)
