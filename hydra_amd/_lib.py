@@ -26,7 +26,7 @@ EXPORTS = [  # every symbol include/hydra_hip.h declares
     "hydra_abi_version", "hydra_last_error", "hydra_device_count", "hydra_device_arch",
     "hydra_device_check", "hydra_event_create", "hydra_event_record", "hydra_event_synchronize",
     "hydra_event_destroy",
-    "hydra_reduce", "hydra_chunk_sum", "hydra_acc_bf16_f32", "hydra_f32_to_bf16",
+    "hydra_reduce", "hydra_chunk_sum", "hydra_reduce_batch", "hydra_acc_bf16_f32", "hydra_f32_to_bf16",
     "hydra_set_variant", "hydra_ctx_create", "hydra_ctx_destroy", "hydra_reduce_host",
     "hydra_chunk_sum_host", "hydra_host_register", "hydra_host_unregister",
     "hydra_stream_create", "hydra_stream_destroy", "hydra_stream_synchronize", "hydra_malloc",
@@ -68,6 +68,12 @@ class PlanOp(ctypes.Structure):
 OP_SEND, OP_RECV, OP_GROUP, OP_REDUCE, OP_FOLD, OP_ALLTOALL, OP_ALLGATHER = 1, 2, 3, 4, 5, 6, 7
 
 
+class Segment(ctypes.Structure):
+    """hydra_segment_t (include/hydra_hip.h): one c = op(a, b) of a hydra_reduce_batch call."""
+    _fields_ = [("c", ctypes.c_void_p), ("a", ctypes.c_void_p), ("b", ctypes.c_void_p),
+                ("n", ctypes.c_size_t)]
+
+
 class HydraError(RuntimeError):
     """A non-zero hydra_status_t (or a missing library)."""
 
@@ -101,6 +107,7 @@ def _declare(L) -> None:
     L.hydra_event_destroy.argtypes = [vp]
     L.hydra_reduce.argtypes = [i, i, vp, vp, vp, sz, vp]
     L.hydra_chunk_sum.argtypes = [i, vp, vp, vp, sz, vp]
+    L.hydra_reduce_batch.argtypes = [i, i, vp, sz, vp]
     L.hydra_acc_bf16_f32.argtypes = [vp, vp, sz, vp]
     L.hydra_f32_to_bf16.argtypes = [vp, vp, sz, vp]
     L.hydra_set_variant.argtypes = [i]

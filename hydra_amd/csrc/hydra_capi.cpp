@@ -150,6 +150,23 @@ int hydra_chunk_sum(int dtype, void* c, const void* a, const void* b, size_t n,
   return hydra_reduce(HYDRA_SUM, dtype, c, a, b, n, stream);
 }
 
+int hydra_reduce_batch(int op, int dtype, const hydra_segment_t* segs, size_t count,
+                       hydra_stream_t stream) {
+  if (count && !segs) return fail(HYDRA_ERR_INVALID, "null segment list");
+  static_assert(sizeof(hydra_segment_t) == sizeof(hydra::BatchSegDesc), "layout");
+  for (size_t i = 0; i < count; i++) {  // every segment obeys hydra_reduce's contract
+    int rc = check_args(op, dtype, segs[i].c, segs[i].a, segs[i].b, segs[i].n);
+    if (rc) return fail(rc, "segment " + std::to_string(i) + ": " + hydra_last_error());
+  }
+  if (op < HYDRA_SUM || op > HYDRA_MIN || !hydra::dtype_size(dtype))
+    return fail(HYDRA_ERR_INVALID, "invalid op/dtype");
+  hipError_t e = hydra::launch_reduce_batch(op, dtype,
+                                            reinterpret_cast<const hydra::BatchSegDesc*>(segs),
+                                            count, static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return hip_fail(e, "batched reduce kernel launch");
+  return ok();
+}
+
 int hydra_fold(int op, int dtype, int flags, void* dst, const void* const* srcs, int nsrc,
                size_t n, hydra_stream_t stream) {
   if (op < HYDRA_SUM || op > HYDRA_MIN) return fail(HYDRA_ERR_INVALID, "invalid op");

@@ -23,6 +23,16 @@ hipError_t launch_reduce(int variant, int op, int dtype, void* c, const void* a,
 // acc32: bf16 data, fp32 accumulation, one rounding.  dst may equal srcs[0].
 hipError_t launch_fold(int op, int dtype, bool acc32, void* dst, const void* const* srcs,
                        int nsrc, size_t n, hipStream_t s);
+// K independent segments c_k = op(a_k, b_k) in as few launches as possible (kMaxBatch each)
+constexpr int kMaxBatch = 32;
+struct BatchSegDesc {
+  void* c;
+  const void* a;
+  const void* b;
+  size_t n;
+};
+hipError_t launch_reduce_batch(int op, int dtype, const BatchSegDesc* segs, size_t count,
+                               hipStream_t s);
 hipError_t launch_acc_bf16_f32(float* acc, const void* b_bf16, size_t n, hipStream_t s);
 hipError_t launch_f32_to_bf16(void* out_bf16, const float* acc, size_t n, hipStream_t s);
 

@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
 #include <type_traits>
 
 #include "errors.h"
@@ -350,6 +351,69 @@ __global__ __launch_bounds__(kBlock) void k_fold(E* dst, FoldSrcs S, int nsrc, s
 }
 
 // -------------------------------------------------------------------------------------------
+// Batched chunk-sum: K independent segments c_k = op(a_k, b_k) in ONE launch.  A caller that
+// holds several arrived segments (consecutive ring segments, both rails of bew_allreduce_a)
+// pays one dispatch and one completion instead of K: below ~1 Mi elements a launch costs a
+// dispatch plus one dependent HBM round trip (~3 us) whatever its size (DESIGN.md 4.2 sweep).
+// Block b serves tile b - tile0[k] of the segment k whose tile range holds b (wave-uniform
+// lookup over the kernarg table); tile 0 of each segment also does its ragged head and tail.
+// -------------------------------------------------------------------------------------------
+struct BatchSeg {
+  char* c;             // at the vector body: c 16-B aligned
+  const char* a;
+  const char* b;
+  uint64_t nvec;       // 16-B vectors in the body
+  int32_t head, tail;  // ragged elements before / after the body
+  uint32_t tile0;      // first block of this segment
+  uint32_t c_old;      // float16 store quirk with c != a: load c's old bits
+};
+struct BatchArgs {
+  BatchSeg s[kMaxBatch];
+  int32_t count;
+};
+
+template <typename E, int OP>
+__device__ __forceinline__ void batch_edges(const BatchSeg& g, int t) {
+  constexpr int N = Vec<E>::N;
+  E* c_ = reinterpret_cast<E*>(g.c);
+  const E* a_ = reinterpret_cast<const E*>(g.a);
+  const E* b_ = reinterpret_cast<const E*>(g.b);
+  const bool head = t < g.head, tail = t >= 64 && t - 64 < g.tail;
+  if (!head && !tail) return;
+  const ptrdiff_t i = head ? (ptrdiff_t)t - g.head : (ptrdiff_t)(g.nvec * N) + (t - 64);
+  const E ea = a_[i], eb = b_[i];
+  const E ec = g.c_old ? c_[i] : ea;
+  c_[i] = Elem<E, OP>::apply(ea, eb, ec);
+}
+
+template <typename E, int OP>
+__global__ __launch_bounds__(kBlock) void k_reduce_batch(const BatchArgs args) {
+  const uint32_t bid = blockIdx.x;
+  int k = 0;  // wave-uniform: the last segment whose first tile is <= this block
+#pragma unroll
+  for (int j = 1; j < kMaxBatch; j++)
+    if (j < args.count && args.s[j].tile0 <= bid) k = j;
+  const BatchSeg& g = args.s[k];
+  const int t = threadIdx.x;
+  const uint32_t tile = bid - g.tile0;
+  if (tile == 0 && (g.head | g.tail)) batch_edges<E, OP>(g, t);
+  const size_t v0 = (size_t)tile * kBlock;
+  if (v0 >= g.nvec) return;
+  const uint32_t off = (uint32_t)t * 16;
+  const char* at = g.a + v0 * 16;
+  const char* bt = g.b + v0 * 16;
+  char* ct = g.c + v0 * 16;
+  if (v0 + (size_t)t < g.nvec) {
+    const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4_u*>(at + off));
+    const u32x4 y = __builtin_nontemporal_load(reinterpret_cast<const u32x4_u*>(bt + off));
+    const u32x4 z = g.c_old ? ld_u(ct + off) : x;
+    // write-through (sc1) store through a block-uniform descriptor, as the tuned chunk-sum
+    const auto w = rsrc<kBuf | 16>(ct, kBlock * 16);
+    st<kBuf | 16>(ct, w, off, vapply<E, OP>(x, y, z));
+  }
+}
+
+// -------------------------------------------------------------------------------------------
 // launch
 // -------------------------------------------------------------------------------------------
 int g_cu_count = 0;
@@ -623,6 +687,69 @@ hipError_t launch_fold(int op, int dtype, bool acc32, void* dst, const void* con
     case kProduct: return fold_dtype<kProduct>(dtype, acc32, dst, srcs, nsrc, n, s);
     case kMax: return fold_dtype<kMax>(dtype, acc32, dst, srcs, nsrc, n, s);
     case kMin: return fold_dtype<kMin>(dtype, acc32, dst, srcs, nsrc, n, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+namespace {
+template <typename E, int OP>
+hipError_t launch_batch_t(const BatchSegDesc* segs, size_t count, hipStream_t st) {
+  size_t i = 0;
+  while (i < count) {  // up to kMaxBatch segments (and < 2^31 blocks) per launch
+    BatchArgs args{};
+    uint64_t blocks = 0;
+    int k = 0;
+    for (; i < count && k < kMaxBatch; i++) {
+      const BatchSegDesc& d = segs[i];
+      if (d.n == 0) continue;
+      const Split sp = split_call<E>(d.c, d.n);
+      const uint64_t tiles = std::max<uint64_t>(1, (sp.nvec + kBlock - 1) / kBlock);
+      if (blocks + tiles > 0x7fffffffull) break;
+      BatchSeg& g = args.s[k++];
+      g.c = static_cast<char*>(d.c) + (size_t)sp.head * sizeof(E);
+      g.a = static_cast<const char*>(d.a) + (size_t)sp.head * sizeof(E);
+      g.b = static_cast<const char*>(d.b) + (size_t)sp.head * sizeof(E);
+      g.nvec = sp.nvec;
+      g.head = sp.head;
+      g.tail = sp.tail;
+      g.tile0 = (uint32_t)blocks;
+      g.c_old = (Elem<E, OP>::kNeedsOld && d.c != d.a) ? 1u : 0u;
+      blocks += tiles;
+    }
+    if (k == 0) continue;
+    args.count = k;
+    hipLaunchKernelGGL((k_reduce_batch<E, OP>), dim3((unsigned)blocks), dim3(kBlock), 0, st, args);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+template <int OP>
+hipError_t batch_dtype(int dtype, const BatchSegDesc* segs, size_t count, hipStream_t st) {
+  switch (dtype) {
+    case kI8: return launch_batch_t<int8_t, OP>(segs, count, st);
+    case kU8: return launch_batch_t<uint8_t, OP>(segs, count, st);
+    case kI32: return launch_batch_t<int32_t, OP>(segs, count, st);
+    case kU32: return launch_batch_t<uint32_t, OP>(segs, count, st);
+    case kI64: return launch_batch_t<int64_t, OP>(segs, count, st);
+    case kU64: return launch_batch_t<uint64_t, OP>(segs, count, st);
+    case kF32: return launch_batch_t<float, OP>(segs, count, st);
+    case kF64: return launch_batch_t<double, OP>(segs, count, st);
+    case kF16: return launch_batch_t<f16_t, OP>(segs, count, st);
+    case kBF16: return launch_batch_t<bf16_t, OP>(segs, count, st);
+  }
+  return hipErrorInvalidValue;
+}
+}  // namespace
+
+hipError_t launch_reduce_batch(int op, int dtype, const BatchSegDesc* segs, size_t count,
+                               hipStream_t st) {
+  switch (op) {
+    case kSum: return batch_dtype<kSum>(dtype, segs, count, st);
+    case kProduct: return batch_dtype<kProduct>(dtype, segs, count, st);
+    case kMax: return batch_dtype<kMax>(dtype, segs, count, st);
+    case kMin: return batch_dtype<kMin>(dtype, segs, count, st);
   }
   return hipErrorInvalidValue;
 }

@@ -86,6 +86,19 @@ int hydra_reduce(int op, int dtype, void* c, const void* a, const void* b, size_
                  hydra_stream_t stream);
 int hydra_chunk_sum(int dtype, void* c, const void* a, const void* b, size_t n,
                     hydra_stream_t stream);
+/* count independent segments c_k = op(a_k, b_k) in ONE launch (up to 32 segments per launch):
+ * the same contract per segment as hydra_reduce.  Replaces `count` consecutive gloo::sum<T>
+ * calls (allreduce.cc:301-305, one per arriving segment) for a caller that holds several
+ * segments at once: below ~1 Mi elements a launch costs a dispatch plus one dependent HBM round
+ * trip whatever its size, so K segments in one launch pay that once. */
+typedef struct {
+  void* c;
+  const void* a;
+  const void* b;
+  size_t n; /* elements */
+} hydra_segment_t;
+int hydra_reduce_batch(int op, int dtype, const hydra_segment_t* segs, size_t count,
+                       hydra_stream_t stream);
 
 /* Mixed-precision bucket (BASELINE config 5): acc[i] = acc[i] + (float)b_bf16[i]. */
 int hydra_acc_bf16_f32(float* acc, const void* b_bf16, size_t n, hydra_stream_t stream);

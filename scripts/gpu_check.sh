@@ -24,6 +24,8 @@ step() {  # step NAME TIMEOUT CMD...
 
 rocminfo 2>/dev/null | grep -m2 -E "gfx|Marketing" > "$OUT/device.txt" || true
 nproc > "$OUT/host.txt"; grep -m1 "model name" /proc/cpuinfo >> "$OUT/host.txt" || true
+# the chunk-sum kernel sources this session profiles (scripts/pmc_summary.py, bench.py traffic)
+(cd hydra_amd/csrc && cat reduce_kernels.hip reduce_ops.h reduce_kernels.h | sha256sum | cut -d' ' -f1) > "$OUT/kernel_src.sha256"
 
 if [ "${SKIP_TESTS:-0}" != "1" ]; then
   step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -p no:cacheprovider

@@ -21,10 +21,16 @@ root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 prof = os.path.join(root, "profiles")
 os.makedirs(prof, exist_ok=True)
 HOT = "k_reduce<float, 0"
-h = hashlib.sha256()  # the same hash bench.py's kernel_src_hash() computes
-for f in ("reduce_kernels.hip", "reduce_ops.h", "reduce_kernels.h"):
-    h.update(open(os.path.join(root, "hydra_amd", "csrc", f), "rb").read())
-src_hash = h.hexdigest()
+# the kernel sources the profiled run used: gpu_check.sh records their hash on the box (the same
+# hash bench.py's kernel_src_hash() computes); fall back to the working tree
+rec = os.path.join(src, "kernel_src.sha256")
+if os.path.exists(rec):
+    src_hash = open(rec).read().split()[0]
+else:
+    h = hashlib.sha256()
+    for f in ("reduce_kernels.hip", "reduce_ops.h", "reduce_kernels.h"):
+        h.update(open(os.path.join(root, "hydra_amd", "csrc", f), "rb").read())
+    src_hash = h.hexdigest()
 
 shutil.copy(os.path.join(src, "prof_kt", "run_kernel_stats.csv"),
             os.path.join(prof, f"{tag}_kernel_stats.csv"))

@@ -24,7 +24,30 @@ for n in sizes:
     b = torch.rand(n + 4, device=dev)
     c = torch.empty(n, device=dev)
     flush = torch.empty(1 << 28, dtype=torch.float32, device=dev)  # 1 GiB: evicts the 256 MiB MALL
+    # "rotate": bench.py's HBM-resident headline -- in place on 4 buffer pairs in turn, the
+    # event span over `reps` launches / reps (no per-launch events)
+    rot = [(torch.rand(n, device=dev), torch.rand(n, device=dev)) for _ in range(4)] \
+        if "rotate" in os.environ.get("MODES", "") else []
     for mode in os.environ.get("MODES", "inplace,outofplace").split(","):
+        if mode == "rotate":
+            for r in range(rounds):
+                for v in variants:
+                    L.hydra_set_variant(v)
+                    for k in range(4):
+                        x, y = rot[k]
+                        _lib.check(L.hydra_chunk_sum(6, x.data_ptr(), x.data_ptr(), y.data_ptr(),
+                                                     n, s.cuda_stream))
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record(s)
+                    for k in range(reps):
+                        x, y = rot[k % 4]
+                        _lib.check(L.hydra_chunk_sum(6, x.data_ptr(), x.data_ptr(), y.data_ptr(),
+                                                     n, s.cuda_stream))
+                    e1.record(s)
+                    torch.cuda.synchronize()
+                    res.setdefault(f"{n}/{mode}", {}).setdefault(v, []).append(
+                        e0.elapsed_time(e1) / reps * 1e3)
+            continue
         pc = c.data_ptr() if mode == "outofplace" else a.data_ptr()
         # misalign: in place, b one element past 16-B alignment (the ring's tmp slot 1 at
         # +segmentBytes, allreduce.cc:236, when segmentBytes is not a multiple of 16)
@@ -45,7 +68,7 @@ for n in sizes:
                 torch.cuda.synchronize()
                 t = float(np.median([e0.elapsed_time(e1) for e0, e1 in ev])) * 1e3
                 res.setdefault(f"{n}/{mode}", {}).setdefault(v, []).append(t)
-    del a, b, c, flush
+    del a, b, c, flush, rot
 L.hydra_set_variant(0)
 out = {}
 for k, d in res.items():

@@ -383,3 +383,63 @@ def test_graph_capture_replay(gpu, O):
         exp = O.op(exp, bb, "sum", 6)
     torch.cuda.synchronize()
     assert np.array_equal(a.cpu().numpy().view(np.uint32), exp.view(np.uint32))
+
+
+@pytest.mark.parametrize("name,code,dt", [("f32", 6, np.float32), ("i8", 0, np.int8),
+                                          ("f16", 8, np.uint16), ("f64", 7, np.float64),
+                                          ("bf16", 9, np.uint16)])
+@pytest.mark.parametrize("kind", ["sum", "max"])
+def test_reduce_batch_matches_single_calls(dev, O, name, code, dt, kind):
+    """hydra_reduce_batch == one hydra_reduce per segment: 70 segments (three launches of up to
+    32), ragged sizes 0..300k, every byte misalignment of c/a/b the element size allows, in place
+    and out of place (float16's store quirk reads c's old bits when c != a), empty segments."""
+    L = _lib.lib()
+    rng = np.random.default_rng(code * 11 + len(kind))
+    es = np.dtype(dt).itemsize
+    segs, expect, bufs = [], [], []
+    for k in range(70):
+        n = int(rng.choice([0, 1, 3, 17, 255, 4099, 65537, 262144, 300007]))
+        if dt in (np.float32, np.float64):
+            a = rng.uniform(-2, 2, n).astype(dt)
+            b = rng.uniform(-2, 2, n).astype(dt)
+        elif code in (8, 9):
+            a = rng.integers(0, 1 << 16, n).astype(np.uint16)
+            b = rng.integers(0, 1 << 16, n).astype(np.uint16)
+        else:
+            a = rng.integers(-100, 100, n).astype(dt)
+            b = rng.integers(-100, 100, n).astype(dt)
+        oa, ob = es * int(rng.integers(0, 16 // es)), es * int(rng.integers(0, 16 // es))
+        inplace = bool(k % 3)
+        ta, pa = dev.put(a, oa)
+        tb, pb = dev.put(b, ob)
+        c0 = rng.integers(0, 1 << 16, n).astype(np.uint16).view(dt) if es == 2 else np.zeros_like(a)
+        if inplace:
+            tc, pc, oc = ta, pa, oa
+        else:
+            oc = es * int(rng.integers(0, 16 // es))
+            tc, pc = dev.put(c0, oc)
+        # in place: the oracle; out of place (float16 reads c's old bits) and bf16 (no reference
+        # counterpart): a single hydra_reduce call, itself pinned to the oracle elsewhere
+        ea = O.op(a, b, kind, code) if inplace and code != 9 else None
+        segs.append(_lib.Segment(pc, pa, pb, n))
+        expect.append((ea, a, b, c0, inplace))
+        bufs.append((ta, tb, tc, oc, n))
+    arr = (_lib.Segment * len(segs))(*segs)
+    _lib.check(L.hydra_reduce_batch(OPC[kind], code, ctypes.cast(arr, ctypes.c_void_p), len(segs),
+                                    None))
+    dev.torch.cuda.synchronize()
+    for (ea, a, b, c0, inplace), (ta, tb, tc, oc, n) in zip(expect, bufs):
+        got = dev.get(tc, oc, a)
+        if ea is None:
+            ea = dev_reduce(dev, kind, code, a, b, c0=c0, inplace=inplace)
+        assert np.array_equal(bits(got), bits(ea)), (name, kind, n)
+
+
+def test_reduce_batch_argument_checks(dev):
+    L = _lib.lib()
+    t = dev.torch.zeros(1024, dtype=dev.torch.float32, device=dev.gpu)
+    p = t.data_ptr()
+    bad = (_lib.Segment * 2)(_lib.Segment(p, p, p + 2048, 100), _lib.Segment(p + 2, p, p, 10))
+    rc = L.hydra_reduce_batch(0, 6, ctypes.cast(bad, ctypes.c_void_p), 2, None)
+    assert rc == _lib.ERR_INVALID and b"segment 1" in L.hydra_last_error()
+    assert L.hydra_reduce_batch(0, 6, None, 0, None) == 0
