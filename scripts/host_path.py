@@ -2,10 +2,11 @@
 """Host-resident path measurements: what the reduction costs when the segment
 lives in host memory, as it does in the reference's TCP ring.
 
-  1. isolated: hydra_reduce_host on 1 MiB / 16 MiB / 64 MiB fp32 segments, pageable vs
+  1. isolated: hydra_reduce_host on 262 144 / 4 Mi / 16 Mi fp32 elements, pageable vs
      hipHostRegister'ed buffers, vs the reference's gloo::sum<float> on the same host core
-  2. config 1: new_allreduce_ring, 2 ranks, loopback TCP -- the reference itself (oracle/_ref)
-     vs the hydra C++ host runtime with the GPU reducer
+  2. config 1: new_allreduce_ring, 2 ranks, loopback TCP, the whole 4 .. 64 Mi doubling sweep
+     -- the reference itself (oracle/_ref, CPU sum) timed beside the hydra C++ host runtime with
+     the GPU reducer (staged and zero-copy), in the same run
   3. config 3: bew_allreduce_a, 2 ranks x 2 loopback rails -- hydra host runtime with the
      reference's gloo::sum<float> as reducer vs the GPU reducer (H2D + sum + D2H per segment)
 Prints one JSON document.
@@ -80,10 +81,15 @@ def dist(s, n):
 
 
 ref_fn = ctypes.cast(O.ref().ref_sum_f32, ctypes.c_void_p).value if O.ref_available() else None
-sizes = [4, 4096, 262144, 1 << 20, 1 << 22, 1 << 24]
+# BASELINE configs 1 and 3: the benchmark's whole doubling sweep, 4 .. 67 108 864 elements
+# (runner.cc:338-362); SIZES=... overrides (comma-separated)
+sizes = ([int(x) for x in os.environ["SIZES"].split(",")] if os.environ.get("SIZES")
+         else [4 << k for k in range(25)])
 c1, c3 = [], []
 for n in sizes:
-    iters = 20 if n >= 1 << 22 else 50
+    iters = max(5, min(50, (1 << 27) // max(n, 1)))
+    sys.stderr.write(f"[host_path] n={n} iters={iters}\n")
+    sys.stderr.flush()
     if O.ref_available():
         c1.append({"impl": "reference (gloo, CPU sum)", **dist(O.ref_bench_ring(2, n, 3, iters), n)})
     c1.append({"impl": "hydra host runtime, GPU sum", **dist(host.bench(1, 2, n, 3, iters), n)})
