@@ -85,8 +85,10 @@ res["sync"] = {"wall_us_per_segment": w, "event_us_per_segment": e}
 
 g = torch.cuda.CUDAGraph()
 with torch.cuda.graph(g):
+    cs = torch.cuda.current_stream(dev).cuda_stream  # the capture stream, not `sp`
     for k in range(32):
-        single(k)
+        c, a, b = seg_ptrs(k)
+        _lib.check(L.hydra_chunk_sum(6, c, a, b, SEG, cs))
 torch.cuda.synchronize()
 
 
