@@ -649,10 +649,12 @@ hipError_t launch_fold_t(void* dst, const void* const* srcs, int nsrc, size_t n,
     case 5: return launch_fold_v<E, OP, ACC32, false, 1>(dst, srcs, nsrc, n, s, 0);  // full grid
     case 6: return launch_fold_v<E, OP, ACC32, true, 1>(dst, srcs, nsrc, n, s, 0);   // 3, XCD map
     case 7: return launch_fold_v<E, OP, ACC32, true, 1>(dst, srcs, nsrc, n, s, 8);   // 2, XCD map
-    default:  // tuned (profiles/r01_tune_fold_xcd.json): same-type folds plain loads, full grid,
-              // XCD-contiguous (P=8 fp32 6.75 TB/s); bf16->fp32 nontemporal, full grid (6.4)
+    default:  // tuned HBM-resident (profiles/r02_tune_fold_rot.json, 3 rotating source sets):
+              // same-type folds nontemporal loads, full grid, XCD-contiguous (variant 6: P=8
+              // fp32 46.5 us = 6.49 TB/s, vs 55.3 us for round 1's plain-load choice, which had
+              // won the MALL-assisted steady state); bf16->fp32 nontemporal, full grid (6.53)
       if constexpr (ACC32) return launch_fold_v<E, OP, ACC32, true>(dst, srcs, nsrc, n, s, 0);
-      else return launch_fold_v<E, OP, ACC32, false, 1>(dst, srcs, nsrc, n, s, 0);
+      else return launch_fold_v<E, OP, ACC32, true, 1>(dst, srcs, nsrc, n, s, 0);
   }
 }
 
