@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Summarise scripts/gpu_fold_pmc.sh output into profiles/r01_pmc_fold.json: per-launch kernel
+"""Summarise scripts/gpu_fold_pmc.sh output into profiles/<tag>_pmc_fold.json: per-launch kernel
 time (trace median) and HBM bytes (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE, KiB x1024,
 MI355X_MICROARCH.md §HBM) of the P-way fold at the BASELINE owner-block sizes, against the
 algorithmic (P + 1) x E bytes per element."""
@@ -10,9 +10,10 @@ import statistics
 import sys
 
 src = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/fold_pmc"
+tag = sys.argv[2] if len(sys.argv) > 2 else "r02"
 root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CASES = {  # kernel template marker -> (label, elements, algorithmic bytes per launch)
-    "k_fold<float, 0, false, false, 1>": ("config 4 owner block: P=8, 8 Mi fp32", 8 << 20,
+    "k_fold<float, 0, false, true, 1>": ("config 4 owner block: P=8, 8 Mi fp32", 8 << 20,
                                           9 * 4 * (8 << 20)),
     "k_fold<hydra::bf16_t, 0, true, true, 0>": ("config 5 owner block: P=8, 32 Mi bf16, fp32 "
                                                 "accumulate", 32 << 20, 9 * 2 * (32 << 20)),
@@ -44,6 +45,6 @@ for marker, (label, n, algo) in CASES.items():
         "fetch_size_kib_median": statistics.median(fs),
         "write_size_kib_median": statistics.median(ws),
         "hbm_bytes": hbm, "traffic_over_algorithmic": round(hbm / algo, 5)})
-with open(os.path.join(root, "profiles", "r01_pmc_fold.json"), "w") as f:
+with open(os.path.join(root, "profiles", f"{tag}_pmc_fold.json"), "w") as f:
     json.dump(out, f, indent=1)
 print(json.dumps(out, indent=1))

@@ -1,7 +1,7 @@
 #!/bin/bash
 # rocprofv3 kernel trace + separate FETCH_SIZE / WRITE_SIZE passes of the P-way fold kernel.
 set -u
-O=$PWD/gpurun_out/fold_pmc
+O=$PWD/gpurun_out/${1:-fold_pmc}
 mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o run -- python3 scripts/fold_pmc.py > $O/kt.log 2>&1 || { echo "kt rc=$?"; tail $O/kt.log; exit 1; }
