@@ -194,19 +194,28 @@ def cpu_baseline(n, seconds):
     a = np.arange(n, dtype=np.float32)
     b = np.ones(n, dtype=np.float32)
     kind = "reference" if O.ref_available() else "port"
-    # calibrate, then run ~`seconds` of work (3 repetitions, best mean)
-    if kind == "reference":
-        per = O.ref_time_sum(6, a, a, b, 1, 1)
-        iters = max(1, int(seconds / max(per, 1e-6) / 3))
-        per = O.ref_time_sum(6, a, a, b, iters, 3)
-    else:
-        t0 = time.perf_counter()
-        k = 0
-        while time.perf_counter() - t0 < seconds:
-            O.orc().orc_op(0, 6, a.ctypes.data, a.ctypes.data, b.ctypes.data, n)
-            k += 1
-        iters = k
-        per = (time.perf_counter() - t0) / k
+    # pinned to ONE host core for the measurement, restored afterwards
+    prev_aff = os.sched_getaffinity(0) if hasattr(os, "sched_getaffinity") else None
+    core = min(prev_aff) if prev_aff else None
+    if core is not None:
+        os.sched_setaffinity(0, {core})
+    try:
+        # calibrate, then run ~`seconds` of work (3 repetitions, best mean)
+        if kind == "reference":
+            per = O.ref_time_sum(6, a, a, b, 1, 1)
+            iters = max(1, int(seconds / max(per, 1e-6) / 3))
+            per = O.ref_time_sum(6, a, a, b, iters, 3)
+        else:
+            t0 = time.perf_counter()
+            k = 0
+            while time.perf_counter() - t0 < seconds:
+                O.orc().orc_op(0, 6, a.ctypes.data, a.ctypes.data, b.ctypes.data, n)
+                k += 1
+            iters = k
+            per = (time.perf_counter() - t0) / k
+    finally:
+        if core is not None:
+            os.sched_setaffinity(0, prev_aff)
     gbs = 12.0 * n / per / 1e9
     model = None
     try:
@@ -218,8 +227,8 @@ def cpu_baseline(n, seconds):
     return {"value": round(gbs, 3), "unit": "GB/s", "cores": 1, "kind": kind,
             "host_cpu": model, "host_logical_cpus": os.cpu_count(),
             "sample": f"gloo::sum<float> in place over {n} fp32 elements (the headline's size, "
-                      f"12 B/element), single thread, {iters} calls x 3 repetitions "
-                      f"(~{seconds:.0f} s), best-of-3 mean",
+                      f"12 B/element), single thread pinned to host core {core}, {iters} calls x "
+                      f"3 repetitions (~{seconds:.0f} s), best-of-3 mean",
             "per_call_ms": round(per * 1e3, 3)}
 
 
