@@ -434,7 +434,8 @@ def bench_allreduce(args, dev) -> dict:
         parity = {}
         tp = torch.empty(pn, dtype=torch.float32, device=dev)
         peer_register(tp)
-        for a in ("direct", "ring", "a2a", "peer2", "peer1"):
+        peer_algos = ("peer2", "peer1") if getattr(args, "peer", False) else ()
+        for a in ("direct", "ring", "a2a") + peer_algos:
             tp.copy_(torch.from_numpy(xs[rank]))
             try:
                 run(a, tp)
@@ -585,7 +586,7 @@ def bench_allreduce(args, dev) -> dict:
                            else "MISMATCH")
         k = max(5, args.steps // 4)
         for a in ("ring", "direct", "a2a", "rccl", "ring_old", "ring_chunked", "bcube",
-                  "halving_doubling", "peer2", "peer1"):
+                  "halving_doubling") + peer_algos:
             if a == chosen:
                 continue
 
