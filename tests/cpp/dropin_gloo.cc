@@ -1,7 +1,10 @@
 // tests/cpp/dropin_gloo.cc -- TEST HARNESS: the drop-in proven inside the reference itself.
 //
-// Runs the REFERENCE's own collectives -- gloo::allreduce's ring (gloo/gloo/allreduce.cc:147-422)
-// and the old-style gloo::AllreduceRing<T> (gloo/gloo/allreduce_ring.h:20-125) -- compiled from
+// Runs the REFERENCE's own collectives -- gloo::allreduce's ring (gloo/gloo/allreduce.cc:147-422,
+// its multi-input local reduce :46-83 with two pointers per rank), gloo::reduce
+// (gloo/gloo/reduce.cc:21-262, the Func's other new-style caller, :195), and the old-style
+// gloo::AllreduceRing<T> / AllreduceRingChunked<T> (allreduce_ring.h:20-125,
+// allreduce_ring_chunked.h:20-248) -- compiled from
 // /root/reference by oracle/Makefile into oracle/_ref/libgloo_ref.so, on thread-ranks with an
 // in-process HashStore and a loopback TCP device (the reference's own test setup,
 // gloo/gloo/test/base_test.h:73-156).  Each case runs twice on identical inputs:
@@ -16,7 +19,9 @@
 // Built by oracle/Makefile (it needs the reference headers, present only in the build
 // container); the binary travels to the GPU box, where tests/test_gpu_dropin.py runs it.
 //
-// usage: dropin_gloo <new_ring|old_ring> <P> <n> <f32|i32> [timed_iters] [max_segment]
+// usage: dropin_gloo <mode> <P> <n> <f32|i32> [timed_iters] [max_segment]
+//   mode: new_ring | new_ring2 (2 pointers per rank) | new_reduce (root P-1) | old_ring |
+//         old_ring_chunked
 // prints one JSON object on stdout; exit 0 iff both runs finished (equality is in the JSON).
 
 #include <algorithm>
@@ -37,6 +42,8 @@
 #include "gloo/algorithm.h"
 #include "gloo/allreduce.h"
 #include "gloo/allreduce_ring.h"
+#include "gloo/allreduce_ring_chunked.h"
+#include "gloo/reduce.h"
 #include "gloo/math.h"
 #include "gloo/rendezvous/context.h"
 #include "gloo/rendezvous/hash_store.h"
@@ -111,27 +118,46 @@ RunOut run_case(const std::string& mode, int P, size_t n, bool hydra, int iters,
         auto ctx = std::make_shared<gloo::rendezvous::Context>(r, P);
         ctx->connectFullMesh(store, dev);
         std::vector<T> x = make_input<T>(P, r, n);
+        std::vector<T> x2 = make_input<T>(P, r + P, n);  // new_ring2's second pointer
+        std::vector<T> rin = x;                          // new_reduce's input (out of place)
         std::function<void()> once;
-        std::unique_ptr<gloo::AllreduceRing<T>> old;
-        if (mode == "new_ring") {
+        std::unique_ptr<gloo::Algorithm> old;
+        // the drop-in: the gfx950 chunk-sum behind the Func / ReductionFunction plug-points
+        const gloo::AllreduceOptions::Func func =
+            hydra ? gloo::AllreduceOptions::Func(hydra::gloo_compat::hostSum<T>())
+                  : gloo::AllreduceOptions::Func(
+                        static_cast<void (*)(void*, const void*, const void*, size_t)>(&gloo::sum<T>));
+        const gloo::ReductionFunction<T>* fn =
+            hydra ? hydra::gloo_compat::gpuReductionFunction<gloo::ReductionFunction<T>, T>(gloo::SUM)
+                  : gloo::ReductionFunction<T>::sum;
+        if (mode == "new_ring" || mode == "new_ring2") {
           once = [&]() {
             gloo::AllreduceOptions o(ctx);
             o.setAlgorithm(gloo::AllreduceOptions::Algorithm::RING);
-            o.setOutput(x.data(), n);
-            if (ms) o.setMaxSegmentSize(ms);
-            if (hydra)  // the drop-in: the gfx950 chunk-sum behind AllreduceOptions::Func
-              o.setReduceFunction(hydra::gloo_compat::hostSum<T>());
+            if (mode == "new_ring2")  // two local inputs: the Func also pre-reduces (:61-80)
+              o.setOutputs(std::vector<T*>{x.data(), x2.data()}, n);
             else
-              o.setReduceFunction(
-                  gloo::AllreduceOptions::Func(static_cast<void (*)(void*, const void*, const void*, size_t)>(&gloo::sum<T>)));
+              o.setOutput(x.data(), n);
+            if (ms) o.setMaxSegmentSize(ms);
+            o.setReduceFunction(func);
             gloo::allreduce(o);
           };
+        } else if (mode == "new_reduce") {
+          once = [&]() {  // out of place to the last rank: reduce(out+off, in+off, tmp, n)
+            gloo::ReduceOptions o(ctx);
+            o.setInput(rin.data(), n);
+            o.setOutput(x.data(), n);
+            o.setRoot(P - 1);
+            if (ms) o.setMaxSegmentSize(ms);
+            o.setReduceFunction(func);
+            gloo::reduce(o);
+          };
         } else {
-          const gloo::ReductionFunction<T>* fn =
-              hydra ? hydra::gloo_compat::gpuReductionFunction<gloo::ReductionFunction<T>, T>(gloo::SUM)
-                    : gloo::ReductionFunction<T>::sum;
           std::vector<T*> ptrs{x.data()};
-          old.reset(new gloo::AllreduceRing<T>(ctx, ptrs, (int)n, fn));
+          if (mode == "old_ring_chunked")
+            old.reset(new gloo::AllreduceRingChunked<T>(ctx, ptrs, (int)n, fn));
+          else
+            old.reset(new gloo::AllreduceRing<T>(ctx, ptrs, (int)n, fn));
           once = [&]() { old->run(); };
         }
         bar.wait();
@@ -140,6 +166,9 @@ RunOut run_case(const std::string& mode, int P, size_t n, bool hydra, int iters,
           std::lock_guard<std::mutex> g(mu);
           out.bytes[r].assign(reinterpret_cast<uint8_t*>(x.data()),
                               reinterpret_cast<uint8_t*>(x.data()) + n * sizeof(T));
+          if (mode == "new_ring2")  // both outputs of the rank
+            out.bytes[r].insert(out.bytes[r].end(), reinterpret_cast<uint8_t*>(x2.data()),
+                                reinterpret_cast<uint8_t*>(x2.data()) + n * sizeof(T));
         }
         for (int it = 0; it < iters + 1; it++) {  // one untimed warm-up, then `iters`
           bar.wait();
@@ -229,13 +258,14 @@ int main(int argc, char** argv) {
   const size_t n = std::strtoull(argv[3], nullptr, 10);
   const int iters = argc > 5 ? std::atoi(argv[5]) : 0;
   const size_t ms = argc > 6 ? std::strtoull(argv[6], nullptr, 10) : 0;
-  if ((mode != "new_ring" && mode != "old_ring") || P < 1 || P > 16 || n < 1 ||
-      (dt != "f32" && dt != "i32")) {
+  const bool known = mode == "new_ring" || mode == "new_ring2" || mode == "new_reduce" ||
+                     mode == "old_ring" || mode == "old_ring_chunked";
+  if (!known || P < 1 || P > 16 || n < 1 || (dt != "f32" && dt != "i32")) {
     std::fprintf(stderr, "bad arguments\n");
     return 64;
   }
-  if (mode == "old_ring" && ms) {
-    std::fprintf(stderr, "max_segment applies to new_ring only\n");
+  if (mode.rfind("old_", 0) == 0 && ms) {
+    std::fprintf(stderr, "max_segment applies to the new-style collectives only\n");
     return 64;
   }
   return dt == "f32" ? run_all<float>(mode, P, n, iters, ms, "f32")

@@ -59,6 +59,33 @@ def test_reference_allreduce_ring_old_with_hydra_reduction_function(gpu, P, n, d
     assert j["mismatched_bytes"] == 0, j
 
 
+@pytest.mark.parametrize("P,n,ms", [(2, 1001, 128), (3, 262147, 0), (4, 1 << 20, 0)])
+def test_reference_allreduce_two_pointers_with_hydra_func(gpu, P, n, ms):
+    """Two local pointers per rank: the Func also pre-reduces the local inputs
+    (genLocalReduceFunction, allreduce.cc:46-83) before the ring; both outputs of every rank."""
+    j = dropin("new_ring2", P, n, ms=ms)
+    assert j["mismatched_bytes"] == 0, j
+
+
+@pytest.mark.parametrize("P,n,ms,dt", [(2, 100, 128, "f32"), (3, 4099, 128, "f32"),
+                                       (4, 1 << 20, 0, "f32"), (7, 262147, 0, "f32"),
+                                       (3, 100003, 4096, "i32")])
+def test_reference_reduce_with_hydra_func(gpu, P, n, ms, dt):
+    """gloo::reduce to the last rank (reduce.cc:21-262), the Func's other new-style caller
+    (reduce.cc:195, out of place): every rank's bytes, the non-roots' partial sums included."""
+    j = dropin("new_reduce", P, n, dt=dt, ms=ms)
+    assert j["mismatched_bytes"] == 0, j
+
+
+@pytest.mark.parametrize("P,n,dt", [(2, 1, "f32"), (3, 1000, "f32"), (5, 4099, "f32"),
+                                    (8, 1 << 20, "f32"), (4, 100003, "i32")])
+def test_reference_allreduce_ring_chunked_with_hydra_reduction_function(gpu, P, n, dt):
+    """old-style AllreduceRingChunked<T> (allreduce_ring_chunked.h:20-248) with the hydra
+    ReductionFunction<T>, incl. partial and empty chunks."""
+    j = dropin("old_ring_chunked", P, n, dt=dt)
+    assert j["mismatched_bytes"] == 0, j
+
+
 @pytest.mark.parametrize("n", [16 << 20, 64 << 20])
 def test_config1_full_size_inside_the_reference(gpu, n):
     """BASELINE config 1 at its top sizes (new_allreduce_ring, fp32, 2 ranks, loopback TCP):
