@@ -351,6 +351,61 @@ __global__ __launch_bounds__(kBlock) void k_fold(E* dst, FoldSrcs S, int nsrc, s
 }
 
 // -------------------------------------------------------------------------------------------
+// Persistent, software-pipelined variant (measurement: variants 45-47).  A capped grid of
+// CUs x W workgroups; each workgroup streams ONE contiguous range of tiles (XCD-contiguous
+// logical ids), loading tile k+1 while it adds and stores tile k, so every wave keeps its loads
+// in flight across tiles without the dispatcher launching a new workgroup per 4 KiB tile.
+// -------------------------------------------------------------------------------------------
+template <typename E, int OP>
+__global__ __launch_bounds__(kBlock) void k_reduce_pers(E* c_, const E* a_, const E* b_,
+                                                        size_t nvec, int head, int tail) {
+  constexpr int N = Vec<E>::N;
+  char* c = reinterpret_cast<char*>(c_);
+  const char* a = reinterpret_cast<const char*>(a_);
+  const char* b = reinterpret_cast<const char*>(b_);
+  const int t = threadIdx.x;
+  if (blockIdx.x == 0) {
+    if (t < head) {
+      const int i = t - head;
+      c_[i] = Elem<E, OP>::apply(a_[i], b_[i], a_[i]);
+    } else if (t >= 64 && t - 64 < tail) {
+      const size_t i = nvec * N + (size_t)(t - 64);
+      c_[i] = Elem<E, OP>::apply(a_[i], b_[i], a_[i]);
+    }
+  }
+  const uint32_t G = gridDim.x;
+  uint32_t L = blockIdx.x;
+  if ((G & 7) == 0) L = (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
+  const size_t ntiles = nvec / kBlock;
+  const size_t per = (ntiles + G - 1) / G;
+  const size_t t0 = std::min(ntiles, (size_t)L * per), t1 = std::min(ntiles, t0 + per);
+  if (t0 < t1) {
+    size_t off = (t0 * kBlock + t) * 16;
+    u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4_u*>(a + off));
+    u32x4 y = __builtin_nontemporal_load(reinterpret_cast<const u32x4_u*>(b + off));
+    for (size_t tile = t0; tile < t1; tile++) {
+      const size_t cur = off;
+      u32x4 xn = x, yn = y;
+      if (tile + 1 < t1) {  // block-uniform
+        off += (size_t)kBlock * 16;
+        xn = __builtin_nontemporal_load(reinterpret_cast<const u32x4_u*>(a + off));
+        yn = __builtin_nontemporal_load(reinterpret_cast<const u32x4_u*>(b + off));
+      }
+      __builtin_nontemporal_store(vapply<E, OP>(x, y, x), reinterpret_cast<u32x4*>(c + cur));
+      x = xn;
+      y = yn;
+    }
+  }
+  if (L == G - 1) {  // the ragged last tile (< kBlock vectors)
+    const size_t v = ntiles * kBlock + t;
+    if (v < nvec) {
+      const size_t o = v * 16;
+      st_a(c + o, vapply<E, OP>(ld_u(a + o), ld_u(b + o), ld_u(a + o)));
+    }
+  }
+}
+
+// -------------------------------------------------------------------------------------------
 // Batched chunk-sum: K independent segments c_k = op(a_k, b_k) in ONE launch.  A caller that
 // holds several arrived segments (consecutive ring segments, both rails of bew_allreduce_a)
 // pays one dispatch and one completion instead of K: below ~1 Mi elements a launch costs a
@@ -492,6 +547,20 @@ hipError_t launch_lds(void* c, const void* a, const void* b, size_t n, hipStream
 }
 
 template <typename E, int OP>
+hipError_t launch_pers(void* c, const void* a, const void* b, size_t n, hipStream_t s, int per_cu) {
+  const Split sp = split_call<E>(c, n);
+  E* cb = reinterpret_cast<E*>(c) + sp.head;
+  const E* ab = reinterpret_cast<const E*>(a) + sp.head;
+  const E* bb = reinterpret_cast<const E*>(b) + sp.head;
+  size_t grid = (size_t)cu_count() * per_cu;
+  const size_t tiles = (sp.nvec + kBlock - 1) / kBlock;
+  if (grid > tiles) grid = tiles ? tiles : 1;
+  hipLaunchKernelGGL((k_reduce_pers<E, OP>), dim3((unsigned)grid), dim3(kBlock), 0, s, cb, ab, bb,
+                     sp.nvec, sp.head, sp.tail);
+  return hipGetLastError();
+}
+
+template <typename E, int OP>
 hipError_t launch_shfl(void* c, const void* a, const void* b, size_t n, hipStream_t s) {
   const Split sp = split_call<E>(c, n);
   E* cb = reinterpret_cast<E*>(c) + sp.head;
@@ -569,6 +638,9 @@ hipError_t launch_tuning(int variant, void* c, const void* a, const void* b, siz
     case 42: return launch_t<E, OP, 1, kNT, kNT, kBlock, 1>(c, a, b, n, s, 0);     // 17, XCD map
     case 43: return launch_t<E, OP, 2, kNT, B | 16, kBlock, 1>(c, a, b, n, s, 0);  // 34, XCD map
     case 44: return launch_shfl<E, OP>(c, a, b, n, s);  // 40 + aligned loads, DPP realignment
+    case 45: return launch_pers<E, OP>(c, a, b, n, s, 4);   // persistent, pipelined, 4 WG/CU
+    case 46: return launch_pers<E, OP>(c, a, b, n, s, 8);   // 8 WG/CU
+    case 47: return launch_pers<E, OP>(c, a, b, n, s, 16);  // 16 WG/CU
     default: return launch_default<E, OP>(c, a, b, n, s);
   }
 }
