@@ -462,8 +462,9 @@ __global__ __launch_bounds__(kBlock) void k_reduce_batch(const BatchArgs args) {
     const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4_u*>(at + off));
     const u32x4 y = __builtin_nontemporal_load(reinterpret_cast<const u32x4_u*>(bt + off));
     const u32x4 z = g.c_old ? ld_u(ct + off) : x;
-    // nontemporal store, as the tuned chunk-sum (launch_default)
-    __builtin_nontemporal_store(vapply<E, OP>(x, y, z), reinterpret_cast<u32x4*>(ct + off));
+    // write-through (sc1) store through a block-uniform descriptor, as the tuned chunk-sum
+    const auto w = rsrc<kBuf | 16>(ct, kBlock * 16);
+    st<kBuf | 16>(ct, w, off, vapply<E, OP>(x, y, z));
   }
 }
 
@@ -578,14 +579,16 @@ hipError_t launch_shfl(void* c, const void* a, const void* b, size_t n, hipStrea
   return hipGetLastError();
 }
 
-// The tuned default: one 16-B vector per lane per operand, nontemporal loads
-// AND stores, tiles mapped XCD-contiguously (variant 42).  HBM-resident A/B (bench.py's
-// headline, 4 rotating buffer pairs; profiles/r02_tune_rotate.json): 122.7 us for 64 Mi fp32 in
-// place = 6.56 TB/s, ahead of round 1's sc1-store default (variant 40, 123.9 us), which had won
-// the MALL-assisted steady state of one buffer pair (profiles/r01_tune_xcd.json).
+// The tuned default: one 16-B vector per lane per operand, nontemporal loads,
+// write-through sc1 stores, tiles mapped XCD-contiguously (variant 40).  Fully HBM-resident
+// (bench.py's headline, 4 rotating buffer pairs; profiles/r02_tune_rotate*.json) nontemporal
+// stores (variant 42) are 1 % faster at 64 Mi; but wherever the working set can live in the
+// 256 MiB Infinity Cache -- ring chunks, 4-16 Mi buckets, a bucket reduced again soon -- the sc1
+// store keeps it there and wins by 16-38 % (profiles/r02_sweep_kernel_trace.txt vs
+// r01_sweep_kernel_trace.txt; one pair back to back 7.5 vs 6.2 TB/s).
 template <typename E, int OP>
 hipError_t launch_default(void* c, const void* a, const void* b, size_t n, hipStream_t s) {
-  return launch_t<E, OP, 1, kNT, kNT, kBlock, 1>(c, a, b, n, s, 0);
+  return launch_t<E, OP, 1, kNT, kBuf | 16, kBlock, 1>(c, a, b, n, s, 0);
 }
 
 template <typename E, int OP>
