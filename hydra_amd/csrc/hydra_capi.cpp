@@ -272,14 +272,20 @@ int hydra_reduce_host(hydra_ctx_t ctx, int op, int dtype, void* c, const void* a
   const size_t es = hydra::dtype_size(dtype);
   const size_t per = ctx->chunk_bytes / es;
   const int variant = g_variant.load(std::memory_order_relaxed);
-  // Zero-copy: when all three ranges are pinned/registered host memory (the ring's receive
-  // slots and output after hydra_host_register), the kernel streams them over PCIe directly --
-  // one pass, no staging copies.  kVariantForceStaging keeps the staged path for A/B.
+  // Each operand that is pinned/registered host memory (the ring's receive slots after
+  // Context::setScratchAllocator(pinnedAlloc), an output after hydra_host_register) is read or
+  // written by the kernel in place over PCIe (zero-copy); only the pageable ones are staged
+  // through device buffers.  All three pinned: one kernel pass, no copies at all.  The reference
+  // ring's own scratch is pageable (allreduce.cc:225), so with a registered bucket only b is
+  // staged.  kVariantForceStaging stages everything (A/B).
+  void* mc = nullptr;
+  void* ma = nullptr;
+  void* mb = nullptr;
   if (variant != kVariantForceStaging) {
-    void* mc = mapped_device_ptr(c);
-    void* ma = mc ? (a == c ? mc : mapped_device_ptr(a)) : nullptr;
-    void* mb = ma ? (b == c ? mc : mapped_device_ptr(b)) : nullptr;
-    if (mb) {
+    mc = mapped_device_ptr(c);
+    ma = a == c ? mc : mapped_device_ptr(a);
+    mb = b == c ? mc : (b == a ? ma : mapped_device_ptr(b));
+    if (mc && ma && mb) {
       hipError_t e = hydra::launch_reduce(0, op, dtype, mc, ma, mb, n, ctx->stream[0]);
       if (e != hipSuccess) return hip_fail(e, "reduce kernel launch (zero-copy)");
       HIP_TRY(hipStreamSynchronize(ctx->stream[0]));
@@ -292,21 +298,40 @@ int hydra_reduce_host(hydra_ctx_t ctx, int op, int dtype, void* c, const void* a
     const size_t bytes = cnt * es;
     const int s = (int)(k & 1);
     hipStream_t st = ctx->stream[s];
-    const char* pa = static_cast<const char*>(a) + off * es;
-    const char* pb = static_cast<const char*>(b) + off * es;
-    char* pc = static_cast<char*>(c) + off * es;
-    HIP_TRY(hipMemcpyAsync(ctx->da[s], pa, bytes, hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemcpyAsync(ctx->db[s], pb, bytes, hipMemcpyHostToDevice, st));
-    void* dc = ctx->da[s];  // in place on the staged a: c == a, the ring's form
-    if (dtype == HYDRA_FLOAT16 && c != a) {
-      // float16 stores depend on c's old bits (gloo store quirk): stage them too
-      if (!ctx->dc[s]) HIP_TRY(hipMalloc(&ctx->dc[s], ctx->chunk_bytes));
-      dc = ctx->dc[s];
-      HIP_TRY(hipMemcpyAsync(dc, pc, bytes, hipMemcpyHostToDevice, st));
+    const size_t ob = off * es;
+    const char* pa = static_cast<const char*>(a) + ob;
+    const char* pb = static_cast<const char*>(b) + ob;
+    char* pc = static_cast<char*>(c) + ob;
+    // operand a: mapped in place, else staged
+    const void* ka = ma ? static_cast<const void*>(static_cast<char*>(ma) + ob) : ctx->da[s];
+    if (!ma) HIP_TRY(hipMemcpyAsync(ctx->da[s], pa, bytes, hipMemcpyHostToDevice, st));
+    const void* kb;
+    if (b == a) {
+      kb = ka;
+    } else if (mb) {
+      kb = static_cast<char*>(mb) + ob;
+    } else {
+      HIP_TRY(hipMemcpyAsync(ctx->db[s], pb, bytes, hipMemcpyHostToDevice, st));
+      kb = ctx->db[s];
     }
-    hipError_t e = hydra::launch_reduce(variant, op, dtype, dc, ctx->da[s], ctx->db[s], cnt, st);
+    // destination: mapped in place; else in place on the staged a (c == a, the ring's form) or a
+    // staging buffer of its own -- which must hold c's old bits for float16's store quirk
+    void* kc;
+    bool copy_back = false;
+    if (mc) {
+      kc = static_cast<char*>(mc) + ob;
+    } else if (c == a) {
+      kc = ctx->da[s];  // (a is pageable too: c == a and mc == null)
+      copy_back = true;
+    } else {
+      if (!ctx->dc[s]) HIP_TRY(hipMalloc(&ctx->dc[s], ctx->chunk_bytes));
+      kc = ctx->dc[s];
+      if (dtype == HYDRA_FLOAT16) HIP_TRY(hipMemcpyAsync(kc, pc, bytes, hipMemcpyHostToDevice, st));
+      copy_back = true;
+    }
+    hipError_t e = hydra::launch_reduce(variant, op, dtype, kc, ka, kb, cnt, st);
     if (e != hipSuccess) return hip_fail(e, "reduce kernel launch");
-    HIP_TRY(hipMemcpyAsync(pc, dc, bytes, hipMemcpyDeviceToHost, st));
+    if (copy_back) HIP_TRY(hipMemcpyAsync(pc, kc, bytes, hipMemcpyDeviceToHost, st));
   }
   HIP_TRY(hipStreamSynchronize(ctx->stream[0]));
   HIP_TRY(hipStreamSynchronize(ctx->stream[1]));

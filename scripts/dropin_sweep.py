@@ -19,12 +19,24 @@ for n in sizes:
     iters = max(5, min(50, (1 << 27) // n))
     sys.stderr.write(f"[dropin_sweep] n={n} iters={iters}\n")
     sys.stderr.flush()
-    r = subprocess.run([EXE, "new_ring", "2", str(n), "f32", str(iters)], capture_output=True,
-                       text=True, timeout=600)
-    if r.returncode:
-        rows.append({"n": n, "error": (r.stdout + r.stderr)[-500:]})
+    row = {"n": n}
+    for reg in ("0", "1"):  # the hydra Func alone; and with the bucket registered once
+        r = subprocess.run([EXE, "new_ring", "2", str(n), "f32", str(iters)],
+                           capture_output=True, text=True, timeout=600,
+                           env=dict(os.environ, HYDRA_DROPIN_REGISTER=reg))
+        if r.returncode:
+            row["error"] = (r.stdout + r.stderr)[-500:]
+            break
+        j = json.loads(r.stdout.strip().splitlines()[-1])
+        if reg == "0":
+            row.update({k: j[k] for k in ("mismatched_bytes", "iters", "ref_ms", "hydra_ms")})
+        else:
+            row["mismatched_bytes_registered"] = j["mismatched_bytes"]
+            row["hydra_registered_ms"] = j["hydra_ms"]
+    rows.append(row)
+    if "error" in row:
         break
-    j = json.loads(r.stdout.strip().splitlines()[-1])
-    rows.append({k: j[k] for k in ("n", "mismatched_bytes", "iters", "ref_ms", "hydra_ms")})
 print(json.dumps({"harness": "tests/cpp/dropin_gloo new_ring P=2 f32 (reference ring, "
-                             "gloo::sum<float> vs hydra Func)", "rows": rows}))
+                             "gloo::sum<float> vs hydra Func; hydra_registered: the bucket "
+                             "hydra_host_register'ed once, HYDRA_DROPIN_REGISTER=1)",
+                  "rows": rows}))

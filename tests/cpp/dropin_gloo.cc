@@ -160,6 +160,16 @@ RunOut run_case(const std::string& mode, int P, size_t n, bool hydra, int iters,
             old.reset(new gloo::AllreduceRing<T>(ctx, ptrs, (int)n, fn));
           once = [&]() { old->run(); };
         }
+        // HYDRA_DROPIN_REGISTER=1: a maintainer who also registers the bucket once
+        // (hydra_host_register): the kernel then reads and writes it in place
+        // over PCIe and only the reference's pageable scratch is staged
+        const char* rg = std::getenv("HYDRA_DROPIN_REGISTER");
+        const bool reg = hydra && rg && rg[0] == '1';
+        if (reg) {
+          hydra::gloo_compat::enforce(hydra_host_register(x.data(), n * sizeof(T)));
+          if (mode == "new_ring2")
+            hydra::gloo_compat::enforce(hydra_host_register(x2.data(), n * sizeof(T)));
+        }
         bar.wait();
         once();
         {
@@ -180,6 +190,10 @@ RunOut run_case(const std::string& mode, int P, size_t n, bool hydra, int iters,
         }
         bar.wait();  // nobody closes its pairs while a peer still runs (base_test.h:142-155)
         old.reset();
+        if (reg) {
+          hydra_host_unregister(x.data());
+          if (mode == "new_ring2") hydra_host_unregister(x2.data());
+        }
       } catch (const std::exception& e) {
         std::lock_guard<std::mutex> g(mu);
         if (out.error.empty()) out.error = e.what();

@@ -22,10 +22,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 EXE = os.path.join(ROOT, "tests", "cpp", "dropin_gloo")
 
 
-def dropin(mode, P, n, dt="f32", iters=0, ms=0, timeout=240):
+def dropin(mode, P, n, dt="f32", iters=0, ms=0, timeout=240, register=False):
     assert os.path.exists(EXE), "built with the reference by oracle/Makefile (build())"
     args = [EXE, mode, str(P), str(n), dt, str(iters)] + ([str(ms)] if ms else [])
-    r = subprocess.run(args, capture_output=True, text=True, timeout=timeout)
+    env = dict(os.environ, HYDRA_DROPIN_REGISTER="1" if register else "0")
+    r = subprocess.run(args, capture_output=True, text=True, timeout=timeout, env=env)
     assert r.returncode == 0, r.stdout + r.stderr
     return json.loads(r.stdout.strip().splitlines()[-1])
 
@@ -92,4 +93,13 @@ def test_config1_full_size_inside_the_reference(gpu, n):
     the reference's ring with the hydra Func equals the reference's ring with gloo::sum<float>
     byte for byte at 16 Mi and 64 Mi elements (the published row is README.md:86)."""
     j = dropin("new_ring", 2, n, iters=1, timeout=600)
+    assert j["mismatched_bytes"] == 0, j
+
+
+@pytest.mark.parametrize("mode,P,n", [("new_ring", 2, 1 << 20), ("new_ring", 3, 4099),
+                                      ("new_ring2", 2, 262147), ("old_ring", 4, 100003)])
+def test_reference_with_hydra_func_registered_bucket(gpu, mode, P, n):
+    """The bucket registered once (hydra_host_register): the kernel reads and writes it in place
+    over PCIe while only the reference's pageable scratch is staged -- same bytes."""
+    j = dropin(mode, P, n, register=True)
     assert j["mismatched_bytes"] == 0, j

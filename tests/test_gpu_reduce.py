@@ -443,3 +443,56 @@ def test_reduce_batch_argument_checks(dev):
     rc = L.hydra_reduce_batch(0, 6, ctypes.cast(bad, ctypes.c_void_p), 2, None)
     assert rc == _lib.ERR_INVALID and b"segment 1" in L.hydra_last_error()
     assert L.hydra_reduce_batch(0, 6, None, 0, None) == 0
+
+
+@pytest.mark.parametrize("n", [1, 4099, 262144, (9 << 20) + 3])
+@pytest.mark.parametrize("pinned", ["a", "b", "c", "ab", "ac", "bc"])
+@pytest.mark.parametrize("code", [6, 8])
+def test_host_path_mixed_pinned(gpu, O, n, pinned, code):
+    """hydra_reduce_host with SOME operands registered: those are read / written by the kernel in
+    place over PCIe, the pageable ones staged -- e.g. a registered bucket with the reference
+    ring's pageable scratch (allreduce.cc:225) stages only b.  In place (c == a) and out of
+    place (float16 out of place reads c's old bits: the store quirk), over chunk boundaries."""
+    L = _lib.lib()
+    rng = np.random.default_rng(n + len(pinned) + code)
+    if code == 6:
+        a = synth.stress_f32(2, 0, n)
+        b = synth.stress_f32(2, 1, n)
+    else:
+        a = rng.integers(0, 1 << 16, n).astype(np.uint16)
+        b = rng.integers(0, 1 << 16, n).astype(np.uint16)
+    c0 = (rng.integers(0, 1 << 16, n).astype(np.uint16) if code == 8
+          else np.full(n, 3, np.float32))
+    ctx = HostContext(0)
+    regs = []
+    try:
+        for inplace in (True, False):
+            ha, hb, hc = a.copy(), b.copy(), (None if inplace else c0.copy())
+            tgt = {"a": ha, "b": hb, "c": ha if inplace else hc}
+            for k in set(pinned):
+                arr = tgt[k]
+                if any(arr is r for r in regs):
+                    continue
+                _lib.check(L.hydra_host_register(arr.ctypes.data, arr.nbytes))
+                regs.append(arr)
+            cptr = ha.ctypes.data if inplace else hc.ctypes.data
+            _lib.check(L.hydra_reduce_host(ctx.handle, 0, code, cptr, ha.ctypes.data,
+                                           hb.ctypes.data, n))
+            got = ha if inplace else hc
+            if inplace or code != 8:
+                exp = O.op(a, b, "sum", code)
+            else:  # float16 out of place: single device call with the same old bits of c
+                import torch
+
+                td = [torch.from_numpy(x.view(np.int16).copy()).to(gpu) for x in (a, b, c0)]
+                _lib.check(L.hydra_reduce(0, 8, td[2].data_ptr(), td[0].data_ptr(),
+                                          td[1].data_ptr(), n, None))
+                exp = td[2].cpu().numpy().view(np.uint16)
+            assert np.array_equal(bits(got), bits(exp)), (pinned, inplace)
+            for r in regs:
+                L.hydra_host_unregister(r.ctypes.data)
+            regs.clear()
+    finally:
+        for r in regs:
+            L.hydra_host_unregister(r.ctypes.data)
+        ctx.close()
