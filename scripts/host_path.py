@@ -41,13 +41,16 @@ ctx = HostContext(0)
 for n in (1 << 18, 1 << 22, 1 << 24):
     a = np.arange(n, dtype=np.float32)
     b = np.ones(n, dtype=np.float32)
-    for mode in ("pageable", "registered", "registered_zero_copy"):
+    for mode in ("pageable", "registered", "registered_zero_copy", "bucket_registered_b_pageable"):
         # "registered": staged copies on registered memory; "_zero_copy": the kernel reads and
         # writes the registered host ranges over PCIe directly (hydra_reduce_host's default
-        # whenever all three ranges are pinned/registered)
+        # whenever all three ranges are pinned/registered); "bucket_registered_b_pageable": only
+        # c == a registered (a bucket registered once), b pageable like the reference ring's
+        # scratch -- a and c in place over PCIe, b staged
         prev = L.hydra_set_variant(1000 if mode == "registered" else 0)
         if mode != "pageable":
             _lib.check(L.hydra_host_register(a.ctypes.data, a.nbytes))
+        if mode in ("registered", "registered_zero_copy"):
             _lib.check(L.hydra_host_register(b.ctypes.data, b.nbytes))
         reps = max(3, int(2e8 / (12 * n)))
         _lib.check(L.hydra_reduce_host(ctx.handle, 0, 6, a.ctypes.data, a.ctypes.data,
@@ -60,6 +63,7 @@ for n in (1 << 18, 1 << 22, 1 << 24):
         L.hydra_set_variant(prev)
         if mode != "pageable":
             L.hydra_host_unregister(a.ctypes.data)
+        if mode in ("registered", "registered_zero_copy"):
             L.hydra_host_unregister(b.ctypes.data)
         iso.append({"elements": n, "mode": mode, "us": round(dt * 1e6, 1),
                     "GBps_12B": round(12 * n / dt / 1e9, 2)})
