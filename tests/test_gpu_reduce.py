@@ -496,3 +496,59 @@ def test_host_path_mixed_pinned(gpu, O, n, pinned, code):
         for r in regs:
             L.hydra_host_unregister(r.ctypes.data)
         ctx.close()
+
+
+def test_chunk_sum_beyond_32bit_indices(gpu):
+    """Maximum sizes: a bucket of 2^32 + 33 int8 elements (indices past 2^32) and one of
+    2^31 + 5 fp32 elements (8 GiB, byte offsets past 2^33), through hydra_reduce and
+    hydra_reduce_batch: every element, including the ragged tail, summed exactly once."""
+    import torch
+
+    L = _lib.lib()
+    for n, dt, code in ((2 ** 32 + 33, torch.int8, 0), (2 ** 31 + 5, torch.float32, 6)):
+        a = torch.full((n,), 3, dtype=dt, device=gpu)
+        b = torch.full((n,), 4, dtype=dt, device=gpu)
+        marks = [0, 1, 2 ** 31 - 1, 2 ** 31, 2 ** 31 + 1, n - 2, n - 1] + \
+                ([2 ** 32 - 1, 2 ** 32, 2 ** 32 + 7] if n > 2 ** 32 else [])
+        for i, m in enumerate(marks):
+            a[m] = 10 + i
+        exp = torch.full((len(marks),), 4, dtype=dt, device=gpu) + \
+            torch.tensor([10 + i for i in range(len(marks))], dtype=dt, device=gpu)
+        _lib.check(L.hydra_reduce(0, code, a.data_ptr(), a.data_ptr(), b.data_ptr(), n, None))
+        torch.cuda.synchronize()
+        idx = torch.tensor(marks, device=gpu)
+        assert torch.equal(a[idx], exp), (n, a[idx], exp)
+        a[idx] = 7  # every other element is 3 + 4
+        assert int((a != 7).sum().item()) == 0, n
+        # the batched form: the same bucket as two segments split past the 2^31 boundary
+        a.fill_(3)
+        cut = 2 ** 31 + 3
+        es = a.element_size()
+        segs = (_lib.Segment * 2)(_lib.Segment(a.data_ptr(), a.data_ptr(), b.data_ptr(), cut),
+                                  _lib.Segment(a.data_ptr() + cut * es, a.data_ptr() + cut * es,
+                                               b.data_ptr() + cut * es, n - cut))
+        _lib.check(L.hydra_reduce_batch(0, code, ctypes.cast(segs, ctypes.c_void_p), 2, None))
+        torch.cuda.synchronize()
+        assert int((a != 7).sum().item()) == 0, ("batch", n)
+        del a, b
+        torch.cuda.empty_cache()
+
+
+def test_fold_beyond_32bit_indices(gpu):
+    """hydra_fold (the DIRECT owner step) over 2^31 + 5 fp32 elements, P = 3, in place on the
+    owner's own block: indices and byte offsets past 32 bits, ragged tail."""
+    import torch
+
+    L = _lib.lib()
+    n = 2 ** 31 + 5
+    srcs = [torch.full((n,), float(v), dtype=torch.float32, device=gpu) for v in (1.0, 2.0, 4.0)]
+    for m in (n - 1, 2 ** 31):
+        srcs[2][m] = 8.0
+    ptrs = (ctypes.c_void_p * 3)(*[t.data_ptr() for t in srcs])
+    _lib.check(L.hydra_fold(0, 6, 0, srcs[0].data_ptr(), ptrs, 3, n, None))
+    torch.cuda.synchronize()
+    d = srcs[0]
+    assert d[n - 1].item() == 11.0 and d[2 ** 31].item() == 11.0
+    d[n - 1] = 7.0
+    d[2 ** 31] = 7.0
+    assert int((d != 7.0).sum().item()) == 0
