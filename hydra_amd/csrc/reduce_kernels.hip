@@ -781,7 +781,8 @@ hipError_t launch_batch_t(const BatchSegDesc* segs, size_t count, hipStream_t st
       if (d.n == 0) continue;
       const Split sp = split_call<E>(d.c, d.n);
       const uint64_t tiles = std::max<uint64_t>(1, (sp.nvec + kBlock - 1) / kBlock);
-      if (blocks + tiles > 0x7fffffffull) break;
+      if (tiles > 0x7fffffffull) return hipErrorInvalidValue;  // > 2^39 elements: no such bucket
+      if (blocks + tiles > 0x7fffffffull) break;  // next launch
       BatchSeg& g = args.s[k++];
       g.c = static_cast<char*>(d.c) + (size_t)sp.head * sizeof(E);
       g.a = static_cast<const char*>(d.a) + (size_t)sp.head * sizeof(E);
