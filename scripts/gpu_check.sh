@@ -1,5 +1,6 @@
 #!/bin/bash
-# One GPU-box session: parity tests, bench, rocprofv3 kernel trace + PMC passes.
+# One GPU-box session: parity tests, rocprofv3 kernel trace + PMC passes (summarised on the box),
+# then the bench, which reads that summary for roofline.traffic.
 # Every GPU step runs under its own timeout; a crash/timeout/abort ends the script there.
 # Usage (via gpurun): bash scripts/gpu_check.sh [tag]
 set -u
@@ -30,9 +31,6 @@ nproc > "$OUT/host.txt"; grep -m1 "model name" /proc/cpuinfo >> "$OUT/host.txt" 
 if [ "${SKIP_TESTS:-0}" != "1" ]; then
   step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -p no:cacheprovider
 fi
-step bench 600 python bench.py --steps 200 --warmup 20 ${BENCH_ARGS:-}
-cp "$OUT/bench.log" "$OUT/bench.json" 2>/dev/null
-
 if [ "${SKIP_PROF:-0}" != "1" ]; then
   export TMPDIR=/tmp
   step rocprof_kt 600 rocprofv3 --kernel-trace --stats --output-format csv \
@@ -41,5 +39,11 @@ if [ "${SKIP_PROF:-0}" != "1" ]; then
       -d "$OUT/prof_fetch" -o run -- python3 "$ROOT/bench.py" --steps 20 --warmup 2 --no-cpu-baseline
   step rocprof_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv \
       -d "$OUT/prof_write" -o run -- python3 "$ROOT/bench.py" --steps 20 --warmup 2 --no-cpu-baseline
+  # the PMC summary of THESE kernel sources, written on the box before the bench reads it, so
+  # the bench line below carries roofline.traffic (profiles/ itself is not merged back:
+  # re-run scripts/pmc_summary.py on gpurun_out/<tag> in the build container to commit it)
+  python3 scripts/pmc_summary.py "$OUT" "${ROUND:-r02}" > "$OUT/pmc_summary.json" 2>&1 || true
 fi
+step bench 600 python bench.py --steps 200 --warmup 20 ${BENCH_ARGS:-}
+cp "$OUT/bench.log" "$OUT/bench.json" 2>/dev/null
 echo done >> "$OUT/status"
