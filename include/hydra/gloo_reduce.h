@@ -159,6 +159,16 @@ void hostSumInPlace(T* x, const T* y, size_t n) {
   enforce(hydra_reduce_host(lease.get(), HYDRA_SUM, dtype_of<T>(), x, x, y, n));
 }
 
+// Explicit-dtype form for element types that are not C++ arithmetic types: gloo::float16 (a
+// 2-byte struct, HYDRA_FLOAT16, with its store quirk) or a bf16 struct (HYDRA_BFLOAT16).
+template <typename T, int DTYPE>
+void hostSumInPlaceAs(T* x, const T* y, size_t n) {
+  static_assert(DTYPE == HYDRA_FLOAT16 || DTYPE == HYDRA_BFLOAT16 || sizeof(T) != 2,
+                "2-byte element types need HYDRA_FLOAT16 or HYDRA_BFLOAT16");
+  auto lease = ContextPool::instance().acquire();
+  enforce(hydra_reduce_host(lease.get(), HYDRA_SUM, DTYPE, x, x, y, n));
+}
+
 // --- an old-style ReductionFunction<T> whose fn is the GPU sum ------------------------------
 // Works for gloo::ReductionFunction<T> (algorithm.h:59-96) and hydra::ReductionFunction<T>
 // (include/hydra/allreduce.h):  gpuReductionFunction<gloo::ReductionFunction<float>, float>(
@@ -166,6 +176,15 @@ void hostSumInPlace(T* x, const T* y, size_t n) {
 template <typename RF, typename T, typename Enum>
 const RF* gpuReductionFunction(Enum sum) {
   static const RF fn(sum, &hostSumInPlace<T>);
+  return &fn;
+}
+
+// the same for explicit-dtype element types, e.g.
+//   gpuReductionFunctionAs<gloo::ReductionFunction<gloo::float16>, gloo::float16, HYDRA_FLOAT16>(
+//       gloo::SUM)
+template <typename RF, typename T, int DTYPE, typename Enum>
+const RF* gpuReductionFunctionAs(Enum sum) {
+  static const RF fn(sum, &hostSumInPlaceAs<T, DTYPE>);
   return &fn;
 }
 

@@ -19,7 +19,7 @@
 // Built by oracle/Makefile (it needs the reference headers, present only in the build
 // container); the binary travels to the GPU box, where tests/test_gpu_dropin.py runs it.
 //
-// usage: dropin_gloo <mode> <P> <n> <f32|i32> [timed_iters] [max_segment]
+// usage: dropin_gloo <mode> <P> <n> <f32|i32|f16> [timed_iters] [max_segment]
 //   mode: new_ring | new_ring2 (2 pointers per rank) | new_reduce (root P-1) | old_ring |
 //         old_ring_chunked
 // prints one JSON object on stdout; exit 0 iff both runs finished (equality is in the JSON).
@@ -48,6 +48,7 @@
 #include "gloo/rendezvous/context.h"
 #include "gloo/rendezvous/hash_store.h"
 #include "gloo/transport/tcp/device.h"
+#include "gloo/types.h"
 
 #include "hydra/gloo_reduce.h"
 
@@ -95,6 +96,36 @@ std::vector<int32_t> make_input<int32_t>(int P, int r, size_t n) {
   return x;
 }
 
+// gloo::float16 (types.h): uniform [-4, 4) through the reference's own conversion; the in-place
+// ring exercises float16's store quirk (types.h:112-130) on both sides
+template <>
+std::vector<gloo::float16> make_input<gloo::float16>(int P, int r, size_t n) {
+  std::mt19937 g(4321u + 97u * (unsigned)P + (unsigned)r);
+  std::uniform_real_distribution<float> u(-4.0f, 4.0f);
+  std::vector<gloo::float16> x(n);
+  for (auto& v : x) v = gloo::cpu_float2half_rn(u(g));
+  return x;
+}
+
+// the hydra plug-ins per element type: the Func and the old-style ReductionFunction<T>
+template <typename T>
+gloo::AllreduceOptions::Func hydra_func() {
+  return gloo::AllreduceOptions::Func(hydra::gloo_compat::hostSum<T>());
+}
+template <>
+gloo::AllreduceOptions::Func hydra_func<gloo::float16>() {
+  return gloo::AllreduceOptions::Func(hydra::gloo_compat::hostReduce(HYDRA_SUM, HYDRA_FLOAT16));
+}
+template <typename T>
+const gloo::ReductionFunction<T>* hydra_rf() {
+  return hydra::gloo_compat::gpuReductionFunction<gloo::ReductionFunction<T>, T>(gloo::SUM);
+}
+template <>
+const gloo::ReductionFunction<gloo::float16>* hydra_rf<gloo::float16>() {
+  return hydra::gloo_compat::gpuReductionFunctionAs<gloo::ReductionFunction<gloo::float16>,
+                                                    gloo::float16, HYDRA_FLOAT16>(gloo::SUM);
+}
+
 struct RunOut {
   std::vector<std::vector<uint8_t>> bytes;  // [rank] output after the first collective
   std::vector<double> iter_ms;              // rank 0, timed iterations
@@ -124,12 +155,10 @@ RunOut run_case(const std::string& mode, int P, size_t n, bool hydra, int iters,
         std::unique_ptr<gloo::Algorithm> old;
         // the drop-in: the gfx950 chunk-sum behind the Func / ReductionFunction plug-points
         const gloo::AllreduceOptions::Func func =
-            hydra ? gloo::AllreduceOptions::Func(hydra::gloo_compat::hostSum<T>())
+            hydra ? hydra_func<T>()
                   : gloo::AllreduceOptions::Func(
                         static_cast<void (*)(void*, const void*, const void*, size_t)>(&gloo::sum<T>));
-        const gloo::ReductionFunction<T>* fn =
-            hydra ? hydra::gloo_compat::gpuReductionFunction<gloo::ReductionFunction<T>, T>(gloo::SUM)
-                  : gloo::ReductionFunction<T>::sum;
+        const gloo::ReductionFunction<T>* fn = hydra ? hydra_rf<T>() : gloo::ReductionFunction<T>::sum;
         if (mode == "new_ring" || mode == "new_ring2") {
           once = [&]() {
             gloo::AllreduceOptions o(ctx);
@@ -274,7 +303,7 @@ int main(int argc, char** argv) {
   const size_t ms = argc > 6 ? std::strtoull(argv[6], nullptr, 10) : 0;
   const bool known = mode == "new_ring" || mode == "new_ring2" || mode == "new_reduce" ||
                      mode == "old_ring" || mode == "old_ring_chunked";
-  if (!known || P < 1 || P > 16 || n < 1 || (dt != "f32" && dt != "i32")) {
+  if (!known || P < 1 || P > 16 || n < 1 || (dt != "f32" && dt != "i32" && dt != "f16")) {
     std::fprintf(stderr, "bad arguments\n");
     return 64;
   }
@@ -282,6 +311,7 @@ int main(int argc, char** argv) {
     std::fprintf(stderr, "max_segment applies to the new-style collectives only\n");
     return 64;
   }
+  if (dt == "f16") return run_all<gloo::float16>(mode, P, n, iters, ms, "f16");
   return dt == "f32" ? run_all<float>(mode, P, n, iters, ms, "f32")
                      : run_all<int32_t>(mode, P, n, iters, ms, "i32");
 }

@@ -103,3 +103,19 @@ def test_reference_with_hydra_func_registered_bucket(gpu, mode, P, n):
     over PCIe while only the reference's pageable scratch is staged -- same bytes."""
     j = dropin(mode, P, n, register=True)
     assert j["mismatched_bytes"] == 0, j
+
+
+@pytest.mark.parametrize("mode,P,n,ms", [("new_ring", 2, 100, 128), ("new_ring", 3, 4099, 0),
+                                         ("new_ring", 8, 262147, 0), ("new_ring2", 3, 20011, 1024),
+                                         ("new_reduce", 4, 30011, 4096),
+                                         ("old_ring", 3, 4099, 0), ("old_ring", 5, 100003, 0),
+                                         ("old_ring_chunked", 4, 20011, 0)])
+def test_reference_float16_with_hydra(gpu, mode, P, n, ms):
+    """gloo::float16 inside the reference: its sum<float16> stores through float16::operator=,
+    whose `if (rhs != *this)` compares the new value with the OLD bits read as an integer
+    (types.h:112-130) -- the store quirk.  The hydra plug-ins (hostReduce(SUM, FLOAT16) as the
+    Func, gpuReductionFunctionAs<..., HYDRA_FLOAT16> as the ReductionFunction) reproduce it in
+    every call site: in-place ring hops, the two-pointer local reduce, gloo::reduce's out-of-place
+    form and the old-style rings."""
+    j = dropin(mode, P, n, dt="f16", ms=ms)
+    assert j["mismatched_bytes"] == 0, j
