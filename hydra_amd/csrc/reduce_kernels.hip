@@ -644,6 +644,11 @@ hipError_t launch_tuning(int variant, void* c, const void* a, const void* b, siz
     case 45: return launch_pers<E, OP>(c, a, b, n, s, 4);   // persistent, pipelined, 4 WG/CU
     case 46: return launch_pers<E, OP>(c, a, b, n, s, 8);   // 8 WG/CU
     case 47: return launch_pers<E, OP>(c, a, b, n, s, 16);  // 16 WG/CU
+    case 48: return launch_t<E, OP, 1, kNT, B | 17, kBlock, 1>(c, a, b, n, s, 0);  // st sc0 sc1
+    case 49: return launch_t<E, OP, 1, kNT, B | 19, kBlock, 1>(c, a, b, n, s, 0);  // st sc0 sc1 nt
+    case 50: return launch_t<E, OP, 1, kNT, B | 16, 128, 1>(c, a, b, n, s, 0);     // 40, 128 thr
+    case 51: return launch_t<E, OP, 1, kNT, B | 16, 64, 1>(c, a, b, n, s, 0);      // 40, 64 thr
+    case 52: return launch_t<E, OP, 1, B | 2, B | 16, kBlock, 1>(c, a, b, n, s, 0); // buffer nt ld
     default: return launch_default<E, OP>(c, a, b, n, s);
   }
 }
