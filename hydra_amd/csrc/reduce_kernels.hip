@@ -45,6 +45,7 @@ __global__ __launch_bounds__(BS) void k_reduce(E* c_, const E* a_, const E* b_, 
                                                int head, int tail) {
   constexpr int N = Vec<E>::N;
   constexpr size_t TILE = (size_t)BS * UNROLL;
+  static_assert(BS >= 128, "waves 0 and 1 of block 0 do the ragged head and tail");
   char* c = reinterpret_cast<char*>(c_);
   const char* a = reinterpret_cast<const char*>(a_);
   const char* b = reinterpret_cast<const char*>(b_);
@@ -647,7 +648,6 @@ hipError_t launch_tuning(int variant, void* c, const void* a, const void* b, siz
     case 48: return launch_t<E, OP, 1, kNT, B | 17, kBlock, 1>(c, a, b, n, s, 0);  // st sc0 sc1
     case 49: return launch_t<E, OP, 1, kNT, B | 19, kBlock, 1>(c, a, b, n, s, 0);  // st sc0 sc1 nt
     case 50: return launch_t<E, OP, 1, kNT, B | 16, 128, 1>(c, a, b, n, s, 0);     // 40, 128 thr
-    case 51: return launch_t<E, OP, 1, kNT, B | 16, 64, 1>(c, a, b, n, s, 0);      // 40, 64 thr
     case 52: return launch_t<E, OP, 1, B | 2, B | 16, kBlock, 1>(c, a, b, n, s, 0); // buffer nt ld
     default: return launch_default<E, OP>(c, a, b, n, s);
   }
