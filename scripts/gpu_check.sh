@@ -45,5 +45,5 @@ if [ "${SKIP_PROF:-0}" != "1" ]; then
   python3 scripts/pmc_summary.py "$OUT" "${ROUND:-r02}" > "$OUT/pmc_summary.json" 2>&1 || true
 fi
 step bench 600 python bench.py --steps 200 --warmup 20 ${BENCH_ARGS:-}
-cp "$OUT/bench.log" "$OUT/bench.json" 2>/dev/null
+tail -1 "$OUT/bench.log" > "$OUT/bench.json" 2>/dev/null  # the JSON line alone
 echo done >> "$OUT/status"
