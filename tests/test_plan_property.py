@@ -86,8 +86,6 @@ def test_old_style_plans_vs_reference(O, algo, P, n, ch, seed):
 @given(**geometry)
 def test_reduce_root_plan_vs_reference(O, P, n, ms, ch, seed):
     """gloo::reduce to a drawn root (reduce.cc:21-262): the root's bucket."""
-    from plan_interp import interpret  # noqa: F401  (run_plan_numpy drives it)
-
     root = seed % P
     xs = inputs(P, n, seed)
     plans, scr = [], 0
