@@ -92,7 +92,7 @@ int export_blob(hydra_peer* p, void* ptr, size_t bytes, void* out) {
   unsigned long long id = 0;
   HIP_TRY(hipPointerGetAttribute(&id, HIP_POINTER_ATTRIBUTE_BUFFER_ID,
                                  reinterpret_cast<hipDeviceptr_t>(base)));
-  // Register once: an allocation base this group exported before must still be the SAME
+  // Register once: an allocation base this group has an OPEN registration of must still be the SAME
   // allocation.  Freeing a registered bucket and exporting a new allocation at that address
   // while peers may still map the old one (round 1: peers read zeros/garbage after free +
   // re-register) is refused; hydra_peer_close the old registration on every rank first.
@@ -103,7 +103,6 @@ int export_blob(hydra_peer* p, void* ptr, size_t bytes, void* out) {
                 "(register a bucket once; hydra_peer_close it on every rank before freeing it)");
   hipIpcMemHandle_t h;
   HIP_TRY(hipIpcGetMemHandle(&h, base));
-  p->exported[base] = (uint64_t)id;
   Blob blob{};
   std::memcpy(blob.ipc, &h, kIpcBytes);
   blob.offset = (uint64_t)(q - b);
@@ -229,10 +228,13 @@ int hydra_peer_open(hydra_peer_t p, void* buf, size_t bytes, const void* handles
   hydra_peer::Reg reg{};
   reg.base = static_cast<char*>(buf);
   reg.bytes = bytes;
+  unsigned long long alloc_id = 0;
   {
     void* ab = nullptr;
     size_t asz = 0;
     HIP_TRY(hipMemGetAddressRange(&ab, &asz, buf));
+    HIP_TRY(hipPointerGetAttribute(&alloc_id, HIP_POINTER_ATTRIBUTE_BUFFER_ID,
+                                   reinterpret_cast<hipDeviceptr_t>(ab)));
     reg.alloc_base = ab;
   }
   reg.peer[p->rank] = reg.base;
@@ -251,6 +253,10 @@ int hydra_peer_open(hydra_peer_t p, void* buf, size_t bytes, const void* handles
       return rc;
     }
   }
+  // the export record starts once the registration is open on this rank (peers may map it
+  // from now on); hydra_peer_close ends it.  An export that never got opened (a collective
+  // register that failed elsewhere) leaves no record behind.
+  p->exported[reg.alloc_base] = (uint64_t)alloc_id;
   p->regs.push_back(reg);
   return ok();
 }
