@@ -92,8 +92,8 @@ int export_blob(hydra_peer* p, void* ptr, size_t bytes, void* out) {
   unsigned long long id = 0;
   HIP_TRY(hipPointerGetAttribute(&id, HIP_POINTER_ATTRIBUTE_BUFFER_ID,
                                  reinterpret_cast<hipDeviceptr_t>(base)));
-  // Register once: an allocation base this group has an OPEN registration of must still be the SAME
-  // allocation.  Freeing a registered bucket and exporting a new allocation at that address
+  // Register once: an allocation base with an OPEN registration in this group must still be
+  // the SAME allocation.  Freeing a registered bucket and exporting a new allocation there
   // while peers may still map the old one (round 1: peers read zeros/garbage after free +
   // re-register) is refused; hydra_peer_close the old registration on every rank first.
   auto ex = p->exported.find(base);
