@@ -85,6 +85,7 @@ struct hydra_ctx {
 namespace {
 constexpr size_t kChunkBytes = 8u << 20;
 constexpr int kVariantForceStaging = 1000;  // hydra_set_variant value: host path always stages
+constexpr int kVariantNoPinOnTheFly = 1001;  // pageable operands staged, not pinned per call
 
 void ctx_release(hydra_ctx* x) {
   for (int i = 0; i < 2; i++) {
@@ -245,20 +246,60 @@ int hydra_ctx_destroy(hydra_ctx_t ctx) {
 }
 
 namespace {
-// Device address of a pinned (hipHostMalloc) or registered (hipHostRegister) host byte, or null
-// for pageable memory.  The runtime reports the mapping of the allocation's base; interior
-// pointers keep their offset.
-void* mapped_device_ptr(const void* p) {
+// Device address of the host range [p, p + bytes) when ALL of it lies in one pinned
+// (hipHostMalloc) or registered (hipHostRegister) range, else null (pageable, or only partly
+// covered: a kernel must never stream past a registration's end).
+void* mapped_device_range(const void* p, size_t bytes) {
   hipPointerAttribute_t at{};
   if (hipPointerGetAttributes(&at, p) != hipSuccess) {
     (void)hipGetLastError();
     return nullptr;
   }
   if (at.type != hipMemoryTypeHost || !at.devicePointer) return nullptr;
+  void* start = nullptr;
+  size_t size = 0;
+  if (hipPointerGetAttribute(&start, HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR,
+                             reinterpret_cast<hipDeviceptr_t>(const_cast<void*>(p))) != hipSuccess ||
+      hipPointerGetAttribute(&size, HIP_POINTER_ATTRIBUTE_RANGE_SIZE,
+                             reinterpret_cast<hipDeviceptr_t>(const_cast<void*>(p))) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  const char* s0 = static_cast<const char*>(start);
+  const char* q = static_cast<const char*>(p);
+  if (q < s0 || bytes > size || (size_t)(q - s0) > size - bytes) return nullptr;
   if (!at.hostPointer) return at.devicePointer;
   return static_cast<char*>(at.devicePointer) +
          (static_cast<const char*>(p) - static_cast<const char*>(at.hostPointer));
 }
+
+// Pins a pageable operand for the duration of one call (hipHostRegister of exactly its range:
+// a few microseconds, and registrations of overlapping pages are independent of each other, so
+// concurrent callers -- the two rails of bew_allreduce_a -- cannot disturb one another), and
+// unpins it when the call is done.  Failure to pin leaves the operand to the staged path.
+struct TempPin {
+  void* host = nullptr;
+  void* dev = nullptr;
+  bool pin(const void* p, size_t bytes) {
+    if (hipHostRegister(const_cast<void*>(p), bytes, hipHostRegisterDefault) != hipSuccess) {
+      (void)hipGetLastError();
+      return false;
+    }
+    host = const_cast<void*>(p);
+    dev = mapped_device_range(p, bytes);
+    if (!dev) {
+      release();
+      return false;
+    }
+    return true;
+  }
+  void release() {
+    if (host) (void)hipHostUnregister(host);
+    host = nullptr;
+    dev = nullptr;
+  }
+  ~TempPin() { release(); }
+};
 }  // namespace
 
 int hydra_reduce_host(hydra_ctx_t ctx, int op, int dtype, void* c, const void* a, const void* b,
@@ -274,22 +315,40 @@ int hydra_reduce_host(hydra_ctx_t ctx, int op, int dtype, void* c, const void* a
   const int variant = g_variant.load(std::memory_order_relaxed);
   // Each operand that is pinned/registered host memory (the ring's receive slots after
   // Context::setScratchAllocator(pinnedAlloc), an output after hydra_host_register) is read or
-  // written by the kernel in place over PCIe (zero-copy); only the pageable ones are staged
-  // through device buffers.  All three pinned: one kernel pass, no copies at all.  The reference
-  // ring's own scratch is pageable (allreduce.cc:225), so with a registered bucket only b is
-  // staged.  kVariantForceStaging stages everything (A/B).
+  // written by the kernel in place over PCIe (zero-copy); an operand that cannot be pinned is
+  // staged through device buffers.  All three pinned: one kernel pass, no copies at all.
+  // kVariantForceStaging stages everything (A/B).
+  // Pageable operands are pinned for the call itself (TempPin: hipHostRegister of exactly the
+  // operand, ~4 us) so the kernel streams them too; where that fails they are staged.
+  // kVariantNoPinOnTheFly keeps pageable operands on the staged path (A/B).
+  const size_t nbytes = n * es;
   void* mc = nullptr;
   void* ma = nullptr;
   void* mb = nullptr;
+  TempPin pc_, pa_, pb_;
   if (variant != kVariantForceStaging) {
-    mc = mapped_device_ptr(c);
-    ma = a == c ? mc : mapped_device_ptr(a);
-    mb = b == c ? mc : (b == a ? ma : mapped_device_ptr(b));
+    const bool fly = variant != kVariantNoPinOnTheFly;
+    mc = mapped_device_range(c, nbytes);
+    if (!mc && fly && pc_.pin(c, nbytes)) mc = pc_.dev;
+    if (a == c) {
+      ma = mc;
+    } else {
+      ma = mapped_device_range(a, nbytes);
+      if (!ma && fly && pa_.pin(a, nbytes)) ma = pa_.dev;
+    }
+    if (b == c) {
+      mb = mc;
+    } else if (b == a) {
+      mb = ma;
+    } else {
+      mb = mapped_device_range(b, nbytes);
+      if (!mb && fly && pb_.pin(b, nbytes)) mb = pb_.dev;
+    }
     if (mc && ma && mb) {
       hipError_t e = hydra::launch_reduce(0, op, dtype, mc, ma, mb, n, ctx->stream[0]);
       if (e != hipSuccess) return hip_fail(e, "reduce kernel launch (zero-copy)");
       HIP_TRY(hipStreamSynchronize(ctx->stream[0]));
-      return ok();
+      return ok();  // the TempPins unpin here, after the kernel finished
     }
   }
   size_t k = 0;

@@ -41,14 +41,17 @@ ctx = HostContext(0)
 for n in (1 << 18, 1 << 22, 1 << 24):
     a = np.arange(n, dtype=np.float32)
     b = np.ones(n, dtype=np.float32)
-    for mode in ("pageable", "registered", "registered_zero_copy", "bucket_registered_b_pageable"):
+    for mode in ("pageable", "pageable_staged", "registered", "registered_zero_copy",
+                 "bucket_registered_b_pageable"):
         # "registered": staged copies on registered memory; "_zero_copy": the kernel reads and
         # writes the registered host ranges over PCIe directly (hydra_reduce_host's default
         # whenever all three ranges are pinned/registered); "bucket_registered_b_pageable": only
         # c == a registered (a bucket registered once), b pageable like the reference ring's
         # scratch -- a and c in place over PCIe, b staged
-        prev = L.hydra_set_variant(1000 if mode == "registered" else 0)
-        if mode != "pageable":
+        # "pageable": pinned for the call (hydra_reduce_host's default); "pageable_staged": the
+        # staged path for pageable operands (variant 1001)
+        prev = L.hydra_set_variant({"registered": 1000, "pageable_staged": 1001}.get(mode, 0))
+        if mode not in ("pageable", "pageable_staged"):
             _lib.check(L.hydra_host_register(a.ctypes.data, a.nbytes))
         if mode in ("registered", "registered_zero_copy"):
             _lib.check(L.hydra_host_register(b.ctypes.data, b.nbytes))
@@ -61,7 +64,7 @@ for n in (1 << 18, 1 << 22, 1 << 24):
                                            b.ctypes.data, n))
         dt = (time.perf_counter() - t0) / reps
         L.hydra_set_variant(prev)
-        if mode != "pageable":
+        if mode not in ("pageable", "pageable_staged"):
             L.hydra_host_unregister(a.ctypes.data)
         if mode in ("registered", "registered_zero_copy"):
             L.hydra_host_unregister(b.ctypes.data)

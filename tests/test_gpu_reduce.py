@@ -236,12 +236,15 @@ def test_ring_call_pattern(dev, O):
                 assert np.array_equal(bits(out[lo:hi]), bits(exp[lo:hi])), (P, n, q)
 
 
+@pytest.mark.parametrize("variant", [0, 1001])
 @pytest.mark.parametrize("n", [1, 1000, 3 * (1 << 20) + 7, 9 * (1 << 20)])
-def test_host_path(gpu, O, n):
-    """hydra_reduce_host: host buffers staged H2D -> kernel -> D2H over 8 MiB chunks."""
+def test_host_path(gpu, O, n, variant):
+    """hydra_reduce_host on pageable buffers: pinned for the call and streamed by the kernel
+    (default), or staged H2D -> kernel -> D2H over 8 MiB chunks (variant 1001)."""
     a = synth.stress_f32(2, 0, n)
     b = synth.stress_f32(2, 1, n)
     ctx = HostContext(0)
+    prev = _lib.lib().hydra_set_variant(variant)
     try:
         c = a.copy()
         _lib.check(_lib.lib().hydra_reduce_host(ctx.handle, 0, 6, c.ctypes.data, c.ctypes.data,
@@ -252,6 +255,7 @@ def test_host_path(gpu, O, n):
                                                 b.ctypes.data, n))
         assert np.array_equal(bits(c), bits(O.op(a, b, "sum", 6)))
     finally:
+        _lib.lib().hydra_set_variant(prev)
         ctx.close()
 
 
@@ -448,7 +452,8 @@ def test_reduce_batch_argument_checks(dev):
 @pytest.mark.parametrize("n", [1, 4099, 262144, (9 << 20) + 3])
 @pytest.mark.parametrize("pinned", ["a", "b", "c", "ab", "ac", "bc"])
 @pytest.mark.parametrize("code", [6, 8])
-def test_host_path_mixed_pinned(gpu, O, n, pinned, code):
+@pytest.mark.parametrize("variant", [0, 1001])
+def test_host_path_mixed_pinned(gpu, O, n, pinned, code, variant):
     """hydra_reduce_host with SOME operands registered: those are read / written by the kernel in
     place over PCIe, the pageable ones staged -- e.g. a registered bucket with the reference
     ring's pageable scratch (allreduce.cc:225) stages only b.  In place (c == a) and out of
@@ -465,6 +470,7 @@ def test_host_path_mixed_pinned(gpu, O, n, pinned, code):
           else np.full(n, 3, np.float32))
     ctx = HostContext(0)
     regs = []
+    prev = L.hydra_set_variant(variant)  # 1001: the pageable operands staged, not pinned per call
     try:
         for inplace in (True, False):
             ha, hb, hc = a.copy(), b.copy(), (None if inplace else c0.copy())
@@ -493,6 +499,7 @@ def test_host_path_mixed_pinned(gpu, O, n, pinned, code):
                 L.hydra_host_unregister(r.ctypes.data)
             regs.clear()
     finally:
+        L.hydra_set_variant(prev)
         for r in regs:
             L.hydra_host_unregister(r.ctypes.data)
         ctx.close()
