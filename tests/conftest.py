@@ -7,17 +7,17 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
-# Mitigation for the intermittent late-reported device fault: four faults in ~20
-# GPU sessions, each in a different multi-stream / multi-thread test, each surfacing only at a
-# HIP call AFTER the work's own synchronisation had returned success, none reproducible from an
-# out-of-bounds plan or kernel argument.  The two runtime paths that can fault after a
-# successful sync -- kernel arguments fetched from device memory before the host's
-# write-combined stores land (HIP_FORCE_DEV_KERNARG=1, the MI300-class default) and copies on
-# the SDMA engines -- are switched to host-memory kernel arguments and shader (blit) copies in
-# the test processes.  setdefault: an explicit setting from outside wins.  Must run before the
-# HIP runtime initialises (no torch import above this line).
+# Mitigation for the intermittent late-reported device fault: faults in a few of
+# ~20 GPU sessions, each in a different multi-stream / multi-thread test, each surfacing only at
+# a HIP call AFTER the work's own synchronisation had returned success, none reproducible from an
+# out-of-bounds plan or kernel argument.  One runtime path that can make a kernel read arguments
+# other than the ones it was launched with is kernel arguments fetched from device memory before
+# the host's write-combined stores land (HIP_FORCE_DEV_KERNARG=1, the default on this part);
+# the test processes use host-memory kernel arguments instead.  (Shader copies instead of SDMA,
+# HSA_ENABLE_SDMA=0, were tried in r02s and dropped: that session returned a wrong result in a
+# path whose D2H copy then went through the GPU's L2.)  setdefault: an explicit setting from
+# outside wins.  Must run before the HIP runtime initialises (no torch import above this line).
 os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "0")
-os.environ.setdefault("HSA_ENABLE_SDMA", "0")
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 

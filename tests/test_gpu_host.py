@@ -9,6 +9,20 @@ from hydra_amd import host, synth
 pytestmark = pytest.mark.gpu
 
 
+def assert_bits(got, exp, ctx):
+    """Bit-exact, and on a mismatch say how many elements differ and where (a stale chunk, a
+    torn tail and a single bad element read differently)."""
+    g, e = got.view(np.uint32), exp.view(np.uint32)
+    if np.array_equal(g, e):
+        return
+    bad = np.flatnonzero(g != e)
+    runs = np.split(bad, np.flatnonzero(np.diff(bad) != 1) + 1)
+    spans = [(int(r[0]), int(r[-1]) + 1) for r in runs[:8]]
+    raise AssertionError(f"{ctx}: {bad.size} of {g.size} elements differ; spans {spans}"
+                         f"{' ...' if len(runs) > 8 else ''}; got[:4] at first "
+                         f"{g[bad[0]:bad[0] + 4].tolist()} exp {e[bad[0]:bad[0] + 4].tolist()}")
+
+
 @pytest.mark.parametrize("P,n,ms", [(2, 100, 0), (2, 262145, 0), (3, 100003, 4096),
                                     (4, 1 << 20, 0)])
 def test_host_ring_gpu_reducer(gpu, O, P, n, ms):
@@ -174,7 +188,7 @@ def test_hip_allreduce_ring(gpu, O, workspace, P, nptr, n, dt):
         for r in range(P):
             for i in range(nptr):
                 got = ts[r][i].cpu().numpy()
-                assert np.array_equal(got.view(np.uint32), exp[r][0].view(np.uint32)), (r, i)
+                assert_bits(got, exp[r][0], (r, i, user_streams))
 
 
 def test_hip_allreduce_ring_rejects_host_pointers(gpu):
@@ -286,7 +300,7 @@ def test_hip_allreduce_ring_chunked(gpu, O, workspace, P, nptr, n, dt):
         for r in range(P):
             for i in range(nptr):
                 got = ts[r][i].cpu().numpy()
-                assert np.array_equal(got.view(np.uint32), exp[r][0].view(np.uint32)), (r, i)
+                assert_bits(got, exp[r][0], (r, i, user_streams))
 
 
 @pytest.mark.parametrize("workspace", ["host", "device"])
@@ -317,7 +331,7 @@ def test_hip_allreduce_halving_doubling(gpu, O, workspace, P, nptr, n, dt):
         for r in range(P):
             for i in range(nptr):
                 got = ts[r][i].cpu().numpy()
-                assert np.array_equal(got.view(np.uint32), exp[r][0].view(np.uint32)), (r, i)
+                assert_bits(got, exp[r][0], (r, i, user_streams))
 
 
 @pytest.mark.parametrize("P,nptr,n,dt", [(1, 1, 1000, "f32"), (1, 2, 262145, "f32"),
@@ -341,7 +355,7 @@ def test_hip_allreduce_local(gpu, O, P, nptr, n, dt):
         for r in range(P):
             for i in range(nptr):
                 got = ts[r][i].cpu().numpy()
-                assert np.array_equal(got.view(np.uint32), exp[r].view(np.uint32)), (r, i)
+                assert_bits(got, exp[r], (r, i, user_streams))
 
 
 @pytest.mark.parametrize("workspace", ["host", "device"])
@@ -371,7 +385,7 @@ def test_hip_allreduce_bcube(gpu, O, workspace, P, nptr, n, dt):
             want = exp if exp is not None else loc[r]
             for i in range(nptr):
                 got = ts[r][i].cpu().numpy()
-                assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), (r, i)
+                assert_bits(got, want, (r, i, user_streams))
 
 
 @pytest.mark.parametrize("n", [16 << 20, 64 << 20])
