@@ -234,10 +234,10 @@ class HipAllreduceRing {
   bool synchronize_outputs_;
   int device_ = -1;
   std::vector<hydra_stream_t> streams_, owned_;
-  detail::OutputFence fence_;  // declared last: destroyed first, before any scratch
   detail::Pinned boxes_[2], scratch_host_;
   detail::DeviceMem inbox_dev_, local_dev_;
   std::unique_ptr<gloo_compat::ContextPool::Lease> lease_;
+  detail::OutputFence fence_;  // declared last: destroyed first, before any scratch
 };
 
 // hydra::HipAllreduceRingChunked<T, W> -- the HIP analog of gloo::CudaAllreduceRingChunked<T, W>
@@ -365,10 +365,10 @@ class HipAllreduceRingChunked {
   bool synchronize_outputs_;
   int device_ = -1;
   std::vector<hydra_stream_t> streams_, owned_;
-  detail::OutputFence fence_;  // declared last: destroyed first, before any scratch
   detail::Pinned scratch_host_, inbox_[2];
   detail::DeviceMem inbox_dev_;
   std::unique_ptr<gloo_compat::ContextPool::Lease> lease_;
+  detail::OutputFence fence_;  // declared last: destroyed first, before any scratch
 };
 
 // hydra::HipAllreduceBcube<T, W> -- gloo::CudaAllreduceBcube<T, W> (cuda_allreduce_bcube.cc:
@@ -496,11 +496,11 @@ class HipAllreduceBcube {
   bool synchronize_outputs_;
   int device_ = -1;
   std::vector<hydra_stream_t> streams_, owned_;
-  detail::OutputFence fence_;  // declared last: destroyed first, before any scratch
   detail::Pinned scratch_host_;
   detail::DeviceMem local_dev_, inbox_dev_;
   std::vector<std::unique_ptr<detail::DeviceMem>> temps_;
   std::unique_ptr<gloo_compat::ContextPool::Lease> lease_;
+  detail::OutputFence fence_;  // declared last: destroyed first, before any scratch
 };
 
 // hydra::HipAllreduceLocal<T> -- gloo::CudaAllreduceLocal<T> (cuda_allreduce_local.cc:17-66):
@@ -691,10 +691,10 @@ class HipAllreduceHalvingDoubling {
   detail::HalvingDoublingGeometry geo_;
   int device_ = -1;
   std::vector<hydra_stream_t> streams_, owned_;
-  detail::OutputFence fence_;  // declared last: destroyed first, before any scratch
   detail::Pinned scratch_host_, inbox_;
   detail::DeviceMem inbox_dev_;
   std::unique_ptr<gloo_compat::ContextPool::Lease> lease_;
+  detail::OutputFence fence_;  // declared last: destroyed first, before any scratch
 };
 
 }  // namespace hydra
