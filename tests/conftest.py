@@ -18,6 +18,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # path whose D2H copy then went through the GPU's L2.)  setdefault: an explicit setting from
 # outside wins.  Must run before the HIP runtime initialises (no torch import above this line).
 os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "0")
+# The HIP runtime's error-level log (quiet unless something fails): a device fault is then
+# reported with its faulting address and reason in the failing test's captured stderr.
+os.environ.setdefault("AMD_LOG_LEVEL", "1")
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
