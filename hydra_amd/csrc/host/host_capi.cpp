@@ -164,6 +164,13 @@ int hip_ring(int P, int nptr, size_t n, void** bufs, int workspace, int user_str
       hydra::gloo_compat::enforce(hydra_stream_synchronize(s));
       hydra_stream_destroy(s);
     }
+    // the algorithm has been destroyed (its streams, events, pinned and device scratch freed):
+    // a device fault first reported here belongs to that teardown
+    int dev = 0;
+    if (n) hydra::gloo_compat::enforce(hydra_pointer_device(ptrs[0], &dev));
+    if (hydra_device_check(dev) != 0)
+      throw hydra::EnforceNotMet(std::string("after the algorithm's teardown: ") +
+                                 hydra_last_error());
   });
 }
 }  // namespace

@@ -360,16 +360,29 @@ int hydra_comm_destroy(hydra_comm_t c) {
   // Drain the DEVICE, not only cs/ks: the caller's stream may still hold waits on ev_cs/ev_ks
   // and on plan events (join_streams), and kernels of an earlier allreduce may still read the
   // scratch freed below.  Destroy is rare; a full drain is the safe order.
-  (void)hipDeviceSynchronize();
-  if (c->nccl) (void)ncclCommDestroy(c->nccl);
-  for (auto e : c->events) (void)hipEventDestroy(e);
+  // Every step is checked and the first failure returned (the rest still runs, so nothing
+  // leaks): a late-reported device fault then names the teardown step it first
+  // shows at, instead of surfacing in the caller's next HIP call.
+  int rc = 0;
+  auto step = [&rc](hipError_t e, const char* what) {
+    if (e != hipSuccess && !rc) rc = hydra::hip_fail(e, what);
+  };
+  step(hipDeviceSynchronize(), "comm teardown: hipDeviceSynchronize");
+  if (c->nccl) {
+    ncclResult_t r = ncclCommDestroy(c->nccl);
+    if (r != ncclSuccess && !rc)
+      rc = fail(HYDRA_ERR_HIP, std::string("comm teardown: ncclCommDestroy: ") +
+                                   ncclGetErrorString(r));
+  }
+  for (auto e : c->events) step(hipEventDestroy(e), "comm teardown: hipEventDestroy");
   for (auto e : {c->ev_start, c->ev_cs, c->ev_ks})
-    if (e) (void)hipEventDestroy(e);
-  if (c->cs) (void)hipStreamDestroy(c->cs);
-  if (c->ks) (void)hipStreamDestroy(c->ks);
-  if (c->scratch) (void)hipFree(c->scratch);
+    if (e) step(hipEventDestroy(e), "comm teardown: hipEventDestroy");
+  if (c->cs) step(hipStreamDestroy(c->cs), "comm teardown: hipStreamDestroy");
+  if (c->ks) step(hipStreamDestroy(c->ks), "comm teardown: hipStreamDestroy");
+  if (c->scratch) step(hipFree(c->scratch), "comm teardown: hipFree(scratch)");
+  step(hipDeviceSynchronize(), "comm teardown: hipDeviceSynchronize after the frees");
   delete c;
-  return ok();
+  return rc ? rc : ok();
 }
 
 }  // extern "C"
@@ -752,9 +765,23 @@ int simulate_impl(int algo, int root, int op, int dtype, int flags, int P, void*
   }
   SIM_TRY(hipStreamSynchronize(st));
   SIM_TRY(hipGetLastError());
-  cleanup();
 #undef SIM_TRY
-  return ok();
+  // Teardown, every step checked: the intermittent late-reported fault has so
+  // far surfaced at the first HIP call after a teardown like this one, so a fault reported here
+  // names the step it first shows at instead of surfacing in the caller's next call.
+  auto step = [](hipError_t e, const char* what) {
+    return e == hipSuccess ? 0 : hydra::hip_fail(e, what);
+  };
+  rc = step(hipDeviceSynchronize(), "simulate teardown: hipDeviceSynchronize before the frees");
+  for (auto& r : R) {
+    if (r.scratch && !rc) rc = step(hipFree(r.scratch), "simulate teardown: hipFree(scratch)");
+    else if (r.scratch) (void)hipFree(r.scratch);
+    r.scratch = nullptr;
+  }
+  hipError_t ed = hipStreamDestroy(st);
+  if (!rc) rc = step(ed, "simulate teardown: hipStreamDestroy");
+  if (!rc) rc = step(hipDeviceSynchronize(), "simulate teardown: hipDeviceSynchronize after the frees");
+  return rc ? rc : ok();
 }
 }  // namespace
 

@@ -222,9 +222,10 @@ class XgmiComm:
                                              scratch_bytes, s))
 
     def close(self) -> None:
+        """Destroy the communicator; raises if a teardown step reports a device error."""
         if self._h:
-            _lib.lib().hydra_comm_destroy(self._h)
-            self._h = ctypes.c_void_p()
+            h, self._h = self._h, ctypes.c_void_p()
+            check(_lib.lib().hydra_comm_destroy(h))
 
     def __del__(self):
         # never call into HIP/RCCL while the interpreter is finalizing (the runtime may be gone);
@@ -633,11 +634,18 @@ def bench_allreduce(args, dev) -> dict:
             state["result"] = lambda: _result(ms, lat_ms, others, c5)
             del xb
     finally:
-        if pg["peer"] is not None:
-            pg["peer"].close()
-        comm.close()
-        rail2.close()
-        dog.cancel()
+        errs = []
+        for closer in ((pg["peer"].close if pg["peer"] is not None else None), comm.close,
+                       rail2.close):
+            if closer is None:
+                continue
+            try:
+                closer()
+            except HydraError as e:  # a teardown fault fails the run, after every close ran
+                errs.append(e)
+        dog.cancel()  # (after the closes: a hung communicator teardown is still caught)
+        if errs:
+            raise errs[0]
     return _result(ms, lat_ms, others, c5)
 
 
