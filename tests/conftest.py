@@ -7,19 +7,11 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
-# Mitigation for the intermittent late-reported device fault: faults in a few of
-# ~20 GPU sessions, each in a different multi-stream / multi-thread test, each surfacing only at
-# a HIP call AFTER the work's own synchronisation had returned success, none reproducible from an
-# out-of-bounds plan or kernel argument.  One runtime path that can make a kernel read arguments
-# other than the ones it was launched with is kernel arguments fetched from device memory before
-# the host's write-combined stores land (HIP_FORCE_DEV_KERNARG=1, the default on this part);
-# the test processes use host-memory kernel arguments instead.  (Shader copies instead of SDMA,
-# HSA_ENABLE_SDMA=0, were tried in r02s and dropped: that session returned a wrong result in a
-# path whose D2H copy then went through the GPU's L2.)  setdefault: an explicit setting from
-# outside wins.  Must run before the HIP runtime initialises (no torch import above this line).
-os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "0")
-# The HIP runtime's error-level log (quiet unless something fails): a device fault is then
-# reported with its faulting address and reason in the failing test's captured stderr.
+# The HIP runtime's error-level log (quiet unless something fails): a device fault then leaves
+# the runtime's own report in the failing test's captured stderr.  setdefault: an
+# explicit setting from outside wins.  Must run before the HIP runtime initialises (no torch
+# import above this line).  (r02t-r02w ran the tests with host-memory kernel arguments,
+# HIP_FORCE_DEV_KERNARG=0, as a candidate mitigation; r02w faulted with it, so it was dropped.)
 os.environ.setdefault("AMD_LOG_LEVEL", "1")
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
