@@ -33,7 +33,7 @@ EXPORTS = [  # every symbol include/hydra_hip.h declares
     "hydra_free", "hydra_memcpy", "hydra_ring_plan",
     "hydra_comm_get_unique_id", "hydra_comm_init", "hydra_comm_destroy", "hydra_allreduce",
     "hydra_plan", "hydra_allreduce_simulate", "hydra_fold", "hydra_memcpy_async",
-    "hydra_malloc_host", "hydra_free_host", "hydra_pointer_device", "hydra_split_elements",
+    "hydra_malloc_host", "hydra_free_host", "hydra_cache_trim", "hydra_pointer_device", "hydra_split_elements",
     "hydra_apipe_allreduce", "hydra_apipe_allreduce_simulate", "hydra_comm_run_plan",
     "hydra_peer_create", "hydra_peer_connect", "hydra_peer_register", "hydra_peer_open",
     "hydra_peer_close", "hydra_peer_set_option", "hydra_peer_error", "hydra_peer_allreduce",
@@ -126,6 +126,7 @@ def _declare(L) -> None:
     L.hydra_memcpy_async.argtypes = [vp, vp, sz, vp]
     L.hydra_malloc_host.argtypes = [sz, ctypes.POINTER(vp)]
     L.hydra_free_host.argtypes = [vp]
+    L.hydra_cache_trim.argtypes = []
     L.hydra_pointer_device.argtypes = [vp, ctypes.POINTER(i)]
     L.hydra_split_elements.argtypes = [i, i, sz, ctypes.POINTER(sz), ctypes.POINTER(sz)]
     L.hydra_split_elements.restype = None

@@ -14,6 +14,7 @@
 
 #include "../../include/hydra_hip.h"
 #include "errors.h"
+#include "resource_cache.h"
 #include "reduce_kernels.h"
 #include "trace.h"
 
@@ -89,10 +90,10 @@ constexpr int kVariantNoPinOnTheFly = 1001;  // pageable operands staged, not pi
 
 void ctx_release(hydra_ctx* x) {
   for (int i = 0; i < 2; i++) {
-    if (x->stream[i]) (void)hipStreamDestroy(x->stream[i]);
-    if (x->da[i]) (void)hipFree(x->da[i]);
-    if (x->db[i]) (void)hipFree(x->db[i]);
-    if (x->dc[i]) (void)hipFree(x->dc[i]);
+    if (x->stream[i]) (void)hydra::release_stream(x->stream[i]);
+    if (x->da[i]) (void)hydra::cached_free(x->da[i]);
+    if (x->db[i]) (void)hydra::cached_free(x->db[i]);
+    if (x->dc[i]) (void)hydra::cached_free(x->dc[i]);
   }
 }
 }  // namespace
@@ -222,9 +223,9 @@ int hydra_ctx_create(int device, hydra_ctx_t* out) {
   x->chunk_bytes = kChunkBytes;
   hipError_t e = hipSetDevice(device);
   for (int i = 0; i < 2 && e == hipSuccess; i++) {
-    e = hipStreamCreateWithFlags(&x->stream[i], hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipMalloc(&x->da[i], kChunkBytes);
-    if (e == hipSuccess) e = hipMalloc(&x->db[i], kChunkBytes);
+    e = hydra::cached_stream(device, &x->stream[i]);
+    if (e == hipSuccess) e = hydra::cached_malloc(device, kChunkBytes, &x->da[i]);
+    if (e == hipSuccess) e = hydra::cached_malloc(device, kChunkBytes, &x->db[i]);
   }
   if (e != hipSuccess) {
     ctx_release(x);
@@ -383,7 +384,7 @@ int hydra_reduce_host(hydra_ctx_t ctx, int op, int dtype, void* c, const void* a
       kc = ctx->da[s];  // (a is pageable too: c == a and mc == null)
       copy_back = true;
     } else {
-      if (!ctx->dc[s]) HIP_TRY(hipMalloc(&ctx->dc[s], ctx->chunk_bytes));
+      if (!ctx->dc[s]) HIP_TRY(hydra::cached_malloc(ctx->device, ctx->chunk_bytes, &ctx->dc[s]));
       kc = ctx->dc[s];
       if (dtype == HYDRA_FLOAT16) HIP_TRY(hipMemcpyAsync(kc, pc, bytes, hipMemcpyHostToDevice, st));
       copy_back = true;
@@ -423,15 +424,14 @@ int hydra_host_unregister(void* ptr) {
 // ---- helpers --------------------------------------------------------------------------------
 int hydra_stream_create(int device, hydra_stream_t* out) {
   if (!out) return fail(HYDRA_ERR_INVALID, "null out");
-  HIP_TRY(hipSetDevice(device));
   hipStream_t s = nullptr;
-  HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  HIP_TRY(hydra::cached_stream(device, &s));
   *out = s;
   return ok();
 }
 
 int hydra_stream_destroy(hydra_stream_t s) {
-  if (s) HIP_TRY(hipStreamDestroy(static_cast<hipStream_t>(s)));
+  if (s) HIP_TRY(hydra::release_stream(static_cast<hipStream_t>(s)));
   return ok();
 }
 
@@ -443,7 +443,7 @@ int hydra_stream_synchronize(hydra_stream_t s) {
 int hydra_event_create(hydra_event_t* out) {
   if (!out) return fail(HYDRA_ERR_INVALID, "null out");
   hipEvent_t e = nullptr;
-  HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  HIP_TRY(hydra::cached_event(&e));
   *out = e;
   return ok();
 }
@@ -461,19 +461,23 @@ int hydra_event_synchronize(hydra_event_t e) {
 }
 
 int hydra_event_destroy(hydra_event_t e) {
-  if (e) HIP_TRY(hipEventDestroy(static_cast<hipEvent_t>(e)));
+  if (e) HIP_TRY(hydra::release_event(static_cast<hipEvent_t>(e)));
   return ok();
 }
 
 int hydra_malloc(int device, size_t bytes, void** out) {
   if (!out) return fail(HYDRA_ERR_INVALID, "null out");
-  HIP_TRY(hipSetDevice(device));
-  HIP_TRY(hipMalloc(out, bytes));
+  HIP_TRY(hydra::cached_malloc(device, bytes, out));
   return ok();
 }
 
 int hydra_free(void* p) {
-  if (p) HIP_TRY(hipFree(p));
+  if (p) HIP_TRY(hydra::cached_free(p));
+  return ok();
+}
+
+int hydra_cache_trim(void) {
+  HIP_TRY(hydra::trim_caches());
   return ok();
 }
 
@@ -491,12 +495,12 @@ int hydra_memcpy_async(void* dst, const void* src, size_t bytes, hydra_stream_t 
 
 int hydra_malloc_host(size_t bytes, void** out) {
   if (!out) return fail(HYDRA_ERR_INVALID, "null out");
-  HIP_TRY(hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault));
+  HIP_TRY(hydra::cached_malloc_host(bytes, out));
   return ok();
 }
 
 int hydra_free_host(void* p) {
-  if (p) HIP_TRY(hipHostFree(p));
+  if (p) HIP_TRY(hydra::cached_free_host(p));
   return ok();
 }
 

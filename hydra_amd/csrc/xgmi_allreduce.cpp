@@ -24,6 +24,7 @@
 
 #include "../../include/hydra_hip.h"
 #include "errors.h"
+#include "resource_cache.h"
 #include "reduce_kernels.h"
 #include "split_table.h"
 #include "trace.h"
@@ -204,7 +205,7 @@ namespace {
 int ensure_events(hydra_comm* c, size_t n) {
   while (c->events.size() < n) {
     hipEvent_t e;
-    HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    HIP_TRY(hydra::cached_event(&e));
     c->events.push_back(e);
   }
   return HYDRA_OK;
@@ -316,11 +317,11 @@ int hydra_comm_init(hydra_comm_t* out, int nranks, int rank, const void* id, int
     delete c;
     return nccl_fail(r, "ncclCommInitRank");
   }
-  hipError_t e = hipStreamCreateWithFlags(&c->cs, hipStreamNonBlocking);
-  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->ks, hipStreamNonBlocking);
-  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_start, hipEventDisableTiming);
-  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_cs, hipEventDisableTiming);
-  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_ks, hipEventDisableTiming);
+  hipError_t e = hydra::cached_stream(device, &c->cs);
+  if (e == hipSuccess) e = hydra::cached_stream(device, &c->ks);
+  if (e == hipSuccess) e = hydra::cached_event(&c->ev_start);
+  if (e == hipSuccess) e = hydra::cached_event(&c->ev_cs);
+  if (e == hipSuccess) e = hydra::cached_event(&c->ev_ks);
   if (e != hipSuccess) {
     hydra_comm_destroy(c);
     return hydra::hip_fail(e, "hydra_comm_init streams");
@@ -374,12 +375,12 @@ int hydra_comm_destroy(hydra_comm_t c) {
       rc = fail(HYDRA_ERR_HIP, std::string("comm teardown: ncclCommDestroy: ") +
                                    ncclGetErrorString(r));
   }
-  for (auto e : c->events) step(hipEventDestroy(e), "comm teardown: hipEventDestroy");
+  for (auto e : c->events) step(hydra::release_event(e), "comm teardown: release event");
   for (auto e : {c->ev_start, c->ev_cs, c->ev_ks})
-    if (e) step(hipEventDestroy(e), "comm teardown: hipEventDestroy");
-  if (c->cs) step(hipStreamDestroy(c->cs), "comm teardown: hipStreamDestroy");
-  if (c->ks) step(hipStreamDestroy(c->ks), "comm teardown: hipStreamDestroy");
-  if (c->scratch) step(hipFree(c->scratch), "comm teardown: hipFree(scratch)");
+    if (e) step(hydra::release_event(e), "comm teardown: release event");
+  if (c->cs) step(hydra::release_stream(c->cs), "comm teardown: release stream");
+  if (c->ks) step(hydra::release_stream(c->ks), "comm teardown: release stream");
+  if (c->scratch) step(hydra::cached_free(c->scratch), "comm teardown: release scratch");
   step(hipDeviceSynchronize(), "comm teardown: hipDeviceSynchronize after the frees");
   delete c;
   return rc ? rc : ok();
@@ -430,11 +431,10 @@ int prepare(hydra_comm* c, int* algo, int op, int dtype, int flags, void* buf, s
     c->waited = waited_set(c->plan);
     if (need > c->scratch_bytes) {
       // (re)allocation happens outside any capture: first call with a new geometry
-      HIP_TRY(hipDeviceSynchronize());
-      if (c->scratch) HIP_TRY(hipFree(c->scratch));
+      if (c->scratch) HIP_TRY(hydra::cached_free(c->scratch));  // (drains the device first)
       c->scratch = nullptr;
       c->scratch_bytes = 0;
-      HIP_TRY(hipMalloc(&c->scratch, need));
+      HIP_TRY(hydra::cached_malloc(c->device, need, &c->scratch));
       c->scratch_bytes = need;
     }
     rc = ensure_events(c, c->plan.size());
@@ -644,8 +644,8 @@ int simulate_impl(int algo, int root, int op, int dtype, int flags, int P, void*
   auto cleanup = [&]() {
     (void)hipDeviceSynchronize();
     for (auto& r : R)
-      if (r.scratch) (void)hipFree(r.scratch);
-    if (st) (void)hipStreamDestroy(st);
+      if (r.scratch) (void)hydra::cached_free(r.scratch);
+    if (st) (void)hydra::release_stream(st);
   };
 #define SIM_TRY(expr)                               \
   do {                                              \
@@ -658,9 +658,11 @@ int simulate_impl(int algo, int root, int op, int dtype, int flags, int P, void*
   } while (0)
 
   SIM_TRY(hipDeviceSynchronize());
-  SIM_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  int dev = 0;
+  SIM_TRY(hipGetDevice(&dev));
+  SIM_TRY(hydra::cached_stream(dev, &st));
   for (int r = 0; r < P; r++)
-    if (sbytes) SIM_TRY(hipMalloc(&R[r].scratch, sbytes));
+    if (sbytes) SIM_TRY(hydra::cached_malloc(dev, sbytes, reinterpret_cast<void**>(&R[r].scratch)));
   struct Posted {
     int rank;
     size_t idx;
@@ -774,12 +776,12 @@ int simulate_impl(int algo, int root, int op, int dtype, int flags, int P, void*
   };
   rc = step(hipDeviceSynchronize(), "simulate teardown: hipDeviceSynchronize before the frees");
   for (auto& r : R) {
-    if (r.scratch && !rc) rc = step(hipFree(r.scratch), "simulate teardown: hipFree(scratch)");
-    else if (r.scratch) (void)hipFree(r.scratch);
+    if (r.scratch && !rc) rc = step(hydra::cached_free(r.scratch), "simulate teardown: release scratch");
+    else if (r.scratch) (void)hydra::cached_free(r.scratch);
     r.scratch = nullptr;
   }
-  hipError_t ed = hipStreamDestroy(st);
-  if (!rc) rc = step(ed, "simulate teardown: hipStreamDestroy");
+  hipError_t ed = hydra::release_stream(st);
+  if (!rc) rc = step(ed, "simulate teardown: release stream");
   if (!rc) rc = step(hipDeviceSynchronize(), "simulate teardown: hipDeviceSynchronize after the frees");
   return rc ? rc : ok();
 }
@@ -814,11 +816,10 @@ int hydra_comm_run_plan(hydra_comm_t c, const hydra_plan_op_t* ops, size_t nops,
   rc = validate_plan(plan, c->nranks, es, buf_bytes, scratch_bytes);
   if (rc) return rc;
   if (scratch_bytes > c->scratch_bytes) {
-    HIP_TRY(hipDeviceSynchronize());
-    if (c->scratch) HIP_TRY(hipFree(c->scratch));
+    if (c->scratch) HIP_TRY(hydra::cached_free(c->scratch));  // (drains the device first)
     c->scratch = nullptr;
     c->scratch_bytes = 0;
-    HIP_TRY(hipMalloc(&c->scratch, scratch_bytes));
+    HIP_TRY(hydra::cached_malloc(c->device, scratch_bytes, &c->scratch));
     c->scratch_bytes = scratch_bytes;
   }
   c->plan = std::move(plan);

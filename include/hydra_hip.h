@@ -131,6 +131,15 @@ int hydra_host_register(void* ptr, size_t bytes);
 int hydra_host_unregister(void* ptr);
 
 /* ---- streams / memory helpers for C callers (the Python layer uses torch instead) -------- */
+/* Streams, events, device blocks and pinned blocks come from process-wide caches, like torch's
+ * caching allocator: a destroy / free first waits for the work that may still use the object
+ * (stream synchronise, event synchronise, device drain -- hipFree's own implicit
+ * synchronisation), then keeps it for the next create / malloc of the same kind, size class
+ * (64 KiB granules) and device.  At most 4 GiB of device blocks per device, 2 GiB of pinned
+ * blocks and 64 streams / events per device are kept; the rest is really released.  Pointers
+ * and handles the caches did not hand out are released directly.  hydra_cache_trim() really
+ * releases everything kept (e.g. before handing the memory to another allocator). */
+int hydra_cache_trim(void);
 int hydra_stream_create(int device, hydra_stream_t* out);
 int hydra_stream_destroy(hydra_stream_t s);
 int hydra_stream_synchronize(hydra_stream_t s);

@@ -1,0 +1,86 @@
+"""hydra's process-wide caches of streams, events, device and pinned blocks
+(hydra_amd/csrc/resource_cache.cpp, include/hydra_hip.h): a release keeps the object for the
+next request of the same kind, size class and device; hydra_cache_trim really releases
+everything kept; a released block is never handed out while work enqueued before its release
+may still use it."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from hydra_amd import _lib
+
+pytestmark = pytest.mark.gpu
+
+
+def _malloc(L, nbytes):
+    p = ctypes.c_void_p()
+    _lib.check(L.hydra_malloc(0, nbytes, ctypes.byref(p)))
+    return p
+
+
+def test_blocks_streams_events_are_reused_and_trimmed(gpu):
+    L = _lib.lib()
+    _lib.check(L.hydra_cache_trim())
+    a = _malloc(L, 3 << 20)
+    _lib.check(L.hydra_free(a))
+    b = _malloc(L, (3 << 20) - 100)  # same 64 KiB size class
+    assert b.value == a.value
+    c = _malloc(L, 5 << 20)  # another size class: a different block
+    assert c.value != b.value
+    for p in (b, c):
+        _lib.check(L.hydra_free(p))
+
+    h = ctypes.c_void_p()
+    _lib.check(L.hydra_malloc_host(1 << 20, ctypes.byref(h)))
+    _lib.check(L.hydra_free_host(h))
+    h2 = ctypes.c_void_p()
+    _lib.check(L.hydra_malloc_host(1 << 20, ctypes.byref(h2)))
+    assert h2.value == h.value
+    _lib.check(L.hydra_free_host(h2))
+
+    s = ctypes.c_void_p()
+    _lib.check(L.hydra_stream_create(0, ctypes.byref(s)))
+    e = ctypes.c_void_p()
+    _lib.check(L.hydra_event_create(ctypes.byref(e)))
+    _lib.check(L.hydra_event_record(e, s))
+    _lib.check(L.hydra_event_destroy(e))
+    e2 = ctypes.c_void_p()
+    _lib.check(L.hydra_event_create(ctypes.byref(e2)))
+    assert e2.value == e.value
+    _lib.check(L.hydra_event_destroy(e2))
+    _lib.check(L.hydra_stream_destroy(s))
+    s2 = ctypes.c_void_p()
+    _lib.check(L.hydra_stream_create(0, ctypes.byref(s2)))
+    assert s2.value == s.value
+    _lib.check(L.hydra_stream_destroy(s2))
+
+    _lib.check(L.hydra_cache_trim())
+    _lib.check(L.hydra_device_check(0))
+
+
+def test_released_block_waits_for_pending_work(gpu):
+    """A block released while a long reduce still writes it comes back only after that reduce:
+    the next owner's bytes are never overwritten by the previous owner's kernel."""
+    import torch
+
+    L = _lib.lib()
+    n = 32 << 20
+    nbytes = 4 * n
+    p = _malloc(L, nbytes)
+    s = ctypes.c_void_p()
+    _lib.check(L.hydra_stream_create(0, ctypes.byref(s)))
+    ones = torch.ones(n, dtype=torch.float32, device=gpu)
+    torch.cuda.synchronize()
+    for _ in range(8):  # queue a few hundred microseconds of writes into p on stream s
+        _lib.check(L.hydra_reduce(0, 6, p, ones.data_ptr(), ones.data_ptr(), n, s))
+    _lib.check(L.hydra_free(p))  # returns only once the device is drained
+    q = _malloc(L, nbytes)
+    assert q.value == p.value
+    zero = np.zeros(n, np.float32)
+    _lib.check(L.hydra_memcpy(q, zero.ctypes.data, nbytes))
+    back = np.empty(n, np.float32)
+    _lib.check(L.hydra_memcpy(back.ctypes.data, q, nbytes))
+    assert not back.any()
+    _lib.check(L.hydra_free(q))
+    _lib.check(L.hydra_stream_destroy(s))

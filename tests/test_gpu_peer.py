@@ -182,7 +182,9 @@ def test_register_refuses_a_changed_allocation(gpu):
     """Register once: a peer group refuses to export an address whose allocation
     changed since it was exported (freed and reallocated without hydra_peer_close), and accepts
     it again once the old registration is closed.  A 1-rank group in this process; the check
-    needs the allocator to hand back the freed address, which a same-size hipMalloc does."""
+    needs a NEW allocation at the freed address: hydra_free keeps the block in hydra's cache
+    (the same allocation comes back, which is safe), so the cache is trimmed first and a
+    same-size hipMalloc then hands the address back."""
     import ctypes
 
     L = _lib.lib()
@@ -199,6 +201,7 @@ def test_register_refuses_a_changed_allocation(gpu):
         _lib.check(L.hydra_peer_open(h, a, nbytes, blob))
         _lib.check(L.hydra_peer_register(h, a, nbytes, blob))  # same allocation again: fine
         _lib.check(L.hydra_free(a))
+        _lib.check(L.hydra_cache_trim())  # really free it
         b = ctypes.c_void_p()
         _lib.check(L.hydra_malloc(0, nbytes, ctypes.byref(b)))
         reused = b.value == a.value
