@@ -194,6 +194,7 @@ def test_register_refuses_a_changed_allocation(gpu):
     try:
         _lib.check(L.hydra_peer_connect(h, sig))
         nbytes = 64 << 20
+        _lib.check(L.hydra_cache_trim())  # nothing else kept: a's address is the one freed below
         a = ctypes.c_void_p()
         _lib.check(L.hydra_malloc(0, nbytes, ctypes.byref(a)))
         blob = ctypes.create_string_buffer(_lib.PEER_HANDLE_BYTES)
