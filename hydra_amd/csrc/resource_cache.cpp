@@ -5,6 +5,7 @@
 #include <mutex>
 #include <tuple>
 #include <unordered_map>
+#include <unordered_set>
 #include <utility>
 #include <vector>
 
@@ -31,11 +32,14 @@ struct Caches {
   std::mutex m;
   std::unordered_map<void*, BlockKey> live_blocks;  // handed out, not yet released
   std::multimap<BlockKey, void*> blocks;            // kept for reuse
+  std::unordered_set<void*> kept;                   // the pointers in `blocks`
   std::map<int, size_t> kept_bytes;                 // per device; -1 = pinned host
   std::unordered_map<hipStream_t, int> live_streams;
   std::multimap<int, hipStream_t> streams;
+  std::unordered_set<hipStream_t> kept_streams;
   std::unordered_map<hipEvent_t, int> live_events;
   std::multimap<int, hipEvent_t> events;
+  std::unordered_set<hipEvent_t> kept_events;
 };
 
 // Never destroyed: no HIP call may run from a static destructor after the runtime is gone.
@@ -64,13 +68,15 @@ hipError_t take_block(const BlockKey& k, void** out) {
     if (it != c.blocks.end()) {
       *out = it->second;
       c.blocks.erase(it);
+      c.kept.erase(*out);
       c.kept_bytes[k.host ? -1 : k.device] -= k.bytes;
       c.live_blocks[*out] = k;
       return hipSuccess;
     }
   }
   void* p = nullptr;
-  hipError_t e = k.host ? hipHostMalloc(&p, k.bytes, hipHostMallocDefault) : hipMalloc(&p, k.bytes);
+  hipError_t e =
+      k.host ? hipHostMalloc(&p, k.bytes, hipHostMallocDefault) : hipMalloc(&p, k.bytes);
   if (e != hipSuccess) return e;
   std::lock_guard<std::mutex> g(c.m);
   c.live_blocks[p] = k;
@@ -84,10 +90,12 @@ hipError_t give_block(void* p, bool host) {
   BlockKey k{};
   {
     std::lock_guard<std::mutex> g(c.m);
+    if (c.kept.count(p)) return hipErrorInvalidValue;  // released twice
     auto it = c.live_blocks.find(p);
     if (it == c.live_blocks.end() || it->second.host != host)  // not ours: release directly
       return host ? hipHostFree(p) : hipFree(p);
     k = it->second;
+    c.live_blocks.erase(it);  // a second release of p now fails above or below, never twice
   }
   // hipFree's implicit synchronisation: work enqueued before the release may still use p
   hipError_t e;
@@ -97,11 +105,11 @@ hipError_t give_block(void* p, bool host) {
   }
   {
     std::lock_guard<std::mutex> g(c.m);
-    c.live_blocks.erase(p);
     size_t& kept = c.kept_bytes[k.host ? -1 : k.device];
     if (e == hipSuccess && kept + k.bytes <= (k.host ? kMaxCachedHost : kMaxCachedDevice)) {
       kept += k.bytes;
       c.blocks.emplace(k, p);
+      c.kept.insert(p);
       return hipSuccess;
     }
   }
@@ -136,6 +144,7 @@ hipError_t cached_stream(int device, hipStream_t* out) {
     if (it != c.streams.end()) {
       *out = it->second;
       c.streams.erase(it);
+      c.kept_streams.erase(*out);
       c.live_streams[*out] = device;
       return hipSuccess;
     }
@@ -155,16 +164,18 @@ hipError_t release_stream(hipStream_t s) {
   int device;
   {
     std::lock_guard<std::mutex> g(c.m);
+    if (c.kept_streams.count(s)) return hipErrorInvalidValue;  // released twice
     auto it = c.live_streams.find(s);
     if (it == c.live_streams.end()) return hipStreamDestroy(s);
     device = it->second;
+    c.live_streams.erase(it);
   }
   hipError_t e = hipStreamSynchronize(s);
   {
     std::lock_guard<std::mutex> g(c.m);
-    c.live_streams.erase(s);
     if (e == hipSuccess && c.streams.count(device) < kMaxCachedHandles) {
       c.streams.emplace(device, s);
+      c.kept_streams.insert(s);
       return hipSuccess;
     }
   }
@@ -184,6 +195,7 @@ hipError_t cached_event(hipEvent_t* out) {
     if (it != c.events.end()) {
       *out = it->second;
       c.events.erase(it);
+      c.kept_events.erase(*out);
       c.live_events[*out] = device;
       return hipSuccess;
     }
@@ -203,16 +215,18 @@ hipError_t release_event(hipEvent_t ev) {
   int device;
   {
     std::lock_guard<std::mutex> g(c.m);
+    if (c.kept_events.count(ev)) return hipErrorInvalidValue;  // released twice
     auto it = c.live_events.find(ev);
     if (it == c.live_events.end()) return hipEventDestroy(ev);
     device = it->second;
+    c.live_events.erase(it);
   }
   hipError_t e = hipEventSynchronize(ev);  // its last record (if any) has completed
   {
     std::lock_guard<std::mutex> g(c.m);
-    c.live_events.erase(ev);
     if (e == hipSuccess && c.events.count(device) < kMaxCachedHandles) {
       c.events.emplace(device, ev);
+      c.kept_events.insert(ev);
       return hipSuccess;
     }
   }
@@ -231,6 +245,9 @@ hipError_t trim_caches() {
     blocks.swap(c.blocks);
     streams.swap(c.streams);
     events.swap(c.events);
+    c.kept.clear();
+    c.kept_streams.clear();
+    c.kept_events.clear();
     c.kept_bytes.clear();
   }
   hipError_t first = hipSuccess;

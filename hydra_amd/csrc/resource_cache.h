@@ -11,7 +11,9 @@
 //     while work enqueued before its release may still touch it); at most kMaxCachedDevice /
 //     kMaxCachedHost bytes are kept, the rest is really freed;
 //   * streams are synchronised and events waited on before they are kept (at most 64 each);
-//   * pointers the caches did not hand out are freed / destroyed directly;
+//   * pointers the caches did not hand out are freed / destroyed directly; releasing a kept
+//     object again (a double free) fails with hipErrorInvalidValue instead of freeing memory
+//     the cache would hand out later;
 //   * trim_caches() really frees everything kept (hydra_cache_trim in the C-ABI).
 // Every function returns the first HIP error it met (hipSuccess otherwise).
 #pragma once

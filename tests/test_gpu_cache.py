@@ -84,3 +84,27 @@ def test_released_block_waits_for_pending_work(gpu):
     assert not back.any()
     _lib.check(L.hydra_free(q))
     _lib.check(L.hydra_stream_destroy(s))
+
+
+def test_double_release_is_refused(gpu):
+    """Releasing a kept block / stream / event again fails (hipErrorInvalidValue) instead of
+    freeing what the cache would hand out next; the cache stays consistent."""
+    L = _lib.lib()
+    p = _malloc(L, 1 << 20)
+    _lib.check(L.hydra_free(p))
+    assert L.hydra_free(p) != 0
+    q = _malloc(L, 1 << 20)
+    assert q.value == p.value  # still handed out once, and only once
+    r = _malloc(L, 1 << 20)
+    assert r.value != q.value
+    for x in (q, r):
+        _lib.check(L.hydra_free(x))
+    s = ctypes.c_void_p()
+    _lib.check(L.hydra_stream_create(0, ctypes.byref(s)))
+    _lib.check(L.hydra_stream_destroy(s))
+    assert L.hydra_stream_destroy(s) != 0
+    e = ctypes.c_void_p()
+    _lib.check(L.hydra_event_create(ctypes.byref(e)))
+    _lib.check(L.hydra_event_destroy(e))
+    assert L.hydra_event_destroy(e) != 0
+    _lib.check(L.hydra_device_check(0))
