@@ -10,6 +10,16 @@ from hydra_amd import _lib, ring, synth
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(scope="module")
+def comm1(gpu):
+    """One 1-rank RCCL communicator shared by the executor tests that leave it usable (a
+    communicator per test would re-create RCCL's own buffers, streams and proxy thread each
+    time).  Tests that abort a communicator or capture one build their own."""
+    c = ring.XgmiComm(0, 1, gpu.index or 0, ring._rccl_unique_id())
+    yield c
+    c.close()
+
+
 def dev_bufs(gpu, xs, view=None):
     import torch
 
@@ -121,19 +131,14 @@ def test_simulated_ops_dtypes(gpu, O, op, name, code, dt):
                                   outs[0][0].view(f"u{got.itemsize}")), (algo, op, name)
 
 
-def test_allreduce_argument_checks(gpu):
+def test_allreduce_argument_checks(gpu, comm1):
     import torch
 
-    uid = ring._rccl_unique_id()
-    comm = ring.XgmiComm(0, 1, gpu.index or 0, uid)
-    try:
-        t = torch.zeros(16, device=gpu)
-        with pytest.raises(_lib.HydraError):
-            comm.allreduce_(t, dtype_code=42)
-        with pytest.raises(_lib.HydraError):
-            comm.allreduce_(t, dtype_code=_lib.FLOAT32, flags=_lib.ACC_F32)
-    finally:
-        comm.close()
+    t = torch.zeros(16, device=gpu)
+    with pytest.raises(_lib.HydraError):
+        comm1.allreduce_(t, dtype_code=42)
+    with pytest.raises(_lib.HydraError):
+        comm1.allreduce_(t, dtype_code=_lib.FLOAT32, flags=_lib.ACC_F32)
 
 
 @pytest.mark.parametrize("P,n", [(2, 1 << 20), (4, 1 << 22), (8, 1 << 23), (8, 1 << 16)])
@@ -396,7 +401,7 @@ def test_simulated_halving_doubling_large(gpu, O, P, n):
                                          ("bcube", 8, 1 << 20, 0), ("bcube", 6, 6 << 12, 0),
                                          ("halving_doubling", 8, 1 << 20, 0),
                                          ("a2a", 2, 1 << 20, 0), ("a2a", 8, 1 << 20, 0)])
-def test_rccl_executor_self_loop(gpu, O, algo, P, n, ch):
+def test_rccl_executor_self_loop(gpu, O, comm1, algo, P, n, ch):
     """The real RCCL executor on one GPU: rank 0's plan with every peer remapped to itself runs
     on a 1-rank communicator (RCCL send/recv-to-self), through the same groups, streams and
     event edges as on 8 GPUs (A2A: ncclAllToAll / ncclAllGather on the 1-rank communicator).
@@ -411,19 +416,15 @@ def test_rccl_executor_self_loop(gpu, O, algo, P, n, ch):
             o["peer"] = 0
     x = synth.stress_f32(P, 0, n)
     exp = run_plan_numpy(O, algo, [x], 0, ch, plans=[ops], scr=scr)[0]
-    comm = ring.XgmiComm(0, 1, gpu.index or 0, ring._rccl_unique_id())
-    try:
-        t = torch.from_numpy(x.copy()).to(gpu)
-        comm.run_plan_(ops, t, scr)
-        torch.cuda.synchronize()
-        assert np.array_equal(t.cpu().numpy().view(np.uint32), exp.view(np.uint32))
-        # a plan reaching outside the buffers is refused before anything is launched
-        bad = [dict(o) for o in ops]
-        bad[0]["off"] = 4 * n
-        with pytest.raises(_lib.HydraError):
-            comm.run_plan_(bad, t, scr)
-    finally:
-        comm.close()
+    t = torch.from_numpy(x.copy()).to(gpu)
+    comm1.run_plan_(ops, t, scr)
+    torch.cuda.synchronize()
+    assert np.array_equal(t.cpu().numpy().view(np.uint32), exp.view(np.uint32))
+    # a plan reaching outside the buffers is refused before anything is launched
+    bad = [dict(o) for o in ops]
+    bad[0]["off"] = 4 * n
+    with pytest.raises(_lib.HydraError):
+        comm1.run_plan_(bad, t, scr)
 
 
 def test_executor_graph_replay(gpu, O):
@@ -559,7 +560,7 @@ def test_simulated_reduce_root_int32_bf16(gpu, O):
     assert torch.equal(bb[1].view(torch.bfloat16), want)
 
 
-def test_reduce_root_public_entry(gpu):
+def test_reduce_root_public_entry(gpu, comm1):
     """hydra_reduce_root through a live 1-rank RCCL communicator: P = 1 is the identity
     (reduce.cc:52-58), and bad roots are refused before anything is enqueued.  (A remapped
     self-loop of the multi-rank plan, as for the allreduces, cannot run: the gather half only
@@ -567,14 +568,10 @@ def test_reduce_root_public_entry(gpu):
     import torch
 
     x = synth.stress_f32(2, 0, 100003)
-    comm = ring.XgmiComm(0, 1, gpu.index or 0, ring._rccl_unique_id())
-    try:
-        y = torch.from_numpy(x.copy()).to(gpu)
-        comm.reduce_(y, 0)
-        torch.cuda.synchronize()
-        assert np.array_equal(y.cpu().numpy().view(np.uint32), x.view(np.uint32))
-        for bad in (-1, 1):
-            with pytest.raises(_lib.HydraError):
-                comm.reduce_(y, bad)
-    finally:
-        comm.close()
+    y = torch.from_numpy(x.copy()).to(gpu)
+    comm1.reduce_(y, 0)
+    torch.cuda.synchronize()
+    assert np.array_equal(y.cpu().numpy().view(np.uint32), x.view(np.uint32))
+    for bad in (-1, 1):
+        with pytest.raises(_lib.HydraError):
+            comm1.reduce_(y, bad)
