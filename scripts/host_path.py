@@ -93,21 +93,41 @@ ref_fn = ctypes.cast(O.ref().ref_sum_f32, ctypes.c_void_p).value if O.ref_availa
 sizes = ([int(x) for x in os.environ["SIZES"].split(",")] if os.environ.get("SIZES")
          else [4 << k for k in range(25)])
 c1, c3 = [], []
+raw = {}  # impl -> [(elements, samples_ns)], for the reference-format tables (TABLE=path)
+
+
+def keep(impl, n, samples):
+    raw.setdefault(impl, []).append((n, samples))
+    return samples
+
+
 for n in sizes:
     iters = max(5, min(50, (1 << 27) // max(n, 1)))
     sys.stderr.write(f"[host_path] n={n} iters={iters}\n")
     sys.stderr.flush()
     if O.ref_available():
-        c1.append({"impl": "reference (gloo, CPU sum)", **dist(O.ref_bench_ring(2, n, 3, iters), n)})
-    c1.append({"impl": "hydra host runtime, GPU sum", **dist(host.bench(1, 2, n, 3, iters), n)})
+        c1.append({"impl": "reference (gloo, CPU sum)",
+                   **dist(keep("c1 reference", n, O.ref_bench_ring(2, n, 3, iters)), n)})
+    c1.append({"impl": "hydra host runtime, GPU sum",
+               **dist(keep("c1 hydra GPU sum", n, host.bench(1, 2, n, 3, iters)), n)})
     c1.append({"impl": "hydra host runtime, GPU sum zero-copy (pinned slots, registered out)",
-               **dist(host.bench(1, 2, n, 3, iters, pinned=True), n)})
+               **dist(keep("c1 hydra GPU sum zero-copy", n,
+                           host.bench(1, 2, n, 3, iters, pinned=True)), n)})
     if ref_fn:
         c3.append({"impl": "hydra split + reference gloo::sum (CPU)",
-                   **dist(host.bench(3, 2, n, 3, iters, reducer_fn=ref_fn), n)})
-    c3.append({"impl": "hydra split, GPU sum (H2D+sum+D2H)", **dist(host.bench(3, 2, n, 3, iters), n)})
+                   **dist(keep("c3 hydra split + reference sum", n,
+                               host.bench(3, 2, n, 3, iters, reducer_fn=ref_fn)), n)})
+    c3.append({"impl": "hydra split, GPU sum (H2D+sum+D2H)",
+               **dist(keep("c3 hydra GPU sum", n, host.bench(3, 2, n, 3, iters)), n)})
     c3.append({"impl": "hydra split, GPU sum zero-copy (pinned slots, registered out)",
                **dist(host.bench(3, 2, n, 3, iters, pinned=True), n)})
 out["config1_new_allreduce_ring_P2"] = c1
 out["config3_bew_allreduce_a_P2"] = c3
+if os.environ.get("TABLE"):  # the reference benchmark's own table per implementation
+    from hydra_amd import report
+
+    algo = {"c1": "new_allreduce_ring", "c3": "bew_allreduce_a"}
+    with open(os.environ["TABLE"], "w") as f:
+        for impl, rows in raw.items():
+            f.write(f"# {impl}\n" + report.table(algo[impl[:2]], 2, rows) + "\n\n")
 print(json.dumps(out))
