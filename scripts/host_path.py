@@ -2,7 +2,7 @@
 """Host-resident path measurements: what the reduction costs when the segment
 lives in host memory, as it does in the reference's TCP ring.
 
-  1. isolated: hydra_reduce_host on 262 144 / 4 Mi / 16 Mi fp32 elements, pageable vs
+  1. isolated: hydra_reduce_host on 262 144 / 4 Mi / 16 Mi fp32 elements (ISO_SIZES=...), pageable vs
      hipHostRegister'ed buffers, vs the reference's gloo::sum<float> on the same host core
   2. config 1: new_allreduce_ring, 2 ranks, loopback TCP, the whole 4 .. 64 Mi doubling sweep
      -- the reference itself (oracle/_ref, CPU sum) timed beside the hydra C++ host runtime with
@@ -38,7 +38,9 @@ except Exception:
 # 1. isolated
 iso = []
 ctx = HostContext(0)
-for n in (1 << 18, 1 << 22, 1 << 24):
+iso_sizes = ([int(x) for x in os.environ["ISO_SIZES"].split(",")] if os.environ.get("ISO_SIZES")
+             else [1 << 18, 1 << 22, 1 << 24])
+for n in iso_sizes:
     a = np.arange(n, dtype=np.float32)
     b = np.ones(n, dtype=np.float32)
     for mode in ("pageable", "pageable_staged", "registered", "registered_zero_copy",
@@ -92,6 +94,8 @@ ref_fn = ctypes.cast(O.ref().ref_sum_f32, ctypes.c_void_p).value if O.ref_availa
 # (runner.cc:338-362); SIZES=... overrides (comma-separated)
 sizes = ([int(x) for x in os.environ["SIZES"].split(",")] if os.environ.get("SIZES")
          else [4 << k for k in range(25)])
+if os.environ.get("SKIP_CONFIGS") == "1":  # the isolated measurements only
+    sizes = []
 c1, c3 = [], []
 raw = {}  # impl -> [(elements, samples_ns)], for the reference-format tables (TABLE=path)
 
