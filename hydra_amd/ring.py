@@ -670,7 +670,12 @@ def _bench_result(n, world, args, chosen, chunk, tuning, parity, full_ok, ms, la
                                + " (BASELINE config 4)", "elements": n, "algo": chosen,
                    ("peer_workgroups" if chosen in _lib.PEER_ALGOS else "chunk_bytes"): chunk,
                    "autotune_ms": tuning,
-                   "parallelism": f"dp{world}"},
+                   "parallelism": f"dp{world}",
+                   "scaling_note": "value = N x allreduce algbw of a fixed per-rank bucket "
+                                   "(weak scaling, xGMI-bound); bench.py at N = 1 reports the "
+                                   "HBM chunk-sum instead (BASELINE's metric names both), so "
+                                   "the N = 1 value is not the base of an allreduce efficiency "
+                                   "(DESIGN.md 7)"},
         "algbw_GBps": round(algbw, 2), "busbw_GBps": round(busbw, 2),
         "roofline": {"bound": "xgmi", "achieved": round(busbw, 2),
                      "peak": round(link * max(1, world - 1), 1), "unit": "GB/s",
