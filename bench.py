@@ -162,6 +162,43 @@ def time_chunk_sum(torch, L, dev, pairs, code, steps, warmup, per_launch=0, cold
     return wall, region_ms, ms, cold
 
 
+def hbm_ceiling(torch, dev, pairs, launches=40, rounds=3):
+    """What THIS HBM delivers, measured in the same run under the headline's rotation: two
+    pure read streams (2R) and a copy (1R1W) over the same buffer pairs, with the chunk-sum's
+    launch shape (hydra_amd/libhydra_probe.so, measurement-only kernels).  GB/s of algorithmic
+    bytes (8 B per element for both), median over `rounds`.  None if the probe library is
+    absent.  The copy overwrites each pair's b with a, so it runs after every chunk-sum leg."""
+    import ctypes
+
+    path = os.path.join(ROOT, "hydra_amd", "libhydra_probe.so")
+    if not os.path.exists(path):
+        return None
+    P = ctypes.CDLL(path)
+    vp = ctypes.c_void_p
+    P.hydra_probe_launch.argtypes = [ctypes.c_int, vp, vp, vp, vp, ctypes.c_size_t, vp]
+    n = pairs[0][0].numel()
+    s = torch.cuda.current_stream(dev)
+    sink = torch.empty(max(1, n // 1024), dtype=torch.float32, device=dev)
+    out = {}
+    for kind, name in ((0, "read_2R"), (1, "copy_1R1W")):
+        rates = []
+        for r in range(rounds + 1):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            for k in range(launches):
+                a, b = pairs[k % len(pairs)]
+                rc = P.hydra_probe_launch(kind, b.data_ptr(), a.data_ptr(), b.data_ptr(),
+                                          sink.data_ptr(), n, s.cuda_stream)
+                if rc:
+                    raise RuntimeError(f"hydra_probe_launch({kind}) failed: hipError {rc}")
+            e1.record(s)
+            torch.cuda.synchronize(dev)
+            if r:  # the first round warms up
+                rates.append(8.0 * n / (e0.elapsed_time(e1) / launches * 1e-3) / 1e9)
+        out[name] = round(float(np.median(rates)), 1)
+    return out
+
+
 def pmc_traffic():
     """HBM bytes per launch of the 64 Mi chunk-sum from the committed rocprofv3 PMC summary
     (profiles/pmc_chunk_sum.json, written by scripts/pmc_summary.py from separate --pmc
@@ -286,6 +323,19 @@ def run_single(args):
                                  "launches); part of its 512 MiB working set is served by the "
                                  "256 MiB Infinity Cache, so this is not an HBM rate"}},
     }
+    try:  # the ceiling this HBM delivers, same run, same rotation (after every chunk-sum leg)
+        ceil = hbm_ceiling(torch, dev, pairs)
+    except Exception as e:  # context for the roofline, never the product
+        ceil = {"error": str(e)}
+    if ceil and "read_2R" in ceil:
+        out["roofline"]["measured_ceiling"] = dict(
+            ceil, unit="GB/s", note="same run, same 4-pair rotation: two pure read streams and "
+                                   "a copy with the chunk-sum's launch shape "
+                                   "(hydra_amd/csrc/probe_kernels.hip); a 2-read + 1-write "
+                                   "stream cannot exceed the pure-read rate")
+        out["roofline"]["frac_of_measured_read_ceiling"] = round(achieved / ceil["read_2R"], 4)
+    elif ceil:
+        out["roofline"]["measured_ceiling"] = ceil
     del pairs
     if args.sweep:
         # config 2's size range: back-to-back launches, wall time per launch (what a caller
