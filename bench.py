@@ -334,6 +334,13 @@ def run_single(args):
                                    "(hydra_amd/csrc/probe_kernels.hip); a 2-read + 1-write "
                                    "stream cannot exceed the pure-read rate")
         out["roofline"]["frac_of_measured_read_ceiling"] = round(achieved / ceil["read_2R"], 4)
+        if ceil.get("copy_1R1W"):
+            # per-byte cost model fitted to the two probes: a read byte costs 1/read_2R, a
+            # written byte (8/copy - 4/read_2R)/4, so the chunk-sum's mix of 8 read + 4 written
+            # bytes per element is bounded by 12 / (4/read_2R + 8/copy_1R1W)
+            mix = 12.0 / (4.0 / ceil["read_2R"] + 8.0 / ceil["copy_1R1W"])
+            out["roofline"]["measured_ceiling"]["mix_2R1W_model"] = round(mix, 1)
+            out["roofline"]["frac_of_measured_mix_ceiling"] = round(achieved / mix, 4)
     elif ceil:
         out["roofline"]["measured_ceiling"] = ceil
     del pairs
