@@ -1,7 +1,7 @@
 // transport.cpp -- minimal TCP transport + rendezvous stores for the host runtime.
 //
 // One connected socket per pair (full mesh).  Each pair owns a writer thread (FIFO of posted
-// sends: header {slot, nbytes} + payload via writev) and a reader thread (reads a header, waits
+// sends: header {slot, nbytes} + payload via one sendmsg) and a reader thread (reads a header, waits
 // for the FIFO-next posted receive on that pair, then reads the payload straight into it).
 // Matching is FIFO per pair; slots are checked (a mismatch is a protocol error).
 
@@ -159,9 +159,16 @@ class Pair {
     for (auto& o : r) o->finish(e);
   }
 
+  // sendmsg with MSG_NOSIGNAL, not writev: a peer that died makes the write fail with EPIPE
+  // (-> "Connection closed by peer", IoException at the caller) instead of raising SIGPIPE,
+  // which would kill this whole process (the reference's tests ignore SIGPIPE process-wide for
+  // the same reason, gloo/gloo/test/main.cc:11-15; the library does not rely on its caller).
   bool writeAll(struct iovec* iov, int n) {
     while (n > 0) {
-      ssize_t w = ::writev(fd_, iov, n);
+      struct msghdr m {};
+      m.msg_iov = iov;
+      m.msg_iovlen = (size_t)n;
+      ssize_t w = ::sendmsg(fd_, &m, MSG_NOSIGNAL);
       if (w < 0) {
         if (errno == EINTR) continue;
         return false;

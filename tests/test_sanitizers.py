@@ -20,9 +20,11 @@ def test_host_runtime_sanitized(tmp_path, san):
     cmd = ["g++", "-std=c++17", "-O1", "-g", "-pthread", f"-fsanitize={san}",
            "-fno-omit-frame-pointer", "-I", os.path.join(ROOT, "include"), *SRCS, "-o", str(exe)]
     subprocess.check_call(cmd)
+    # the environment is passed through unchanged; an inherited preload list is tolerated
+    # (verify_asan_link_order=0) rather than edited
     env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1",
-               ASAN_OPTIONS="detect_leaks=1", UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1")
-    env.pop("LD_PRELOAD", None)
+               ASAN_OPTIONS="detect_leaks=1:verify_asan_link_order=0",
+               UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1")
     p = subprocess.run([str(exe)], capture_output=True, text=True, timeout=600, env=env)
     assert p.returncode == 0 and "OK" in p.stdout, (p.stdout[-2000:], p.stderr[-4000:])
     assert "ThreadSanitizer" not in p.stderr and "AddressSanitizer" not in p.stderr
