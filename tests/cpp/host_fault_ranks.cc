@@ -6,7 +6,11 @@
 // end: every survivor must leave with kExitWithIoException (10, multiproc_test.h:26), within
 // half the timeout after a kill and at the timeout after a stop.
 //
-// Usage: host_fault_ranks RANK SIZE STORE_DIR N TIMEOUT_MS [bigsend]
+// Usage: host_fault_ranks RANK SIZE STORE_DIR N TIMEOUT_MS [bigsend | gpu]
+// gpu (built with -DHYDRA_FAULT_GPU, tests/cpp/host_fault_ranks_gpu via hydra_amd/csrc/Makefile):
+// the reducer is the gfx950 chunk-sum behind the drop-in Func (gloo_compat::hostSum<float>) and
+// the ring's receive slots are pinned (gloo_compat::pinnedAlloc), the configuration the GPU host
+// path runs in; a survivor must still leave with IoException, its GPU state released by exit.
 // bigsend (SIZE 2): rank 0 never receives; rank 1 sends N floats to it, more than the socket
 // buffers hold, so its writer blocks inside the write until rank 0 is killed -- the write then
 // fails (EPIPE / ECONNRESET), which must surface as IoException, not as SIGPIPE.
@@ -22,6 +26,9 @@
 #include <vector>
 
 #include "hydra/allreduce.h"
+#ifdef HYDRA_FAULT_GPU
+#include "hydra/gloo_reduce.h"
+#endif
 
 namespace {
 constexpr int kExitWithIoException = 10;  // gloo/gloo/test/multiproc_test.h:26
@@ -45,6 +52,16 @@ int main(int argc, char** argv) {
     auto ctx = std::make_shared<hydra::Context>(rank, size);
     ctx->setTimeout(std::chrono::milliseconds(timeout_ms));
     ctx->connectFullMesh(store, "127.0.0.1");
+    const bool gpu = argc > 6 && std::string(argv[6]) == "gpu";
+#ifdef HYDRA_FAULT_GPU
+    if (gpu)
+      ctx->setScratchAllocator({&hydra::gloo_compat::pinnedAlloc, &hydra::gloo_compat::pinnedFree});
+#else
+    if (gpu) {
+      std::fprintf(stderr, "built without HYDRA_FAULT_GPU\n");
+      return 2;
+    }
+#endif
     std::vector<float> buf(n);
     if (argc > 6 && std::string(argv[6]) == "bigsend") {
       std::printf("ready\n");
@@ -62,7 +79,12 @@ int main(int argc, char** argv) {
       hydra::AllreduceOptions opts(ctx);
       opts.setAlgorithm(hydra::AllreduceOptions::RING);
       opts.setOutput(buf.data(), n);
-      opts.setReduceFunction(&sum_f32);
+#ifdef HYDRA_FAULT_GPU
+      if (gpu)
+        opts.setReduceFunction(hydra::gloo_compat::hostSum<float>());
+      else
+#endif
+        opts.setReduceFunction(&sum_f32);
       opts.setTag((uint32_t)(it & 0xffff));
       hydra::allreduce(opts);
       if (it == 0) {

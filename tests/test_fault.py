@@ -113,3 +113,27 @@ def test_blocked_write_to_a_killed_rank_raises_not_sigpipe(exe, tmp_path):
     procs[0].wait()
     assert codes == [K_EXIT_WITH_IO_EXCEPTION], (codes, errs)
     assert "Connection closed by peer 0" in errs[0], errs
+
+
+GPU_EXE = os.path.join(ROOT, "tests", "cpp", "host_fault_ranks_gpu")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("P", [2, 3])
+def test_io_errors_after_sigkill_gpu_reducer(tmp_path, P):
+    """The same SIGKILL test with the drop-in GPU Func (gloo_compat::hostSum<float>, the gfx950
+    chunk-sum) as the reducer and pinned receive slots, P processes sharing the GPU: every
+    survivor still leaves with IoException (10) within half the timeout -- a rank blocked in the
+    ring, with kernels, pinned memory and streams in use, is not wedged by a dead peer."""
+    if not os.path.exists(GPU_EXE):
+        pytest.fail(f"{GPU_EXE} missing: build() (hydra_amd/csrc/Makefile) makes it")
+    timeout_ms = 4000
+    procs = _spawn(GPU_EXE, tmp_path, P, 1 << 20, timeout_ms, "gpu")
+    time.sleep(0.05)
+    t0 = time.monotonic()
+    procs[0].send_signal(signal.SIGKILL)
+    codes, errs = _finish(procs, 60)
+    dt = time.monotonic() - t0
+    procs[0].wait()
+    assert codes == [K_EXIT_WITH_IO_EXCEPTION] * (P - 1), (codes, errs)
+    assert dt < timeout_ms / 2 / 1000, dt
