@@ -373,8 +373,15 @@ def expected_bcube_f32(xs: list[np.ndarray]) -> np.ndarray:
     return out
 
 
-def bench_allreduce(args, dev) -> dict:
-    """bench.py --gpus N (N > 1): BASELINE config 4 (fp32 64 Mi per rank) on this rank."""
+def bench_allreduce(args, dev, make_comm=None, sync=None) -> dict:
+    """bench.py --gpus N (N > 1): BASELINE config 4 (fp32 64 Mi per rank) on this rank.
+
+    make_comm() -> a communicator with XgmiComm's allreduce_ / reduce_ / apipe_allreduce_ /
+    close (default: an RCCL XgmiComm over this rank's GPU, its unique id broadcast over the
+    process group); sync() waits for this rank's enqueued work (default: the device).  The two
+    hooks let tests/test_bench_gloo.py run this whole orchestration -- parity self-checks,
+    autotune, timed region, context legs, JSON line -- at world size 2 and 3 on the CPU, with
+    the same plans executed over gloo p2p."""
     import torch
     import torch.distributed as dist
 
@@ -389,9 +396,14 @@ def bench_allreduce(args, dev) -> dict:
 
     state = {}  # "result": builds the JSON line once the headline measurement is complete
     dog = watchdog.start(rank, float(getattr(args, "watchdog_s", 420)), state)
-    uid = exchange_unique_id(rank, dev)
-    comm = XgmiComm(rank, world, dev.index, uid)
-    rail2 = XgmiComm(rank, world, dev.index, exchange_unique_id(rank, dev))  # apipe's 2nd rail
+    if make_comm is None:
+        def make_comm():
+            return XgmiComm(rank, world, dev.index, exchange_unique_id(rank, dev))
+    if sync is None:
+        def sync():
+            torch.cuda.synchronize(dev)
+    comm = make_comm()
+    rail2 = make_comm()  # apipe's 2nd rail
     from .peer import PeerComm
 
     pg = {"peer": None, "err": None}  # IPC-mapped buckets, one kernel per allreduce
@@ -443,7 +455,7 @@ def bench_allreduce(args, dev) -> dict:
             except HydraError as e:  # e.g. A2A with unequal blocks at this P
                 parity[a] = f"n/a: {e}"
                 continue
-            torch.cuda.synchronize(dev)
+            sync()
             ok = bool(np.array_equal(tp.cpu().numpy().view(np.uint32), exp.view(np.uint32)))
             ok_all = max_over_ranks(0.0 if ok else 1.0, dev) == 0.0
             if a.startswith("peer") and not peer_ok():
@@ -457,8 +469,6 @@ def bench_allreduce(args, dev) -> dict:
         peer_register(x)
         full_exp = torch.from_numpy(((j % 1024) * (world * (world + 1) // 2))
                                     .astype(np.float32)).to(dev)
-        sync = lambda: torch.cuda.synchronize(dev)  # noqa: E731
-
         def full_exact(a, ch=0):
             x.copy_(x0)
             run(a, x, ch)
@@ -548,7 +558,7 @@ def bench_allreduce(args, dev) -> dict:
             try:
                 t = torch.from_numpy(xs[rank].copy()).to(dev)
                 call(t)
-                torch.cuda.synchronize(dev)
+                sync()
                 ok = expect is None or bool(np.array_equal(t.cpu().numpy().view(np.uint32),
                                                            expect.view(np.uint32)))
             except HydraError as e:  # argument errors are the same on every rank

@@ -1,0 +1,157 @@
+"""CPU executor of the device allreduce plans over torch.distributed gloo (test infrastructure).
+
+`execute` runs one rank's op list (hydra_plan / hydra_reduce_root_plan, xgmi_plan.h) on a CPU
+bucket with real inter-process p2p: SEND/RECV groups through batch_isend_irecv, ALLTOALL as
+p2p (gloo has no alltoall), ALLGATHER through all_gather, and REDUCE / FOLD through the
+oracle's element ops in the kernels' fold order (the C restatement standing in for the HIP
+kernels).  `GlooPlanComm` wraps it in XgmiComm's interface, so the N>1 bench orchestration
+(hydra_amd.ring.bench_allreduce) runs unchanged at world size 2 and 3 on the CPU."""
+import numpy as np
+
+SEND, RECV, GROUP, REDUCE, FOLD, ALLTOALL, ALLGATHER = 1, 2, 3, 4, 5, 6, 7
+_NP = {4: np.int32, 6: np.float32}  # dtype codes the executor folds (hydra_dtype_t INT32, FLOAT32)
+
+
+def fold_slot(o, j):
+    """xgmi_plan.h fold_slot: scratch offset of contribution j of a FOLD."""
+    if o["peer"] < 0:
+        return o["src_off"] + (j - 1) * o["slot_stride"]
+    return o["src_off"] + ((o["peer"] + j) % o["nsrc"]) * o["slot_stride"]
+
+
+def execute(O, ops, scratch_bytes, user, code=6, op="sum"):
+    """Run `ops` on `user` (a contiguous CPU uint8 tensor, modified in place) on this rank."""
+    import torch
+    import torch.distributed as dist
+
+    rank, world = dist.get_rank(), dist.get_world_size()
+    dt = _NP[code]
+    scratch = torch.zeros(scratch_bytes + 16, dtype=torch.uint8)
+    i = 0
+    while i < len(ops):
+        o = ops[i]
+        if o["kind"] == ALLTOALL:  # ncclAllToAll semantics via p2p
+            B = o["bytes"]
+            scratch[o["src_off"] + rank * B:o["src_off"] + (rank + 1) * B] = \
+                user[o["off"] + rank * B:o["off"] + (rank + 1) * B]
+            p2p = []
+            for pr in range(world):
+                if pr == rank:
+                    continue
+                p2p.append(dist.P2POp(dist.isend, user[o["off"] + pr * B:o["off"] + (pr + 1) * B],
+                                      pr))
+                p2p.append(dist.P2POp(dist.irecv, scratch[o["src_off"] + pr * B:
+                                                          o["src_off"] + (pr + 1) * B], pr))
+            for req in dist.batch_isend_irecv(p2p):
+                req.wait()
+            i += 1
+            continue
+        if o["kind"] == ALLGATHER:
+            B = o["bytes"]
+            mine = user[o["off"] + rank * B:o["off"] + (rank + 1) * B].clone()
+            parts = [torch.empty_like(mine) for _ in range(world)]
+            dist.all_gather(parts, mine)
+            for pr in range(world):
+                user[o["off"] + pr * B:o["off"] + (pr + 1) * B] = parts[pr]
+            i += 1
+            continue
+        if o["kind"] in (REDUCE, FOLD):
+            u = user.numpy()
+            sc = scratch.numpy()
+            local = u[o["off"]:o["off"] + o["bytes"]].view(dt).copy()
+            if o["kind"] == REDUCE:
+                recv = sc[o["src_off"]:o["src_off"] + o["bytes"]].view(dt)
+                out = O.op(local, recv, op, code)
+            else:
+                slots = [sc[fold_slot(o, j):fold_slot(o, j) + o["bytes"]].view(dt)
+                         for j in range(1, o["nsrc"])]
+                acc = slots[-1].copy()
+                for s in reversed(slots[:-1]):
+                    acc = O.op(s.copy(), acc, op, code)
+                out = O.op(local, acc, op, code)
+            u[o["off"]:o["off"] + o["bytes"]] = out.view(np.uint8)
+            i += 1
+            continue
+        g = i
+        p2p = []
+        while ops[g]["kind"] != GROUP:
+            it = ops[g]
+            t = (user if it["buf"] == 0 else scratch)[it["off"]:it["off"] + it["bytes"]]
+            p2p.append(dist.P2POp(dist.isend if it["kind"] == SEND else dist.irecv, t, it["peer"]))
+            g += 1
+        if p2p:
+            for req in dist.batch_isend_irecv(p2p):
+                req.wait()
+        i = g + 1
+
+
+class GlooPlanComm:
+    """XgmiComm's interface over `execute` (the library still plans and validates every
+    schedule: argument and geometry errors are the library's own HydraErrors)."""
+
+    def __init__(self, O):
+        import torch.distributed as dist
+
+        self.O = O
+        self.rank, self.world = dist.get_rank(), dist.get_world_size()
+        self.closed = False
+
+    def _code(self, t, dtype_code):
+        from hydra_amd._lib import HydraError
+
+        code = dtype_code if dtype_code is not None else {4: 6}.get(t.element_size(), -1)
+        if code not in _NP:
+            raise HydraError(2, "GlooPlanComm folds fp32 / int32 only")
+        return code
+
+    def allreduce_(self, t, algo="auto", op="sum", dtype_code=None, flags=0, max_segment=0,
+                   chunk_bytes=0, stream=None):
+        import torch
+        import torch.distributed as dist
+
+        from hydra_amd import ring
+        from hydra_amd._lib import HydraError
+
+        if flags:
+            raise HydraError(2, "GlooPlanComm: no ACC_F32")
+        code = self._code(t, dtype_code)
+        n = t.numel()
+        if algo == "rccl":
+            dist.all_reduce(t)
+            return
+        if n == 0 or self.world == 1:
+            return
+        ops, scr = ring.plan("direct" if algo == "auto" else algo, self.world, self.rank, n,
+                             4, max_segment, chunk_bytes)
+        execute(self.O, ops, scr, t.view(-1).view(torch.uint8), code, op)
+
+    def reduce_(self, t, root, op="sum", dtype_code=None, flags=0, max_segment=0,
+                chunk_bytes=0, stream=None):
+        import torch
+
+        from hydra_amd import ring
+
+        code = self._code(t, dtype_code)
+        n = t.numel()
+        if n == 0 or self.world == 1:
+            return
+        ops, scr = ring.plan_reduce(root, self.world, self.rank, n, 4, max_segment, chunk_bytes)
+        execute(self.O, ops, scr, t.view(-1).view(torch.uint8), code, op)
+
+    def apipe_allreduce_(self, rail2, t, table=0, algo="auto", op="sum", dtype_code=None,
+                         flags=0, max_segment=0, chunk_bytes=0, stream=None):
+        """The two rails one after the other (hydra_apipe_allreduce runs them concurrently on
+        two communicators; every rank issues them in the same order either way)."""
+        from hydra_amd import ring
+
+        e1, _ = ring.split_elements(table, self.world, t.numel())
+        flat = t.view(-1)
+        kw = dict(algo=algo, op=op, dtype_code=dtype_code, flags=flags,
+                  max_segment=max_segment, chunk_bytes=chunk_bytes)
+        if e1:
+            self.allreduce_(flat[:e1], **kw)
+        if e1 < flat.numel():
+            rail2.allreduce_(flat[e1:], **kw)
+
+    def close(self):
+        self.closed = True

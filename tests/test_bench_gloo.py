@@ -1,0 +1,99 @@
+"""The N>1 bench orchestration (hydra_amd.ring.bench_allreduce, what `bench.py --gpus N` runs on
+each rank) at world size 2, 3 and 4 on the CPU: the same code path the driver's 8-GPU run takes --
+fold-order parity self-checks of every schedule, the safe DIRECT headline, the autotune over
+bit-exact candidates, full-size exactness, the timed region with max over ranks, the context
+schedules' parity and timings, gloo::reduce to a root, the two-rail split, and the JSON line --
+with the communicator swapped for tests/gloo_plan_exec.GlooPlanComm (the library's own plans
+over gloo p2p, the oracle folding) and the device sync for a no-op.  Every rank must take the
+same branches (a divergence deadlocks a collective and fails the test by its timeout) and the
+line must report every schedule bit-exact."""
+import argparse
+import os
+import socket
+
+import pytest
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    import sys
+
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch
+    import torch.distributed as dist
+
+    from gloo_plan_exec import GlooPlanComm
+    from hydra_amd import ring
+    from oracle import oracle as O
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    comms = []
+
+    def make_comm():
+        comms.append(GlooPlanComm(O))
+        return comms[-1]
+
+    try:
+        args = argparse.Namespace(elements=1 << 16, steps=3, warmup=1, algo="auto",
+                                  watchdog_s=600.0, no_config5=True, peer=False)
+        res = ring.bench_allreduce(args, torch.device("cpu"), make_comm=make_comm,
+                                   sync=lambda: None)
+        q.put((rank, res, all(c.closed for c in comms) and len(comms) == 2))
+    except Exception as e:  # report instead of hanging the parent
+        import traceback
+
+        q.put((rank, repr(e) + traceback.format_exc(), False))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_bench_allreduce_orchestration(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        out = {}
+        for _ in range(world):
+            r, res, closed = q.get(timeout=300)
+            out[r] = (res, closed)
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    for r, (res, closed) in out.items():
+        assert isinstance(res, dict), res
+        assert closed, f"rank {r} left a communicator open"
+    res = out[0][0]
+    assert res["n_gpus"] == world and res["scaling"] == "weak" and res["value"] > 0
+    par = res["parity"]["fold_order_1M"]
+    for a in ("direct", "ring", "ring_old", "ring_chunked", "bcube", "reduce_root", "apipe"):
+        assert par[a] == "bit-exact", (a, par)
+    # A2A needs P equal reference blocks: 1 Mi fp32 has them at P = 2 and 4, not at P = 3
+    assert (par["a2a"] == "bit-exact" if world != 3 else par["a2a"].startswith("n/a")), par
+    assert all(res["parity"]["full_size_exact"].values()), res["parity"]
+    assert res["config"]["algo"] in ("direct", "a2a", "ring")
+    assert res["config"]["autotune_ms"], res["config"]
+    for a in ("ring", "direct", "rccl", "ring_old", "ring_chunked", "bcube", "halving_doubling",
+              "reduce_root0", "apipe_direct"):
+        if a != res["config"]["algo"]:
+            assert isinstance(res["other_algos_ms"][a], float), (a, res["other_algos_ms"])
+    # every rank reports the same (max-over-ranks) timing
+    assert all(out[r][0]["ms_per_step"] == res["ms_per_step"] for r in out)

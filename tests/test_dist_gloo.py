@@ -1,5 +1,5 @@
 """World-size-2 (and 3) CPU runs of the N>1 path over torch.distributed gloo: the rank-local
-plans from libhydra_hip.so executed with real inter-process p2p (batch_isend_irecv), the
+plans from libhydra_hip.so executed with real inter-process p2p (tests/gloo_plan_exec.py), the
 oracle's reduction standing in for the HIP kernels (CPU-only test of the distributed
 orchestration), plus the bench harness helpers (unique-id broadcast, max-over-ranks timing)."""
 import os
@@ -8,15 +8,6 @@ import socket
 import numpy as np
 import pytest
 import torch.multiprocessing as mp
-
-SEND, RECV, GROUP, REDUCE, FOLD, ALLTOALL, ALLGATHER = 1, 2, 3, 4, 5, 6, 7
-
-
-def fold_slot(o, j):
-    if o["peer"] < 0:
-        return o["src_off"] + (j - 1) * o["slot_stride"]
-    return o["src_off"] + ((o["peer"] + j) % o["nsrc"]) * o["slot_stride"]
-
 
 def _free_port():
     s = socket.socket()
@@ -35,6 +26,8 @@ def _worker(rank, world, port, algo, n, ms, ch, q):
     import torch
     import torch.distributed as dist
 
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from gloo_plan_exec import execute
     from hydra_amd import ring, synth
     from oracle import oracle as O
 
@@ -47,63 +40,7 @@ def _worker(rank, world, port, algo, n, ms, ch, q):
         else:
             ops, scr = ring.plan(algo, world, rank, n, 4, ms, ch)
         user = torch.from_numpy(x.copy().view(np.uint8))
-        scratch = torch.zeros(scr + 16, dtype=torch.uint8)
-        i = 0
-        while i < len(ops):
-            o = ops[i]
-            if o["kind"] == ALLTOALL:  # ncclAllToAll semantics via p2p (gloo has no alltoall)
-                B = o["bytes"]
-                scratch[o["src_off"] + rank * B:o["src_off"] + (rank + 1) * B] = \
-                    user[o["off"] + rank * B:o["off"] + (rank + 1) * B]
-                p2p = []
-                for pr in range(world):
-                    if pr == rank:
-                        continue
-                    p2p.append(dist.P2POp(dist.isend,
-                                          user[o["off"] + pr * B:o["off"] + (pr + 1) * B], pr))
-                    p2p.append(dist.P2POp(dist.irecv, scratch[o["src_off"] + pr * B:
-                                                              o["src_off"] + (pr + 1) * B], pr))
-                for req in dist.batch_isend_irecv(p2p):
-                    req.wait()
-                i += 1
-                continue
-            if o["kind"] == ALLGATHER:
-                B = o["bytes"]
-                mine = user[o["off"] + rank * B:o["off"] + (rank + 1) * B].clone()
-                parts = [torch.empty_like(mine) for _ in range(world)]
-                dist.all_gather(parts, mine)
-                for pr in range(world):
-                    user[o["off"] + pr * B:o["off"] + (pr + 1) * B] = parts[pr]
-                i += 1
-                continue
-            if o["kind"] in (REDUCE, FOLD):
-                u = user.numpy()
-                sc = scratch.numpy()
-                local = u[o["off"]:o["off"] + o["bytes"]].view(np.float32).copy()
-                if o["kind"] == REDUCE:
-                    recv = sc[o["src_off"]:o["src_off"] + o["bytes"]].view(np.float32)
-                    out = O.op(local, recv, "sum")
-                else:
-                    slots = [sc[fold_slot(o, j):fold_slot(o, j) + o["bytes"]].view(np.float32)
-                             for j in range(1, o["nsrc"])]
-                    acc = slots[-1].copy()
-                    for s in reversed(slots[:-1]):
-                        acc = O.op(s.copy(), acc, "sum")
-                    out = O.op(local, acc, "sum")
-                u[o["off"]:o["off"] + o["bytes"]] = out.view(np.uint8)
-                i += 1
-                continue
-            g = i
-            p2p = []
-            while ops[g]["kind"] != GROUP:
-                it = ops[g]
-                t = (user if it["buf"] == 0 else scratch)[it["off"]:it["off"] + it["bytes"]]
-                p2p.append(dist.P2POp(dist.isend if it["kind"] == SEND else dist.irecv, t,
-                                      it["peer"]))
-                g += 1
-            for req in dist.batch_isend_irecv(p2p):
-                req.wait()
-            i = g + 1
+        execute(O, ops, scr, user)
         got = user.numpy().view(np.float32)
         # harness helpers
         uid = ring.exchange_unique_id(rank, make_id=lambda: bytes(range(128)))
