@@ -616,9 +616,10 @@ def bench_allreduce(args, dev, make_comm=None, sync=None) -> dict:
             others["apipe_direct"] = f"n/a: {e}"
         # 5) BASELINE config 5: bf16 bucket of 256 Mi elements, fp32 accumulation
         if not getattr(args, "no_config5", False):
-            n5 = 256 << 20
-            xb = torch.from_numpy(synth.bf16_bits((j[: 1 << 20] % 7 - 3).astype(np.float32))
-                                  .view(np.int16)).to(dev).repeat(n5 >> 20)
+            n5 = int(getattr(args, "config5_elements", 256 << 20))  # a multiple of 1 Mi
+            base = np.arange(1 << 20, dtype=np.int64) % 7 - 3
+            xb = torch.from_numpy(synth.bf16_bits(base.astype(np.float32)).view(np.int16)) \
+                .to(dev).repeat(n5 >> 20)
 
             c5_algo = chosen if chosen in ("direct", "a2a", "peer2") else "direct"
             if c5_algo == "peer2":
@@ -633,6 +634,16 @@ def bench_allreduce(args, dev, make_comm=None, sync=None) -> dict:
 
             k5 = max(5, args.steps // 10)
             try:
+                # full-size check first: every rank holds the same small integers, so one
+                # allreduce must give exactly world x base in bf16 (|sum| <= 3P: exact in fp32
+                # and in bf16); the timed steps then keep folding in place
+                want = torch.from_numpy(synth.bf16_bits((base * world).astype(np.float32))
+                                        .view(np.int16)).to(dev).repeat(n5 >> 20)
+                bstep()
+                sync()
+                good = bool(torch.equal(xb, want))
+                del want
+                full_ok["config5_bf16_acc32"] = max_over_ranks(0.0 if good else 1.0, dev) == 0.0
                 bw = max_over_ranks(timed_steps(bstep, k5, 2, sync, dist.barrier), dev)
                 bms = bw / k5 * 1e3
                 b_alg = 2.0 * n5 / (bms * 1e-3) / 1e9

@@ -9,7 +9,18 @@ kernels).  `GlooPlanComm` wraps it in XgmiComm's interface, so the N>1 bench orc
 import numpy as np
 
 SEND, RECV, GROUP, REDUCE, FOLD, ALLTOALL, ALLGATHER = 1, 2, 3, 4, 5, 6, 7
-_NP = {4: np.int32, 6: np.float32}  # dtype codes the executor folds (hydra_dtype_t INT32, FLOAT32)
+_NP = {4: np.int32, 6: np.float32, 9: np.uint16}  # hydra_dtype_t INT32, FLOAT32, BFLOAT16
+BF16 = 9
+
+
+def _f32(h):
+    return (h.astype(np.uint32) << np.uint32(16)).view(np.float32)
+
+
+def _bf16(x):  # round to nearest even (finite values)
+    u = x.astype(np.float32).view(np.uint32).astype(np.uint64)
+    return ((u + np.uint64(0x7FFF) + ((u >> np.uint64(16)) & np.uint64(1))) >> np.uint64(16)) \
+        .astype(np.uint16)
 
 
 def fold_slot(o, j):
@@ -20,7 +31,9 @@ def fold_slot(o, j):
 
 
 def execute(O, ops, scratch_bytes, user, code=6, op="sum"):
-    """Run `ops` on `user` (a contiguous CPU uint8 tensor, modified in place) on this rank."""
+    """Run `ops` on `user` (a contiguous CPU uint8 tensor, modified in place) on this rank.
+    code BFLOAT16 is the ACC_F32 form (config 5): each fold in fp32 in the same order, one
+    round to bf16 at the end, as k_fold<bf16, ACC32> computes it (sum only)."""
     import torch
     import torch.distributed as dist
 
@@ -59,7 +72,15 @@ def execute(O, ops, scratch_bytes, user, code=6, op="sum"):
             u = user.numpy()
             sc = scratch.numpy()
             local = u[o["off"]:o["off"] + o["bytes"]].view(dt).copy()
-            if o["kind"] == REDUCE:
+            if code == BF16:
+                srcs = ([sc[o["src_off"]:o["src_off"] + o["bytes"]]] if o["kind"] == REDUCE else
+                        [sc[fold_slot(o, j):fold_slot(o, j) + o["bytes"]]
+                         for j in range(1, o["nsrc"])])
+                acc = _f32(srcs[-1].view(dt))
+                for s_ in reversed(srcs[:-1]):
+                    acc = _f32(s_.view(dt)) + acc
+                out = _bf16(_f32(local) + acc)
+            elif o["kind"] == REDUCE:
                 recv = sc[o["src_off"]:o["src_off"] + o["bytes"]].view(dt)
                 out = O.op(local, recv, op, code)
             else:
@@ -101,7 +122,7 @@ class GlooPlanComm:
 
         code = dtype_code if dtype_code is not None else {4: 6}.get(t.element_size(), -1)
         if code not in _NP:
-            raise HydraError(2, "GlooPlanComm folds fp32 / int32 only")
+            raise HydraError(2, "GlooPlanComm folds fp32, int32 and bf16 (ACC_F32) only")
         return code
 
     def allreduce_(self, t, algo="auto", op="sum", dtype_code=None, flags=0, max_segment=0,
@@ -112,9 +133,11 @@ class GlooPlanComm:
         from hydra_amd import ring
         from hydra_amd._lib import HydraError
 
-        if flags:
-            raise HydraError(2, "GlooPlanComm: no ACC_F32")
         code = self._code(t, dtype_code)
+        if (code == BF16) != bool(flags):
+            raise HydraError(2, "GlooPlanComm: bf16 only with ACC_F32, ACC_F32 only for bf16")
+        if code == BF16 and algo == "rccl":
+            raise HydraError(2, "ACC_F32 with RCCL")
         n = t.numel()
         if algo == "rccl":
             dist.all_reduce(t)
@@ -122,7 +145,7 @@ class GlooPlanComm:
         if n == 0 or self.world == 1:
             return
         ops, scr = ring.plan("direct" if algo == "auto" else algo, self.world, self.rank, n,
-                             4, max_segment, chunk_bytes)
+                             t.element_size(), max_segment, chunk_bytes)
         execute(self.O, ops, scr, t.view(-1).view(torch.uint8), code, op)
 
     def reduce_(self, t, root, op="sum", dtype_code=None, flags=0, max_segment=0,
@@ -135,7 +158,8 @@ class GlooPlanComm:
         n = t.numel()
         if n == 0 or self.world == 1:
             return
-        ops, scr = ring.plan_reduce(root, self.world, self.rank, n, 4, max_segment, chunk_bytes)
+        ops, scr = ring.plan_reduce(root, self.world, self.rank, n, t.element_size(), max_segment,
+                                    chunk_bytes)
         execute(self.O, ops, scr, t.view(-1).view(torch.uint8), code, op)
 
     def apipe_allreduce_(self, rail2, t, table=0, algo="auto", op="sum", dtype_code=None,

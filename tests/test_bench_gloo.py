@@ -48,7 +48,8 @@ def _worker(rank, world, port, q):
 
     try:
         args = argparse.Namespace(elements=1 << 16, steps=3, warmup=1, algo="auto",
-                                  watchdog_s=600.0, no_config5=True, peer=False)
+                                  watchdog_s=600.0, no_config5=False, config5_elements=1 << 20,
+                                  peer=False)
         res = ring.bench_allreduce(args, torch.device("cpu"), make_comm=make_comm,
                                    sync=lambda: None)
         q.put((rank, res, all(c.closed for c in comms) and len(comms) == 2))
@@ -95,5 +96,8 @@ def test_bench_allreduce_orchestration(world):
               "reduce_root0", "apipe_direct"):
         if a != res["config"]["algo"]:
             assert isinstance(res["other_algos_ms"][a], float), (a, res["other_algos_ms"])
+    c5 = res["config5_bf16"]  # config 5's leg (bf16, fp32 accumulate) ran, at 1 Mi here
+    assert "error" not in c5 and c5["elements"] == 1 << 20 and c5["ms"] > 0, c5
+    assert res["parity"]["full_size_exact"]["config5_bf16_acc32"] is True, res["parity"]
     # every rank reports the same (max-over-ranks) timing
     assert all(out[r][0]["ms_per_step"] == res["ms_per_step"] for r in out)
