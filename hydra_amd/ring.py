@@ -575,13 +575,6 @@ def bench_allreduce(args, dev, make_comm=None, sync=None) -> dict:
         # gloo::reduce to the last rank (hydra_reduce_root): only the root's bucket is defined
         check_parity("reduce_root", lambda t: comm.reduce_(t, world - 1),
                      expected_reduce_f32(xs) if rank == world - 1 else None)
-        # two rails (bew_allreduce_a): each part is the reference ring on its slice
-        e1, _ = split_elements(0, world, pn)
-        exp2 = np.concatenate([expected_fold_f32([x[:e1] for x in xs]) if e1 else
-                               np.empty(0, np.float32),
-                               expected_fold_f32([x[e1:] for x in xs]) if e1 < pn else
-                               np.empty(0, np.float32)])
-        check_parity("apipe", lambda t: comm.apipe_allreduce_(rail2, t, algo="direct"), exp2)
         k = max(5, args.steps // 4)
         for a in ("ring", "direct", "a2a", "rccl", "ring_old", "ring_chunked", "bcube",
                   "halving_doubling") + peer_algos:
@@ -606,14 +599,6 @@ def bench_allreduce(args, dev, make_comm=None, sync=None) -> dict:
         except _lib.HydraError as e:
             others["reduce_root0"] = f"n/a: {e}"
 
-        def astep():
-            comm.apipe_allreduce_(rail2, x, algo="direct")
-
-        try:  # two rails split by calculateElements_AA, DIRECT on each
-            ow = max_over_ranks(timed_steps(astep, k, 3, sync, dist.barrier), dev)
-            others["apipe_direct"] = round(ow / k * 1e3, 4)
-        except _lib.HydraError as e:
-            others["apipe_direct"] = f"n/a: {e}"
         # 5) BASELINE config 5: bf16 bucket of 256 Mi elements, fp32 accumulation
         if not getattr(args, "no_config5", False):
             n5 = int(getattr(args, "config5_elements", 256 << 20))  # a multiple of 1 Mi
@@ -654,6 +639,12 @@ def bench_allreduce(args, dev, make_comm=None, sync=None) -> dict:
                 c5 = {"elements": n5, "algo": c5_algo, "error": str(e)}
             state["result"] = lambda: _result(ms, lat_ms, others, c5)
             del xb
+        # 6) two rails (bew_allreduce_a, calculateElements_AA, DIRECT on each): the only leg in
+        #    which two RCCL communicators run at once (pipeallreduce-a.cc:32-50's two threads).
+        #    Last, and every wait bounded: a stall between the communicators aborts both (and
+        #    ends this leg on every rank, each by its own timeout) instead of wedging the run.
+        _rails_leg(args, comm, rail2, xs, x, rank, world, pn, parity, others, dev)
+        state["result"] = lambda: _result(ms, lat_ms, others, c5)
     finally:
         errs = []
         for closer in ((pg["peer"].close if pg["peer"] is not None else None), comm.close,
@@ -668,6 +659,65 @@ def bench_allreduce(args, dev, make_comm=None, sync=None) -> dict:
         if errs:
             raise errs[0]
     return _result(ms, lat_ms, others, c5)
+
+
+def _rails_leg(args, comm, rail2, xs, x, rank, world, pn, parity, others, dev) -> None:
+    """bench_allreduce's two-rail leg: parity on the fold-order inputs (each part is the
+    reference ring on its slice), then `k` timed calls, each waited for with a bound
+    (hydra_comm_wait aborts the communicator past it).  Every rank runs the same collectives
+    whatever happens locally, so one rank's timeout cannot strand the others in a barrier."""
+    import torch.distributed as dist
+
+    timeout_ms = int(float(getattr(args, "rail_timeout_s", 60.0)) * 1000)
+
+    def step(t):
+        comm.apipe_allreduce_(rail2, t, algo="direct")
+        try:
+            comm.wait(timeout_ms)
+        except HydraError:
+            try:  # comm is aborted; abort the second rail too if its work is still pending
+                rail2.wait(1)
+            except HydraError:
+                pass
+            raise
+
+    e1, _ = split_elements(0, world, pn)
+    exp2 = np.concatenate([expected_fold_f32([v[:e1] for v in xs]) if e1 else
+                           np.empty(0, np.float32),
+                           expected_fold_f32([v[e1:] for v in xs]) if e1 < pn else
+                           np.empty(0, np.float32)])
+    import torch
+
+    err, good = None, False
+    try:
+        t = torch.from_numpy(xs[rank].copy()).to(dev)
+        step(t)
+        good = bool(np.array_equal(t.cpu().numpy().view(np.uint32), exp2.view(np.uint32)))
+    except HydraError as e:
+        err = str(e)
+    failed = max_over_ranks(1.0 if err else 0.0, dev) > 0
+    if failed:
+        parity["apipe"] = f"n/a: {err or 'another rank failed'}"
+        others["apipe_direct"] = parity["apipe"]
+        return
+    parity["apipe"] = "bit-exact" if max_over_ranks(0.0 if good else 1.0, dev) == 0.0 \
+        else "MISMATCH"
+    k = max(5, args.steps // 4)
+    err, t0, t1 = None, 0.0, 0.0
+    dist.barrier()
+    try:
+        for _ in range(3):
+            step(x)
+        t0 = time.perf_counter()
+        for _ in range(k):
+            step(x)
+        t1 = time.perf_counter()
+    except HydraError as e:
+        err = str(e)
+    failed = max_over_ranks(1.0 if err else 0.0, dev) > 0
+    wall = max_over_ranks(t1 - t0, dev)
+    others["apipe_direct"] = (f"n/a: {err or 'another rank failed'}" if failed else
+                              round(wall / k * 1e3, 4))
 
 
 def _bench_result(n, world, args, chosen, chunk, tuning, parity, full_ok, ms, lat_ms, others,

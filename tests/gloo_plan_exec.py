@@ -177,5 +177,8 @@ class GlooPlanComm:
         if e1 < flat.numel():
             rail2.allreduce_(flat[e1:], **kw)
 
+    def wait(self, timeout_ms, stream=None):
+        """XgmiComm.wait: the executor is synchronous, so there is never anything pending."""
+
     def close(self):
         self.closed = True

@@ -25,7 +25,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, stall_rank=-1):
     import sys
 
     sys.path.insert(0, ROOT)
@@ -42,8 +42,16 @@ def _worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     comms = []
 
+    class StalledRails(GlooPlanComm):
+        """As if the two-rail work never finished on this rank: its bounded wait expires."""
+
+        def wait(self, timeout_ms, stream=None):
+            from hydra_amd._lib import HydraError
+
+            raise HydraError(5, f"Timed out waiting {timeout_ms}ms for allreduce to complete")
+
     def make_comm():
-        comms.append(GlooPlanComm(O))
+        comms.append((StalledRails if rank == stall_rank else GlooPlanComm)(O))
         return comms[-1]
 
     try:
@@ -101,3 +109,34 @@ def test_bench_allreduce_orchestration(world):
     assert res["parity"]["full_size_exact"]["config5_bf16_acc32"] is True, res["parity"]
     # every rank reports the same (max-over-ranks) timing
     assert all(out[r][0]["ms_per_step"] == res["ms_per_step"] for r in out)
+
+
+def test_two_rail_stall_on_one_rank_ends_only_that_leg():
+    """bench_allreduce's two-rail leg (the only one with two communicators in flight) when one
+    rank's bounded wait expires: every rank reports the leg n/a, the run still completes with
+    the headline and every other leg, and nobody is left waiting in a collective."""
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, 1)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        out = {}
+        for _ in range(world):
+            r, res, closed = q.get(timeout=300)
+            out[r] = res
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    for r, res in out.items():
+        assert isinstance(res, dict), res
+        assert res["parity"]["fold_order_1M"]["apipe"].startswith("n/a"), res["parity"]
+        assert str(res["other_algos_ms"]["apipe_direct"]).startswith("n/a")
+    res = out[0]
+    assert res["parity"]["fold_order_1M"]["direct"] == "bit-exact" and res["value"] > 0
+    assert "Timed out" in res["parity"]["fold_order_1M"]["apipe"] or \
+        "another rank" in res["parity"]["fold_order_1M"]["apipe"]
