@@ -54,6 +54,9 @@ def parse():
     p.add_argument("--watchdog-s", type=float, default=420.0,
                    help="N>1: abort (exit 3) if the run exceeds this many seconds")
     p.add_argument("--no-config5", action="store_true", help="N>1: skip the bf16 config-5 leg")
+    p.add_argument("--config5-elements", type=int, default=256 << 20,
+                   help="N>1: bf16 elements of the config-5 leg (a multiple of 1 Mi; "
+                        "BASELINE: 256 Mi)")
     p.add_argument("--peer", action="store_true",
                    help="N>1: also check, autotune and time the peer-access (IPC) schedules; "
                         "off by default -- the cross-GPU IPC path has not run on an xGMI node")

@@ -552,17 +552,57 @@ def bench_allreduce(args, dev, make_comm=None, sync=None) -> dict:
         stall = float(os.environ.get("HYDRA_BENCH_STALL_CONTEXT", "0"))
         if stall > 0:  # test hook: a context phase that hangs (tests the watchdog's report)
             time.sleep(stall)
-        # parity of the schedules the headline does not use (after it: a hang here cannot lose
-        # the measured line, and an error is recorded in the line instead of failing the run)
+        # Everything after the headline is context: every wait is bounded (past
+        # `context_timeout_s` the RCCL communicator is aborted and the rest of the legs fail
+        # fast on it), an error is recorded in the line instead of failing the run, and every
+        # rank runs the same collectives whatever happened locally, so one rank's failure
+        # cannot strand the others in a barrier.
+        ctx_timeout_ms = int(float(getattr(args, "context_timeout_s", 60.0)) * 1000)
+
+        def bounded_wait():
+            comm.wait(ctx_timeout_ms)
+
+        def any_rank(err):
+            """Collective: did any rank fail?  (err: this rank's error message or None)"""
+            return max_over_ranks(1.0 if err else 0.0, dev) > 0
+
+        def context_leg(step, k, warm=3):
+            """ms per call of `step` over k timed calls after `warm` untimed ones, max over
+            ranks; or 'n/a: <why>' on every rank if any rank failed."""
+            err, t0, t1 = None, 0.0, 0.0
+            try:
+                for _ in range(warm):
+                    step()
+                bounded_wait()
+            except HydraError as e:
+                err = str(e)
+            if any_rank(err):  # (also the barrier before the timed calls)
+                return f"n/a: {err or 'another rank failed'}"
+            try:
+                t0 = time.perf_counter()
+                for _ in range(k):
+                    step()
+                bounded_wait()
+                t1 = time.perf_counter()
+            except HydraError as e:
+                err = str(e)
+            failed = any_rank(err)
+            wall = max_over_ranks(t1 - t0, dev)
+            return f"n/a: {err or 'another rank failed'}" if failed else round(wall / k * 1e3, 4)
+
+        # parity of the schedules the headline does not use
         def check_parity(name, call, expect):
+            err, ok = None, False
             try:
                 t = torch.from_numpy(xs[rank].copy()).to(dev)
                 call(t)
-                sync()
+                bounded_wait()
                 ok = expect is None or bool(np.array_equal(t.cpu().numpy().view(np.uint32),
                                                            expect.view(np.uint32)))
-            except HydraError as e:  # argument errors are the same on every rank
-                parity[name] = f"n/a: {e}"
+            except HydraError as e:
+                err = str(e)
+            if any_rank(err):
+                parity[name] = f"n/a: {err or 'another rank failed'}"
                 return
             parity[name] = ("bit-exact" if max_over_ranks(0.0 if ok else 1.0, dev) == 0.0
                             else "MISMATCH")
@@ -584,20 +624,13 @@ def bench_allreduce(args, dev, make_comm=None, sync=None) -> dict:
             def ostep(a=a):
                 run(a, x)
 
-            try:
-                ow = max_over_ranks(timed_steps(ostep, k, 3, sync, dist.barrier), dev)
-                others[a] = round(ow / k * 1e3, 4)
-            except _lib.HydraError as e:
-                others[a] = f"n/a: {e}"
+            others[a] = context_leg(ostep, k)
 
         def rstep():
             comm.reduce_(x, 0)
 
-        try:  # gloo::reduce of the same bucket to rank 0 (context: no all-gather half)
-            ow = max_over_ranks(timed_steps(rstep, k, 3, sync, dist.barrier), dev)
-            others["reduce_root0"] = round(ow / k * 1e3, 4)
-        except _lib.HydraError as e:
-            others["reduce_root0"] = f"n/a: {e}"
+        # gloo::reduce of the same bucket to rank 0 (context: no all-gather half)
+        others["reduce_root0"] = context_leg(rstep, k)
 
         # 5) BASELINE config 5: bf16 bucket of 256 Mi elements, fp32 accumulation
         if not getattr(args, "no_config5", False):
@@ -618,25 +651,31 @@ def bench_allreduce(args, dev, make_comm=None, sync=None) -> dict:
                     dtype_code=_lib.BFLOAT16, flags=_lib.ACC_F32)
 
             k5 = max(5, args.steps // 10)
+            # full-size check first: every rank holds the same small integers, so one
+            # allreduce must give exactly world x base in bf16 (|sum| <= 3P: exact in fp32 and
+            # in bf16); the timed steps then keep folding in place
+            err, good = None, False
             try:
-                # full-size check first: every rank holds the same small integers, so one
-                # allreduce must give exactly world x base in bf16 (|sum| <= 3P: exact in fp32
-                # and in bf16); the timed steps then keep folding in place
                 want = torch.from_numpy(synth.bf16_bits((base * world).astype(np.float32))
                                         .view(np.int16)).to(dev).repeat(n5 >> 20)
                 bstep()
-                sync()
+                bounded_wait()
                 good = bool(torch.equal(xb, want))
                 del want
-                full_ok["config5_bf16_acc32"] = max_over_ranks(0.0 if good else 1.0, dev) == 0.0
-                bw = max_over_ranks(timed_steps(bstep, k5, 2, sync, dist.barrier), dev)
-                bms = bw / k5 * 1e3
-                b_alg = 2.0 * n5 / (bms * 1e-3) / 1e9
-                c5 = {"elements": n5, "dtype": "bf16 (fp32 accumulate, one rounding)",
-                      "algo": c5_algo, "ms": round(bms, 4), "algbw_GBps": round(b_alg, 2),
-                      "busbw_GBps": round(b_alg * 2 * (world - 1) / world, 2)}
             except HydraError as e:
-                c5 = {"elements": n5, "algo": c5_algo, "error": str(e)}
+                err = str(e)
+            if any_rank(err):
+                c5 = {"elements": n5, "algo": c5_algo, "error": err or "another rank failed"}
+            else:
+                full_ok["config5_bf16_acc32"] = max_over_ranks(0.0 if good else 1.0, dev) == 0.0
+                r5 = context_leg(bstep, k5, warm=2)
+                if isinstance(r5, str):
+                    c5 = {"elements": n5, "algo": c5_algo, "error": r5}
+                else:
+                    b_alg = 2.0 * n5 / (r5 * 1e-3) / 1e9
+                    c5 = {"elements": n5, "dtype": "bf16 (fp32 accumulate, one rounding)",
+                          "algo": c5_algo, "ms": r5, "algbw_GBps": round(b_alg, 2),
+                          "busbw_GBps": round(b_alg * 2 * (world - 1) / world, 2)}
             state["result"] = lambda: _result(ms, lat_ms, others, c5)
             del xb
         # 6) two rails (bew_allreduce_a, calculateElements_AA, DIRECT on each): the only leg in

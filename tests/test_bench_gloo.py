@@ -25,7 +25,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q, stall_rank=-1):
+def _worker(rank, world, port, q, stall_rank=-1, stall_waits=0):
     import sys
 
     sys.path.insert(0, ROOT)
@@ -42,16 +42,20 @@ def _worker(rank, world, port, q, stall_rank=-1):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     comms = []
 
-    class StalledRails(GlooPlanComm):
-        """As if the two-rail work never finished on this rank: its bounded wait expires."""
+    left = [stall_waits]  # bounded waits that expire on stall_rank (-1: every one)
+
+    class Stalled(GlooPlanComm):
+        """As if this rank's work never finished: its bounded waits expire."""
 
         def wait(self, timeout_ms, stream=None):
             from hydra_amd._lib import HydraError
 
-            raise HydraError(5, f"Timed out waiting {timeout_ms}ms for allreduce to complete")
+            if left[0] != 0:
+                left[0] -= 1
+                raise HydraError(5, f"Timed out waiting {timeout_ms}ms for allreduce to complete")
 
     def make_comm():
-        comms.append((StalledRails if rank == stall_rank else GlooPlanComm)(O))
+        comms.append((Stalled if rank == stall_rank else GlooPlanComm)(O))
         return comms[-1]
 
     try:
@@ -111,15 +115,12 @@ def test_bench_allreduce_orchestration(world):
     assert all(out[r][0]["ms_per_step"] == res["ms_per_step"] for r in out)
 
 
-def test_two_rail_stall_on_one_rank_ends_only_that_leg():
-    """bench_allreduce's two-rail leg (the only one with two communicators in flight) when one
-    rank's bounded wait expires: every rank reports the leg n/a, the run still completes with
-    the headline and every other leg, and nobody is left waiting in a collective."""
-    world = 3
+def _run(world, stall_rank, stall_waits):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, 1)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, stall_rank, stall_waits))
+             for r in range(world)]
     for p in procs:
         p.start()
     try:
@@ -134,9 +135,34 @@ def test_two_rail_stall_on_one_rank_ends_only_that_leg():
                 p.kill()
     for r, res in out.items():
         assert isinstance(res, dict), res
-        assert res["parity"]["fold_order_1M"]["apipe"].startswith("n/a"), res["parity"]
-        assert str(res["other_algos_ms"]["apipe_direct"]).startswith("n/a")
+    return out
+
+
+def test_context_waits_expiring_on_one_rank():
+    """Every bounded wait after the headline expires on rank 1 (its communicator would be
+    aborted): every context leg is n/a on EVERY rank, the headline and its parity stand, and the
+    run completes -- nobody is stranded in a collective."""
+    out = _run(3, 1, -1)
+    for r, res in out.items():
+        par = res["parity"]["fold_order_1M"]
+        for a in ("ring_old", "ring_chunked", "bcube", "reduce_root", "apipe"):
+            assert par[a].startswith("n/a"), (r, a, par)
+        assert all(str(v).startswith("n/a") for v in res["other_algos_ms"].values()), res
+        assert "error" in res["config5_bf16"], res["config5_bf16"]
     res = out[0]
     assert res["parity"]["fold_order_1M"]["direct"] == "bit-exact" and res["value"] > 0
-    assert "Timed out" in res["parity"]["fold_order_1M"]["apipe"] or \
-        "another rank" in res["parity"]["fold_order_1M"]["apipe"]
+    assert "another rank failed" in res["parity"]["fold_order_1M"]["ring_old"]
+    assert "Timed out" in out[1]["parity"]["fold_order_1M"]["ring_old"]
+
+
+def test_one_expired_wait_costs_one_leg():
+    """Only rank 1's first bounded wait (the old-style ring's parity check) expires: that entry
+    is n/a on every rank, every later leg is measured."""
+    out = _run(2, 1, 1)
+    res = out[0]
+    par = res["parity"]["fold_order_1M"]
+    assert par["ring_old"].startswith("n/a"), par
+    for a in ("ring_chunked", "bcube", "reduce_root", "apipe"):
+        assert par[a] == "bit-exact", (a, par)
+    assert all(isinstance(v, float) for v in res["other_algos_ms"].values()), res
+    assert "error" not in res["config5_bf16"], res["config5_bf16"]

@@ -26,7 +26,8 @@ def _free_port():
 def test_bench_multi_path_world1(gpu):
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
     p = subprocess.run([sys.executable, "-u", "bench.py", "--force-dist", "--steps", "5",
-                        "--warmup", "1", "--no-config5", "--watchdog-s", "100"],
+                        "--warmup", "1", "--config5-elements", str(1 << 20),
+                        "--watchdog-s", "100"],
                        cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
     assert p.returncode == 0, (p.returncode, p.stdout[-2000:], p.stderr[-2000:])
     line = [ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1]
@@ -39,3 +40,7 @@ def test_bench_multi_path_world1(gpu):
     assert not any(v == "MISMATCH" for v in parity.values()), parity
     assert all(res["parity"]["full_size_exact"].values()), res["parity"]
     assert "watchdog" not in res, res
+    # every context leg measured (bounded waits, none expired), config 5 checked and timed
+    assert all(isinstance(v, float) for v in res["other_algos_ms"].values()), res
+    assert "error" not in res["config5_bf16"] and res["config5_bf16"]["elements"] == 1 << 20
+    assert res["parity"]["full_size_exact"]["config5_bf16_acc32"] is True
