@@ -566,14 +566,14 @@ def bench_allreduce(args, dev, make_comm=None, sync=None) -> dict:
             """Collective: did any rank fail?  (err: this rank's error message or None)"""
             return max_over_ranks(1.0 if err else 0.0, dev) > 0
 
-        def context_leg(step, k, warm=3):
+        def context_leg(step, k, warm=3, wait=bounded_wait):
             """ms per call of `step` over k timed calls after `warm` untimed ones, max over
             ranks; or 'n/a: <why>' on every rank if any rank failed."""
             err, t0, t1 = None, 0.0, 0.0
             try:
                 for _ in range(warm):
                     step()
-                bounded_wait()
+                wait()
             except HydraError as e:
                 err = str(e)
             if any_rank(err):  # (also the barrier before the timed calls)
@@ -582,7 +582,7 @@ def bench_allreduce(args, dev, make_comm=None, sync=None) -> dict:
                 t0 = time.perf_counter()
                 for _ in range(k):
                     step()
-                bounded_wait()
+                wait()
                 t1 = time.perf_counter()
             except HydraError as e:
                 err = str(e)
@@ -591,12 +591,12 @@ def bench_allreduce(args, dev, make_comm=None, sync=None) -> dict:
             return f"n/a: {err or 'another rank failed'}" if failed else round(wall / k * 1e3, 4)
 
         # parity of the schedules the headline does not use
-        def check_parity(name, call, expect):
+        def check_parity(name, call, expect, wait=bounded_wait):
             err, ok = None, False
             try:
                 t = torch.from_numpy(xs[rank].copy()).to(dev)
                 call(t)
-                bounded_wait()
+                wait()
                 ok = expect is None or bool(np.array_equal(t.cpu().numpy().view(np.uint32),
                                                            expect.view(np.uint32)))
             except HydraError as e:
@@ -682,7 +682,27 @@ def bench_allreduce(args, dev, make_comm=None, sync=None) -> dict:
         #    which two RCCL communicators run at once (pipeallreduce-a.cc:32-50's two threads).
         #    Last, and every wait bounded: a stall between the communicators aborts both (and
         #    ends this leg on every rank, each by its own timeout) instead of wedging the run.
-        _rails_leg(args, comm, rail2, xs, x, rank, world, pn, parity, others, dev)
+        def rails_wait():  # past the bound BOTH rails are aborted
+            try:
+                comm.wait(ctx_timeout_ms)
+            except HydraError:
+                try:
+                    rail2.wait(1)
+                except HydraError:
+                    pass
+                raise
+
+        e1, _ = split_elements(0, world, pn)
+        exp2 = np.concatenate([expected_fold_f32([v[:e1] for v in xs]) if e1 else
+                               np.empty(0, np.float32),
+                               expected_fold_f32([v[e1:] for v in xs]) if e1 < pn else
+                               np.empty(0, np.float32)])
+        check_parity("apipe", lambda t: comm.apipe_allreduce_(rail2, t, algo="direct"), exp2,
+                     wait=rails_wait)
+        others["apipe_direct"] = (
+            parity["apipe"] if parity["apipe"].startswith("n/a") else
+            context_leg(lambda: comm.apipe_allreduce_(rail2, x, algo="direct"), k,
+                        wait=rails_wait))
         state["result"] = lambda: _result(ms, lat_ms, others, c5)
     finally:
         errs = []
@@ -698,65 +718,6 @@ def bench_allreduce(args, dev, make_comm=None, sync=None) -> dict:
         if errs:
             raise errs[0]
     return _result(ms, lat_ms, others, c5)
-
-
-def _rails_leg(args, comm, rail2, xs, x, rank, world, pn, parity, others, dev) -> None:
-    """bench_allreduce's two-rail leg: parity on the fold-order inputs (each part is the
-    reference ring on its slice), then `k` timed calls, each waited for with a bound
-    (hydra_comm_wait aborts the communicator past it).  Every rank runs the same collectives
-    whatever happens locally, so one rank's timeout cannot strand the others in a barrier."""
-    import torch.distributed as dist
-
-    timeout_ms = int(float(getattr(args, "rail_timeout_s", 60.0)) * 1000)
-
-    def step(t):
-        comm.apipe_allreduce_(rail2, t, algo="direct")
-        try:
-            comm.wait(timeout_ms)
-        except HydraError:
-            try:  # comm is aborted; abort the second rail too if its work is still pending
-                rail2.wait(1)
-            except HydraError:
-                pass
-            raise
-
-    e1, _ = split_elements(0, world, pn)
-    exp2 = np.concatenate([expected_fold_f32([v[:e1] for v in xs]) if e1 else
-                           np.empty(0, np.float32),
-                           expected_fold_f32([v[e1:] for v in xs]) if e1 < pn else
-                           np.empty(0, np.float32)])
-    import torch
-
-    err, good = None, False
-    try:
-        t = torch.from_numpy(xs[rank].copy()).to(dev)
-        step(t)
-        good = bool(np.array_equal(t.cpu().numpy().view(np.uint32), exp2.view(np.uint32)))
-    except HydraError as e:
-        err = str(e)
-    failed = max_over_ranks(1.0 if err else 0.0, dev) > 0
-    if failed:
-        parity["apipe"] = f"n/a: {err or 'another rank failed'}"
-        others["apipe_direct"] = parity["apipe"]
-        return
-    parity["apipe"] = "bit-exact" if max_over_ranks(0.0 if good else 1.0, dev) == 0.0 \
-        else "MISMATCH"
-    k = max(5, args.steps // 4)
-    err, t0, t1 = None, 0.0, 0.0
-    dist.barrier()
-    try:
-        for _ in range(3):
-            step(x)
-        t0 = time.perf_counter()
-        for _ in range(k):
-            step(x)
-        t1 = time.perf_counter()
-    except HydraError as e:
-        err = str(e)
-    failed = max_over_ranks(1.0 if err else 0.0, dev) > 0
-    wall = max_over_ranks(t1 - t0, dev)
-    others["apipe_direct"] = (f"n/a: {err or 'another rank failed'}" if failed else
-                              round(wall / k * 1e3, 4))
 
 
 def _bench_result(n, world, args, chosen, chunk, tuning, parity, full_ok, ms, lat_ms, others,
