@@ -222,13 +222,16 @@ int hydra_host_apipe_threads(int P, int dtype, size_t n, void** in, void** out, 
 
 int hydra_host_bench(int config, int P, size_t n, int warmup, int iters, int reducer_mode,
                      hydra_reduce_fn fn, double* samples_ns, char* err, size_t errlen) {
-  if ((config != 1 && config != 3) || P < 1 || !samples_ns) {
+  if ((config != 1 && config != 3) || P < 1 || !samples_ns ||
+      (reducer_mode == HYDRA_REDUCER_GPU_PINNED_RANK0 && !fn)) {
     set_err(err, errlen, "invalid arguments");
     return 2;
   }
   return spawn(P, config == 3 ? 2 : 1, err, errlen,
                [&](int r, std::vector<std::shared_ptr<hydra::Context>>& c) {
     int reducer = reducer_mode;
+    if (reducer == HYDRA_REDUCER_GPU_PINNED_RANK0)
+      reducer = r == 0 ? HYDRA_REDUCER_GPU_PINNED : HYDRA_REDUCER_FN;
     std::vector<float> in(n), out(n);
     // GPU_PINNED: the receive slots are pinned and the output registered, so every segment
     // reduce is the zero-copy kernel over PCIe

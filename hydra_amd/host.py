@@ -220,12 +220,18 @@ def hip_ring_threads(tensors, workspace: str = "host", user_streams: bool = Fals
 
 
 def bench(config: int, P: int, n: int, warmup: int, iters: int, reducer_fn=None,
-          pinned: bool = False) -> np.ndarray:
+          pinned: bool = False, gpu_rank0_only: bool = False) -> np.ndarray:
     """Per-iteration ns of rank 0.  pinned (GPU reducer only): pinned receive slots and a
-    registered output, so each segment reduce is the zero-copy kernel."""
+    registered output, so each segment reduce is the zero-copy kernel.  gpu_rank0_only: rank 0
+    reduces zero-copy on the GPU, the other ranks with reducer_fn (HYDRA_REDUCER_GPU_PINNED_RANK0:
+    rank 0 has the box's one PCIe link to itself, as with one MI355X per rank)."""
     s = np.zeros(iters, np.float64)
     red, fp = _fn(reducer_fn)
-    if pinned:
+    if gpu_rank0_only:
+        if reducer_fn is None:
+            raise _lib.HydraError(1, "gpu_rank0_only needs reducer_fn for the other ranks")
+        red = 3
+    elif pinned:
         if reducer_fn is not None:
             raise _lib.HydraError(1, "pinned applies to the GPU reducer")
         red = 2

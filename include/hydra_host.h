@@ -25,6 +25,10 @@ typedef void (*hydra_reduce_fn)(void* c, const void* a, const void* b, size_t n)
 #define HYDRA_REDUCER_GPU 0
 #define HYDRA_REDUCER_FN 1
 #define HYDRA_REDUCER_GPU_PINNED 2
+/* hydra_host_bench only: rank 0 reduces with HYDRA_REDUCER_GPU_PINNED, every other rank with
+ * the caller's fn.  On a one-GPU box this gives rank 0 the PCIe link to itself, as BASELINE
+ * config 3 (one MI355X per rank) would; rank 0's per-iteration times are the ones reported. */
+#define HYDRA_REDUCER_GPU_PINNED_RANK0 3
 #ifndef HYDRA_SPLIT_AA
 #define HYDRA_SPLIT_AA 0 /* calculateElements_AA, pipeallreduce-a.h:296-376 (default) */
 #define HYDRA_SPLIT_AG 1 /* calculateElements_AG, pipeallreduce-a.h:137-294 (ALLREDUCE_GLEX) */

@@ -117,6 +117,11 @@ for n in sizes:
     c1.append({"impl": "hydra host runtime, GPU sum zero-copy (pinned slots, registered out)",
                **dist(keep("c1 hydra GPU sum zero-copy", n,
                            host.bench(1, 2, n, 3, iters, pinned=True)), n)})
+    if ref_fn:  # one GPU per rank, approximated: only rank 0's reduces use the box's one GPU
+        c1.append({"impl": "hydra host runtime, GPU sum zero-copy on rank 0 only "
+                           "(rank 1: reference gloo::sum)",
+                   **dist(host.bench(1, 2, n, 3, iters, reducer_fn=ref_fn,
+                                     gpu_rank0_only=True), n)})
     if ref_fn:
         c3.append({"impl": "hydra split + reference gloo::sum (CPU)",
                    **dist(keep("c3 hydra split + reference sum", n,
@@ -125,6 +130,11 @@ for n in sizes:
                **dist(keep("c3 hydra GPU sum", n, host.bench(3, 2, n, 3, iters)), n)})
     c3.append({"impl": "hydra split, GPU sum zero-copy (pinned slots, registered out)",
                **dist(host.bench(3, 2, n, 3, iters, pinned=True), n)})
+    if ref_fn:
+        c3.append({"impl": "hydra split, GPU sum zero-copy on rank 0 only "
+                           "(rank 1: reference gloo::sum)",
+                   **dist(host.bench(3, 2, n, 3, iters, reducer_fn=ref_fn,
+                                     gpu_rank0_only=True), n)})
 out["config1_new_allreduce_ring_P2"] = c1
 out["config3_bew_allreduce_a_P2"] = c3
 if os.environ.get("TABLE"):  # the reference benchmark's own table per implementation

@@ -204,9 +204,15 @@ def test_hip_allreduce_ring_rejects_host_pointers(gpu):
 
 
 @pytest.mark.parametrize("config", [1, 3])
-def test_host_bench_pinned_zero_copy(gpu, config):
+def test_host_bench_pinned_zero_copy(gpu, O, config):
     """Config 1 / 3 with pinned receive slots + registered output (zero-copy reduces) runs."""
     s = host.bench(config, 2, 1 << 18, 1, 3, pinned=True)
+    assert s.shape == (3,) and np.all(s > 0)
+    # one GPU per rank, approximated on the one-GPU box: rank 0 zero-copy, rank 1 a CPU sum
+    import ctypes
+
+    fn = ctypes.cast(O.orc().orc_sum_f32, ctypes.c_void_p).value
+    s = host.bench(config, 2, 1 << 18, 1, 3, reducer_fn=fn, gpu_rank0_only=True)
     assert s.shape == (3,) and np.all(s > 0)
 
 

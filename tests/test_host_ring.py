@@ -8,6 +8,7 @@ import numpy as np
 import pytest
 
 from hydra_amd import host, synth
+from hydra_amd._lib import HydraError
 
 
 def fnptr(O, name):
@@ -101,6 +102,8 @@ def test_bench_bodies_run(O):
     assert s.shape == (3,) and np.all(s > 0)
     s = host.bench(3, 2, 1 << 16, 1, 3, reducer_fn=fnptr(O, "orc_sum_f32"))
     assert np.all(s > 0)
+    with pytest.raises(HydraError):  # the other ranks' reducer is required
+        host.bench(3, 2, 1 << 16, 1, 3, gpu_rank0_only=True)
 
 
 def test_old_style_allreduce_ring_vs_golden(O, golden, golden_meta):
