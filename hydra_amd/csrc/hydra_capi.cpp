@@ -327,6 +327,17 @@ int hydra_reduce_host(hydra_ctx_t ctx, int op, int dtype, void* c, const void* a
   void* ma = nullptr;
   void* mb = nullptr;
   TempPin pc_, pa_, pb_;
+  // Declared after the pins, so destroyed before them: an early error return drains both
+  // streams before any operand is unpinned (work enqueued earlier may still use it).
+  struct DrainOnError {
+    hipStream_t* st;
+    bool armed = true;
+    ~DrainOnError() {
+      if (armed)
+        for (int i = 0; i < 2; i++)
+          if (st[i]) (void)hipStreamSynchronize(st[i]);
+    }
+  } drain_{ctx->stream};
   if (variant != kVariantForceStaging) {
     const bool fly = variant != kVariantNoPinOnTheFly;
     mc = mapped_device_range(c, nbytes);
@@ -349,6 +360,7 @@ int hydra_reduce_host(hydra_ctx_t ctx, int op, int dtype, void* c, const void* a
       hipError_t e = hydra::launch_reduce(0, op, dtype, mc, ma, mb, n, ctx->stream[0]);
       if (e != hipSuccess) return hip_fail(e, "reduce kernel launch (zero-copy)");
       HIP_TRY(hipStreamSynchronize(ctx->stream[0]));
+      drain_.armed = false;
       return ok();  // the TempPins unpin here, after the kernel finished
     }
   }
@@ -395,6 +407,7 @@ int hydra_reduce_host(hydra_ctx_t ctx, int op, int dtype, void* c, const void* a
   }
   HIP_TRY(hipStreamSynchronize(ctx->stream[0]));
   HIP_TRY(hipStreamSynchronize(ctx->stream[1]));
+  drain_.armed = false;
   return ok();
 }
 

@@ -51,9 +51,10 @@ Caches& C() {
 // Makes `device` current for a scope and restores the caller's device.
 struct DeviceScope {
   int old = -1;
+  hipError_t err = hipSuccess;  // of switching to `device` (an invalid device fails here)
   explicit DeviceScope(int device) {
     if (hipGetDevice(&old) != hipSuccess) old = -1;
-    if (device >= 0 && device != old) (void)hipSetDevice(device);
+    if (device >= 0 && device != old) err = hipSetDevice(device);
   }
   ~DeviceScope() {
     if (old >= 0) (void)hipSetDevice(old);
@@ -121,8 +122,9 @@ hipError_t give_block(void* p, bool host) {
 }  // namespace
 
 hipError_t cached_malloc(int device, size_t bytes, void** out) {
-  hipError_t e = hipSetDevice(device);
-  if (e != hipSuccess) return e;
+  if (device < 0) return hipErrorInvalidDevice;
+  DeviceScope ds(device);  // the caller's current device is left as it was
+  if (ds.err != hipSuccess) return ds.err;
   return take_block(BlockKey{false, device, size_class(bytes)}, out);
 }
 
@@ -135,8 +137,9 @@ hipError_t cached_malloc_host(size_t bytes, void** out) {
 hipError_t cached_free_host(void* p) { return give_block(p, true); }
 
 hipError_t cached_stream(int device, hipStream_t* out) {
-  hipError_t e = hipSetDevice(device);
-  if (e != hipSuccess) return e;
+  if (device < 0) return hipErrorInvalidDevice;
+  DeviceScope ds(device);  // the caller's current device is left as it was
+  if (ds.err != hipSuccess) return ds.err;
   Caches& c = C();
   {
     std::lock_guard<std::mutex> g(c.m);
@@ -150,7 +153,7 @@ hipError_t cached_stream(int device, hipStream_t* out) {
     }
   }
   hipStream_t s = nullptr;
-  e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+  hipError_t e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
   if (e != hipSuccess) return e;
   std::lock_guard<std::mutex> g(c.m);
   c.live_streams[s] = device;

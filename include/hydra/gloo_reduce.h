@@ -22,6 +22,7 @@
 #include <cstddef>
 #include <cstdint>
 #include <functional>
+#include <map>
 #include <mutex>
 #include <stdexcept>
 #include <string>
@@ -89,10 +90,14 @@ class ContextPool {
   };
 
   static ContextPool& instance(int device = 0) {
-    // one pool per process (device of the first caller); deliberately never destroyed: at
-    // process exit the HIP runtime may already be torn down, so no HIP call may run then
-    static ContextPool* pool = new ContextPool(device);
-    return *pool;
+    // one pool per device and process; deliberately never destroyed: at process exit the HIP
+    // runtime may already be torn down, so no HIP call may run then
+    static std::mutex* m = new std::mutex;
+    static std::map<int, ContextPool*>* pools = new std::map<int, ContextPool*>;
+    std::lock_guard<std::mutex> g(*m);
+    ContextPool*& p = (*pools)[device];
+    if (!p) p = new ContextPool(device);
+    return *p;
   }
   Lease acquire() {
     {

@@ -108,3 +108,23 @@ def test_double_release_is_refused(gpu):
     _lib.check(L.hydra_event_destroy(e))
     assert L.hydra_event_destroy(e) != 0
     _lib.check(L.hydra_device_check(0))
+
+
+def test_invalid_device_is_refused_and_current_device_kept(gpu):
+    """hydra_malloc / hydra_stream_create on a device that does not exist fail (nothing is
+    handed out on another device instead), and neither call changes the caller's current
+    device."""
+    import torch
+
+    L = _lib.lib()
+    before = torch.cuda.current_device()
+    p = ctypes.c_void_p()
+    assert L.hydra_malloc(99, 1 << 20, ctypes.byref(p)) != 0
+    s = ctypes.c_void_p()
+    assert L.hydra_stream_create(99, ctypes.byref(s)) != 0
+    assert torch.cuda.current_device() == before
+    L.hydra_device_check(0)  # collects the refused calls' (non-sticky) last error
+    q = _malloc(L, 1 << 20)  # the device the caller is on still works
+    _lib.check(L.hydra_free(q))
+    assert torch.cuda.current_device() == before
+    _lib.check(L.hydra_device_check(0))
