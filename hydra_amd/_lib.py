@@ -24,7 +24,8 @@ ESIZE = {INT8: 1, UINT8: 1, INT32: 4, UINT32: 4, INT64: 8, UINT64: 8, FLOAT32: 4
 
 EXPORTS = [  # every symbol include/hydra_hip.h declares
     "hydra_abi_version", "hydra_last_error", "hydra_device_count", "hydra_device_arch",
-    "hydra_device_check", "hydra_event_create", "hydra_event_record", "hydra_event_synchronize",
+    "hydra_device_check", "hydra_fault_report_enable", "hydra_fault_last", "hydra_fault_lookup",
+    "hydra_event_create", "hydra_event_record", "hydra_event_synchronize",
     "hydra_event_destroy",
     "hydra_reduce", "hydra_chunk_sum", "hydra_reduce_batch", "hydra_acc_bf16_f32", "hydra_f32_to_bf16",
     "hydra_set_variant", "hydra_ctx_create", "hydra_ctx_destroy", "hydra_reduce_host",
@@ -86,6 +87,22 @@ _lock = threading.Lock()
 _lib = None
 
 
+def fault_lookup(addr: int) -> str:
+    """Where `addr` lies: its /proc/self/maps line and every hydra block, registration or
+    per-call pin whose pages hold it (hydra_fault_lookup; the fault report's body)."""
+    buf = ctypes.create_string_buffer(8192)
+    check(lib().hydra_fault_lookup(addr, buf, len(buf)))
+    return buf.value.decode(errors="replace")
+
+
+def fault_last():
+    """(virtual address, reason mask, count) of the last GPU memory fault seen since
+    hydra_fault_report_enable (count 0: none)."""
+    va, reason, count = ctypes.c_uint64(), ctypes.c_uint32(), ctypes.c_uint64()
+    check(lib().hydra_fault_last(ctypes.byref(va), ctypes.byref(reason), ctypes.byref(count)))
+    return va.value, reason.value, count.value
+
+
 def build(force: bool = False) -> str:
     """Compile libhydra_hip.so for gfx950 (hipcc cross-compiles without a GPU)."""
     if force:
@@ -101,6 +118,9 @@ def _declare(L) -> None:
     L.hydra_device_count.argtypes = [ctypes.POINTER(i)]
     L.hydra_device_arch.argtypes = [i, ctypes.c_char_p, sz]
     L.hydra_device_check.argtypes = [i]
+    L.hydra_fault_last.argtypes = [ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint32),
+                                   ctypes.POINTER(ctypes.c_uint64)]
+    L.hydra_fault_lookup.argtypes = [ctypes.c_uint64, ctypes.c_char_p, sz]
     L.hydra_event_create.argtypes = [ctypes.POINTER(vp)]
     L.hydra_event_record.argtypes = [vp, vp]
     L.hydra_event_synchronize.argtypes = [vp]

@@ -14,6 +14,7 @@
 
 #include "../../include/hydra_hip.h"
 #include "errors.h"
+#include "fault_report.h"
 #include "resource_cache.h"
 #include "reduce_kernels.h"
 #include "trace.h"
@@ -287,6 +288,7 @@ struct TempPin {
       return false;
     }
     host = const_cast<void*>(p);
+    hydra::ledger_add(hydra::kLedgerTempPin, p, bytes);
     dev = mapped_device_range(p, bytes);
     if (!dev) {
       release();
@@ -295,7 +297,10 @@ struct TempPin {
     return true;
   }
   void release() {
-    if (host) (void)hipHostUnregister(host);
+    if (host) {
+      (void)hipHostUnregister(host);
+      hydra::ledger_release(hydra::kLedgerTempPin, host);
+    }
     host = nullptr;
     dev = nullptr;
   }
@@ -424,11 +429,13 @@ int hydra_host_register(void* ptr, size_t bytes) {
     return ok();
   }
   if (e != hipSuccess) return hip_fail(e, "hipHostRegister");
+  hydra::ledger_add(hydra::kLedgerHostRegister, ptr, bytes);
   return ok();
 }
 
 int hydra_host_unregister(void* ptr) {
   hipError_t e = hipHostUnregister(ptr);
+  if (e == hipSuccess) hydra::ledger_release(hydra::kLedgerHostRegister, ptr);
   if (e != hipSuccess && e != hipErrorHostMemoryNotRegistered) return hip_fail(e, "unregister");
   (void)hipGetLastError();
   return ok();

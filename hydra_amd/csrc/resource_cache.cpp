@@ -1,6 +1,8 @@
 // resource_cache.cpp -- see resource_cache.h.
 #include "resource_cache.h"
 
+#include "fault_report.h"
+
 #include <map>
 #include <mutex>
 #include <tuple>
@@ -79,6 +81,7 @@ hipError_t take_block(const BlockKey& k, void** out) {
   hipError_t e =
       k.host ? hipHostMalloc(&p, k.bytes, hipHostMallocDefault) : hipMalloc(&p, k.bytes);
   if (e != hipSuccess) return e;
+  ledger_add(k.host ? kLedgerPinnedBlock : kLedgerDeviceBlock, p, k.bytes);
   std::lock_guard<std::mutex> g(c.m);
   c.live_blocks[p] = k;
   *out = p;
@@ -116,6 +119,7 @@ hipError_t give_block(void* p, bool host) {
   }
   DeviceScope ds(k.host ? -1 : k.device);
   hipError_t f = k.host ? hipHostFree(p) : hipFree(p);
+  ledger_release(k.host ? kLedgerPinnedBlock : kLedgerDeviceBlock, p);
   return e != hipSuccess ? e : f;
 }
 
@@ -268,6 +272,7 @@ hipError_t trim_caches() {
   for (auto& kv : blocks) {
     DeviceScope ds(kv.first.host ? -1 : kv.first.device);
     note(kv.first.host ? hipHostFree(kv.second) : hipFree(kv.second));
+    ledger_release(kv.first.host ? kLedgerPinnedBlock : kLedgerDeviceBlock, kv.second);
   }
   return first;
 }

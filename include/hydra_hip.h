@@ -75,6 +75,14 @@ int hydra_device_arch(int device, char* buf, size_t len); /* e.g. "gfx950:sramec
 /* Drain every stream of `device` and report a pending asynchronous error (a faulting kernel,
  * an illegal address).  Test attribution: the GPU suite calls it after every test. */
 int hydra_device_check(int device);
+/* Fault diagnostics.  After enable, a GPU memory fault prints to stderr its
+ * virtual address and reason, the /proc/self/maps line holding it, and every range hydra knows
+ * whose pages hold it (cache blocks, hydra_host_register ranges, per-call pins of pageable
+ * operands; live or released, with times).  hydra_fault_last: the last fault seen (count 0 =
+ * none).  hydra_fault_lookup: the same report for any address into buf (no fault needed). */
+int hydra_fault_report_enable(void);
+int hydra_fault_last(uint64_t* va, uint32_t* reason, uint64_t* count);
+int hydra_fault_lookup(uint64_t va, char* buf, size_t len);
 
 /* ---- device-resident reduction (the hot path) ---------------------------------------------
  * c[i] = op(a[i], b[i]) for i < n, enqueued on `stream` (asynchronous, graph-capturable: no

@@ -71,7 +71,29 @@ def _gpu_fault_attribution(request):
         return
     from hydra_amd import _lib
 
-    _lib.check(_lib.lib().hydra_device_check(0))
+    rc = _lib.lib().hydra_device_check(0)
+    if rc != 0:
+        msg = _lib.lib().hydra_last_error().decode(errors="replace")
+        raise _lib.HydraError(rc, msg + _fault_context(torch, _lib))
+
+
+def _fault_context(torch, _lib) -> str:
+    """The last GPU memory fault's address (hydra_fault_report_enable's handler) and whether it
+    lies in one of torch's caching-allocator segments; the handler's own report (maps line, hydra's
+    ledger) is in the test's captured stderr."""
+    try:
+        va, reason, count = _lib.fault_last()
+        if not count:
+            return " [no GPU memory fault event seen by hydra's handler]"
+        owner = "no torch segment"
+        for seg in torch.cuda.memory_snapshot():
+            lo, size = seg.get("address", 0), seg.get("total_size", 0)
+            if lo <= va < lo + size:
+                owner = f"torch segment [{lo:#x}, {lo + size:#x}) ({seg.get('segment_type', '?')})"
+                break
+        return f" [GPU memory fault #{count} at VA {va:#x}, reason {reason:#x}; {owner}]"
+    except Exception as e:  # diagnostics must not mask the failure itself
+        return f" [fault context unavailable: {e}]"
 
 
 @pytest.fixture(scope="session")
@@ -89,4 +111,6 @@ def gpu():
     buf = ctypes.create_string_buffer(128)
     _lib.check(L.hydra_device_arch(0, buf, 128))
     assert buf.value.decode().startswith("gfx950"), buf.value
+    # a GPU memory fault prints where its address lies
+    _lib.check(L.hydra_fault_report_enable())
     return torch.device("cuda", 0)

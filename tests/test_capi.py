@@ -125,3 +125,16 @@ def test_examples_and_headers_compile(tmp_path):
         src.write_text(f'#include "{h}"\nint main() {{ return 0; }}\n')
         subprocess.check_call(["g++", "-std=c++17", "-fsyntax-only", "-Wall", "-I" + inc,
                                str(src)])
+
+
+def test_fault_lookup_names_the_mapping():
+    """hydra_fault_lookup (the body of the GPU-fault report) without a GPU: a host
+    array's address is inside a /proc/self/maps mapping, the zero page is not, and hydra's ledger
+    holds no range for either."""
+    from hydra_amd import _lib
+
+    x = np.zeros(1 << 16, np.float32)
+    r = _lib.fault_lookup(x.ctypes.data)
+    assert "mapped by:" in r and "no block, registration or per-call pin" in r, r
+    r0 = _lib.fault_lookup(8)
+    assert "not mapped" in r0, r0

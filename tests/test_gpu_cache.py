@@ -128,3 +128,29 @@ def test_invalid_device_is_refused_and_current_device_kept(gpu):
     _lib.check(L.hydra_free(q))
     assert torch.cuda.current_device() == before
     _lib.check(L.hydra_device_check(0))
+
+
+def test_fault_ledger_names_blocks_and_registrations(gpu):
+    """The fault report's ledger (hydra_fault_lookup): a live cache block, a host range registered
+    by hydra_host_register and, once released, the same range as RELEASED; a report for torch's
+    own memory.  Nothing faults here: the report is read directly."""
+    import torch
+
+    L = _lib.lib()
+    p = _malloc(L, 3 << 20)
+    r = _lib.fault_lookup(p.value + 4096)
+    assert "device block" in r and "LIVE" in r, r
+    _lib.check(L.hydra_free(p))
+    h = np.zeros(1 << 20, np.float32)
+    _lib.check(L.hydra_host_register(h.ctypes.data, h.nbytes))
+    try:
+        r = _lib.fault_lookup(h.ctypes.data + 100)
+        assert "hydra_host_register" in r and "LIVE" in r, r
+    finally:
+        _lib.check(L.hydra_host_unregister(h.ctypes.data))
+    r = _lib.fault_lookup(h.ctypes.data + 100)
+    assert "hydra_host_register" in r and "RELEASED" in r, r
+    t = torch.empty(1 << 20, device=gpu)
+    r = _lib.fault_lookup(t.data_ptr())
+    assert "mapped" in r, r  # a well-formed report for device memory too
+    assert _lib.fault_last()[2] == 0  # no fault seen in this process
