@@ -79,7 +79,9 @@ int hydra_device_check(int device);
  * virtual address and reason, the /proc/self/maps line holding it, and every range hydra knows
  * whose pages hold it (cache blocks, hydra_host_register ranges, per-call pins of pageable
  * operands; live or released, with times).  hydra_fault_last: the last fault seen (count 0 =
- * none).  hydra_fault_lookup: the same report for any address into buf (no fault needed). */
+ * none).  hydra_fault_lookup: the same report for any address into buf (no fault needed).
+ * The handler stays installed for the life of the process: do not unload the library after
+ * enabling it. */
 int hydra_fault_report_enable(void);
 int hydra_fault_last(uint64_t* va, uint32_t* reason, uint64_t* count);
 int hydra_fault_lookup(uint64_t va, char* buf, size_t len);
