@@ -24,7 +24,11 @@ def bits(x):
 
 
 class Dev:
-    """Raw device byte buffers so tests can place operands at arbitrary byte offsets."""
+    """Raw device byte buffers so tests can place operands at arbitrary byte offsets.  The bytes
+    around an operand (the offset before it, `pad` after it) hold a guard pattern, and get()
+    checks that it is intact: a kernel writing outside its range fails the test that ran it."""
+
+    GUARD = 0xA5
 
     def __init__(self, gpu):
         import torch
@@ -33,7 +37,8 @@ class Dev:
         self.gpu = gpu
 
     def put(self, arr, off_bytes=0, pad=64):
-        t = self.torch.zeros(arr.nbytes + off_bytes + pad, dtype=self.torch.uint8, device=self.gpu)
+        t = self.torch.full((arr.nbytes + off_bytes + pad,), self.GUARD, dtype=self.torch.uint8,
+                            device=self.gpu)
         if arr.nbytes:
             t[off_bytes:off_bytes + arr.nbytes] = self.torch.from_numpy(
                 np.ascontiguousarray(arr).view(np.uint8).copy()).to(self.gpu)
@@ -41,6 +46,10 @@ class Dev:
 
     def get(self, t, off_bytes, like):
         raw = t[off_bytes:off_bytes + like.nbytes].cpu().numpy()
+        before = t[:off_bytes].cpu().numpy()
+        after = t[off_bytes + like.nbytes:].cpu().numpy()
+        assert (before == self.GUARD).all() and (after == self.GUARD).all(), \
+            f"write outside the operand: guard bytes changed ({off_bytes} before, {after.size} after)"
         return raw.view(like.dtype).copy()
 
 
