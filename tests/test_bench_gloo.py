@@ -1,5 +1,5 @@
 """The N>1 bench orchestration (hydra_amd.ring.bench_allreduce, what `bench.py --gpus N` runs on
-each rank) at world size 2, 3 and 4 on the CPU: the same code path the driver's 8-GPU run takes --
+each rank) at world size 2, 3, 4 and 8 (the driver's node) on the CPU: the same code path the driver's 8-GPU run takes --
 fold-order parity self-checks of every schedule, the safe DIRECT headline, the autotune over
 bit-exact candidates, full-size exactness, the timed region with max over ranks, the context
 schedules' parity and timings, gloo::reduce to a root, the two-rail split, and the JSON line --
@@ -73,7 +73,7 @@ def _worker(rank, world, port, q, stall_rank=-1, stall_waits=0):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3, 4])
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
 def test_bench_allreduce_orchestration(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -99,7 +99,7 @@ def test_bench_allreduce_orchestration(world):
     par = res["parity"]["fold_order_1M"]
     for a in ("direct", "ring", "ring_old", "ring_chunked", "bcube", "reduce_root", "apipe"):
         assert par[a] == "bit-exact", (a, par)
-    # A2A needs P equal reference blocks: 1 Mi fp32 has them at P = 2 and 4, not at P = 3
+    # A2A needs P equal reference blocks: 1 Mi fp32 has them at P = 2, 4 and 8, not at P = 3
     assert (par["a2a"] == "bit-exact" if world != 3 else par["a2a"].startswith("n/a")), par
     assert all(res["parity"]["full_size_exact"].values()), res["parity"]
     assert res["config"]["algo"] in ("direct", "a2a", "ring")
