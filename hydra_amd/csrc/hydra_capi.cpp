@@ -9,6 +9,7 @@
 #include <atomic>
 #include <cstdio>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <string>
 
@@ -421,19 +422,41 @@ int hydra_chunk_sum_host(hydra_ctx_t ctx, int dtype, void* c, const void* a, con
   return hydra_reduce_host(ctx, HYDRA_SUM, dtype, c, a, b, n);
 }
 
+namespace {
+// Registrations made by hydra_host_register, reference-counted per start address: each register
+// needs its own unregister, so two owners of one buffer (two rank threads, a caller and a ring
+// class) cannot release each other's registration.
+std::mutex g_reg_mu;
+std::map<void*, std::pair<size_t, int>> g_regs;  // ptr -> (bytes, count)
+}  // namespace
+
 int hydra_host_register(void* ptr, size_t bytes) {
   if (!ptr || !bytes) return fail(HYDRA_ERR_INVALID, "null/empty range");
+  std::lock_guard<std::mutex> g(g_reg_mu);
+  auto it = g_regs.find(ptr);
+  if (it != g_regs.end()) {
+    if (bytes > it->second.first)
+      return fail(HYDRA_ERR_INVALID, "already registered with a shorter range: unregister it first");
+    it->second.second++;
+    return ok();
+  }
   hipError_t e = hipHostRegister(ptr, bytes, hipHostRegisterDefault);
-  if (e == hipErrorHostMemoryAlreadyRegistered) {
+  if (e == hipErrorHostMemoryAlreadyRegistered) {  // registered by its owner: used, never released here
     (void)hipGetLastError();
     return ok();
   }
   if (e != hipSuccess) return hip_fail(e, "hipHostRegister");
+  g_regs[ptr] = {bytes, 1};
   hydra::ledger_add(hydra::kLedgerHostRegister, ptr, bytes);
   return ok();
 }
 
 int hydra_host_unregister(void* ptr) {
+  std::lock_guard<std::mutex> g(g_reg_mu);
+  auto it = g_regs.find(ptr);
+  if (it == g_regs.end()) return ok();  // not registered here (or already released)
+  if (--it->second.second > 0) return ok();
+  g_regs.erase(it);
   hipError_t e = hipHostUnregister(ptr);
   if (e == hipSuccess) hydra::ledger_release(hydra::kLedgerHostRegister, ptr);
   if (e != hipSuccess && e != hipErrorHostMemoryNotRegistered) return hip_fail(e, "unregister");

@@ -136,7 +136,11 @@ int hydra_reduce_host(hydra_ctx_t ctx, int op, int dtype, void* c, const void* a
                       size_t n);
 int hydra_chunk_sum_host(hydra_ctx_t ctx, int dtype, void* c, const void* a, const void* b,
                          size_t n);
-/* Page-lock caller memory so staging copies run at full PCIe rate (optional, idempotent). */
+/* Page-lock caller memory: hydra_reduce_host then reads / writes it in place over PCIe
+ * (optional).  Reference-counted per start address: every hydra_host_register needs one
+ * hydra_host_unregister, and a second register of the same address may not cover more bytes.
+ * A range its owner registered directly (hipHostRegister) is used as it is and never released
+ * here; unregistering an address not registered here is a no-op. */
 int hydra_host_register(void* ptr, size_t bytes);
 int hydra_host_unregister(void* ptr);
 

@@ -154,3 +154,32 @@ def test_fault_ledger_names_blocks_and_registrations(gpu):
     r = _lib.fault_lookup(t.data_ptr())
     assert "mapped" in r, r  # a well-formed report for device memory too
     assert _lib.fault_last()[2] == 0  # no fault seen in this process
+
+
+def test_host_register_is_reference_counted(gpu):
+    """Two owners of one buffer each register and unregister it: the registration lives until the
+    last unregister (the fault ledger shows it LIVE, then RELEASED); a second register may not
+    cover more bytes than the first; unregistering an unknown address is a no-op."""
+    L = _lib.lib()
+    h = np.zeros(1 << 20, np.float32)
+    p = h.ctypes.data
+    _lib.check(L.hydra_host_register(p, h.nbytes))
+    _lib.check(L.hydra_host_register(p, h.nbytes // 2))  # a second owner, a shorter range: fine
+    assert L.hydra_host_register(p, h.nbytes + 4096) == _lib.ERR_INVALID
+    _lib.check(L.hydra_host_unregister(p))
+    assert "LIVE" in _lib.fault_lookup(p), _lib.fault_lookup(p)  # the first owner still holds it
+    # and it is still what hydra_reduce_host streams in place: same bits as the oracle
+    from hydra_amd.reduce import HostContext
+
+    b = np.ones(h.size, np.float32)
+    ctx = HostContext(0)
+    try:
+        _lib.check(L.hydra_reduce_host(ctx.handle, 0, 6, p, p, b.ctypes.data, h.size))
+    finally:
+        ctx.close()
+    assert (h == 1).all()
+    _lib.check(L.hydra_host_unregister(p))
+    assert "RELEASED" in _lib.fault_lookup(p), _lib.fault_lookup(p)
+    _lib.check(L.hydra_host_unregister(p))  # nothing left to release: no-op
+    x = np.zeros(16, np.float32)
+    _lib.check(L.hydra_host_unregister(x.ctypes.data))
