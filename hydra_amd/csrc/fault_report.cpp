@@ -60,6 +60,8 @@ const char* kind_name(int k) {
     case kLedgerPinnedBlock: return "pinned block (block cache hipHostMalloc)";
     case kLedgerHostRegister: return "host range registered by hydra_host_register";
     case kLedgerTempPin: return "pageable operand pinned for one hydra_reduce_host call";
+    case kLedgerPeerMapping: return "peer allocation mapped by IPC (hydra_peer_*)";
+    case kLedgerPeerLocal: return "peer group scratch / signal block (hydra_peer_*)";
   }
   return "?";
 }

@@ -6,8 +6,9 @@
 // virtual address and reason, the /proc/self/maps line that holds it (a GPU buffer object, an
 // anonymous host mapping, or nothing: unmapped), and every range hydra's own ledger knows that
 // contains its page: device and pinned blocks the caches allocated, host ranges registered by
-// hydra_host_register, and pageable operands pinned for one hydra_reduce_host call -- live or
-// already released (with when).  The last fault is kept for hydra_fault_last().
+// hydra_host_register, pageable operands pinned for one hydra_reduce_host call, peer
+// allocations mapped by IPC and peer groups' own blocks -- live or already released (with
+// when).  The last fault is kept for hydra_fault_last().
 #pragma once
 
 #include <cstddef>
@@ -19,6 +20,8 @@ enum LedgerKind : int {
   kLedgerPinnedBlock = 2,   // hipHostMalloc by the block cache
   kLedgerHostRegister = 3,  // hydra_host_register
   kLedgerTempPin = 4,       // hydra_reduce_host: a pageable operand pinned for one call
+  kLedgerPeerMapping = 5,   // a peer's allocation mapped into this process by IPC (hydra_peer_*)
+  kLedgerPeerLocal = 6,     // a peer group's own scratch / signal block (hydra_peer_*)
 };
 
 void ledger_add(LedgerKind kind, const void* p, size_t bytes);

@@ -17,6 +17,7 @@
 #include <string>
 #include <vector>
 
+#include "fault_report.h"
 #include "../../include/hydra_hip.h"
 #include "errors.h"
 #include "peer_kernels.h"
@@ -134,6 +135,15 @@ int open_mapping(hydra_peer* p, const Blob& b, std::string* key, char** base) {
     std::memcpy(&h, b.ipc, kIpcBytes);
     void* m = nullptr;
     HIP_TRY(hipIpcOpenMemHandle(&m, h, hipIpcMemLazyEnablePeerAccess));
+    {
+      void* mb = nullptr;
+      size_t msz = 0;
+      if (hipMemGetAddressRange(&mb, &msz, m) != hipSuccess || mb != m) {
+        (void)hipGetLastError();
+        msz = b.offset + b.bytes;  // at least what this registration reads
+      }
+      hydra::ledger_add(hydra::kLedgerPeerMapping, m, msz);
+    }
     if (std::getenv("HYDRA_PEER_DEBUG"))
       std::fprintf(stderr, "[hydra_peer] rank %d mapped rank %d's allocation (+%llu B) at %p\n",
                    p->rank, b.rank, (unsigned long long)b.bytes, m);
@@ -149,6 +159,7 @@ void close_mapping(hydra_peer* p, const std::string& key) {
   if (it == p->opened.end()) return;
   if (--it->second.refs <= 0) {
     (void)hipIpcCloseMemHandle(it->second.base);
+    hydra::ledger_release(hydra::kLedgerPeerMapping, it->second.base);
     p->opened.erase(it);
   }
 }
@@ -176,6 +187,7 @@ int hydra_peer_create(int nranks, int rank, int device, hydra_peer_t* out, void*
   p->device = device;
   hipError_t e = hipExtMallocWithFlags(reinterpret_cast<void**>(&p->sig),
                                        sizeof(hydra::PeerSignals), hipDeviceMallocUncached);
+  if (e == hipSuccess) hydra::ledger_add(hydra::kLedgerPeerLocal, p->sig, sizeof(hydra::PeerSignals));
   if (e == hipSuccess) e = hipMemset(p->sig, 0, sizeof(hydra::PeerSignals));
   if (e == hipSuccess)
     e = hipHostMalloc(reinterpret_cast<void**>(&p->err_host), sizeof(uint32_t),
@@ -363,10 +375,14 @@ int hydra_peer_allreduce(hydra_peer_t p, int algo, int op, int dtype, int flags,
   if (algo == HYDRA_PEER_ONE_SHOT) {
     if (p->scratch_bytes < n * es) {
       HIP_TRY(hipDeviceSynchronize());  // first call at a new size: outside any capture
-      if (p->scratch) HIP_TRY(hipFree(p->scratch));
+      if (p->scratch) {
+        HIP_TRY(hipFree(p->scratch));
+        hydra::ledger_release(hydra::kLedgerPeerLocal, p->scratch);
+      }
       p->scratch = nullptr;
       p->scratch_bytes = 0;
       HIP_TRY(hipMalloc(reinterpret_cast<void**>(&p->scratch), n * es));
+      hydra::ledger_add(hydra::kLedgerPeerLocal, p->scratch, n * es);
       p->scratch_bytes = n * es;
     }
     A.scratch = p->scratch;
@@ -383,7 +399,10 @@ int hydra_peer_detach(hydra_peer_t p) {
   if (p->detached) return ok();
   (void)hipSetDevice(p->device);
   (void)hipDeviceSynchronize();  // no kernel of ours may still read through the mappings
-  for (auto& kv : p->opened) (void)hipIpcCloseMemHandle(kv.second.base);
+  for (auto& kv : p->opened) {
+    (void)hipIpcCloseMemHandle(kv.second.base);
+    hydra::ledger_release(hydra::kLedgerPeerMapping, kv.second.base);
+  }
   p->opened.clear();
   p->regs.clear();
   for (int q = 0; q < p->P; q++)
@@ -395,8 +414,14 @@ int hydra_peer_detach(hydra_peer_t p) {
 int hydra_peer_destroy(hydra_peer_t p) {
   if (!p) return ok();
   (void)hydra_peer_detach(p);  // local; callers detach + barrier first (hydra_hip.h)
-  if (p->scratch) (void)hipFree(p->scratch);
-  if (p->sig) (void)hipFree(p->sig);
+  if (p->scratch) {
+    (void)hipFree(p->scratch);
+    hydra::ledger_release(hydra::kLedgerPeerLocal, p->scratch);
+  }
+  if (p->sig) {
+    (void)hipFree(p->sig);
+    hydra::ledger_release(hydra::kLedgerPeerLocal, p->sig);
+  }
   if (p->err_host) (void)hipHostFree(p->err_host);
   delete p;
   return ok();
