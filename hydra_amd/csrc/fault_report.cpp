@@ -165,7 +165,10 @@ void ledger_add(LedgerKind kind, const void* p, size_t bytes) {
   std::lock_guard<std::timed_mutex> g(l.m);
   const uint64_t seq = l.next++;
   Entry& e = l.ring[seq % kLedgerSize];
-  if (e.t_rel < 0 && e.end) l.live.erase({e.kind, e.start});  // overwritten while live
+  if (e.t_rel < 0 && e.end) {  // overwritten while live: drop its index, unless a newer entry owns it
+    auto it = l.live.find({e.kind, e.start});
+    if (it != l.live.end() && it->second == e.seq) l.live.erase(it);
+  }
   e.start = reinterpret_cast<uint64_t>(p);
   e.end = e.start + bytes;
   e.kind = kind;
