@@ -601,3 +601,21 @@ def test_chunk_sum_property_vs_oracle(dev, O):
         assert np.array_equal(bits(c), bits(O.op(a, b, kind, code))), (code, kind, n, oa, ob)
 
     check()
+
+
+@pytest.mark.parametrize("name,code,dt", TYPES)
+def test_math_test_sum_on_gpu(dev, O, name, code, dt):
+    """The reference's MathTest.Sum (gloo/gloo/test/math_test.cc:55-75) on the gfx950 kernel: a = 1
+    except a[i] = 2, b = 1 gives c[i] = 3 and 2 elsewhere, for both argument orders, every i of
+    a 50-element buffer, every Gloo type (float16 as its bits)."""
+    num = 50
+    one, two, three = ((O.f2h(1.0), O.f2h(2.0), O.f2h(3.0)) if name == "f16" else (1, 2, 3))
+    for i in range(num):
+        a = np.full(num, one, dt)
+        b = np.full(num, one, dt)
+        a[i] = two
+        exp = np.full(num, two, dt)
+        exp[i] = three
+        for x, y in ((a, b), (b, a)):
+            got = dev_reduce(dev, "sum", code, x, y, inplace=True)
+            assert np.array_equal(bits(got), bits(exp)), (name, i)
