@@ -119,6 +119,10 @@ def gpu():
     buf = ctypes.create_string_buffer(128)
     _lib.check(L.hydra_device_arch(0, buf, 128))
     assert buf.value.decode().startswith("gfx950"), buf.value
-    # a GPU memory fault prints where its address lies
-    _lib.check(L.hydra_fault_report_enable())
+    # a GPU memory fault prints where its address lies; a diagnostic, so a
+    # failure to install it is reported, never a reason to skip the tests
+    if L.hydra_fault_report_enable() != 0:
+        import warnings
+
+        warnings.warn("fault report not installed: " + L.hydra_last_error().decode())
     return torch.device("cuda", 0)
