@@ -112,7 +112,9 @@ std::string maps_line(uint64_t va) {
 std::string ledger_matches(uint64_t va) {
   Ledger& l = L();
   std::unique_lock<std::timed_mutex> g(l.m, std::defer_lock);
-  const bool locked = g.try_lock_for(std::chrono::milliseconds(200));  // never block the reporter
+  // never block the reporter for long; the lock is only ever held for a few map operations
+  if (!g.try_lock_for(std::chrono::milliseconds(200)))
+    return "  hydra: ledger busy for 200 ms (held by another thread), not read\n";
   std::string out;
   char buf[320];
   int n = 0;
@@ -134,7 +136,6 @@ std::string ledger_matches(uint64_t va) {
   }
   if (!n) out = "  hydra: no block, registration or per-call pin of hydra's holds this address "
                 "(torch's own memory, or a host buffer the HIP runtime pinned for a copy)\n";
-  if (!locked) out += "  (ledger read without its lock)\n";
   return out;
 }
 
