@@ -35,6 +35,9 @@ if [ "${SKIP_PROF:-0}" != "1" ]; then
   export TMPDIR=/tmp
   step rocprof_kt 600 rocprofv3 --kernel-trace --stats --output-format csv \
       -d "$OUT/prof_kt" -o run -- python3 "$ROOT/bench.py" --steps 100 --warmup 10 --no-cpu-baseline
+  # the headline's own dispatches from that trace (W = 10, S = 100 as above)
+  python3 scripts/headline_from_trace.py "$OUT/prof_kt/run_kernel_trace.csv" 10 100 "$TAG" \
+      > "$OUT/headline_from_trace.json" 2>&1 || true
   step rocprof_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv \
       -d "$OUT/prof_fetch" -o run -- python3 "$ROOT/bench.py" --steps 20 --warmup 2 --no-cpu-baseline
   step rocprof_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv \
