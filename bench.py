@@ -60,6 +60,9 @@ def parse():
     p.add_argument("--peer", action="store_true",
                    help="N>1: also check, autotune and time the peer-access (IPC) schedules; "
                         "off by default -- the cross-GPU IPC path has not run on an xGMI node")
+    p.add_argument("--extra-legs", action="store_true",
+                   help="N>1: also check and time the schedules outside north_star's path "
+                        "(old-style rings, BCUBE, halving-doubling, gloo::reduce to a root)")
     p.add_argument("--force-dist", action="store_true",
                    help="run the N>1 (RCCL) path even at world size 1 (code-path check)")
     return p.parse_args()
@@ -370,6 +373,43 @@ def run_single(args):
 
 
 # ------------------------------------------------------------------------------- N > 1
+def ring_cpu_baseline(P, n, seconds):
+    """The reference's own new_allreduce_ring benchmark body (oracle/_ref: gloo::allreduce RING
+    with gloo::sum<float>, compiled from /root/reference; benchmark/main.cc:321-358) on P
+    thread-ranks over loopback TCP on this host, n fp32 elements per rank, per-iteration wall
+    time of rank 0 as runner.cc:683-702 measures it.  A bounded sample: one calibration
+    allreduce, then as many as fit in ~`seconds` (1..20).  Falls back to nothing (an error
+    entry) when the reference library was not built -- never to the product."""
+    from oracle import oracle as O
+
+    if not O.ref_available():
+        raise RuntimeError("oracle/_ref (the reference built from its sources) is not present")
+    t0 = time.perf_counter()
+    O.ref_bench_ring(P, n, 0, 1)  # calibration (connect + one allreduce)
+    per = max(time.perf_counter() - t0, 1e-3)
+    iters = int(max(1, min(20, seconds / per)))
+    s = O.ref_bench_ring(P, n, 1, iters) * 1e-9  # seconds per iteration, rank 0
+    avg = float(np.mean(s))
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")),
+                         None)
+    except OSError:
+        pass
+    return {"value": round(P * 4.0 * n / avg / 1e9, 3), "unit": "GB/s", "cores": 2 * P,
+            "kind": "reference",
+            "sample": f"{iters} allreduces (after 1 warm-up) of the reference's gloo::allreduce "
+                      f"RING + gloo::sum<float> over {n} fp32 elements per rank on {P} "
+                      "thread-ranks, loopback TCP (1 user + 1 event-loop thread per rank)",
+            "value_def": "P x n x 4 B / mean per-iteration time (the same whole-job definition "
+                         "as this line's value)",
+            "ms_p50": round(float(np.percentile(s, 50)) * 1e3, 3),
+            "ms_avg": round(avg * 1e3, 3),
+            "GiBps_runner": round(4.0 * n / avg / 2 ** 30, 4),
+            "host_cpu": model, "host_logical_cpus": os.cpu_count()}
+
+
 def run_multi(args):
     import torch
     import torch.distributed as dist
@@ -386,7 +426,11 @@ def run_multi(args):
     dev = torch.device("cuda", local)
     dist.init_process_group("nccl", device_id=dev)
     try:
-        res = ring.bench_allreduce(args, dev)
+        base = None
+        if not args.no_cpu_baseline:
+            def base(P, n):
+                return ring_cpu_baseline(P, n, args.cpu_seconds)
+        res = ring.bench_allreduce(args, dev, cpu_baseline=base)
     finally:
         dist.destroy_process_group()
     if rank == 0:

@@ -25,14 +25,15 @@ ESIZE = {INT8: 1, UINT8: 1, INT32: 4, UINT32: 4, INT64: 8, UINT64: 8, FLOAT32: 4
 EXPORTS = [  # every symbol include/hydra_hip.h declares
     "hydra_abi_version", "hydra_last_error", "hydra_device_count", "hydra_device_arch",
     "hydra_device_check", "hydra_fault_report_enable", "hydra_fault_last", "hydra_fault_lookup",
-    "hydra_event_create", "hydra_event_record", "hydra_event_synchronize",
+    "hydra_event_create", "hydra_event_create_on", "hydra_event_record", "hydra_event_synchronize",
     "hydra_event_destroy",
     "hydra_reduce", "hydra_chunk_sum", "hydra_reduce_batch", "hydra_acc_bf16_f32", "hydra_f32_to_bf16",
     "hydra_set_variant", "hydra_ctx_create", "hydra_ctx_destroy", "hydra_reduce_host",
     "hydra_chunk_sum_host", "hydra_host_register", "hydra_host_unregister",
+    "hydra_page_interior", "hydra_host_mappings",
     "hydra_stream_create", "hydra_stream_destroy", "hydra_stream_synchronize", "hydra_malloc",
     "hydra_free", "hydra_memcpy", "hydra_ring_plan",
-    "hydra_comm_get_unique_id", "hydra_comm_init", "hydra_comm_destroy", "hydra_allreduce",
+    "hydra_comm_get_unique_id", "hydra_comm_init", "hydra_comm_destroy", "hydra_comm_info", "hydra_allreduce",
     "hydra_plan", "hydra_allreduce_simulate", "hydra_fold", "hydra_memcpy_async",
     "hydra_malloc_host", "hydra_free_host", "hydra_cache_trim", "hydra_pointer_device", "hydra_split_elements",
     "hydra_apipe_allreduce", "hydra_apipe_allreduce_simulate", "hydra_comm_run_plan",
@@ -73,6 +74,16 @@ class Segment(ctypes.Structure):
     """hydra_segment_t (include/hydra_hip.h): one c = op(a, b) of a hydra_reduce_batch call."""
     _fields_ = [("c", ctypes.c_void_p), ("a", ctypes.c_void_p), ("b", ctypes.c_void_p),
                 ("n", ctypes.c_size_t)]
+
+
+class HostMapping(ctypes.Structure):
+    """hydra_host_mapping_t (include/hydra_hip.h): one of hydra's live host mappings."""
+    _fields_ = [("lo", ctypes.c_uint64), ("hi", ctypes.c_uint64), ("kind", ctypes.c_int32),
+                ("owners", ctypes.c_int32), ("users", ctypes.c_int32),
+                ("owner_lo", ctypes.c_uint64), ("owner_hi", ctypes.c_uint64)]
+
+
+MAP_REGISTER, MAP_PIN, MAP_PINNED_BLOCK = 1, 2, 3
 
 
 class HydraError(RuntimeError):
@@ -122,6 +133,7 @@ def _declare(L) -> None:
                                    ctypes.POINTER(ctypes.c_uint64)]
     L.hydra_fault_lookup.argtypes = [ctypes.c_uint64, ctypes.c_char_p, sz]
     L.hydra_event_create.argtypes = [ctypes.POINTER(vp)]
+    L.hydra_event_create_on.argtypes = [ctypes.c_int, ctypes.POINTER(vp)]
     L.hydra_event_record.argtypes = [vp, vp]
     L.hydra_event_synchronize.argtypes = [vp]
     L.hydra_event_destroy.argtypes = [vp]
@@ -137,6 +149,12 @@ def _declare(L) -> None:
     L.hydra_chunk_sum_host.argtypes = [vp, i, vp, vp, vp, sz]
     L.hydra_host_register.argtypes = [vp, sz]
     L.hydra_host_unregister.argtypes = [vp]
+    L.hydra_page_interior.argtypes = [ctypes.c_uint64, sz, ctypes.POINTER(ctypes.c_uint64),
+                                      ctypes.POINTER(ctypes.c_uint64)]
+    L.hydra_page_interior.restype = None
+    L.hydra_host_mappings.argtypes = [ctypes.POINTER(HostMapping), sz, ctypes.POINTER(sz),
+                                      ctypes.POINTER(ctypes.c_uint64),
+                                      ctypes.POINTER(ctypes.c_uint64)]
     L.hydra_stream_create.argtypes = [i, ctypes.POINTER(vp)]
     L.hydra_stream_destroy.argtypes = [vp]
     L.hydra_stream_synchronize.argtypes = [vp]
@@ -159,6 +177,7 @@ def _declare(L) -> None:
     L.hydra_comm_get_unique_id.argtypes = [vp]
     L.hydra_comm_init.argtypes = [ctypes.POINTER(vp), i, i, vp, i]
     L.hydra_comm_destroy.argtypes = [vp]
+    L.hydra_comm_info.argtypes = [vp, ctypes.POINTER(i), ctypes.POINTER(i), ctypes.POINTER(i)]
     L.hydra_allreduce.argtypes = [vp, i, i, i, i, vp, sz, sz, sz, vp]
     L.hydra_plan.argtypes = [i, i, i, sz, sz, sz, sz, ctypes.POINTER(PlanOp), sz,
                              ctypes.POINTER(sz), ctypes.POINTER(sz)]
@@ -209,6 +228,26 @@ def ring_plan(P: int, n: int, esize: int, max_segment: int = 1 << 20):
     lib().hydra_ring_plan(P, n, esize, max_segment, ctypes.byref(ns), ctypes.byref(sb),
                           ctypes.byref(S))
     return ns.value, sb.value, S.value
+
+
+def page_interior(ptr: int, nbytes: int):
+    """The whole pages inside [ptr, ptr + nbytes): (lo, hi), lo == hi when there are none."""
+    lo, hi = ctypes.c_uint64(), ctypes.c_uint64()
+    lib().hydra_page_interior(ptr, nbytes, ctypes.byref(lo), ctypes.byref(hi))
+    return lo.value, hi.value
+
+
+def host_mappings():
+    """(live mappings as dicts, hipHostRegister calls made, calls that covered a byte outside
+    their caller range)."""
+    cap = 256
+    buf = (HostMapping * cap)()
+    cnt, regs, out = ctypes.c_size_t(), ctypes.c_uint64(), ctypes.c_uint64()
+    check(lib().hydra_host_mappings(buf, cap, ctypes.byref(cnt), ctypes.byref(regs),
+                                    ctypes.byref(out)))
+    live = [{f: getattr(buf[i], f) for f, _ in HostMapping._fields_}
+            for i in range(min(cnt.value, cap))]
+    return live, regs.value, out.value
 
 
 def set_variant(v: int) -> int:

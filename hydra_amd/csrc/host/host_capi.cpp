@@ -14,98 +14,39 @@
 #include "../../../include/hydra/gloo_reduce.h"
 #include "../../../include/hydra/hip_allreduce_ring.h"
 #include "../../../include/hydra_host.h"
+#include "capi_util.h"
 
-namespace {
-
-void set_err(char* err, size_t len, const std::string& s) {
-  if (err && len) {
-    std::strncpy(err, s.c_str(), len - 1);
-    err[len - 1] = 0;
-  }
-}
-
-hydra::AllreduceOptions::Func make_reducer(int reducer, int op, int dtype, hydra_reduce_fn fn) {
-  if (reducer == HYDRA_REDUCER_FN) {
-    if (!fn) throw hydra::EnforceNotMet("null reduce function");
-    return [fn](void* c, const void* a, const void* b, size_t n) { fn(c, a, b, n); };
-  }
-  return hydra::gloo_compat::hostReduce(op, dtype, 0);
-}
-
-size_t esize_of(int dtype) {
-  static const size_t sz[] = {1, 1, 4, 4, 8, 8, 4, 8, 2, 2};
-  return (dtype >= 0 && dtype <= 9) ? sz[dtype] : 0;
-}
-
-// Spawn P threads; each gets a connected context (two when rails == 2).
-int spawn(int P, int rails, char* err, size_t errlen,
-          const std::function<void(int, std::vector<std::shared_ptr<hydra::Context>>&)>& body) {
-  hydra::HashStore store;
-  std::mutex mu;
-  std::condition_variable cv;
-  int arrived = 0;
-  std::string first;
-  std::vector<std::thread> th;
-  for (int r = 0; r < P; r++) {
-    th.emplace_back([&, r] {
-      std::vector<std::shared_ptr<hydra::Context>> ctx;
-      try {
-        for (int k = 0; k < rails; k++) {
-          ctx.push_back(std::make_shared<hydra::Context>(r, P));
-          ctx.back()->connectFullMesh(store, "127.0.0.1", "rail" + std::to_string(k));
-        }
-        body(r, ctx);
-      } catch (const std::exception& e) {
-        std::lock_guard<std::mutex> g(mu);
-        if (first.empty()) first = e.what();
-      }
-      // every rank finishes before any connection closes (base_test.h:142-155)
-      std::unique_lock<std::mutex> l(mu);
-      arrived++;
-      cv.notify_all();
-      cv.wait(l, [&] { return arrived == P; });
-    });
-  }
-  for (auto& t : th) t.join();
-  if (!first.empty()) {
-    set_err(err, errlen, first);
-    return 1;
-  }
-  return 0;
-}
-
-}  // namespace
+using hydra::capi::esize_of;
+using hydra::capi::make_reducer;
+using hydra::capi::set_err;
+using hydra::capi::spawn;
 
 namespace {
 template <typename T>
-int old_ring(int kind, int P, int nptr, size_t n, void** bufs, int reducer, hydra_inplace_fn fn,
-             char* err, size_t errlen) {  // kind: 0 AllreduceRing, 1 chunked, 2 halving-doubling, 3 bcube, 4 local
+const hydra::ReductionFunction<T>* reduction_function(int reducer, hydra_inplace_fn fn,
+                                                      std::unique_ptr<hydra::ReductionFunction<T>>* custom) {
   using RF = hydra::ReductionFunction<T>;
-  const RF* rf = nullptr;
-  std::unique_ptr<RF> custom;
   if (reducer == HYDRA_REDUCER_FN) {
-    if (!fn) {
-      set_err(err, errlen, "null reduce function");
-      return 2;
-    }
-    custom.reset(new RF(hydra::CUSTOM, reinterpret_cast<typename RF::Function*>(fn)));
-    rf = custom.get();
-  } else {
-    rf = hydra::gloo_compat::gpuReductionFunction<RF, T>(hydra::SUM);
+    if (!fn) return nullptr;
+    custom->reset(new RF(hydra::CUSTOM, reinterpret_cast<typename RF::Function*>(fn)));
+    return custom->get();
+  }
+  return hydra::gloo_compat::gpuReductionFunction<RF, T>(hydra::SUM);
+}
+
+template <typename T>
+int old_ring(int kind, int P, int nptr, size_t n, void** bufs, int reducer, hydra_inplace_fn fn,
+             char* err, size_t errlen) {  // kind: 0 AllreduceRing, 1 AllreduceRingChunked
+  std::unique_ptr<hydra::ReductionFunction<T>> custom;
+  const hydra::ReductionFunction<T>* rf = reduction_function<T>(reducer, fn, &custom);
+  if (!rf) {
+    set_err(err, errlen, "null reduce function");
+    return 2;
   }
   return spawn(P, 1, err, errlen, [&](int r, std::vector<std::shared_ptr<hydra::Context>>& c) {
     std::vector<T*> ptrs;
     for (int i = 0; i < nptr; i++) ptrs.push_back(static_cast<T*>(bufs[r * nptr + i]));
-    if (kind == 4) {
-      hydra::AllreduceLocal<T> algo(c[0], ptrs, (int)n, rf);
-      algo.run();
-    } else if (kind == 3) {
-      hydra::AllreduceBcube<T> algo(c[0], ptrs, (int)n, rf);
-      algo.run();
-    } else if (kind == 2) {
-      hydra::AllreduceHalvingDoubling<T> algo(c[0], ptrs, (int)n, rf);
-      algo.run();
-    } else if (kind == 1) {
+    if (kind == 1) {
       hydra::AllreduceRingChunked<T> algo(c[0], ptrs, (int)n, rf);
       algo.run();
     } else {
@@ -116,7 +57,7 @@ int old_ring(int kind, int P, int nptr, size_t n, void** bufs, int reducer, hydr
 }
 template <typename T>
 int hip_ring(int P, int nptr, size_t n, void** bufs, int workspace, int user_streams, char* err,
-             size_t errlen, int kind = 0) {  // kind: 0 ring, 1 chunked, 2 halving-doubling, 3 local, 4 bcube
+             size_t errlen, int kind = 0) {  // kind: 0 ring, 1 chunked
   const bool chunked = kind == 1;
   return spawn(P, 1, err, errlen, [&](int r, std::vector<std::shared_ptr<hydra::Context>>& c) {
     std::vector<T*> ptrs;
@@ -128,24 +69,7 @@ int hip_ring(int P, int nptr, size_t n, void** bufs, int workspace, int user_str
       streams.resize(nptr);
       for (auto& s : streams) hydra::gloo_compat::enforce(hydra_stream_create(dev, &s));
     }
-    if (kind == 4 && workspace == HYDRA_WORKSPACE_DEVICE) {
-      hydra::HipAllreduceBcube<T, hydra::HipDeviceWorkspace<T>> algo(c[0], ptrs, (int)n, streams);
-      algo.run();
-    } else if (kind == 4) {
-      hydra::HipAllreduceBcube<T, hydra::HipHostWorkspace<T>> algo(c[0], ptrs, (int)n, streams);
-      algo.run();
-    } else if (kind == 3) {
-      hydra::HipAllreduceLocal<T> algo(c[0], ptrs, (int)n, streams);
-      algo.run();
-    } else if (kind == 2 && workspace == HYDRA_WORKSPACE_DEVICE) {
-      hydra::HipAllreduceHalvingDoubling<T, hydra::HipDeviceWorkspace<T>> algo(c[0], ptrs, (int)n,
-                                                                               streams);
-      algo.run();
-    } else if (kind == 2) {
-      hydra::HipAllreduceHalvingDoubling<T, hydra::HipHostWorkspace<T>> algo(c[0], ptrs, (int)n,
-                                                                             streams);
-      algo.run();
-    } else if (chunked && workspace == HYDRA_WORKSPACE_DEVICE) {
+    if (chunked && workspace == HYDRA_WORKSPACE_DEVICE) {
       hydra::HipAllreduceRingChunked<T, hydra::HipDeviceWorkspace<T>> algo(c[0], ptrs, (int)n,
                                                                            streams);
       algo.run();
@@ -307,24 +231,6 @@ int hydra_host_allreduce_ring_chunked_threads(int P, int nptr, int dtype, size_t
   return algorithm_ring(1, P, nptr, dtype, n, bufs, reducer, fn, err, errlen);
 }
 
-int hydra_host_allreduce_halving_doubling_threads(int P, int nptr, int dtype, size_t n,
-                                                  void** bufs, int reducer, hydra_inplace_fn fn,
-                                                  char* err, size_t errlen) {
-  return algorithm_ring(2, P, nptr, dtype, n, bufs, reducer, fn, err, errlen);
-}
-
-int hydra_host_allreduce_bcube_old_threads(int P, int nptr, int dtype, size_t n, void** bufs,
-                                           int reducer, hydra_inplace_fn fn, char* err,
-                                           size_t errlen) {
-  return algorithm_ring(3, P, nptr, dtype, n, bufs, reducer, fn, err, errlen);
-}
-
-int hydra_host_allreduce_local_threads(int P, int nptr, int dtype, size_t n, void** bufs,
-                                       int reducer, hydra_inplace_fn fn, char* err,
-                                       size_t errlen) {
-  return algorithm_ring(4, P, nptr, dtype, n, bufs, reducer, fn, err, errlen);
-}
-
 int hydra_host_hip_ring_threads(int P, int nptr, int dtype, size_t n, void** dev_bufs,
                                 int workspace, int user_streams, char* err, size_t errlen) {
   if (P < 1 || nptr < 1 || !dev_bufs || n > (size_t)INT32_MAX) {
@@ -359,69 +265,6 @@ int hydra_host_hip_ring_chunked_threads(int P, int nptr, int dtype, size_t n, vo
       return hip_ring<int64_t>(P, nptr, n, dev_bufs, workspace, user_streams, err, errlen, 1);
   }
   set_err(err, errlen, "unsupported dtype for HipAllreduceRingChunked");
-  return 3;
-}
-
-int hydra_host_hip_halving_doubling_threads(int P, int nptr, int dtype, size_t n, void** dev_bufs,
-                                        int workspace, int user_streams, char* err,
-                                        size_t errlen) {
-  if (P < 1 || nptr < 1 || !dev_bufs || n > (size_t)INT32_MAX) {
-    set_err(err, errlen, "invalid arguments");
-    return 2;
-  }
-  switch (dtype) {
-    case HYDRA_FLOAT32:
-      return hip_ring<float>(P, nptr, n, dev_bufs, workspace, user_streams, err, errlen, 2);
-    case HYDRA_INT32:
-      return hip_ring<int32_t>(P, nptr, n, dev_bufs, workspace, user_streams, err, errlen, 2);
-    case HYDRA_FLOAT64:
-      return hip_ring<double>(P, nptr, n, dev_bufs, workspace, user_streams, err, errlen, 2);
-    case HYDRA_INT64:
-      return hip_ring<int64_t>(P, nptr, n, dev_bufs, workspace, user_streams, err, errlen, 2);
-  }
-  set_err(err, errlen, "unsupported dtype for HipAllreduceHalvingDoubling");
-  return 3;
-}
-
-int hydra_host_hip_bcube_threads(int P, int nptr, int dtype, size_t n, void** dev_bufs,
-                                        int workspace, int user_streams, char* err,
-                                        size_t errlen) {
-  if (P < 1 || nptr < 1 || !dev_bufs || n > (size_t)INT32_MAX) {
-    set_err(err, errlen, "invalid arguments");
-    return 2;
-  }
-  switch (dtype) {
-    case HYDRA_FLOAT32:
-      return hip_ring<float>(P, nptr, n, dev_bufs, workspace, user_streams, err, errlen, 4);
-    case HYDRA_INT32:
-      return hip_ring<int32_t>(P, nptr, n, dev_bufs, workspace, user_streams, err, errlen, 4);
-    case HYDRA_FLOAT64:
-      return hip_ring<double>(P, nptr, n, dev_bufs, workspace, user_streams, err, errlen, 4);
-    case HYDRA_INT64:
-      return hip_ring<int64_t>(P, nptr, n, dev_bufs, workspace, user_streams, err, errlen, 4);
-  }
-  set_err(err, errlen, "unsupported dtype for HipAllreduceBcube");
-  return 3;
-}
-
-int hydra_host_hip_local_threads(int P, int nptr, int dtype, size_t n, void** dev_bufs,
-                                        int workspace, int user_streams, char* err,
-                                        size_t errlen) {
-  if (P < 1 || nptr < 1 || !dev_bufs || n > (size_t)INT32_MAX) {
-    set_err(err, errlen, "invalid arguments");
-    return 2;
-  }
-  switch (dtype) {
-    case HYDRA_FLOAT32:
-      return hip_ring<float>(P, nptr, n, dev_bufs, workspace, user_streams, err, errlen, 3);
-    case HYDRA_INT32:
-      return hip_ring<int32_t>(P, nptr, n, dev_bufs, workspace, user_streams, err, errlen, 3);
-    case HYDRA_FLOAT64:
-      return hip_ring<double>(P, nptr, n, dev_bufs, workspace, user_streams, err, errlen, 3);
-    case HYDRA_INT64:
-      return hip_ring<int64_t>(P, nptr, n, dev_bufs, workspace, user_streams, err, errlen, 3);
-  }
-  set_err(err, errlen, "unsupported dtype for HipAllreduceLocal");
   return 3;
 }
 

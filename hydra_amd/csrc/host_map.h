@@ -1,0 +1,81 @@
+// host_map.h -- which caller host memory a kernel may touch in place (zero-copy), and for how long.
+//
+// hydra_reduce_host lets the chunk-sum kernel read and write host operands over PCIe when they
+// are mapped for the GPU.  A mapping the kernel uses must stay mapped until the kernel is done,
+// and hydra must never map a page that holds memory outside the operand it was asked about: the
+// HIP runtime maps registered host pages at their own address, and two owners registering one
+// page (say, a per-call pin of a sub-page operand and the runtime's page-rounded lock of a
+// neighbouring buffer for a pageable copy) share that GPU mapping until the first one releases
+// it -- the leading suspect for round 2's late device faults.  So:
+//
+//   * every registration hydra makes (hydra_host_register, a per-call pin of a pageable operand)
+//     covers only the WHOLE PAGES strictly inside the caller's range; the ragged head / tail
+//     bytes are staged through device buffers instead;
+//   * hydra's registrations never overlap each other: one registry (an interval map) holds them,
+//     plus the pinned blocks of the block cache; a call that finds its operand inside a registry
+//     entry takes a reference on it, so the entry outlives the call's kernel whatever its owner
+//     does meanwhile (the case round 2's advisor raised: one thread's operand inside another
+//     thread's per-call pin);
+//   * a mapping hydra did not make (the caller's own hipHostRegister / hipHostMalloc, e.g. torch
+//     pinned tensors) is looked up with the registry lock held, so no hydra registration can
+//     appear or vanish between the lookup and its use; the caller keeps it alive for the call,
+//     as for any asynchronous copy from it.
+//
+// Windows are byte ranges [lo, hi) inside the operand; the rest of the operand is staged.
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+
+namespace hydra {
+
+size_t page_size();
+
+// Whole pages strictly inside [p, p + bytes): [*lo, *hi) (empty: *lo == *hi).
+void page_interior(uintptr_t p, size_t bytes, uintptr_t* lo, uintptr_t* hi);
+
+enum HostMapKind : int {
+  kMapNone = 0,
+  kMapRegister = 1,     // hydra_host_register (whole interior pages)
+  kMapPin = 2,          // pinned for one hydra_reduce_host call (whole interior pages)
+  kMapPinnedBlock = 3,  // hipHostMalloc block of the cache (hydra_malloc_host)
+  kMapCaller = 4,       // mapped by the caller, not by hydra (no reference taken)
+};
+
+struct HostWindow {
+  const char* lo = nullptr;  // [lo, hi) of the operand is mapped; dev is lo's device address
+  const char* hi = nullptr;
+  char* dev = nullptr;
+  int kind = kMapNone;
+  uintptr_t key = 0;  // registry entry referenced by this window (0: none)
+  bool empty() const { return lo >= hi; }
+};
+
+// The mapped window of the operand [p, p + bytes) (referenced until host_window_release).
+// pin: a pageable operand's interior pages may be registered for the call.
+HostWindow host_window_acquire(const void* p, size_t bytes, bool pin);
+void host_window_release(HostWindow* w);
+
+// hydra_host_register / hydra_host_unregister (C-ABI semantics in include/hydra_hip.h).
+// Return a hydra status; *what names the failing step.
+int host_register(void* p, size_t bytes, const char** what);
+int host_unregister(void* p, const char** what);
+
+// The block cache's pinned blocks (whole allocations; never registered, never unregistered here).
+void host_map_add_block(void* p, size_t bytes);
+void host_map_remove_block(void* p);
+
+// Test hook: the registry's live entries.
+struct HostMapEntry {
+  uintptr_t lo, hi;
+  int kind;
+  int owners;  // hydra_host_register owners of the entry
+  int users;   // calls holding a window on it
+  uintptr_t owner_lo, owner_hi;  // the caller range that created it (kMapRegister / kMapPin)
+};
+size_t host_map_snapshot(HostMapEntry* out, size_t cap);
+// Registrations (hipHostRegister calls) hydra has made so far, and how many of them covered a
+// byte outside the caller range they were made for (must stay 0).
+void host_map_counters(uint64_t* registrations, uint64_t* outside);
+
+}  // namespace hydra

@@ -12,10 +12,12 @@
 #include <map>
 #include <mutex>
 #include <string>
+#include <vector>
 
 #include "../../include/hydra_hip.h"
 #include "errors.h"
 #include "fault_report.h"
+#include "host_map.h"
 #include "resource_cache.h"
 #include "reduce_kernels.h"
 #include "trace.h"
@@ -129,6 +131,14 @@ int hydra_device_arch(int device, char* buf, size_t len) {
 }
 
 int hydra_device_check(int device) {
+  int prev = -1;
+  if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+  struct Restore {  // the caller's current device is left as it was
+    int d;
+    ~Restore() {
+      if (d >= 0) (void)hipSetDevice(d);
+    }
+  } restore_{prev};
   HIP_TRY(hipSetDevice(device));
   HIP_TRY(hipDeviceSynchronize());  // surfaces an asynchronous fault of any enqueued work
   const hipError_t e = hipGetLastError();
@@ -249,63 +259,45 @@ int hydra_ctx_destroy(hydra_ctx_t ctx) {
 }
 
 namespace {
-// Device address of the host range [p, p + bytes) when ALL of it lies in one pinned
-// (hipHostMalloc) or registered (hipHostRegister) range, else null (pageable, or only partly
-// covered: a kernel must never stream past a registration's end).
-void* mapped_device_range(const void* p, size_t bytes) {
-  hipPointerAttribute_t at{};
-  if (hipPointerGetAttributes(&at, p) != hipSuccess) {
-    (void)hipGetLastError();
-    return nullptr;
+// Host copies of pageable memory go in pieces of at most 1 MiB: up to that size the HIP runtime
+// copies through its own staging buffers, above it it locks the caller's pages for the copy --
+// page-rounded, so the lock's edge pages hold the operand's neighbours.  hydra
+// never asks the runtime to lock memory outside an operand.
+constexpr size_t kCopyPiece = 1u << 20;
+
+hipError_t copy_pieces(void* dst, const void* src, size_t bytes, hipMemcpyKind kind,
+                       hipStream_t st) {
+  for (size_t off = 0; off < bytes; off += kCopyPiece) {
+    const size_t b = std::min(kCopyPiece, bytes - off);
+    hipError_t e = hipMemcpyAsync(static_cast<char*>(dst) + off,
+                                  static_cast<const char*>(src) + off, b, kind, st);
+    if (e != hipSuccess) return e;
   }
-  if (at.type != hipMemoryTypeHost || !at.devicePointer) return nullptr;
-  void* start = nullptr;
-  size_t size = 0;
-  if (hipPointerGetAttribute(&start, HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR,
-                             reinterpret_cast<hipDeviceptr_t>(const_cast<void*>(p))) != hipSuccess ||
-      hipPointerGetAttribute(&size, HIP_POINTER_ATTRIBUTE_RANGE_SIZE,
-                             reinterpret_cast<hipDeviceptr_t>(const_cast<void*>(p))) != hipSuccess) {
-    (void)hipGetLastError();
-    return nullptr;
-  }
-  const char* s0 = static_cast<const char*>(start);
-  const char* q = static_cast<const char*>(p);
-  if (q < s0 || bytes > size || (size_t)(q - s0) > size - bytes) return nullptr;
-  if (!at.hostPointer) return at.devicePointer;
-  return static_cast<char*>(at.devicePointer) +
-         (static_cast<const char*>(p) - static_cast<const char*>(at.hostPointer));
+  return hipSuccess;
 }
 
-// Pins a pageable operand for the duration of one call (hipHostRegister of exactly its range:
-// a few microseconds, and registrations of overlapping pages are independent of each other, so
-// concurrent callers -- the two rails of bew_allreduce_a -- cannot disturb one another), and
-// unpins it when the call is done.  Failure to pin leaves the operand to the staged path.
-struct TempPin {
-  void* host = nullptr;
-  void* dev = nullptr;
-  bool pin(const void* p, size_t bytes) {
-    if (hipHostRegister(const_cast<void*>(p), bytes, hipHostRegisterDefault) != hipSuccess) {
-      (void)hipGetLastError();
-      return false;
-    }
-    host = const_cast<void*>(p);
-    hydra::ledger_add(hydra::kLedgerTempPin, p, bytes);
-    dev = mapped_device_range(p, bytes);
-    if (!dev) {
-      release();
-      return false;
-    }
-    return true;
+// The mapped windows of one call's operands, released (after the call's kernels finished)
+// when the call returns.
+struct Windows {
+  hydra::HostWindow w[3];
+  ~Windows() {
+    for (auto& x : w) hydra::host_window_release(&x);
   }
-  void release() {
-    if (host) {
-      (void)hipHostUnregister(host);
-      hydra::ledger_release(hydra::kLedgerTempPin, host);
-    }
-    host = nullptr;
-    dev = nullptr;
+};
+
+// An operand's window in elements: [lo, hi) of [0, n) (empty: lo == hi == 0).
+struct ElemRange {
+  size_t lo = 0, hi = 0;
+  bool covers(size_t a, size_t b) const { return lo <= a && b <= hi && a < b; }
+  static ElemRange of(const hydra::HostWindow& w, const void* base, size_t es, size_t n) {
+    ElemRange r;
+    if (w.empty()) return r;
+    const char* b = static_cast<const char*>(base);
+    r.lo = (size_t(w.lo - b) + es - 1) / es;
+    r.hi = std::min(n, size_t(w.hi - b) / es);
+    if (r.lo >= r.hi) r = ElemRange{};
+    return r;
   }
-  ~TempPin() { release(); }
 };
 }  // namespace
 
@@ -320,21 +312,16 @@ int hydra_reduce_host(hydra_ctx_t ctx, int op, int dtype, void* c, const void* a
   const size_t es = hydra::dtype_size(dtype);
   const size_t per = ctx->chunk_bytes / es;
   const int variant = g_variant.load(std::memory_order_relaxed);
-  // Each operand that is pinned/registered host memory (the ring's receive slots after
-  // Context::setScratchAllocator(pinnedAlloc), an output after hydra_host_register) is read or
-  // written by the kernel in place over PCIe (zero-copy); an operand that cannot be pinned is
-  // staged through device buffers.  All three pinned: one kernel pass, no copies at all.
-  // kVariantForceStaging stages everything (A/B).
-  // Pageable operands are pinned for the call itself (TempPin: hipHostRegister of exactly the
-  // operand, ~4 us) so the kernel streams them too; where that fails they are staged.
-  // kVariantNoPinOnTheFly keeps pageable operands on the staged path (A/B).
   const size_t nbytes = n * es;
-  void* mc = nullptr;
-  void* ma = nullptr;
-  void* mb = nullptr;
-  TempPin pc_, pa_, pb_;
-  // Declared after the pins, so destroyed before them: an early error return drains both
-  // streams before any operand is unpinned (work enqueued earlier may still use it).
+  // Each operand's mapped window (host_map.h): the part of it the kernel may read / write in
+  // place over PCIe -- a registered bucket (hydra_host_register), a pinned block
+  // (hydra_malloc_host, e.g. the ring's receive slots after setScratchAllocator(pinnedAlloc)),
+  // the caller's own pinned / registered memory, or, for a pageable operand, the whole pages
+  // inside it pinned for this call.  Elements inside all three windows are reduced in one
+  // zero-copy pass; the rest (the ragged edge pages of pageable operands, anything unmapped) is
+  // staged through device buffers, per operand.  kVariantForceStaging stages everything;
+  // kVariantNoPinOnTheFly maps only memory that is already mapped (A/B).
+  Windows win;  // declared before the drain: released only after every stream is drained
   struct DrainOnError {
     hipStream_t* st;
     bool armed = true;
@@ -344,77 +331,98 @@ int hydra_reduce_host(hydra_ctx_t ctx, int op, int dtype, void* c, const void* a
           if (st[i]) (void)hipStreamSynchronize(st[i]);
     }
   } drain_{ctx->stream};
+  ElemRange rc_, ra_, rb_;
   if (variant != kVariantForceStaging) {
-    const bool fly = variant != kVariantNoPinOnTheFly;
-    mc = mapped_device_range(c, nbytes);
-    if (!mc && fly && pc_.pin(c, nbytes)) mc = pc_.dev;
+    const bool pin = variant != kVariantNoPinOnTheFly;
+    win.w[0] = hydra::host_window_acquire(c, nbytes, pin);
+    rc_ = ElemRange::of(win.w[0], c, es, n);
     if (a == c) {
-      ma = mc;
+      ra_ = rc_;
     } else {
-      ma = mapped_device_range(a, nbytes);
-      if (!ma && fly && pa_.pin(a, nbytes)) ma = pa_.dev;
+      win.w[1] = hydra::host_window_acquire(a, nbytes, pin);
+      ra_ = ElemRange::of(win.w[1], a, es, n);
     }
     if (b == c) {
-      mb = mc;
+      rb_ = rc_;
     } else if (b == a) {
-      mb = ma;
+      rb_ = ra_;
     } else {
-      mb = mapped_device_range(b, nbytes);
-      if (!mb && fly && pb_.pin(b, nbytes)) mb = pb_.dev;
-    }
-    if (mc && ma && mb) {
-      hipError_t e = hydra::launch_reduce(0, op, dtype, mc, ma, mb, n, ctx->stream[0]);
-      if (e != hipSuccess) return hip_fail(e, "reduce kernel launch (zero-copy)");
-      HIP_TRY(hipStreamSynchronize(ctx->stream[0]));
-      drain_.armed = false;
-      return ok();  // the TempPins unpin here, after the kernel finished
+      win.w[2] = hydra::host_window_acquire(b, nbytes, pin);
+      rb_ = ElemRange::of(win.w[2], b, es, n);
     }
   }
-  size_t k = 0;
-  for (size_t off = 0; off < n; off += per, k++) {
-    const size_t cnt = std::min(per, n - off);
-    const size_t bytes = cnt * es;
-    const int s = (int)(k & 1);
-    hipStream_t st = ctx->stream[s];
-    const size_t ob = off * es;
-    const char* pa = static_cast<const char*>(a) + ob;
-    const char* pb = static_cast<const char*>(b) + ob;
-    char* pc = static_cast<char*>(c) + ob;
-    // operand a: mapped in place, else staged
-    const void* ka = ma ? static_cast<const void*>(static_cast<char*>(ma) + ob) : ctx->da[s];
-    if (!ma) HIP_TRY(hipMemcpyAsync(ctx->da[s], pa, bytes, hipMemcpyHostToDevice, st));
-    const void* kb;
-    if (b == a) {
-      kb = ka;
-    } else if (mb) {
-      kb = static_cast<char*>(mb) + ob;
-    } else {
-      HIP_TRY(hipMemcpyAsync(ctx->db[s], pb, bytes, hipMemcpyHostToDevice, st));
-      kb = ctx->db[s];
+  const hydra::HostWindow& wc = win.w[0];
+  const hydra::HostWindow& wa = a == c ? win.w[0] : win.w[1];
+  const hydra::HostWindow& wb = b == c ? win.w[0] : b == a ? wa : win.w[2];
+  // device address of element i of an operand inside its window
+  auto dev = [es](const hydra::HostWindow& w, const void* base, size_t i) -> char* {
+    return w.dev + (static_cast<const char*>(base) + i * es - w.lo);
+  };
+  // zero-copy region: inside all three windows
+  const size_t z0 = std::max({rc_.lo, ra_.lo, rb_.lo});
+  const size_t z1 = std::min({rc_.hi, ra_.hi, rb_.hi});
+  const bool zero = z0 < z1;
+  if (zero) {
+    hipError_t e = hydra::launch_reduce(0, op, dtype, dev(wc, c, z0), dev(wa, a, z0),
+                                        dev(wb, b, z0), z1 - z0, ctx->stream[0]);
+    if (e != hipSuccess) return hip_fail(e, "reduce kernel launch (zero-copy)");
+  }
+  // the rest, staged per operand in chunks over both streams
+  struct Span {
+    size_t lo, hi;
+  };
+  Span spans[2] = {{0, zero ? z0 : n}, {zero ? z1 : n, n}};
+  size_t k = zero ? 1 : 0;  // the zero-copy pass ran on stream 0
+  for (const Span& sp : spans) {
+    for (size_t off = sp.lo; off < sp.hi; off += per, k++) {
+      const size_t cnt = std::min(per, sp.hi - off);
+      const size_t bytes = cnt * es;
+      const int s = (int)(k & 1);
+      hipStream_t st = ctx->stream[s];
+      const size_t ob = off * es;
+      const char* pa = static_cast<const char*>(a) + ob;
+      const char* pb = static_cast<const char*>(b) + ob;
+      char* pc = static_cast<char*>(c) + ob;
+      const bool ma = ra_.covers(off, off + cnt);
+      const bool mb = rb_.covers(off, off + cnt);
+      const bool mc = rc_.covers(off, off + cnt);
+      // operand a: mapped in place, else staged
+      const void* ka = ma ? static_cast<const void*>(dev(wa, a, off)) : ctx->da[s];
+      if (!ma) HIP_TRY(copy_pieces(ctx->da[s], pa, bytes, hipMemcpyHostToDevice, st));
+      const void* kb;
+      if (b == a) {
+        kb = ka;
+      } else if (mb) {
+        kb = dev(wb, b, off);
+      } else {
+        HIP_TRY(copy_pieces(ctx->db[s], pb, bytes, hipMemcpyHostToDevice, st));
+        kb = ctx->db[s];
+      }
+      // destination: mapped in place; else in place on the staged a (c == a, the ring's form)
+      // or a staging buffer of its own -- which must hold c's old bits for float16's store quirk
+      void* kc;
+      bool copy_back = false;
+      if (mc) {
+        kc = dev(wc, c, off);
+      } else if (c == a && !ma) {
+        kc = ctx->da[s];
+        copy_back = true;
+      } else {
+        if (!ctx->dc[s]) HIP_TRY(hydra::cached_malloc(ctx->device, ctx->chunk_bytes, &ctx->dc[s]));
+        kc = ctx->dc[s];
+        if (dtype == HYDRA_FLOAT16) HIP_TRY(copy_pieces(kc, pc, bytes, hipMemcpyHostToDevice, st));
+        copy_back = true;
+      }
+      hipError_t e = hydra::launch_reduce(variant >= 1000 ? 0 : variant, op, dtype, kc, ka, kb,
+                                          cnt, st);
+      if (e != hipSuccess) return hip_fail(e, "reduce kernel launch");
+      if (copy_back) HIP_TRY(copy_pieces(pc, kc, bytes, hipMemcpyDeviceToHost, st));
     }
-    // destination: mapped in place; else in place on the staged a (c == a, the ring's form) or a
-    // staging buffer of its own -- which must hold c's old bits for float16's store quirk
-    void* kc;
-    bool copy_back = false;
-    if (mc) {
-      kc = static_cast<char*>(mc) + ob;
-    } else if (c == a) {
-      kc = ctx->da[s];  // (a is pageable too: c == a and mc == null)
-      copy_back = true;
-    } else {
-      if (!ctx->dc[s]) HIP_TRY(hydra::cached_malloc(ctx->device, ctx->chunk_bytes, &ctx->dc[s]));
-      kc = ctx->dc[s];
-      if (dtype == HYDRA_FLOAT16) HIP_TRY(hipMemcpyAsync(kc, pc, bytes, hipMemcpyHostToDevice, st));
-      copy_back = true;
-    }
-    hipError_t e = hydra::launch_reduce(variant, op, dtype, kc, ka, kb, cnt, st);
-    if (e != hipSuccess) return hip_fail(e, "reduce kernel launch");
-    if (copy_back) HIP_TRY(hipMemcpyAsync(pc, kc, bytes, hipMemcpyDeviceToHost, st));
   }
   HIP_TRY(hipStreamSynchronize(ctx->stream[0]));
   HIP_TRY(hipStreamSynchronize(ctx->stream[1]));
   drain_.armed = false;
-  return ok();
+  return ok();  // the windows are released here, after every kernel finished
 }
 
 int hydra_chunk_sum_host(hydra_ctx_t ctx, int dtype, void* c, const void* a, const void* b,
@@ -422,46 +430,37 @@ int hydra_chunk_sum_host(hydra_ctx_t ctx, int dtype, void* c, const void* a, con
   return hydra_reduce_host(ctx, HYDRA_SUM, dtype, c, a, b, n);
 }
 
-namespace {
-// Registrations made by hydra_host_register, reference-counted per start address: each register
-// needs its own unregister, so two owners of one buffer (two rank threads, a caller and a ring
-// class) cannot release each other's registration.
-std::mutex g_reg_mu;
-std::map<void*, std::pair<size_t, int>> g_regs;  // ptr -> (bytes, count)
-}  // namespace
-
 int hydra_host_register(void* ptr, size_t bytes) {
-  if (!ptr || !bytes) return fail(HYDRA_ERR_INVALID, "null/empty range");
-  std::lock_guard<std::mutex> g(g_reg_mu);
-  auto it = g_regs.find(ptr);
-  if (it != g_regs.end()) {
-    if (bytes > it->second.first)
-      return fail(HYDRA_ERR_INVALID, "already registered with a shorter range: unregister it first");
-    it->second.second++;
-    return ok();
-  }
-  hipError_t e = hipHostRegister(ptr, bytes, hipHostRegisterDefault);
-  if (e == hipErrorHostMemoryAlreadyRegistered) {  // registered by its owner: used, never released here
-    (void)hipGetLastError();
-    return ok();
-  }
-  if (e != hipSuccess) return hip_fail(e, "hipHostRegister");
-  g_regs[ptr] = {bytes, 1};
-  hydra::ledger_add(hydra::kLedgerHostRegister, ptr, bytes);
+  const char* what = "";
+  const int rc = hydra::host_register(ptr, bytes, &what);
+  if (rc != HYDRA_OK) return fail(rc, std::string("hydra_host_register: ") + what);
   return ok();
 }
 
 int hydra_host_unregister(void* ptr) {
-  std::lock_guard<std::mutex> g(g_reg_mu);
-  auto it = g_regs.find(ptr);
-  if (it == g_regs.end()) return ok();  // not registered here (or already released)
-  if (--it->second.second > 0) return ok();
-  g_regs.erase(it);
-  hipError_t e = hipHostUnregister(ptr);
-  if (e == hipSuccess) hydra::ledger_release(hydra::kLedgerHostRegister, ptr);
-  if (e != hipSuccess && e != hipErrorHostMemoryNotRegistered) return hip_fail(e, "unregister");
-  (void)hipGetLastError();
+  const char* what = "";
+  const int rc = hydra::host_unregister(ptr, &what);
+  if (rc != HYDRA_OK) return fail(rc, std::string("hydra_host_unregister: ") + what);
   return ok();
+}
+
+int hydra_host_mappings(hydra_host_mapping_t* out, size_t cap, size_t* count,
+                        uint64_t* registrations, uint64_t* outside) {
+  std::vector<hydra::HostMapEntry> v(cap);
+  const size_t k = hydra::host_map_snapshot(v.data(), cap);
+  for (size_t i = 0; i < std::min(k, cap) && out; i++)
+    out[i] = hydra_host_mapping_t{v[i].lo, v[i].hi, v[i].kind, v[i].owners, v[i].users,
+                                  v[i].owner_lo, v[i].owner_hi};
+  if (count) *count = k;
+  hydra::host_map_counters(registrations, outside);
+  return ok();
+}
+
+void hydra_page_interior(uint64_t ptr, size_t bytes, uint64_t* lo, uint64_t* hi) {
+  uintptr_t l = 0, h = 0;
+  hydra::page_interior(static_cast<uintptr_t>(ptr), bytes, &l, &h);
+  if (lo) *lo = l;
+  if (hi) *hi = h;
 }
 
 // ---- helpers --------------------------------------------------------------------------------
@@ -483,10 +482,12 @@ int hydra_stream_synchronize(hydra_stream_t s) {
   return ok();
 }
 
-int hydra_event_create(hydra_event_t* out) {
+int hydra_event_create(hydra_event_t* out) { return hydra_event_create_on(-1, out); }
+
+int hydra_event_create_on(int device, hydra_event_t* out) {
   if (!out) return fail(HYDRA_ERR_INVALID, "null out");
   hipEvent_t e = nullptr;
-  HIP_TRY(hydra::cached_event(&e));
+  HIP_TRY(hydra::cached_event(device, &e));
   *out = e;
   return ok();
 }

@@ -2,7 +2,10 @@
 #include "resource_cache.h"
 
 #include "fault_report.h"
+#include "host_map.h"
 
+#include <atomic>
+#include <cstdint>
 #include <map>
 #include <mutex>
 #include <tuple>
@@ -63,6 +66,28 @@ struct DeviceScope {
   }
 };
 
+// Devices hydra has created streams, events or blocks on (bit d), plus the caller's current one:
+// the devices whose kernels may be reading a pinned block.  Touching any other device would
+// create a context on it.
+std::atomic<uint64_t> g_devices{0};
+void note_device(int d) {
+  if (d >= 0 && d < 64) g_devices.fetch_or(uint64_t(1) << d, std::memory_order_relaxed);
+}
+
+// Drains those devices; the caller's current device is left as it was.
+hipError_t sync_all_devices() {
+  int cur = -1;
+  if (hipGetDevice(&cur) == hipSuccess) note_device(cur);
+  const uint64_t m = g_devices.load(std::memory_order_relaxed);
+  hipError_t e = hipSuccess;
+  for (int d = 0; d < 64 && e == hipSuccess; d++) {
+    if (!(m >> d & 1)) continue;
+    DeviceScope ds(d);
+    e = ds.err != hipSuccess ? ds.err : hipDeviceSynchronize();
+  }
+  return e;
+}
+
 hipError_t take_block(const BlockKey& k, void** out) {
   Caches& c = C();
   {
@@ -82,6 +107,7 @@ hipError_t take_block(const BlockKey& k, void** out) {
       k.host ? hipHostMalloc(&p, k.bytes, hipHostMallocDefault) : hipMalloc(&p, k.bytes);
   if (e != hipSuccess) return e;
   ledger_add(k.host ? kLedgerPinnedBlock : kLedgerDeviceBlock, p, k.bytes);
+  if (k.host) host_map_add_block(p, k.bytes);  // zero-copy operands may lie in it
   std::lock_guard<std::mutex> g(c.m);
   c.live_blocks[p] = k;
   *out = p;
@@ -101,10 +127,11 @@ hipError_t give_block(void* p, bool host) {
     k = it->second;
     c.live_blocks.erase(it);  // a second release of p now fails above or below, never twice
   }
-  // hipFree's implicit synchronisation: work enqueued before the release may still use p
-  hipError_t e;
-  {
-    DeviceScope ds(k.host ? -1 : k.device);
+  // hipFree's implicit synchronisation: work enqueued before the release may still use p (a
+  // pinned block: on any device -- the kernels of every device can read it in place)
+  hipError_t e = k.host ? sync_all_devices() : hipSuccess;
+  if (!k.host) {
+    DeviceScope ds(k.device);
     e = hipDeviceSynchronize();
   }
   {
@@ -118,6 +145,7 @@ hipError_t give_block(void* p, bool host) {
     }
   }
   DeviceScope ds(k.host ? -1 : k.device);
+  if (k.host) host_map_remove_block(p);
   hipError_t f = k.host ? hipHostFree(p) : hipFree(p);
   ledger_release(k.host ? kLedgerPinnedBlock : kLedgerDeviceBlock, p);
   return e != hipSuccess ? e : f;
@@ -129,6 +157,7 @@ hipError_t cached_malloc(int device, size_t bytes, void** out) {
   if (device < 0) return hipErrorInvalidDevice;
   DeviceScope ds(device);  // the caller's current device is left as it was
   if (ds.err != hipSuccess) return ds.err;
+  note_device(device);
   return take_block(BlockKey{false, device, size_class(bytes)}, out);
 }
 
@@ -144,6 +173,7 @@ hipError_t cached_stream(int device, hipStream_t* out) {
   if (device < 0) return hipErrorInvalidDevice;
   DeviceScope ds(device);  // the caller's current device is left as it was
   if (ds.err != hipSuccess) return ds.err;
+  note_device(device);
   Caches& c = C();
   {
     std::lock_guard<std::mutex> g(c.m);
@@ -191,10 +221,13 @@ hipError_t release_stream(hipStream_t s) {
   return e != hipSuccess ? e : f;
 }
 
-hipError_t cached_event(hipEvent_t* out) {
-  int device = 0;
-  hipError_t e = hipGetDevice(&device);
+hipError_t cached_event(int device, hipEvent_t* out) {
+  hipError_t e = hipSuccess;
+  if (device < 0) e = hipGetDevice(&device);
   if (e != hipSuccess) return e;
+  DeviceScope ds(device);  // created on `device`; the caller's current device is left as it was
+  if (ds.err != hipSuccess) return ds.err;
+  note_device(device);
   Caches& c = C();
   {
     std::lock_guard<std::mutex> g(c.m);
@@ -271,6 +304,7 @@ hipError_t trim_caches() {
   }
   for (auto& kv : blocks) {
     DeviceScope ds(kv.first.host ? -1 : kv.first.device);
+    if (kv.first.host) host_map_remove_block(kv.second);
     note(kv.first.host ? hipHostFree(kv.second) : hipFree(kv.second));
     ledger_release(kv.first.host ? kLedgerPinnedBlock : kLedgerDeviceBlock, kv.second);
   }

@@ -30,7 +30,7 @@ hipError_t cached_malloc_host(size_t bytes, void** out);
 hipError_t cached_free_host(void* p);
 hipError_t cached_stream(int device, hipStream_t* out);  // non-blocking
 hipError_t release_stream(hipStream_t s);
-hipError_t cached_event(hipEvent_t* out);  // hipEventDisableTiming
+hipError_t cached_event(int device, hipEvent_t* out);  // hipEventDisableTiming; -1: current device
 hipError_t release_event(hipEvent_t e);
 hipError_t trim_caches();
 

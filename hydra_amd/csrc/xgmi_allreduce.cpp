@@ -205,7 +205,7 @@ namespace {
 int ensure_events(hydra_comm* c, size_t n) {
   while (c->events.size() < n) {
     hipEvent_t e;
-    HIP_TRY(hydra::cached_event(&e));
+    HIP_TRY(hydra::cached_event(-1, &e));
     c->events.push_back(e);
   }
   return HYDRA_OK;
@@ -319,9 +319,9 @@ int hydra_comm_init(hydra_comm_t* out, int nranks, int rank, const void* id, int
   }
   hipError_t e = hydra::cached_stream(device, &c->cs);
   if (e == hipSuccess) e = hydra::cached_stream(device, &c->ks);
-  if (e == hipSuccess) e = hydra::cached_event(&c->ev_start);
-  if (e == hipSuccess) e = hydra::cached_event(&c->ev_cs);
-  if (e == hipSuccess) e = hydra::cached_event(&c->ev_ks);
+  if (e == hipSuccess) e = hydra::cached_event(-1, &c->ev_start);
+  if (e == hipSuccess) e = hydra::cached_event(-1, &c->ev_cs);
+  if (e == hipSuccess) e = hydra::cached_event(-1, &c->ev_ks);
   if (e != hipSuccess) {
     hydra_comm_destroy(c);
     return hydra::hip_fail(e, "hydra_comm_init streams");
@@ -353,6 +353,19 @@ int hydra_comm_wait(hydra_comm_t c, hydra_stream_t stream, int64_t timeout_ms) {
     }
     if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(50));
   }
+}
+
+int hydra_comm_info(hydra_comm_t c, int* nranks, int* rank, int* device) {
+  if (!c || !c->nccl) return fail(HYDRA_ERR_INVALID, "null communicator");
+  int cnt = 0, r = 0, d = 0;
+  ncclResult_t e = ncclCommCount(c->nccl, &cnt);
+  if (e == ncclSuccess) e = ncclCommUserRank(c->nccl, &r);
+  if (e == ncclSuccess) e = ncclCommCuDevice(c->nccl, &d);
+  if (e != ncclSuccess) return fail(HYDRA_ERR_HIP, std::string("ncclCommCount: ") + ncclGetErrorString(e));
+  if (nranks) *nranks = cnt;
+  if (rank) *rank = r;
+  if (device) *device = d;
+  return ok();
 }
 
 int hydra_comm_destroy(hydra_comm_t c) {

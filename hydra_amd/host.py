@@ -11,11 +11,14 @@ import numpy as np
 from . import _lib
 
 LIB_PATH = os.path.join(_lib.HERE, "libhydra_host.so")
+# OUT OF SCOPE, opt-in: the other Algorithm-API classes (include/hydra_host_extra.h)
+EXTRA_LIB_PATH = os.path.join(_lib.HERE, "libhydra_host_extra.so")
 REDUCER_GPU, REDUCER_FN = 0, 1
 SPLIT_AA, SPLIT_AG = 0, 1
 REDUCE_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                              ctypes.c_size_t)
 _h = None
+_x = None
 
 
 def lib():
@@ -38,18 +41,8 @@ def lib():
                                                             ctypes.c_char_p, sz]
         L.hydra_host_hip_ring_threads.argtypes = [i, i, i, sz, vp, i, i, ctypes.c_char_p, sz]
         L.hydra_host_hip_ring_chunked_threads.argtypes = L.hydra_host_hip_ring_threads.argtypes
-        L.hydra_host_hip_halving_doubling_threads.argtypes = \
-            L.hydra_host_hip_ring_threads.argtypes
         L.hydra_host_allreduce_ring_chunked_threads.argtypes = \
             L.hydra_host_allreduce_ring_old_threads.argtypes
-        L.hydra_host_allreduce_halving_doubling_threads.argtypes = \
-            L.hydra_host_allreduce_ring_old_threads.argtypes
-        L.hydra_host_allreduce_bcube_old_threads.argtypes = \
-            L.hydra_host_allreduce_ring_old_threads.argtypes
-        L.hydra_host_allreduce_local_threads.argtypes = \
-            L.hydra_host_allreduce_ring_old_threads.argtypes
-        L.hydra_host_hip_local_threads.argtypes = L.hydra_host_hip_ring_threads.argtypes
-        L.hydra_host_hip_bcube_threads.argtypes = L.hydra_host_hip_ring_threads.argtypes
         L.hydra_host_reduce_threads.argtypes = [i, i, i, sz, vp, vp, i, sz, i, vp,
                                                 ctypes.c_long, ctypes.c_char_p, sz]
         L.hydra_host_reduce_timeout_probe.argtypes = [ctypes.c_long, ctypes.c_char_p, sz]
@@ -57,6 +50,26 @@ def lib():
                                                  ctypes.c_char_p, sz, ctypes.POINTER(ctypes.c_int)]
         _h = L
     return _h
+
+
+def extra_lib():
+    """libhydra_host_extra.so: AllreduceHalvingDoubling / old-style AllreduceBcube /
+    AllreduceLocal and their Hip* twins -- only the `extra` tests use it."""
+    global _x
+    if _x is None:
+        lib()
+        if not os.path.exists(EXTRA_LIB_PATH):
+            raise _lib.HydraError(-1, f"{EXTRA_LIB_PATH} is not built")
+        L = ctypes.CDLL(EXTRA_LIB_PATH)
+        vp, sz, i = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
+        old = [i, i, i, sz, vp, i, vp, ctypes.c_char_p, sz]
+        hip = [i, i, i, sz, vp, i, i, ctypes.c_char_p, sz]
+        for nm in ("halving_doubling", "bcube_old", "local"):
+            getattr(L, f"hydra_host_allreduce_{nm}_threads").argtypes = old
+        for nm in ("halving_doubling", "local", "bcube"):
+            getattr(L, f"hydra_host_hip_{nm}_threads").argtypes = hip
+        _x = L
+    return _x
 
 
 def _ptrs(arrs):
@@ -160,11 +173,11 @@ def allreduce_ring_old_threads(bufs, dtype_code=None, reducer_fn=None, chunked=F
     f = (lib().hydra_host_allreduce_ring_chunked_threads if chunked
          else lib().hydra_host_allreduce_ring_old_threads)
     if halving_doubling:
-        f = lib().hydra_host_allreduce_halving_doubling_threads
+        f = extra_lib().hydra_host_allreduce_halving_doubling_threads
     if bcube:
-        f = lib().hydra_host_allreduce_bcube_old_threads
+        f = extra_lib().hydra_host_allreduce_bcube_old_threads
     if local:
-        f = lib().hydra_host_allreduce_local_threads
+        f = extra_lib().hydra_host_allreduce_local_threads
     rc = f(
         P, nptr, code, n, ctypes.cast(_ptrs([b for r in bufs for b in r]), ctypes.c_void_p), red,
         fp, err, 512)
@@ -206,11 +219,11 @@ def hip_ring_threads(tensors, workspace: str = "host", user_streams: bool = Fals
     fn = (lib().hydra_host_hip_ring_chunked_threads if chunked
           else lib().hydra_host_hip_ring_threads)
     if halving_doubling:
-        fn = lib().hydra_host_hip_halving_doubling_threads
+        fn = extra_lib().hydra_host_hip_halving_doubling_threads
     if local:  # HipAllreduceLocal<T> (gloo::CudaAllreduceLocal)
-        fn = lib().hydra_host_hip_local_threads
+        fn = extra_lib().hydra_host_hip_local_threads
     if bcube:  # HipAllreduceBcube<T, W> (gloo::CudaAllreduceBcube)
-        fn = lib().hydra_host_hip_bcube_threads
+        fn = extra_lib().hydra_host_hip_bcube_threads
     rc = fn(
         P, nptr, code, n, ctypes.cast(_ptrs_int([t.data_ptr() for r in tensors for t in r]),
                                       ctypes.c_void_p), ws, int(user_streams), err, 512)

@@ -145,6 +145,13 @@ class XgmiComm:
         self._h = h
         self.rank, self.world = rank, world
 
+    def info(self) -> dict:
+        """What RCCL itself reports: ncclCommCount / ncclCommUserRank / ncclCommCuDevice."""
+        cnt, r, d = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        check(_lib.lib().hydra_comm_info(self._h, ctypes.byref(cnt), ctypes.byref(r),
+                                         ctypes.byref(d)))
+        return {"nccl_comm_count": cnt.value, "nccl_user_rank": r.value, "nccl_device": d.value}
+
     def allreduce_(self, t, algo: str = "auto", op: str = "sum", dtype_code: int | None = None,
                    flags: int = 0, max_segment: int = 0, chunk_bytes: int = 0,
                    stream: int | None = None) -> None:
@@ -373,7 +380,7 @@ def expected_bcube_f32(xs: list[np.ndarray]) -> np.ndarray:
     return out
 
 
-def bench_allreduce(args, dev, make_comm=None, sync=None) -> dict:
+def bench_allreduce(args, dev, make_comm=None, sync=None, cpu_baseline=None) -> dict:
     """bench.py --gpus N (N > 1): BASELINE config 4 (fp32 64 Mi per rank) on this rank.
 
     make_comm() -> a communicator with XgmiComm's allreduce_ / reduce_ / apipe_allreduce_ /
@@ -404,6 +411,22 @@ def bench_allreduce(args, dev, make_comm=None, sync=None) -> dict:
             torch.cuda.synchronize(dev)
     comm = make_comm()
     rail2 = make_comm()  # apipe's 2nd rail
+    # what RCCL itself reports for the communicator (ncclCommCount / UserRank / CuDevice): the
+    # line shows that RCCL saw N ranks, and that every rank agrees
+    try:
+        info = comm.info()
+    except HydraError as e:
+        info = {"error": str(e)}
+    cnt = float(info.get("nccl_comm_count", -1))
+    comm_seen = {"nccl_comm_count": int(cnt),
+                 "min_over_ranks": int(-max_over_ranks(-cnt, dev)),
+                 "max_over_ranks": int(max_over_ranks(cnt, dev)),
+                 "user_rank": info.get("nccl_user_rank"), "device": info.get("nccl_device"),
+                 "backend": info.get("backend", "rccl")}
+    if "error" in info:
+        comm_seen["error"] = info["error"]
+    extra_legs = bool(getattr(args, "extra_legs", False))
+    cpu_base = None
     from .peer import PeerComm
 
     pg = {"peer": None, "err": None}  # IPC-mapped buckets, one kernel per allreduce
@@ -507,7 +530,7 @@ def bench_allreduce(args, dev, make_comm=None, sync=None) -> dict:
             ms_safe, lat_safe = measure("direct", 0)
             state["result"] = lambda: _bench_result(
                 n, world, args, "direct", 0, dict(tuning), parity, full_ok, ms_safe, lat_safe,
-                {}, None)
+                {}, None, comm_seen)
         # 3) pick the algorithm: "auto" = the fastest bit-exact schedule on this node
         #    (DIRECT / A2A / RING / PEER two-shot), chosen on a few untimed steps
         chosen, chunk = algo, 0
@@ -546,7 +569,17 @@ def bench_allreduce(args, dev, make_comm=None, sync=None) -> dict:
 
         def _result(ms_, lat_, others_, c5_):
             return _bench_result(n, world, args, chosen, chunk, tuning, parity, full_ok, ms_,
-                                 lat_, dict(others_), c5_)
+                                 lat_, dict(others_), c5_, comm_seen, cpu_base)
+
+        # the reference's own ring on this host's cores (bench.py's baseline leg: rank 0 only,
+        # outside every timed region; the other ranks wait at the barrier)
+        if cpu_baseline is not None:
+            if rank == 0:
+                try:
+                    cpu_base = cpu_baseline(world, n)
+                except Exception as e:  # a reported baseline, never the product
+                    cpu_base = {"value": None, "error": str(e)}
+            dist.barrier()
 
         state["result"] = lambda: _result(ms, lat_ms, others, c5)
         stall = float(os.environ.get("HYDRA_BENCH_STALL_CONTEXT", "0"))
@@ -607,17 +640,23 @@ def bench_allreduce(args, dev, make_comm=None, sync=None) -> dict:
             parity[name] = ("bit-exact" if max_over_ranks(0.0 if ok else 1.0, dev) == 0.0
                             else "MISMATCH")
 
-        check_parity("ring_old", lambda t: comm.allreduce_(t, algo="ring_old"),
-                     expected_old_ring_f32(xs, rank))
-        check_parity("ring_chunked", lambda t: comm.allreduce_(t, algo="ring_chunked"),
-                     expected_chunked_ring_f32(xs))
-        check_parity("bcube", lambda t: comm.allreduce_(t, algo="bcube"), expected_bcube_f32(xs))
-        # gloo::reduce to the last rank (hydra_reduce_root): only the root's bucket is defined
-        check_parity("reduce_root", lambda t: comm.reduce_(t, world - 1),
-                     expected_reduce_f32(xs) if rank == world - 1 else None)
+        # --extra-legs: the schedules outside north_star's path (old-style rings, BCUBE,
+        # halving-doubling, gloo::reduce to a root) -- parity and timings; off by default
+        if extra_legs:
+            check_parity("ring_old", lambda t: comm.allreduce_(t, algo="ring_old"),
+                         expected_old_ring_f32(xs, rank))
+            check_parity("ring_chunked", lambda t: comm.allreduce_(t, algo="ring_chunked"),
+                         expected_chunked_ring_f32(xs))
+            check_parity("bcube", lambda t: comm.allreduce_(t, algo="bcube"),
+                         expected_bcube_f32(xs))
+            # gloo::reduce to the last rank (hydra_reduce_root): only the root's bucket is defined
+            check_parity("reduce_root", lambda t: comm.reduce_(t, world - 1),
+                         expected_reduce_f32(xs) if rank == world - 1 else None)
         k = max(5, args.steps // 4)
-        for a in ("ring", "direct", "a2a", "rccl", "ring_old", "ring_chunked", "bcube",
-                  "halving_doubling") + peer_algos:
+        legs = ("ring", "direct", "a2a", "rccl") + peer_algos
+        if extra_legs:
+            legs += ("ring_old", "ring_chunked", "bcube", "halving_doubling")
+        for a in legs:
             if a == chosen:
                 continue
 
@@ -626,11 +665,12 @@ def bench_allreduce(args, dev, make_comm=None, sync=None) -> dict:
 
             others[a] = context_leg(ostep, k)
 
-        def rstep():
-            comm.reduce_(x, 0)
+        if extra_legs:
+            def rstep():
+                comm.reduce_(x, 0)
 
-        # gloo::reduce of the same bucket to rank 0 (context: no all-gather half)
-        others["reduce_root0"] = context_leg(rstep, k)
+            # gloo::reduce of the same bucket to rank 0 (context: no all-gather half)
+            others["reduce_root0"] = context_leg(rstep, k)
 
         # 5) BASELINE config 5: bf16 bucket of 256 Mi elements, fp32 accumulation
         if not getattr(args, "no_config5", False):
@@ -721,7 +761,7 @@ def bench_allreduce(args, dev, make_comm=None, sync=None) -> dict:
 
 
 def _bench_result(n, world, args, chosen, chunk, tuning, parity, full_ok, ms, lat_ms, others,
-                  c5) -> dict:
+                  c5, comm_seen=None, cpu_base=None) -> dict:
     """The N>1 bench JSON line (bench_allreduce; also printed by its watchdog once the headline
     is measured)."""
     bucket = 4.0 * n
@@ -760,4 +800,6 @@ def _bench_result(n, world, args, chosen, chunk, tuning, parity, full_ok, ms, la
                                    if isinstance(v, float) and a != "reduce_root0"},
         "config5_bf16": c5,
         "parity": {"fold_order_1M": parity, "full_size_exact": full_ok},
+        "rccl_comm": comm_seen,
+        "cpu_baseline": cpu_base,
     }

@@ -13,11 +13,20 @@
 //   gloo::CudaReductionFunction<T> device fn  void(T*, const T*, size_t, stream) (cuda.h:286-350)
 //     -> hydra::gloo_compat::deviceSumInPlace<T>
 //
-// Errors: a non-zero hydra status throws hydra::gloo_compat::EnforceNotMet carrying
-// hydra_last_error(), like GLOO_ENFORCE -> gloo::EnforceNotMet (gloo/gloo/common/logging.h:21,42).
+// Errors: a non-zero hydra status is handed to an error policy, a template parameter of every
+// shim (`Errors`, default HYDRA_GLOO_ERRORS):
+//   HYDRA_ERR_TIMEOUT           -> Errors::io_failed      (gloo: IoException, common/error.h:45,
+//                                                           as tcp/unbound_buffer.cc:80-84 throws)
+//   any other non-zero status   -> Errors::enforce_failed (gloo: EnforceNotMet, as GLOO_ENFORCE,
+//                                                           common/logging.h:21,42)
+// DefaultErrors throws this header's own EnforceNotMet / IoException (no Gloo headers needed).
+// A caller built against Gloo includes include/hydra/gloo_errors.h INSTEAD: it makes
+// GlooErrors -- gloo::EnforceNotMet and gloo::IoException themselves -- the default, so a
+// reference caller's existing `catch (const gloo::EnforceNotMet&)` sees the shim's failures.
 // Threading: staging contexts come from a process-wide pool (one per concurrent caller), so the
 // two rails of bew_allreduce_a (pipeallreduce-a.cc:32-50) reduce concurrently without sharing.
 #pragma once
+#define HYDRA_GLOO_REDUCE_H_INCLUDED 1
 
 #include <cstddef>
 #include <cstdint>
@@ -45,8 +54,39 @@ class EnforceNotMet : public std::runtime_error {
   int code_;
 };
 
-inline void enforce(int rc) {
-  if (rc != HYDRA_OK) throw EnforceNotMet(rc, hydra_last_error());
+class IoException : public std::runtime_error {
+ public:
+  IoException(int code, const std::string& what)
+      : std::runtime_error("[hydra_hip] " + what), code_(code) {}
+  int code() const { return code_; }
+
+ private:
+  int code_;
+};
+
+// The error policy's shape: [[noreturn]] static hooks taking the status, hydra_last_error() and
+// the failing call's text.
+struct DefaultErrors {
+  [[noreturn]] static void enforce_failed(int code, const std::string& msg, const char* call) {
+    (void)call;
+    throw EnforceNotMet(code, msg);
+  }
+  [[noreturn]] static void io_failed(int code, const std::string& msg, const char* call) {
+    (void)call;
+    throw IoException(code, msg);
+  }
+};
+
+#ifndef HYDRA_GLOO_ERRORS
+#define HYDRA_GLOO_ERRORS ::hydra::gloo_compat::DefaultErrors
+#endif
+
+template <typename Errors = HYDRA_GLOO_ERRORS>
+inline void enforce(int rc, const char* call = "hydra_hip call") {
+  if (rc == HYDRA_OK) return;
+  const std::string msg = hydra_last_error();
+  if (rc == HYDRA_ERR_TIMEOUT) Errors::io_failed(rc, msg, call);
+  Errors::enforce_failed(rc, msg, call);
 }
 
 // dtype tag of a C++ element type (gloo::float16 is a 2-byte struct: pass HYDRA_FLOAT16 via
@@ -99,6 +139,7 @@ class ContextPool {
     if (!p) p = new ContextPool(device);
     return *p;
   }
+  template <typename Errors = HYDRA_GLOO_ERRORS>
   Lease acquire() {
     {
       std::lock_guard<std::mutex> g(mu_);
@@ -109,7 +150,7 @@ class ContextPool {
       }
     }
     hydra_ctx_t c = nullptr;
-    enforce(hydra_ctx_create(device_, &c));
+    enforce<Errors>(hydra_ctx_create(device_, &c), "hydra_ctx_create");
     return Lease(this, c);
   }
  private:
@@ -134,69 +175,73 @@ inline void pinnedFree(void* p) { hydra_free_host(p); }
 using Func = std::function<void(void*, const void*, const void*, size_t)>;
 
 // --- AllreduceOptions::Func ------------------------------------------------------------------
-inline Func hostReduce(int op, int dtype, int device = 0) {
+template <typename Errors = HYDRA_GLOO_ERRORS>
+Func hostReduce(int op, int dtype, int device = 0) {
   return [op, dtype, device](void* c, const void* a, const void* b, size_t n) {
-    auto lease = ContextPool::instance(device).acquire();
-    enforce(hydra_reduce_host(lease.get(), op, dtype, c, a, b, n));
+    auto lease = ContextPool::instance(device).acquire<Errors>();
+    enforce<Errors>(hydra_reduce_host(lease.get(), op, dtype, c, a, b, n), "hydra_reduce_host");
   };
 }
 
-template <typename T>
+template <typename T, typename Errors = HYDRA_GLOO_ERRORS>
 Func hostSum(int device = 0) {
-  return hostReduce(HYDRA_SUM, dtype_of<T>(), device);
+  return hostReduce<Errors>(HYDRA_SUM, dtype_of<T>(), device);
 }
 
-inline Func deviceReduce(int op, int dtype, hydra_stream_t stream = nullptr) {
+template <typename Errors = HYDRA_GLOO_ERRORS>
+Func deviceReduce(int op, int dtype, hydra_stream_t stream = nullptr) {
   return [op, dtype, stream](void* c, const void* a, const void* b, size_t n) {
-    enforce(hydra_reduce(op, dtype, c, a, b, n, stream));
+    enforce<Errors>(hydra_reduce(op, dtype, c, a, b, n, stream), "hydra_reduce");
   };
 }
 
-template <typename T>
+template <typename T, typename Errors = HYDRA_GLOO_ERRORS>
 Func deviceSum(hydra_stream_t stream = nullptr) {
-  return deviceReduce(HYDRA_SUM, dtype_of<T>(), stream);
+  return deviceReduce<Errors>(HYDRA_SUM, dtype_of<T>(), stream);
 }
 
 // --- ReductionFunction<T>::Function (x = op(x, y)) ---------------------------------------------
-template <typename T>
+template <typename T, typename Errors = HYDRA_GLOO_ERRORS>
 void hostSumInPlace(T* x, const T* y, size_t n) {
-  auto lease = ContextPool::instance().acquire();
-  enforce(hydra_reduce_host(lease.get(), HYDRA_SUM, dtype_of<T>(), x, x, y, n));
+  auto lease = ContextPool::instance().acquire<Errors>();
+  enforce<Errors>(hydra_reduce_host(lease.get(), HYDRA_SUM, dtype_of<T>(), x, x, y, n),
+                  "hydra_reduce_host");
 }
 
 // Explicit-dtype form for element types that are not C++ arithmetic types: gloo::float16 (a
 // 2-byte struct, HYDRA_FLOAT16, with its store quirk) or a bf16 struct (HYDRA_BFLOAT16).
-template <typename T, int DTYPE>
+template <typename T, int DTYPE, typename Errors = HYDRA_GLOO_ERRORS>
 void hostSumInPlaceAs(T* x, const T* y, size_t n) {
   static_assert(DTYPE == HYDRA_FLOAT16 || DTYPE == HYDRA_BFLOAT16 || sizeof(T) != 2,
                 "2-byte element types need HYDRA_FLOAT16 or HYDRA_BFLOAT16");
-  auto lease = ContextPool::instance().acquire();
-  enforce(hydra_reduce_host(lease.get(), HYDRA_SUM, DTYPE, x, x, y, n));
+  auto lease = ContextPool::instance().acquire<Errors>();
+  enforce<Errors>(hydra_reduce_host(lease.get(), HYDRA_SUM, DTYPE, x, x, y, n),
+                  "hydra_reduce_host");
 }
 
 // --- an old-style ReductionFunction<T> whose fn is the GPU sum ------------------------------
 // Works for gloo::ReductionFunction<T> (algorithm.h:59-96) and hydra::ReductionFunction<T>
 // (include/hydra/allreduce.h):  gpuReductionFunction<gloo::ReductionFunction<float>, float>(
 // gloo::SUM)  ->  a pointer usable wherever ReductionFunction<float>::sum is.
-template <typename RF, typename T, typename Enum>
+template <typename RF, typename T, typename Errors = HYDRA_GLOO_ERRORS, typename Enum>
 const RF* gpuReductionFunction(Enum sum) {
-  static const RF fn(sum, &hostSumInPlace<T>);
+  static const RF fn(sum, &hostSumInPlace<T, Errors>);
   return &fn;
 }
 
 // the same for explicit-dtype element types, e.g.
 //   gpuReductionFunctionAs<gloo::ReductionFunction<gloo::float16>, gloo::float16, HYDRA_FLOAT16>(
 //       gloo::SUM)
-template <typename RF, typename T, int DTYPE, typename Enum>
+template <typename RF, typename T, int DTYPE, typename Errors = HYDRA_GLOO_ERRORS, typename Enum>
 const RF* gpuReductionFunctionAs(Enum sum) {
-  static const RF fn(sum, &hostSumInPlaceAs<T, DTYPE>);
+  static const RF fn(sum, &hostSumInPlaceAs<T, DTYPE, Errors>);
   return &fn;
 }
 
 // --- CudaReductionFunction<T> device function shape (x = op(x, y) on a stream) ---------------
-template <typename T>
+template <typename T, typename Errors = HYDRA_GLOO_ERRORS>
 void deviceSumInPlace(T* x, const T* y, size_t n, hydra_stream_t stream) {
-  enforce(hydra_reduce(HYDRA_SUM, dtype_of<T>(), x, x, y, n, stream));
+  enforce<Errors>(hydra_reduce(HYDRA_SUM, dtype_of<T>(), x, x, y, n, stream), "hydra_reduce");
 }
 
 }  // namespace gloo_compat

@@ -136,13 +136,40 @@ int hydra_reduce_host(hydra_ctx_t ctx, int op, int dtype, void* c, const void* a
                       size_t n);
 int hydra_chunk_sum_host(hydra_ctx_t ctx, int dtype, void* c, const void* a, const void* b,
                          size_t n);
-/* Page-lock caller memory: hydra_reduce_host then reads / writes it in place over PCIe
- * (optional).  Reference-counted per start address: every hydra_host_register needs one
- * hydra_host_unregister, and a second register of the same address may not cover more bytes.
- * A range its owner registered directly (hipHostRegister) is used as it is and never released
- * here; unregistering an address not registered here is a no-op. */
+/* Which host memory the kernel reads / writes in place (zero-copy over PCIe), per operand:
+ *   - a range registered with hydra_host_register, a pinned block from hydra_malloc_host, or
+ *     memory the caller pinned / registered itself (hipHostMalloc, hipHostRegister, torch pinned
+ *     tensors; the caller keeps it so for the call, as for any copy from it);
+ *   - a pageable operand: the WHOLE PAGES inside it, pinned for the call and released before it
+ *     returns (hydra_set_variant(1001) turns this off).
+ * Everything else -- in particular the ragged first and last page of a pageable operand, which
+ * hold memory outside it -- is staged through device buffers in copies of at most 1 MiB (the HIP
+ * runtime's own staging; larger pageable copies would make the runtime lock the caller's pages,
+ * page-rounded).  hydra never registers or locks a page that holds memory outside the operand
+ * it was given, and its registrations never overlap one another. */
+/* Page-lock caller memory for zero-copy use (optional): registers the whole pages inside
+ * [ptr, ptr + bytes) (the ragged edges stay staged).  Reference-counted per start address: every
+ * hydra_host_register needs one hydra_host_unregister, and a second register of the same address
+ * may not cover more bytes.  Pages already mapped by their owner (hipHostRegister /
+ * hipHostMalloc) are used as they are and never released here; pages another hydra registration
+ * holds are shared with it; unregistering an address not registered here is a no-op.  The pages
+ * stay registered until the last unregister AND the last in-flight call using them are done. */
 int hydra_host_register(void* ptr, size_t bytes);
 int hydra_host_unregister(void* ptr);
+/* Inspection (tests): the whole pages inside [ptr, ptr + bytes), [*lo, *hi) (empty: equal). */
+void hydra_page_interior(uint64_t ptr, size_t bytes, uint64_t* lo, uint64_t* hi);
+/* Inspection (tests): hydra's live host mappings (registrations, per-call pins, pinned blocks),
+ * how many hipHostRegister calls hydra has made, and how many of those covered a byte outside
+ * the caller range they were made for (0 by construction). */
+typedef struct {
+  uint64_t lo, hi;  /* mapped host range */
+  int32_t kind;     /* 1 hydra_host_register, 2 per-call pin, 3 pinned block */
+  int32_t owners;   /* hydra_host_register owners */
+  int32_t users;    /* in-flight calls using it */
+  uint64_t owner_lo, owner_hi; /* the caller range it was made for */
+} hydra_host_mapping_t;
+int hydra_host_mappings(hydra_host_mapping_t* out, size_t cap, size_t* count,
+                        uint64_t* registrations, uint64_t* outside);
 
 /* ---- streams / memory helpers for C callers (the Python layer uses torch instead) -------- */
 /* Streams, events, device blocks and pinned blocks come from process-wide caches, like torch's
@@ -160,7 +187,8 @@ int hydra_stream_synchronize(hydra_stream_t s);
 /* Events (hipEvent_t, timing disabled): completion markers an owner records on a caller's
  * stream, so it can later wait for ITS work without touching a stream it does not own. */
 typedef void* hydra_event_t;
-int hydra_event_create(hydra_event_t* out);
+int hydra_event_create(hydra_event_t* out);                 /* on the caller's current device */
+int hydra_event_create_on(int device, hydra_event_t* out);  /* on `device` (-1: current) */
 int hydra_event_record(hydra_event_t e, hydra_stream_t s);
 int hydra_event_synchronize(hydra_event_t e);
 int hydra_event_destroy(hydra_event_t e);
@@ -236,6 +264,9 @@ typedef struct {
 int hydra_comm_get_unique_id(void* id /* HYDRA_UNIQUE_ID_BYTES */);
 int hydra_comm_init(hydra_comm_t* out, int nranks, int rank, const void* id, int device);
 int hydra_comm_destroy(hydra_comm_t comm);
+/* What RCCL itself reports for the communicator: ncclCommCount, ncclCommUserRank and
+ * ncclCommCuDevice (the bench line records them, so a multi-GPU line shows RCCL saw N ranks). */
+int hydra_comm_info(hydra_comm_t comm, int* nranks, int* rank, int* device);
 int hydra_allreduce(hydra_comm_t comm, int algo, int op, int dtype, int flags, void* buf,
                     size_t n, size_t max_segment, size_t chunk_bytes, hydra_stream_t stream);
 

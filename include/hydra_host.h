@@ -78,44 +78,10 @@ int hydra_host_hip_ring_chunked_threads(int P, int nptr, int dtype, size_t n, vo
                                         int workspace, int user_streams, char* err,
                                         size_t errlen);
 
-/* hydra::HipAllreduceHalvingDoubling<T, W> (gloo::CudaAllreduceHalvingDoubling<T, W>,
- * cuda_allreduce_halving_doubling.cc), same arguments as hydra_host_hip_ring_threads. */
-int hydra_host_hip_halving_doubling_threads(int P, int nptr, int dtype, size_t n,
-                                            void** dev_bufs, int workspace, int user_streams,
-                                            char* err, size_t errlen);
-
 /* gloo::AllreduceRingChunked<T>::run() (allreduce_ring_chunked.h:20-248), same arguments. */
 int hydra_host_allreduce_ring_chunked_threads(int P, int nptr, int dtype, size_t n, void** bufs,
                                               int reducer, hydra_inplace_fn fn, char* err,
                                               size_t errlen);
-
-/* gloo::AllreduceHalvingDoubling<T>::run() (allreduce_halving_doubling.h:37-358), same
- * arguments as hydra_host_allreduce_ring_old_threads. */
-int hydra_host_allreduce_halving_doubling_threads(int P, int nptr, int dtype, size_t n,
-                                                  void** bufs, int reducer, hydra_inplace_fn fn,
-                                                  char* err, size_t errlen);
-
-/* Old-style gloo::AllreduceBcube<T>::run() (allreduce_bcube.h:255-691, base 2; P must be a
- * power of two), same arguments as hydra_host_allreduce_ring_old_threads. */
-int hydra_host_allreduce_bcube_old_threads(int P, int nptr, int dtype, size_t n, void** bufs,
-                                           int reducer, hydra_inplace_fn fn, char* err,
-                                           size_t errlen);
-
-/* gloo::AllreduceLocal<T>::run() (allreduce_local.cc:28-38): each rank's pointers only, same
- * arguments as hydra_host_allreduce_ring_old_threads. */
-int hydra_host_allreduce_local_threads(int P, int nptr, int dtype, size_t n, void** bufs,
-                                       int reducer, hydra_inplace_fn fn, char* err,
-                                       size_t errlen);
-
-/* hydra::HipAllreduceLocal<T> (gloo::CudaAllreduceLocal<T>, cuda_allreduce_local.cc), same
- * arguments as hydra_host_hip_ring_threads (workspace unused). */
-int hydra_host_hip_local_threads(int P, int nptr, int dtype, size_t n, void** dev_bufs,
-                                 int workspace, int user_streams, char* err, size_t errlen);
-
-/* hydra::HipAllreduceBcube<T, W> (gloo::CudaAllreduceBcube<T, W>, cuda_allreduce_bcube.cc; P a
- * power of two), same arguments as hydra_host_hip_ring_threads. */
-int hydra_host_hip_bcube_threads(int P, int nptr, int dtype, size_t n, void** dev_bufs,
-                                 int workspace, int user_streams, char* err, size_t errlen);
 
 /* gloo::reduce (reduce.cc:21-262) to `root` on P thread-ranks.  in/out: P pointers each
  * (in == NULL: in place on out, reduce_test.cc:27-33).  Every rank's out is left as the

@@ -21,7 +21,7 @@
 //
 // usage: dropin_gloo <mode> <P> <n> <f32|i32|f16> [timed_iters] [max_segment]
 //   mode: new_ring | new_ring2 (2 pointers per rank) | new_reduce (root P-1) | old_ring |
-//         old_ring_chunked
+//         old_ring_chunked | errors (the shim's failures as the reference's exception types)
 // prints one JSON object on stdout; exit 0 iff both runs finished (equality is in the JSON).
 
 #include <algorithm>
@@ -50,7 +50,8 @@
 #include "gloo/transport/tcp/device.h"
 #include "gloo/types.h"
 
-#include "hydra/gloo_reduce.h"
+// the shim with Gloo's own exception types (gloo::EnforceNotMet / gloo::IoException)
+#include "hydra/gloo_errors.h"
 
 namespace {
 
@@ -288,9 +289,83 @@ int run_all(const std::string& mode, int P, size_t n, int iters, size_t ms, cons
   return 0;
 }
 
+// mode "errors": the shim's failures reach a reference caller as the reference's own types.
+//  (1) an invalid call inside the reference's gloo::allreduce: one process (the P = 1
+//      short-circuit, allreduce.cc:129-133) with two outputs, so allreduce runs the local reduce
+//      (genLocalReduceFunction, :46-83) through the hydra Func -- with an element type code the
+//      library rejects.  The failure must leave gloo::allreduce as gloo::EnforceNotMet
+//      (common/logging.h:21,42), caught where a reference caller catches GLOO_ENFORCE failures.
+//      (With P > 1 the ring would unwind with its scratch receive still posted, allreduce.cc:
+//      225-300 -- the reference's own timeout tests leave the process after that, too.)
+//  (2) the timeout status (HYDRA_ERR_TIMEOUT, e.g. hydra_comm_wait) through the same policy:
+//      gloo::IoException (common/error.h:45), what tcp/unbound_buffer.cc:80-84 throws.
+int run_errors(size_t n) {
+  auto caught = [](const std::function<void()>& f, std::string* msg) -> std::string {
+    try {
+      f();
+    } catch (const gloo::EnforceNotMet& e) {
+      *msg = e.what();
+      return "gloo::EnforceNotMet";
+    } catch (const gloo::IoException& e) {
+      *msg = e.what();
+      return "gloo::IoException";
+    } catch (const std::exception& e) {
+      *msg = e.what();
+      return "other";
+    }
+    return "none";
+  };
+  gloo::rendezvous::HashStore store;
+  gloo::transport::tcp::attr attr;
+  attr.hostname = "127.0.0.1";
+  auto dev = gloo::transport::tcp::CreateDevice(attr);
+  auto ctx = std::make_shared<gloo::rendezvous::Context>(0, 1);
+  ctx->connectFullMesh(store, dev);
+  std::vector<float> x(n, 1.0f), x2(n, 2.0f);
+  std::string m1, m2, m3;
+  const std::string t1 = caught(
+      [&]() {
+        gloo::AllreduceOptions o(ctx);
+        o.setOutputs(std::vector<float*>{x.data(), x2.data()}, n);
+        o.setReduceFunction(hydra::gloo_compat::hostReduce(HYDRA_SUM, 42 /* no such dtype */));
+        gloo::allreduce(o);
+      },
+      &m1);
+  // the same allreduce with a valid Func still runs afterwards (nothing left half-done)
+  const std::string t2 = caught(
+      [&]() {
+        gloo::AllreduceOptions o(ctx);
+        o.setOutputs(std::vector<float*>{x.data(), x2.data()}, n);
+        o.setReduceFunction(hydra_func<float>());
+        gloo::allreduce(o);
+      },
+      &m2);
+  const bool sum_ok = x[0] == 3.0f && x[n - 1] == 3.0f && x2[n - 1] == 3.0f;
+  const std::string t3 = caught(
+      [&]() { hydra::gloo_compat::enforce(HYDRA_ERR_TIMEOUT, "hydra_comm_wait"); }, &m3);
+  auto esc = [](std::string v) {
+    std::string o;
+    for (char ch : v) {
+      if (ch == '"' || ch == '\\') o += '\\';
+      if (ch == '\n') ch = ' ';
+      o += ch;
+    }
+    return o;
+  };
+  std::printf(
+      "{\"mode\": \"errors\", \"invalid_call\": \"%s\", \"invalid_msg\": \"%s\", "
+      "\"valid_after\": \"%s\", \"valid_msg\": \"%s\", \"valid_sum_ok\": %s, "
+      "\"timeout_status\": \"%s\", \"timeout_msg\": \"%s\"}\n",
+      t1.c_str(), esc(m1).c_str(), t2.c_str(), esc(m2).c_str(), sum_ok ? "true" : "false",
+      t3.c_str(), esc(m3).c_str());
+  return 0;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
+  if (argc >= 2 && std::string(argv[1]) == "errors")
+    return run_errors(argc > 3 ? std::strtoull(argv[3], nullptr, 10) : 1000);
   if (argc < 5) {
     std::fprintf(stderr, "usage: %s <new_ring|old_ring> <P> <n> <f32|i32> [iters] [max_segment]\n",
                  argv[0]);

@@ -13,6 +13,7 @@
 #include <vector>
 
 #include "hydra/allreduce.h"
+#include "hydra/allreduce_extra.h"  // the opt-in classes are race-checked too
 
 static void sum_u64(void* c, const void* a, const void* b, size_t n) {
   for (size_t i = 0; i < n; i++)

@@ -177,6 +177,13 @@ class GlooPlanComm:
         if e1 < flat.numel():
             rail2.allreduce_(flat[e1:], **kw)
 
+    def info(self):
+        """XgmiComm.info's shape (no RCCL here: the process group's own size and rank)."""
+        import torch.distributed as dist
+
+        return {"nccl_comm_count": dist.get_world_size(), "nccl_user_rank": dist.get_rank(),
+                "nccl_device": -1, "backend": "gloo (test executor)"}
+
     def wait(self, timeout_ms, stream=None):
         """XgmiComm.wait: the executor is synchronous, so there is never anything pending."""
 

@@ -25,7 +25,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q, stall_rank=-1, stall_waits=0):
+def _worker(rank, world, port, q, stall_rank=-1, stall_waits=0, extra_legs=False):
     import sys
 
     sys.path.insert(0, ROOT)
@@ -35,6 +35,7 @@ def _worker(rank, world, port, q, stall_rank=-1, stall_waits=0):
     import torch
     import torch.distributed as dist
 
+    import bench
     from gloo_plan_exec import GlooPlanComm
     from hydra_amd import ring
     from oracle import oracle as O
@@ -61,9 +62,10 @@ def _worker(rank, world, port, q, stall_rank=-1, stall_waits=0):
     try:
         args = argparse.Namespace(elements=1 << 16, steps=3, warmup=1, algo="auto",
                                   watchdog_s=600.0, no_config5=False, config5_elements=1 << 20,
-                                  peer=False)
+                                  peer=False, extra_legs=extra_legs)
+        base = ((lambda P, n: bench.ring_cpu_baseline(P, n, 0.5)) if O.ref_available() else None)
         res = ring.bench_allreduce(args, torch.device("cpu"), make_comm=make_comm,
-                                   sync=lambda: None)
+                                   sync=lambda: None, cpu_baseline=base)
         q.put((rank, res, all(c.closed for c in comms) and len(comms) == 2))
     except Exception as e:  # report instead of hanging the parent
         import traceback
@@ -73,12 +75,13 @@ def _worker(rank, world, port, q, stall_rank=-1, stall_waits=0):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3, 4, 8])
-def test_bench_allreduce_orchestration(world):
+def _start(world, stall_rank=-1, stall_waits=0, extra_legs=False):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, stall_rank, stall_waits,
+                                               extra_legs))
+             for r in range(world)]
     for p in procs:
         p.start()
     try:
@@ -91,51 +94,67 @@ def test_bench_allreduce_orchestration(world):
             p.join(timeout=30)
             if p.is_alive():
                 p.kill()
+    return out
+
+
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
+def test_bench_allreduce_orchestration(world):
+    """The default line: north_star's schedules only (DIRECT / A2A / RING / RCCL, config 5, the
+    two rails), the communicator's own rank count, and the reference ring's CPU baseline."""
+    from oracle import oracle as O
+
+    out = _start(world)
     for r, (res, closed) in out.items():
         assert isinstance(res, dict), res
         assert closed, f"rank {r} left a communicator open"
     res = out[0][0]
     assert res["n_gpus"] == world and res["scaling"] == "weak" and res["value"] > 0
     par = res["parity"]["fold_order_1M"]
-    for a in ("direct", "ring", "ring_old", "ring_chunked", "bcube", "reduce_root", "apipe"):
+    for a in ("direct", "ring", "apipe"):
         assert par[a] == "bit-exact", (a, par)
+    # no leg outside north_star by default
+    assert not set(par) & {"ring_old", "ring_chunked", "bcube", "reduce_root"}, par
+    assert not set(res["other_algos_ms"]) & {"ring_old", "ring_chunked", "bcube",
+                                             "halving_doubling", "reduce_root0"}, res
     # A2A needs P equal reference blocks: 1 Mi fp32 has them at P = 2, 4 and 8, not at P = 3
     assert (par["a2a"] == "bit-exact" if world != 3 else par["a2a"].startswith("n/a")), par
     assert all(res["parity"]["full_size_exact"].values()), res["parity"]
     assert res["config"]["algo"] in ("direct", "a2a", "ring")
     assert res["config"]["autotune_ms"], res["config"]
-    for a in ("ring", "direct", "rccl", "ring_old", "ring_chunked", "bcube", "halving_doubling",
-              "reduce_root0", "apipe_direct"):
+    for a in ("ring", "direct", "rccl", "apipe_direct"):
         if a != res["config"]["algo"]:
             assert isinstance(res["other_algos_ms"][a], float), (a, res["other_algos_ms"])
     c5 = res["config5_bf16"]  # config 5's leg (bf16, fp32 accumulate) ran, at 1 Mi here
     assert "error" not in c5 and c5["elements"] == 1 << 20 and c5["ms"] > 0, c5
     assert res["parity"]["full_size_exact"]["config5_bf16_acc32"] is True, res["parity"]
+    # the communicator's own rank count, the same on every rank
+    rc = res["rccl_comm"]
+    assert rc["nccl_comm_count"] == rc["min_over_ranks"] == rc["max_over_ranks"] == world, rc
+    # the reference ring on P thread-ranks beside the line (rank 0 only)
+    cb = res["cpu_baseline"]
+    if O.ref_available():
+        assert cb["kind"] == "reference" and cb["value"] > 0 and cb["cores"] == 2 * world, cb
     # every rank reports the same (max-over-ranks) timing
     assert all(out[r][0]["ms_per_step"] == res["ms_per_step"] for r in out)
 
 
+def test_bench_allreduce_extra_legs():
+    """--extra-legs adds the schedules outside north_star's path, each bit-exact."""
+    out = _start(3, extra_legs=True)
+    res = out[0][0]
+    assert isinstance(res, dict), res
+    par = res["parity"]["fold_order_1M"]
+    for a in ("ring_old", "ring_chunked", "bcube", "reduce_root"):
+        assert par[a] == "bit-exact", (a, par)
+    for a in ("ring_old", "ring_chunked", "bcube", "halving_doubling", "reduce_root0"):
+        assert isinstance(res["other_algos_ms"][a], float), (a, res["other_algos_ms"])
+
+
 def _run(world, stall_rank, stall_waits):
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, stall_rank, stall_waits))
-             for r in range(world)]
-    for p in procs:
-        p.start()
-    try:
-        out = {}
-        for _ in range(world):
-            r, res, closed = q.get(timeout=300)
-            out[r] = res
-    finally:
-        for p in procs:
-            p.join(timeout=30)
-            if p.is_alive():
-                p.kill()
-    for r, res in out.items():
+    out = _start(world, stall_rank, stall_waits, extra_legs=True)
+    for r, (res, _) in out.items():
         assert isinstance(res, dict), res
-    return out
+    return {r: res for r, (res, _) in out.items()}
 
 
 def test_context_waits_expiring_on_one_rank():

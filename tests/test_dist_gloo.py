@@ -72,7 +72,7 @@ def _worker(rank, world, port, algo, n, ms, ch, q):
 
 @pytest.mark.parametrize("world", [2, 3])
 @pytest.mark.parametrize("algo", ["ring", "direct", "a2a", "ring_old", "ring_chunked",
-                                  "bcube", "reduce", "halving_doubling"])
+                                  "bcube", "reduce", pytest.param("halving_doubling", marks=pytest.mark.extra)])
 def test_gloo_multiprocess_plan(algo, world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

@@ -119,3 +119,16 @@ def test_reference_float16_with_hydra(gpu, mode, P, n, ms):
     form and the old-style rings."""
     j = dropin(mode, P, n, dt="f16", ms=ms)
     assert j["mismatched_bytes"] == 0, j
+
+
+def test_shim_failures_are_gloos_own_exception_types(gpu):
+    """include/hydra/gloo_errors.h: an invalid call inside the reference's gloo::allreduce (the
+    hydra Func with an element type the library rejects, run by allreduce's local reduce,
+    allreduce.cc:46-83, 129-133) leaves it as gloo::EnforceNotMet (common/logging.h:21,42) -- the
+    type a reference caller already catches -- and a valid call on the same context then still
+    sums; the timeout status maps to gloo::IoException (common/error.h:45)."""
+    j = dropin("errors", 1, 1000)
+    assert j["invalid_call"] == "gloo::EnforceNotMet", j
+    assert "invalid dtype" in j["invalid_msg"], j
+    assert j["valid_after"] == "none" and j["valid_sum_ok"], j
+    assert j["timeout_status"] == "gloo::IoException", j

@@ -97,6 +97,7 @@ def test_chunked_allreduce_ring_gpu_reducer_vs_reference(gpu, golden, golden_met
                 assert np.array_equal(bufs[r][i].view(np.uint32), exp.view(np.uint32)), key
 
 
+@pytest.mark.extra
 def test_halving_doubling_gpu_reducer_vs_reference(gpu, golden_algo):
     """hydra::AllreduceHalvingDoubling<T> with the GPU in-place sum (gpuReductionFunction) ==
     the reference's own AllreduceHalvingDoubling<T> outputs (f32/i32), every rank and pointer,
@@ -115,6 +116,7 @@ def test_halving_doubling_gpu_reducer_vs_reference(gpu, golden_algo):
                 assert np.array_equal(bufs[r][i].view(np.uint32), exp.view(np.uint32)), (key, r)
 
 
+@pytest.mark.extra
 def test_bcube_old_gpu_reducer_vs_reference(gpu, golden_algo):
     """Old-style hydra::AllreduceBcube<T> with the GPU in-place sum == the reference's own
     AllreduceBcube<T> outputs (f32/i32), every rank and pointer."""
@@ -309,6 +311,7 @@ def test_hip_allreduce_ring_chunked(gpu, O, workspace, P, nptr, n, dt):
                 assert_bits(got, exp[r][0], (r, i, user_streams))
 
 
+@pytest.mark.extra
 @pytest.mark.parametrize("workspace", ["host", "device"])
 @pytest.mark.parametrize("P,nptr,n,dt", [(1, 2, 1000, "f32"), (2, 1, 262145, "f32"),
                                          (3, 2, 100003, "f32"), (4, 4, 4099, "f32"),
@@ -340,6 +343,7 @@ def test_hip_allreduce_halving_doubling(gpu, O, workspace, P, nptr, n, dt):
                 assert_bits(got, exp[r][0], (r, i, user_streams))
 
 
+@pytest.mark.extra
 @pytest.mark.parametrize("P,nptr,n,dt", [(1, 1, 1000, "f32"), (1, 2, 262145, "f32"),
                                          (2, 3, 100003, "f32"), (1, 5, 4099, "i32"),
                                          (1, 8, 7, "f32"), (1, 2, 0, "f32")])
@@ -364,6 +368,7 @@ def test_hip_allreduce_local(gpu, O, P, nptr, n, dt):
                 assert_bits(got, exp[r], (r, i, user_streams))
 
 
+@pytest.mark.extra
 @pytest.mark.parametrize("workspace", ["host", "device"])
 @pytest.mark.parametrize("P,nptr,n,dt", [(1, 2, 1000, "f32"), (2, 1, 262145, "f32"),
                                          (4, 3, 1000, "f32"), (4, 3, 100003, "f32"),

@@ -358,6 +358,7 @@ def test_simulated_bcube_vs_reference_fixtures(gpu, golden, golden_meta):
                 assert hashlib.sha256(got.tobytes()).hexdigest() == row["output_sha256"], key
 
 
+@pytest.mark.extra
 def test_simulated_halving_doubling_vs_reference_fixtures(gpu, golden_algo):
     """Device HALVING_DOUBLING plan == the reference's own AllreduceHalvingDoubling<T> on every
     rank (tests/golden/golden_algo: P = 1..12, one to three binary blocks, fp32 stress / int32 /
@@ -379,6 +380,7 @@ def test_simulated_halving_doubling_vs_reference_fixtures(gpu, golden_algo):
             assert np.array_equal(bufs[r].cpu().numpy(), exp), (key, r)
 
 
+@pytest.mark.extra
 @pytest.mark.parametrize("P,n", [(8, 1 << 22), (6, 3000017), (7, 1 << 20)])
 def test_simulated_halving_doubling_large(gpu, O, P, n):
     """Multi-MiB buckets through the simulator: bit-exact vs the oracle on every rank."""
@@ -399,7 +401,7 @@ def test_simulated_halving_doubling_large(gpu, O, P, n):
                                          ("ring_old", 3, 300000, 1 << 18),
                                          ("ring_chunked", 4, 1 << 20, 0),
                                          ("bcube", 8, 1 << 20, 0), ("bcube", 6, 6 << 12, 0),
-                                         ("halving_doubling", 8, 1 << 20, 0),
+                                         pytest.param("halving_doubling", 8, 1 << 20, 0, marks=pytest.mark.extra),
                                          ("a2a", 2, 1 << 20, 0), ("a2a", 8, 1 << 20, 0)])
 def test_rccl_executor_self_loop(gpu, O, comm1, algo, P, n, ch):
     """The real RCCL executor on one GPU: rank 0's plan with every peer remapped to itself runs

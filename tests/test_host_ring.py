@@ -303,6 +303,7 @@ def test_allreduce_test_single_pointer_p1_to_15(O, chunked):
                 assert np.all(bufs[r][0] == P * (P - 1) / 2), (P, n, r)
 
 
+@pytest.mark.extra
 def test_halving_doubling_vs_golden(O, golden_algo):
     """hydra::AllreduceHalvingDoubling<T> (allreduce_halving_doubling.h:37-358) reproduces the
     reference's result on every rank and pointer: one, two and three binary blocks (P = 1..12),
@@ -323,6 +324,7 @@ def test_halving_doubling_vs_golden(O, golden_algo):
                                       exp.view(f"u{exp.itemsize}")), (key, r, i)
 
 
+@pytest.mark.extra
 @pytest.mark.parametrize("P,n", [(4, (1 << 20) + 7), (6, 300001), (7, 1 << 18), (13, 70001)])
 def test_halving_doubling_large(O, P, n):
     """Messages far beyond the socket buffers (the FIFO transport must not deadlock) with
@@ -336,6 +338,7 @@ def test_halving_doubling_large(O, P, n):
         assert np.array_equal(bufs[r][0].view(np.uint32), exp[r][0].view(np.uint32)), r
 
 
+@pytest.mark.extra
 def test_bcube_old_vs_golden(O, golden_algo):
     """Old-style hydra::AllreduceBcube<T> (allreduce_bcube.h:255-691) reproduces the
     reference's own class on every rank and pointer (P = 1, 2, 4, 8; 1-2 pointers; f32 / i32
@@ -356,6 +359,7 @@ def test_bcube_old_vs_golden(O, golden_algo):
                                       exp.view(f"u{exp.itemsize}")), (key, r, i)
 
 
+@pytest.mark.extra
 def test_bcube_old_rejects_non_power_of_two(O):
     """The reference's ranks disagree for such P; the drop-in refuses them."""
     bufs = [[np.ones(10, np.float32)] for _ in range(3)]
@@ -363,6 +367,7 @@ def test_bcube_old_rejects_non_power_of_two(O):
         host.allreduce_bcube_old_threads(bufs, reducer_fn=fnptr(O, "orc_isum_f32"))
 
 
+@pytest.mark.extra
 @pytest.mark.parametrize("P,nptr,n", [(1, 1, 100), (1, 3, 1000), (2, 4, 4099), (3, 2, 0)])
 def test_allreduce_local(O, P, nptr, n):
     """gloo::AllreduceLocal<T> (allreduce_local.cc:28-38): each rank's pointers left-folded in

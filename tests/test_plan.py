@@ -330,6 +330,7 @@ def test_bench_reduce_self_check_helper(O):
                               exp[P - 1].view(np.uint32)), (P, n)
 
 
+@pytest.mark.extra
 @pytest.mark.parametrize("P,n", [(2, 1), (2, 1000), (3, 7), (4, 4099), (5, 100), (6, 100003),
                                  (7, 262145), (8, 30011), (11, 5000), (12, 3), (13, 20011)])
 def test_halving_doubling_plan(O, P, n):
@@ -345,7 +346,7 @@ def test_halving_doubling_plan(O, P, n):
         race_check(ring.plan("halving_doubling", P, r, n, 4, 0, 0)[0])
 
 
-BOUNDS_ALGOS = ["ring", "direct", "ring_old", "ring_chunked", "bcube", "halving_doubling"]
+BOUNDS_ALGOS = ["ring", "direct", "ring_old", "ring_chunked", "bcube", pytest.param("halving_doubling", marks=pytest.mark.extra)]
 
 
 @pytest.mark.parametrize("algo", BOUNDS_ALGOS)

@@ -62,7 +62,7 @@ def test_bcube_plan_vs_reference(O, P, n, ms, ch, seed):
     assert_ranks(got, expect_new_style(O, xs, ms, algorithm=2), ("bcube", P, n))
 
 
-@pytest.mark.parametrize("algo", ["ring_old", "ring_chunked", "halving_doubling"])
+@pytest.mark.parametrize("algo", ["ring_old", "ring_chunked", pytest.param("halving_doubling", marks=pytest.mark.extra)])
 @settings(**SETTINGS)
 @given(P=st.integers(2, 8), n=st.integers(1, 3000), ch=st.sampled_from([0, 16, 48, 1024]),
        seed=st.integers(0, 10 ** 6))
