@@ -4,7 +4,10 @@
 #include <hip/hip_runtime.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <map>
+#include <utility>
+#include <vector>
 #include <mutex>
 
 #include "../../include/hydra_hip.h"
@@ -76,14 +79,17 @@ std::map<uintptr_t, Entry>::iterator first_intersecting(Registry& r, uintptr_t l
 // A mapping of p's page the caller made (hipHostRegister / hipHostMalloc): its host range and
 // device address.  Called with the registry lock held and only where no registry entry
 // intersects, so it can never return one of hydra's own registrations.
-bool caller_mapping(uintptr_t p, uintptr_t* start, size_t* size, char** dev_at_p) {
+bool caller_mapping(uintptr_t p, uintptr_t* start, size_t* size, char** dev_at_p,
+                    bool* device = nullptr) {
   hipPointerAttribute_t at{};
   const void* q = reinterpret_cast<const void*>(p);
   if (hipPointerGetAttributes(&at, q) != hipSuccess) {
     (void)hipGetLastError();
     return false;
   }
-  if (at.type != hipMemoryTypeHost || !at.devicePointer) return false;
+  if (device) *device = at.type == hipMemoryTypeDevice || at.type == hipMemoryTypeArray;
+  if ((at.type != hipMemoryTypeHost && at.type != hipMemoryTypeManaged) || !at.devicePointer)
+    return false;
   void* s = nullptr;
   size_t sz = 0;
   hipDeviceptr_t dq = reinterpret_cast<hipDeviceptr_t>(const_cast<void*>(q));
@@ -151,84 +157,97 @@ void retire(Registry& r, std::unique_lock<std::mutex>& g, std::map<uintptr_t, En
 
 }  // namespace
 
-HostWindow host_window_acquire(const void* ptr, size_t bytes, bool pin) {
-  HostWindow w;
-  if (!ptr || !bytes) return w;
+void host_windows_acquire(const void* ptr, size_t bytes, bool pin, HostWindows* out) {
+  *out = HostWindows{};
+  if (!ptr || !bytes) return;
   Registry& r = R();
   const uintptr_t p = reinterpret_cast<uintptr_t>(ptr);
   const uintptr_t end = p + bytes;
   std::unique_lock<std::mutex> g(r.m);
-  auto it = first_intersecting(r, p, end);
-  if (it != r.entries.end()) {
-    Entry& x = it->second;
-    if (x.pending || x.dying) return w;  // being (un)registered by another call: stage
-    const uintptr_t lo = std::max(p, it->first), hi = std::min(end, x.hi);
-    x.users++;
+  auto add = [&](uintptr_t lo, uintptr_t hi, char* dev, int kind, uintptr_t key) {
+    HostWindow& w = out->w[out->count++];
     w.lo = reinterpret_cast<const char*>(lo);
     w.hi = reinterpret_cast<const char*>(hi);
-    w.dev = x.dev + (lo - it->first);
-    w.kind = x.kind;
-    w.key = it->first;
-    return w;
+    w.dev = dev;
+    w.kind = kind;
+    w.key = key;
+  };
+  // 1. hydra's own mappings inside the operand (one being (un)registered by another call is
+  //    not used -- its bytes are staged -- but its pages are never registered again here)
+  std::vector<std::pair<uintptr_t, uintptr_t>> taken;  // intersecting entries, address order
+  for (auto it = first_intersecting(r, p, end); it != r.entries.end() && it->first < end; ++it) {
+    Entry& x = it->second;
+    taken.emplace_back(it->first, x.hi);
+    if (x.pending || x.dying || out->count == kMaxWindows) continue;
+    const uintptr_t lo = std::max(p, it->first), hi = std::min(end, x.hi);
+    x.users++;
+    add(lo, hi, x.dev + (lo - it->first), x.kind, it->first);
   }
-  // no hydra mapping touches the operand: one the caller made?
   uintptr_t s = 0;
   size_t sz = 0;
   char* d = nullptr;
-  if (caller_mapping(p, &s, &sz, &d)) {
-    w.lo = static_cast<const char*>(ptr);
-    w.hi = reinterpret_cast<const char*>(std::min(end, s + sz));
-    w.dev = d;
-    w.kind = kMapCaller;
-    return w;
+  if (taken.empty() && caller_mapping(p, &s, &sz, &d, &out->device)) {
+    // a mapping the caller made (no reference: the caller keeps it for the call)
+    add(p, std::min(end, s + sz), d, kMapCaller, 0);
+    return;
   }
-  if (!pin) return w;
-  uintptr_t lo, hi;
-  page_interior(p, bytes, &lo, &hi);
-  if (lo >= hi) return w;
-  // the interior's first page mapped by the caller (p's page was not): use that, register nothing
-  if (caller_mapping(lo, &s, &sz, &d)) {
-    w.lo = reinterpret_cast<const char*>(lo);
-    w.hi = reinterpret_cast<const char*>(std::min(end, s + sz));
-    w.dev = d;
-    w.kind = kMapCaller;
-    return w;
+  if (out->device || !pin) return;
+  // 2. pin the whole pages of every gap between them (all of the operand when there is none)
+  std::vector<std::pair<uintptr_t, uintptr_t>> mine;  // pending entries this call reserved
+  uintptr_t cur = p;
+  for (size_t k = 0; k <= taken.size() && out->count + (int)mine.size() < kMaxWindows; k++) {
+    const uintptr_t gap_hi = k < taken.size() ? std::max(cur, taken[k].first) : end;
+    uintptr_t lo, hi;
+    page_interior(cur, gap_hi - cur, &lo, &hi);
+    if (k < taken.size()) cur = std::max(cur, taken[k].second);
+    if (lo >= hi) continue;
+    // never overlap a mapping the caller made (the caller's pages are used as they are only
+    // when they cover p; a partial one leaves this gap staged)
+    if (caller_mapping(lo, &s, &sz, &d) || caller_mapping(hi - 1, &s, &sz, &d)) continue;
+    Entry x{};
+    x.hi = hi;
+    x.kind = kMapPin;
+    x.users = 1;
+    x.pending = true;
+    x.owner_lo = p;
+    x.owner_hi = end;
+    r.entries.emplace(lo, x);
+    mine.emplace_back(lo, hi);
   }
-  if (caller_mapping(hi - 1, &s, &sz, &d)) return w;  // caller mapping inside: never overlap it
-  Entry x{};
-  x.hi = hi;
-  x.kind = kMapPin;
-  x.users = 1;
-  x.pending = true;
-  x.owner_lo = p;
-  x.owner_hi = end;
-  r.entries.emplace(lo, x);
+  if (mine.empty()) return;
   g.unlock();
-  char* dev = nullptr;
-  const hipError_t e = do_register(lo, hi, &dev);
+  std::vector<std::pair<hipError_t, char*>> res;
+  for (const auto& m : mine) {  // (the map is not touched without the lock)
+    char* dev = nullptr;
+    const hipError_t e = do_register(m.first, m.second, &dev);
+    res.emplace_back(e, dev);
+  }
   g.lock();
-  settle(r, lo, e, dev, kLedgerTempPin);
-  if (e != hipSuccess) return w;
-  w.lo = reinterpret_cast<const char*>(lo);
-  w.hi = reinterpret_cast<const char*>(hi);
-  w.dev = dev;
-  w.kind = kMapPin;
-  w.key = lo;
-  return w;
+  for (size_t k = 0; k < mine.size(); k++) {
+    const uintptr_t lo = mine[k].first, hi = mine[k].second;
+    settle(r, lo, res[k].first, res[k].second, kLedgerTempPin);
+    if (res[k].first == hipSuccess) add(lo, hi, res[k].second, kMapPin, lo);
+  }
+  std::sort(out->w, out->w + out->count,
+            [](const HostWindow& x, const HostWindow& y) { return x.lo < y.lo; });
 }
 
-void host_window_release(HostWindow* w) {
-  if (!w) return;
-  const uintptr_t key = w->key;
-  *w = HostWindow{};
-  if (!key) return;
+void host_windows_release(HostWindows* ws) {
+  if (!ws) return;
   Registry& r = R();
-  std::unique_lock<std::mutex> g(r.m);
-  auto it = r.entries.find(key);
-  if (it == r.entries.end()) return;
-  Entry& x = it->second;
-  if (--x.users > 0) return;
-  if (x.kind == kMapPin || (x.kind == kMapRegister && x.owners == 0)) retire(r, g, it);
+  std::unique_lock<std::mutex> g(r.m, std::defer_lock);
+  for (int i = 0; i < ws->count; i++) {
+    const uintptr_t key = ws->w[i].key;
+    ws->w[i] = HostWindow{};
+    if (!key) continue;
+    if (!g.owns_lock()) g.lock();
+    auto it = r.entries.find(key);
+    if (it == r.entries.end()) continue;
+    Entry& x = it->second;
+    if (--x.users > 0) continue;
+    if (x.kind == kMapPin || (x.kind == kMapRegister && x.owners == 0)) retire(r, g, it);
+  }
+  ws->count = 0;
 }
 
 int host_register(void* ptr, size_t bytes, const char** what) {

@@ -10,7 +10,8 @@
 //
 //   * every registration hydra makes (hydra_host_register, a per-call pin of a pageable operand)
 //     covers only the WHOLE PAGES strictly inside the caller's range; the ragged head / tail
-//     bytes are staged through device buffers instead;
+//     bytes are copied by the CPU through hydra's own pinned staging instead (hydra never hands
+//     a caller's pageable range to a HIP copy, which would lock its pages page-rounded);
 //   * hydra's registrations never overlap each other: one registry (an interval map) holds them,
 //     plus the pinned blocks of the block cache; a call that finds its operand inside a registry
 //     entry takes a reference on it, so the entry outlives the call's kernel whatever its owner
@@ -21,7 +22,8 @@
 //     appear or vanish between the lookup and its use; the caller keeps it alive for the call,
 //     as for any asynchronous copy from it.
 //
-// Windows are byte ranges [lo, hi) inside the operand; the rest of the operand is staged.
+// Windows are byte ranges [lo, hi) inside the operand; the rest of the operand is staged by the
+// CPU.
 #pragma once
 
 #include <cstddef>
@@ -51,10 +53,20 @@ struct HostWindow {
   bool empty() const { return lo >= hi; }
 };
 
-// The mapped window of the operand [p, p + bytes) (referenced until host_window_release).
-// pin: a pageable operand's interior pages may be registered for the call.
-HostWindow host_window_acquire(const void* p, size_t bytes, bool pin);
-void host_window_release(HostWindow* w);
+// The mapped windows of the operand [p, p + bytes), in address order, each referenced until
+// host_windows_release: every hydra registry entry intersecting the operand (at most
+// kMaxWindows); if there is none, the caller's own mapping of p's page (or, for a pageable
+// operand with pin set, its interior pages registered for the call).  The bytes outside the
+// windows are the caller's pageable memory: hydra only ever reads / writes them with CPU loads
+// and stores.  `device` is set (and no window returned) when the operand is device memory.
+constexpr int kMaxWindows = 4;
+struct HostWindows {
+  HostWindow w[kMaxWindows];
+  int count = 0;
+  bool device = false;
+};
+void host_windows_acquire(const void* p, size_t bytes, bool pin, HostWindows* out);
+void host_windows_release(HostWindows* ws);
 
 // hydra_host_register / hydra_host_unregister (C-ABI semantics in include/hydra_hip.h).
 // Return a hydra status; *what names the failing step.

@@ -76,28 +76,28 @@ int check_args(int op, int dtype, const void* c, const void* a, const void* b, s
 }  // namespace
 
 // ---- host staging context ----------------------------------------------------------------
-// Two streams ping-pong over fixed-size chunks: H2D(a,b) -> reduce -> D2H(c) on stream k%2, so
-// chunk k+1's copies overlap chunk k's kernel and copy-back.
+// A stream, two completion events and two pinned staging buffers (hipHostMalloc blocks of the
+// cache).  Operand bytes the kernel cannot reach in place (hydra_reduce_host) are copied into
+// a staging buffer by the CPU and read / written by the kernel there over PCIe; the two
+// buffers alternate, so the CPU fills round r + 1 while the GPU reduces round r.
 struct hydra_ctx {
   int device = 0;
-  hipStream_t stream[2] = {nullptr, nullptr};
-  void* da[2] = {nullptr, nullptr};
-  void* db[2] = {nullptr, nullptr};
-  void* dc[2] = {nullptr, nullptr};  // only for float16 with c != a
-  size_t chunk_bytes = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t done[2] = {nullptr, nullptr};
+  char* stage[2] = {nullptr, nullptr};      // host address
+  char* stage_dev[2] = {nullptr, nullptr};  // its device address
 };
 
 namespace {
-constexpr size_t kChunkBytes = 8u << 20;
+constexpr size_t kSlotBytes = 4u << 20;  // per operand and staging buffer (3 slots: a, b, c)
 constexpr int kVariantForceStaging = 1000;  // hydra_set_variant value: host path always stages
 constexpr int kVariantNoPinOnTheFly = 1001;  // pageable operands staged, not pinned per call
 
 void ctx_release(hydra_ctx* x) {
+  if (x->stream) (void)hydra::release_stream(x->stream);
   for (int i = 0; i < 2; i++) {
-    if (x->stream[i]) (void)hydra::release_stream(x->stream[i]);
-    if (x->da[i]) (void)hydra::cached_free(x->da[i]);
-    if (x->db[i]) (void)hydra::cached_free(x->db[i]);
-    if (x->dc[i]) (void)hydra::cached_free(x->dc[i]);
+    if (x->done[i]) (void)hydra::release_event(x->done[i]);
+    if (x->stage[i]) (void)hydra::cached_free_host(x->stage[i]);
   }
 }
 }  // namespace
@@ -232,12 +232,16 @@ int hydra_ctx_create(int device, hydra_ctx_t* out) {
   if (device < 0 || device >= count) return fail(HYDRA_ERR_NO_DEVICE, "no such device");
   auto* x = new hydra_ctx();
   x->device = device;
-  x->chunk_bytes = kChunkBytes;
   hipError_t e = hipSetDevice(device);
+  if (e == hipSuccess) e = hydra::cached_stream(device, &x->stream);
   for (int i = 0; i < 2 && e == hipSuccess; i++) {
-    e = hydra::cached_stream(device, &x->stream[i]);
-    if (e == hipSuccess) e = hydra::cached_malloc(device, kChunkBytes, &x->da[i]);
-    if (e == hipSuccess) e = hydra::cached_malloc(device, kChunkBytes, &x->db[i]);
+    e = hydra::cached_event(device, &x->done[i]);
+    void* p = nullptr;
+    if (e == hipSuccess) e = hydra::cached_malloc_host(3 * kSlotBytes, &p);
+    x->stage[i] = static_cast<char*>(p);
+    void* d = nullptr;
+    if (e == hipSuccess) e = hipHostGetDevicePointer(&d, p, 0);
+    x->stage_dev[i] = static_cast<char*>(d);
   }
   if (e != hipSuccess) {
     ctx_release(x);
@@ -251,53 +255,56 @@ int hydra_ctx_create(int device, hydra_ctx_t* out) {
 int hydra_ctx_destroy(hydra_ctx_t ctx) {
   if (!ctx) return ok();
   (void)hipSetDevice(ctx->device);
-  for (int i = 0; i < 2; i++)
-    if (ctx->stream[i]) (void)hipStreamSynchronize(ctx->stream[i]);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   ctx_release(ctx);
   delete ctx;
   return ok();
 }
 
 namespace {
-// Host copies of pageable memory go in pieces of at most 1 MiB: up to that size the HIP runtime
-// copies through its own staging buffers, above it it locks the caller's pages for the copy --
-// page-rounded, so the lock's edge pages hold the operand's neighbours.  hydra
-// never asks the runtime to lock memory outside an operand.
-constexpr size_t kCopyPiece = 1u << 20;
-
-hipError_t copy_pieces(void* dst, const void* src, size_t bytes, hipMemcpyKind kind,
-                       hipStream_t st) {
-  for (size_t off = 0; off < bytes; off += kCopyPiece) {
-    const size_t b = std::min(kCopyPiece, bytes - off);
-    hipError_t e = hipMemcpyAsync(static_cast<char*>(dst) + off,
-                                  static_cast<const char*>(src) + off, b, kind, st);
-    if (e != hipSuccess) return e;
-  }
-  return hipSuccess;
-}
-
-// The mapped windows of one call's operands, released (after the call's kernels finished)
-// when the call returns.
-struct Windows {
-  hydra::HostWindow w[3];
-  ~Windows() {
-    for (auto& x : w) hydra::host_window_release(&x);
+// One operand of a host call: its mapped windows (host_map.h) in element units.
+struct Operand {
+  const char* base = nullptr;
+  hydra::HostWindows win;
+  size_t lo[hydra::kMaxWindows] = {}, hi[hydra::kMaxWindows] = {};
+  int n = 0;
+  // device address of element i if [i, j) lies in one window, else null
+  char* dev(size_t i, size_t j, size_t es) const {
+    for (int k = 0; k < n; k++)
+      if (lo[k] <= i && j <= hi[k]) return win.w[k].dev + (base + i * es - win.w[k].lo);
+    return nullptr;
   }
 };
 
-// An operand's window in elements: [lo, hi) of [0, n) (empty: lo == hi == 0).
-struct ElemRange {
-  size_t lo = 0, hi = 0;
-  bool covers(size_t a, size_t b) const { return lo <= a && b <= hi && a < b; }
-  static ElemRange of(const hydra::HostWindow& w, const void* base, size_t es, size_t n) {
-    ElemRange r;
-    if (w.empty()) return r;
-    const char* b = static_cast<const char*>(base);
-    r.lo = (size_t(w.lo - b) + es - 1) / es;
-    r.hi = std::min(n, size_t(w.hi - b) / es);
-    if (r.lo >= r.hi) r = ElemRange{};
-    return r;
+void set_ranges(Operand* o, size_t es, size_t n) {
+  o->n = 0;
+  for (int k = 0; k < o->win.count; k++) {
+    const hydra::HostWindow& w = o->win.w[k];
+    size_t l = (size_t(w.lo - o->base) + es - 1) / es;
+    size_t h = std::min(n, size_t(w.hi - o->base) / es);
+    if (l < h) {
+      o->lo[o->n] = l;
+      o->hi[o->n] = h;
+      if (o->n != k) o->win.w[o->n] = o->win.w[k];  // (keys stay in win for the release)
+      o->n++;
+    }
   }
+}
+
+// Releases the windows of a call when it returns -- declared before the drain, so any work
+// still enqueued is drained first.
+struct WindowsGuard {
+  hydra::HostWindows* w[3];
+  int k = 0;
+  ~WindowsGuard() {
+    for (int i = 0; i < k; i++) hydra::host_windows_release(w[i]);
+  }
+};
+
+struct CopyOut {
+  char* host;
+  const char* stage;
+  size_t bytes;
 };
 }  // namespace
 
@@ -310,117 +317,144 @@ int hydra_reduce_host(hydra_ctx_t ctx, int op, int dtype, void* c, const void* a
   if (n == 0) return ok();
   HIP_TRY(hipSetDevice(ctx->device));
   const size_t es = hydra::dtype_size(dtype);
-  const size_t per = ctx->chunk_bytes / es;
   const int variant = g_variant.load(std::memory_order_relaxed);
   const size_t nbytes = n * es;
-  // Each operand's mapped window (host_map.h): the part of it the kernel may read / write in
-  // place over PCIe -- a registered bucket (hydra_host_register), a pinned block
-  // (hydra_malloc_host, e.g. the ring's receive slots after setScratchAllocator(pinnedAlloc)),
-  // the caller's own pinned / registered memory, or, for a pageable operand, the whole pages
-  // inside it pinned for this call.  Elements inside all three windows are reduced in one
-  // zero-copy pass; the rest (the ragged edge pages of pageable operands, anything unmapped) is
-  // staged through device buffers, per operand.  kVariantForceStaging stages everything;
+  // Each operand's mapped windows (host_map.h): the parts the kernel reads / writes in place
+  // over PCIe -- a registered bucket (hydra_host_register), a pinned block (hydra_malloc_host,
+  // e.g. the ring's receive slots after setScratchAllocator(pinnedAlloc)), the caller's own
+  // pinned / registered memory, or, for a pageable operand, the whole pages inside it pinned
+  // for this call.  Everything else -- the ragged first / last page of a pageable operand, any
+  // unmapped remainder -- is copied by the CPU into the context's pinned staging and reduced
+  // there.  The whole call is one batched kernel launch per staging round (one round unless
+  // more than kSlotBytes per operand must be staged).  kVariantForceStaging stages everything;
   // kVariantNoPinOnTheFly maps only memory that is already mapped (A/B).
-  Windows win;  // declared before the drain: released only after every stream is drained
-  struct DrainOnError {
-    hipStream_t* st;
+  Operand oc, oa, ob;
+  oc.base = static_cast<const char*>(c);
+  oa.base = static_cast<const char*>(a);
+  ob.base = static_cast<const char*>(b);
+  Operand* A = a == c ? &oc : &oa;
+  Operand* B = b == c ? &oc : b == a ? A : &ob;
+  WindowsGuard guard_;
+  struct Drain {  // an early return drains the stream before the windows are released
+    hipStream_t st;
     bool armed = true;
-    ~DrainOnError() {
-      if (armed)
-        for (int i = 0; i < 2; i++)
-          if (st[i]) (void)hipStreamSynchronize(st[i]);
+    ~Drain() {
+      if (armed) (void)hipStreamSynchronize(st);
     }
   } drain_{ctx->stream};
-  ElemRange rc_, ra_, rb_;
   if (variant != kVariantForceStaging) {
     const bool pin = variant != kVariantNoPinOnTheFly;
-    win.w[0] = hydra::host_window_acquire(c, nbytes, pin);
-    rc_ = ElemRange::of(win.w[0], c, es, n);
-    if (a == c) {
-      ra_ = rc_;
-    } else {
-      win.w[1] = hydra::host_window_acquire(a, nbytes, pin);
-      ra_ = ElemRange::of(win.w[1], a, es, n);
-    }
-    if (b == c) {
-      rb_ = rc_;
-    } else if (b == a) {
-      rb_ = ra_;
-    } else {
-      win.w[2] = hydra::host_window_acquire(b, nbytes, pin);
-      rb_ = ElemRange::of(win.w[2], b, es, n);
+    for (Operand* o : {&oc, A, B}) {
+      bool seen = false;
+      for (int i = 0; i < guard_.k; i++) seen = seen || guard_.w[i] == &o->win;
+      if (seen) continue;
+      hydra::host_windows_acquire(o->base, nbytes, pin, &o->win);
+      guard_.w[guard_.k++] = &o->win;
+      if (o->win.device)
+        return fail(HYDRA_ERR_INVALID,
+                    "hydra_reduce_host: an operand is device memory (use hydra_reduce)");
+      set_ranges(o, es, n);
     }
   }
-  const hydra::HostWindow& wc = win.w[0];
-  const hydra::HostWindow& wa = a == c ? win.w[0] : win.w[1];
-  const hydra::HostWindow& wb = b == c ? win.w[0] : b == a ? wa : win.w[2];
-  // device address of element i of an operand inside its window
-  auto dev = [es](const hydra::HostWindow& w, const void* base, size_t i) -> char* {
-    return w.dev + (static_cast<const char*>(base) + i * es - w.lo);
+  // intervals between window edges: inside one, every operand is either mapped throughout or
+  // staged throughout
+  std::vector<size_t> cut{0, n};
+  for (const Operand* o : {&oc, A, B})
+    for (int k = 0; k < o->n; k++) cut.insert(cut.end(), {o->lo[k], o->hi[k]});
+  std::sort(cut.begin(), cut.end());
+  cut.erase(std::unique(cut.begin(), cut.end()), cut.end());
+
+  const bool c_old_bits = dtype == HYDRA_FLOAT16 && c != a && c != b;  // store quirk: read c
+  std::vector<hydra::BatchSegDesc> segs;
+  std::vector<CopyOut> outs[2];
+  size_t used[3] = {0, 0, 0};  // bytes of the current buffer's a, b, c slots
+  int buf = 0;
+  bool pending[2] = {false, false};
+  // launch the current round on the stream, then make the other buffer reusable
+  auto flush = [&]() -> int {
+    if (segs.empty() && outs[buf].empty()) return HYDRA_OK;
+    hipError_t e = hydra::launch_reduce_batch(op, dtype, segs.data(), segs.size(), ctx->stream);
+    if (e != hipSuccess) return hip_fail(e, "batched reduce kernel launch (host)");
+    HIP_TRY(hipEventRecord(ctx->done[buf], ctx->stream));
+    pending[buf] = true;
+    segs.clear();
+    used[0] = used[1] = used[2] = 0;
+    buf ^= 1;
+    if (pending[buf]) {  // the round before: done, its staged results back to c
+      HIP_TRY(hipEventSynchronize(ctx->done[buf]));
+      for (const CopyOut& o : outs[buf]) std::memcpy(o.host, o.stage, o.bytes);
+      outs[buf].clear();
+      pending[buf] = false;
+    }
+    return HYDRA_OK;
   };
-  // zero-copy region: inside all three windows
-  const size_t z0 = std::max({rc_.lo, ra_.lo, rb_.lo});
-  const size_t z1 = std::min({rc_.hi, ra_.hi, rb_.hi});
-  const bool zero = z0 < z1;
-  if (zero) {
-    hipError_t e = hydra::launch_reduce(0, op, dtype, dev(wc, c, z0), dev(wa, a, z0),
-                                        dev(wb, b, z0), z1 - z0, ctx->stream[0]);
-    if (e != hipSuccess) return hip_fail(e, "reduce kernel launch (zero-copy)");
-  }
-  // the rest, staged per operand in chunks over both streams
-  struct Span {
-    size_t lo, hi;
-  };
-  Span spans[2] = {{0, zero ? z0 : n}, {zero ? z1 : n, n}};
-  size_t k = zero ? 1 : 0;  // the zero-copy pass ran on stream 0
-  for (const Span& sp : spans) {
-    for (size_t off = sp.lo; off < sp.hi; off += per, k++) {
-      const size_t cnt = std::min(per, sp.hi - off);
+  for (size_t q = 0; q + 1 < cut.size(); q++) {
+    size_t off = cut[q];
+    const size_t end = cut[q + 1];
+    while (off < end) {
+      char* dc = oc.dev(off, end, es);
+      char* da = A->dev(off, end, es);
+      char* db = B->dev(off, end, es);
+      if (dc && da && db) {  // in place over PCIe
+        segs.push_back({dc, da, db, end - off});
+        off = end;
+        continue;
+      }
+      // staged: as much of [off, end) as the current buffer's slots still hold
+      const size_t room = kSlotBytes - std::max({used[0], used[1], used[2]});
+      if (room < 64 * es) {
+        if ((rc = flush())) return rc;
+        continue;
+      }
+      const size_t cnt = std::min(end - off, room / es);
       const size_t bytes = cnt * es;
-      const int s = (int)(k & 1);
-      hipStream_t st = ctx->stream[s];
       const size_t ob = off * es;
-      const char* pa = static_cast<const char*>(a) + ob;
-      const char* pb = static_cast<const char*>(b) + ob;
-      char* pc = static_cast<char*>(c) + ob;
-      const bool ma = ra_.covers(off, off + cnt);
-      const bool mb = rb_.covers(off, off + cnt);
-      const bool mc = rc_.covers(off, off + cnt);
-      // operand a: mapped in place, else staged
-      const void* ka = ma ? static_cast<const void*>(dev(wa, a, off)) : ctx->da[s];
-      if (!ma) HIP_TRY(copy_pieces(ctx->da[s], pa, bytes, hipMemcpyHostToDevice, st));
-      const void* kb;
-      if (b == a) {
-        kb = ka;
-      } else if (mb) {
-        kb = dev(wb, b, off);
-      } else {
-        HIP_TRY(copy_pieces(ctx->db[s], pb, bytes, hipMemcpyHostToDevice, st));
-        kb = ctx->db[s];
+      char* host_st = ctx->stage[buf];
+      char* dev_st = ctx->stage_dev[buf];
+      auto slot = [&](int k, const char* src, bool fill) -> char* {  // k: 0 a, 1 b, 2 c
+        const size_t at = size_t(k) * kSlotBytes + used[k];
+        if (fill) std::memcpy(host_st + at, src, bytes);
+        used[k] += (bytes + 255) / 256 * 256;
+        return dev_st + at;
+      };
+      const size_t mark_a = size_t(0) * kSlotBytes + used[0];
+      if (!da) da = slot(0, oa.base + ob, true);
+      if (!db) {
+        if (B == A)
+          db = da;
+        else
+          db = slot(1, B->base + ob, true);
       }
-      // destination: mapped in place; else in place on the staged a (c == a, the ring's form)
-      // or a staging buffer of its own -- which must hold c's old bits for float16's store quirk
-      void* kc;
-      bool copy_back = false;
-      if (mc) {
-        kc = dev(wc, c, off);
-      } else if (c == a && !ma) {
-        kc = ctx->da[s];
-        copy_back = true;
-      } else {
-        if (!ctx->dc[s]) HIP_TRY(hydra::cached_malloc(ctx->device, ctx->chunk_bytes, &ctx->dc[s]));
-        kc = ctx->dc[s];
-        if (dtype == HYDRA_FLOAT16) HIP_TRY(copy_pieces(kc, pc, bytes, hipMemcpyHostToDevice, st));
-        copy_back = true;
+      if (!dc) {
+        if (c == a) {
+          dc = da;
+          outs[buf].push_back({static_cast<char*>(c) + ob, host_st + mark_a, bytes});
+        } else if (c == b) {
+          dc = db;
+          outs[buf].push_back({static_cast<char*>(c) + ob,
+                               host_st + (size_t(dc - dev_st)), bytes});
+        } else {
+          const size_t at = size_t(2) * kSlotBytes + used[2];
+          dc = slot(2, oc.base + ob, c_old_bits);
+          outs[buf].push_back({static_cast<char*>(c) + ob, host_st + at, bytes});
+        }
       }
-      hipError_t e = hydra::launch_reduce(variant >= 1000 ? 0 : variant, op, dtype, kc, ka, kb,
-                                          cnt, st);
-      if (e != hipSuccess) return hip_fail(e, "reduce kernel launch");
-      if (copy_back) HIP_TRY(copy_pieces(pc, kc, bytes, hipMemcpyDeviceToHost, st));
+      segs.push_back({dc, da, db, cnt});
+      off += cnt;
     }
   }
-  HIP_TRY(hipStreamSynchronize(ctx->stream[0]));
-  HIP_TRY(hipStreamSynchronize(ctx->stream[1]));
+  if ((rc = flush())) return rc;
+  for (int k = 0; k < 2; k++) {  // the last rounds: done, results back
+    if (!pending[buf]) {
+      buf ^= 1;
+      continue;
+    }
+    HIP_TRY(hipEventSynchronize(ctx->done[buf]));
+    for (const CopyOut& o : outs[buf]) std::memcpy(o.host, o.stage, o.bytes);
+    outs[buf].clear();
+    pending[buf] = false;
+    buf ^= 1;
+  }
   drain_.armed = false;
   return ok();  // the windows are released here, after every kernel finished
 }

@@ -87,7 +87,15 @@ int check_plan_args(int algo, int op, int dtype, int flags, size_t* esize) {
   return HYDRA_OK;
 }
 
-int resolve_algo(int algo) { return algo == HYDRA_ALGO_AUTO ? HYDRA_ALGO_DIRECT : algo; }
+// HYDRA_ALGO_AUTO: A2A when the reference geometry gives P equal blocks (three launches per
+// allreduce -- ncclAllToAll, one fold, ncclAllGather -- so the host enqueue is independent of the
+// bucket size), else DIRECT.  Both are bit-identical to the reference ring.
+int resolve_algo(int algo, int P, size_t n, size_t es, size_t max_segment) {
+  if (algo != HYDRA_ALGO_AUTO) return algo;
+  const hydra::PlanGeom g =
+      hydra::make_geom(P, n, es, max_segment ? max_segment : (1u << 20), 0);
+  return P > 1 && hydra::blocks_equal(g) ? HYDRA_ALGO_A2A : HYDRA_ALGO_DIRECT;
+}
 
 int check_geometry(int algo, const hydra::PlanGeom& g) {
   if (algo == HYDRA_ALGO_A2A && !hydra::blocks_equal(g))
@@ -417,7 +425,7 @@ int prepare(hydra_comm* c, int* algo, int op, int dtype, int flags, void* buf, s
   if (!buf) return fail(HYDRA_ERR_INVALID, "null buffer");
   if (reinterpret_cast<uintptr_t>(buf) % es)
     return fail(HYDRA_ERR_INVALID, "buffer not aligned to the element size");
-  *algo = resolve_algo(*algo);
+  *algo = root >= 0 ? *algo : resolve_algo(*algo, c->nranks, n, es, max_segment);
   if (*algo == HYDRA_ALGO_RCCL) {
     if (flags & HYDRA_ACC_F32) return fail(HYDRA_ERR_UNSUPPORTED, "ACC_F32 with RCCL");
     return HYDRA_OK;
@@ -566,7 +574,7 @@ int plan_impl(int algo, int root, int P, int rank, size_t n, size_t esize, size_
   if (esize != 1 && esize != 2 && esize != 4 && esize != 8)
     return fail(HYDRA_ERR_INVALID, "bad element size");
   if (root >= P) return fail(HYDRA_ERR_INVALID, "root out of range");
-  algo = root >= 0 ? hydra::kAlgoReduce : resolve_algo(algo);
+  algo = root >= 0 ? hydra::kAlgoReduce : resolve_algo(algo, P, n, esize, max_segment);
   if (algo == HYDRA_ALGO_RCCL) return fail(HYDRA_ERR_UNSUPPORTED, "RCCL has no plan");
   const size_t ms = max_segment ? max_segment : (1u << 20);
   if (root >= 0 && ms < esize) return fail(HYDRA_ERR_INVALID, "max_segment below the element size");
@@ -623,7 +631,7 @@ int simulate_impl(int algo, int root, int op, int dtype, int flags, int P, void*
   if (rc) return rc;
   if (P < 1 || P > hydra::kMaxRanks || !bufs) return fail(HYDRA_ERR_INVALID, "bad P/bufs");
   if (root >= P) return fail(HYDRA_ERR_INVALID, "root out of range");
-  algo = root >= 0 ? hydra::kAlgoReduce : resolve_algo(algo);
+  algo = root >= 0 ? hydra::kAlgoReduce : resolve_algo(algo, P, n, es, max_segment);
   if (algo == HYDRA_ALGO_RCCL) return fail(HYDRA_ERR_UNSUPPORTED, "no RCCL in the simulator");
   if (n == 0 || P == 1) return ok();
   const bool acc32 = (flags & HYDRA_ACC_F32) != 0;

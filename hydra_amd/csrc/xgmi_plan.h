@@ -127,6 +127,12 @@ inline void reduce_geometry(int P, size_t n, size_t esize, size_t max_segment, s
   *S = *ns / (size_t)P;
 }
 
+// Pipelining chunk when the caller passes 0.  16 MiB keeps the host's enqueue of a DIRECT
+// allreduce of BASELINE config 4 (P = 8, 64 Mi fp32: 62 plan ops, ~0.19 ms) well under its
+// ~0.9 ms of xGMI time; 4 MiB (248 ops, ~0.82 ms of ncclSend/ncclRecv calls) sat at the
+// CPU-bound edge (scripts/executor_overhead.py).
+constexpr size_t kDefaultChunk = 16u << 20;
+
 inline PlanGeom make_geom(int P, size_t n, size_t esize, size_t max_segment, size_t chunk) {
   PlanGeom g;
   g.P = P;
@@ -136,7 +142,7 @@ inline PlanGeom make_geom(int P, size_t n, size_t esize, size_t max_segment, siz
   ring_geometry(P, n, esize, max_segment ? max_segment : (1u << 20), &g.num_segments,
                 &g.segment_bytes, &g.S);
   const size_t unit = 16;  // every element size (1, 2, 4, 8) divides 16
-  g.chunk = round_up_sz(std::max<size_t>(chunk ? chunk : (4u << 20), unit), unit);
+  g.chunk = round_up_sz(std::max<size_t>(chunk ? chunk : kDefaultChunk, unit), unit);
   // never pipeline in chunks larger than a block (small buckets keep a small scratch)
   g.chunk = std::min(g.chunk, round_up_sz(std::max<size_t>(g.max_block(), 1), unit));
   return g;
@@ -148,7 +154,7 @@ inline PlanGeom make_geom_reduce(int P, size_t n, size_t esize, size_t max_segme
   reduce_geometry(P, n, esize, max_segment ? max_segment : (1u << 20), &g.num_segments,
                   &g.segment_bytes, &g.S);
   const size_t unit = 16;
-  g.chunk = round_up_sz(std::max<size_t>(chunk ? chunk : (4u << 20), unit), unit);
+  g.chunk = round_up_sz(std::max<size_t>(chunk ? chunk : kDefaultChunk, unit), unit);
   g.chunk = std::min(g.chunk, round_up_sz(std::max<size_t>(g.max_block(), 1), unit));
   g.root = root;
   return g;

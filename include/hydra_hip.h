@@ -127,9 +127,13 @@ int hydra_fold(int op, int dtype, int flags, void* dst, const void* const* srcs,
 int hydra_set_variant(int variant);
 
 /* ---- host-resident reduction --------------------------------------------------------------
- * Same contract on HOST buffers, synchronous like gloo::sum<T>: the context stages a and b to
- * the device, reduces, and copies c back, pipelined in chunks over two HIP streams.  One
- * context per calling thread (bew_allreduce_a runs two rails concurrently: one context each). */
+ * Same contract on HOST buffers, synchronous like gloo::sum<T>: the kernel reads and writes the
+ * mapped parts of a, b and c in place over PCIe (see below) and the rest through the context's
+ * pinned staging, which the CPU fills and empties; one batched launch per call (per 4 MiB of
+ * staged bytes per operand beyond that, double-buffered).  Device pointers are rejected
+ * (HYDRA_ERR_INVALID: use hydra_reduce).  One context per calling thread (bew_allreduce_a runs
+ * two rails concurrently: one context each).  hydra_set_variant(1000) stages every operand,
+ * hydra_set_variant(1001) pins no pageable operand for the call (A/B measurements). */
 int hydra_ctx_create(int device, hydra_ctx_t* out);
 int hydra_ctx_destroy(hydra_ctx_t ctx);
 int hydra_reduce_host(hydra_ctx_t ctx, int op, int dtype, void* c, const void* a, const void* b,
@@ -143,10 +147,10 @@ int hydra_chunk_sum_host(hydra_ctx_t ctx, int dtype, void* c, const void* a, con
  *   - a pageable operand: the WHOLE PAGES inside it, pinned for the call and released before it
  *     returns (hydra_set_variant(1001) turns this off).
  * Everything else -- in particular the ragged first and last page of a pageable operand, which
- * hold memory outside it -- is staged through device buffers in copies of at most 1 MiB (the HIP
- * runtime's own staging; larger pageable copies would make the runtime lock the caller's pages,
- * page-rounded).  hydra never registers or locks a page that holds memory outside the operand
- * it was given, and its registrations never overlap one another. */
+ * hold memory outside it -- is read and written by the CPU only (memcpy through the context's
+ * pinned staging): hydra never hands a caller's pageable range to a HIP copy (which would lock
+ * its pages, page-rounded), never registers a page that holds memory outside the operand it was
+ * given, and its registrations never overlap one another. */
 /* Page-lock caller memory for zero-copy use (optional): registers the whole pages inside
  * [ptr, ptr + bytes) (the ragged edges stay staged).  Reference-counted per start address: every
  * hydra_host_register needs one hydra_host_unregister, and a second register of the same address
@@ -231,9 +235,10 @@ void hydra_ring_plan(int P, size_t n, size_t esize, size_t max_segment, size_t* 
  *                      (allreduce_halving_doubling.h:37-358): recursive halving / doubling in
  *                      binary blocks of P, bit-reversed exchange between blocks; identical
  *                      bits on every rank (max_segment, chunk_bytes unused)
- *   HYDRA_ALGO_AUTO    DIRECT
+ *   HYDRA_ALGO_AUTO    A2A when the reference blocks are equal (n*E a multiple of P*S*segmentBytes),
+ *                      else DIRECT
  * max_segment: the reference's maxSegmentSize (0 = 1 MiB, allreduce.h:78) -- it fixes block
- * ownership; chunk_bytes: pipelining granularity (0 = 4 MiB), does not change results.
+ * ownership; chunk_bytes: pipelining granularity (0 = 16 MiB), does not change results.
  * flags: HYDRA_ACC_F32 -- bf16 bucket, fp32 accumulation, one rounding (BASELINE config 5;
  * DIRECT/A2A/AUTO). */
 #define HYDRA_UNIQUE_ID_BYTES 128

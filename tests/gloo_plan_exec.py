@@ -144,7 +144,7 @@ class GlooPlanComm:
             return
         if n == 0 or self.world == 1:
             return
-        ops, scr = ring.plan("direct" if algo == "auto" else algo, self.world, self.rank, n,
+        ops, scr = ring.plan(algo, self.world, self.rank, n,
                              t.element_size(), max_segment, chunk_bytes)
         execute(self.O, ops, scr, t.view(-1).view(torch.uint8), code, op)
 

@@ -23,24 +23,45 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def test_bench_multi_path_world1(gpu):
+def _run(extra=()):
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
     p = subprocess.run([sys.executable, "-u", "bench.py", "--force-dist", "--steps", "5",
                         "--warmup", "1", "--config5-elements", str(1 << 20),
-                        "--watchdog-s", "100"],
+                        "--watchdog-s", "100", "--cpu-seconds", "2", *extra],
                        cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
     assert p.returncode == 0, (p.returncode, p.stdout[-2000:], p.stderr[-2000:])
     line = [ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1]
-    res = json.loads(line)
+    return json.loads(line)
+
+
+def test_bench_multi_path_world1(gpu):
+    """The default line: north_star's schedules, RCCL's own rank count, the reference ring's
+    CPU baseline (rank 0), config 5, the two rails."""
+    res = _run()
     assert res["n_gpus"] == 1 and res["value"] > 0
     parity = res["parity"]["fold_order_1M"]
-    for algo in ("direct", "ring", "a2a", "ring_old", "ring_chunked", "bcube", "reduce_root",
-                 "apipe"):
+    for algo in ("direct", "ring", "a2a", "apipe"):
         assert parity[algo] == "bit-exact", (algo, parity)
     assert not any(v == "MISMATCH" for v in parity.values()), parity
     assert all(res["parity"]["full_size_exact"].values()), res["parity"]
     assert "watchdog" not in res, res
     # every context leg measured (bounded waits, none expired), config 5 checked and timed
     assert all(isinstance(v, float) for v in res["other_algos_ms"].values()), res
+    assert "ring_old" not in res["other_algos_ms"] and "ring_old" not in parity, res
     assert "error" not in res["config5_bf16"] and res["config5_bf16"]["elements"] == 1 << 20
     assert res["parity"]["full_size_exact"]["config5_bf16_acc32"] is True
+    # what RCCL itself counted (ncclCommCount) and the reference ring's CPU baseline
+    rc = res["rccl_comm"]
+    assert rc["nccl_comm_count"] == rc["min_over_ranks"] == rc["max_over_ranks"] == 1, rc
+    assert rc["backend"] == "rccl" and rc["device"] == 0, rc
+    cb = res["cpu_baseline"]
+    assert cb["kind"] == "reference" and cb["value"] > 0 and cb["cores"] == 2, cb
+
+
+@pytest.mark.extra
+def test_bench_multi_path_world1_extra_legs(gpu):
+    res = _run(["--extra-legs"])
+    parity = res["parity"]["fold_order_1M"]
+    for algo in ("ring_old", "ring_chunked", "bcube", "reduce_root"):
+        assert parity[algo] == "bit-exact", (algo, parity)
+    assert all(isinstance(v, float) for v in res["other_algos_ms"].values()), res

@@ -143,12 +143,13 @@ def test_fault_ledger_names_blocks_and_registrations(gpu):
     _lib.check(L.hydra_free(p))
     h = np.zeros(1 << 20, np.float32)
     _lib.check(L.hydra_host_register(h.ctypes.data, h.nbytes))
+    lo, _ = _lib.page_interior(h.ctypes.data, h.nbytes)  # only whole pages inside are registered
     try:
-        r = _lib.fault_lookup(h.ctypes.data + 100)
+        r = _lib.fault_lookup(lo + 100)
         assert "hydra_host_register" in r and "LIVE" in r, r
     finally:
         _lib.check(L.hydra_host_unregister(h.ctypes.data))
-    r = _lib.fault_lookup(h.ctypes.data + 100)
+    r = _lib.fault_lookup(lo + 100)
     assert "hydra_host_register" in r and "RELEASED" in r, r
     t = torch.empty(1 << 20, device=gpu)
     r = _lib.fault_lookup(t.data_ptr())
@@ -167,7 +168,8 @@ def test_host_register_is_reference_counted(gpu):
     _lib.check(L.hydra_host_register(p, h.nbytes // 2))  # a second owner, a shorter range: fine
     assert L.hydra_host_register(p, h.nbytes + 4096) == _lib.ERR_INVALID
     _lib.check(L.hydra_host_unregister(p))
-    assert "LIVE" in _lib.fault_lookup(p), _lib.fault_lookup(p)  # the first owner still holds it
+    lo, _ = _lib.page_interior(p, h.nbytes)  # the registration: the whole pages inside h
+    assert "LIVE" in _lib.fault_lookup(lo), _lib.fault_lookup(lo)  # the first owner still holds it
     # and it is still what hydra_reduce_host streams in place: same bits as the oracle
     from hydra_amd.reduce import HostContext
 
@@ -179,7 +181,7 @@ def test_host_register_is_reference_counted(gpu):
         ctx.close()
     assert (h == 1).all()
     _lib.check(L.hydra_host_unregister(p))
-    assert "RELEASED" in _lib.fault_lookup(p), _lib.fault_lookup(p)
+    assert "RELEASED" in _lib.fault_lookup(lo), _lib.fault_lookup(lo)
     _lib.check(L.hydra_host_unregister(p))  # nothing left to release: no-op
     x = np.zeros(16, np.float32)
     _lib.check(L.hydra_host_unregister(x.ctypes.data))

@@ -63,6 +63,7 @@ def test_host_register_maps_only_interior_pages(ctx, O, off, nelem):
     else; the call that uses it reduces the interior zero-copy and stages the ragged edges --
     bits exact, every byte around the operands untouched."""
     L = _lib.lib()
+    registered = False
     size = off + 4 * nelem + 2 * PAGE
     base = libc.malloc(size)
     other = libc.malloc(4 * nelem + 64)
@@ -75,6 +76,7 @@ def test_host_register_maps_only_interior_pages(ctx, O, off, nelem):
         b[:] = synth.stress_f32(2, 1, nelem)
         exp = O.op(a.copy(), b.copy(), "sum", 6)
         _lib.check(L.hydra_host_register(base + off, 4 * nelem))
+        registered = True
         regs, _ = live_registrations()
         mine = [m for m in regs if m["owner_lo"] == base + off]
         lo, hi = _lib.page_interior(base + off, 4 * nelem)
@@ -86,10 +88,13 @@ def test_host_register_maps_only_interior_pages(ctx, O, off, nelem):
         _lib.check(L.hydra_reduce_host(ctx.handle, 0, 6, base + off, base + off, other, nelem))
         assert np.array_equal(bits(a), bits(exp))
         assert (raw[:off] == 0xA5).all() and (raw[off + 4 * nelem:] == 0xA5).all()
+        registered = False
         _lib.check(L.hydra_host_unregister(base + off))
         regs, _ = live_registrations()
         assert not [m for m in regs if m["owner_lo"] == base + off]
     finally:
+        if registered:  # never free registered pages (a stale registration poisons the address)
+            L.hydra_host_unregister(base + off)
         libc.free(other)
         libc.free(base)
 
@@ -191,6 +196,7 @@ def test_release_free_realloc_then_pageable_copies(ctx, O, gpu):
     size = (6 << 20) + 123
     addrs = []
     for rnd in range(3):
+        registered = False
         base = libc.malloc(size)
         addrs.append(base)
         try:
@@ -198,6 +204,7 @@ def test_release_free_realloc_then_pageable_copies(ctx, O, gpu):
             raw[:] = rnd
             # a registration of a sub-page-aligned range and per-call pins of odd operands
             _lib.check(L.hydra_host_register(base + 100, (1 << 20) + 10))
+            registered = True
             n = 300_001
             a = f32_at(base + 4 + (2 << 20), n)
             b = f32_at(base + 40 + (4 << 20), n)
@@ -206,10 +213,13 @@ def test_release_free_realloc_then_pageable_copies(ctx, O, gpu):
             _lib.check(L.hydra_reduce_host(ctx.handle, 0, 6, a.ctypes.data, a.ctypes.data,
                                            b.ctypes.data, n))
             assert np.array_equal(bits(a), bits(exp))
+            registered = False
             _lib.check(L.hydra_host_unregister(base + 100))
             regs, _ = live_registrations()
             assert not [r for r in regs if base <= r["lo"] < base + size]
         finally:
+            if registered:
+                L.hydra_host_unregister(base + 100)
             libc.free(base)
         # reallocated (same address on glibc) and copied through torch's pageable path
         again = libc.malloc(size)
