@@ -19,7 +19,7 @@ enum LedgerKind : int {
   kLedgerDeviceBlock = 1,   // hipMalloc by the block cache
   kLedgerPinnedBlock = 2,   // hipHostMalloc by the block cache
   kLedgerHostRegister = 3,  // hydra_host_register
-  kLedgerTempPin = 4,       // hydra_reduce_host: a pageable operand pinned for one call
+  kLedgerTempPin = 4,       // (round 2 only: a pageable operand pinned for one call; retired)
   kLedgerPeerMapping = 5,   // a peer's allocation mapped into this process by IPC (hydra_peer_*)
   kLedgerPeerLocal = 6,     // a peer group's own scratch / signal block (hydra_peer_*)
 };

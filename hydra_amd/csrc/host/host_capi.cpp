@@ -156,22 +156,28 @@ int hydra_host_bench(int config, int P, size_t n, int warmup, int iters, int red
     int reducer = reducer_mode;
     if (reducer == HYDRA_REDUCER_GPU_PINNED_RANK0)
       reducer = r == 0 ? HYDRA_REDUCER_GPU_PINNED : HYDRA_REDUCER_FN;
-    std::vector<float> in(n), out(n);
-    // GPU_PINNED: the receive slots are pinned and the output registered, so every segment
-    // reduce is the zero-copy kernel over PCIe
+    // GPU_PINNED: the receive slots and the output are pinned blocks (hydra_malloc_host), so
+    // every segment reduce is the zero-copy kernel over PCIe.  (Round 2
+    // registered a heap vector instead; hydra registers no transient heap memory any more:
+    // DESIGN.md §10.)
     const bool pinned = reducer == HYDRA_REDUCER_GPU_PINNED;
+    std::vector<float> in(n), out_heap(pinned ? 0 : n);
+    struct PinnedOut {
+      float* p = nullptr;
+      ~PinnedOut() {
+        if (p) hydra_free_host(p);
+      }
+    } pout;
     if (pinned) {
       for (auto& ctx : c)
         ctx->setScratchAllocator({&hydra::gloo_compat::pinnedAlloc, &hydra::gloo_compat::pinnedFree});
-      if (n) hydra::gloo_compat::enforce(hydra_host_register(out.data(), n * sizeof(float)));
+      void* q = nullptr;
+      hydra::gloo_compat::enforce(hydra_malloc_host((n ? n : 1) * sizeof(float), &q));
+      pout.p = static_cast<float*>(q);
+      std::fill(pout.p, pout.p + n, 0.0f);
       reducer = HYDRA_REDUCER_GPU;
     }
-    struct Unreg {
-      void* p;
-      ~Unreg() {
-        if (p) hydra_host_unregister(p);
-      }
-    } unreg{pinned && n ? out.data() : nullptr};
+    float* out = pinned ? pout.p : out_heap.data();
     auto time_it = [&](const std::function<void()>& run) {
       for (int i = 0; i < warmup; i++) run();
       for (int i = 0; i < iters; i++) {
@@ -185,7 +191,7 @@ int hydra_host_bench(int config, int P, size_t n, int warmup, int iters, int red
       for (size_t j = 0; j < n; j++) in[j] = float(j * (size_t)P + (size_t)r);
       hydra::AllreduceOptions o(c[0]);
       o.setInput(in.data(), n);
-      o.setOutput(out.data(), n);
+      o.setOutput(out, n);
       o.setAlgorithm(hydra::AllreduceOptions::RING);
       o.setReduceFunction(make_reducer(reducer, HYDRA_SUM, HYDRA_FLOAT32, fn));
       time_it([&] { hydra::allreduce(o); });
@@ -193,7 +199,7 @@ int hydra_host_bench(int config, int P, size_t n, int warmup, int iters, int red
       for (size_t j = 0; j < n; j++) in[j] = float((double)j * (r + 1.0));
       hydra::APipeAllreduceOptions o(c[0], c[1]);
       o.setInput(in.data(), n);
-      o.setOutput(out.data(), n);
+      o.setOutput(out, n);
       o.setAlgorithm(hydra::AllreduceOptions::RING);
       o.setReduceFunction(make_reducer(reducer, HYDRA_SUM, HYDRA_FLOAT32, fn));
       time_it([&] { hydra::apipe_allreduce(o); });

@@ -145,7 +145,7 @@ void settle(Registry& r, uintptr_t lo, hipError_t e, char* dev, LedgerKind lk) {
 // Unregister and erase entry `it` (lock held on entry via `g`, released around the HIP call).
 void retire(Registry& r, std::unique_lock<std::mutex>& g, std::map<uintptr_t, Entry>::iterator it) {
   const uintptr_t lo = it->first;
-  const LedgerKind lk = it->second.kind == kMapPin ? kLedgerTempPin : kLedgerHostRegister;
+  const LedgerKind lk = kLedgerHostRegister;
   it->second.dying = true;  // still intersects: nobody maps or registers these pages meanwhile
   g.unlock();
   (void)hipHostUnregister(reinterpret_cast<void*>(lo));
@@ -157,7 +157,7 @@ void retire(Registry& r, std::unique_lock<std::mutex>& g, std::map<uintptr_t, En
 
 }  // namespace
 
-void host_windows_acquire(const void* ptr, size_t bytes, bool pin, HostWindows* out) {
+void host_windows_acquire(const void* ptr, size_t bytes, HostWindows* out) {
   *out = HostWindows{};
   if (!ptr || !bytes) return;
   Registry& r = R();
@@ -172,64 +172,23 @@ void host_windows_acquire(const void* ptr, size_t bytes, bool pin, HostWindows* 
     w.kind = kind;
     w.key = key;
   };
-  // 1. hydra's own mappings inside the operand (one being (un)registered by another call is
-  //    not used -- its bytes are staged -- but its pages are never registered again here)
-  std::vector<std::pair<uintptr_t, uintptr_t>> taken;  // intersecting entries, address order
+  // hydra's own mappings inside the operand (one being (un)registered meanwhile is not used:
+  // its bytes are staged)
+  bool any = false;
   for (auto it = first_intersecting(r, p, end); it != r.entries.end() && it->first < end; ++it) {
     Entry& x = it->second;
-    taken.emplace_back(it->first, x.hi);
+    any = true;
     if (x.pending || x.dying || out->count == kMaxWindows) continue;
     const uintptr_t lo = std::max(p, it->first), hi = std::min(end, x.hi);
     x.users++;
     add(lo, hi, x.dev + (lo - it->first), x.kind, it->first);
   }
+  if (any) return;
+  // none: a mapping the caller made (no reference: the caller keeps it for the call)
   uintptr_t s = 0;
   size_t sz = 0;
   char* d = nullptr;
-  if (taken.empty() && caller_mapping(p, &s, &sz, &d, &out->device)) {
-    // a mapping the caller made (no reference: the caller keeps it for the call)
-    add(p, std::min(end, s + sz), d, kMapCaller, 0);
-    return;
-  }
-  if (out->device || !pin) return;
-  // 2. pin the whole pages of every gap between them (all of the operand when there is none)
-  std::vector<std::pair<uintptr_t, uintptr_t>> mine;  // pending entries this call reserved
-  uintptr_t cur = p;
-  for (size_t k = 0; k <= taken.size() && out->count + (int)mine.size() < kMaxWindows; k++) {
-    const uintptr_t gap_hi = k < taken.size() ? std::max(cur, taken[k].first) : end;
-    uintptr_t lo, hi;
-    page_interior(cur, gap_hi - cur, &lo, &hi);
-    if (k < taken.size()) cur = std::max(cur, taken[k].second);
-    if (lo >= hi) continue;
-    // never overlap a mapping the caller made (the caller's pages are used as they are only
-    // when they cover p; a partial one leaves this gap staged)
-    if (caller_mapping(lo, &s, &sz, &d) || caller_mapping(hi - 1, &s, &sz, &d)) continue;
-    Entry x{};
-    x.hi = hi;
-    x.kind = kMapPin;
-    x.users = 1;
-    x.pending = true;
-    x.owner_lo = p;
-    x.owner_hi = end;
-    r.entries.emplace(lo, x);
-    mine.emplace_back(lo, hi);
-  }
-  if (mine.empty()) return;
-  g.unlock();
-  std::vector<std::pair<hipError_t, char*>> res;
-  for (const auto& m : mine) {  // (the map is not touched without the lock)
-    char* dev = nullptr;
-    const hipError_t e = do_register(m.first, m.second, &dev);
-    res.emplace_back(e, dev);
-  }
-  g.lock();
-  for (size_t k = 0; k < mine.size(); k++) {
-    const uintptr_t lo = mine[k].first, hi = mine[k].second;
-    settle(r, lo, res[k].first, res[k].second, kLedgerTempPin);
-    if (res[k].first == hipSuccess) add(lo, hi, res[k].second, kMapPin, lo);
-  }
-  std::sort(out->w, out->w + out->count,
-            [](const HostWindow& x, const HostWindow& y) { return x.lo < y.lo; });
+  if (caller_mapping(p, &s, &sz, &d, &out->device)) add(p, std::min(end, s + sz), d, kMapCaller, 0);
 }
 
 void host_windows_release(HostWindows* ws) {
@@ -245,7 +204,7 @@ void host_windows_release(HostWindows* ws) {
     if (it == r.entries.end()) continue;
     Entry& x = it->second;
     if (--x.users > 0) continue;
-    if (x.kind == kMapPin || (x.kind == kMapRegister && x.owners == 0)) retire(r, g, it);
+    if (x.kind == kMapRegister && x.owners == 0) retire(r, g, it);
   }
   ws->count = 0;
 }

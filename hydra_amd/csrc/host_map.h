@@ -1,22 +1,26 @@
 // host_map.h -- which caller host memory a kernel may touch in place (zero-copy), and for how long.
 //
 // hydra_reduce_host lets the chunk-sum kernel read and write host operands over PCIe when they
-// are mapped for the GPU.  A mapping the kernel uses must stay mapped until the kernel is done,
-// and hydra must never map a page that holds memory outside the operand it was asked about: the
-// HIP runtime maps registered host pages at their own address, and two owners registering one
-// page (say, a per-call pin of a sub-page operand and the runtime's page-rounded lock of a
-// neighbouring buffer for a pageable copy) share that GPU mapping until the first one releases
-// it -- the leading suspect for round 2's late device faults.  So:
+// are mapped for the GPU.  A mapping the kernel uses must stay mapped until the kernel is done.
 //
-//   * every registration hydra makes (hydra_host_register, a per-call pin of a pageable operand)
-//     covers only the WHOLE PAGES strictly inside the caller's range; the ragged head / tail
-//     bytes are copied by the CPU through hydra's own pinned staging instead (hydra never hands
-//     a caller's pageable range to a HIP copy, which would lock its pages page-rounded);
+// Round 3 found what the late device faults of rounds 1-2 were (DESIGN.md §10,
+// profiles/r03_fault_report.txt): host pages that hydra had hipHostRegister'ed and
+// hipHostUnregister'ed -- per-call pins of pageable operands, or test buffers registered with
+// hydra_host_register -- were later freed, reused by the allocator, and copied by the HIP
+// runtime's own pageable copy path (above 1 MiB it locks the caller's pages); that copy faulted
+// on the GPU, seconds after hydra had released the range.  So:
+//
+//   * hydra never registers host memory on its own: a pageable operand is read and written by
+//     the CPU only (memcpy through the context's pinned staging), never pinned for a call and
+//     never handed to a HIP copy;
+//   * hydra_host_register (an explicit, long-lived registration the caller asks for) covers only
+//     the WHOLE PAGES strictly inside the caller's range, never a page shared with other
+//     objects; the ragged head / tail bytes are staged;
 //   * hydra's registrations never overlap each other: one registry (an interval map) holds them,
 //     plus the pinned blocks of the block cache; a call that finds its operand inside a registry
 //     entry takes a reference on it, so the entry outlives the call's kernel whatever its owner
-//     does meanwhile (the case round 2's advisor raised: one thread's operand inside another
-//     thread's per-call pin);
+//     does meanwhile (the case round 2's advisor raised: one thread's operand inside another's
+//     mapping);
 //   * a mapping hydra did not make (the caller's own hipHostRegister / hipHostMalloc, e.g. torch
 //     pinned tensors) is looked up with the registry lock held, so no hydra registration can
 //     appear or vanish between the lookup and its use; the caller keeps it alive for the call,
@@ -39,7 +43,7 @@ void page_interior(uintptr_t p, size_t bytes, uintptr_t* lo, uintptr_t* hi);
 enum HostMapKind : int {
   kMapNone = 0,
   kMapRegister = 1,     // hydra_host_register (whole interior pages)
-  kMapPin = 2,          // pinned for one hydra_reduce_host call (whole interior pages)
+  kMapPin = 2,          // (retired in round 3: pageable operands are no longer pinned per call)
   kMapPinnedBlock = 3,  // hipHostMalloc block of the cache (hydra_malloc_host)
   kMapCaller = 4,       // mapped by the caller, not by hydra (no reference taken)
 };
@@ -55,17 +59,16 @@ struct HostWindow {
 
 // The mapped windows of the operand [p, p + bytes), in address order, each referenced until
 // host_windows_release: every hydra registry entry intersecting the operand (at most
-// kMaxWindows); if there is none, the caller's own mapping of p's page (or, for a pageable
-// operand with pin set, its interior pages registered for the call).  The bytes outside the
-// windows are the caller's pageable memory: hydra only ever reads / writes them with CPU loads
-// and stores.  `device` is set (and no window returned) when the operand is device memory.
+// kMaxWindows) or, if there is none, the caller's own mapping of p's page.  The bytes outside
+// the windows are the caller's pageable memory: hydra only ever reads / writes them with CPU
+// loads and stores.  `device` is set (and no window returned) when the operand is device memory.
 constexpr int kMaxWindows = 4;
 struct HostWindows {
   HostWindow w[kMaxWindows];
   int count = 0;
   bool device = false;
 };
-void host_windows_acquire(const void* p, size_t bytes, bool pin, HostWindows* out);
+void host_windows_acquire(const void* p, size_t bytes, HostWindows* out);
 void host_windows_release(HostWindows* ws);
 
 // hydra_host_register / hydra_host_unregister (C-ABI semantics in include/hydra_hip.h).

@@ -91,7 +91,6 @@ struct hydra_ctx {
 namespace {
 constexpr size_t kSlotBytes = 4u << 20;  // per operand and staging buffer (3 slots: a, b, c)
 constexpr int kVariantForceStaging = 1000;  // hydra_set_variant value: host path always stages
-constexpr int kVariantNoPinOnTheFly = 1001;  // pageable operands staged, not pinned per call
 
 void ctx_release(hydra_ctx* x) {
   if (x->stream) (void)hydra::release_stream(x->stream);
@@ -321,13 +320,12 @@ int hydra_reduce_host(hydra_ctx_t ctx, int op, int dtype, void* c, const void* a
   const size_t nbytes = n * es;
   // Each operand's mapped windows (host_map.h): the parts the kernel reads / writes in place
   // over PCIe -- a registered bucket (hydra_host_register), a pinned block (hydra_malloc_host,
-  // e.g. the ring's receive slots after setScratchAllocator(pinnedAlloc)), the caller's own
-  // pinned / registered memory, or, for a pageable operand, the whole pages inside it pinned
-  // for this call.  Everything else -- the ragged first / last page of a pageable operand, any
-  // unmapped remainder -- is copied by the CPU into the context's pinned staging and reduced
-  // there.  The whole call is one batched kernel launch per staging round (one round unless
-  // more than kSlotBytes per operand must be staged).  kVariantForceStaging stages everything;
-  // kVariantNoPinOnTheFly maps only memory that is already mapped (A/B).
+  // e.g. the ring's receive slots after setScratchAllocator(pinnedAlloc)) or the caller's own
+  // pinned / registered memory.  Everything else -- pageable memory, the ragged first / last
+  // page of a registered range -- is copied by the CPU into the context's pinned staging and
+  // reduced there (pageable memory is never pinned for a call: DESIGN.md §10).  The whole call
+  // is one batched kernel launch per staging round (one round unless more than kSlotBytes per
+  // operand must be staged).  kVariantForceStaging stages everything (A/B).
   Operand oc, oa, ob;
   oc.base = static_cast<const char*>(c);
   oa.base = static_cast<const char*>(a);
@@ -343,12 +341,11 @@ int hydra_reduce_host(hydra_ctx_t ctx, int op, int dtype, void* c, const void* a
     }
   } drain_{ctx->stream};
   if (variant != kVariantForceStaging) {
-    const bool pin = variant != kVariantNoPinOnTheFly;
     for (Operand* o : {&oc, A, B}) {
       bool seen = false;
       for (int i = 0; i < guard_.k; i++) seen = seen || guard_.w[i] == &o->win;
       if (seen) continue;
-      hydra::host_windows_acquire(o->base, nbytes, pin, &o->win);
+      hydra::host_windows_acquire(o->base, nbytes, &o->win);
       guard_.w[guard_.k++] = &o->win;
       if (o->win.device)
         return fail(HYDRA_ERR_INVALID,

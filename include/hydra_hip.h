@@ -132,42 +132,44 @@ int hydra_set_variant(int variant);
  * pinned staging, which the CPU fills and empties; one batched launch per call (per 4 MiB of
  * staged bytes per operand beyond that, double-buffered).  Device pointers are rejected
  * (HYDRA_ERR_INVALID: use hydra_reduce).  One context per calling thread (bew_allreduce_a runs
- * two rails concurrently: one context each).  hydra_set_variant(1000) stages every operand,
- * hydra_set_variant(1001) pins no pageable operand for the call (A/B measurements). */
+ * two rails concurrently: one context each).  hydra_set_variant(1000) stages every operand
+ * (A/B measurements). */
 int hydra_ctx_create(int device, hydra_ctx_t* out);
 int hydra_ctx_destroy(hydra_ctx_t ctx);
 int hydra_reduce_host(hydra_ctx_t ctx, int op, int dtype, void* c, const void* a, const void* b,
                       size_t n);
 int hydra_chunk_sum_host(hydra_ctx_t ctx, int dtype, void* c, const void* a, const void* b,
                          size_t n);
-/* Which host memory the kernel reads / writes in place (zero-copy over PCIe), per operand:
- *   - a range registered with hydra_host_register, a pinned block from hydra_malloc_host, or
- *     memory the caller pinned / registered itself (hipHostMalloc, hipHostRegister, torch pinned
- *     tensors; the caller keeps it so for the call, as for any copy from it);
- *   - a pageable operand: the WHOLE PAGES inside it, pinned for the call and released before it
- *     returns (hydra_set_variant(1001) turns this off).
- * Everything else -- in particular the ragged first and last page of a pageable operand, which
- * hold memory outside it -- is read and written by the CPU only (memcpy through the context's
- * pinned staging): hydra never hands a caller's pageable range to a HIP copy (which would lock
- * its pages, page-rounded), never registers a page that holds memory outside the operand it was
- * given, and its registrations never overlap one another. */
+/* Which host memory the kernel reads / writes in place (zero-copy over PCIe), per operand: a
+ * range registered with hydra_host_register, a pinned block from hydra_malloc_host, or memory
+ * the caller pinned / registered itself (hipHostMalloc, hipHostRegister, torch pinned tensors;
+ * the caller keeps it so for the call, as for any copy from it).  Everything else -- pageable
+ * memory, and the ragged first and last page of a registered range, which hold memory outside
+ * it -- is read and written by the CPU only (memcpy through the context's pinned staging).
+ * hydra never registers host memory on its own and never hands a caller's pageable range to a
+ * HIP copy: on ROCm 7.2 host pages once registered and released, then reused and copied by the
+ * runtime's page-locking pageable copy path, faulted the GPU.  Its
+ * registrations never overlap one another and never cover a page holding memory outside the
+ * range it was asked for. */
 /* Page-lock caller memory for zero-copy use (optional): registers the whole pages inside
  * [ptr, ptr + bytes) (the ragged edges stay staged).  Reference-counted per start address: every
  * hydra_host_register needs one hydra_host_unregister, and a second register of the same address
  * may not cover more bytes.  Pages already mapped by their owner (hipHostRegister /
  * hipHostMalloc) are used as they are and never released here; pages another hydra registration
  * holds are shared with it; unregistering an address not registered here is a no-op.  The pages
- * stay registered until the last unregister AND the last in-flight call using them are done. */
+ * stay registered until the last unregister AND the last in-flight call using them are done.
+ * Register long-lived buffers only: do not free a registered range and hand its pages to
+ * pageable HIP copies afterwards in the same process (the fault described above). */
 int hydra_host_register(void* ptr, size_t bytes);
 int hydra_host_unregister(void* ptr);
 /* Inspection (tests): the whole pages inside [ptr, ptr + bytes), [*lo, *hi) (empty: equal). */
 void hydra_page_interior(uint64_t ptr, size_t bytes, uint64_t* lo, uint64_t* hi);
-/* Inspection (tests): hydra's live host mappings (registrations, per-call pins, pinned blocks),
+/* Inspection (tests): hydra's live host mappings (registrations and pinned blocks),
  * how many hipHostRegister calls hydra has made, and how many of those covered a byte outside
  * the caller range they were made for (0 by construction). */
 typedef struct {
   uint64_t lo, hi;  /* mapped host range */
-  int32_t kind;     /* 1 hydra_host_register, 2 per-call pin, 3 pinned block */
+  int32_t kind;     /* 1 hydra_host_register, 3 pinned block */
   int32_t owners;   /* hydra_host_register owners */
   int32_t users;    /* in-flight calls using it */
   uint64_t owner_lo, owner_hi; /* the caller range it was made for */

@@ -9,8 +9,8 @@
  * reducer: HYDRA_REDUCER_GPU  -> hydra_reduce_host (H2D -> gfx950 kernel -> D2H, synchronous)
  *          HYDRA_REDUCER_FN   -> the caller's function (CPU-side tests plug the oracle in here)
  *          HYDRA_REDUCER_GPU_PINNED -> GPU with pinned receive slots (Context scratch allocator);
- *                               with a registered output every segment reduce is zero-copy
- *                               (hydra_host_bench registers its output itself)
+ *                               with a pinned output every segment reduce is zero-copy
+ *                               (hydra_host_bench allocates its output pinned itself)
  */
 #ifndef HYDRA_HOST_H_
 #define HYDRA_HOST_H_

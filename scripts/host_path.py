@@ -41,34 +41,38 @@ ctx = HostContext(0)
 iso_sizes = ([int(x) for x in os.environ["ISO_SIZES"].split(",")] if os.environ.get("ISO_SIZES")
              else [1 << 18, 1 << 22, 1 << 24])
 for n in iso_sizes:
-    a = np.arange(n, dtype=np.float32)
-    b = np.ones(n, dtype=np.float32)
-    for mode in ("pageable", "pageable_staged", "registered", "registered_zero_copy",
+    import mmap  # registered memory never returns to the allocator
+
+    a = np.frombuffer(mmap.mmap(-1, 4 * n), np.float32)
+    b = np.frombuffer(mmap.mmap(-1, 4 * n), np.float32)
+    a[:] = np.arange(n, dtype=np.float32)
+    b[:] = 1
+    for mode in ("pageable", "registered_staged", "registered_zero_copy",
                  "bucket_registered_b_pageable"):
-        # "registered": staged copies on registered memory; "_zero_copy": the kernel reads and
-        # writes the registered host ranges over PCIe directly (hydra_reduce_host's default
-        # whenever all three ranges are pinned/registered); "bucket_registered_b_pageable": only
-        # c == a registered (a bucket registered once), b pageable like the reference ring's
-        # scratch -- a and c in place over PCIe, b staged
-        # "pageable": pinned for the call (hydra_reduce_host's default); "pageable_staged": the
-        # staged path for pageable operands (variant 1001)
-        prev = L.hydra_set_variant({"registered": 1000, "pageable_staged": 1001}.get(mode, 0))
-        if mode not in ("pageable", "pageable_staged"):
+        # "pageable": copied by the CPU through the context's pinned staging (hydra never pins
+        # pageable memory for a call); "registered_staged": registered, but forced through the
+        # staging (variant 1000); "_zero_copy": the kernel reads and writes the registered host
+        # ranges over PCIe directly (hydra_reduce_host's default whenever all three ranges are
+        # pinned/registered); "bucket_registered_b_pageable": only c == a registered (a bucket
+        # registered once), b pageable like the reference ring's scratch
+        prev = L.hydra_set_variant(1000 if mode == "registered_staged" else 0)
+        bb = b if mode != "bucket_registered_b_pageable" else np.ones(n, np.float32)
+        if mode != "pageable":
             _lib.check(L.hydra_host_register(a.ctypes.data, a.nbytes))
-        if mode in ("registered", "registered_zero_copy"):
+        if mode in ("registered_staged", "registered_zero_copy"):
             _lib.check(L.hydra_host_register(b.ctypes.data, b.nbytes))
         reps = max(3, int(2e8 / (12 * n)))
         _lib.check(L.hydra_reduce_host(ctx.handle, 0, 6, a.ctypes.data, a.ctypes.data,
-                                       b.ctypes.data, n))
+                                       bb.ctypes.data, n))
         t0 = time.perf_counter()
         for _ in range(reps):
             _lib.check(L.hydra_reduce_host(ctx.handle, 0, 6, a.ctypes.data, a.ctypes.data,
-                                           b.ctypes.data, n))
+                                           bb.ctypes.data, n))
         dt = (time.perf_counter() - t0) / reps
         L.hydra_set_variant(prev)
-        if mode not in ("pageable", "pageable_staged"):
+        if mode != "pageable":
             L.hydra_host_unregister(a.ctypes.data)
-        if mode in ("registered", "registered_zero_copy"):
+        if mode in ("registered_staged", "registered_zero_copy"):
             L.hydra_host_unregister(b.ctypes.data)
         iso.append({"elements": n, "mode": mode, "us": round(dt * 1e6, 1),
                     "GBps_12B": round(12 * n / dt / 1e9, 2)})

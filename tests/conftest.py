@@ -117,6 +117,48 @@ def _fault_context(torch, _lib) -> str:
         return f" [fault context unavailable: {e}]"
 
 
+class _HostPool:
+    """Host buffers for hydra_host_register, each in its own anonymous mapping that stays mapped
+    for the whole test session and is handed out again to later tests.  The suite registers no
+    other host memory: round 3 caught the late device fault of rounds 1-2 -- host pages that had
+    been registered and released, then reused by the allocator and copied by the HIP runtime's
+    page-locking pageable copy path, faulted the GPU.  Pages from this pool are
+    never returned to the allocator, so no pageable copy ever lands on them."""
+
+    def __init__(self):
+        self.free = {}  # size -> [mmap]
+        self.lent = []
+
+    def get(self, n, dtype, fill=None):
+        import mmap
+
+        dt = np.dtype(dtype)
+        size = max(4096, -(-(n * dt.itemsize) // 4096) * 4096)
+        lst = self.free.setdefault(size, [])
+        m = lst.pop() if lst else mmap.mmap(-1, size)
+        self.lent.append((size, m))
+        a = np.frombuffer(m, dtype=dt, count=n)
+        if fill is not None:
+            a[:] = fill
+        return a
+
+    def give_back(self):
+        for size, m in self.lent:
+            self.free.setdefault(size, []).append(m)
+        self.lent.clear()
+
+
+_POOL = _HostPool()
+
+
+@pytest.fixture
+def host_buf():
+    """host_buf(n, dtype, fill=None) -> a numpy array safe to hydra_host_register (see _HostPool);
+    unregister it before the test ends."""
+    yield _POOL.get
+    _POOL.give_back()
+
+
 @pytest.fixture(scope="session")
 def gpu():
     """cuda:0 with libhydra_hip.so loaded; the HIP path must be the one that runs."""

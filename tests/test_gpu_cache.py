@@ -130,7 +130,7 @@ def test_invalid_device_is_refused_and_current_device_kept(gpu):
     _lib.check(L.hydra_device_check(0))
 
 
-def test_fault_ledger_names_blocks_and_registrations(gpu):
+def test_fault_ledger_names_blocks_and_registrations(gpu, host_buf):
     """The fault report's ledger (hydra_fault_lookup): a live cache block, a host range registered
     by hydra_host_register and, once released, the same range as RELEASED; a report for torch's
     own memory.  Nothing faults here: the report is read directly."""
@@ -141,7 +141,7 @@ def test_fault_ledger_names_blocks_and_registrations(gpu):
     r = _lib.fault_lookup(p.value + 4096)
     assert "device block" in r and "LIVE" in r, r
     _lib.check(L.hydra_free(p))
-    h = np.zeros(1 << 20, np.float32)
+    h = host_buf(1 << 20, np.float32, 0)
     _lib.check(L.hydra_host_register(h.ctypes.data, h.nbytes))
     lo, _ = _lib.page_interior(h.ctypes.data, h.nbytes)  # only whole pages inside are registered
     try:
@@ -157,12 +157,12 @@ def test_fault_ledger_names_blocks_and_registrations(gpu):
     assert _lib.fault_last()[2] == 0  # no fault seen in this process
 
 
-def test_host_register_is_reference_counted(gpu):
+def test_host_register_is_reference_counted(gpu, host_buf):
     """Two owners of one buffer each register and unregister it: the registration lives until the
     last unregister (the fault ledger shows it LIVE, then RELEASED); a second register may not
     cover more bytes than the first; unregistering an unknown address is a no-op."""
     L = _lib.lib()
-    h = np.zeros(1 << 20, np.float32)
+    h = host_buf(1 << 20, np.float32, 0)
     p = h.ctypes.data
     _lib.check(L.hydra_host_register(p, h.nbytes))
     _lib.check(L.hydra_host_register(p, h.nbytes // 2))  # a second owner, a shorter range: fine

@@ -218,7 +218,7 @@ def test_host_bench_pinned_zero_copy(gpu, O, config):
     assert s.shape == (3,) and np.all(s > 0)
 
 
-def test_host_ring_pinned_scratch_zero_copy(gpu, O):
+def test_host_ring_pinned_scratch_zero_copy(gpu, O, host_buf):
     """The ring over pinned receive slots and a registered output (zero-copy GPU reduces) is
     bit-exact vs the reference ring: the default GPU reducer path picks zero-copy by itself."""
     import ctypes
@@ -228,7 +228,7 @@ def test_host_ring_pinned_scratch_zero_copy(gpu, O):
     L = _lib.lib()
     P, n = 3, 100003
     xs = [synth.stress_f32(P, r, n) for r in range(P)]
-    outs = [[x.copy()] for x in xs]
+    outs = [[host_buf(n, np.float32, x)] for x in xs]
     for o in outs:
         _lib.check(L.hydra_host_register(o[0].ctypes.data, o[0].nbytes))
     try:

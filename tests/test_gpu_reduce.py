@@ -245,11 +245,12 @@ def test_ring_call_pattern(dev, O):
                 assert np.array_equal(bits(out[lo:hi]), bits(exp[lo:hi])), (P, n, q)
 
 
-@pytest.mark.parametrize("variant", [0, 1001])
+@pytest.mark.parametrize("variant", [0, 1000])
 @pytest.mark.parametrize("n", [1, 1000, 3 * (1 << 20) + 7, 9 * (1 << 20)])
 def test_host_path(gpu, O, n, variant):
-    """hydra_reduce_host on pageable buffers: pinned for the call and streamed by the kernel
-    (default), or staged H2D -> kernel -> D2H over 8 MiB chunks (variant 1001)."""
+    """hydra_reduce_host on pageable buffers: copied by the CPU through the context's pinned
+    staging (never pinned for the call), 4 MiB per operand per round, double-buffered -- and the
+    same with everything forced through staging (variant 1000)."""
     a = synth.stress_f32(2, 0, n)
     b = synth.stress_f32(2, 1, n)
     ctx = HostContext(0)
@@ -269,14 +270,14 @@ def test_host_path(gpu, O, n, variant):
 
 
 @pytest.mark.parametrize("n", [1, 1000, 262144, 3 * (1 << 20) + 7])
-def test_host_path_zero_copy(gpu, O, n):
+def test_host_path_zero_copy(gpu, O, n, host_buf):
     """hydra_reduce_host on registered / pinned host memory takes the zero-copy path (the kernel
     streams the host ranges over PCIe): same bits as the oracle, interior pointers included,
     mixed pinned + pageable falls back to staging."""
     L = _lib.lib()
     pad = 3  # interior pointers: the ranges start 3 elements into the registered allocations
-    a = synth.stress_f32(2, 0, n + pad)
-    b = synth.stress_f32(2, 1, n + pad)
+    a = host_buf(n + pad, np.float32, synth.stress_f32(2, 0, n + pad))
+    b = host_buf(n + pad, np.float32, synth.stress_f32(2, 1, n + pad))
     exp = O.op(a[pad:], b[pad:], "sum", 6)
     ctx = HostContext(0)
     _lib.check(L.hydra_host_register(a.ctypes.data, a.nbytes))
@@ -461,8 +462,8 @@ def test_reduce_batch_argument_checks(dev):
 @pytest.mark.parametrize("n", [1, 4099, 262144, (9 << 20) + 3])
 @pytest.mark.parametrize("pinned", ["a", "b", "c", "ab", "ac", "bc"])
 @pytest.mark.parametrize("code", [6, 8])
-@pytest.mark.parametrize("variant", [0, 1001])
-def test_host_path_mixed_pinned(gpu, O, n, pinned, code, variant):
+@pytest.mark.parametrize("variant", [0, 1000])
+def test_host_path_mixed_pinned(gpu, O, n, pinned, code, variant, host_buf):
     """hydra_reduce_host with SOME operands registered: those are read / written by the kernel in
     place over PCIe, the pageable ones staged -- e.g. a registered bucket with the reference
     ring's pageable scratch (allreduce.cc:225) stages only b.  In place (c == a) and out of
@@ -479,10 +480,11 @@ def test_host_path_mixed_pinned(gpu, O, n, pinned, code, variant):
           else np.full(n, 3, np.float32))
     ctx = HostContext(0)
     regs = []
-    prev = L.hydra_set_variant(variant)  # 1001: the pageable operands staged, not pinned per call
+    prev = L.hydra_set_variant(variant)  # 1000: every operand staged, registered or not
     try:
         for inplace in (True, False):
-            ha, hb, hc = a.copy(), b.copy(), (None if inplace else c0.copy())
+            ha, hb = host_buf(n, a.dtype, a), host_buf(n, b.dtype, b)
+            hc = None if inplace else host_buf(n, c0.dtype, c0)
             tgt = {"a": ha, "b": hb, "c": ha if inplace else hc}
             for k in set(pinned):
                 arr = tgt[k]
