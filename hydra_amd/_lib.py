@@ -30,7 +30,7 @@ EXPORTS = [  # every symbol include/hydra_hip.h declares
     "hydra_reduce", "hydra_chunk_sum", "hydra_reduce_batch", "hydra_acc_bf16_f32", "hydra_f32_to_bf16",
     "hydra_set_variant", "hydra_ctx_create", "hydra_ctx_destroy", "hydra_reduce_host",
     "hydra_chunk_sum_host", "hydra_host_register", "hydra_host_unregister",
-    "hydra_page_interior", "hydra_host_mappings",
+    "hydra_page_interior", "hydra_host_mappings", "hydra_ctx_stats",
     "hydra_stream_create", "hydra_stream_destroy", "hydra_stream_synchronize", "hydra_malloc",
     "hydra_free", "hydra_memcpy", "hydra_ring_plan",
     "hydra_comm_get_unique_id", "hydra_comm_init", "hydra_comm_destroy", "hydra_comm_info", "hydra_allreduce",
@@ -149,6 +149,8 @@ def _declare(L) -> None:
     L.hydra_chunk_sum_host.argtypes = [vp, i, vp, vp, vp, sz]
     L.hydra_host_register.argtypes = [vp, sz]
     L.hydra_host_unregister.argtypes = [vp]
+    L.hydra_ctx_stats.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64),
+                                  ctypes.POINTER(ctypes.c_uint64)]
     L.hydra_page_interior.argtypes = [ctypes.c_uint64, sz, ctypes.POINTER(ctypes.c_uint64),
                                       ctypes.POINTER(ctypes.c_uint64)]
     L.hydra_page_interior.restype = None

@@ -1,0 +1,191 @@
+// resident.hip -- the resident reducer's kernel (see resident.h for the protocol).
+#include "resident.h"
+
+#include "reduce_kernels.h"
+#include "reduce_ops.h"
+
+namespace hydra {
+namespace {
+
+constexpr uint64_t kWorkerGraceTicks = 1000000000ull;  // 10 s of s_memrealtime (100 MHz)
+
+template <typename E, int OP>
+__device__ __forceinline__ void res_tile(const ResSeg& g, uint32_t tile, int t) {
+  if (tile == 0 && (g.head | g.tail)) {  // ragged edges, one element per lane (waves 0 and 1)
+    constexpr int N = Vec<E>::N;
+    E* c_ = reinterpret_cast<E*>(g.c);
+    const E* a_ = reinterpret_cast<const E*>(g.a);
+    const E* b_ = reinterpret_cast<const E*>(g.b);
+    const bool head = t < g.head, tail = t >= 64 && t - 64 < g.tail;
+    if (head || tail) {
+      const ptrdiff_t i = head ? (ptrdiff_t)t - g.head : (ptrdiff_t)(g.nvec * N) + (t - 64);
+      const E ea = a_[i], eb = b_[i];
+      const E ec = g.c_old ? c_[i] : ea;
+      c_[i] = Elem<E, OP>::apply(ea, eb, ec);
+    }
+  }
+  const size_t v = (size_t)tile * kBlock + t;
+  if (v < g.nvec) {
+    const size_t o = v * 16;
+    const u32x4 x = ld_u(g.a + o);
+    const u32x4 y = ld_u(g.b + o);
+    const u32x4 z = g.c_old ? ld_u(g.c + o) : x;
+    st_a(g.c + o, vapply<E, OP>(x, y, z));
+  }
+}
+
+template <typename E>
+__device__ __forceinline__ void res_op(int op, const ResSeg& g, uint32_t tile, int t) {
+  switch (op) {
+    case kSum: res_tile<E, kSum>(g, tile, t); break;
+    case kProduct: res_tile<E, kProduct>(g, tile, t); break;
+    case kMax: res_tile<E, kMax>(g, tile, t); break;
+    case kMin: res_tile<E, kMin>(g, tile, t); break;
+  }
+}
+
+__device__ __forceinline__ void res_dispatch(int op, int dtype, const ResSeg& g, uint32_t tile,
+                                             int t) {
+  switch (dtype) {
+    case kI8: res_op<int8_t>(op, g, tile, t); break;
+    case kU8: res_op<uint8_t>(op, g, tile, t); break;
+    case kI32: res_op<int32_t>(op, g, tile, t); break;
+    case kU32: res_op<uint32_t>(op, g, tile, t); break;
+    case kI64: res_op<int64_t>(op, g, tile, t); break;
+    case kU64: res_op<uint64_t>(op, g, tile, t); break;
+    case kF32: res_op<float>(op, g, tile, t); break;
+    case kF64: res_op<double>(op, g, tile, t); break;
+    case kF16: res_op<f16_t>(op, g, tile, t); break;
+    case kBF16: res_op<bf16_t>(op, g, tile, t); break;
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ T ld_sys(const T* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+template <typename T>
+__device__ __forceinline__ T ld_agent(const T* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+constexpr int kDescWords = (int)(sizeof(ResDesc) / 8);
+static_assert(sizeof(ResDesc) % 8 == 0 && kDescWords <= 2 * 64, "descriptor copy: 2 words/lane");
+
+__global__ __launch_bounds__(kBlock) void k_resident(ResHost* h, ResDev* d, uint64_t served,
+                                                     uint64_t gen, uint64_t idle_ticks) {
+  __shared__ uint64_t s_seq;
+  __shared__ int s_exit;
+  __shared__ ResDesc s_desc;
+  const int t = threadIdx.x;
+  uint64_t last = served;
+  for (;;) {
+    if (blockIdx.x == 0) {
+      if (t < 64) {  // wave 0: the doorbell (every lane loads the same word: one request)
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        uint64_t s = last;
+        int quit = 0;
+        for (;;) {
+          s = ld_sys(&h->doorbell);
+          if (s != last) break;
+          if (ld_sys(&h->quit) != 0u || __builtin_amdgcn_s_memrealtime() - t0 > idle_ticks) {
+            quit = 1;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(2);
+        }
+        if (!quit) {
+          // the descriptor was written before the doorbell: acquire, then copy it to the
+          // device (two words per lane, write-through) and publish the sequence number
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+          const uint64_t* src = reinterpret_cast<const uint64_t*>(&h->desc);
+          uint64_t* dst = reinterpret_cast<uint64_t*>(&d->desc);
+          uint64_t w0 = 0, w1 = 0;
+          if (t < kDescWords) w0 = src[t];
+          if (t + 64 < kDescWords) w1 = src[t + 64];
+          if (t < kDescWords) __hip_atomic_store(dst + t, w0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (t + 64 < kDescWords)
+            __hip_atomic_store(dst + t + 64, w1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          if (t == 0) __hip_atomic_store(&d->seq, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else if (t == 0) {
+          __hip_atomic_store(&d->exit_gen, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (t == 0) {
+          s_seq = s;
+          s_exit = quit;
+        }
+      }
+    } else if (t == 0) {  // the other workgroups: the device word workgroup 0 publishes
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      uint64_t s = last;
+      int quit = 0;
+      for (;;) {
+        s = ld_agent(&d->seq);
+        if (s != last) break;
+        if (ld_agent(&d->exit_gen) == gen) {
+          quit = 1;
+          break;
+        }
+        if (__builtin_amdgcn_s_memrealtime() - t0 > idle_ticks + kWorkerGraceTicks) {
+          __hip_atomic_store(&h->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          quit = 1;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+      s_seq = s;
+      s_exit = quit;
+    }
+    if (t == 0) {
+      // the descriptor (device, agent) and the operands / staging the host wrote (system)
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    if (s_exit) break;
+    const uint64_t s = s_seq;
+    {
+      const uint64_t* src = reinterpret_cast<const uint64_t*>(&d->desc);
+      uint64_t* dst = reinterpret_cast<uint64_t*>(&s_desc);
+      for (int k = t; k < kDescWords; k += kBlock) dst[k] = ld_agent(src + k);
+    }
+    __syncthreads();
+    const int count = s_desc.count;
+    for (uint32_t tile = blockIdx.x; tile < s_desc.tiles; tile += gridDim.x) {
+      int k = 0;  // the last segment whose first tile is <= this tile (uniform)
+      for (int j = 1; j < count; j++)
+        if (s_desc.s[j].tile0 <= tile) k = j;
+      res_dispatch(s_desc.op, s_desc.dtype, s_desc.s[k], tile - s_desc.s[k].tile0, t);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // this workgroup's stores reach the host
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const uint32_t old =
+          __hip_atomic_fetch_add(&d->arrive, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+      if (old == gridDim.x - 1) {
+        __hip_atomic_store(&d->arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&h->done, s, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+    last = s;
+    __syncthreads();  // s_seq / s_desc are rewritten next round
+  }
+  if (blockIdx.x == 0 && t == 0)
+    __hip_atomic_store(&h->alive, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+}  // namespace
+
+hipError_t launch_resident(ResHost* h, ResDev* d, uint64_t served, uint64_t gen,
+                           uint64_t idle_ticks, hipStream_t s) {
+  hipLaunchKernelGGL(k_resident, dim3(kResidentBlocks), dim3(kBlock), 0, s, h, d, served, gen,
+                     idle_ticks);
+  return hipGetLastError();
+}
+
+}  // namespace hydra

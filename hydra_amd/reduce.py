@@ -98,7 +98,8 @@ def f32_to_bf16_(out_bf16, acc, stream: int | None = None) -> None:
 
 # --------------------------------------------------------------------------- host buffers
 class HostContext:
-    """One staging context (two HIP streams + device chunks) per calling thread."""
+    """One host-call context per calling thread (hydra_ctx_t): pinned staging, a stream, and the
+    resident reducer that serves small synchronous calls without a launch."""
 
     def __init__(self, device: int = 0):
         h = ctypes.c_void_p()
@@ -108,6 +109,12 @@ class HostContext:
     @property
     def handle(self) -> int:
         return self._h.value
+
+    def stats(self) -> dict:
+        """Calls the resident reducer served and instances launched (hydra_ctx_stats)."""
+        calls, launches = ctypes.c_uint64(), ctypes.c_uint64()
+        check(_lib.lib().hydra_ctx_stats(self._h, ctypes.byref(calls), ctypes.byref(launches)))
+        return {"resident_calls": calls.value, "resident_launches": launches.value}
 
     def close(self) -> None:
         if self._h:

@@ -140,6 +140,13 @@ int hydra_reduce_host(hydra_ctx_t ctx, int op, int dtype, void* c, const void* a
                       size_t n);
 int hydra_chunk_sum_host(hydra_ctx_t ctx, int dtype, void* c, const void* a, const void* b,
                          size_t n);
+/* Low latency: a call whose staged bytes fit one round (4 MiB per operand) and that has at most
+ * 16 segments is served by the context's RESIDENT reducer -- one launch of 32 workgroups kept on
+ * a private stream while calls keep coming, woken by a host-mapped doorbell instead of a fresh
+ * dispatch; it leaves after HYDRA_RESIDENT_IDLE_US (default 2000) without a call, at
+ * hydra_ctx_destroy and at process exit.  HYDRA_RESIDENT=0 turns it off.  Stats (tests):
+ * calls served by it and instances launched. */
+int hydra_ctx_stats(hydra_ctx_t ctx, uint64_t* resident_calls, uint64_t* resident_launches);
 /* Which host memory the kernel reads / writes in place (zero-copy over PCIe), per operand: a
  * range registered with hydra_host_register, a pinned block from hydra_malloc_host, or memory
  * the caller pinned / registered itself (hipHostMalloc, hipHostRegister, torch pinned tensors;

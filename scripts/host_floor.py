@@ -12,7 +12,8 @@ Modes (operands c == a, b, as the ring passes them):
   registered_staged the registered operands with everything forced through staging (1000)
 and, for reference, the device-resident launch + synchronise floor (hydra_reduce on device
 buffers followed by hydra_stream_synchronize) and one Zen core's gloo::sum<float>.
-Median and p10 of individually timed calls.  Prints one JSON document.
+Median and p10 of individually timed calls.  Prints one JSON document.  Run it with
+HYDRA_RESIDENT=0 as well: the same calls as one batched launch each (no resident reducer).
 Usage (GPU box): python scripts/host_floor.py > out.json
 """
 import ctypes
@@ -104,13 +105,16 @@ def main():
                                  "us_median": round(per * 1e6, 3)})
             except Exception as e:  # noqa: BLE001
                 rows.append({"elements": n, "mode": "reference", "error": str(e)})
+        ctx_stats = ctx.stats()
     finally:
         L.hydra_host_unregister(ra.ctypes.data)
         L.hydra_host_unregister(rb.ctypes.data)
         L.hydra_free_host(pa)
         L.hydra_free_host(pb)
         ctx.close()
-    print(json.dumps({"probe": "scripts/host_floor.py", "rows": rows}))
+    print(json.dumps({"probe": "scripts/host_floor.py",
+                      "resident": os.environ.get("HYDRA_RESIDENT", "1") != "0",
+                      "stats": ctx_stats, "rows": rows}))
 
 
 if __name__ == "__main__":

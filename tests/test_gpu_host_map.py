@@ -92,7 +92,7 @@ def test_pageable_operands_are_never_registered(ctx, O, n, offs):
     not move), and the result is bit-exact."""
     L = _lib.lib()
     live0, regs0 = live_registrations()
-    bufs = [np.empty(n + 8, np.float32) for _ in offs]
+    bufs = [np.empty(n + o // 4 + 16, np.float32) for o in offs]
     c, a, b = (buf.view(np.uint8)[o:o + 4 * n].view(np.float32) for buf, o in zip(bufs, offs))
     x, y = synth.stress_f32(2, 0, n), synth.stress_f32(2, 1, n)
     exp = O.op(x, y, "sum", 6)

@@ -1,0 +1,147 @@
+"""The resident reducer (hydra_amd/csrc/resident.h): hydra_reduce_host's low-latency form for
+the reference ring's synchronous per-segment Func (allreduce.cc:301-305).  Bit-exact against the
+reference's own outputs (golden fixtures: every Gloo dtype x {sum, product, max, min}) and the
+oracle, through every lifecycle edge: back-to-back calls on one instance, idle gaps long enough
+for an instance to leave (the next call launches a new one), two contexts at once, a context
+destroyed with its instance running, and HYDRA_RESIDENT=0."""
+import os
+import subprocess
+import sys
+import threading
+import time
+
+import numpy as np
+import pytest
+
+from hydra_amd import _lib, synth
+from hydra_amd.reduce import HostContext
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+TYPES = [("i8", 0, np.int8), ("u8", 1, np.uint8), ("i32", 2, np.int32), ("u32", 3, np.uint32),
+         ("i64", 4, np.int64), ("u64", 5, np.uint64), ("f32", 6, np.float32),
+         ("f64", 7, np.float64), ("f16", 8, np.uint16)]
+OPC = {"sum": 0, "product": 1, "max": 2, "min": 3}
+
+
+def bits(x):
+    return np.ascontiguousarray(x).view(f"u{x.itemsize}")
+
+
+@pytest.fixture
+def ctx(gpu):
+    c = HostContext(0)
+    yield c
+    c.close()
+
+
+@pytest.mark.parametrize("name,code,dt", TYPES)
+def test_resident_golden_ops(ctx, golden, name, code, dt):
+    """The reference's own sum/product/max/min<T> outputs (tests/golden, incl. inf/NaN/-0/
+    subnormal/overflow), in place c == a as the ring calls it, every one served resident."""
+    L = _lib.lib()
+    s0 = ctx.stats()
+    for kind in OPC:
+        if name == "i32" and kind == "product":
+            a, b = golden[f"ops_{name}_pa"], golden[f"ops_{name}_pb"]
+        else:
+            a, b = golden[f"ops_{name}_a"], golden[f"ops_{name}_b"]
+        exp = golden[f"ops_{name}_{kind}"]
+        c = np.ascontiguousarray(a.copy())
+        _lib.check(L.hydra_reduce_host(ctx.handle, OPC[kind], code, c.ctypes.data, c.ctypes.data,
+                                       np.ascontiguousarray(b).ctypes.data, a.size))
+        assert np.array_equal(bits(c), bits(exp)), (name, kind)
+    s1 = ctx.stats()
+    assert s1["resident_calls"] > s0["resident_calls"], (s0, s1)
+
+
+def test_resident_back_to_back_and_idle_gaps(ctx, O):
+    """200 synchronous calls of ragged sizes on pageable buffers, with gaps of 0, 1 and 6 ms
+    (past the 2 ms idle limit: the instance leaves and the next call starts a new one) --
+    every result bit-exact; more than one instance was launched, far fewer than calls."""
+    L = _lib.lib()
+    rng = np.random.default_rng(5)
+    for i in range(200):
+        n = int(rng.integers(1, 70000))
+        a = synth.stress_f32(2, 0, n, seed=i)
+        b = synth.stress_f32(2, 1, n, seed=i)
+        exp = O.op(a, b, "sum", 6)
+        _lib.check(L.hydra_reduce_host(ctx.handle, 0, 6, a.ctypes.data, a.ctypes.data,
+                                       b.ctypes.data, n))
+        assert np.array_equal(bits(a), bits(exp)), (i, n)
+        if i % 50 == 49:
+            time.sleep(0.006)
+        elif i % 10 == 9:
+            time.sleep(0.001)
+    st = ctx.stats()
+    assert st["resident_calls"] == 200, st
+    assert 2 <= st["resident_launches"] < 60, st
+
+
+def test_resident_two_contexts_concurrently(gpu, O):
+    """Two threads, one context (and one resident instance) each -- the two rails of
+    bew_allreduce_a (pipeallreduce-a.cc:32-50) -- 300 calls each, every result exact."""
+    L = _lib.lib()
+    errs = []
+
+    def rail(r):
+        c = HostContext(0)
+        try:
+            for i in range(300):
+                n = 1000 + 37 * i + r
+                a = synth.stress_f32(3, r, n, seed=i)
+                b = synth.stress_f32(3, r + 1, n, seed=i)
+                exp = O.op(a, b, "sum", 6)
+                rc = L.hydra_reduce_host(c.handle, 0, 6, a.ctypes.data, a.ctypes.data,
+                                         b.ctypes.data, n)
+                if rc or not np.array_equal(bits(a), bits(exp)):
+                    errs.append((r, i, rc))
+                    return
+        finally:
+            c.close()
+
+    ts = [threading.Thread(target=rail, args=(r,)) for r in range(2)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errs, errs
+
+
+def test_resident_destroy_while_running(gpu, O):
+    """A context destroyed right after a call (its instance still waiting for the next one)
+    tells it to leave; a new context works at once."""
+    L = _lib.lib()
+    for k in range(5):
+        c = HostContext(0)
+        n = 4099 + k
+        a, b = synth.stress_f32(2, 0, n), synth.stress_f32(2, 1, n)
+        exp = O.op(a, b, "sum", 6)
+        _lib.check(L.hydra_reduce_host(c.handle, 0, 6, a.ctypes.data, a.ctypes.data,
+                                       b.ctypes.data, n))
+        c.close()
+        assert np.array_equal(bits(a), bits(exp))
+    _lib.check(L.hydra_device_check(0))
+
+
+def test_resident_off_by_environment(gpu):
+    """HYDRA_RESIDENT=0: every call is one batched launch on the context's stream; same bits."""
+    code = (
+        "import sys, numpy as np; sys.path.insert(0, %r)\n"
+        "import torch\n"
+        "from hydra_amd import _lib, synth\n"
+        "from hydra_amd.reduce import HostContext\n"
+        "from oracle import oracle as O\n"
+        "c = HostContext(0); L = _lib.lib()\n"
+        "for n in (1, 1000, 262145):\n"
+        "    a, b = synth.stress_f32(2, 0, n), synth.stress_f32(2, 1, n)\n"
+        "    e = O.op(a, b, 'sum', 6)\n"
+        "    _lib.check(L.hydra_reduce_host(c.handle, 0, 6, a.ctypes.data, a.ctypes.data,"
+        " b.ctypes.data, n))\n"
+        "    assert np.array_equal(a.view(np.uint32), e.view(np.uint32)), n\n"
+        "assert c.stats()['resident_calls'] == 0, c.stats()\n"
+        "c.close(); print('ok')\n" % ROOT)
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120,
+                       env=dict(os.environ, HYDRA_RESIDENT="0"))
+    assert p.returncode == 0 and "ok" in p.stdout, (p.stdout, p.stderr[-2000:])
