@@ -130,12 +130,17 @@ class Pair {
   }
   void close() { abort("Connection closed"); }
   // Fail every pending operation with `e`, refuse new ones, shut the socket and join both
-  // threads: when this returns no transport thread touches any operation's memory again.
+  // threads: when this returns no transport thread touches any operation's memory again -- for
+  // EVERY caller: a second, concurrent abort (two timed-out waits, a timeout racing
+  // closeConnections) waits until the first one has joined both threads.
   void abort(const std::string& e) {
     fail(e);
     {
-      std::lock_guard<std::mutex> g(mu_);
-      if (closed_) return;
+      std::unique_lock<std::mutex> l(mu_);
+      if (closed_) {
+        cv_.wait(l, [&] { return joined_; });
+        return;
+      }
       closed_ = true;
       cv_.notify_all();
     }
@@ -143,6 +148,9 @@ class Pair {
     if (writer_.joinable()) writer_.join();
     if (reader_.joinable()) reader_.join();
     ::close(fd_);
+    std::lock_guard<std::mutex> g(mu_);
+    joined_ = true;
+    cv_.notify_all();
   }
 
  private:
@@ -258,6 +266,7 @@ class Pair {
   std::condition_variable cv_;
   std::deque<std::shared_ptr<UnboundBuffer::Op>> sendq_, recvq_;
   bool closed_ = false;
+  bool joined_ = false;  // both threads joined and the socket closed (abort() finished)
   std::string error_;
   std::thread writer_, reader_;
 };

@@ -192,8 +192,51 @@ static int run_reduce(int P, size_t n, bool inplace) {
   return 0;
 }
 
+// Concurrent aborts of the same pairs (round 2 advisor: a second abort() must not return before
+// the first has joined the pair's threads): three threads per rank call signalException /
+// closeConnections at once after an allreduce; every call returns, nothing races.
+static int run_concurrent_abort(int P) {
+  hydra::HashStore store;
+  std::vector<std::thread> th;
+  std::vector<int> bad(P, 0);
+  for (int r = 0; r < P; r++) {
+    th.emplace_back([&, r] {
+      try {
+        auto c = std::make_shared<hydra::Context>(r, P);
+        c->connectFullMesh(store, "127.0.0.1", "abort");
+        std::vector<uint64_t> x(4096, (uint64_t)r);
+        hydra::AllreduceOptions o(c);
+        o.setOutput(x.data(), x.size());
+        o.setReduceFunction(&sum_u64);
+        hydra::allreduce(o);
+        std::vector<std::thread> q;
+        for (int k = 0; k < 3; k++)
+          q.emplace_back([&, k] {
+            if (k == 1)
+              c->closeConnections();
+            else
+              c->signalException("concurrent abort " + std::to_string(k));
+          });
+        for (auto& t : q) t.join();
+      } catch (const std::exception& e) {
+        std::fprintf(stderr, "rank %d: %s\n", r, e.what());
+        bad[r] = 1;
+      }
+    });
+  }
+  for (auto& t : th) t.join();
+  for (int b : bad)
+    if (b) return 1;
+  return 0;
+}
+
 int main() {
   int fails = 0;
+  for (int P : {2, 3})
+    if (run_concurrent_abort(P)) {
+      std::fprintf(stderr, "FAIL concurrent abort P=%d\n", P);
+      fails++;
+    }
   for (int P : {1, 2, 3, 4})
     for (bool inplace : {true, false})
       for (size_t n : {(size_t)1, (size_t)1000, (size_t)20011})
