@@ -72,10 +72,24 @@ __device__ __forceinline__ T ld_agent(const T* p) {
 constexpr int kDescWords = (int)(sizeof(ResDesc) / 8);
 static_assert(sizeof(ResDesc) % 8 == 0 && kDescWords <= 2 * 64, "descriptor copy: 2 words/lane");
 
+// A call of at most kSoloTiles tiles (16 KiB of c) is served by workgroup 0 alone: no device
+// hop to the other workgroups, no arrival counter -- the reference ring's small segments.
+constexpr uint32_t kSoloTiles = 4;
+
+__device__ __forceinline__ void res_tiles(const ResDesc& D, uint32_t first, uint32_t stride,
+                                          int t) {
+  for (uint32_t tile = first; tile < D.tiles; tile += stride) {
+    int k = 0;  // the last segment whose first tile is <= this tile (uniform)
+    for (int j = 1; j < D.count; j++)
+      if (D.s[j].tile0 <= tile) k = j;
+    res_dispatch(D.op, D.dtype, D.s[k], tile - D.s[k].tile0, t);
+  }
+}
+
 __global__ __launch_bounds__(kBlock) void k_resident(ResHost* h, ResDev* d, uint64_t served,
                                                      uint64_t gen, uint64_t idle_ticks) {
   __shared__ uint64_t s_seq;
-  __shared__ int s_exit;
+  __shared__ int s_mode;  // 0 all workgroups, 1 workgroup 0 alone, 2 leave
   __shared__ ResDesc s_desc;
   const int t = threadIdx.x;
   uint64_t last = served;
@@ -84,60 +98,70 @@ __global__ __launch_bounds__(kBlock) void k_resident(ResHost* h, ResDev* d, uint
       if (t < 64) {  // wave 0: the doorbell (every lane loads the same word: one request)
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         uint64_t s = last;
-        int quit = 0;
+        int mode = 0;
         for (;;) {
           s = ld_sys(&h->doorbell);
           if (s != last) break;
           if (ld_sys(&h->quit) != 0u || __builtin_amdgcn_s_memrealtime() - t0 > idle_ticks) {
-            quit = 1;
+            mode = 2;
             break;
           }
-          __builtin_amdgcn_s_sleep(2);
+          __builtin_amdgcn_s_sleep(1);
         }
-        if (!quit) {
-          // the descriptor was written before the doorbell: acquire, then copy it to the
-          // device (two words per lane, write-through) and publish the sequence number
+        if (mode != 2) {
+          // the descriptor was written before the doorbell: acquire, then read it (two words
+          // per lane, one host round trip)
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
           const uint64_t* src = reinterpret_cast<const uint64_t*>(&h->desc);
-          uint64_t* dst = reinterpret_cast<uint64_t*>(&d->desc);
           uint64_t w0 = 0, w1 = 0;
           if (t < kDescWords) w0 = src[t];
           if (t + 64 < kDescWords) w1 = src[t + 64];
-          if (t < kDescWords) __hip_atomic_store(dst + t, w0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if (t + 64 < kDescWords)
-            __hip_atomic_store(dst + t + 64, w1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          if (t == 0) __hip_atomic_store(&d->seq, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          // word 1 holds {count, tiles}: a small call stays in this workgroup
+          const uint32_t tiles = (uint32_t)(__shfl((unsigned long long)w0, 1) >> 32);
+          if (tiles <= kSoloTiles) {
+            uint64_t* dst = reinterpret_cast<uint64_t*>(&s_desc);
+            if (t < kDescWords) dst[t] = w0;
+            if (t + 64 < kDescWords) dst[t + 64] = w1;
+            mode = 1;
+          } else {  // to the device, write-through, then publish the sequence number
+            uint64_t* dst = reinterpret_cast<uint64_t*>(&d->desc);
+            if (t < kDescWords)
+              __hip_atomic_store(dst + t, w0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (t + 64 < kDescWords)
+              __hip_atomic_store(dst + t + 64, w1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (t == 0) __hip_atomic_store(&d->seq, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
         } else if (t == 0) {
           __hip_atomic_store(&d->exit_gen, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         if (t == 0) {
           s_seq = s;
-          s_exit = quit;
+          s_mode = mode;
         }
       }
     } else if (t == 0) {  // the other workgroups: the device word workgroup 0 publishes
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
       uint64_t s = last;
-      int quit = 0;
+      int mode = 0;
       for (;;) {
         s = ld_agent(&d->seq);
         if (s != last) break;
         if (ld_agent(&d->exit_gen) == gen) {
-          quit = 1;
+          mode = 2;
           break;
         }
         if (__builtin_amdgcn_s_memrealtime() - t0 > idle_ticks + kWorkerGraceTicks) {
           __hip_atomic_store(&h->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          quit = 1;
+          mode = 2;
           break;
         }
         __builtin_amdgcn_s_sleep(2);
       }
       s_seq = s;
-      s_exit = quit;
+      s_mode = mode;
     }
     if (t == 0) {
       // the descriptor (device, agent) and the operands / staging the host wrote (system)
@@ -145,21 +169,29 @@ __global__ __launch_bounds__(kBlock) void k_resident(ResHost* h, ResDev* d, uint
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
-    if (s_exit) break;
+    const int mode = s_mode;
+    if (mode == 2) break;
     const uint64_t s = s_seq;
+    if (mode == 1) {  // workgroup 0 alone: every tile here, then the completion word
+      res_tiles(s_desc, 0, 1, t);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (t == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(&h->done, s, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      last = s;
+      __syncthreads();
+      continue;
+    }
     {
       const uint64_t* src = reinterpret_cast<const uint64_t*>(&d->desc);
       uint64_t* dst = reinterpret_cast<uint64_t*>(&s_desc);
       for (int k = t; k < kDescWords; k += kBlock) dst[k] = ld_agent(src + k);
     }
     __syncthreads();
-    const int count = s_desc.count;
-    for (uint32_t tile = blockIdx.x; tile < s_desc.tiles; tile += gridDim.x) {
-      int k = 0;  // the last segment whose first tile is <= this tile (uniform)
-      for (int j = 1; j < count; j++)
-        if (s_desc.s[j].tile0 <= tile) k = j;
-      res_dispatch(s_desc.op, s_desc.dtype, s_desc.s[k], tile - s_desc.s[k].tile0, t);
-    }
+    res_tiles(s_desc, blockIdx.x, gridDim.x, t);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (t == 0) {
