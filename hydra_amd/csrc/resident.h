@@ -60,7 +60,7 @@ struct alignas(64) ResHost {  // host-mapped (pinned), written by the host unles
 };
 
 struct alignas(64) ResDev {  // device memory, zeroed at creation
-  uint64_t seq;
+  uint64_t seq;  // the last multi-workgroup call published: (generation << 40) | sequence
   uint64_t exit_gen;
   uint32_t pad0[12];
   alignas(64) uint32_t arrive;

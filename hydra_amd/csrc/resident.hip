@@ -9,6 +9,16 @@ namespace {
 
 constexpr uint64_t kWorkerGraceTicks = 1000000000ull;  // 10 s of s_memrealtime (100 MHz)
 
+// The device word workgroup 0 publishes a multi-workgroup call in: the instance's generation in
+// the top 24 bits, the call's sequence number below.  A word another instance left behind (its
+// generation differs) never wakes this one's workers -- solo calls (kSoloTiles) do not
+// publish, so the word can lag the sequence number across instances.
+constexpr int kPubShift = 40;
+constexpr uint64_t kSeqMask = (uint64_t(1) << kPubShift) - 1;
+__device__ __forceinline__ uint64_t pub_word(uint64_t gen, uint64_t seq) {
+  return (gen << kPubShift) | (seq & kSeqMask);
+}
+
 template <typename E, int OP>
 __device__ __forceinline__ void res_tile(const ResSeg& g, uint32_t tile, int t) {
   if (tile == 0 && (g.head | g.tail)) {  // ragged edges, one element per lane (waves 0 and 1)
@@ -132,7 +142,9 @@ __global__ __launch_bounds__(kBlock) void k_resident(ResHost* h, ResDev* d, uint
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (t == 0) __hip_atomic_store(&d->seq, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (t == 0)
+              __hip_atomic_store(&d->seq, pub_word(gen, s), __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
           }
         } else if (t == 0) {
           __hip_atomic_store(&d->exit_gen, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -144,11 +156,15 @@ __global__ __launch_bounds__(kBlock) void k_resident(ResHost* h, ResDev* d, uint
       }
     } else if (t == 0) {  // the other workgroups: the device word workgroup 0 publishes
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      const uint64_t mine = pub_word(gen, last);
       uint64_t s = last;
       int mode = 0;
       for (;;) {
-        s = ld_agent(&d->seq);
-        if (s != last) break;
+        const uint64_t p = ld_agent(&d->seq);
+        if (p != mine && (p >> kPubShift) == (gen & ((uint64_t(1) << (64 - kPubShift)) - 1))) {
+          s = p & kSeqMask;
+          break;
+        }
         if (ld_agent(&d->exit_gen) == gen) {
           mode = 2;
           break;

@@ -145,3 +145,34 @@ def test_resident_off_by_environment(gpu):
     p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120,
                        env=dict(os.environ, HYDRA_RESIDENT="0"))
     assert p.returncode == 0 and "ok" in p.stdout, (p.stdout, p.stderr[-2000:])
+
+
+def test_resident_solo_and_spread_calls_across_instances(ctx, O, host_buf):
+    """Small calls (<= 4 tiles: workgroup 0 alone, nothing published to the others) and larger
+    ones (every workgroup) interleaved across instance restarts (idle gaps): a worker of a new
+    instance must never take the publication an earlier instance left behind for a new call
+    -- it would redo that old call on its old pointers.  The old call's output buffer is
+    registered (kept mapped) and refilled with a canary afterwards: it must stay untouched."""
+    L = _lib.lib()
+    big = 40000  # 10 tiles: every workgroup
+    old_c = host_buf(big, np.float32, 0)
+    _lib.check(L.hydra_host_register(old_c.ctypes.data, old_c.nbytes))
+    try:
+        a0, b0 = synth.stress_f32(2, 0, big), synth.stress_f32(2, 1, big)
+        _lib.check(L.hydra_reduce_host(ctx.handle, 0, 6, old_c.ctypes.data, a0.ctypes.data,
+                                       b0.ctypes.data, big))
+        assert np.array_equal(bits(old_c), bits(O.op(a0, b0, "sum", 6)))
+        old_c[:] = np.float32(-7.0)  # canary
+        for rnd in range(4):
+            time.sleep(0.006)  # past the idle limit: the next call starts a new instance
+            for i, n in enumerate((100, 3000, 4096, 50000, 17, 70001)):
+                a = synth.stress_f32(2, 0, n, seed=rnd * 10 + i)
+                b = synth.stress_f32(2, 1, n, seed=rnd * 10 + i)
+                exp = O.op(a, b, "sum", 6)
+                _lib.check(L.hydra_reduce_host(ctx.handle, 0, 6, a.ctypes.data, a.ctypes.data,
+                                               b.ctypes.data, n))
+                assert np.array_equal(bits(a), bits(exp)), (rnd, n)
+        _lib.check(L.hydra_device_check(0))
+        assert (old_c == np.float32(-7.0)).all(), "an old call was redone on its old output"
+    finally:
+        _lib.check(L.hydra_host_unregister(old_c.ctypes.data))

@@ -380,3 +380,18 @@ def test_plan_bounds_check_covers_reduce_root():
             for root in range(P):
                 for r in range(P):
                     ring.plan_reduce(root, P, r, n, 4, 128, 1024)
+
+
+def test_auto_is_a2a_on_equal_blocks_and_default_chunk_is_16mib():
+    """HYDRA_ALGO_AUTO resolves to A2A (three launches: ncclAllToAll, one fold, ncclAllGather)
+    when the reference geometry gives P equal blocks, else DIRECT; the default pipelining chunk
+    is 16 MiB, which keeps config 4's DIRECT enqueue at 62 plan ops."""
+    kinds = lambda ops: {o["kind"] for o in ops}  # noqa: E731
+    ops, _ = ring.plan("auto", 8, 0, 64 << 20, 4, 0, 0)
+    assert kinds(ops) == {_lib.OP_ALLTOALL, _lib.OP_FOLD, _lib.OP_ALLGATHER}, kinds(ops)
+    ops3, _ = ring.plan("auto", 3, 0, 1 << 20, 4, 0, 0)  # 1 Mi fp32 at P=3: unequal blocks
+    assert _lib.OP_ALLTOALL not in kinds(ops3) and _lib.OP_SEND in kinds(ops3)
+    d_default, _ = ring.plan("direct", 8, 0, 64 << 20, 4, 0, 0)
+    d16, _ = ring.plan("direct", 8, 0, 64 << 20, 4, 0, 16 << 20)
+    d4, _ = ring.plan("direct", 8, 0, 64 << 20, 4, 0, 4 << 20)
+    assert len(d_default) == len(d16) == 62 and len(d4) == 248, (len(d_default), len(d4))
