@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <mutex>
 #include <string>
@@ -90,14 +91,8 @@ struct hydra_ctx {
   hipEvent_t done[2] = {nullptr, nullptr};
   char* stage[2] = {nullptr, nullptr};      // host address
   char* stage_dev[2] = {nullptr, nullptr};  // its device address
-  // the resident reducer (resident.h): control block, device word, its own stream
-  hydra::ResHost* rh = nullptr;
-  hydra::ResHost* rh_dev = nullptr;
-  hydra::ResDev* rd = nullptr;
-  hipStream_t rstream = nullptr;
-  uint64_t rseq = 0;  // last doorbell rung (== last call served: calls are synchronous)
-  uint64_t rgen = 0;  // instances launched
-  bool rlaunched = false;
+  // a slot of the device's resident reducer (resident.h); null: off, or every slot leased
+  hydra::ResidentLease* lease = nullptr;
 };
 
 namespace {
@@ -106,130 +101,14 @@ constexpr int kVariantForceStaging = 1000;  // hydra_set_variant value: host pat
 
 void ctx_release(hydra_ctx* x) {
   if (x->stream) (void)hydra::release_stream(x->stream);
-  if (x->rstream) (void)hydra::release_stream(x->rstream);
   for (int i = 0; i < 2; i++) {
     if (x->done[i]) (void)hydra::release_event(x->done[i]);
     if (x->stage[i]) (void)hydra::cached_free_host(x->stage[i]);
   }
-  if (x->rh) (void)hydra::cached_free_host(x->rh);
-  if (x->rd) (void)hydra::cached_free(x->rd);
+  hydra::resident_release(x->lease);
+  x->lease = nullptr;
 }
 
-// Resident reducer settings: HYDRA_RESIDENT=0 turns it off (every call is one batched launch),
-// HYDRA_RESIDENT_IDLE_US (default 2000) is how long an instance waits for the next call.
-bool resident_enabled() {
-  static const bool on = [] {
-    const char* v = std::getenv("HYDRA_RESIDENT");
-    return !(v && v[0] == '0');
-  }();
-  return on;
-}
-uint64_t resident_idle_ticks() {  // s_memrealtime runs at 100 MHz
-  static const uint64_t t = [] {
-    const char* v = std::getenv("HYDRA_RESIDENT_IDLE_US");
-    const long us = v ? std::atol(v) : 2000;
-    return (uint64_t)std::max(50L, std::min(us, 1000000L)) * 100;
-  }();
-  return t;
-}
-
-// Contexts with a resident instance that may still be running: told to quit at exit, so the
-// grid has drained before the process ends.
-std::mutex g_res_mu;
-std::vector<hydra_ctx*>* g_res_ctx = nullptr;
-void resident_quit_all() {
-  std::lock_guard<std::mutex> g(g_res_mu);
-  if (!g_res_ctx) return;
-  for (hydra_ctx* x : *g_res_ctx)
-    if (x->rh) reinterpret_cast<volatile uint32_t&>(x->rh->quit) = 1u;
-  for (hydra_ctx* x : *g_res_ctx) {  // bounded: an instance leaves within microseconds
-    if (!x->rh) continue;
-    const auto t0 = std::chrono::steady_clock::now();
-    while (reinterpret_cast<volatile uint32_t&>(x->rh->alive) != 0u &&
-           std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(200))
-      std::this_thread::yield();
-  }
-}
-void resident_track(hydra_ctx* x, bool add) {
-  std::lock_guard<std::mutex> g(g_res_mu);
-  if (!g_res_ctx) {
-    g_res_ctx = new std::vector<hydra_ctx*>;
-    std::atexit(resident_quit_all);
-  }
-  auto it = std::find(g_res_ctx->begin(), g_res_ctx->end(), x);
-  if (add && it == g_res_ctx->end()) g_res_ctx->push_back(x);
-  if (!add && it != g_res_ctx->end()) g_res_ctx->erase(it);
-}
-
-// One synchronous call through the resident reducer: the descriptor, the doorbell, the wait.
-int resident_call(hydra_ctx* x, int op, int dtype, size_t es,
-                  const std::vector<hydra::BatchSegDesc>& segs) {
-  using hydra::ResSeg;
-  hydra::ResHost* h = x->rh;
-  hydra::ResDesc& D = h->desc;
-  const size_t N = 16 / es;
-  uint32_t tiles = 0;
-  int k = 0;
-  for (const hydra::BatchSegDesc& g : segs) {
-    if (g.n == 0) continue;
-    const uintptr_t cp = reinterpret_cast<uintptr_t>(g.c);
-    size_t head = ((16 - (cp & 15)) & 15) / es;
-    if (head > g.n) head = g.n;
-    const size_t nvec = (g.n - head) / N;
-    ResSeg& r = D.s[k++];
-    r.c = static_cast<char*>(g.c) + head * es;
-    r.a = static_cast<const char*>(g.a) + head * es;
-    r.b = static_cast<const char*>(g.b) + head * es;
-    r.nvec = nvec;
-    r.head = (int32_t)head;
-    r.tail = (int32_t)(g.n - head - nvec * N);
-    r.tile0 = tiles;
-    r.c_old = (dtype == HYDRA_FLOAT16 && g.c != g.a) ? 1u : 0u;
-    tiles += (uint32_t)std::max<size_t>(1, (nvec + hydra::kBlock - 1) / hydra::kBlock);
-  }
-  if (k == 0) return HYDRA_OK;
-  D.op = op;
-  D.dtype = dtype;
-  D.count = k;
-  D.tiles = tiles;
-  volatile uint32_t& alive = reinterpret_cast<volatile uint32_t&>(h->alive);
-  volatile uint64_t& done = reinterpret_cast<volatile uint64_t&>(h->done);
-  auto launch = [&]() -> int {  // a new instance, behind the last one on the same stream
-    alive = 1u;
-    std::atomic_thread_fence(std::memory_order_seq_cst);
-    const hipError_t e = hydra::launch_resident(x->rh_dev, x->rd, x->rseq - 1, ++x->rgen,
-                                                resident_idle_ticks(), x->rstream);
-    if (e != hipSuccess) return hip_fail(e, "resident reducer launch");
-    x->rlaunched = true;
-    return HYDRA_OK;
-  };
-  const uint64_t seq = ++x->rseq;
-  std::atomic_thread_fence(std::memory_order_release);  // the descriptor before the doorbell
-  reinterpret_cast<volatile uint64_t&>(h->doorbell) = seq;
-  if (!x->rlaunched || alive == 0u) {
-    if (int rc = launch()) return rc;
-    resident_track(x, true);
-  }
-  const auto t0 = std::chrono::steady_clock::now();
-  for (uint32_t spins = 0;; spins++) {
-    if (done >= seq) break;
-    if (alive == 0u && done < seq) {  // it left without seeing the doorbell: a new instance
-      if (int rc = launch()) return rc;
-      continue;
-    }
-    if ((spins & 1023) == 0) {
-      if (reinterpret_cast<volatile uint32_t&>(h->err))
-        return fail(HYDRA_ERR_HIP, "resident reducer: a workgroup gave up waiting");
-      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(20)) {
-        reinterpret_cast<volatile uint32_t&>(h->quit) = 1u;
-        return fail(HYDRA_ERR_TIMEOUT, "Timed out waiting 20000ms for the resident reducer");
-      }
-    }
-    __builtin_ia32_pause();
-  }
-  std::atomic_thread_fence(std::memory_order_acquire);  // the results after `done`
-  return HYDRA_OK;
-}
 }  // namespace
 
 extern "C" {
@@ -373,21 +252,15 @@ int hydra_ctx_create(int device, hydra_ctx_t* out) {
     if (e == hipSuccess) e = hipHostGetDevicePointer(&d, p, 0);
     x->stage_dev[i] = static_cast<char*>(d);
   }
-  if (e == hipSuccess && resident_enabled()) {
-    void* p = nullptr;
-    e = hydra::cached_malloc_host(sizeof(hydra::ResHost), &p);
-    x->rh = static_cast<hydra::ResHost*>(p);
-    void* d = nullptr;
-    if (e == hipSuccess) {
-      std::memset(p, 0, sizeof(hydra::ResHost));
-      e = hipHostGetDevicePointer(&d, p, 0);
-    }
-    x->rh_dev = static_cast<hydra::ResHost*>(d);
-    void* q = nullptr;
-    if (e == hipSuccess) e = hydra::cached_malloc(device, sizeof(hydra::ResDev), &q);
-    x->rd = static_cast<hydra::ResDev*>(q);
-    if (e == hipSuccess) e = hipMemset(q, 0, sizeof(hydra::ResDev));
-    if (e == hipSuccess) e = hydra::cached_stream(device, &x->rstream);
+  if (e != hipSuccess) {
+    ctx_release(x);
+    delete x;
+    return hip_fail(e, "hydra_ctx_create");
+  }
+  if (int rc = hydra::resident_lease(device, &x->lease)) {
+    ctx_release(x);
+    delete x;
+    return rc;
   }
   if (e != hipSuccess) {
     ctx_release(x);
@@ -401,11 +274,8 @@ int hydra_ctx_create(int device, hydra_ctx_t* out) {
 int hydra_ctx_destroy(hydra_ctx_t ctx) {
   if (!ctx) return ok();
   (void)hipSetDevice(ctx->device);
-  if (ctx->rlaunched) {  // tell the resident instance to leave, then wait for its stream
-    resident_track(ctx, false);
-    reinterpret_cast<volatile uint32_t&>(ctx->rh->quit) = 1u;
-    (void)hipStreamSynchronize(ctx->rstream);
-  }
+  // (its calls were synchronous: nothing of this context is left on the resident reducer,
+  // whose instance leaves by itself when idle)
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   ctx_release(ctx);
   delete ctx;
@@ -466,7 +336,6 @@ int hydra_reduce_host(hydra_ctx_t ctx, int op, int dtype, void* c, const void* a
   int rc = check_args(op, dtype, c, a, b, n);
   if (rc) return rc;
   if (n == 0) return ok();
-  HIP_TRY(hipSetDevice(ctx->device));
   const size_t es = hydra::dtype_size(dtype);
   const int variant = g_variant.load(std::memory_order_relaxed);
   const size_t nbytes = n * es;
@@ -485,13 +354,6 @@ int hydra_reduce_host(hydra_ctx_t ctx, int op, int dtype, void* c, const void* a
   Operand* A = a == c ? &oc : &oa;
   Operand* B = b == c ? &oc : b == a ? A : &ob;
   WindowsGuard guard_;
-  struct Drain {  // an early return drains the stream before the windows are released
-    hipStream_t st;
-    bool armed = true;
-    ~Drain() {
-      if (armed) (void)hipStreamSynchronize(st);
-    }
-  } drain_{ctx->stream};
   if (variant != kVariantForceStaging) {
     for (Operand* o : {&oc, A, B}) {
       bool seen = false;
@@ -514,35 +376,72 @@ int hydra_reduce_host(hydra_ctx_t ctx, int op, int dtype, void* c, const void* a
   cut.erase(std::unique(cut.begin(), cut.end()), cut.end());
 
   const bool c_old_bits = dtype == HYDRA_FLOAT16 && c != a && c != b;  // store quirk: read c
+  // Rounds: a round is one batched call over at most kResidentSegs intervals and one staging
+  // buffer's slots.  Round r is submitted once round r - 1 is done; its staged results go back
+  // to c while round r runs, and the CPU fills the other buffer meanwhile.  Submitted to the
+  // resident reducer when the context holds a slot, else launched on the context's stream.
+  hydra::ResidentLease* const lease = ctx->lease;
   std::vector<hydra::BatchSegDesc> segs;
+  segs.reserve(hydra::kResidentSegs);
   std::vector<CopyOut> outs[2];
   size_t used[3] = {0, 0, 0};  // bytes of the current buffer's a, b, c slots
   int buf = 0;
-  bool pending[2] = {false, false};
-  int rounds = 0;
-  // launch the current round on the stream, then make the other buffer reusable
-  auto flush = [&]() -> int {
-    if (segs.empty() && outs[buf].empty()) return HYDRA_OK;
-    rounds++;
-    hipError_t e = hydra::launch_reduce_batch(op, dtype, segs.data(), segs.size(), ctx->stream);
-    if (e != hipSuccess) return hip_fail(e, "batched reduce kernel launch (host)");
-    HIP_TRY(hipEventRecord(ctx->done[buf], ctx->stream));
-    pending[buf] = true;
-    segs.clear();
-    used[0] = used[1] = used[2] = 0;
-    buf ^= 1;
-    if (pending[buf]) {  // the round before: done, its staged results back to c
-      HIP_TRY(hipEventSynchronize(ctx->done[buf]));
-      for (const CopyOut& o : outs[buf]) std::memcpy(o.host, o.stage, o.bytes);
-      outs[buf].clear();
-      pending[buf] = false;
+  bool pending = false;  // the other buffer's round is in flight
+  auto wait_round = [&](int k) -> int {
+    if (lease) {
+      if (int r = hydra::resident_wait(lease)) return r;
+    } else {
+      HIP_TRY(hipEventSynchronize(ctx->done[k]));
     }
     return HYDRA_OK;
   };
+  struct Drain {  // an early return waits for the round in flight before the windows go
+    std::function<void()> f;
+    ~Drain() {
+      if (f) f();
+    }
+  } drain_;
+  auto flush = [&]() -> int {  // submit the current buffer's round
+    if (segs.empty() && outs[buf].empty()) return HYDRA_OK;
+    const int other = buf ^ 1;
+    if (pending) {
+      if (int r = wait_round(other)) return r;
+      pending = false;
+    }
+    if (!segs.empty()) {
+      if (lease) {
+        if (int r = hydra::resident_submit(lease, op, dtype, es, segs.data(), segs.size()))
+          return r;
+      } else {
+        hipError_t e =
+            hydra::launch_reduce_batch(op, dtype, segs.data(), segs.size(), ctx->stream);
+        if (e != hipSuccess) return hip_fail(e, "batched reduce kernel launch (host)");
+        HIP_TRY(hipEventRecord(ctx->done[buf], ctx->stream));
+      }
+      pending = true;
+      if (!drain_.f) {
+        drain_.f = lease ? std::function<void()>([lease] { (void)hydra::resident_wait(lease); })
+                         : std::function<void()>([st = ctx->stream] {
+                             (void)hipStreamSynchronize(st);
+                           });
+      }
+    }
+    // the previous round is done: its staged results back to c (overlapping this round)
+    for (const CopyOut& o : outs[other]) std::memcpy(o.host, o.stage, o.bytes);
+    outs[other].clear();
+    segs.clear();
+    used[0] = used[1] = used[2] = 0;
+    buf = other;
+    return HYDRA_OK;
+  };
+  if (!lease) HIP_TRY(hipSetDevice(ctx->device));
   for (size_t q = 0; q + 1 < cut.size(); q++) {
     size_t off = cut[q];
     const size_t end = cut[q + 1];
     while (off < end) {
+      if (segs.size() == (size_t)hydra::kResidentSegs) {
+        if ((rc = flush())) return rc;
+      }
       char* dc = oc.dev(off, end, es);
       char* da = A->dev(off, end, es);
       char* db = B->dev(off, end, es);
@@ -594,33 +493,20 @@ int hydra_reduce_host(hydra_ctx_t ctx, int op, int dtype, void* c, const void* a
       off += cnt;
     }
   }
-  if (rounds == 0 && ctx->rh && !segs.empty() && segs.size() <= (size_t)hydra::kResidentSegs) {
-    // one round: the resident reducer serves it (no launch, no stream wait)
-    if ((rc = resident_call(ctx, op, dtype, es, segs))) return rc;
-    for (const CopyOut& o : outs[buf]) std::memcpy(o.host, o.stage, o.bytes);
-    drain_.armed = false;
-    return ok();
-  }
   if ((rc = flush())) return rc;
-  for (int k = 0; k < 2; k++) {  // the last rounds: done, results back
-    if (!pending[buf]) {
-      buf ^= 1;
-      continue;
-    }
-    HIP_TRY(hipEventSynchronize(ctx->done[buf]));
-    for (const CopyOut& o : outs[buf]) std::memcpy(o.host, o.stage, o.bytes);
-    outs[buf].clear();
-    pending[buf] = false;
-    buf ^= 1;
+  if (pending) {  // the last round: done, results back
+    if ((rc = wait_round(buf ^ 1))) return rc;
+    pending = false;
+    for (const CopyOut& o : outs[buf ^ 1]) std::memcpy(o.host, o.stage, o.bytes);
   }
-  drain_.armed = false;
-  return ok();  // the windows are released here, after every kernel finished
+  drain_.f = nullptr;
+  return ok();  // the windows are released here, after every round finished
 }
 
 int hydra_ctx_stats(hydra_ctx_t ctx, uint64_t* resident_calls, uint64_t* resident_launches) {
   if (!ctx) return fail(HYDRA_ERR_INVALID, "null context");
-  if (resident_calls) *resident_calls = ctx->rseq;
-  if (resident_launches) *resident_launches = ctx->rgen;
+  if (resident_calls) *resident_calls = hydra::resident_calls(ctx->lease);
+  if (resident_launches) *resident_launches = hydra::resident_launches(ctx->device);
   return ok();
 }
 

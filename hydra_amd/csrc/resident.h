@@ -1,26 +1,30 @@
-// resident.h -- the resident reducer: a low-latency form of hydra_reduce_host's one batched
-// launch for the synchronous host Func (the reference ring calls it once per arriving segment,
+// resident.h -- the resident reducer: a low-latency form of hydra_reduce_host's batched launch
+// for the synchronous host Func (the reference ring calls it once per arriving segment,
 // allreduce.cc:301-305, and waits for it).
 //
 // A fresh launch costs a dispatch (~4 us of host enqueue, ~2-3 us until the first wave runs)
-// plus the completion wait: ~13 us per synchronous call however small.  The
-// resident reducer instead keeps kResidentBlocks workgroups of one launch alive on a private
-// stream while calls keep coming:
-//   * the host writes the call's descriptor (<= kResidentSegs segments, the same split as
-//     hydra_reduce_batch) into a host-mapped control block, then rings a doorbell (a sequence
-//     number);
-//   * wave 0 of workgroup 0 polls the doorbell (system-scope relaxed loads, s_sleep backoff),
-//     copies the descriptor into device memory and publishes the sequence number there; the
-//     other workgroups poll that device word (agent scope);
-//   * every workgroup does a system-scope acquire (the host wrote the operands / staging), sums
-//     its share of the tiles, releases its stores at system scope and arrives on a device
-//     counter; the last to arrive resets it and writes the sequence number into the host-mapped
-//     completion word, on which the host spins.
-// Exit: workgroup 0 publishes an exit generation when the doorbell has been idle for the idle
+// plus the completion wait: ~15 us per synchronous call however small.  The
+// resident reducer instead keeps kResidentBlocks workgroups of one launch alive while calls
+// keep coming.  ONE instance per device per process serves every host context:
+//   * each context leases a slot of the device's host-mapped control block; a call writes its
+//     descriptor (<= kResidentSegs segments, the same split as hydra_reduce_batch) into the
+//     slot, then rings the slot's doorbell (the slot's sequence number);
+//   * wave 0 of workgroup 0 polls every slot's doorbell at once (lane i loads slot i; system-
+//     scope relaxed loads, s_sleep backoff) and serves pending slots round robin;
+//   * a call of at most kSoloTiles tiles is summed by workgroup 0 alone; a larger one is copied
+//     to device memory and published as a job to every workgroup (a device word tagged with
+//     the instance's generation); each workgroup acquires at system scope, sums its share,
+//     releases at system scope and arrives on a device counter; the last to arrive writes the
+//     slot's completion word, on which the host spins;
+//   * the instance runs on a non-blocking stream of the greatest priority, whose hardware queue
+//     pool ordinary streams (torch's, RCCL's, hydra's own) do not use, so their work never
+//     queues behind the persistent grid (tests/test_gpu_resident.py times it).
+// Exit: workgroup 0 publishes an exit generation when every doorbell has been idle for the idle
 // limit (default 2 ms) or the host sets `quit`; every spin is bounded, so the grid always
 // drains.  The kernel clears `alive` (host-mapped) when it leaves; a host that rang while the
 // kernel was deciding to leave sees alive == 0 with its call not done and launches a new
-// instance on the same stream, which serves the pending doorbell (served < doorbell).
+// instance on the same stream, which serves the pending doorbells (each slot's done word says
+// what was served).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -28,10 +32,13 @@
 #include <cstddef>
 #include <cstdint>
 
+#include "reduce_kernels.h"
+
 namespace hydra {
 
 constexpr int kResidentSegs = 16;
 constexpr int kResidentBlocks = 32;
+constexpr int kResidentSlots = 32;  // contexts served at once per device (lanes of wave 0)
 
 struct ResSeg {  // one c = op(a, b): vector body + ragged head / tail, split on c (as the batch)
   char* c;       // at the vector body (16-B aligned)
@@ -49,26 +56,55 @@ struct ResDesc {
   ResSeg s[kResidentSegs];
 };
 
-struct alignas(64) ResHost {  // host-mapped (pinned), written by the host unless noted
-  uint64_t doorbell;  // the call's sequence number, written after desc
-  uint32_t quit;
-  uint32_t pad0[13];
+struct alignas(128) ResSlot {  // one context's channel (host-mapped)
+  uint64_t doorbell;           // host: the slot's sequence number, written after desc
+  uint32_t pad0[14];
+  ResDesc desc;                // host
+  alignas(64) uint64_t done;   // kernel: the slot's last finished sequence number
+};
+
+struct alignas(128) ResCtl {  // host-mapped (pinned), one per device
+  uint32_t quit;             // host: leave now
+  uint32_t pad0[15];
+  alignas(64) uint32_t alive;  // host sets it before a launch, the kernel clears it on leaving
+  uint32_t err;                // kernel: 1 = a wait inside the grid expired
+  alignas(128) ResSlot slot[kResidentSlots];
+};
+
+struct ResJob {  // a call spread over every workgroup (device memory)
+  uint64_t seq;
+  uint32_t slot, pad;
   ResDesc desc;
-  alignas(64) uint64_t done;  // written by the kernel: last finished sequence number
-  alignas(64) uint32_t alive;  // cleared by the kernel when it leaves
-  uint32_t err;                // set by the kernel: 1 = a worker's wait for workgroup 0 expired
 };
 
 struct alignas(64) ResDev {  // device memory, zeroed at creation
-  uint64_t seq;  // the last multi-workgroup call published: (generation << 40) | sequence
+  uint64_t pub;              // the last job published: (generation << 40) | job number
   uint64_t exit_gen;
-  uint32_t pad0[12];
   alignas(64) uint32_t arrive;
-  alignas(64) ResDesc desc;
+  alignas(64) uint64_t finished;  // the last job every workgroup finished (same tagging)
+  alignas(64) ResJob job;
 };
 
-// Launch one instance (generation `gen`, last served sequence number `served`) on `s`.
-hipError_t launch_resident(ResHost* h, ResDev* d, uint64_t served, uint64_t gen,
-                           uint64_t idle_ticks, hipStream_t s);
+// Launch one instance (generation `gen`) on `s`.
+hipError_t launch_resident(ResCtl* h, ResDev* d, uint64_t gen, uint64_t idle_ticks,
+                           hipStream_t s);
+
+// ---- host side (resident_host.cpp) -------------------------------------------------------
+// A context's slot on its device's resident reducer.  Calls through one lease are made by one
+// thread at a time and are synchronous per round: submit, then wait, then the next submit.
+struct ResidentLease;
+
+bool resident_enabled();  // HYDRA_RESIDENT != "0"
+// A slot of `device`'s reducer, or null when it is off or every slot is leased (the caller
+// then launches).  Errors (device setup) are returned as HYDRA codes with the message set.
+int resident_lease(int device, ResidentLease** out);
+void resident_release(ResidentLease* l);
+// Ring the slot with `count` (1..kResidentSegs) segments; makes sure an instance is running.
+int resident_submit(ResidentLease* l, int op, int dtype, size_t es, const BatchSegDesc* segs,
+                    size_t count);
+// Wait until the last submitted call is done (bounded: 20 s, then HYDRA_ERR_TIMEOUT).
+int resident_wait(ResidentLease* l);
+uint64_t resident_calls(const ResidentLease* l);  // calls this lease submitted
+uint64_t resident_launches(int device);            // instances launched on the device so far
 
 }  // namespace hydra

@@ -9,10 +9,9 @@ namespace {
 
 constexpr uint64_t kWorkerGraceTicks = 1000000000ull;  // 10 s of s_memrealtime (100 MHz)
 
-// The device word workgroup 0 publishes a multi-workgroup call in: the instance's generation in
-// the top 24 bits, the call's sequence number below.  A word another instance left behind (its
-// generation differs) never wakes this one's workers -- solo calls (kSoloTiles) do not
-// publish, so the word can lag the sequence number across instances.
+// The device word workgroup 0 publishes a job in: the instance's generation in the top 24 bits,
+// the job number below.  A word another instance left behind (its generation differs) never
+// wakes this one's workers.
 constexpr int kPubShift = 40;
 constexpr uint64_t kSeqMask = (uint64_t(1) << kPubShift) - 1;
 __device__ __forceinline__ uint64_t pub_word(uint64_t gen, uint64_t seq) {
@@ -96,22 +95,53 @@ __device__ __forceinline__ void res_tiles(const ResDesc& D, uint32_t first, uint
   }
 }
 
-__global__ __launch_bounds__(kBlock) void k_resident(ResHost* h, ResDev* d, uint64_t served,
-                                                     uint64_t gen, uint64_t idle_ticks) {
+// Workgroup 0 (wave 0) picks the next call: the first pending slot after the one served last.
+__device__ __forceinline__ int pick_slot(uint64_t pending, int last) {
+  const uint64_t after = pending & ~((uint64_t(2) << last) - 1);
+  return (int)__builtin_ctzll(after ? after : pending);
+}
+
+// Bounded agent-scope wait for every workgroup to finish job `want` (workgroup 0 reuses the
+// device job record only after that).  false: the wait expired (err set).
+__device__ __forceinline__ bool wait_finished(ResCtl* h, ResDev* d, uint64_t want) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  while (ld_agent(&d->finished) != want) {
+    if (__builtin_amdgcn_s_memrealtime() - t0 > kWorkerGraceTicks) {
+      __hip_atomic_store(&h->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  return true;
+}
+
+__global__ __launch_bounds__(kBlock) void k_resident(ResCtl* h, ResDev* d, uint64_t gen,
+                                                     uint64_t idle_ticks) {
   __shared__ uint64_t s_seq;
-  __shared__ int s_mode;  // 0 all workgroups, 1 workgroup 0 alone, 2 leave
+  __shared__ int s_slot;
+  __shared__ int s_mode;  // 0 every workgroup (a published job), 1 workgroup 0 alone, 2 leave
   __shared__ ResDesc s_desc;
   const int t = threadIdx.x;
-  uint64_t last = served;
+  const uint64_t gtag = gen & ((uint64_t(1) << (64 - kPubShift)) - 1);
+  uint64_t job = 0;  // the last job published (workgroup 0) / served (the others)
+  // workgroup 0, wave 0: lane i < kResidentSlots tracks slot i's last served sequence number
+  uint64_t served = 0;
+  int last_slot = kResidentSlots - 1;
+  if (blockIdx.x == 0 && t < kResidentSlots) served = ld_sys(&h->slot[t].done);
   for (;;) {
     if (blockIdx.x == 0) {
-      if (t < 64) {  // wave 0: the doorbell (every lane loads the same word: one request)
+      if (t < 64) {  // wave 0: every slot's doorbell in one load instruction
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        uint64_t s = last;
-        int mode = 0;
+        uint64_t s = 0;
+        int k = 0, mode = 0;
         for (;;) {
-          s = ld_sys(&h->doorbell);
-          if (s != last) break;
+          const uint64_t db = t < kResidentSlots ? ld_sys(&h->slot[t].doorbell) : 0;
+          const uint64_t pending = __ballot(t < kResidentSlots && db != served);
+          if (pending) {
+            k = pick_slot(pending, last_slot);
+            s = __shfl((unsigned long long)db, k);
+            break;
+          }
           if (ld_sys(&h->quit) != 0u || __builtin_amdgcn_s_memrealtime() - t0 > idle_ticks) {
             mode = 2;
             break;
@@ -119,10 +149,12 @@ __global__ __launch_bounds__(kBlock) void k_resident(ResHost* h, ResDev* d, uint
           __builtin_amdgcn_s_sleep(1);
         }
         if (mode != 2) {
+          if (t == k) served = s;
+          last_slot = k;
           // the descriptor was written before the doorbell: acquire, then read it (two words
           // per lane, one host round trip)
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-          const uint64_t* src = reinterpret_cast<const uint64_t*>(&h->desc);
+          const uint64_t* src = reinterpret_cast<const uint64_t*>(&h->slot[k].desc);
           uint64_t w0 = 0, w1 = 0;
           if (t < kDescWords) w0 = src[t];
           if (t + 64 < kDescWords) w1 = src[t + 64];
@@ -133,36 +165,48 @@ __global__ __launch_bounds__(kBlock) void k_resident(ResHost* h, ResDev* d, uint
             if (t < kDescWords) dst[t] = w0;
             if (t + 64 < kDescWords) dst[t + 64] = w1;
             mode = 1;
-          } else {  // to the device, write-through, then publish the sequence number
-            uint64_t* dst = reinterpret_cast<uint64_t*>(&d->desc);
+          } else if (job != 0 && !wait_finished(h, d, pub_word(gen, job))) {
+            mode = 2;  // a workgroup never finished the last job: leave (err is set)
+          } else {  // the job record, write-through, then publish it
+            uint64_t* dst = reinterpret_cast<uint64_t*>(&d->job.desc);
             if (t < kDescWords)
               __hip_atomic_store(dst + t, w0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (t + 64 < kDescWords)
               __hip_atomic_store(dst + t + 64, w1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (t == 0) {
+              __hip_atomic_store(&d->job.seq, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              __hip_atomic_store(&d->job.slot, (uint32_t)k, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+            }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            job++;
             if (t == 0)
-              __hip_atomic_store(&d->seq, pub_word(gen, s), __ATOMIC_RELAXED,
+              __hip_atomic_store(&d->pub, pub_word(gen, job), __ATOMIC_RELAXED,
                                  __HIP_MEMORY_SCOPE_AGENT);
           }
-        } else if (t == 0) {
-          __hip_atomic_store(&d->exit_gen, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+          // leave: once every workgroup finished the last job (so none is still to wake for
+          // it), publish the exit
+          if (job != 0) (void)wait_finished(h, d, pub_word(gen, job));
+          if (t == 0)
+            __hip_atomic_store(&d->exit_gen, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         if (t == 0) {
           s_seq = s;
+          s_slot = k;
           s_mode = mode;
         }
       }
-    } else if (t == 0) {  // the other workgroups: the device word workgroup 0 publishes
+    } else if (t == 0) {  // the other workgroups: the job word workgroup 0 publishes
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      const uint64_t mine = pub_word(gen, last);
-      uint64_t s = last;
+      const uint64_t mine = pub_word(gen, job);
       int mode = 0;
       for (;;) {
-        const uint64_t p = ld_agent(&d->seq);
-        if (p != mine && (p >> kPubShift) == (gen & ((uint64_t(1) << (64 - kPubShift)) - 1))) {
-          s = p & kSeqMask;
+        const uint64_t p = ld_agent(&d->pub);
+        if (p != mine && (p >> kPubShift) == gtag) {
+          job = p & kSeqMask;
           break;
         }
         if (ld_agent(&d->exit_gen) == gen) {
@@ -176,35 +220,34 @@ __global__ __launch_bounds__(kBlock) void k_resident(ResHost* h, ResDev* d, uint
         }
         __builtin_amdgcn_s_sleep(2);
       }
-      s_seq = s;
       s_mode = mode;
     }
     if (t == 0) {
-      // the descriptor (device, agent) and the operands / staging the host wrote (system)
+      // the job record (device, agent) and the operands / staging the host wrote (system)
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
     const int mode = s_mode;
     if (mode == 2) break;
-    const uint64_t s = s_seq;
-    if (mode == 1) {  // workgroup 0 alone: every tile here, then the completion word
+    if (mode == 1) {  // workgroup 0 alone: every tile here, then the slot's completion word
       res_tiles(s_desc, 0, 1, t);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (t == 0) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(&h->done, s, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&h->slot[s_slot].done, s_seq, __ATOMIC_RELEASE,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
       }
-      last = s;
       __syncthreads();
       continue;
     }
-    {
-      const uint64_t* src = reinterpret_cast<const uint64_t*>(&d->desc);
+    {  // a published job: its record into LDS
+      const uint64_t* src = reinterpret_cast<const uint64_t*>(&d->job);
       uint64_t* dst = reinterpret_cast<uint64_t*>(&s_desc);
-      for (int k = t; k < kDescWords; k += kBlock) dst[k] = ld_agent(src + k);
+      constexpr int kHead = (int)(offsetof(ResJob, desc) / 8);
+      for (int q = t; q < kDescWords; q += kBlock) dst[q] = ld_agent(src + kHead + q);
     }
     __syncthreads();
     res_tiles(s_desc, blockIdx.x, gridDim.x, t);
@@ -216,12 +259,15 @@ __global__ __launch_bounds__(kBlock) void k_resident(ResHost* h, ResDev* d, uint
       const uint32_t old =
           __hip_atomic_fetch_add(&d->arrive, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
       if (old == gridDim.x - 1) {
+        const uint64_t seq = ld_agent(&d->job.seq);
+        const uint32_t slot = ld_agent(&d->job.slot);
         __hip_atomic_store(&d->arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&h->done, s, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&d->finished, pub_word(gen, job), __ATOMIC_RELEASE,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&h->slot[slot].done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
       }
     }
-    last = s;
-    __syncthreads();  // s_seq / s_desc are rewritten next round
+    __syncthreads();  // s_desc is rewritten next round
   }
   if (blockIdx.x == 0 && t == 0)
     __hip_atomic_store(&h->alive, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -229,9 +275,9 @@ __global__ __launch_bounds__(kBlock) void k_resident(ResHost* h, ResDev* d, uint
 
 }  // namespace
 
-hipError_t launch_resident(ResHost* h, ResDev* d, uint64_t served, uint64_t gen,
-                           uint64_t idle_ticks, hipStream_t s) {
-  hipLaunchKernelGGL(k_resident, dim3(kResidentBlocks), dim3(kBlock), 0, s, h, d, served, gen,
+hipError_t launch_resident(ResCtl* h, ResDev* d, uint64_t gen, uint64_t idle_ticks,
+                           hipStream_t s) {
+  hipLaunchKernelGGL(k_resident, dim3(kResidentBlocks), dim3(kBlock), 0, s, h, d, gen,
                      idle_ticks);
   return hipGetLastError();
 }

@@ -1,0 +1,279 @@
+// resident_host.cpp -- the host side of the resident reducer (resident.h): one server per
+// device per process (control block, device record, its own hardware queue), slots leased by
+// host contexts, launches on demand.
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "../../include/hydra_hip.h"
+#include "errors.h"
+#include "resident.h"
+#include "resource_cache.h"
+
+namespace hydra {
+
+struct ResidentServer {
+  int device = 0;
+  ResCtl* h = nullptr;      // host address of the control block
+  ResCtl* h_dev = nullptr;  // its device address
+  ResDev* d = nullptr;
+  hipStream_t s = nullptr;
+  std::mutex mu;  // launches and slot leases
+  uint64_t gen = 0;
+  uint32_t leased = 0;  // bit i: slot i has a holder
+  std::atomic<uint64_t> launches{0};
+};
+
+struct ResidentLease {
+  ResidentServer* srv;
+  int slot;
+  uint64_t seq;    // the slot's last sequence number rung
+  uint64_t calls;  // calls submitted through this lease
+};
+
+namespace {
+static_assert(kResidentSlots <= 32, "leased is a 32-bit mask");
+
+constexpr int kMaxDevices = 64;
+std::mutex g_mu;
+ResidentServer* g_srv[kMaxDevices] = {};
+std::atomic<bool> g_exiting{false};
+
+uint64_t idle_ticks() {  // s_memrealtime runs at 100 MHz
+  static const uint64_t t = [] {
+    const char* v = std::getenv("HYDRA_RESIDENT_IDLE_US");
+    const long us = v ? std::atol(v) : 2000;
+    return (uint64_t)std::max(50L, std::min(us, 1000000L)) * 100;
+  }();
+  return t;
+}
+
+template <typename T>
+volatile T& vol(T& x) {
+  return reinterpret_cast<volatile T&>(x);
+}
+
+// At process exit every running instance is told to leave, so each grid has drained before
+// the runtime tears down (registered after the runtime initialised: runs before its teardown).
+void quit_all() {
+  g_exiting.store(true);
+  std::lock_guard<std::mutex> g(g_mu);
+  for (ResidentServer* v : g_srv)
+    if (v) vol(v->h->quit) = 1u;
+  for (ResidentServer* v : g_srv) {  // bounded: an instance leaves within microseconds
+    if (!v) continue;
+    const auto t0 = std::chrono::steady_clock::now();
+    while (vol(v->h->alive) != 0u &&
+           std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(200))
+      std::this_thread::yield();
+  }
+}
+
+// The instance's stream must not hold anything else up behind the persistent grid:
+//  * non-blocking, or every kernel on the legacy default stream (torch's default stream) waits
+//    for the grid to leave;
+//  * on a hardware queue no other stream uses: the runtime shares its GPU_MAX_HW_QUEUES queues
+//    per priority level among a process's streams, so a plain stream can land behind the grid.
+//    The greatest-priority level has a pool of its own, which ordinary code (torch's default
+//    and pool streams, RCCL) does not use.
+// HYDRA_RESIDENT_QUEUE=shared (a plain non-blocking stream) and =cumask (a CU-masked stream:
+// a queue of its own, but blocking) are A/B settings only (scripts/probe_queue_block.py).
+hipError_t make_stream(int device, hipStream_t* out) {
+  const char* v = std::getenv("HYDRA_RESIDENT_QUEUE");
+  if (v && std::strcmp(v, "shared") == 0)
+    return hipStreamCreateWithFlags(out, hipStreamNonBlocking);
+  if (v && std::strcmp(v, "cumask") == 0) {
+    hipDeviceProp_t p;
+    hipError_t e = hipGetDeviceProperties(&p, device);
+    if (e != hipSuccess) return e;
+    const int cus = std::max(1, p.multiProcessorCount);
+    std::vector<uint32_t> mask((cus + 31) / 32, 0u);
+    for (int i = 0; i < cus; i++) mask[i / 32] |= 1u << (i % 32);
+    return hipExtStreamCreateWithCUMask(out, (uint32_t)mask.size(), mask.data());
+  }
+  int least = 0, greatest = 0;
+  hipError_t e = hipDeviceGetStreamPriorityRange(&least, &greatest);
+  if (e != hipSuccess) return e;
+  return hipStreamCreateWithPriority(out, hipStreamNonBlocking, greatest);
+}
+
+int server(int device, ResidentServer** out) {
+  *out = nullptr;
+  if (device < 0 || device >= kMaxDevices) return fail(HYDRA_ERR_INVALID, "device out of range");
+  std::lock_guard<std::mutex> g(g_mu);
+  if (g_srv[device]) {
+    *out = g_srv[device];
+    return HYDRA_OK;
+  }
+  int prev = -1;
+  (void)hipGetDevice(&prev);
+  auto* v = new ResidentServer();
+  v->device = device;
+  void* p = nullptr;
+  void* q = nullptr;
+  void* hd = nullptr;
+  hipError_t e = hipSetDevice(device);
+  if (e == hipSuccess) e = cached_malloc_host(sizeof(ResCtl), &p);
+  if (e == hipSuccess) {
+    std::memset(p, 0, sizeof(ResCtl));
+    e = hipHostGetDevicePointer(&hd, p, 0);
+  }
+  if (e == hipSuccess) e = cached_malloc(device, sizeof(ResDev), &q);
+  if (e == hipSuccess) e = hipMemset(q, 0, sizeof(ResDev));
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  if (e == hipSuccess) e = make_stream(device, &v->s);
+  if (prev >= 0) (void)hipSetDevice(prev);
+  if (e != hipSuccess) {
+    if (p) (void)cached_free_host(p);
+    if (q) (void)cached_free(q);
+    delete v;
+    return hip_fail(e, "resident reducer setup");
+  }
+  v->h = static_cast<ResCtl*>(p);
+  v->h_dev = static_cast<ResCtl*>(hd);
+  v->d = static_cast<ResDev*>(q);
+  static bool registered = false;
+  if (!registered) {
+    std::atexit(quit_all);
+    registered = true;
+  }
+  g_srv[device] = v;  // lives for the process
+  *out = v;
+  return HYDRA_OK;
+}
+
+// A new instance unless one is running (alive); `alive` is set before the launch, cleared by
+// the kernel as it leaves.
+int ensure_running(ResidentServer* v) {
+  if (vol(v->h->alive) != 0u) return HYDRA_OK;
+  std::lock_guard<std::mutex> g(v->mu);
+  if (vol(v->h->alive) != 0u) return HYDRA_OK;
+  if (g_exiting.load()) return fail(HYDRA_ERR_INVALID, "resident reducer: process is exiting");
+  vol(v->h->quit) = 0u;
+  vol(v->h->alive) = 1u;
+  std::atomic_thread_fence(std::memory_order_seq_cst);
+  int prev = -1;
+  (void)hipGetDevice(&prev);
+  if (prev != v->device) (void)hipSetDevice(v->device);
+  const hipError_t e = launch_resident(v->h_dev, v->d, ++v->gen, idle_ticks(), v->s);
+  if (prev >= 0 && prev != v->device) (void)hipSetDevice(prev);
+  if (e != hipSuccess) {
+    vol(v->h->alive) = 0u;
+    return hip_fail(e, "resident reducer launch");
+  }
+  v->launches.fetch_add(1);
+  return HYDRA_OK;
+}
+}  // namespace
+
+bool resident_enabled() {
+  static const bool on = [] {
+    const char* v = std::getenv("HYDRA_RESIDENT");
+    return !(v && v[0] == '0');
+  }();
+  return on;
+}
+
+int resident_lease(int device, ResidentLease** out) {
+  *out = nullptr;
+  if (!resident_enabled()) return HYDRA_OK;
+  ResidentServer* v = nullptr;
+  if (int rc = server(device, &v)) return rc;
+  std::lock_guard<std::mutex> g(v->mu);
+  for (int k = 0; k < kResidentSlots; k++) {
+    if (v->leased & (1u << k)) continue;
+    v->leased |= 1u << k;
+    // numbering continues from the slot's last doorbell (a slot is reused by later contexts)
+    *out = new ResidentLease{v, k, vol(v->h->slot[k].doorbell), 0};
+    return HYDRA_OK;
+  }
+  return HYDRA_OK;  // every slot leased: this context launches
+}
+
+void resident_release(ResidentLease* l) {
+  if (!l) return;
+  {
+    std::lock_guard<std::mutex> g(l->srv->mu);
+    l->srv->leased &= ~(1u << l->slot);
+  }
+  delete l;
+}
+
+int resident_submit(ResidentLease* l, int op, int dtype, size_t es, const BatchSegDesc* segs,
+                    size_t count) {
+  if (count == 0 || count > (size_t)kResidentSegs)
+    return fail(HYDRA_ERR_INVALID, "resident reducer: 1..16 segments per call");
+  ResidentServer* v = l->srv;
+  ResSlot& S = v->h->slot[l->slot];
+  ResDesc& D = S.desc;
+  const size_t N = 16 / es;
+  uint32_t tiles = 0;
+  int k = 0;
+  for (size_t i = 0; i < count; i++) {
+    const BatchSegDesc& g = segs[i];
+    if (g.n == 0) continue;
+    const uintptr_t cp = reinterpret_cast<uintptr_t>(g.c);
+    size_t head = ((16 - (cp & 15)) & 15) / es;
+    if (head > g.n) head = g.n;
+    const size_t nvec = (g.n - head) / N;
+    ResSeg& r = D.s[k++];
+    r.c = static_cast<char*>(g.c) + head * es;
+    r.a = static_cast<const char*>(g.a) + head * es;
+    r.b = static_cast<const char*>(g.b) + head * es;
+    r.nvec = nvec;
+    r.head = (int32_t)head;
+    r.tail = (int32_t)(g.n - head - nvec * N);
+    r.tile0 = tiles;
+    r.c_old = (dtype == HYDRA_FLOAT16 && g.c != g.a) ? 1u : 0u;
+    tiles += (uint32_t)std::max<size_t>(1, (nvec + kBlock - 1) / kBlock);
+  }
+  if (k == 0) return fail(HYDRA_ERR_INVALID, "resident reducer: empty call");
+  D.op = op;
+  D.dtype = dtype;
+  D.count = k;
+  D.tiles = tiles;
+  std::atomic_thread_fence(std::memory_order_release);  // the descriptor before the doorbell
+  vol(S.doorbell) = ++l->seq;
+  l->calls++;
+  return ensure_running(v);
+}
+
+int resident_wait(ResidentLease* l) {
+  ResidentServer* v = l->srv;
+  volatile uint64_t& done = vol(v->h->slot[l->slot].done);
+  const uint64_t seq = l->seq;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint32_t spins = 0;; spins++) {
+    if (done >= seq) break;
+    if (vol(v->h->alive) == 0u && done < seq) {  // it left without serving us: a new instance
+      if (int rc = ensure_running(v)) return rc;
+      continue;
+    }
+    if ((spins & 1023) == 0) {
+      if (vol(v->h->err))
+        return fail(HYDRA_ERR_HIP, "resident reducer: a wait inside the grid expired");
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(20)) {
+        vol(v->h->quit) = 1u;
+        return fail(HYDRA_ERR_TIMEOUT, "Timed out waiting 20000ms for the resident reducer");
+      }
+    }
+    __builtin_ia32_pause();
+  }
+  std::atomic_thread_fence(std::memory_order_acquire);  // the results after `done`
+  return HYDRA_OK;
+}
+
+uint64_t resident_calls(const ResidentLease* l) { return l ? l->calls : 0; }
+
+uint64_t resident_launches(int device) {
+  if (device < 0 || device >= kMaxDevices) return 0;
+  std::lock_guard<std::mutex> g(g_mu);
+  return g_srv[device] ? g_srv[device]->launches.load() : 0;
+}
+
+}  // namespace hydra

@@ -129,23 +129,25 @@ int hydra_set_variant(int variant);
 /* ---- host-resident reduction --------------------------------------------------------------
  * Same contract on HOST buffers, synchronous like gloo::sum<T>: the kernel reads and writes the
  * mapped parts of a, b and c in place over PCIe (see below) and the rest through the context's
- * pinned staging, which the CPU fills and empties; one batched launch per call (per 4 MiB of
- * staged bytes per operand beyond that, double-buffered).  Device pointers are rejected
- * (HYDRA_ERR_INVALID: use hydra_reduce).  One context per calling thread (bew_allreduce_a runs
- * two rails concurrently: one context each).  hydra_set_variant(1000) stages every operand
- * (A/B measurements). */
+ * pinned staging, which the CPU fills and empties; one batched round per call (per 4 MiB of
+ * staged bytes per operand, or per 16 intervals, beyond that: the CPU fills round r + 1 while
+ * round r runs).  Device pointers are rejected (HYDRA_ERR_INVALID: use hydra_reduce).  One
+ * context per calling thread (bew_allreduce_a runs two rails concurrently: one context each).
+ * hydra_set_variant(1000) stages every operand (A/B measurements). */
 int hydra_ctx_create(int device, hydra_ctx_t* out);
 int hydra_ctx_destroy(hydra_ctx_t ctx);
 int hydra_reduce_host(hydra_ctx_t ctx, int op, int dtype, void* c, const void* a, const void* b,
                       size_t n);
 int hydra_chunk_sum_host(hydra_ctx_t ctx, int dtype, void* c, const void* a, const void* b,
                          size_t n);
-/* Low latency: a call whose staged bytes fit one round (4 MiB per operand) and that has at most
- * 16 segments is served by the context's RESIDENT reducer -- one launch of 32 workgroups kept on
- * a private stream while calls keep coming, woken by a host-mapped doorbell instead of a fresh
- * dispatch; it leaves after HYDRA_RESIDENT_IDLE_US (default 2000) without a call, at
- * hydra_ctx_destroy and at process exit.  HYDRA_RESIDENT=0 turns it off.  Stats (tests):
- * calls served by it and instances launched. */
+/* Low latency: the rounds are served by the device's RESIDENT reducer -- ONE launch of 32
+ * workgroups per device per process, kept running while calls keep coming on a stream with a
+ * hardware queue of its own (no other stream's work waits behind it), woken by a host-mapped
+ * doorbell instead of a fresh dispatch.  Each context leases one of its 32 slots at
+ * hydra_ctx_create (a context created when all are leased launches instead).  The instance
+ * leaves after HYDRA_RESIDENT_IDLE_US (default 2000) without a call and at process exit.
+ * HYDRA_RESIDENT=0 turns it off (every round is one launch on the context's stream).  Stats
+ * (tests): rounds this context had served by it, and instances launched on its device. */
 int hydra_ctx_stats(hydra_ctx_t ctx, uint64_t* resident_calls, uint64_t* resident_launches);
 /* Which host memory the kernel reads / writes in place (zero-copy over PCIe), per operand: a
  * range registered with hydra_host_register, a pinned block from hydra_malloc_host, or memory
