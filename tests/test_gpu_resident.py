@@ -230,10 +230,11 @@ def test_resident_instance_never_blocks_other_streams(gpu):
 
 
 def test_resident_more_contexts_than_slots(gpu, O):
-    """33 contexts on one device: 32 lease the reducer's slots, the 33rd launches; every
-    context's calls are exact, and the slots are reused after the contexts close."""
+    """40 contexts on one device (the reducer has 32 slots, some perhaps held by other live
+    contexts of this process): those beyond the free slots launch; every context's calls are
+    exact, and a slot is free again once the contexts close."""
     L = _lib.lib()
-    ctxs = [HostContext(0) for _ in range(33)]
+    ctxs = [HostContext(0) for _ in range(40)]
     try:
         for k, c in enumerate(ctxs):
             n = 3000 + 517 * k
@@ -243,7 +244,9 @@ def test_resident_more_contexts_than_slots(gpu, O):
                                            b.ctypes.data, n))
             assert np.array_equal(bits(a), bits(exp)), k
         served = [c.stats()["resident_calls"] for c in ctxs]
-        assert sum(1 for v in served if v == 1) == 32 and served.count(0) == 1, served
+        leased = sum(1 for v in served if v == 1)
+        assert set(served) <= {0, 1} and 1 <= leased <= 32 and served.count(0) >= 8, served
+        assert served == sorted(served, reverse=True), served  # the first ones got the slots
     finally:
         for c in ctxs:
             c.close()
