@@ -111,8 +111,14 @@ def ref():
     return _ref
 
 
+_ESIZE = (1, 1, 4, 4, 8, 8, 4, 8, 2, 2)  # element size per hydra_dtype_t code
+
+
 def _dt(arr: np.ndarray, dtype_code: int | None) -> int:
     if dtype_code is not None:
+        # the C side walks arr.size elements of the code's size: they must be arr's own
+        if not (0 <= dtype_code < len(_ESIZE)) or _ESIZE[dtype_code] != arr.itemsize:
+            raise ValueError(f"dtype code {dtype_code} does not match a {arr.dtype} array")
         return dtype_code
     return DTYPES[arr.dtype]
 

@@ -1,15 +1,21 @@
-"""CPU executor of the device allreduce plans over torch.distributed gloo (test infrastructure).
+"""Executor of the device allreduce plans over torch.distributed gloo (test infrastructure).
 
-`execute` runs one rank's op list (hydra_plan / hydra_reduce_root_plan, xgmi_plan.h) on a CPU
-bucket with real inter-process p2p: SEND/RECV groups through batch_isend_irecv, ALLTOALL as
-p2p (gloo has no alltoall), ALLGATHER through all_gather, and REDUCE / FOLD through the
-oracle's element ops in the kernels' fold order (the C restatement standing in for the HIP
-kernels).  `GlooPlanComm` wraps it in XgmiComm's interface, so the N>1 bench orchestration
+`execute` runs one rank's op list (hydra_plan / hydra_reduce_root_plan, xgmi_plan.h) with real
+inter-process p2p: SEND/RECV groups through batch_isend_irecv, ALLTOALL as p2p (gloo has no
+alltoall), ALLGATHER through all_gather.  REDUCE / FOLD run
+  * on a CPU bucket (default): through the oracle's element ops in the kernels' fold order (the
+    C restatement standing in for the HIP kernels) -- the CPU suite's world-size 2/3 runs;
+  * on a GPU bucket (`execute_device`): through the library's own gfx950 kernels
+    (hydra_reduce / hydra_fold, exactly as the RCCL executor's launch_compute calls them), the
+    gloo transport staging each message through host memory -- several processes sharing the
+    one GPU of the test box (RCCL refuses two ranks on one GPU), so the plans run across
+    processes with the product kernels (tests/test_gpu_dist_plans.py).
+`GlooPlanComm` wraps the CPU form in XgmiComm's interface, so the N>1 bench orchestration
 (hydra_amd.ring.bench_allreduce) runs unchanged at world size 2 and 3 on the CPU."""
 import numpy as np
 
 SEND, RECV, GROUP, REDUCE, FOLD, ALLTOALL, ALLGATHER = 1, 2, 3, 4, 5, 6, 7
-_NP = {4: np.int32, 6: np.float32, 9: np.uint16}  # hydra_dtype_t INT32, FLOAT32, BFLOAT16
+_NP = {2: np.int32, 6: np.float32, 9: np.uint16}  # hydra_dtype_t INT32, FLOAT32, BFLOAT16
 BF16 = 9
 
 
@@ -104,6 +110,90 @@ def execute(O, ops, scratch_bytes, user, code=6, op="sum"):
             for req in dist.batch_isend_irecv(p2p):
                 req.wait()
         i = g + 1
+
+
+_OPC = {"sum": 0, "product": 1, "max": 2, "min": 3}
+
+
+def execute_device(ops, scratch_bytes, user, code=6, op="sum"):
+    """`execute` on a GPU bucket (`user`: contiguous uint8 CUDA tensor, modified in place):
+    REDUCE / FOLD are the library's kernels on the current stream; every p2p message is staged
+    through host memory for gloo.  code BFLOAT16 folds with HYDRA_ACC_F32 (config 5)."""
+    import ctypes
+
+    import torch
+    import torch.distributed as dist
+
+    from hydra_amd import _lib
+
+    L = _lib.lib()
+    rank, world = dist.get_rank(), dist.get_world_size()
+    dev = user.device
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    scratch = torch.zeros(scratch_bytes + 16, dtype=torch.uint8, device=dev)
+    es = np.dtype(_NP[code]).itemsize
+    flags = 1 if code == BF16 else 0
+    ub, sb = user.data_ptr(), scratch.data_ptr()
+
+    def exchange(sends, recvs):  # [(device view, peer)] -> gloo p2p through host copies
+        p2p, back = [], []
+        for t, pr in sends:
+            p2p.append(dist.P2POp(dist.isend, t.cpu(), pr))
+        for t, pr in recvs:
+            h = torch.empty(t.numel(), dtype=torch.uint8)
+            p2p.append(dist.P2POp(dist.irecv, h, pr))
+            back.append((t, h))
+        if p2p:
+            for req in dist.batch_isend_irecv(p2p):
+                req.wait()
+        for t, h in back:
+            t.copy_(h)
+
+    i = 0
+    while i < len(ops):
+        o = ops[i]
+        if o["kind"] == ALLTOALL:
+            B = o["bytes"]
+            scratch[o["src_off"] + rank * B:o["src_off"] + (rank + 1) * B] = \
+                user[o["off"] + rank * B:o["off"] + (rank + 1) * B]
+            exchange([(user[o["off"] + pr * B:o["off"] + (pr + 1) * B], pr)
+                      for pr in range(world) if pr != rank],
+                     [(scratch[o["src_off"] + pr * B:o["src_off"] + (pr + 1) * B], pr)
+                      for pr in range(world) if pr != rank])
+            i += 1
+            continue
+        if o["kind"] == ALLGATHER:
+            B = o["bytes"]
+            mine = user[o["off"] + rank * B:o["off"] + (rank + 1) * B].cpu()
+            parts = [torch.empty_like(mine) for _ in range(world)]
+            dist.all_gather(parts, mine)
+            for pr in range(world):
+                if pr != rank:
+                    user[o["off"] + pr * B:o["off"] + (pr + 1) * B].copy_(parts[pr])
+            i += 1
+            continue
+        if o["kind"] == REDUCE:
+            _lib.check(L.hydra_reduce(_OPC[op], code, ub + o["off"], ub + o["off"],
+                                      sb + o["src_off"], o["bytes"] // es, stream))
+            i += 1
+            continue
+        if o["kind"] == FOLD:
+            srcs = (ctypes.c_void_p * o["nsrc"])(
+                ub + o["off"], *[sb + fold_slot(o, j) for j in range(1, o["nsrc"])])
+            _lib.check(L.hydra_fold(_OPC[op], code, flags, ub + o["off"], srcs, o["nsrc"],
+                                    o["bytes"] // es, stream))
+            i += 1
+            continue
+        g = i
+        sends, recvs = [], []
+        while ops[g]["kind"] != GROUP:
+            it = ops[g]
+            t = (user if it["buf"] == 0 else scratch)[it["off"]:it["off"] + it["bytes"]]
+            (sends if it["kind"] == SEND else recvs).append((t, it["peer"]))
+            g += 1
+        exchange(sends, recvs)
+        i = g + 1
+    torch.cuda.current_stream(dev).synchronize()
 
 
 class GlooPlanComm:
