@@ -19,6 +19,7 @@
 #include <vector>
 
 #include "../../include/hydra_hip.h"
+#include "copy_pool.h"
 #include "errors.h"
 #include "fault_report.h"
 #include "host_map.h"
@@ -322,11 +323,6 @@ struct WindowsGuard {
   }
 };
 
-struct CopyOut {
-  char* host;
-  const char* stage;
-  size_t bytes;
-};
 }  // namespace
 
 int hydra_reduce_host(hydra_ctx_t ctx, int op, int dtype, void* c, const void* a, const void* b,
@@ -383,7 +379,8 @@ int hydra_reduce_host(hydra_ctx_t ctx, int op, int dtype, void* c, const void* a
   hydra::ResidentLease* const lease = ctx->lease;
   std::vector<hydra::BatchSegDesc> segs;
   segs.reserve(hydra::kResidentSegs);
-  std::vector<CopyOut> outs[2];
+  std::vector<hydra::CopyJob> ins;      // the current round's copies into the staging
+  std::vector<hydra::CopyJob> outs[2];  // each buffer's staged results, back to c
   size_t used[3] = {0, 0, 0};  // bytes of the current buffer's a, b, c slots
   int buf = 0;
   bool pending = false;  // the other buffer's round is in flight
@@ -404,6 +401,8 @@ int hydra_reduce_host(hydra_ctx_t ctx, int op, int dtype, void* c, const void* a
   auto flush = [&]() -> int {  // submit the current buffer's round
     if (segs.empty() && outs[buf].empty()) return HYDRA_OK;
     const int other = buf ^ 1;
+    hydra::copy_all(ins.data(), ins.size());  // the staged operands (fanned out when large)
+    ins.clear();
     if (pending) {
       if (int r = wait_round(other)) return r;
       pending = false;
@@ -427,7 +426,7 @@ int hydra_reduce_host(hydra_ctx_t ctx, int op, int dtype, void* c, const void* a
       }
     }
     // the previous round is done: its staged results back to c (overlapping this round)
-    for (const CopyOut& o : outs[other]) std::memcpy(o.host, o.stage, o.bytes);
+    hydra::copy_all(outs[other].data(), outs[other].size());
     outs[other].clear();
     segs.clear();
     used[0] = used[1] = used[2] = 0;
@@ -463,7 +462,7 @@ int hydra_reduce_host(hydra_ctx_t ctx, int op, int dtype, void* c, const void* a
       char* dev_st = ctx->stage_dev[buf];
       auto slot = [&](int k, const char* src, bool fill) -> char* {  // k: 0 a, 1 b, 2 c
         const size_t at = size_t(k) * kSlotBytes + used[k];
-        if (fill) std::memcpy(host_st + at, src, bytes);
+        if (fill) ins.push_back({host_st + at, src, bytes});
         used[k] += (bytes + 255) / 256 * 256;
         return dev_st + at;
       };
@@ -497,7 +496,7 @@ int hydra_reduce_host(hydra_ctx_t ctx, int op, int dtype, void* c, const void* a
   if (pending) {  // the last round: done, results back
     if ((rc = wait_round(buf ^ 1))) return rc;
     pending = false;
-    for (const CopyOut& o : outs[buf ^ 1]) std::memcpy(o.host, o.stage, o.bytes);
+    hydra::copy_all(outs[buf ^ 1].data(), outs[buf ^ 1].size());
   }
   drain_.f = nullptr;
   return ok();  // the windows are released here, after every round finished

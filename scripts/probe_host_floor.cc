@@ -30,7 +30,8 @@ int main(int argc, char** argv) {
   std::vector<size_t> sizes;
   for (int i = 1; i < argc; i++) sizes.push_back(std::strtoull(argv[i], nullptr, 10));
   if (sizes.empty()) sizes = {64, 1024, 16384, 262144};
-  const size_t big = 1 << 22;  // elements per buffer
+  size_t big = 1 << 22;  // elements per buffer (room for the largest size + the offsets)
+  for (size_t n : sizes) big = std::max(big, (n + 4096 + 1023) / 1024 * 1024);
   hydra_ctx_t ctx;
   CK(hydra_ctx_create(0, &ctx));
   // registered: mmap'ed, never returned to the allocator
@@ -61,7 +62,7 @@ int main(int argc, char** argv) {
     for (auto& m : modes) {
       const int k = (int)std::max<size_t>(100, std::min<size_t>(5000, 200000000 / (12 * n + 1)));
       std::vector<double> us(k);
-      for (int w = 0; w < 50; w++) CK(hydra_reduce_host(ctx, HYDRA_SUM, HYDRA_FLOAT32, m.a, m.a, m.b, n));
+      for (int w = 0; w < std::min(50, k); w++) CK(hydra_reduce_host(ctx, HYDRA_SUM, HYDRA_FLOAT32, m.a, m.a, m.b, n));
       for (int i = 0; i < k; i++) {
         const auto t0 = std::chrono::steady_clock::now();
         CK(hydra_reduce_host(ctx, HYDRA_SUM, HYDRA_FLOAT32, m.a, m.a, m.b, n));

@@ -29,3 +29,21 @@ def test_host_runtime_sanitized(tmp_path, san):
     assert p.returncode == 0 and "OK" in p.stdout, (p.stdout[-2000:], p.stderr[-4000:])
     assert "ThreadSanitizer" not in p.stderr and "AddressSanitizer" not in p.stderr
     assert "runtime error" not in p.stderr
+
+
+@pytest.mark.parametrize("san", ["thread", "address,undefined"])
+def test_copy_pool_sanitized(tmp_path, san):
+    """The staging copy fan-out (hydra_amd/csrc/copy_pool.cpp): concurrent callers sharing the
+    helper threads, every byte and the guard bytes checked, under TSan and ASan + UBSan."""
+    exe = tmp_path / f"copy_pool_{san.split(',')[0]}"
+    srcs = [os.path.join(ROOT, "tests", "cpp", "copy_pool_stress.cc"),
+            os.path.join(ROOT, "hydra_amd", "csrc", "copy_pool.cpp")]
+    subprocess.check_call(["g++", "-std=c++17", "-O1", "-g", "-pthread", f"-fsanitize={san}",
+                           "-fno-omit-frame-pointer", *srcs, "-o", str(exe)])
+    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1",
+               ASAN_OPTIONS="detect_leaks=0:verify_asan_link_order=0",
+               UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1")
+    p = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300, env=env)
+    assert p.returncode == 0 and "OK" in p.stdout, (p.stdout[-2000:], p.stderr[-4000:])
+    assert "ThreadSanitizer" not in p.stderr and "AddressSanitizer" not in p.stderr
+    assert "runtime error" not in p.stderr
