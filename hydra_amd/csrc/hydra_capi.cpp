@@ -99,6 +99,19 @@ struct hydra_ctx {
 namespace {
 constexpr size_t kSlotBytes = 4u << 20;  // per operand and staging buffer (3 slots: a, b, c)
 constexpr int kVariantForceStaging = 1000;  // hydra_set_variant value: host path always stages
+constexpr int kVariantSplit = 1100;         // hydra_set_variant 1101..1164: staging split (A/B)
+constexpr size_t kRoundMin = 512u << 10;    // smallest staging round per operand (probe_stage_split)
+
+// Rounds a staged call is cut into (HYDRA_STAGE_SPLIT, default 4; 1 = one round per slot).
+size_t stage_split(int variant) {
+  if (variant > kVariantSplit && variant <= kVariantSplit + 64) return variant - kVariantSplit;
+  static const size_t k = [] {
+    const char* v = std::getenv("HYDRA_STAGE_SPLIT");
+    const long x = v ? std::atol(v) : 4;
+    return (size_t)std::max(1L, std::min(x, 64L));
+  }();
+  return k;
+}
 
 void ctx_release(hydra_ctx* x) {
   if (x->stream) (void)hydra::release_stream(x->stream);
@@ -434,6 +447,11 @@ int hydra_reduce_host(hydra_ctx_t ctx, int op, int dtype, void* c, const void* a
     return HYDRA_OK;
   };
   if (!lease) HIP_TRY(hipSetDevice(ctx->device));
+  // A staged call is cut into about stage_split() rounds (>= kRoundMin bytes per operand, at
+  // most a slot), so its copies overlap the GPU's rounds: in at round r + 1 and out at round
+  // r - 1 while round r runs.
+  const size_t round_cap =
+      std::min(kSlotBytes, std::max(kRoundMin, (nbytes / stage_split(variant) + 255) / 256 * 256));
   for (size_t q = 0; q + 1 < cut.size(); q++) {
     size_t off = cut[q];
     const size_t end = cut[q + 1];
@@ -450,7 +468,7 @@ int hydra_reduce_host(hydra_ctx_t ctx, int op, int dtype, void* c, const void* a
         continue;
       }
       // staged: as much of [off, end) as the current buffer's slots still hold
-      const size_t room = kSlotBytes - std::max({used[0], used[1], used[2]});
+      const size_t room = round_cap - std::min(round_cap, std::max({used[0], used[1], used[2]}));
       if (room < 64 * es) {
         if ((rc = flush())) return rc;
         continue;

@@ -76,7 +76,8 @@ def test_resident_back_to_back_and_idle_gaps(ctx, O):
         elif i % 10 == 9:
             time.sleep(0.001)
     st = ctx.stats()
-    assert st["resident_calls"] - s0["resident_calls"] == 200, (s0, st)
+    # (a staged call of more than 256 KiB per operand is served as 2+ rounds: HYDRA_STAGE_SPLIT)
+    assert 200 <= st["resident_calls"] - s0["resident_calls"] < 400, (s0, st)
     assert 2 <= st["resident_launches"] - s0["resident_launches"] < 60, (s0, st)
 
 
