@@ -12,10 +12,11 @@
 //   * wave 0 of workgroup 0 polls every slot's doorbell at once (lane i loads slot i; system-
 //     scope relaxed loads, s_sleep backoff) and serves pending slots round robin;
 //   * a call of at most kSoloTiles tiles is summed by workgroup 0 alone; a larger one is copied
-//     to device memory and published as a job to every workgroup (a device word tagged with
-//     the instance's generation); each workgroup acquires at system scope, sums its share,
-//     releases at system scope and arrives on a device counter; the last to arrive writes the
-//     slot's completion word, on which the host spins;
+//     to device memory and published as a job (a device word tagged with the instance's
+//     generation) to as many workgroups as it has pairs of tiles -- each workgroup's system-
+//     scope fences cost, so a small job wakes few; each of them acquires at system scope, sums
+//     its share, releases at system scope and arrives on a device counter; the last to arrive
+//     writes the slot's completion word, on which the host spins;
 //   * the instance runs on a non-blocking stream of the greatest priority, whose hardware queue
 //     pool ordinary streams (torch's, RCCL's, hydra's own) do not use, so their work never
 //     queues behind the persistent grid (tests/test_gpu_resident.py times it).
@@ -37,7 +38,8 @@
 namespace hydra {
 
 constexpr int kResidentSegs = 16;
-constexpr int kResidentBlocks = 32;
+constexpr int kResidentBlocks = 128;  // default grid (HYDRA_RESIDENT_BLOCKS: 1..1024, A/B)
+constexpr uint32_t kResidentTilesPerBlock = 2;  // a job wakes ceil(tiles / 2) workgroups
 constexpr int kResidentSlots = 32;  // contexts served at once per device (lanes of wave 0)
 
 struct ResSeg {  // one c = op(a, b): vector body + ragged head / tail, split on c (as the batch)
@@ -71,9 +73,9 @@ struct alignas(128) ResCtl {  // host-mapped (pinned), one per device
   alignas(128) ResSlot slot[kResidentSlots];
 };
 
-struct ResJob {  // a call spread over every workgroup (device memory)
+struct ResJob {  // a call spread over workgroups 0 .. nwg-1 (device memory)
   uint64_t seq;
-  uint32_t slot, pad;
+  uint32_t slot, nwg;
   ResDesc desc;
 };
 
@@ -85,8 +87,8 @@ struct alignas(64) ResDev {  // device memory, zeroed at creation
   alignas(64) ResJob job;
 };
 
-// Launch one instance (generation `gen`) on `s`.
-hipError_t launch_resident(ResCtl* h, ResDev* d, uint64_t gen, uint64_t idle_ticks,
+// Launch one instance (generation `gen`, `blocks` workgroups) on `s`.
+hipError_t launch_resident(ResCtl* h, ResDev* d, uint64_t gen, uint64_t idle_ticks, int blocks,
                            hipStream_t s);
 
 // ---- host side (resident_host.cpp) -------------------------------------------------------

@@ -119,7 +119,8 @@ __global__ __launch_bounds__(kBlock) void k_resident(ResCtl* h, ResDev* d, uint6
                                                      uint64_t idle_ticks) {
   __shared__ uint64_t s_seq;
   __shared__ int s_slot;
-  __shared__ int s_mode;  // 0 every workgroup (a published job), 1 workgroup 0 alone, 2 leave
+  __shared__ int s_mode;  // 0 a published job, 1 workgroup 0 alone, 2 leave, 3 not in this job
+  __shared__ uint32_t s_nwg;  // workgroups in the published job
   __shared__ ResDesc s_desc;
   const int t = threadIdx.x;
   const uint64_t gtag = gen & ((uint64_t(1) << (64 - kPubShift)) - 1);
@@ -168,6 +169,9 @@ __global__ __launch_bounds__(kBlock) void k_resident(ResCtl* h, ResDev* d, uint6
           } else if (job != 0 && !wait_finished(h, d, pub_word(gen, job))) {
             mode = 2;  // a workgroup never finished the last job: leave (err is set)
           } else {  // the job record, write-through, then publish it
+            const uint32_t nwg = min(gridDim.x, max(2u, (tiles + kResidentTilesPerBlock - 1) /
+                                                            kResidentTilesPerBlock));
+            if (t == 0) s_nwg = nwg;
             uint64_t* dst = reinterpret_cast<uint64_t*>(&d->job.desc);
             if (t < kDescWords)
               __hip_atomic_store(dst + t, w0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -177,6 +181,7 @@ __global__ __launch_bounds__(kBlock) void k_resident(ResCtl* h, ResDev* d, uint6
               __hip_atomic_store(&d->job.seq, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
               __hip_atomic_store(&d->job.slot, (uint32_t)k, __ATOMIC_RELAXED,
                                  __HIP_MEMORY_SCOPE_AGENT);
+              __hip_atomic_store(&d->job.nwg, nwg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
@@ -220,9 +225,15 @@ __global__ __launch_bounds__(kBlock) void k_resident(ResCtl* h, ResDev* d, uint6
         }
         __builtin_amdgcn_s_sleep(2);
       }
+      if (mode == 0) {  // in this job?  (the record was published before the word: agent acquire)
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        const uint32_t nwg = ld_agent(&d->job.nwg);
+        s_nwg = nwg;
+        if (blockIdx.x >= nwg) mode = 3;
+      }
       s_mode = mode;
     }
-    if (t == 0) {
+    if (t == 0 && s_mode != 3) {
       // the job record (device, agent) and the operands / staging the host wrote (system)
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -230,6 +241,10 @@ __global__ __launch_bounds__(kBlock) void k_resident(ResCtl* h, ResDev* d, uint6
     __syncthreads();
     const int mode = s_mode;
     if (mode == 2) break;
+    if (mode == 3) {  // not needed for this job: wait for the next
+      __syncthreads();
+      continue;
+    }
     if (mode == 1) {  // workgroup 0 alone: every tile here, then the slot's completion word
       res_tiles(s_desc, 0, 1, t);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -250,7 +265,7 @@ __global__ __launch_bounds__(kBlock) void k_resident(ResCtl* h, ResDev* d, uint6
       for (int q = t; q < kDescWords; q += kBlock) dst[q] = ld_agent(src + kHead + q);
     }
     __syncthreads();
-    res_tiles(s_desc, blockIdx.x, gridDim.x, t);
+    res_tiles(s_desc, blockIdx.x, s_nwg, t);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (t == 0) {
@@ -258,7 +273,7 @@ __global__ __launch_bounds__(kBlock) void k_resident(ResCtl* h, ResDev* d, uint6
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const uint32_t old =
           __hip_atomic_fetch_add(&d->arrive, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-      if (old == gridDim.x - 1) {
+      if (old == s_nwg - 1) {
         const uint64_t seq = ld_agent(&d->job.seq);
         const uint32_t slot = ld_agent(&d->job.slot);
         __hip_atomic_store(&d->arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -275,10 +290,9 @@ __global__ __launch_bounds__(kBlock) void k_resident(ResCtl* h, ResDev* d, uint6
 
 }  // namespace
 
-hipError_t launch_resident(ResCtl* h, ResDev* d, uint64_t gen, uint64_t idle_ticks,
+hipError_t launch_resident(ResCtl* h, ResDev* d, uint64_t gen, uint64_t idle_ticks, int blocks,
                            hipStream_t s) {
-  hipLaunchKernelGGL(k_resident, dim3(kResidentBlocks), dim3(kBlock), 0, s, h, d, gen,
-                     idle_ticks);
+  hipLaunchKernelGGL(k_resident, dim3(blocks), dim3(kBlock), 0, s, h, d, gen, idle_ticks);
   return hipGetLastError();
 }
 

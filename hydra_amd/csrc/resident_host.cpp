@@ -53,6 +53,15 @@ uint64_t idle_ticks() {  // s_memrealtime runs at 100 MHz
   return t;
 }
 
+int grid_blocks() {
+  static const int b = [] {
+    const char* v = std::getenv("HYDRA_RESIDENT_BLOCKS");
+    const int k = v ? std::atoi(v) : kResidentBlocks;
+    return std::max(1, std::min(k, 1024));
+  }();
+  return b;
+}
+
 template <typename T>
 volatile T& vol(T& x) {
   return reinterpret_cast<volatile T&>(x);
@@ -160,7 +169,7 @@ int ensure_running(ResidentServer* v) {
   int prev = -1;
   (void)hipGetDevice(&prev);
   if (prev != v->device) (void)hipSetDevice(v->device);
-  const hipError_t e = launch_resident(v->h_dev, v->d, ++v->gen, idle_ticks(), v->s);
+  const hipError_t e = launch_resident(v->h_dev, v->d, ++v->gen, idle_ticks(), grid_blocks(), v->s);
   if (prev >= 0 && prev != v->device) (void)hipSetDevice(prev);
   if (e != hipSuccess) {
     vol(v->h->alive) = 0u;
