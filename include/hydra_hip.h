@@ -140,7 +140,7 @@ int hydra_reduce_host(hydra_ctx_t ctx, int op, int dtype, void* c, const void* a
                       size_t n);
 int hydra_chunk_sum_host(hydra_ctx_t ctx, int dtype, void* c, const void* a, const void* b,
                          size_t n);
-/* Low latency: the rounds are served by the device's RESIDENT reducer -- ONE launch of 32
+/* Low latency: the rounds are served by the device's RESIDENT reducer -- ONE launch of 128
  * workgroups per device per process, kept running while calls keep coming on a stream with a
  * hardware queue of its own (no other stream's work waits behind it), woken by a host-mapped
  * doorbell instead of a fresh dispatch.  Each context leases one of its 32 slots at
