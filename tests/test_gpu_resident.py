@@ -1,9 +1,11 @@
 """The resident reducer (hydra_amd/csrc/resident.h): hydra_reduce_host's low-latency form for
-the reference ring's synchronous per-segment Func (allreduce.cc:301-305).  Bit-exact against the
+the reference ring's synchronous per-segment Func (allreduce.cc:301-305) -- one persistent
+launch per device per process, host contexts on leased slots.  Bit-exact against the
 reference's own outputs (golden fixtures: every Gloo dtype x {sum, product, max, min}) and the
 oracle, through every lifecycle edge: back-to-back calls on one instance, idle gaps long enough
-for an instance to leave (the next call launches a new one), two contexts at once, a context
-destroyed with its instance running, and HYDRA_RESIDENT=0."""
+for an instance to leave (the next call launches a new one), two contexts at once, more
+contexts than slots, a context destroyed while the instance runs, calls of several staging
+rounds, HYDRA_RESIDENT=0 -- and the persistent grid never holds up another stream's work."""
 import os
 import subprocess
 import sys
