@@ -38,8 +38,7 @@
 namespace hydra {
 
 constexpr int kResidentSegs = 16;
-constexpr int kResidentBlocks = 128;  // default grid (HYDRA_RESIDENT_BLOCKS: 1..1024, A/B)
-constexpr uint32_t kResidentTilesPerBlock = 2;  // a job wakes ceil(tiles / 2) workgroups
+constexpr int kResidentBlocks = 128;
 constexpr int kResidentSlots = 32;  // contexts served at once per device (lanes of wave 0)
 
 struct ResSeg {  // one c = op(a, b): vector body + ragged head / tail, split on c (as the batch)
@@ -87,9 +86,20 @@ struct alignas(64) ResDev {  // device memory, zeroed at creation
   alignas(64) ResJob job;
 };
 
-// Launch one instance (generation `gen`, `blocks` workgroups) on `s`.
-hipError_t launch_resident(ResCtl* h, ResDev* d, uint64_t gen, uint64_t idle_ticks, int blocks,
-                           hipStream_t s);
+// The grid's shape (defaults; HYDRA_RESIDENT_SHAPE=blocks,batch,solo,tiles_per_block for A/B):
+// `blocks` workgroups; each issues the loads of `batch` tiles (1, 2 or 4) together; a call of at
+// most `solo` tiles is served by workgroup 0 alone; a larger job wakes ceil(tiles /
+// tiles_per_block) workgroups (each workgroup's system-scope fences cost).
+struct ResidentShape {  // defaults from scripts/gpu_r03s.sh (profiles/r03_resident_shape_ab.json)
+  int blocks = kResidentBlocks;
+  int batch = 4;
+  uint32_t solo = 4;
+  uint32_t tiles_per_block = 4;
+};
+
+// Launch one instance (generation `gen`) on `s`.
+hipError_t launch_resident(ResCtl* h, ResDev* d, uint64_t gen, uint64_t idle_ticks,
+                           const ResidentShape& shape, hipStream_t s);
 
 // ---- host side (resident_host.cpp) -------------------------------------------------------
 // A context's slot on its device's resident reducer.  Calls through one lease are made by one

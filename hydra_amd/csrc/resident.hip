@@ -1,6 +1,8 @@
 // resident.hip -- the resident reducer's kernel (see resident.h for the protocol).
 #include "resident.h"
 
+#include <algorithm>
+
 #include "reduce_kernels.h"
 #include "reduce_ops.h"
 
@@ -18,54 +20,81 @@ __device__ __forceinline__ uint64_t pub_word(uint64_t gen, uint64_t seq) {
   return (gen << kPubShift) | (seq & kSeqMask);
 }
 
+// The ragged head / tail of a segment, one element per lane (waves 0 and 1), with its tile 0.
 template <typename E, int OP>
-__device__ __forceinline__ void res_tile(const ResSeg& g, uint32_t tile, int t) {
-  if (tile == 0 && (g.head | g.tail)) {  // ragged edges, one element per lane (waves 0 and 1)
-    constexpr int N = Vec<E>::N;
-    E* c_ = reinterpret_cast<E*>(g.c);
-    const E* a_ = reinterpret_cast<const E*>(g.a);
-    const E* b_ = reinterpret_cast<const E*>(g.b);
-    const bool head = t < g.head, tail = t >= 64 && t - 64 < g.tail;
-    if (head || tail) {
-      const ptrdiff_t i = head ? (ptrdiff_t)t - g.head : (ptrdiff_t)(g.nvec * N) + (t - 64);
-      const E ea = a_[i], eb = b_[i];
-      const E ec = g.c_old ? c_[i] : ea;
-      c_[i] = Elem<E, OP>::apply(ea, eb, ec);
+__device__ __forceinline__ void res_edges(const ResSeg& g, int t) {
+  constexpr int N = Vec<E>::N;
+  E* c_ = reinterpret_cast<E*>(g.c);
+  const E* a_ = reinterpret_cast<const E*>(g.a);
+  const E* b_ = reinterpret_cast<const E*>(g.b);
+  const bool head = t < g.head, tail = t >= 64 && t - 64 < g.tail;
+  if (head || tail) {
+    const ptrdiff_t i = head ? (ptrdiff_t)t - g.head : (ptrdiff_t)(g.nvec * N) + (t - 64);
+    const E ea = a_[i], eb = b_[i];
+    const E ec = g.c_old ? c_[i] : ea;
+    c_[i] = Elem<E, OP>::apply(ea, eb, ec);
+  }
+}
+
+// This workgroup's tiles first, first + stride, ... of the call, kResidentBatch at a time: all
+// of a batch's loads are issued before its first store, so a workgroup with several tiles pays
+// one PCIe round trip per batch rather than per tile (host operands are latency-bound).
+template <int B, typename E, int OP>
+__device__ __forceinline__ void res_run(const ResDesc& D, uint32_t first, uint32_t stride,
+                                        int t) {
+  for (uint32_t base = first; base < D.tiles; base += stride * B) {
+    u32x4 x[B], y[B], z[B];
+    char* cp[B];
+#pragma unroll
+    for (int u = 0; u < B; u++) {
+      cp[u] = nullptr;
+      const uint32_t tile = base + u * stride;
+      if (tile >= D.tiles) continue;
+      int k = 0;  // the last segment whose first tile is <= this tile (uniform)
+      for (int j = 1; j < D.count; j++)
+        if (D.s[j].tile0 <= tile) k = j;
+      const ResSeg& g = D.s[k];
+      const uint32_t lt = tile - g.tile0;
+      if (lt == 0 && (g.head | g.tail)) res_edges<E, OP>(g, t);
+      const size_t v = (size_t)lt * kBlock + t;
+      if (v < g.nvec) {
+        const size_t o = v * 16;
+        x[u] = ld_u(g.a + o);
+        y[u] = ld_u(g.b + o);
+        z[u] = g.c_old ? ld_u(g.c + o) : x[u];
+        cp[u] = g.c + o;
+      }
     }
-  }
-  const size_t v = (size_t)tile * kBlock + t;
-  if (v < g.nvec) {
-    const size_t o = v * 16;
-    const u32x4 x = ld_u(g.a + o);
-    const u32x4 y = ld_u(g.b + o);
-    const u32x4 z = g.c_old ? ld_u(g.c + o) : x;
-    st_a(g.c + o, vapply<E, OP>(x, y, z));
+#pragma unroll
+    for (int u = 0; u < B; u++)
+      if (cp[u]) st_a(cp[u], vapply<E, OP>(x[u], y[u], z[u]));
   }
 }
 
-template <typename E>
-__device__ __forceinline__ void res_op(int op, const ResSeg& g, uint32_t tile, int t) {
-  switch (op) {
-    case kSum: res_tile<E, kSum>(g, tile, t); break;
-    case kProduct: res_tile<E, kProduct>(g, tile, t); break;
-    case kMax: res_tile<E, kMax>(g, tile, t); break;
-    case kMin: res_tile<E, kMin>(g, tile, t); break;
+template <int B, typename E>
+__device__ __forceinline__ void res_op(const ResDesc& D, uint32_t first, uint32_t stride, int t) {
+  switch (D.op) {
+    case kSum: res_run<B, E, kSum>(D, first, stride, t); break;
+    case kProduct: res_run<B, E, kProduct>(D, first, stride, t); break;
+    case kMax: res_run<B, E, kMax>(D, first, stride, t); break;
+    case kMin: res_run<B, E, kMin>(D, first, stride, t); break;
   }
 }
 
-__device__ __forceinline__ void res_dispatch(int op, int dtype, const ResSeg& g, uint32_t tile,
-                                             int t) {
-  switch (dtype) {
-    case kI8: res_op<int8_t>(op, g, tile, t); break;
-    case kU8: res_op<uint8_t>(op, g, tile, t); break;
-    case kI32: res_op<int32_t>(op, g, tile, t); break;
-    case kU32: res_op<uint32_t>(op, g, tile, t); break;
-    case kI64: res_op<int64_t>(op, g, tile, t); break;
-    case kU64: res_op<uint64_t>(op, g, tile, t); break;
-    case kF32: res_op<float>(op, g, tile, t); break;
-    case kF64: res_op<double>(op, g, tile, t); break;
-    case kF16: res_op<f16_t>(op, g, tile, t); break;
-    case kBF16: res_op<bf16_t>(op, g, tile, t); break;
+template <int B>
+__device__ __forceinline__ void res_tiles(const ResDesc& D, uint32_t first, uint32_t stride,
+                                          int t) {
+  switch (D.dtype) {
+    case kI8: res_op<B, int8_t>(D, first, stride, t); break;
+    case kU8: res_op<B, uint8_t>(D, first, stride, t); break;
+    case kI32: res_op<B, int32_t>(D, first, stride, t); break;
+    case kU32: res_op<B, uint32_t>(D, first, stride, t); break;
+    case kI64: res_op<B, int64_t>(D, first, stride, t); break;
+    case kU64: res_op<B, uint64_t>(D, first, stride, t); break;
+    case kF32: res_op<B, float>(D, first, stride, t); break;
+    case kF64: res_op<B, double>(D, first, stride, t); break;
+    case kF16: res_op<B, f16_t>(D, first, stride, t); break;
+    case kBF16: res_op<B, bf16_t>(D, first, stride, t); break;
   }
 }
 
@@ -81,19 +110,6 @@ __device__ __forceinline__ T ld_agent(const T* p) {
 constexpr int kDescWords = (int)(sizeof(ResDesc) / 8);
 static_assert(sizeof(ResDesc) % 8 == 0 && kDescWords <= 2 * 64, "descriptor copy: 2 words/lane");
 
-// A call of at most kSoloTiles tiles (16 KiB of c) is served by workgroup 0 alone: no device
-// hop to the other workgroups, no arrival counter -- the reference ring's small segments.
-constexpr uint32_t kSoloTiles = 4;
-
-__device__ __forceinline__ void res_tiles(const ResDesc& D, uint32_t first, uint32_t stride,
-                                          int t) {
-  for (uint32_t tile = first; tile < D.tiles; tile += stride) {
-    int k = 0;  // the last segment whose first tile is <= this tile (uniform)
-    for (int j = 1; j < D.count; j++)
-      if (D.s[j].tile0 <= tile) k = j;
-    res_dispatch(D.op, D.dtype, D.s[k], tile - D.s[k].tile0, t);
-  }
-}
 
 // Workgroup 0 (wave 0) picks the next call: the first pending slot after the one served last.
 __device__ __forceinline__ int pick_slot(uint64_t pending, int last) {
@@ -115,8 +131,13 @@ __device__ __forceinline__ bool wait_finished(ResCtl* h, ResDev* d, uint64_t wan
   return true;
 }
 
+// B: tiles whose loads a workgroup issues together; a call of at most `solo` tiles is served by
+// workgroup 0 alone (no device hop to the others, no arrival counter); a job wakes
+// ceil(tiles / tpb) workgroups.
+template <int B>
 __global__ __launch_bounds__(kBlock) void k_resident(ResCtl* h, ResDev* d, uint64_t gen,
-                                                     uint64_t idle_ticks) {
+                                                     uint64_t idle_ticks, uint32_t solo,
+                                                     uint32_t tpb) {
   __shared__ uint64_t s_seq;
   __shared__ int s_slot;
   __shared__ int s_mode;  // 0 a published job, 1 workgroup 0 alone, 2 leave, 3 not in this job
@@ -161,7 +182,7 @@ __global__ __launch_bounds__(kBlock) void k_resident(ResCtl* h, ResDev* d, uint6
           if (t + 64 < kDescWords) w1 = src[t + 64];
           // word 1 holds {count, tiles}: a small call stays in this workgroup
           const uint32_t tiles = (uint32_t)(__shfl((unsigned long long)w0, 1) >> 32);
-          if (tiles <= kSoloTiles) {
+          if (tiles <= solo) {
             uint64_t* dst = reinterpret_cast<uint64_t*>(&s_desc);
             if (t < kDescWords) dst[t] = w0;
             if (t + 64 < kDescWords) dst[t + 64] = w1;
@@ -169,8 +190,7 @@ __global__ __launch_bounds__(kBlock) void k_resident(ResCtl* h, ResDev* d, uint6
           } else if (job != 0 && !wait_finished(h, d, pub_word(gen, job))) {
             mode = 2;  // a workgroup never finished the last job: leave (err is set)
           } else {  // the job record, write-through, then publish it
-            const uint32_t nwg = min(gridDim.x, max(2u, (tiles + kResidentTilesPerBlock - 1) /
-                                                            kResidentTilesPerBlock));
+            const uint32_t nwg = min(gridDim.x, max(2u, (tiles + tpb - 1) / tpb));
             if (t == 0) s_nwg = nwg;
             uint64_t* dst = reinterpret_cast<uint64_t*>(&d->job.desc);
             if (t < kDescWords)
@@ -246,7 +266,7 @@ __global__ __launch_bounds__(kBlock) void k_resident(ResCtl* h, ResDev* d, uint6
       continue;
     }
     if (mode == 1) {  // workgroup 0 alone: every tile here, then the slot's completion word
-      res_tiles(s_desc, 0, 1, t);
+      res_tiles<B>(s_desc, 0, 1, t);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (t == 0) {
@@ -265,7 +285,7 @@ __global__ __launch_bounds__(kBlock) void k_resident(ResCtl* h, ResDev* d, uint6
       for (int q = t; q < kDescWords; q += kBlock) dst[q] = ld_agent(src + kHead + q);
     }
     __syncthreads();
-    res_tiles(s_desc, blockIdx.x, s_nwg, t);
+    res_tiles<B>(s_desc, blockIdx.x, s_nwg, t);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (t == 0) {
@@ -290,9 +310,18 @@ __global__ __launch_bounds__(kBlock) void k_resident(ResCtl* h, ResDev* d, uint6
 
 }  // namespace
 
-hipError_t launch_resident(ResCtl* h, ResDev* d, uint64_t gen, uint64_t idle_ticks, int blocks,
-                           hipStream_t s) {
-  hipLaunchKernelGGL(k_resident, dim3(blocks), dim3(kBlock), 0, s, h, d, gen, idle_ticks);
+hipError_t launch_resident(ResCtl* h, ResDev* d, uint64_t gen, uint64_t idle_ticks,
+                           const ResidentShape& shape, hipStream_t s) {
+  const uint32_t solo = shape.solo, tpb = std::max(1u, shape.tiles_per_block);
+  if (shape.batch >= 4)
+    hipLaunchKernelGGL(k_resident<4>, dim3(shape.blocks), dim3(kBlock), 0, s, h, d, gen,
+                       idle_ticks, solo, tpb);
+  else if (shape.batch == 2)
+    hipLaunchKernelGGL(k_resident<2>, dim3(shape.blocks), dim3(kBlock), 0, s, h, d, gen,
+                       idle_ticks, solo, tpb);
+  else
+    hipLaunchKernelGGL(k_resident<1>, dim3(shape.blocks), dim3(kBlock), 0, s, h, d, gen,
+                       idle_ticks, solo, tpb);
   return hipGetLastError();
 }
 

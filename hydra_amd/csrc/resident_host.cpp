@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -53,13 +54,22 @@ uint64_t idle_ticks() {  // s_memrealtime runs at 100 MHz
   return t;
 }
 
-int grid_blocks() {
-  static const int b = [] {
-    const char* v = std::getenv("HYDRA_RESIDENT_BLOCKS");
-    const int k = v ? std::atoi(v) : kResidentBlocks;
-    return std::max(1, std::min(k, 1024));
+const ResidentShape& shape() {
+  static const ResidentShape sh = [] {
+    ResidentShape r;
+    if (const char* v = std::getenv("HYDRA_RESIDENT_SHAPE")) {
+      int b = r.blocks, u = r.batch;
+      unsigned so = r.solo, tp = r.tiles_per_block;
+      if (std::sscanf(v, "%d,%d,%u,%u", &b, &u, &so, &tp) >= 1) {
+        r.blocks = std::max(1, std::min(b, 1024));
+        r.batch = u >= 4 ? 4 : u >= 2 ? 2 : 1;
+        r.solo = std::min(so, 64u);
+        r.tiles_per_block = std::max(1u, std::min(tp, 64u));
+      }
+    }
+    return r;
   }();
-  return b;
+  return sh;
 }
 
 template <typename T>
@@ -169,7 +179,7 @@ int ensure_running(ResidentServer* v) {
   int prev = -1;
   (void)hipGetDevice(&prev);
   if (prev != v->device) (void)hipSetDevice(v->device);
-  const hipError_t e = launch_resident(v->h_dev, v->d, ++v->gen, idle_ticks(), grid_blocks(), v->s);
+  const hipError_t e = launch_resident(v->h_dev, v->d, ++v->gen, idle_ticks(), shape(), v->s);
   if (prev >= 0 && prev != v->device) (void)hipSetDevice(prev);
   if (e != hipSuccess) {
     vol(v->h->alive) = 0u;
