@@ -296,6 +296,44 @@ def main_algo() -> None:
     print(f"wrote {len(out)} arrays to golden_algo.npz")
 
 
+# Every band edge of the two split tables (pipeallreduce-a.h:137-376), as written there.
+SPLIT_EDGES = (6144, 6145, 65536, 65537, 114975, 131072, 262144, 262145, 524287, 524288, 524289,
+               828343, 828344, 1048576, 1048577, 2097152, 2097153, 4194304, 4194305, 8388608,
+               8388609, 16777216, 16777217, 33554432, 33554433, 67108864, 67108865)
+
+
+def split_cases() -> list:
+    ns = set(range(0, 130)) | {1000, 1500000, 1500001, 200003, 1 << 28, (1 << 28) + 77}
+    for e in SPLIT_EDGES:
+        ns |= {e + d for d in range(-3, 4)}
+    rng = np.random.default_rng(2024)
+    ns |= {int(v) for v in rng.integers(1, 1 << 27, 400)}
+    return sorted(ns)
+
+
+def main_split() -> None:
+    """The two-rail split from the reference's own compiled methods
+    (oracle/split_ref.py -> _ref/libsplit_ref.so): (table, P, n) -> (e1, e2) for both tables,
+    P = 1..9, every band edge +-3, the first 130 n and 400 random n < 2^27."""
+    from oracle import split_ref
+
+    lib = split_ref.load(split_ref.build())
+    rows = []
+    for table in (0, 1):
+        for P in range(1, 10):
+            for n in split_cases():
+                e1, e2 = split_ref.ref_split(lib, table, P, n)
+                rows.append([table, P, n, e1, e2])
+    meta = {"generator": "oracle/gen_golden.py --split",
+            "reference": "APipeAllreduceOptions::calculateElements_AA / _AG "
+                         "(gloo/gloo/pipeallreduce-a.h:137-376), compiled by oracle/split_ref.py "
+                         "(g++ -O3 -DNDEBUG)",
+            "columns": ["table (0 = AA, 1 = AG)", "P", "n", "e1", "e2"], "rows": rows}
+    with open(os.path.join(GOLD, "golden_split.json"), "w") as f:
+        json.dump(meta, f, separators=(",", ":"))
+    print(f"wrote {len(rows)} split rows to golden_split.json")
+
+
 def gen_new_test(meta: dict) -> None:
     """AllreduceNewTest.Default (test/allreduce_test.cc:302-362): confirm the reference meets the
     closed form k*stride^2 + stride(stride-1)/2 for uint64, every combination we test."""
@@ -413,6 +451,9 @@ def main() -> None:
 
 
 if __name__ == "__main__":
+    if "--split" in sys.argv[1:]:  # needs only /root/reference's pipeallreduce-a.h and g++
+        main_split()
+        raise SystemExit(0)
     if not O.ref_available():
         raise SystemExit("oracle/_ref/libgloo_ref.so missing: make -C oracle ref")
     main_algo() if "--algo" in sys.argv[1:] else main()

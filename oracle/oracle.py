@@ -38,6 +38,11 @@ def build(force: bool = False) -> None:
     if os.path.isdir("/root/reference/gloo"):
         if force or not os.path.exists(LIBREF):
             subprocess.check_call(["make", "-s", "-j8", "-C", HERE, "ref"])
+        # the reference's two-rail split, compiled from its header text (split_ref.py)
+        from oracle import split_ref
+
+        if force or not os.path.exists(split_ref.OUT):
+            split_ref.build()
         # the drop-in harness links libhydra_hip.so too: make rebuilds it when either changed
         if os.path.exists(os.path.join(os.path.dirname(HERE), "hydra_amd", "libhydra_hip.so")):
             subprocess.check_call(["make", "-s", "-C", HERE, "dropin"])

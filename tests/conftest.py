@@ -59,6 +59,16 @@ def golden_meta():
 
 
 @pytest.fixture(scope="session")
+def golden_split():
+    """The two-rail split from the reference's own compiled calculateElements_AA / _AG
+    (oracle/gen_golden.py --split): rows [table, P, n, e1, e2]."""
+    import json
+
+    with open(os.path.join(GOLDEN, "golden_split.json")) as f:
+        return json.load(f)["rows"]
+
+
+@pytest.fixture(scope="session")
 def golden_algo():
     """Algorithm-API fixtures (oracle/gen_golden.py --algo): AllreduceHalvingDoubling<T> and
     old-style AllreduceBcube<T> inputs and results, meta."""
