@@ -422,6 +422,15 @@ def run_multi(args):
         os.environ.setdefault("MASTER_PORT", "29533")
         os.environ.setdefault("RANK", "0")
         os.environ.setdefault("WORLD_SIZE", "1")
+    # Rehearsal on a one-GPU box (never the driver's run): every rank on GPU 0, each with its own
+    # RCCL host identity, so RCCL accepts N ranks on one GPU and links them over loopback
+    # sockets.  The whole N>1 path runs with real RCCL ranks; the rates are socket rates.
+    rehearse = os.environ.get("HYDRA_BENCH_SHARED_GPU") == "1"
+    if rehearse:
+        local = 0
+        os.environ["NCCL_HOSTID"] = f"hydra-rehearsal-rank-{rank}"
+        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+        os.environ.setdefault("NCCL_IB_DISABLE", "1")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist.init_process_group("nccl", device_id=dev)
@@ -433,6 +442,9 @@ def run_multi(args):
         res = ring.bench_allreduce(args, dev, cpu_baseline=base)
     finally:
         dist.destroy_process_group()
+    if rehearse:
+        res["rehearsal"] = ("HYDRA_BENCH_SHARED_GPU=1: all ranks on one GPU, RCCL over loopback "
+                            "sockets -- a code-path check, not an xGMI rate")
     if rank == 0:
         print(json.dumps(res), flush=True)
 

@@ -1,0 +1,164 @@
+"""The RCCL executor with 2 and 4 REAL RCCL ranks: every rank a process on the test box's one
+GPU, each process giving RCCL its own host identity (NCCL_HOSTID), so RCCL's duplicate-GPU check
+sees 2 / 4 hosts and connects the ranks over its socket transport on loopback (NCCL_SOCKET_IFNAME
+=lo).  The library's RCCL code paths then run across ranks exactly as on an 8-GPU node --
+ncclCommInitRank with nranks > 1, p2p groups with several peers, ncclAllToAll / ncclAllGather,
+the fold kernels between them, cross-stream events, two communicators at once (the two rails),
+ncclCommCount -- only the wire differs (sockets instead of xGMI, so no rate is measured here).
+
+Every result is compared with the reference's outputs: the oracle's restatement of the ring
+(`allreduce.cc:147-422`, pinned to the reference's own build), gloo::reduce (`reduce.cc`), the
+two-rail split (`pipeallreduce-a.h:296-376`) -- bit for bit; ncclAllReduce (RCCL's own order)
+within a stated fp32 tolerance; config 5's bf16 + fp32 accumulation (no reference counterpart)
+exact on integer-valued inputs."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+# RCCL sees one host per rank (its duplicate-GPU check compares host hash + bus id) and talks
+# over loopback sockets; no InfiniBand.
+RANK_ENV = {"NCCL_SOCKET_IFNAME": "lo", "NCCL_IB_DISABLE": "1"}
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _bits(x):
+    return x.view(f"u{x.itemsize}")
+
+
+def _worker(rank, world, port, q):
+    import sys
+
+    sys.path.insert(0, ROOT)
+    os.environ.update(RANK_ENV)
+    os.environ["NCCL_HOSTID"] = f"hydra-test-rank-{rank}"
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch
+    import torch.distributed as dist
+
+    from hydra_amd import _lib, ring, synth
+    from oracle import oracle as O
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    res = {}
+    comms = []
+    try:
+        torch.cuda.set_device(0)
+        dev = torch.device("cuda", 0)
+        comm = ring.XgmiComm(rank, world, 0, ring.exchange_unique_id(rank))
+        comms.append(comm)
+        info = comm.info()
+        res["comm_info"] = info == {"nccl_comm_count": world, "nccl_user_rank": rank,
+                                    "nccl_device": 0}
+
+        def run(tag, x, exp, **kw):
+            t = torch.from_numpy(x.copy()).to(dev)
+            comm.allreduce_(t, **kw)
+            comm.wait(60000)
+            res[tag] = bool(np.array_equal(_bits(t.cpu().numpy()), _bits(exp)))
+
+        # fp32, fold-order-sensitive inputs: the reference ring's bits on every rank
+        for algo, n, ms, ch in (("ring", 1_000_003, 0, 0), ("ring", 100_003, 4096, 0),
+                                ("direct", 1_000_003, 0, 1 << 20), ("direct", 4 << 20, 0, 0),
+                                ("direct", 100_003, 4096, 16384), ("a2a", 4 << 20, 0, 0),
+                                ("auto", 4 << 20, 0, 0), ("auto", 1_000_003, 0, 0)):
+            xs = [synth.stress_f32(world, r, n) for r in range(world)]
+            run(f"{algo}_f32_n{n}_ms{ms}_ch{ch}", xs[rank], O.ring_result(xs, ms or (1 << 20)),
+                algo=algo, max_segment=ms, chunk_bytes=ch)
+        # int32
+        n = 1 << 20
+        xi = [synth.int32_bucket(world, r, n) for r in range(world)]
+        for algo in ("direct", "a2a", "ring"):
+            run(f"{algo}_i32", xi[rank], O.ring_result(xi, dtype_code=_lib.INT32), algo=algo,
+                dtype_code=_lib.INT32)
+        # config 5's arithmetic: bf16 bucket, fp32 accumulation; integer-valued -> exact
+        n = 1 << 20
+        vals = [((np.arange(n) * (r + 3)) % 61 - 30).astype(np.float32) for r in range(world)]
+        expb = synth.bf16_bits(np.sum(vals, axis=0).astype(np.float32))
+        for algo in ("direct", "a2a"):
+            run(f"{algo}_bf16_acc32", synth.bf16_bits(vals[rank]), expb, algo=algo,
+                dtype_code=_lib.BFLOAT16, flags=_lib.ACC_F32)
+        # ncclAllReduce (RCCL's order): |got - sum| <= (P-1) * 2^-24 * sum|x| per element
+        n = 1 << 20
+        xs = [synth.stress_f32(world, r, n) for r in range(world)]
+        t = torch.from_numpy(xs[rank].copy()).to(dev)
+        comm.allreduce_(t, algo="rccl")
+        comm.wait(60000)
+        got = t.cpu().numpy().astype(np.float64)
+        st = np.stack(xs).astype(np.float64)
+        tol = (world - 1) * 2.0 ** -24 * np.abs(st).sum(axis=0) + 1e-30
+        res["rccl_f32_tol"] = bool(np.all(np.abs(got - st.sum(axis=0)) <= tol))
+        # gloo::reduce to a root (only the root's bucket is defined)
+        root = world - 1
+        n = 1_000_003
+        xs = [synth.stress_f32(world, r, n) for r in range(world)]
+        t = torch.from_numpy(xs[rank].copy()).to(dev)
+        comm.reduce_(t, root)
+        comm.wait(60000)
+        if rank == root:
+            outs = [x.copy() for x in xs]
+            O.reduce(outs, None, root)
+            res["reduce_root"] = bool(np.array_equal(_bits(t.cpu().numpy()), _bits(outs[root])))
+        # bew_allreduce_a on device: two communicators (two rails) at once, the reference split
+        comm2 = ring.XgmiComm(rank, world, 0, ring.exchange_unique_id(rank))
+        comms.append(comm2)
+        for n in (3_000_001, 1 << 20):
+            xs = [synth.stress_f32(world, r, n) for r in range(world)]
+            t = torch.from_numpy(xs[rank].copy()).to(dev)
+            comm.apipe_allreduce_(comm2, t, table=0)
+            comm.wait(60000)
+            comm2.wait(60000)
+            e1, _ = O.split_aa(world, n)
+            exp = np.empty(n, np.float32)
+            if e1:
+                exp[:e1] = O.ring_result([x[:e1].copy() for x in xs])
+            if e1 < n:
+                exp[e1:] = O.ring_result([x[e1:].copy() for x in xs])
+            res[f"apipe_n{n}"] = bool(np.array_equal(_bits(t.cpu().numpy()), _bits(exp)))
+        q.put((rank, res))
+    except Exception as e:  # report instead of hanging the parent
+        import traceback
+
+        q.put((rank, repr(e) + traceback.format_exc()[-1500:]))
+    finally:
+        for c in comms:
+            try:
+                c.close()
+            except Exception:
+                pass
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_rccl_executor_across_ranks(gpu, world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        res = dict(q.get(timeout=150) for _ in range(world))
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    bad = {r: v for r, v in res.items() if not (isinstance(v, dict) and all(v.values()))}
+    assert not bad, bad
+    assert "reduce_root" in res[world - 1]
+    assert len(res[0]) >= 16, res[0]
