@@ -276,11 +276,6 @@ int hydra_ctx_create(int device, hydra_ctx_t* out) {
     delete x;
     return rc;
   }
-  if (e != hipSuccess) {
-    ctx_release(x);
-    delete x;
-    return hip_fail(e, "hydra_ctx_create");
-  }
   *out = x;
   return ok();
 }
