@@ -179,7 +179,14 @@ int ensure_running(ResidentServer* v) {
   int prev = -1;
   (void)hipGetDevice(&prev);
   if (prev != v->device) (void)hipSetDevice(v->device);
-  const hipError_t e = launch_resident(v->h_dev, v->d, ++v->gen, idle_ticks(), shape(), v->s);
+  hipError_t e = hipSuccess;
+  if (vol(v->h->err) != 0u) {
+    // the last instance left on an expired wait: its job counter may hold a partial count, so
+    // the device record starts over (ordered after that instance on the same stream)
+    e = hipMemsetAsync(v->d, 0, sizeof(ResDev), v->s);
+    vol(v->h->err) = 0u;
+  }
+  if (e == hipSuccess) e = launch_resident(v->h_dev, v->d, ++v->gen, idle_ticks(), shape(), v->s);
   if (prev >= 0 && prev != v->device) (void)hipSetDevice(prev);
   if (e != hipSuccess) {
     vol(v->h->alive) = 0u;
