@@ -173,4 +173,4 @@ def test_rccl_executor_across_ranks(gpu, world):
     bad = {r: v for r, v in res.items() if not (isinstance(v, dict) and all(v.values()))}
     assert not bad, bad
     assert "reduce_root" in res[world - 1]
-    assert len(res[0]) >= 16, res[0]
+    assert len(res[0]) >= 15, res[0]
