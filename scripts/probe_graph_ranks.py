@@ -26,6 +26,7 @@ def worker(rank, world, port, out):
                        "NCCL_HOSTID": f"hydra-probe-rank-{rank}", "MASTER_ADDR": "127.0.0.1",
                        "MASTER_PORT": str(port)})
     log = open(os.path.join(out, f"graph_rank{rank}.log"), "w", buffering=1)
+    faulthandler.enable(file=log)  # a native crash leaves the Python stack here
     faulthandler.dump_traceback_later(HANG_S, repeat=True, file=log)
     t0 = time.time()
 
@@ -45,7 +46,7 @@ def worker(rank, world, port, out):
     comm = ring.XgmiComm(rank, world, 0, ring.exchange_unique_id(rank))
     say("comm up")
     n = 1 << 20
-    for algo in ("rccl", "a2a", "direct", "ring"):
+    for algo in os.environ.get("ALGOS", "rccl,a2a,direct,ring").split(","):
         xs = [[synth.stress_f32(world, r, n, seed=s) for r in range(world)] for s in (5, 6, 7)]
         t = torch.from_numpy(xs[0][rank].copy()).to(dev)
         comm.allreduce_(t, algo=algo)
@@ -107,6 +108,7 @@ def main():
             rc = rc or 1
     for r in range(2):
         print(open(os.path.join(out, f"graph_rank{r}.log")).read()[-3000:])
+    print("exit codes:", [p.exitcode for p in procs])
     sys.exit(rc)
 
 
