@@ -174,3 +174,88 @@ def test_rccl_executor_across_ranks(gpu, world):
     assert not bad, bad
     assert "reduce_root" in res[world - 1]
     assert len(res[0]) >= 15, res[0]
+
+
+def _fault_worker(rank, world, port, q, mode):
+    """The reference's TestTimeout (allreduce_test.cc:381-397) on the device allreduce across
+    real RCCL ranks: rank 1 never joins ("absent") or exits abruptly ("dead"); rank 0's
+    hydra_comm_wait must end with HYDRA_ERR_TIMEOUT ("Timed out waiting ...") and abort, and the
+    communicator must tear down cleanly."""
+    import sys
+
+    sys.path.insert(0, ROOT)
+    os.environ.update(RANK_ENV)
+    os.environ["NCCL_HOSTID"] = f"hydra-test-rank-{rank}"
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch
+    import torch.distributed as dist
+
+    from hydra_amd import _lib, ring
+
+    res = {}
+    try:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        torch.cuda.set_device(0)
+        dev = torch.device("cuda", 0)
+        comm = ring.XgmiComm(rank, world, 0, ring.exchange_unique_id(rank))
+        t = torch.ones(1 << 20, dtype=torch.float32, device=dev)
+        comm.allreduce_(t, algo="direct")
+        comm.wait(30000)
+        res["warm_up"] = float(t[0]) == float(world)
+        dist.barrier()
+        if rank == 1:
+            if mode == "dead":
+                q.put((rank, res))
+                q.close()
+                q.join_thread()  # flushed before the abrupt exit
+                os._exit(0)
+            dist.barrier()  # rank 0 reports after its wait ended
+        else:
+            if mode == "dead":
+                import time
+
+                time.sleep(2.0)
+            comm.allreduce_(t, algo="direct")
+            try:
+                comm.wait(3000)
+                res["timed_out"] = False
+            except _lib.HydraError as e:
+                res["timed_out"] = e.code == _lib.ERR_TIMEOUT and "Timed out waiting" in str(e)
+            try:  # an aborted communicator refuses further work
+                comm.allreduce_(t, algo="direct")
+                res["refuses_after_abort"] = False
+            except _lib.HydraError:
+                res["refuses_after_abort"] = True
+            if mode == "absent":
+                dist.barrier()
+        comm.close()
+        res["closed"] = True
+    except Exception as e:  # report instead of hanging the parent
+        import traceback
+
+        res["error"] = repr(e) + traceback.format_exc()[-800:]
+    q.put((rank, res))
+    q.close()
+    q.join_thread()
+    os._exit(0)
+
+
+@pytest.mark.parametrize("mode", ["absent", "dead"])
+def test_rccl_wait_times_out_on_missing_peer(gpu, mode):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_fault_worker, args=(r, 2, port, q, mode)) for r in range(2)]
+    for p in procs:
+        p.start()
+    try:
+        res = dict(q.get(timeout=90) for _ in range(2))
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    assert res[0] == {"warm_up": True, "timed_out": True, "refuses_after_abort": True,
+                      "closed": True}, res
+    assert res[1].get("warm_up") is True and "error" not in res[1], res
