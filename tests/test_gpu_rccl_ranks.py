@@ -1,6 +1,6 @@
-"""The RCCL executor with 2, 3 and 4 REAL RCCL ranks: every rank a process on the test box's one
+"""The RCCL executor with 2, 3, 4 and 8 REAL RCCL ranks: every rank a process on the test box's one
 GPU, each process giving RCCL its own host identity (NCCL_HOSTID), so RCCL's duplicate-GPU check
-sees 2 / 3 / 4 hosts and connects the ranks over its socket transport on loopback (NCCL_SOCKET_IFNAME
+sees 2 / 3 / 4 / 8 hosts and connects the ranks over its socket transport on loopback (NCCL_SOCKET_IFNAME
 =lo).  The library's RCCL code paths then run across ranks exactly as on an 8-GPU node --
 ncclCommInitRank with nranks > 1, p2p groups with several peers, ncclAllToAll / ncclAllGather,
 the fold kernels between them, cross-stream events, two communicators at once (the two rails),
@@ -167,7 +167,7 @@ def _spawn(target, world, timeout=150):
                 p.kill()
 
 
-@pytest.mark.parametrize("world", [2, 3, 4])
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
 def test_rccl_executor_across_ranks(gpu, world):
     res = _spawn(_worker, world)
     bad = {r: v for r, v in res.items() if not (isinstance(v, dict) and all(v.values()))}
