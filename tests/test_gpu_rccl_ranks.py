@@ -151,11 +151,13 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def _spawn(target, world, timeout=150):
+def _spawn(target, world, *extra, timeout=150):
+    """Run target(rank, world, port, queue, *extra) in `world` spawned processes; collect one
+    (rank, result) from each; never leave a process behind."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=target, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=target, args=(r, world, port, q) + extra) for r in range(world)]
     for p in procs:
         p.start()
     try:
@@ -243,19 +245,7 @@ def _fault_worker(rank, world, port, q, mode):
 
 @pytest.mark.parametrize("mode", ["absent", "dead"])
 def test_rccl_wait_times_out_on_missing_peer(gpu, mode):
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_fault_worker, args=(r, 2, port, q, mode)) for r in range(2)]
-    for p in procs:
-        p.start()
-    try:
-        res = dict(q.get(timeout=90) for _ in range(2))
-    finally:
-        for p in procs:
-            p.join(timeout=30)
-            if p.is_alive():
-                p.kill()
+    res = _spawn(_fault_worker, 2, mode, timeout=90)
     assert res[0] == {"warm_up": True, "timed_out": True, "refuses_after_abort": True,
                       "closed": True}, res
     assert res[1].get("warm_up") is True and "error" not in res[1], res
