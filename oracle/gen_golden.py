@@ -334,6 +334,40 @@ def main_split() -> None:
     print(f"wrote {len(rows)} split rows to golden_split.json")
 
 
+# Config 5's arithmetic (bf16 bucket, fp32 accumulation, one rounding) on the reference: its own
+# ring over the bf16 values widened exactly to fp32 is the fp32 fold in the reference order; one
+# round-to-nearest-even to bf16 gives what k_fold<bf16, ACC32> must produce.  n is a multiple of
+# 2P below P x 512 Ki, so the fp32 and the bf16 geometries cut identical element blocks.
+BF16_CASES = [(P, 2 * P * k) for P in (2, 3, 4, 8) for k in (7, 20001)]
+
+
+def main_bf16() -> None:
+    if not O.ref_available():
+        raise SystemExit("oracle/_ref/libgloo_ref.so missing: make -C oracle ref")
+    out: dict = {}
+    rows = []
+    for P, n in BF16_CASES:
+        ns4, sb4, S4 = O.ring_plan(P, n, 4)
+        ns2, sb2, S2 = O.ring_plan(P, n, 2)
+        assert (ns4, sb4 // 4, S4) == (ns2, sb2 // 2, S2), (P, n)  # same element blocks
+        xb = [synth.bf16_bits(synth.stress_f32(P, r, n)) for r in range(P)]
+        outs = [[synth.bf16_to_f32(x).copy()] for x in xb]
+        O.ref_allreduce(P, outs)
+        for r in range(1, P):
+            assert np.array_equal(outs[r][0].view(np.uint32), outs[0][0].view(np.uint32))
+        key = f"bf16acc32_P{P}_n{n}"
+        out[key] = synth.bf16_bits(outs[0][0])
+        rows.append({"key": key, "P": P, "n": n, "inputs_sha256": sha(np.stack(xb))})
+    np.savez_compressed(os.path.join(GOLD, "golden_bf16.npz"), **out)
+    with open(os.path.join(GOLD, "golden_bf16.json"), "w") as f:
+        json.dump({"generator": "oracle/gen_golden.py --bf16",
+                   "what": "bf16 inputs synth.bf16_bits(synth.stress_f32(P, r, n)); the "
+                           "reference's gloo::allreduce RING (maxSegmentSize 1 MiB) on their "
+                           "exact fp32 widening; output = RNE of its fp32 result to bf16",
+                   "cases": rows}, f, indent=1)
+    print(f"wrote {len(out)} bf16 cases to golden_bf16.npz")
+
+
 def gen_new_test(meta: dict) -> None:
     """AllreduceNewTest.Default (test/allreduce_test.cc:302-362): confirm the reference meets the
     closed form k*stride^2 + stride(stride-1)/2 for uint64, every combination we test."""
@@ -453,6 +487,9 @@ def main() -> None:
 if __name__ == "__main__":
     if "--split" in sys.argv[1:]:  # needs only /root/reference's pipeallreduce-a.h and g++
         main_split()
+        raise SystemExit(0)
+    if "--bf16" in sys.argv[1:]:
+        main_bf16()
         raise SystemExit(0)
     if not O.ref_available():
         raise SystemExit("oracle/_ref/libgloo_ref.so missing: make -C oracle ref")

@@ -1,7 +1,8 @@
 """The multi-GPU allreduce on one MI355X: hydra_allreduce_simulate runs every rank's plan with
 the real HIP kernels and the real cross-stream event edges, device copies standing in for xGMI.
 Bar: bit-exact vs the reference ring (oracle) for fp32/int32/f16; bf16 with fp32 accumulation
-within one bf16 rounding of the fp64 sum (no reference counterpart)."""
+bit-exact vs the reference's own fp32 ring on the widened values + one RNE rounding (fixtures),
+and within one bf16 rounding of the fp64 sum."""
 import numpy as np
 import pytest
 
@@ -78,6 +79,39 @@ def test_simulated_bf16_fp32_accumulate(gpu):
     # and every rank holds the same bits
     ref0 = bufs[0].cpu().numpy()
     assert all(np.array_equal(b.cpu().numpy(), ref0) for b in bufs)
+
+
+@pytest.fixture(scope="module")
+def golden_bf16():
+    import json
+    import os
+
+    g = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    with open(os.path.join(g, "golden_bf16.json")) as f:
+        meta = json.load(f)
+    return np.load(os.path.join(g, "golden_bf16.npz"), allow_pickle=False), meta["cases"]
+
+
+@pytest.mark.parametrize("algo", ["direct", "a2a"])
+def test_simulated_bf16_acc32_vs_reference_ring(gpu, golden_bf16, algo):
+    """Config 5's arithmetic pinned to the reference: the bf16 bucket folded with fp32
+    accumulation (k_fold<bf16, ACC32>, DIRECT / A2A plans) equals, bit for bit, the reference's
+    own gloo::allreduce RING run on the same values widened to fp32, rounded once (RNE) to bf16
+    (tests/golden/golden_bf16.*, oracle/gen_golden.py --bf16): P = 2, 3, 4, 8."""
+    import hashlib
+
+    import torch
+
+    npz, cases = golden_bf16
+    for c in cases:
+        P, n = c["P"], c["n"]
+        xs = [synth.bf16_bits(synth.stress_f32(P, r, n)) for r in range(P)]
+        assert hashlib.sha256(np.stack(xs).tobytes()).hexdigest() == c["inputs_sha256"]
+        bufs = [torch.from_numpy(x.view(np.int16).copy()).to(gpu) for x in xs]
+        ring.simulate(bufs, algo=algo, dtype_code=_lib.BFLOAT16, flags=_lib.ACC_F32)
+        exp = npz[c["key"]]
+        for r, b in enumerate(bufs):
+            assert np.array_equal(b.cpu().numpy().view(np.uint16), exp), (algo, P, n, r)
 
 
 def test_acc_f32_rejected_on_ring(gpu):
