@@ -6,7 +6,7 @@ hydra_reduce / hydra_fold launches on its GPU bucket, exactly as the RCCL execut
 (xgmi_allreduce.cpp launch_compute), so the cross-process schedule, the block ownership and the
 fold order are checked end to end on the hardware against the reference's outputs (the oracle's
 ring result, `allreduce.cc:147-422`; gloo::reduce; the old-style rings; bcube).  bf16 with fp32
-accumulation (config 5, parity unpinned: no reference counterpart) is compared with the CPU
+accumulation (config 5; pinned to the reference ring in test_gpu_xgmi.py) is compared with the CPU
 restatement of k_fold<bf16, ACC32> run on the same ranks."""
 import os
 import socket
