@@ -100,6 +100,19 @@ def _worker(rank, world, port, q):
         for algo in ("direct",) + (("a2a",) if world != 3 else ()):
             run(f"{algo}_bf16_acc32", synth.bf16_bits(vals[rank]), expb, algo=algo,
                 dtype_code=_lib.BFLOAT16, flags=_lib.ACC_F32)
+        # config 5's arithmetic against the reference: its fp32 ring on the widened bf16 values,
+        # rounded once (tests/golden/golden_bf16.*, oracle/gen_golden.py --bf16)
+        import json
+
+        gdir = os.path.join(ROOT, "tests", "golden")
+        gnpz = np.load(os.path.join(gdir, "golden_bf16.npz"), allow_pickle=False)
+        with open(os.path.join(gdir, "golden_bf16.json")) as f:
+            gcases = [c for c in json.load(f)["cases"] if c["P"] == world]
+        for c in gcases:
+            xb = synth.bf16_bits(synth.stress_f32(world, rank, c["n"]))
+            for algo in ("direct", "a2a"):
+                run(f"{algo}_bf16_acc32_vs_ref_n{c['n']}", xb, gnpz[c["key"]], algo=algo,
+                    dtype_code=_lib.BFLOAT16, flags=_lib.ACC_F32)
         # ncclAllReduce (RCCL's order): |got - sum| <= (P-1) * 2^-24 * sum|x| per element
         n = 1 << 20
         xs = [synth.stress_f32(world, r, n) for r in range(world)]
