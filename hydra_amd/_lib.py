@@ -41,6 +41,7 @@ EXPORTS = [  # every symbol include/hydra_hip.h declares
     "hydra_peer_close", "hydra_peer_set_option", "hydra_peer_error", "hydra_peer_allreduce",
     "hydra_peer_detach", "hydra_peer_destroy", "hydra_comm_wait",
     "hydra_reduce_root", "hydra_reduce_root_plan", "hydra_reduce_root_simulate",
+    "hydra_comm_profile", "hydra_comm_phases",
 ]
 
 (ALGO_AUTO, ALGO_RING, ALGO_DIRECT, ALGO_RCCL, ALGO_A2A, ALGO_RING_OLD, ALGO_RING_CHUNKED,
@@ -50,6 +51,8 @@ ALGOS = {"auto": ALGO_AUTO, "ring": ALGO_RING, "direct": ALGO_DIRECT, "rccl": AL
          "ring_chunked": ALGO_RING_CHUNKED, "bcube": ALGO_BCUBE,
          "halving_doubling": ALGO_HALVING_DOUBLING}
 ACC_F32 = 1
+ALLOW_CAPTURE = 2
+ERR_UNSUPPORTED = 3
 ERR_INVALID = 1
 ERR_TIMEOUT = 5
 UNIQUE_ID_BYTES = 128
@@ -84,6 +87,16 @@ class HostMapping(ctypes.Structure):
 
 
 MAP_REGISTER, MAP_PIN, MAP_PINNED_BLOCK = 1, 2, 3
+
+
+class CommPhases(ctypes.Structure):
+    """hydra_comm_phases_t (include/hydra_hip.h): per-phase totals of profiled allreduces."""
+    _fields_ = [("calls", ctypes.c_uint64), ("link_ops", ctypes.c_uint64),
+                ("fold_ops", ctypes.c_uint64), ("link_ms", ctypes.c_double),
+                ("fold_ms", ctypes.c_double), ("span_ms", ctypes.c_double),
+                ("sent_bytes", ctypes.c_uint64), ("recv_bytes", ctypes.c_uint64),
+                ("fold_hbm_bytes", ctypes.c_uint64), ("peers", ctypes.c_int32),
+                ("reserved", ctypes.c_int32)]
 
 
 class HydraError(RuntimeError):
@@ -199,6 +212,8 @@ def _declare(L) -> None:
     L.hydra_peer_detach.argtypes = [vp]
     L.hydra_peer_destroy.argtypes = [vp]
     L.hydra_comm_wait.argtypes = [vp, vp, ctypes.c_int64]
+    L.hydra_comm_profile.argtypes = [vp, i]
+    L.hydra_comm_phases.argtypes = [vp, ctypes.POINTER(CommPhases)]
 
 
 def lib():

@@ -154,16 +154,11 @@ int hydra_device_arch(int device, char* buf, size_t len) {
 }
 
 int hydra_device_check(int device) {
-  int prev = -1;
-  if (hipGetDevice(&prev) != hipSuccess) prev = -1;
-  struct Restore {  // the caller's current device is left as it was
-    int d;
-    ~Restore() {
-      if (d >= 0) (void)hipSetDevice(d);
-    }
-  } restore_{prev};
-  HIP_TRY(hipSetDevice(device));
-  HIP_TRY(hipDeviceSynchronize());  // surfaces an asynchronous fault of any enqueued work
+  hydra::DeviceScope ds(device);  // the caller's current device is left as it was
+  HIP_TRY(ds.err);
+  // surfaces an asynchronous fault of any enqueued work (the resident reducer is stopped first,
+  // so the drain does not wait on other threads' host calls)
+  HIP_TRY(hydra::drain_device(device));
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return hydra::hip_fail(e, "sticky device error");
   return ok();
@@ -253,9 +248,10 @@ int hydra_ctx_create(int device, hydra_ctx_t* out) {
   int count = 0;
   HIP_TRY(hipGetDeviceCount(&count));
   if (device < 0 || device >= count) return fail(HYDRA_ERR_NO_DEVICE, "no such device");
+  hydra::DeviceScope ds(device);  // the caller's current device is left as it was
   auto* x = new hydra_ctx();
   x->device = device;
-  hipError_t e = hipSetDevice(device);
+  hipError_t e = ds.err;
   if (e == hipSuccess) e = hydra::cached_stream(device, &x->stream);
   for (int i = 0; i < 2 && e == hipSuccess; i++) {
     e = hydra::cached_event(device, &x->done[i]);
@@ -282,7 +278,7 @@ int hydra_ctx_create(int device, hydra_ctx_t* out) {
 
 int hydra_ctx_destroy(hydra_ctx_t ctx) {
   if (!ctx) return ok();
-  (void)hipSetDevice(ctx->device);
+  hydra::DeviceScope ds(ctx->device);
   // (its calls were synchronous: nothing of this context is left on the resident reducer,
   // whose instance leaves by itself when idle)
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
@@ -384,7 +380,8 @@ int hydra_reduce_host(hydra_ctx_t ctx, int op, int dtype, void* c, const void* a
   // buffer's slots.  Round r is submitted once round r - 1 is done; its staged results go back
   // to c while round r runs, and the CPU fills the other buffer meanwhile.  Submitted to the
   // resident reducer when the context holds a slot, else launched on the context's stream.
-  hydra::ResidentLease* const lease = ctx->lease;
+  hydra::ResidentLease* const lease = hydra::resident_usable(ctx->lease) ? ctx->lease : nullptr;
+  bool poisoned = false;  // a failed resident wait could not confirm the grid gone: keep windows
   std::vector<hydra::BatchSegDesc> segs;
   segs.reserve(hydra::kResidentSegs);
   std::vector<hydra::CopyJob> ins;      // the current round's copies into the staging
@@ -394,7 +391,10 @@ int hydra_reduce_host(hydra_ctx_t ctx, int op, int dtype, void* c, const void* a
   bool pending = false;  // the other buffer's round is in flight
   auto wait_round = [&](int k) -> int {
     if (lease) {
-      if (int r = hydra::resident_wait(lease)) return r;
+      if (int r = hydra::resident_wait(lease, &poisoned)) {
+        if (poisoned) guard_.k = 0;  // the grid may still touch them: they stay mapped
+        return r;
+      }
     } else {
       HIP_TRY(hipEventSynchronize(ctx->done[k]));
     }
@@ -427,7 +427,11 @@ int hydra_reduce_host(hydra_ctx_t ctx, int op, int dtype, void* c, const void* a
       }
       pending = true;
       if (!drain_.f) {
-        drain_.f = lease ? std::function<void()>([lease] { (void)hydra::resident_wait(lease); })
+        drain_.f = lease ? std::function<void()>([lease, &guard_] {
+                             bool p = false;
+                             (void)hydra::resident_wait(lease, &p);
+                             if (p) guard_.k = 0;
+                           })
                          : std::function<void()>([st = ctx->stream] {
                              (void)hipStreamSynchronize(st);
                            });
@@ -441,7 +445,8 @@ int hydra_reduce_host(hydra_ctx_t ctx, int op, int dtype, void* c, const void* a
     buf = other;
     return HYDRA_OK;
   };
-  if (!lease) HIP_TRY(hipSetDevice(ctx->device));
+  hydra::DeviceScope ds(lease ? -1 : ctx->device);  // launches go to the context's device
+  HIP_TRY(ds.err);
   // A staged call is cut into about stage_split() rounds (>= kRoundMin bytes per operand, at
   // most a slot), so its copies overlap the GPU's rounds: in at round r + 1 and out at round
   // r - 1 while round r runs.

@@ -22,6 +22,8 @@
 #include "errors.h"
 #include "peer_kernels.h"
 #include "reduce_kernels.h"
+#include "resident.h"
+#include "resource_cache.h"
 #include "trace.h"
 #include "xgmi_plan.h"
 
@@ -180,7 +182,8 @@ int hydra_peer_create(int nranks, int rank, int device, hydra_peer_t* out, void*
   *out = nullptr;
   if (nranks < 1 || nranks > hydra::kPeerMaxRanks || rank < 0 || rank >= nranks)
     return fail(HYDRA_ERR_INVALID, "bad rank/nranks (peer allreduce: 1..8 ranks)");
-  HIP_TRY(hipSetDevice(device));
+  hydra::DeviceScope ds(device);
+  HIP_TRY(ds.err);
   auto* p = new hydra_peer();
   p->P = nranks;
   p->rank = rank;
@@ -196,7 +199,7 @@ int hydra_peer_create(int nranks, int rank, int device, hydra_peer_t* out, void*
     *p->err_host = 0;
     e = hipHostGetDevicePointer(reinterpret_cast<void**>(&p->err_dev), p->err_host, 0);
   }
-  if (e == hipSuccess) e = hipDeviceSynchronize();
+  if (e == hipSuccess) e = hydra::drain_device(device);
   if (e != hipSuccess) {
     hydra_peer_destroy(p);
     return hydra::hip_fail(e, "hydra_peer_create");
@@ -277,8 +280,7 @@ int hydra_peer_close(hydra_peer_t p, void* buf) {
   if (!p) return fail(HYDRA_ERR_INVALID, "null peer");
   for (size_t i = 0; i < p->regs.size(); i++) {
     if (p->regs[i].base != buf) continue;
-    (void)hipSetDevice(p->device);
-    (void)hipDeviceSynchronize();  // no kernel may still read through the mappings
+    (void)hydra::drain_device(p->device);  // no kernel may still read through the mappings
     for (int q = 0; q < p->P; q++)
       if (q != p->rank) close_mapping(p, p->regs[i].key[q]);
     bool shared = false;  // another open registration in the same allocation keeps its record
@@ -374,7 +376,7 @@ int hydra_peer_allreduce(hydra_peer_t p, int algo, int op, int dtype, int flags,
       p->blocks > 0 ? (size_t)p->blocks : std::min<size_t>(std::max<size_t>(work, 1), 512);
   if (algo == HYDRA_PEER_ONE_SHOT) {
     if (p->scratch_bytes < n * es) {
-      HIP_TRY(hipDeviceSynchronize());  // first call at a new size: outside any capture
+      HIP_TRY(hydra::drain_device(p->device));  // first call at a new size: outside any capture
       if (p->scratch) {
         HIP_TRY(hipFree(p->scratch));
         hydra::ledger_release(hydra::kLedgerPeerLocal, p->scratch);
@@ -397,8 +399,7 @@ int hydra_peer_allreduce(hydra_peer_t p, int algo, int op, int dtype, int flags,
 int hydra_peer_detach(hydra_peer_t p) {
   if (!p) return fail(HYDRA_ERR_INVALID, "null peer");
   if (p->detached) return ok();
-  (void)hipSetDevice(p->device);
-  (void)hipDeviceSynchronize();  // no kernel of ours may still read through the mappings
+  (void)hydra::drain_device(p->device);  // no kernel of ours may still read through the mappings
   for (auto& kv : p->opened) {
     (void)hipIpcCloseMemHandle(kv.second.base);
     hydra::ledger_release(hydra::kLedgerPeerMapping, kv.second.base);

@@ -39,6 +39,7 @@ namespace hydra {
 
 constexpr int kResidentSegs = 16;
 constexpr int kResidentBlocks = 128;
+constexpr int kResidentMaxBlocks = 1024;  // HYDRA_RESIDENT_SHAPE's bound (the job word holds nwg)
 constexpr int kResidentSlots = 32;  // contexts served at once per device (lanes of wave 0)
 
 struct ResSeg {  // one c = op(a, b): vector body + ragged head / tail, split on c (as the batch)
@@ -79,8 +80,9 @@ struct ResJob {  // a call spread over workgroups 0 .. nwg-1 (device memory)
 };
 
 struct alignas(64) ResDev {  // device memory, zeroed at creation
-  uint64_t pub;              // the last job published: (generation << 40) | job number
+  uint64_t pub;              // the last job published: tag | workgroups | job number (resident.hip)
   uint64_t exit_gen;
+  alignas(64) uint64_t beat;  // workgroup 0's heartbeat: calls served by the running instance
   alignas(64) uint32_t arrive;
   alignas(64) uint64_t finished;  // the last job every workgroup finished (same tagging)
   alignas(64) ResJob job;
@@ -97,9 +99,10 @@ struct ResidentShape {  // defaults from scripts/gpu_r03s.sh (profiles/r03_resid
   uint32_t tiles_per_block = 4;
 };
 
-// Launch one instance (generation `gen`) on `s`.
+// Launch one instance (generation `gen`) on `s`.  idle_ticks: leave after that long without a
+// call; grace_ticks: the bound of every wait inside the grid (s_memrealtime ticks, 100 MHz).
 hipError_t launch_resident(ResCtl* h, ResDev* d, uint64_t gen, uint64_t idle_ticks,
-                           const ResidentShape& shape, hipStream_t s);
+                           uint64_t grace_ticks, const ResidentShape& shape, hipStream_t s);
 
 // ---- host side (resident_host.cpp) -------------------------------------------------------
 // A context's slot on its device's resident reducer.  Calls through one lease are made by one
@@ -114,9 +117,32 @@ void resident_release(ResidentLease* l);
 // Ring the slot with `count` (1..kResidentSegs) segments; makes sure an instance is running.
 int resident_submit(ResidentLease* l, int op, int dtype, size_t es, const BatchSegDesc* segs,
                     size_t count);
-// Wait until the last submitted call is done (bounded: 20 s, then HYDRA_ERR_TIMEOUT).
-int resident_wait(ResidentLease* l);
+// Wait until the last submitted call is done (bounded: 20 s, then HYDRA_ERR_TIMEOUT).  On any
+// failure the instance is stopped and waited for before returning; *poisoned (if given) is set
+// when it could not be confirmed gone -- the caller must then keep every buffer of the call
+// mapped (the grid may still touch them), and the server is never used again.
+int resident_wait(ResidentLease* l, bool* poisoned = nullptr);
+// false once the lease's server was poisoned: the caller launches instead.
+bool resident_usable(const ResidentLease* l);
 uint64_t resident_calls(const ResidentLease* l);  // calls this lease submitted
 uint64_t resident_launches(int device);            // instances launched on the device so far
+
+// Device-wide drains while the reducer is serving.  A persistent grid keeps
+// hipDeviceSynchronize -- and every call that synchronises the device implicitly (hipFree,
+// hipHostFree, ...) -- waiting for as long as any thread keeps calling.  resident_pause stops the
+// device's instance (-1: every device's), waiting a bounded time for it to leave, and holds
+// relaunches until the matching resume; a call submitted meanwhile waits in ensure_running and
+// is served by the instance launched after the resume.  drain_device = pause + synchronise +
+// resume.  Every internal device-wide drain of the library goes through one of these.
+void resident_pause(int device);
+void resident_resume(int device);
+struct ResidentPause {
+  int device;
+  explicit ResidentPause(int d) : device(d) { resident_pause(d); }
+  ~ResidentPause() { resident_resume(device); }
+  ResidentPause(const ResidentPause&) = delete;
+  ResidentPause& operator=(const ResidentPause&) = delete;
+};
+hipError_t drain_device(int device);  // -1: the current device
 
 }  // namespace hydra

@@ -9,15 +9,21 @@
 namespace hydra {
 namespace {
 
-constexpr uint64_t kWorkerGraceTicks = 1000000000ull;  // 10 s of s_memrealtime (100 MHz)
-
-// The device word workgroup 0 publishes a job in: the instance's generation in the top 24 bits,
-// the job number below.  A word another instance left behind (its generation differs) never
-// wakes this one's workers.
-constexpr int kPubShift = 40;
-constexpr uint64_t kSeqMask = (uint64_t(1) << kPubShift) - 1;
-__device__ __forceinline__ uint64_t pub_word(uint64_t gen, uint64_t seq) {
-  return (gen << kPubShift) | (seq & kSeqMask);
+// The device word workgroup 0 publishes a job in: the instance's generation tag in the top 16
+// bits, the job's workgroup count in the next 12, the job number in the low 36.  A word another
+// instance left behind (its tag differs) never wakes this one's workers, and a worker learns
+// from ONE load both which job is current and whether it takes part: it never pairs a job
+// number with another job's record (a worker delayed between two loads once could).
+constexpr int kTagShift = 48;
+constexpr int kNwgShift = 36;
+constexpr uint64_t kSeqMask = (uint64_t(1) << kNwgShift) - 1;
+constexpr uint64_t kNwgMask = (uint64_t(1) << (kTagShift - kNwgShift)) - 1;
+static_assert(kResidentMaxBlocks <= kNwgMask, "nwg fits its field");
+__device__ __forceinline__ uint64_t pub_word(uint64_t tag, uint64_t nwg, uint64_t seq) {
+  return (tag << kTagShift) | ((nwg & kNwgMask) << kNwgShift) | (seq & kSeqMask);
+}
+__device__ __forceinline__ uint64_t fin_word(uint64_t tag, uint64_t seq) {  // `finished`
+  return pub_word(tag, 0, seq);
 }
 
 // The ragged head / tail of a segment, one element per lane (waves 0 and 1), with its tile 0.
@@ -119,10 +125,11 @@ __device__ __forceinline__ int pick_slot(uint64_t pending, int last) {
 
 // Bounded agent-scope wait for every workgroup to finish job `want` (workgroup 0 reuses the
 // device job record only after that).  false: the wait expired (err set).
-__device__ __forceinline__ bool wait_finished(ResCtl* h, ResDev* d, uint64_t want) {
+__device__ __forceinline__ bool wait_finished(ResCtl* h, ResDev* d, uint64_t want,
+                                              uint64_t grace_ticks) {
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   while (ld_agent(&d->finished) != want) {
-    if (__builtin_amdgcn_s_memrealtime() - t0 > kWorkerGraceTicks) {
+    if (__builtin_amdgcn_s_memrealtime() - t0 > grace_ticks) {
       __hip_atomic_store(&h->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       return false;
     }
@@ -134,37 +141,51 @@ __device__ __forceinline__ bool wait_finished(ResCtl* h, ResDev* d, uint64_t wan
 // B: tiles whose loads a workgroup issues together; a call of at most `solo` tiles is served by
 // workgroup 0 alone (no device hop to the others, no arrival counter); a job wakes
 // ceil(tiles / tpb) workgroups.
+//
+// Liveness: workgroup 0 bumps the device heartbeat `beat` on every call it serves (solo calls
+// publish no job), and a worker restarts its grace period whenever the job word or the heartbeat
+// moves.  A worker gives up (err) only when neither moved for idle + grace -- i.e. only if
+// workgroup 0 itself is gone without publishing the exit, which a correct grid never does.
 template <int B>
 __global__ __launch_bounds__(kBlock) void k_resident(ResCtl* h, ResDev* d, uint64_t gen,
-                                                     uint64_t idle_ticks, uint32_t solo,
-                                                     uint32_t tpb) {
+                                                     uint64_t idle_ticks, uint64_t grace_ticks,
+                                                     uint32_t solo, uint32_t tpb) {
   __shared__ uint64_t s_seq;
   __shared__ int s_slot;
   __shared__ int s_mode;  // 0 a published job, 1 workgroup 0 alone, 2 leave, 3 not in this job
   __shared__ uint32_t s_nwg;  // workgroups in the published job
   __shared__ ResDesc s_desc;
   const int t = threadIdx.x;
-  const uint64_t gtag = gen & ((uint64_t(1) << (64 - kPubShift)) - 1);
-  uint64_t job = 0;  // the last job published (workgroup 0) / served (the others)
+  const uint64_t gtag = gen & ((uint64_t(1) << (64 - kTagShift)) - 1);
+  uint64_t job = 0;  // the last job published (workgroup 0) / seen (the others)
+  uint64_t beat = 0;  // workgroup 0: calls served by this instance
   // workgroup 0, wave 0: lane i < kResidentSlots tracks slot i's last served sequence number
   uint64_t served = 0;
   int last_slot = kResidentSlots - 1;
   if (blockIdx.x == 0 && t < kResidentSlots) served = ld_sys(&h->slot[t].done);
   for (;;) {
     if (blockIdx.x == 0) {
-      if (t < 64) {  // wave 0: every slot's doorbell in one load instruction
+      if (t < 64) {  // wave 0: every slot's doorbell and the quit word in one load instruction
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         uint64_t s = 0;
         int k = 0, mode = 0;
         for (;;) {
-          const uint64_t db = t < kResidentSlots ? ld_sys(&h->slot[t].doorbell) : 0;
+          const uint64_t db = t < kResidentSlots ? ld_sys(&h->slot[t].doorbell)
+                              : t == 63        ? (uint64_t)ld_sys(&h->quit)
+                                               : 0;
+          // quit first: a host that stops the instance (a drain, a timeout, exit) must not wait
+          // behind other threads' calls; a call rung meanwhile is served by the next instance
+          if (__shfl((unsigned long long)db, 63) != 0) {
+            mode = 2;
+            break;
+          }
           const uint64_t pending = __ballot(t < kResidentSlots && db != served);
           if (pending) {
             k = pick_slot(pending, last_slot);
             s = __shfl((unsigned long long)db, k);
             break;
           }
-          if (ld_sys(&h->quit) != 0u || __builtin_amdgcn_s_memrealtime() - t0 > idle_ticks) {
+          if (__builtin_amdgcn_s_memrealtime() - t0 > idle_ticks) {
             mode = 2;
             break;
           }
@@ -173,6 +194,9 @@ __global__ __launch_bounds__(kBlock) void k_resident(ResCtl* h, ResDev* d, uint6
         if (mode != 2) {
           if (t == k) served = s;
           last_slot = k;
+          beat++;
+          if (t == 0)  // liveness for the workers (solo calls publish nothing)
+            __hip_atomic_store(&d->beat, beat, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           // the descriptor was written before the doorbell: acquire, then read it (two words
           // per lane, one host round trip)
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
@@ -187,7 +211,7 @@ __global__ __launch_bounds__(kBlock) void k_resident(ResCtl* h, ResDev* d, uint6
             if (t < kDescWords) dst[t] = w0;
             if (t + 64 < kDescWords) dst[t + 64] = w1;
             mode = 1;
-          } else if (job != 0 && !wait_finished(h, d, pub_word(gen, job))) {
+          } else if (job != 0 && !wait_finished(h, d, fin_word(gtag, job), grace_ticks)) {
             mode = 2;  // a workgroup never finished the last job: leave (err is set)
           } else {  // the job record, write-through, then publish it
             const uint32_t nwg = min(gridDim.x, max(2u, (tiles + tpb - 1) / tpb));
@@ -208,13 +232,13 @@ __global__ __launch_bounds__(kBlock) void k_resident(ResCtl* h, ResDev* d, uint6
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             job++;
             if (t == 0)
-              __hip_atomic_store(&d->pub, pub_word(gen, job), __ATOMIC_RELAXED,
+              __hip_atomic_store(&d->pub, pub_word(gtag, nwg, job), __ATOMIC_RELAXED,
                                  __HIP_MEMORY_SCOPE_AGENT);
           }
         } else {
           // leave: once every workgroup finished the last job (so none is still to wake for
           // it), publish the exit
-          if (job != 0) (void)wait_finished(h, d, pub_word(gen, job));
+          if (job != 0) (void)wait_finished(h, d, fin_word(gtag, job), grace_ticks);
           if (t == 0)
             __hip_atomic_store(&d->exit_gen, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
@@ -225,31 +249,36 @@ __global__ __launch_bounds__(kBlock) void k_resident(ResCtl* h, ResDev* d, uint6
         }
       }
     } else if (t == 0) {  // the other workgroups: the job word workgroup 0 publishes
-      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      const uint64_t mine = pub_word(gen, job);
+      uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      uint64_t seen_beat = ld_agent(&d->beat);
+      uint32_t nwg = 0;
       int mode = 0;
       for (;;) {
         const uint64_t p = ld_agent(&d->pub);
-        if (p != mine && (p >> kPubShift) == gtag) {
+        if ((p >> kTagShift) == gtag && (p & kSeqMask) != job) {
           job = p & kSeqMask;
+          nwg = (uint32_t)((p >> kNwgShift) & kNwgMask);  // from the same word: this job's
           break;
         }
         if (ld_agent(&d->exit_gen) == gen) {
           mode = 2;
           break;
         }
-        if (__builtin_amdgcn_s_memrealtime() - t0 > idle_ticks + kWorkerGraceTicks) {
+        const uint64_t b = ld_agent(&d->beat);
+        const uint64_t now = __builtin_amdgcn_s_memrealtime();
+        if (b != seen_beat) {  // workgroup 0 is serving (solo) calls: alive
+          seen_beat = b;
+          t0 = now;
+        } else if (now - t0 > idle_ticks + grace_ticks) {
           __hip_atomic_store(&h->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           mode = 2;
           break;
         }
         __builtin_amdgcn_s_sleep(2);
       }
-      if (mode == 0) {  // in this job?  (the record was published before the word: agent acquire)
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        const uint32_t nwg = ld_agent(&d->job.nwg);
+      if (mode == 0) {
         s_nwg = nwg;
-        if (blockIdx.x >= nwg) mode = 3;
+        if (blockIdx.x >= nwg) mode = 3;  // not in this job: its record is never read
       }
       s_mode = mode;
     }
@@ -297,7 +326,7 @@ __global__ __launch_bounds__(kBlock) void k_resident(ResCtl* h, ResDev* d, uint6
         const uint64_t seq = ld_agent(&d->job.seq);
         const uint32_t slot = ld_agent(&d->job.slot);
         __hip_atomic_store(&d->arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&d->finished, pub_word(gen, job), __ATOMIC_RELEASE,
+        __hip_atomic_store(&d->finished, fin_word(gtag, job), __ATOMIC_RELEASE,
                            __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&h->slot[slot].done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
       }
@@ -311,17 +340,17 @@ __global__ __launch_bounds__(kBlock) void k_resident(ResCtl* h, ResDev* d, uint6
 }  // namespace
 
 hipError_t launch_resident(ResCtl* h, ResDev* d, uint64_t gen, uint64_t idle_ticks,
-                           const ResidentShape& shape, hipStream_t s) {
+                           uint64_t grace_ticks, const ResidentShape& shape, hipStream_t s) {
   const uint32_t solo = shape.solo, tpb = std::max(1u, shape.tiles_per_block);
   if (shape.batch >= 4)
     hipLaunchKernelGGL(k_resident<4>, dim3(shape.blocks), dim3(kBlock), 0, s, h, d, gen,
-                       idle_ticks, solo, tpb);
+                       idle_ticks, grace_ticks, solo, tpb);
   else if (shape.batch == 2)
     hipLaunchKernelGGL(k_resident<2>, dim3(shape.blocks), dim3(kBlock), 0, s, h, d, gen,
-                       idle_ticks, solo, tpb);
+                       idle_ticks, grace_ticks, solo, tpb);
   else
     hipLaunchKernelGGL(k_resident<1>, dim3(shape.blocks), dim3(kBlock), 0, s, h, d, gen,
-                       idle_ticks, solo, tpb);
+                       idle_ticks, grace_ticks, solo, tpb);
   return hipGetLastError();
 }
 

@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -25,8 +26,11 @@ struct ResidentServer {
   ResDev* d = nullptr;
   hipStream_t s = nullptr;
   std::mutex mu;  // launches and slot leases
+  std::condition_variable resumed;  // paused dropped to 0
   uint64_t gen = 0;
   uint32_t leased = 0;  // bit i: slot i has a holder
+  int paused = 0;       // resident_pause holders: no launch meanwhile (under mu)
+  std::atomic<bool> poisoned{false};  // an instance could not be confirmed gone: never used again
   std::atomic<uint64_t> launches{0};
 };
 
@@ -42,7 +46,7 @@ static_assert(kResidentSlots <= 32, "leased is a 32-bit mask");
 
 constexpr int kMaxDevices = 64;
 std::mutex g_mu;
-ResidentServer* g_srv[kMaxDevices] = {};
+std::atomic<ResidentServer*> g_srv[kMaxDevices] = {};  // set once each (under g_mu)
 std::atomic<bool> g_exiting{false};
 
 uint64_t idle_ticks() {  // s_memrealtime runs at 100 MHz
@@ -54,6 +58,15 @@ uint64_t idle_ticks() {  // s_memrealtime runs at 100 MHz
   return t;
 }
 
+uint64_t grace_ticks() {  // the bound of every wait inside the grid (default 10 s)
+  static const uint64_t t = [] {
+    const char* v = std::getenv("HYDRA_RESIDENT_GRACE_US");
+    const long us = v ? std::atol(v) : 10000000L;
+    return (uint64_t)std::max(1000L, std::min(us, 600000000L)) * 100;
+  }();
+  return t;
+}
+
 const ResidentShape& shape() {
   static const ResidentShape sh = [] {
     ResidentShape r;
@@ -61,7 +74,7 @@ const ResidentShape& shape() {
       int b = r.blocks, u = r.batch;
       unsigned so = r.solo, tp = r.tiles_per_block;
       if (std::sscanf(v, "%d,%d,%u,%u", &b, &u, &so, &tp) >= 1) {
-        r.blocks = std::max(1, std::min(b, 1024));
+        r.blocks = std::max(1, std::min(b, kResidentMaxBlocks));
         r.batch = u >= 4 ? 4 : u >= 2 ? 2 : 1;
         r.solo = std::min(so, 64u);
         r.tiles_per_block = std::max(1u, std::min(tp, 64u));
@@ -82,9 +95,10 @@ volatile T& vol(T& x) {
 void quit_all() {
   g_exiting.store(true);
   std::lock_guard<std::mutex> g(g_mu);
-  for (ResidentServer* v : g_srv)
-    if (v) vol(v->h->quit) = 1u;
-  for (ResidentServer* v : g_srv) {  // bounded: an instance leaves within microseconds
+  for (auto& x : g_srv)
+    if (ResidentServer* v = x.load()) vol(v->h->quit) = 1u;
+  for (auto& x : g_srv) {  // bounded: an instance leaves within microseconds
+    ResidentServer* v = x.load();
     if (!v) continue;
     const auto t0 = std::chrono::steady_clock::now();
     while (vol(v->h->alive) != 0u &&
@@ -125,8 +139,8 @@ int server(int device, ResidentServer** out) {
   *out = nullptr;
   if (device < 0 || device >= kMaxDevices) return fail(HYDRA_ERR_INVALID, "device out of range");
   std::lock_guard<std::mutex> g(g_mu);
-  if (g_srv[device]) {
-    *out = g_srv[device];
+  if (ResidentServer* have = g_srv[device].load()) {
+    *out = have;
     return HYDRA_OK;
   }
   int prev = -1;
@@ -166,13 +180,31 @@ int server(int device, ResidentServer** out) {
   return HYDRA_OK;
 }
 
+// Tell the running instance (if any) to leave and wait, bounded, until it has: true when no
+// instance of this server is running any more.
+bool stop_instance(ResidentServer* v, std::chrono::milliseconds bound) {
+  vol(v->h->quit) = 1u;
+  std::atomic_thread_fence(std::memory_order_seq_cst);
+  const auto t0 = std::chrono::steady_clock::now();
+  while (vol(v->h->alive) != 0u) {
+    if (std::chrono::steady_clock::now() - t0 > bound) return false;
+    std::this_thread::yield();
+  }
+  return true;
+}
+
 // A new instance unless one is running (alive); `alive` is set before the launch, cleared by
-// the kernel as it leaves.
+// the kernel as it leaves.  While a drain holds the server paused (resident_pause), a caller
+// whose call is pending waits here (bounded) for the drain to finish, then launches.
 int ensure_running(ResidentServer* v) {
   if (vol(v->h->alive) != 0u) return HYDRA_OK;
-  std::lock_guard<std::mutex> g(v->mu);
+  std::unique_lock<std::mutex> g(v->mu);
   if (vol(v->h->alive) != 0u) return HYDRA_OK;
+  if (v->paused > 0 &&
+      !v->resumed.wait_for(g, std::chrono::seconds(20), [v] { return v->paused == 0; }))
+    return fail(HYDRA_ERR_TIMEOUT, "Timed out waiting 20000ms for a device drain to finish");
   if (g_exiting.load()) return fail(HYDRA_ERR_INVALID, "resident reducer: process is exiting");
+  if (v->poisoned.load()) return fail(HYDRA_ERR_HIP, "resident reducer: disabled after a fault");
   vol(v->h->quit) = 0u;
   vol(v->h->alive) = 1u;
   std::atomic_thread_fence(std::memory_order_seq_cst);
@@ -186,7 +218,8 @@ int ensure_running(ResidentServer* v) {
     e = hipMemsetAsync(v->d, 0, sizeof(ResDev), v->s);
     vol(v->h->err) = 0u;
   }
-  if (e == hipSuccess) e = launch_resident(v->h_dev, v->d, ++v->gen, idle_ticks(), shape(), v->s);
+  if (e == hipSuccess)
+    e = launch_resident(v->h_dev, v->d, ++v->gen, idle_ticks(), grace_ticks(), shape(), v->s);
   if (prev >= 0 && prev != v->device) (void)hipSetDevice(prev);
   if (e != hipSuccess) {
     vol(v->h->alive) = 0u;
@@ -194,6 +227,12 @@ int ensure_running(ResidentServer* v) {
   }
   v->launches.fetch_add(1);
   return HYDRA_OK;
+}
+
+// Lock-free (g_mu may be held by a caller that releases a block: server()'s error path).
+ResidentServer* find_server(int device) {
+  if (device < 0 || device >= kMaxDevices) return nullptr;
+  return g_srv[device].load();
 }
 }  // namespace
 
@@ -269,24 +308,49 @@ int resident_submit(ResidentLease* l, int op, int dtype, size_t es, const BatchS
   return ensure_running(v);
 }
 
-int resident_wait(ResidentLease* l) {
+// A failed wait (an expired wait inside the grid, or this bound) must not return while the
+// grid may still touch the caller's buffers: the instance is told to leave and waited for; if it
+// cannot be confirmed gone, the server is poisoned (every later call launches instead) and
+// *poisoned tells the caller to keep its windows mapped.
+int resident_wait(ResidentLease* l, bool* poisoned) {
   ResidentServer* v = l->srv;
+  if (poisoned) *poisoned = false;
   volatile uint64_t& done = vol(v->h->slot[l->slot].done);
   const uint64_t seq = l->seq;
   const auto t0 = std::chrono::steady_clock::now();
+  // the call is abandoned: with relaunches held, stop the instance, then retire the doorbell
+  // (done = seq) so that no later instance serves this descriptor after the caller returned
+  auto give_up = [&](int code, const char* msg) {
+    {
+      std::lock_guard<std::mutex> g(v->mu);
+      v->paused++;
+    }
+    if (stop_instance(v, std::chrono::seconds(2))) {
+      done = seq;
+    } else {
+      v->poisoned.store(true);
+      if (poisoned) *poisoned = true;
+    }
+    {
+      std::lock_guard<std::mutex> g(v->mu);
+      v->paused--;
+    }
+    v->resumed.notify_all();
+    return fail(code, msg);
+  };
   for (uint32_t spins = 0;; spins++) {
     if (done >= seq) break;
     if (vol(v->h->alive) == 0u && done < seq) {  // it left without serving us: a new instance
+      if (vol(v->h->err))  // (it left on an expired wait: report that, do not relaunch)
+        return give_up(HYDRA_ERR_HIP, "resident reducer: a wait inside the grid expired");
       if (int rc = ensure_running(v)) return rc;
       continue;
     }
     if ((spins & 1023) == 0) {
       if (vol(v->h->err))
-        return fail(HYDRA_ERR_HIP, "resident reducer: a wait inside the grid expired");
-      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(20)) {
-        vol(v->h->quit) = 1u;
-        return fail(HYDRA_ERR_TIMEOUT, "Timed out waiting 20000ms for the resident reducer");
-      }
+        return give_up(HYDRA_ERR_HIP, "resident reducer: a wait inside the grid expired");
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(20))
+        return give_up(HYDRA_ERR_TIMEOUT, "Timed out waiting 20000ms for the resident reducer");
     }
     __builtin_ia32_pause();
   }
@@ -294,12 +358,52 @@ int resident_wait(ResidentLease* l) {
   return HYDRA_OK;
 }
 
+bool resident_usable(const ResidentLease* l) { return l && !l->srv->poisoned.load(); }
+
+void resident_pause(int device) {
+  for (int d = 0; d < kMaxDevices; d++) {
+    if (device >= 0 && d != device) continue;
+    ResidentServer* v = find_server(d);
+    if (!v) continue;
+    {
+      std::lock_guard<std::mutex> g(v->mu);
+      v->paused++;
+    }
+    // bounded: an instance finishes the call it is serving, then leaves (quit is checked before
+    // the doorbells); past the bound the caller's drain simply waits for it as before
+    (void)stop_instance(v, std::chrono::milliseconds(500));
+  }
+}
+
+void resident_resume(int device) {
+  for (int d = 0; d < kMaxDevices; d++) {
+    if (device >= 0 && d != device) continue;
+    ResidentServer* v = find_server(d);
+    if (!v) continue;
+    {
+      std::lock_guard<std::mutex> g(v->mu);
+      if (v->paused > 0) v->paused--;
+    }
+    v->resumed.notify_all();
+  }
+}
+
+hipError_t drain_device(int device) {
+  ResidentPause p(device);
+  int prev = -1;
+  if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+  hipError_t e = device >= 0 && device != prev ? hipSetDevice(device) : hipSuccess;
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  if (prev >= 0 && device >= 0 && device != prev) (void)hipSetDevice(prev);
+  return e;
+}
+
 uint64_t resident_calls(const ResidentLease* l) { return l ? l->calls : 0; }
 
 uint64_t resident_launches(int device) {
   if (device < 0 || device >= kMaxDevices) return 0;
-  std::lock_guard<std::mutex> g(g_mu);
-  return g_srv[device] ? g_srv[device]->launches.load() : 0;
+  ResidentServer* v = g_srv[device].load();
+  return v ? v->launches.load() : 0;
 }
 
 }  // namespace hydra

@@ -3,6 +3,7 @@
 
 #include "fault_report.h"
 #include "host_map.h"
+#include "resident.h"
 
 #include <atomic>
 #include <cstdint>
@@ -53,19 +54,6 @@ Caches& C() {
   return *c;
 }
 
-// Makes `device` current for a scope and restores the caller's device.
-struct DeviceScope {
-  int old = -1;
-  hipError_t err = hipSuccess;  // of switching to `device` (an invalid device fails here)
-  explicit DeviceScope(int device) {
-    if (hipGetDevice(&old) != hipSuccess) old = -1;
-    if (device >= 0 && device != old) err = hipSetDevice(device);
-  }
-  ~DeviceScope() {
-    if (old >= 0) (void)hipSetDevice(old);
-  }
-};
-
 // Devices hydra has created streams, events or blocks on (bit d), plus the caller's current one:
 // the devices whose kernels may be reading a pinned block.  Touching any other device would
 // create a context on it.
@@ -76,6 +64,7 @@ void note_device(int d) {
 
 // Drains those devices; the caller's current device is left as it was.
 hipError_t sync_all_devices() {
+  ResidentPause pause_(-1);  // a serving resident reducer would hold the drain up indefinitely
   int cur = -1;
   if (hipGetDevice(&cur) == hipSuccess) note_device(cur);
   const uint64_t m = g_devices.load(std::memory_order_relaxed);
@@ -128,7 +117,9 @@ hipError_t give_block(void* p, bool host) {
     c.live_blocks.erase(it);  // a second release of p now fails above or below, never twice
   }
   // hipFree's implicit synchronisation: work enqueued before the release may still use p (a
-  // pinned block: on any device -- the kernels of every device can read it in place)
+  // pinned block: on any device -- the kernels of every device can read it in place).  The
+  // resident reducer is stopped for the drain and the free (both wait for every stream).
+  ResidentPause pause_(-1);
   hipError_t e = k.host ? sync_all_devices() : hipSuccess;
   if (!k.host) {
     DeviceScope ds(k.device);
@@ -290,6 +281,7 @@ hipError_t trim_caches() {
     c.kept_events.clear();
     c.kept_bytes.clear();
   }
+  ResidentPause pause_(-1);  // hipFree / hipHostFree synchronise the device
   hipError_t first = hipSuccess;
   auto note = [&first](hipError_t e) {
     if (e != hipSuccess && first == hipSuccess) first = e;

@@ -34,4 +34,20 @@ hipError_t cached_event(int device, hipEvent_t* out);  // hipEventDisableTiming;
 hipError_t release_event(hipEvent_t e);
 hipError_t trim_caches();
 
+// Makes `device` current for a scope and restores the caller's device (every C-ABI entry that
+// works on an object bound to a device opens one: the caller's current device is never changed).
+struct DeviceScope {
+  int old = -1;
+  hipError_t err = hipSuccess;  // of switching to `device` (an invalid device fails here)
+  explicit DeviceScope(int device) {
+    if (hipGetDevice(&old) != hipSuccess) old = -1;
+    if (device >= 0 && device != old) err = hipSetDevice(device);
+  }
+  ~DeviceScope() {
+    if (old >= 0) (void)hipSetDevice(old);
+  }
+  DeviceScope(const DeviceScope&) = delete;
+  DeviceScope& operator=(const DeviceScope&) = delete;
+};
+
 }  // namespace hydra

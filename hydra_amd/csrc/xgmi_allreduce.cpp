@@ -14,16 +14,19 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstring>
 #include <deque>
 #include <thread>
 #include <map>
+#include <set>
 #include <string>
 #include <vector>
 
 #include "../../include/hydra_hip.h"
 #include "errors.h"
+#include "resident.h"
 #include "resource_cache.h"
 #include "reduce_kernels.h"
 #include "split_table.h"
@@ -206,6 +209,21 @@ struct hydra_comm {
   int key_root = -1;
   std::vector<hydra::PlanOp> plan;
   std::vector<char> waited;
+  // per-phase timing (hydra_comm_profile): timing events around every op, read back lazily
+  struct ProfRec {
+    bool comm;
+    hipEvent_t s, e;
+    uint64_t sent, recv, hbm;
+  };
+  struct ProfCall {
+    hipEvent_t t0;
+    std::vector<ProfRec> ops;
+  };
+  bool profile = false;
+  std::vector<ProfCall> prof_calls;
+  std::vector<hipEvent_t> prof_pool;  // timing events (created on `device`)
+  hydra_comm_phases_t prof{};
+  std::set<int> prof_peers;
 };
 
 namespace {
@@ -213,9 +231,96 @@ namespace {
 int ensure_events(hydra_comm* c, size_t n) {
   while (c->events.size() < n) {
     hipEvent_t e;
-    HIP_TRY(hydra::cached_event(-1, &e));
+    HIP_TRY(hydra::cached_event(c->device, &e));  // the communicator's device, not the caller's
     c->events.push_back(e);
   }
+  return HYDRA_OK;
+}
+
+// ---- phase profiling -------------------------------------------------------------------------
+hipError_t prof_event(hydra_comm* c, hipEvent_t* out) {
+  if (!c->prof_pool.empty()) {
+    *out = c->prof_pool.back();
+    c->prof_pool.pop_back();
+    return hipSuccess;
+  }
+  return hipEventCreate(out);  // timing enabled; the caller holds a DeviceScope(c->device)
+}
+
+// Opens a profiled call: its start on the caller's stream.  No-op unless profiling is on.
+int prof_begin(hydra_comm* c, hipStream_t user_st) {
+  if (!c->profile) return HYDRA_OK;
+  hydra_comm::ProfCall call{};
+  HIP_TRY(prof_event(c, &call.t0));
+  HIP_TRY(hipEventRecord(call.t0, user_st));
+  c->prof_calls.push_back(std::move(call));
+  return HYDRA_OK;
+}
+
+// Brackets one op: `start` recorded before it is enqueued on st, the end after.
+struct ProfOp {
+  hydra_comm* c;
+  hipStream_t st;
+  hydra_comm::ProfRec r{};
+  bool on = false;
+  ProfOp(hydra_comm* c_, hipStream_t st_, bool comm, uint64_t sent, uint64_t recv, uint64_t hbm)
+      : c(c_), st(st_) {
+    if (!c->profile || c->prof_calls.empty()) return;
+    r.comm = comm;
+    r.sent = sent;
+    r.recv = recv;
+    r.hbm = hbm;
+    on = prof_event(c, &r.s) == hipSuccess && hipEventRecord(r.s, st) == hipSuccess;
+  }
+  hipError_t end() {
+    if (!on) return hipSuccess;
+    on = false;
+    hipError_t e = prof_event(c, &r.e);
+    if (e == hipSuccess) e = hipEventRecord(r.e, st);
+    if (e == hipSuccess) c->prof_calls.back().ops.push_back(r);
+    return e;
+  }
+};
+
+// Reads back every finished profiled call into the totals and recycles its events.
+int prof_collect(hydra_comm* c) {
+  for (auto& call : c->prof_calls) {
+    float last = 0.f;
+    for (auto& r : call.ops) {
+      HIP_TRY(hipEventSynchronize(r.e));
+      float d = 0.f, end = 0.f;
+      HIP_TRY(hipEventElapsedTime(&d, r.s, r.e));
+      HIP_TRY(hipEventElapsedTime(&end, call.t0, r.e));
+      (r.comm ? c->prof.link_ms : c->prof.fold_ms) += d;
+      (r.comm ? c->prof.link_ops : c->prof.fold_ops) += 1;
+      c->prof.sent_bytes += r.sent;
+      c->prof.recv_bytes += r.recv;
+      c->prof.fold_hbm_bytes += r.hbm;
+      last = std::max(last, end);
+      c->prof_pool.push_back(r.s);
+      c->prof_pool.push_back(r.e);
+    }
+    c->prof.span_ms += last;
+    c->prof.calls += 1;
+    c->prof_pool.push_back(call.t0);
+  }
+  c->prof_calls.clear();
+  c->prof.peers = (int32_t)c->prof_peers.size();
+  return HYDRA_OK;
+}
+
+// Enqueueing a multi-rank schedule while the caller's stream is being captured: refused unless
+// the caller opted in (HYDRA_ALLOW_CAPTURE).  RCCL's own collectives segfault in
+// hipStreamEndCapture on the socket-linked ranks of the test box.
+int capture_guard(const hydra_comm* c, int flags, hipStream_t st) {
+  if (c->nranks <= 1 || (flags & HYDRA_ALLOW_CAPTURE)) return HYDRA_OK;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  HIP_TRY(hipStreamIsCapturing(st, &cs));
+  if (cs != hipStreamCaptureStatusNone)
+    return fail(HYDRA_ERR_UNSUPPORTED,
+                "multi-rank allreduce under hipGraph capture: ending the capture of RCCL's own "
+                "collectives segfaulted on this transport (profiles/r03g2_graph_ranks_rccl.log); "
+                "pass HYDRA_ALLOW_CAPTURE on a node whose RCCL captures");
   return HYDRA_OK;
 }
 
@@ -248,12 +353,18 @@ int run_plan_rccl(hydra_comm* c, int op, int dtype, bool acc32, char* user, hipE
     const hydra::PlanOp& o = ops[i];
     if (o.kind == hydra::kOpAllToAll || o.kind == hydra::kOpAllGather) {
       wait_on(c->cs, o, ops, c->events);
+      const uint64_t off_rank = (uint64_t)o.bytes * (uint64_t)(c->nranks - 1);
+      if (c->profile)
+        for (int q = 0; q < c->nranks; q++)
+          if (q != c->rank) c->prof_peers.insert(q);
+      ProfOp pr(c, c->cs, true, off_rank, off_rank, 0);
       if (o.kind == hydra::kOpAllToAll)
         NCCL_TRY(ncclAllToAll(user + o.off, scratch + o.src_off, (size_t)o.bytes, ncclUint8,
                               c->nccl, c->cs));
       else
         NCCL_TRY(ncclAllGather(user + o.off + (int64_t)c->rank * o.bytes, user + o.off,
                                (size_t)o.bytes, ncclUint8, c->nccl, c->cs));
+      HIP_TRY(pr.end());
       if (c->waited[i]) HIP_TRY(hipEventRecord(c->events[i], c->cs));
       i++;
       continue;
@@ -263,6 +374,16 @@ int run_plan_rccl(hydra_comm* c, int op, int dtype, bool acc32, char* user, hipE
       while (g < ops.size() && ops[g].kind != hydra::kOpGroup) g++;
       if (g == ops.size()) return fail(HYDRA_ERR_INVALID, "plan: unterminated p2p group");
       wait_on(c->cs, ops[g], ops, c->events);
+      uint64_t sent = 0, recv = 0;
+      for (size_t j = i; j < g; j++) {
+        if (ops[j].kind == hydra::kOpSend) {
+          sent += (uint64_t)ops[j].bytes;
+          if (c->profile) c->prof_peers.insert(ops[j].peer);
+        } else {
+          recv += (uint64_t)ops[j].bytes;
+        }
+      }
+      ProfOp pr(c, c->cs, true, sent, recv, 0);
       NCCL_TRY(ncclGroupStart());
       ncclResult_t r = ncclSuccess;
       for (size_t j = i; j < g && r == ncclSuccess; j++) {
@@ -275,12 +396,16 @@ int run_plan_rccl(hydra_comm* c, int op, int dtype, bool acc32, char* user, hipE
       const ncclResult_t e = ncclGroupEnd();  // always close the group, even after a failure
       if (r != ncclSuccess) return nccl_fail(r, "ncclSend/ncclRecv");
       if (e != ncclSuccess) return nccl_fail(e, "ncclGroupEnd");
+      HIP_TRY(pr.end());
       if (c->waited[g]) HIP_TRY(hipEventRecord(c->events[g], c->cs));
       i = g + 1;
     } else {
       wait_on(c->ks, o, ops, c->events);
+      const uint64_t hbm = (uint64_t)o.bytes * (o.kind == hydra::kOpReduce ? 3u : (uint64_t)o.nsrc + 1);
+      ProfOp pr(c, c->ks, false, 0, 0, hbm);
       hipError_t e = launch_compute(o, op, dtype, acc32, user, scratch, es, c->ks);
       if (e != hipSuccess) return hydra::hip_fail(e, "fused reduction kernel");
+      HIP_TRY(pr.end());
       if (c->waited[i]) HIP_TRY(hipEventRecord(c->events[i], c->ks));
       i++;
     }
@@ -313,7 +438,8 @@ int hydra_comm_init(hydra_comm_t* out, int nranks, int rank, const void* id, int
   if (nranks < 1 || nranks > hydra::kMaxRanks || rank < 0 || rank >= nranks)
     return fail(HYDRA_ERR_INVALID, "bad rank/nranks");
   *out = nullptr;
-  HIP_TRY(hipSetDevice(device));
+  hydra::DeviceScope ds(device);  // RCCL binds the communicator to the current device
+  HIP_TRY(ds.err);
   auto* c = new hydra_comm();
   c->rank = rank;
   c->nranks = nranks;
@@ -327,9 +453,9 @@ int hydra_comm_init(hydra_comm_t* out, int nranks, int rank, const void* id, int
   }
   hipError_t e = hydra::cached_stream(device, &c->cs);
   if (e == hipSuccess) e = hydra::cached_stream(device, &c->ks);
-  if (e == hipSuccess) e = hydra::cached_event(-1, &c->ev_start);
-  if (e == hipSuccess) e = hydra::cached_event(-1, &c->ev_cs);
-  if (e == hipSuccess) e = hydra::cached_event(-1, &c->ev_ks);
+  if (e == hipSuccess) e = hydra::cached_event(device, &c->ev_start);
+  if (e == hipSuccess) e = hydra::cached_event(device, &c->ev_cs);
+  if (e == hipSuccess) e = hydra::cached_event(device, &c->ev_ks);
   if (e != hipSuccess) {
     hydra_comm_destroy(c);
     return hydra::hip_fail(e, "hydra_comm_init streams");
@@ -341,6 +467,7 @@ int hydra_comm_init(hydra_comm_t* out, int nranks, int rank, const void* id, int
 int hydra_comm_wait(hydra_comm_t c, hydra_stream_t stream, int64_t timeout_ms) {
   if (!c) return fail(HYDRA_ERR_INVALID, "null comm");
   if (c->aborted) return fail(HYDRA_ERR_TIMEOUT, "communicator was aborted by an earlier timeout");
+  hydra::DeviceScope ds(c->device);
   hipStream_t st = static_cast<hipStream_t>(stream);
   const auto t0 = std::chrono::steady_clock::now();
   for (int spin = 0;; spin++) {
@@ -376,9 +503,29 @@ int hydra_comm_info(hydra_comm_t c, int* nranks, int* rank, int* device) {
   return ok();
 }
 
+int hydra_comm_profile(hydra_comm_t c, int enable) {
+  if (!c) return fail(HYDRA_ERR_INVALID, "null comm");
+  hydra::DeviceScope ds(c->device);
+  if (int rc = prof_collect(c)) return rc;  // recycle what an earlier session left
+  c->profile = enable != 0;
+  if (c->profile) {
+    c->prof = hydra_comm_phases_t{};
+    c->prof_peers.clear();
+  }
+  return ok();
+}
+
+int hydra_comm_phases(hydra_comm_t c, hydra_comm_phases_t* out) {
+  if (!c || !out) return fail(HYDRA_ERR_INVALID, "null argument");
+  hydra::DeviceScope ds(c->device);
+  if (int rc = prof_collect(c)) return rc;
+  *out = c->prof;
+  return ok();
+}
+
 int hydra_comm_destroy(hydra_comm_t c) {
   if (!c) return ok();
-  (void)hipSetDevice(c->device);
+  hydra::DeviceScope ds(c->device);  // the caller's current device is restored on return
   // Drain the DEVICE, not only cs/ks: the caller's stream may still hold waits on ev_cs/ev_ks
   // and on plan events (join_streams), and kernels of an earlier allreduce may still read the
   // scratch freed below.  Destroy is rare; a full drain is the safe order.
@@ -389,7 +536,7 @@ int hydra_comm_destroy(hydra_comm_t c) {
   auto step = [&rc](hipError_t e, const char* what) {
     if (e != hipSuccess && !rc) rc = hydra::hip_fail(e, what);
   };
-  step(hipDeviceSynchronize(), "comm teardown: hipDeviceSynchronize");
+  step(hydra::drain_device(c->device), "comm teardown: hipDeviceSynchronize");
   if (c->nccl) {
     ncclResult_t r = ncclCommDestroy(c->nccl);
     if (r != ncclSuccess && !rc)
@@ -402,7 +549,12 @@ int hydra_comm_destroy(hydra_comm_t c) {
   if (c->cs) step(hydra::release_stream(c->cs), "comm teardown: release stream");
   if (c->ks) step(hydra::release_stream(c->ks), "comm teardown: release stream");
   if (c->scratch) step(hydra::cached_free(c->scratch), "comm teardown: release scratch");
-  step(hipDeviceSynchronize(), "comm teardown: hipDeviceSynchronize after the frees");
+  for (auto& call : c->prof_calls) {
+    c->prof_pool.push_back(call.t0);
+    for (auto& r : call.ops) c->prof_pool.insert(c->prof_pool.end(), {r.s, r.e});
+  }
+  for (auto e : c->prof_pool) step(hipEventDestroy(e), "comm teardown: destroy timing event");
+  step(hydra::drain_device(c->device), "comm teardown: hipDeviceSynchronize after the frees");
   delete c;
   return rc ? rc : ok();
 }
@@ -475,7 +627,11 @@ int enqueue(hydra_comm* c, int algo, int op, int dtype, int flags, void* buf, si
             hipEvent_t start) {
   if (algo == HYDRA_ALGO_RCCL) {
     HIP_TRY(hipStreamWaitEvent(c->cs, start, 0));
+    // (RCCL's own ring: 2(P-1)/P of the bucket leaves this rank; its peers are RCCL's choice)
+    const uint64_t link = (uint64_t)n * hydra::dtype_size(dtype) * 2 * (c->nranks - 1) / c->nranks;
+    ProfOp pr(c, c->cs, true, link, link, 0);
     NCCL_TRY(ncclAllReduce(buf, buf, n, nccl_type(dtype), nccl_op(op), c->nccl, c->cs));
+    HIP_TRY(pr.end());
     HIP_TRY(hipEventRecord(c->ev_cs, c->cs));
     HIP_TRY(hipEventRecord(c->ev_ks, c->ks));
     return HYDRA_OK;
@@ -490,10 +646,15 @@ extern "C" {
 int hydra_allreduce(hydra_comm_t c, int algo, int op, int dtype, int flags, void* buf, size_t n,
                     size_t max_segment, size_t chunk_bytes, hydra_stream_t stream) {
   hydra::TraceRange trace_("hydra_allreduce");
-  bool skip = false;
-  int rc = prepare(c, &algo, op, dtype, flags, buf, n, max_segment, chunk_bytes, &skip);
-  if (rc || skip) return rc ? rc : ok();
+  hydra::DeviceScope ds(c ? c->device : -1);  // the communicator's device, restored on return
   hipStream_t st = static_cast<hipStream_t>(stream);
+  int rc = HYDRA_OK;
+  // before prepare: nothing (not even a first scratch allocation) happens under a refused capture
+  if (c && n && (rc = capture_guard(c, flags, st))) return rc;
+  bool skip = false;
+  rc = prepare(c, &algo, op, dtype, flags, buf, n, max_segment, chunk_bytes, &skip);
+  if (rc || skip) return rc ? rc : ok();
+  if ((rc = prof_begin(c, st))) return rc;
   HIP_TRY(hipEventRecord(c->ev_start, st));
   rc = enqueue(c, algo, op, dtype, flags, buf, n, c->ev_start);
   if (rc) return rc;
@@ -507,11 +668,15 @@ int hydra_reduce_root(hydra_comm_t c, int root, int op, int dtype, int flags, vo
   hydra::TraceRange trace_("hydra_reduce_root");
   // checked before the single-rank / empty short cuts, as the reference does (reduce.cc:31)
   if (root < 0 || (c && root >= c->nranks)) return fail(HYDRA_ERR_INVALID, "root out of range");
+  hydra::DeviceScope ds(c ? c->device : -1);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  int rc = HYDRA_OK;
+  if (c && n && (rc = capture_guard(c, flags, st))) return rc;
   int algo = HYDRA_ALGO_DIRECT;
   bool skip = false;
-  int rc = prepare(c, &algo, op, dtype, flags, buf, n, max_segment, chunk_bytes, &skip, root);
+  rc = prepare(c, &algo, op, dtype, flags, buf, n, max_segment, chunk_bytes, &skip, root);
   if (rc || skip) return rc ? rc : ok();
-  hipStream_t st = static_cast<hipStream_t>(stream);
+  if ((rc = prof_begin(c, st))) return rc;
   HIP_TRY(hipEventRecord(c->ev_start, st));
   rc = enqueue(c, algo, op, dtype, flags, buf, n, c->ev_start);
   if (rc) return rc;
@@ -548,13 +713,17 @@ int hydra_apipe_allreduce(hydra_comm_t rail1, hydra_comm_t rail2, int table, int
   if (e2 == 0)
     return hydra_allreduce(rail1, algo, op, dtype, flags, buf, e1, max_segment, chunk_bytes,
                            stream);
+  hydra::DeviceScope ds(rail1->device);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  int rc = capture_guard(rail1, flags, st);
+  if (rc) return rc;
   int a1 = algo, a2 = algo;
   bool s1 = false, s2 = false;
-  int rc = prepare(rail1, &a1, op, dtype, flags, buf, e1, max_segment, chunk_bytes, &s1);
+  rc = prepare(rail1, &a1, op, dtype, flags, buf, e1, max_segment, chunk_bytes, &s1);
   if (!rc) rc = prepare(rail2, &a2, op, dtype, flags, p2, e2, max_segment, chunk_bytes, &s2);
   if (rc) return rc;
   if (s1 && s2) return ok();  // single rank
-  hipStream_t st = static_cast<hipStream_t>(stream);
+  if ((rc = prof_begin(rail1, st)) || (rc = prof_begin(rail2, st))) return rc;
   // both rails fork from one event on the caller's stream and run concurrently on their own
   // streams (the two std::threads of pipeallreduce-a.cc:32-50); the caller's stream joins both
   HIP_TRY(hipEventRecord(rail1->ev_start, st));
@@ -663,7 +832,7 @@ int simulate_impl(int algo, int root, int op, int dtype, int flags, int P, void*
   int coll_done = 0;  // collectives performed (every rank matched)
   hipStream_t st = nullptr;
   auto cleanup = [&]() {
-    (void)hipDeviceSynchronize();
+    (void)hydra::drain_device(-1);
     for (auto& r : R)
       if (r.scratch) (void)hydra::cached_free(r.scratch);
     if (st) (void)hydra::release_stream(st);
@@ -678,7 +847,7 @@ int simulate_impl(int algo, int root, int op, int dtype, int flags, int P, void*
     }                                               \
   } while (0)
 
-  SIM_TRY(hipDeviceSynchronize());
+  SIM_TRY(hydra::drain_device(-1));
   int dev = 0;
   SIM_TRY(hipGetDevice(&dev));
   SIM_TRY(hydra::cached_stream(dev, &st));
@@ -795,7 +964,7 @@ int simulate_impl(int algo, int root, int op, int dtype, int flags, int P, void*
   auto step = [](hipError_t e, const char* what) {
     return e == hipSuccess ? 0 : hydra::hip_fail(e, what);
   };
-  rc = step(hipDeviceSynchronize(), "simulate teardown: hipDeviceSynchronize before the frees");
+  rc = step(hydra::drain_device(-1), "simulate teardown: hipDeviceSynchronize before the frees");
   for (auto& r : R) {
     if (r.scratch && !rc) rc = step(hydra::cached_free(r.scratch), "simulate teardown: release scratch");
     else if (r.scratch) (void)hydra::cached_free(r.scratch);
@@ -803,7 +972,7 @@ int simulate_impl(int algo, int root, int op, int dtype, int flags, int P, void*
   }
   hipError_t ed = hydra::release_stream(st);
   if (!rc) rc = step(ed, "simulate teardown: release stream");
-  if (!rc) rc = step(hipDeviceSynchronize(), "simulate teardown: hipDeviceSynchronize after the frees");
+  if (!rc) rc = step(hydra::drain_device(-1), "simulate teardown: hipDeviceSynchronize after the frees");
   return rc ? rc : ok();
 }
 }  // namespace
@@ -828,9 +997,11 @@ int hydra_comm_run_plan(hydra_comm_t c, const hydra_plan_op_t* ops, size_t nops,
                         hydra_stream_t stream) {
   if (!c || (!ops && nops)) return fail(HYDRA_ERR_INVALID, "null argument");
   if (c->aborted) return fail(HYDRA_ERR_TIMEOUT, "communicator was aborted by an earlier timeout");
+  hydra::DeviceScope ds(c->device);
   size_t es;
   int rc = check_plan_args(HYDRA_ALGO_RING, op, dtype, flags, &es);
   if (rc) return rc;
+  if ((rc = capture_guard(c, flags, static_cast<hipStream_t>(stream)))) return rc;
   std::vector<hydra::PlanOp> plan(nops);
   if (nops) std::memcpy(plan.data(), ops, nops * sizeof(hydra::PlanOp));
   // every access must stay inside buf / scratch: a bad plan must fail here, not fault the GPU
@@ -851,6 +1022,7 @@ int hydra_comm_run_plan(hydra_comm_t c, const hydra_plan_op_t* ops, size_t nops,
   hipStream_t st = static_cast<hipStream_t>(stream);
   // deterministic scratch for the hook (slots a 1-rank collective leaves untouched read as 0)
   if (scratch_bytes) HIP_TRY(hipMemsetAsync(c->scratch, 0, scratch_bytes, st));
+  if ((rc = prof_begin(c, st))) return rc;
   HIP_TRY(hipEventRecord(c->ev_start, st));
   rc = run_plan_rccl(c, op, dtype, (flags & HYDRA_ACC_F32) != 0, static_cast<char*>(buf),
                      c->ev_start);

@@ -201,6 +201,16 @@ class XgmiComm:
                                                code, flags, t.data_ptr(), _count(t, code),
                                                max_segment, chunk_bytes, s))
 
+    def profile(self, enable: bool) -> None:
+        """hydra_comm_profile: time every op of the following allreduces (measurement only)."""
+        check(_lib.lib().hydra_comm_profile(self._h, 1 if enable else 0))
+
+    def phases(self) -> dict:
+        """hydra_comm_phases: per-phase totals of the allreduces since profile(True)."""
+        ph = _lib.CommPhases()
+        check(_lib.lib().hydra_comm_phases(self._h, ctypes.byref(ph)))
+        return {f: getattr(ph, f) for f, _ in _lib.CommPhases._fields_ if f != "reserved"}
+
     def wait(self, timeout_ms: int, stream: int | None = None) -> None:
         """Block until the work enqueued on `stream` (default: current) is done; past timeout_ms
         the communicator is aborted and HydraError(ERR_TIMEOUT, "Timed out waiting ...") is
@@ -377,6 +387,47 @@ def expected_bcube_f32(xs: list[np.ndarray]) -> np.ndarray:
     for r in range(P):
         mo, ml = rng[r]
         out[mo:mo + ml] = part[r][mo:mo + ml]
+    return out
+
+
+HBM_PEAK_GBS = 8000.0
+XGMI_LINK_GBS = 153.0
+
+
+def phase_report(ph: dict, P: int, n: int, esize: int) -> dict:
+    """The N>1 line's own roofline evidence from one profiled (untimed) allreduce: comm-stream
+    (link) vs compute-stream (fold) busy time, their overlap, per-link GB/s against one xGMI
+    link, and the fold kernels' HBM fraction.  Algorithmic bytes: per-rank link bytes
+    2(P-1)/P*n*E and fused-sum HBM bytes (P-1)/P*n*3E (SURVEY.md 8(d): 12 B/element for fp32);
+    the fold kernels' own algorithmic bytes ((nsrc+1) x block per FOLD, 3 x segment per REDUCE)
+    beside them."""
+    calls = max(1, int(ph.get("calls", 0)))
+    link, fold, span = ph["link_ms"] / calls, ph["fold_ms"] / calls, ph["span_ms"] / calls
+    sent = ph["sent_bytes"] / calls
+    peers = max(1, int(ph.get("peers", 0)))
+    fused = (P - 1) / P * n * 3 * esize
+    kern = ph["fold_hbm_bytes"] / calls
+    out = {
+        "calls": int(ph.get("calls", 0)),
+        "link_ms": round(link, 4), "fold_ms": round(fold, 4), "span_ms": round(span, 4),
+        "overlap_ms": round(max(0.0, link + fold - span), 4),
+        "bound": "link" if link >= fold else "fold",
+        "link": {"sent_bytes": int(sent), "recv_bytes": int(ph["recv_bytes"] / calls),
+                 "algorithmic_bytes": int(2 * (P - 1) / P * n * esize), "peers": peers,
+                 "ops": int(ph["link_ops"] / calls),
+                 "aggregate_GBps": round(sent / (link * 1e-3) / 1e9, 2) if link > 0 else None,
+                 "per_link_GBps": (round(sent / peers / (link * 1e-3) / 1e9, 2)
+                                   if link > 0 else None),
+                 "link_peak_GBps": XGMI_LINK_GBS},
+        "fold": {"kernel_hbm_bytes": int(kern), "fused_sum_bytes": int(fused),
+                 "ops": int(ph["fold_ops"] / calls),
+                 "kernel_GBps": round(kern / (fold * 1e-3) / 1e9, 1) if fold > 0 else None,
+                 "hbm_peak_GBps": HBM_PEAK_GBS},
+    }
+    if out["link"]["per_link_GBps"] is not None:
+        out["link"]["frac_of_link"] = round(out["link"]["per_link_GBps"] / XGMI_LINK_GBS, 4)
+    if out["fold"]["kernel_GBps"] is not None:
+        out["fold"]["frac_of_hbm"] = round(out["fold"]["kernel_GBps"] / HBM_PEAK_GBS, 4)
     return out
 
 
@@ -563,13 +614,41 @@ def bench_allreduce(args, dev, make_comm=None, sync=None, cpu_baseline=None) -> 
             if not full_ok[chosen]:  # never time a schedule that missed the reference bits
                 chosen, chunk = "direct", 0
         ms, lat_ms = measure(chosen, chunk)
+        phases = {}
+
+        def profile_step(name, a, t, ch, esize, **kw):
+            """One untimed, profiled allreduce after the timed region (the executor's own
+            timing events on its comm and compute streams): the line's per-phase evidence."""
+            if a in _lib.PEER_ALGOS:
+                phases[name] = "n/a: one peer-access kernel (no separate link / fold phases)"
+                return
+            err = None
+            try:
+                comm.profile(True)
+                try:
+                    run(a, t, ch, **kw)
+                    sync()
+                    ph = comm.phases()
+                finally:
+                    comm.profile(False)
+                phases[name] = dict(phase_report(ph, world, t.numel(), esize), algo=a,
+                                    chunk_bytes=ch)
+            except HydraError as e:
+                err = str(e)
+            if any_rank_failed(err):
+                phases[name] = f"n/a: {err or 'another rank failed'}"
+
+        def any_rank_failed(err):
+            return max_over_ranks(1.0 if err else 0.0, dev) > 0
+
+        profile_step("config4", chosen, x, chunk, 4)
         # 4) context: the other algorithms on the same bucket (fewer steps)
         others = {}
         c5 = None
 
         def _result(ms_, lat_, others_, c5_):
             return _bench_result(n, world, args, chosen, chunk, tuning, parity, full_ok, ms_,
-                                 lat_, dict(others_), c5_, comm_seen, cpu_base)
+                                 lat_, dict(others_), c5_, comm_seen, cpu_base, phases)
 
         # the reference's own ring on this host's cores (bench.py's baseline leg: rank 0 only,
         # outside every timed region; the other ranks wait at the barrier)
@@ -709,6 +788,10 @@ def bench_allreduce(args, dev, make_comm=None, sync=None, cpu_baseline=None) -> 
             else:
                 full_ok["config5_bf16_acc32"] = max_over_ranks(0.0 if good else 1.0, dev) == 0.0
                 r5 = context_leg(bstep, k5, warm=2)
+                if not isinstance(r5, str):
+                    profile_step("config5", c5_algo, xb,
+                                 chunk if c5_algo in ("direct", "peer2") else 0, 2,
+                                 dtype_code=_lib.BFLOAT16, flags=_lib.ACC_F32)
                 if isinstance(r5, str):
                     c5 = {"elements": n5, "algo": c5_algo, "error": r5}
                 else:
@@ -761,7 +844,7 @@ def bench_allreduce(args, dev, make_comm=None, sync=None, cpu_baseline=None) -> 
 
 
 def _bench_result(n, world, args, chosen, chunk, tuning, parity, full_ok, ms, lat_ms, others,
-                  c5, comm_seen=None, cpu_base=None) -> dict:
+                  c5, comm_seen=None, cpu_base=None, phases=None) -> dict:
     """The N>1 bench JSON line (bench_allreduce; also printed by its watchdog once the headline
     is measured)."""
     bucket = 4.0 * n
@@ -790,15 +873,23 @@ def _bench_result(n, world, args, chosen, chunk, tuning, parity, full_ok, ms, la
         "algbw_GBps": round(algbw, 2), "busbw_GBps": round(busbw, 2),
         "roofline": {"bound": "xgmi", "achieved": round(busbw, 2),
                      "peak": round(link * max(1, world - 1), 1), "unit": "GB/s",
-                     "frac": round(busbw / (link * max(1, world - 1)), 4), "traffic": None,
+                     "frac": round(busbw / (link * max(1, world - 1)), 4),
+                     "traffic": int((world - 1) / world * n * 12),
+                     "traffic_kind": "algorithmic, not measured: the fused-sum HBM bytes per "
+                                     "rank per allreduce, (P-1)/P x n x 12 (SURVEY.md 8(d)); no "
+                                     "PMC pass runs at N > 1",
+                     "phases": (phases or {}).get("config4"),
                      "note": "busbw vs (P-1) xGMI links x 153 GB/s; a single ring is bound by "
-                             "1 link (153 GB/s)"},
+                             "1 link (153 GB/s); phases = one profiled untimed allreduce after "
+                             "the timed region (link = comm-stream busy time, fold = compute-"
+                             "stream busy time)"},
         "latency_ms": lat_ms,
         "other_algos_ms": others,
         "other_algos_busbw_GBps": {a: round(bucket / (v * 1e-3) / 1e9 * 2 * (world - 1) / world, 2)
                                    for a, v in others.items()
                                    if isinstance(v, float) and a != "reduce_root0"},
-        "config5_bf16": c5,
+        "config5_bf16": (dict(c5, phases=(phases or {}).get("config5"))
+                         if isinstance(c5, dict) else c5),
         "parity": {"fold_order_1M": parity, "full_size_exact": full_ok},
         "rccl_comm": comm_seen,
         "cpu_baseline": cpu_base,

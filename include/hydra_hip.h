@@ -54,6 +54,12 @@ typedef enum {
 typedef enum { HYDRA_SUM = 0, HYDRA_PRODUCT = 1, HYDRA_MAX = 2, HYDRA_MIN = 3 } hydra_op_t;
 
 #define HYDRA_ACC_F32 1 /* flag: bf16 data, fp32 accumulation, one rounding */
+/* flag (hydra_allreduce & co.): enqueue a multi-rank schedule even while the stream is being
+ * captured into a hipGraph.  Without it such a call fails with HYDRA_ERR_UNSUPPORTED: on the
+ * socket-linked ranks of the test box, ending the capture of RCCL's own ncclAllReduce segfaults
+ * inside hipStreamEndCapture (profiles/r03g2_graph_ranks_rccl.log), so the library refuses
+ * rather than let the caller's process die.  Set it on a node whose RCCL captures. */
+#define HYDRA_ALLOW_CAPTURE 2
 
 typedef enum {
   HYDRA_OK = 0,
@@ -300,6 +306,28 @@ int hydra_reduce_root(hydra_comm_t comm, int root, int op, int dtype, int flags,
  * and HYDRA_ERR_TIMEOUT is returned with "Timed out waiting <ms>ms for ..."; the communicator
  * is then unusable (destroy it).  RCCL's asynchronous errors are reported the same way. */
 int hydra_comm_wait(hydra_comm_t comm, hydra_stream_t stream, int64_t timeout_ms);
+
+/* Per-phase timing of a communicator's allreduces (measurement, not for the timed region): while
+ * profiling is on, every p2p group / collective on the comm stream and every fold kernel on the
+ * compute stream is bracketed by timing events.  hydra_comm_phases waits for the profiled work
+ * and returns the totals since profiling was switched on:
+ *   link_ms   comm-stream busy time (sum over p2p groups and collectives)
+ *   fold_ms   compute-stream busy time (sum over REDUCE / FOLD kernels)
+ *   span_ms   sum over calls of first enqueue (the call's start on the caller's stream) to the
+ *             last op's end; link_ms + fold_ms - span_ms > 0 is the overlap of the two streams
+ *   sent_bytes / recv_bytes   this rank's link bytes (p2p sends / receives and the collectives'
+ *             off-rank share), peers = distinct peers it sent to (links used per call)
+ *   fold_hbm_bytes   the fold kernels' algorithmic HBM bytes ((nsrc + 1) x block bytes per FOLD,
+ *             3 x segment bytes per REDUCE)
+ * A communicator's own device is used whatever the caller's current device is. */
+typedef struct {
+  uint64_t calls, link_ops, fold_ops;
+  double link_ms, fold_ms, span_ms;
+  uint64_t sent_bytes, recv_bytes, fold_hbm_bytes;
+  int32_t peers, reserved;
+} hydra_comm_phases_t;
+int hydra_comm_profile(hydra_comm_t comm, int enable); /* 1: on, totals reset; 0: off */
+int hydra_comm_phases(hydra_comm_t comm, hydra_comm_phases_t* out);
 
 /* ---- bew_allreduce_a on device: two rails (pipeallreduce-a.cc:27-61) ---------------------- */
 #ifndef HYDRA_SPLIT_AA

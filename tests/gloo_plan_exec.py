@@ -36,19 +36,49 @@ def fold_slot(o, j):
     return o["src_off"] + ((o["peer"] + j) % o["nsrc"]) * o["slot_stride"]
 
 
-def execute(O, ops, scratch_bytes, user, code=6, op="sum"):
+class _Prof:
+    """hydra_comm_phases' totals for the synchronous executor (perf_counter per op)."""
+
+    def __init__(self):
+        import time
+
+        self.clock = time.perf_counter
+        self.d = dict(calls=0, link_ops=0, fold_ops=0, link_ms=0.0, fold_ms=0.0, span_ms=0.0,
+                      sent_bytes=0, recv_bytes=0, fold_hbm_bytes=0, peers=0)
+        self.peers = set()
+
+    def op(self, comm, t0, sent=0, recv=0, hbm=0, peers=()):
+        ms = (self.clock() - t0) * 1e3
+        self.d["link_ms" if comm else "fold_ms"] += ms
+        self.d["link_ops" if comm else "fold_ops"] += 1
+        self.d["sent_bytes"] += sent
+        self.d["recv_bytes"] += recv
+        self.d["fold_hbm_bytes"] += hbm
+        self.peers.update(peers)
+        self.d["peers"] = len(self.peers)
+
+
+def execute(O, ops, scratch_bytes, user, code=6, op="sum", prof=None):
     """Run `ops` on `user` (a contiguous CPU uint8 tensor, modified in place) on this rank.
     code BFLOAT16 is the ACC_F32 form (config 5): each fold in fp32 in the same order, one
-    round to bf16 at the end, as k_fold<bf16, ACC32> computes it (sum only)."""
+    round to bf16 at the end, as k_fold<bf16, ACC32> computes it (sum only).  prof: a _Prof
+    that accumulates per-op times and bytes as hydra_comm_phases does."""
+    import time
+
     import torch
     import torch.distributed as dist
 
     rank, world = dist.get_rank(), dist.get_world_size()
     dt = _NP[code]
     scratch = torch.zeros(scratch_bytes + 16, dtype=torch.uint8)
+    others = [q for q in range(world) if q != rank]
+    c0 = time.perf_counter()
     i = 0
     while i < len(ops):
         o = ops[i]
+        t0 = time.perf_counter()
+        if o["kind"] in (ALLTOALL, ALLGATHER) and prof is not None:
+            prof.peers.update(others)  # a collective sends to every other rank
         if o["kind"] == ALLTOALL:  # ncclAllToAll semantics via p2p
             B = o["bytes"]
             scratch[o["src_off"] + rank * B:o["src_off"] + (rank + 1) * B] = \
@@ -63,6 +93,8 @@ def execute(O, ops, scratch_bytes, user, code=6, op="sum"):
                                                           o["src_off"] + (pr + 1) * B], pr))
             for req in dist.batch_isend_irecv(p2p):
                 req.wait()
+            if prof is not None:
+                prof.op(True, t0, B * (world - 1), B * (world - 1))
             i += 1
             continue
         if o["kind"] == ALLGATHER:
@@ -72,6 +104,8 @@ def execute(O, ops, scratch_bytes, user, code=6, op="sum"):
             dist.all_gather(parts, mine)
             for pr in range(world):
                 user[o["off"] + pr * B:o["off"] + (pr + 1) * B] = parts[pr]
+            if prof is not None:
+                prof.op(True, t0, B * (world - 1), B * (world - 1))
             i += 1
             continue
         if o["kind"] in (REDUCE, FOLD):
@@ -97,19 +131,33 @@ def execute(O, ops, scratch_bytes, user, code=6, op="sum"):
                     acc = O.op(s.copy(), acc, op, code)
                 out = O.op(local, acc, op, code)
             u[o["off"]:o["off"] + o["bytes"]] = out.view(np.uint8)
+            if prof is not None:
+                prof.op(False, t0, hbm=o["bytes"] * (3 if o["kind"] == REDUCE else o["nsrc"] + 1))
             i += 1
             continue
         g = i
         p2p = []
+        sent = recv = 0
+        dests = set()
         while ops[g]["kind"] != GROUP:
             it = ops[g]
             t = (user if it["buf"] == 0 else scratch)[it["off"]:it["off"] + it["bytes"]]
             p2p.append(dist.P2POp(dist.isend if it["kind"] == SEND else dist.irecv, t, it["peer"]))
+            if it["kind"] == SEND:
+                sent += it["bytes"]
+                dests.add(it["peer"])
+            else:
+                recv += it["bytes"]
             g += 1
         if p2p:
             for req in dist.batch_isend_irecv(p2p):
                 req.wait()
+        if prof is not None:
+            prof.op(True, t0, sent, recv, peers=dests)
         i = g + 1
+    if prof is not None:
+        prof.d["calls"] += 1
+        prof.d["span_ms"] += (time.perf_counter() - c0) * 1e3
 
 
 _OPC = {"sum": 0, "product": 1, "max": 2, "min": 3}
@@ -206,6 +254,15 @@ class GlooPlanComm:
         self.O = O
         self.rank, self.world = dist.get_rank(), dist.get_world_size()
         self.closed = False
+        self._prof = None
+
+    def profile(self, enable):
+        """XgmiComm.profile: per-op timing of the following calls (perf_counter here)."""
+        self._prof = _Prof() if enable else None
+
+    def phases(self):
+        """XgmiComm.phases: hydra_comm_phases' fields."""
+        return dict(self._prof.d) if self._prof is not None else dict(_Prof().d)
 
     def _code(self, t, dtype_code):
         from hydra_amd._lib import HydraError
@@ -236,7 +293,7 @@ class GlooPlanComm:
             return
         ops, scr = ring.plan(algo, self.world, self.rank, n,
                              t.element_size(), max_segment, chunk_bytes)
-        execute(self.O, ops, scr, t.view(-1).view(torch.uint8), code, op)
+        execute(self.O, ops, scr, t.view(-1).view(torch.uint8), code, op, self._prof)
 
     def reduce_(self, t, root, op="sum", dtype_code=None, flags=0, max_segment=0,
                 chunk_bytes=0, stream=None):

@@ -150,6 +150,33 @@ def _worker(rank, world, port, q):
             if e1 < n:
                 exp[e1:] = O.ring_result([x[e1:].copy() for x in xs])
             res[f"apipe_n{n}"] = bool(np.array_equal(_bits(t.cpu().numpy()), _bits(exp)))
+        # the per-phase profile the N>1 bench line carries: the executor's own timing events on
+        # its comm and compute streams, across real ranks; link bytes are the schedule's
+        n = 4 << 20
+        xs = [synth.stress_f32(world, r, n) for r in range(world)]
+        for algo in ("direct", "ring") + (("a2a",) if world != 3 else ()):
+            t = torch.from_numpy(xs[rank].copy()).to(dev)
+            dev_before = torch.cuda.current_device()
+            comm.profile(True)
+            comm.allreduce_(t, algo=algo)
+            comm.wait(60000)
+            ph = comm.phases()
+            comm.profile(False)
+            ok = (ph["calls"] == 1 and ph["link_ms"] > 0 and ph["fold_ms"] > 0
+                  and ph["span_ms"] >= 0.999 * max(ph["link_ms"], ph["fold_ms"])
+                  and ph["sent_bytes"] == ph["recv_bytes"] and ph["fold_hbm_bytes"] > 0
+                  and ph["peers"] == (1 if algo == "ring" else world - 1)
+                  and torch.cuda.current_device() == dev_before)
+            if world != 3:  # equal blocks: exactly the reference ring's link bytes
+                ok = ok and ph["sent_bytes"] == 2 * (world - 1) * n * 4 // world
+            if algo != "ring" and world != 3:  # one P-way fold per block
+                ok = ok and ph["fold_hbm_bytes"] == (world + 1) * n * 4 // world
+            if algo == "ring" and world != 3:  # P-1 fused 2R1W hops: SURVEY 8(d)'s (P-1)/P*n*12
+                ok = ok and abs(ph["fold_hbm_bytes"] - (world - 1) * n * 12 / world) <= 12 * world
+            res[f"phases_{algo}"] = ok and bool(np.array_equal(
+                _bits(t.cpu().numpy()), _bits(O.ring_result(xs))))
+            if not res[f"phases_{algo}"]:
+                res[f"phases_{algo}_detail"] = str(ph)
         q.put((rank, res))
     except Exception as e:  # report instead of hanging the parent
         import traceback
@@ -262,3 +289,65 @@ def test_rccl_wait_times_out_on_missing_peer(gpu, mode):
     assert res[0] == {"warm_up": True, "timed_out": True, "refuses_after_abort": True,
                       "closed": True}, res
     assert res[1].get("warm_up") is True and "error" not in res[1], res
+
+
+def _capture_worker(rank, world, port, q):
+    """a multi-rank allreduce issued while its stream is being captured into
+    a hipGraph returns HYDRA_ERR_UNSUPPORTED (naming the RCCL capture segfault it avoids) instead
+    of killing the process at hipStreamEndCapture; the communicator keeps working afterwards."""
+    import sys
+
+    sys.path.insert(0, ROOT)
+    os.environ.update(RANK_ENV)
+    os.environ["NCCL_HOSTID"] = f"hydra-test-rank-{rank}"
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch
+    import torch.distributed as dist
+
+    from hydra_amd import _lib, ring
+
+    res = {}
+    comm = None
+    try:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        torch.cuda.set_device(0)
+        dev = torch.device("cuda", 0)
+        comm = ring.XgmiComm(rank, world, 0, ring.exchange_unique_id(rank))
+        t = torch.ones(1 << 20, dtype=torch.float32, device=dev)
+        s = torch.cuda.Stream(dev)
+        g = torch.cuda.CUDAGraph()
+        err = None
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g, stream=s):
+                try:
+                    comm.allreduce_(t, algo="auto", stream=s.cuda_stream)
+                except _lib.HydraError as e:
+                    err = e
+        res["refused"] = (err is not None and err.code == _lib.ERR_UNSUPPORTED
+                          and "r03g2_graph_ranks_rccl" in str(err))
+        torch.cuda.synchronize()
+        comm.allreduce_(t, algo="auto")  # outside the capture: works as before
+        comm.wait(30000)
+        res["after"] = float(t[0]) == float(world) and float(t[-1]) == float(world)
+        comm.close()
+        comm = None
+        res["closed"] = True
+    except Exception as e:  # report instead of hanging the parent
+        import traceback
+
+        res["error"] = repr(e) + traceback.format_exc()[-1200:]
+    finally:
+        if comm is not None:
+            try:
+                comm.close()
+            except Exception:
+                pass
+    q.put((rank, res))
+    dist.destroy_process_group()
+
+
+def test_multi_rank_capture_is_refused(gpu):
+    res = _spawn(_capture_worker, 2, timeout=90)
+    for r in range(2):
+        assert res[r] == {"refused": True, "after": True, "closed": True}, res

@@ -282,3 +282,110 @@ def test_resident_multi_round_calls(ctx, O, n):
     assert np.array_equal(bits(a), bits(exp))
     rounds = ctx.stats()["resident_calls"] - s0["resident_calls"]
     assert rounds >= 2 * (-(-n * 4 // (4 << 20))), rounds
+
+
+_SOLO_STREAM = r"""
+import json, sys, time, numpy as np
+sys.path.insert(0, %r)
+import torch
+from hydra_amd import _lib, synth
+from hydra_amd.reduce import HostContext
+from oracle import oracle as O
+L = _lib.lib()
+c = HostContext(0)
+def call(n, seed):
+    a, b = synth.stress_f32(2, 0, n, seed=seed), synth.stress_f32(2, 1, n, seed=seed)
+    e = O.op(a, b, "sum", 6)
+    _lib.check(L.hydra_reduce_host(c.handle, 0, 6, a.ctypes.data, a.ctypes.data, b.ctypes.data, n))
+    assert np.array_equal(a.view(np.uint32), e.view(np.uint32)), n
+call(50000, 0)  # a published job: every worker has seen one
+t0, k = time.perf_counter(), 0
+while time.perf_counter() - t0 < 0.4:  # solo calls only (<= 4 tiles), well past idle + grace
+    call(1000 + k %% 3000, k)
+    k += 1
+for i in range(3):  # then published jobs again: the workers must still be there
+    call(50000 + 4097 * i, 100 + i)
+st = c.stats()
+c.close()
+print(json.dumps({"solo_calls": k, "launches": st["resident_launches"]}))
+"""
+
+
+def test_resident_solo_calls_past_the_grace_period(gpu):
+    """a steady stream of solo calls (workgroup 0 alone, nothing published)
+    longer than idle + grace must not make the waiting workers give up -- they follow workgroup
+    0's heartbeat -- and a large call afterwards is served by the same instance, exactly.
+    Grace shortened to 20 ms (HYDRA_RESIDENT_GRACE_US) so 0.4 s of solo calls crosses it 16x."""
+    import json
+
+    p = subprocess.run([sys.executable, "-c", _SOLO_STREAM % ROOT], capture_output=True,
+                       text=True, timeout=120,
+                       env=dict(os.environ, HYDRA_RESIDENT_GRACE_US="20000",
+                                HYDRA_RESIDENT_IDLE_US="5000"))
+    assert p.returncode == 0, (p.stdout[-1000:], p.stderr[-3000:])
+    r = json.loads(p.stdout.strip().splitlines()[-1])
+    assert r["solo_calls"] > 100, r
+    assert r["launches"] == 1, r  # one instance served everything: nobody left on an error
+
+
+def test_resident_device_drains_are_bounded(gpu, O):
+    """while another thread keeps the resident reducer busy with host calls,
+    the library's own device-wide drains -- freeing a pinned block, trimming the caches,
+    destroying a context, hydra_device_check -- stop the instance first instead of waiting for
+    the calls to stop.  Each returns within 50 ms; every concurrent call stays bit-exact."""
+    L = _lib.lib()
+    stop = threading.Event()
+    errs, calls = [], [0]
+
+    def loop():
+        c = HostContext(0)
+        try:
+            i = 0
+            while not stop.is_set():
+                n = (3000, 40000, 70001)[i % 3]
+                a, b = synth.stress_f32(2, 0, n, seed=i), synth.stress_f32(2, 1, n, seed=i)
+                exp = O.op(a, b, "sum", 6)
+                rc = L.hydra_reduce_host(c.handle, 0, 6, a.ctypes.data, a.ctypes.data,
+                                         b.ctypes.data, n)
+                if rc or not np.array_equal(bits(a), bits(exp)):
+                    errs.append((i, rc, L.hydra_last_error()))
+                    return
+                i += 1
+                calls[0] = i
+        finally:
+            c.close()
+
+    import ctypes
+
+    th = threading.Thread(target=loop)
+    th.start()
+    times = {}
+    try:
+        time.sleep(0.2)
+        for rep in range(3):
+            p = ctypes.c_void_p()
+            _lib.check(L.hydra_malloc_host(1 << 20, ctypes.byref(p)))
+            t0 = time.perf_counter()
+            _lib.check(L.hydra_free_host(p))
+            times[f"free_pinned_{rep}"] = time.perf_counter() - t0
+            t0 = time.perf_counter()
+            _lib.check(L.hydra_device_check(0))
+            times[f"device_check_{rep}"] = time.perf_counter() - t0
+            c2 = HostContext(0)
+            t0 = time.perf_counter()
+            c2.close()
+            times[f"ctx_destroy_{rep}"] = time.perf_counter() - t0
+            t0 = time.perf_counter()
+            _lib.check(L.hydra_cache_trim())
+            times[f"cache_trim_{rep}"] = time.perf_counter() - t0
+            time.sleep(0.05)
+        n0 = calls[0]
+        time.sleep(0.1)
+        still_serving = calls[0] > n0
+    finally:
+        stop.set()
+        th.join(timeout=60)
+    assert not errs, errs
+    assert still_serving and calls[0] > 50, calls
+    slow = {k: round(v * 1e3, 2) for k, v in times.items() if v > 0.05}
+    assert not slow, (slow, {k: round(v * 1e3, 2) for k, v in times.items()})
