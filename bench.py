@@ -228,50 +228,119 @@ def pmc_traffic():
     return d.get("hbm_bytes_per_launch"), dict(info, status="matches these kernel sources")
 
 
+def _read(path):
+    try:
+        with open(path) as f:
+            return f.read().strip()
+    except OSError:
+        return None
+
+
+def _cpulist(text):
+    out = []
+    for part in (text or "").split(","):
+        if "-" in part:
+            lo, hi = part.split("-")
+            out.extend(range(int(lo), int(hi) + 1))
+        elif part.strip():
+            out.append(int(part))
+    return out
+
+
+def gpu_numa_node(device_index=0):
+    """NUMA node of the GPU (its PCI device's numa_node in sysfs), or None."""
+    try:
+        import torch
+
+        pr = torch.cuda.get_device_properties(device_index)
+        bus = "%04x:%02x:%02x.0" % (getattr(pr, "pci_domain_id", 0), pr.pci_bus_id,
+                                    pr.pci_device_id)
+        node = _read(f"/sys/bus/pci/devices/{bus}/numa_node")
+        return int(node) if node is not None and int(node) >= 0 else None
+    except Exception:
+        return None
+
+
+def baseline_cores(k, device_index=0):
+    """k host CPUs for the CPU baselines: on the GPU's NUMA node (as a rank process runs,
+    DESIGN.md 6.3), never CPU 0 (the housekeeping / interrupt core) nor its SMT sibling, one
+    logical CPU per physical core while there are enough; within this process's affinity.
+    Returns (cpus, node, note)."""
+    aff = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else []
+    node = gpu_numa_node(device_index)
+    pool = [c for c in _cpulist(_read(f"/sys/devices/system/node/node{node}/cpulist"))
+            if c in aff] if node is not None else []
+    note = f"GPU NUMA node {node}" if pool else "GPU NUMA node unknown: process affinity"
+    pool = pool or aff
+    avoid = {0} | set(_cpulist(_read("/sys/devices/system/cpu/cpu0/topology/thread_siblings_list")))
+    cand = [c for c in pool if c not in avoid] or pool
+    firsts, seen = [], set()
+    for c in cand:  # one logical CPU per physical core first
+        sib = tuple(_cpulist(_read(f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list"))
+                    or [c])
+        if sib not in seen:
+            seen.add(sib)
+            firsts.append(c)
+    order = firsts + [c for c in cand if c not in firsts]
+    return order[:max(1, k)], node, note
+
+
+def _host_cpu():
+    try:
+        with open("/proc/cpuinfo") as f:
+            return next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")),
+                        None)
+    except OSError:
+        return None
+
+
 def cpu_baseline(n, seconds):
     """The reference's own gloo::sum<float> (oracle/_ref, compiled from /root/reference) timed
     single-threaded on this host at the headline's size; falls back to the C restatement
-    (oracle/liboracle.so)."""
+    (oracle/liboracle.so).  Pinned to one core of the GPU's NUMA node (not CPU 0); three
+    repetitions, every one reported."""
     from oracle import oracle as O
 
     a = np.arange(n, dtype=np.float32)
     b = np.ones(n, dtype=np.float32)
     kind = "reference" if O.ref_available() else "port"
-    # pinned to ONE host core for the measurement (SURVEY §8d), restored afterwards
     prev_aff = os.sched_getaffinity(0) if hasattr(os, "sched_getaffinity") else None
-    core = min(prev_aff) if prev_aff else None
+    cores, node, note = baseline_cores(1)
+    core = cores[0] if cores else None
     if core is not None:
         os.sched_setaffinity(0, {core})
     try:
-        # calibrate, then run ~`seconds` of work (3 repetitions, best mean)
+        # calibrate, then ~`seconds` of work as 3 timed repetitions (mean per call of each)
+        reps = []
         if kind == "reference":
             per = O.ref_time_sum(6, a, a, b, 1, 1)
             iters = max(1, int(seconds / max(per, 1e-6) / 3))
-            per = O.ref_time_sum(6, a, a, b, iters, 3)
+            for _ in range(3):
+                reps.append(O.ref_time_sum(6, a, a, b, iters, 1))
         else:
+            per = 0.0
             t0 = time.perf_counter()
-            k = 0
-            while time.perf_counter() - t0 < seconds:
-                O.orc().orc_op(0, 6, a.ctypes.data, a.ctypes.data, b.ctypes.data, n)
-                k += 1
-            iters = k
-            per = (time.perf_counter() - t0) / k
+            O.orc().orc_op(0, 6, a.ctypes.data, a.ctypes.data, b.ctypes.data, n)
+            iters = max(1, int(seconds / max(time.perf_counter() - t0, 1e-6) / 3))
+            for _ in range(3):
+                t0 = time.perf_counter()
+                for _ in range(iters):
+                    O.orc().orc_op(0, 6, a.ctypes.data, a.ctypes.data, b.ctypes.data, n)
+                reps.append((time.perf_counter() - t0) / iters)
     finally:
-        if core is not None:
+        if core is not None and prev_aff:
             os.sched_setaffinity(0, prev_aff)
-    gbs = 12.0 * n / per / 1e9
-    model = None
-    try:
-        with open("/proc/cpuinfo") as f:
-            model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")),
-                         None)
-    except OSError:
-        pass
-    return {"value": round(gbs, 3), "unit": "GB/s", "cores": 1, "kind": kind,
-            "host_cpu": model, "host_logical_cpus": os.cpu_count(),
+    rates = [12.0 * n / r / 1e9 for r in reps]
+    per = float(np.median(reps))
+    return {"value": round(12.0 * n / per / 1e9, 3), "unit": "GB/s", "cores": 1, "kind": kind,
+            "host_cpu": _host_cpu(), "host_logical_cpus": os.cpu_count(),
+            "pinned_cpu": core, "numa_node": node, "placement": note,
+            "repetitions_GBps": [round(r, 3) for r in rates],
+            "spread": round((max(rates) - min(rates)) / float(np.median(rates)), 4),
             "sample": f"gloo::sum<float> in place over {n} fp32 elements (the headline's size, "
-                      f"12 B/element), single thread pinned to host core {core}, {iters} calls x "
-                      f"3 repetitions (~{seconds:.0f} s), best-of-3 mean",
+                      f"12 B/element), single thread pinned to host CPU {core} ({note}), "
+                      f"{iters} calls x 3 repetitions (~{seconds:.0f} s); value = the median "
+                      "repetition",
             "per_call_ms": round(per * 1e3, 3)}
 
 
@@ -384,24 +453,29 @@ def ring_cpu_baseline(P, n, seconds):
 
     if not O.ref_available():
         raise RuntimeError("oracle/_ref (the reference built from its sources) is not present")
-    t0 = time.perf_counter()
-    O.ref_bench_ring(P, n, 0, 1)  # calibration (connect + one allreduce)
-    per = max(time.perf_counter() - t0, 1e-3)
-    iters = int(max(1, min(20, seconds / per)))
-    s = O.ref_bench_ring(P, n, 1, iters) * 1e-9  # seconds per iteration, rank 0
-    avg = float(np.mean(s))
-    model = None
+    # the 2P threads (1 user + 1 event loop per rank) on 2P CPUs of the GPU's NUMA node, not
+    # CPU 0 (the reference's threads inherit the process affinity)
+    prev_aff = os.sched_getaffinity(0) if hasattr(os, "sched_getaffinity") else None
+    cores, node, note = baseline_cores(2 * P)
+    if cores:
+        os.sched_setaffinity(0, set(cores))
     try:
-        with open("/proc/cpuinfo") as f:
-            model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")),
-                         None)
-    except OSError:
-        pass
+        t0 = time.perf_counter()
+        O.ref_bench_ring(P, n, 0, 1)  # calibration (connect + one allreduce)
+        per = max(time.perf_counter() - t0, 1e-3)
+        iters = int(max(1, min(20, seconds / per)))
+        s = O.ref_bench_ring(P, n, 1, iters) * 1e-9  # seconds per iteration, rank 0
+    finally:
+        if cores and prev_aff:
+            os.sched_setaffinity(0, prev_aff)
+    avg = float(np.mean(s))
+    model = _host_cpu()
     return {"value": round(P * 4.0 * n / avg / 1e9, 3), "unit": "GB/s", "cores": 2 * P,
-            "kind": "reference",
+            "kind": "reference", "pinned_cpus": cores, "numa_node": node, "placement": note,
             "sample": f"{iters} allreduces (after 1 warm-up) of the reference's gloo::allreduce "
                       f"RING + gloo::sum<float> over {n} fp32 elements per rank on {P} "
-                      "thread-ranks, loopback TCP (1 user + 1 event-loop thread per rank)",
+                      "thread-ranks, loopback TCP (1 user + 1 event-loop thread per rank), "
+                      f"pinned to CPUs {cores} ({note})",
             "value_def": "P x n x 4 B / mean per-iteration time (the same whole-job definition "
                          "as this line's value)",
             "ms_p50": round(float(np.percentile(s, 50)) * 1e3, 3),

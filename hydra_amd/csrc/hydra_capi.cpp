@@ -611,6 +611,35 @@ int hydra_event_destroy(hydra_event_t e) {
   return ok();
 }
 
+int hydra_stream_wait_event(hydra_stream_t s, hydra_event_t e) {
+  if (!e) return fail(HYDRA_ERR_INVALID, "null event");
+  HIP_TRY(hipStreamWaitEvent(static_cast<hipStream_t>(s), static_cast<hipEvent_t>(e), 0));
+  return ok();
+}
+
+int hydra_device_peer_access(int device, int peer, int* can) {
+  if (!can) return fail(HYDRA_ERR_INVALID, "null out");
+  *can = 0;
+  int count = 0;
+  HIP_TRY(hipGetDeviceCount(&count));
+  if (device < 0 || device >= count || peer < 0 || peer >= count)
+    return fail(HYDRA_ERR_NO_DEVICE, "no such device");
+  if (device == peer) {
+    *can = 1;
+    return ok();
+  }
+  int c = 0;
+  HIP_TRY(hipDeviceCanAccessPeer(&c, device, peer));
+  if (!c) return ok();
+  hydra::DeviceScope ds(device);
+  HIP_TRY(ds.err);
+  const hipError_t e = hipDeviceEnablePeerAccess(peer, 0);
+  if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) return hip_fail(e, "hipDeviceEnablePeerAccess");
+  (void)hipGetLastError();  // (already enabled is not an error here)
+  *can = 1;
+  return ok();
+}
+
 int hydra_malloc(int device, size_t bytes, void** out) {
   if (!out) return fail(HYDRA_ERR_INVALID, "null out");
   HIP_TRY(hydra::cached_malloc(device, bytes, out));

@@ -18,13 +18,27 @@
 //       D2H copy of scratch and round k forwards the box received in round k-1 (which holds
 //       exactly the bytes the reference's device outbox would).
 //
-// MI355X layout: one process per GPU, so every pointer must live on the same device (the
-// reference's multi-GPU-per-process peer-access tree is served here by the RCCL plans in
-// hydra_hip.h).  Only ReductionFunction SUM exists on this class, as in the reference
-// (fn_ = CudaReductionFunction<T>::sum, cuda_allreduce_ring.cc:26).
+// Pointers may live on several GPUs of the process, as CudaAllreduceRing accepts them
+// (cuda_allreduce_ring.cc:34-42: one stream per pointer, on the pointer's device):
+//   * every pointer's device is looked up once (hydra_pointer_device); owned streams and the
+//     ordering events are created on it;
+//   * the ring accumulates into one chosen pointer's device (findCudaDevicePointerClosestToDevice,
+//     cuda_allreduce_ring.cc:153-157): the smallest PCI distance to the transport's device.  The
+//     host runtime's TCP transport has no PCI device, so every distance is equal and the first
+//     pointer is chosen (the reference picks one of the equals at random: ours is one outcome);
+//   * each local-reduce step ptrs[a] op= ptrs[b] runs on a's device and stream, after a waits for
+//     b's stream (cuda_collectives_native.h:100-115); across devices the kernel reads b over
+//     peer access where hipDeviceCanAccessPeer allows it (enabled once, :63-84), otherwise b is
+//     first copied to a buffer on a's device (the reference refuses that case);
+//   * the broadcast copies the result to every pointer on that pointer's stream.
+// One GPU cannot exercise the cross-device branches; the bookkeeping (detail::local_steps) is
+// unit-tested on the CPU and the same code runs every single-device case.
+// Only ReductionFunction SUM exists on this class, as in the reference (fn_ =
+// CudaReductionFunction<T>::sum, cuda_allreduce_ring.cc:26).
 #pragma once
 
 #include <algorithm>
+#include <climits>
 #include <cstring>
 #include <memory>
 #include <type_traits>
@@ -65,6 +79,7 @@ struct DeviceMem {
   DeviceMem(int device, size_t bytes) { enforce(hydra_malloc(device, bytes ? bytes : 1, &p)); }
   DeviceMem(const DeviceMem&) = delete;
   DeviceMem& operator=(const DeviceMem&) = delete;
+  DeviceMem(DeviceMem&& o) noexcept : p(o.p) { o.p = nullptr; }
   DeviceMem& operator=(DeviceMem&& o) noexcept {
     std::swap(p, o.p);
     return *this;
@@ -73,6 +88,110 @@ struct DeviceMem {
     if (p) hydra_free(p);
   }
 };
+// ---- several devices per process: the local reduce's bookkeeping ---------------------------
+// One step of a local reduction: buffer a op= buffer b, run on a's device and stream.  `staged`:
+// a's device cannot read b's (no peer access), so b is first copied to a buffer on a's device.
+struct LocalStep {
+  size_t a, b;
+  bool staged;
+};
+
+// CudaLocalNativeReduce's pairwise tree (cuda_collectives_native.h:93-122) in pointer order:
+// level sz pairs (j, j + sz) for j a multiple of 2 sz; the result lands in pointer 0.  (The
+// reference shuffles the order at random, :53, and drops pointers beyond the largest power of
+// two, :36; every pointer is folded here.)
+template <typename CanPeer>
+std::vector<LocalStep> local_tree(const std::vector<int>& dev, CanPeer can_peer) {
+  std::vector<LocalStep> v;
+  for (size_t sz = 1; sz < dev.size(); sz *= 2)
+    for (size_t j = 0; j + sz < dev.size(); j += 2 * sz)
+      v.push_back({j, j + sz, dev[j] != dev[j + sz] && !can_peer(dev[j], dev[j + sz])});
+  return v;
+}
+
+// CudaLocalHostReduce's order (cuda_collectives_host.h:108-119): target = ptrs[0], then
+// target op= ptrs[i] for i = 1, 2, ... (a left fold in pointer order).
+template <typename CanPeer>
+std::vector<LocalStep> local_chain(const std::vector<int>& dev, CanPeer can_peer) {
+  std::vector<LocalStep> v;
+  for (size_t i = 1; i < dev.size(); i++)
+    v.push_back({0, i, dev[0] != dev[i] && !can_peer(dev[0], dev[i])});
+  return v;
+}
+
+// findCudaDevicePointerClosestToDevice (cuda_private.h:58-90): the pointer with the smallest
+// PCI distance to the transport's device; the first of equals.
+inline size_t closest_index(const std::vector<int>& distance) {
+  size_t best = 0;
+  int bd = INT_MAX;
+  for (size_t i = 0; i < distance.size(); i++)
+    if (distance[i] < bd) {
+      bd = distance[i];
+      best = i;
+    }
+  return best;
+}
+
+// Runs a step list on device buffers: per pointer i its device, stream and an ordering event;
+// one staging buffer per destination that needs one.
+class LocalReduce {
+ public:
+  LocalReduce() = default;
+  LocalReduce(const LocalReduce&) = delete;
+  LocalReduce& operator=(const LocalReduce&) = delete;
+  ~LocalReduce() {
+    for (auto e : ev_) hydra_event_destroy(e);
+  }
+  void init(std::vector<LocalStep> steps, const std::vector<int>& dev, size_t bytes) {
+    steps_ = std::move(steps);
+    ev_.assign(dev.size(), nullptr);
+    for (size_t i = 0; i < dev.size(); i++) enforce(hydra_event_create_on(dev[i], &ev_[i]));
+    stage_.clear();
+    stage_.resize(dev.size());
+    for (const LocalStep& s : steps_)
+      if (s.staged && !stage_[s.a].p) stage_[s.a] = DeviceMem(dev[s.a], bytes);
+  }
+  // buf[i]: the buffer standing for pointer i (pointer 0 may be a copy); streams[i] on dev[i]
+  void run(const std::vector<void*>& buf, const std::vector<hydra_stream_t>& streams, int dt,
+           int count, size_t bytes) {
+    for (const LocalStep& s : steps_) {
+      enforce(hydra_event_record(ev_[s.b], streams[s.b]));  // b's pending work first
+      enforce(hydra_stream_wait_event(streams[s.a], ev_[s.b]));
+      const void* src = buf[s.b];
+      if (s.staged) {
+        enforce(hydra_memcpy_async(stage_[s.a].p, buf[s.b], bytes, streams[s.a]));
+        src = stage_[s.a].p;
+      }
+      enforce(hydra_reduce(HYDRA_SUM, dt, buf[s.a], buf[s.a], src, count, streams[s.a]));
+    }
+  }
+  const std::vector<LocalStep>& steps() const { return steps_; }
+
+ private:
+  std::vector<LocalStep> steps_;
+  std::vector<hydra_event_t> ev_;
+  std::vector<DeviceMem> stage_;
+};
+
+// Per-pointer devices (CudaDevicePointer::create, cuda.cu:175-188); every pointer must be
+// device memory.
+template <typename T>
+std::vector<int> pointer_devices(const std::vector<T*>& ptrs, const char* who) {
+  std::vector<int> dev(ptrs.size(), -1);
+  for (size_t i = 0; i < ptrs.size(); i++) {
+    enforce(hydra_pointer_device(ptrs[i], &dev[i]));
+    if (dev[i] < 0) throw EnforceNotMet(std::string(who) + ": ptrs must be device memory");
+  }
+  return dev;
+}
+
+// hydra_device_peer_access as the steps' predicate (enables access where it can).
+inline bool peer_access(int a, int b) {
+  int can = 0;
+  enforce(hydra_device_peer_access(a, b, &can));
+  return can != 0;
+}
+
 // Completion of run()'s last output copies, recorded on each caller stream as an event this
 // object owns.  The destructor waits on these events before the pinned / device scratch the
 // copies read is freed -- never on the caller's streams, which it does not own and which the
@@ -86,12 +205,16 @@ class OutputFence {
     wait_nothrow();
     for (auto e : ev_) hydra_event_destroy(e);
   }
-  // streams: on `device` (events must be created on their stream's device, whatever device is
-  // current on the calling thread)
+  // every stream on `device`
   void record(int device, const std::vector<hydra_stream_t>& streams) {
+    record(std::vector<int>(streams.size(), device), streams);
+  }
+  // streams[i] on devices[i] (events must be created on their stream's device, whatever device
+  // is current on the calling thread)
+  void record(const std::vector<int>& devices, const std::vector<hydra_stream_t>& streams) {
     while (ev_.size() < streams.size()) {
       hydra_event_t e = nullptr;
-      enforce(hydra_event_create_on(device, &e));
+      enforce(hydra_event_create_on(devices[ev_.size()], &e));
       ev_.push_back(e);
     }
     for (size_t i = 0; i < streams.size(); i++) enforce(hydra_event_record(ev_[i], streams[i]));
@@ -124,28 +247,28 @@ class HipAllreduceRing {
     if (!streams.empty() && streams.size() != ptrs_.size())
       throw EnforceNotMet("HipAllreduceRing: streams.size() != ptrs.size()");  // :30-33
     if (count_ == 0) return;  // nothing to move (pointers may be null)
-    enforce(hydra_pointer_device(ptrs_[0], &device_));
-    if (device_ < 0) throw EnforceNotMet("HipAllreduceRing: ptrs must be device memory");
-    for (T* p : ptrs_) {
-      int d = -1;
-      enforce(hydra_pointer_device(p, &d));
-      if (d != device_)
-        throw EnforceNotMet("HipAllreduceRing: all pointers must be on one device");
-    }
+    dev_ = detail::pointer_devices(ptrs_, "HipAllreduceRing");
     if (streams.empty()) {
       owned_.resize(ptrs_.size());
-      for (auto& s : owned_) enforce(hydra_stream_create(device_, &s));
+      for (size_t i = 0; i < owned_.size(); i++) enforce(hydra_stream_create(dev_[i], &owned_[i]));
       streams_ = owned_;
     } else {
       streams_ = streams;
     }
+    // the pointer the ring accumulates into: closest to the transport (no PCI device: the first)
+    root_ = kDeviceWorkspace ? detail::closest_index(std::vector<int>(ptrs_.size(), 0)) : 0;
+    device_ = dev_[root_];
     boxes_[0] = detail::Pinned(bytes_ ? bytes_ : 1);
     boxes_[1] = detail::Pinned(bytes_ ? bytes_ : 1);
     if (kDeviceWorkspace) {
       inbox_dev_ = detail::DeviceMem(device_, bytes_);
+      if (ptrs_.size() > 1) local_.init(detail::local_tree(dev_, detail::peer_access), dev_, bytes_);
     } else {
       scratch_host_ = detail::Pinned(bytes_ ? bytes_ : 1);
-      if (ptrs_.size() > 1) local_dev_ = detail::DeviceMem(device_, bytes_);
+      if (ptrs_.size() > 1) {
+        local_dev_ = detail::DeviceMem(device_, bytes_);
+        local_.init(detail::local_chain(dev_, detail::peer_access), dev_, bytes_);
+      }
     }
   }
 
@@ -162,20 +285,25 @@ class HipAllreduceRing {
     using detail::enforce;
     if (count_ == 0) return;
     const int dt = gloo_compat::dtype_of<T>();
-    hydra_stream_t s0 = streams_[0];
-    for (size_t i = 1; i < streams_.size(); i++) enforce(hydra_stream_synchronize(streams_[i]));
+    hydra_stream_t s0 = streams_[root_];
     // ---- local reduce: scratch holds this rank's value x_r
     void* scratch;
+    std::vector<void*> buf(ptrs_.begin(), ptrs_.end());
     if (kDeviceWorkspace) {
-      for (size_t sz = 1; sz < ptrs_.size(); sz *= 2)  // CudaLocalNativeReduce tree
-        for (size_t j = 0; j + sz < ptrs_.size(); j += 2 * sz)
-          enforce(hydra_reduce(HYDRA_SUM, dt, ptrs_[j], ptrs_[j], ptrs_[j + sz], count_, s0));
-      scratch = ptrs_[0];
+      // CudaLocalNativeReduce tree into ptrs[0] (each step on its destination's device), then
+      // into the ring's pointer when that is another one (cudaDeviceReduce's target copy)
+      local_.run(buf, streams_, dt, count_, bytes_);
+      if (root_ != 0) {
+        enforce(hydra_stream_synchronize(streams_[0]));
+        enforce(hydra_memcpy_async(ptrs_[root_], ptrs_[0], bytes_, s0));
+      }
+      scratch = ptrs_[root_];
     } else {
       if (ptrs_.size() > 1) {  // ptrs[0] op= ptrs[i] in order, in place on a copy of ptrs[0]
+        for (size_t i = 1; i < streams_.size(); i++) enforce(hydra_stream_synchronize(streams_[i]));
         enforce(hydra_memcpy_async(local_dev_.p, ptrs_[0], bytes_, s0));
-        for (size_t i = 1; i < ptrs_.size(); i++)
-          enforce(hydra_reduce(HYDRA_SUM, dt, local_dev_.p, local_dev_.p, ptrs_[i], count_, s0));
+        buf[0] = local_dev_.p;
+        local_.run(buf, streams_, dt, count_, bytes_);
         enforce(hydra_memcpy_async(scratch_host_.p, local_dev_.p, bytes_, s0));
       } else {
         enforce(hydra_memcpy_async(scratch_host_.p, ptrs_[0], bytes_, s0));
@@ -212,17 +340,13 @@ class HipAllreduceRing {
       }
       lease_.reset();
     }
-    // ---- broadcast the result to every device pointer (:114-120)
-    if (kDeviceWorkspace) {
-      enforce(hydra_stream_synchronize(s0));
-      for (size_t i = 1; i < ptrs_.size(); i++)
+    // ---- broadcast the result to every device pointer (:114-120), each on its own stream
+    // (a copy to another device is a peer copy; hipMemcpyDefault routes it)
+    enforce(hydra_stream_synchronize(s0));
+    for (size_t i = 0; i < ptrs_.size(); i++)
+      if (!kDeviceWorkspace || i != root_)
         enforce(hydra_memcpy_async(ptrs_[i], scratch, bytes_, streams_[i]));
-    } else {
-      enforce(hydra_stream_synchronize(s0));
-      for (size_t i = 0; i < ptrs_.size(); i++)
-        enforce(hydra_memcpy_async(ptrs_[i], scratch, bytes_, streams_[i]));
-    }
-    fence_.record(device_, streams_);
+    fence_.record(dev_, streams_);
     if (synchronize_outputs_)
       for (auto s : streams_) enforce(hydra_stream_synchronize(s));
   }
@@ -234,10 +358,13 @@ class HipAllreduceRing {
   int count_;
   size_t bytes_;
   bool synchronize_outputs_;
-  int device_ = -1;
+  int device_ = -1;     // the ring's device (dev_[root_])
+  size_t root_ = 0;     // the pointer the ring accumulates into (device workspace)
+  std::vector<int> dev_;  // per pointer
   std::vector<hydra_stream_t> streams_, owned_;
   detail::Pinned boxes_[2], scratch_host_;
   detail::DeviceMem inbox_dev_, local_dev_;
+  detail::LocalReduce local_;
   std::unique_ptr<gloo_compat::ContextPool::Lease> lease_;
   detail::OutputFence fence_;  // declared last: destroyed first, before any scratch
 };
@@ -274,21 +401,16 @@ class HipAllreduceRingChunked {
     const size_t chunks = 2 * (size_t)ctx_->size;  // cuda_allreduce_ring_chunked.cc:57-60
     chunk_ = std::max<size_t>(256, ((size_t)count_ + chunks - 1) / chunks);
     if (count_ == 0) return;
-    enforce(hydra_pointer_device(ptrs_[0], &device_));
-    if (device_ < 0) throw EnforceNotMet("HipAllreduceRingChunked: ptrs must be device memory");
-    for (T* p : ptrs_) {
-      int d = -1;
-      enforce(hydra_pointer_device(p, &d));
-      if (d != device_)
-        throw EnforceNotMet("HipAllreduceRingChunked: all pointers must be on one device");
-    }
+    dev_ = detail::pointer_devices(ptrs_, "HipAllreduceRingChunked");
+    device_ = dev_[0];  // the tree's root: the ring runs on ptrs[0]'s device
     if (streams.empty()) {
       owned_.resize(ptrs_.size());
-      for (auto& s : owned_) enforce(hydra_stream_create(device_, &s));
+      for (size_t i = 0; i < owned_.size(); i++) enforce(hydra_stream_create(dev_[i], &owned_[i]));
       streams_ = owned_;
     } else {
       streams_ = streams;
     }
+    if (ptrs_.size() > 1) local_.init(detail::local_tree(dev_, detail::peer_access), dev_, bytes_);
     scratch_host_ = detail::Pinned(bytes_);
     inbox_[0] = detail::Pinned(chunk_ * sizeof(T));
     inbox_[1] = detail::Pinned(chunk_ * sizeof(T));
@@ -309,10 +431,8 @@ class HipAllreduceRingChunked {
     if (count_ == 0) return;
     const int dt = gloo_compat::dtype_of<T>();
     hydra_stream_t s0 = streams_[0];
-    for (size_t i = 1; i < streams_.size(); i++) enforce(hydra_stream_synchronize(streams_[i]));
-    for (size_t sz = 1; sz < ptrs_.size(); sz *= 2)  // CudaLocalNativeReduce tree, in place
-      for (size_t j = 0; j + sz < ptrs_.size(); j += 2 * sz)
-        enforce(hydra_reduce(HYDRA_SUM, dt, ptrs_[j], ptrs_[j], ptrs_[j + sz], count_, s0));
+    // CudaLocalNativeReduce tree, in place, each step on its destination's device and stream
+    local_.run(std::vector<void*>(ptrs_.begin(), ptrs_.end()), streams_, dt, count_, bytes_);
     char* const dscratch = reinterpret_cast<char*>(ptrs_[0]);
     char* const hscratch = static_cast<char*>(scratch_host_.p);
     enforce(hydra_memcpy_async(hscratch, dscratch, bytes_, s0));
@@ -344,7 +464,7 @@ class HipAllreduceRingChunked {
                            kSlot, fold, copy);
       lease_.reset();
     }
-    // broadcast (cudaDeviceBroadcast): every pointer gets the result
+    // broadcast (cudaDeviceBroadcast): every pointer gets the result on its own stream
     if (kDeviceWorkspace) {
       enforce(hydra_stream_synchronize(s0));
       for (size_t i = 1; i < ptrs_.size(); i++)
@@ -353,7 +473,7 @@ class HipAllreduceRingChunked {
       for (size_t i = 0; i < ptrs_.size(); i++)
         enforce(hydra_memcpy_async(ptrs_[i], hscratch, bytes_, streams_[i]));
     }
-    fence_.record(device_, streams_);
+    fence_.record(dev_, streams_);
     if (synchronize_outputs_)
       for (auto s : streams_) enforce(hydra_stream_synchronize(s));
   }
@@ -366,9 +486,11 @@ class HipAllreduceRingChunked {
   size_t bytes_, chunk_ = 0;
   bool synchronize_outputs_;
   int device_ = -1;
+  std::vector<int> dev_;  // per pointer
   std::vector<hydra_stream_t> streams_, owned_;
   detail::Pinned scratch_host_, inbox_[2];
   detail::DeviceMem inbox_dev_;
+  detail::LocalReduce local_;
   std::unique_ptr<gloo_compat::ContextPool::Lease> lease_;
   detail::OutputFence fence_;  // declared last: destroyed first, before any scratch
 };

@@ -213,6 +213,15 @@ int hydra_event_create_on(int device, hydra_event_t* out);  /* on `device` (-1: 
 int hydra_event_record(hydra_event_t e, hydra_stream_t s);
 int hydra_event_synchronize(hydra_event_t e);
 int hydra_event_destroy(hydra_event_t e);
+/* Cross-stream ordering (cudaStreamWaitEvent, as CudaLocalNativeReduce orders its tree,
+ * cuda_collectives_native.h:100-115): work enqueued on `s` after this call waits for `e`'s last
+ * record.  The event and the stream may belong to different devices. */
+int hydra_stream_wait_event(hydra_stream_t s, hydra_event_t e);
+/* Peer access for the local reduce tree of several GPUs in one process
+ * (cuda_collectives_native.h:63-84): *can = hipDeviceCanAccessPeer(device, peer); when it can,
+ * `device`'s access to `peer`'s memory is enabled (idempotent; device == peer: *can = 1).  The
+ * caller's current device is left as it was. */
+int hydra_device_peer_access(int device, int peer, int* can);
 int hydra_malloc(int device, size_t bytes, void** out);
 int hydra_free(void* p);
 int hydra_memcpy(void* dst, const void* src, size_t bytes); /* hipMemcpyDefault, synchronous */
