@@ -42,6 +42,7 @@ EXPORTS = [  # every symbol include/hydra_hip.h declares
     "hydra_peer_detach", "hydra_peer_destroy", "hydra_comm_wait",
     "hydra_reduce_root", "hydra_reduce_root_plan", "hydra_reduce_root_simulate",
     "hydra_comm_profile", "hydra_comm_phases", "hydra_stream_wait_event", "hydra_device_peer_access",
+    "hydra_host_trace", "hydra_host_trace_read",
 ]
 
 (ALGO_AUTO, ALGO_RING, ALGO_DIRECT, ALGO_RCCL, ALGO_A2A, ALGO_RING_OLD, ALGO_RING_CHUNKED,
@@ -213,6 +214,8 @@ def _declare(L) -> None:
     L.hydra_peer_destroy.argtypes = [vp]
     L.hydra_comm_wait.argtypes = [vp, vp, ctypes.c_int64]
     L.hydra_stream_wait_event.argtypes = [vp, vp]
+    L.hydra_host_trace.argtypes = [i]
+    L.hydra_host_trace_read.argtypes = [vp, sz, ctypes.POINTER(sz)]
     L.hydra_device_peer_access.argtypes = [i, i, ctypes.POINTER(i)]
     L.hydra_comm_profile.argtypes = [vp, i]
     L.hydra_comm_phases.argtypes = [vp, ctypes.POINTER(CommPhases)]

@@ -97,6 +97,17 @@ struct hydra_ctx {
 };
 
 namespace {
+// hydra_host_trace: per-call records of hydra_reduce_host (measurement only)
+std::atomic<bool> g_trace_on{false};
+std::mutex g_trace_mu;
+std::vector<hydra_host_call_t>* g_trace = new std::vector<hydra_host_call_t>;  // never freed
+constexpr size_t kTraceCap = size_t(1) << 20;
+
+using Clock = std::chrono::steady_clock;
+double us_since(Clock::time_point t0) {
+  return std::chrono::duration<double, std::micro>(Clock::now() - t0).count();
+}
+
 constexpr size_t kSlotBytes = 4u << 20;  // per operand and staging buffer (3 slots: a, b, c)
 constexpr int kVariantForceStaging = 1000;  // hydra_set_variant value: host path always stages
 constexpr int kVariantSplit = 1100;         // hydra_set_variant 1101..1164: staging split (A/B)
@@ -339,6 +350,11 @@ int hydra_reduce_host(hydra_ctx_t ctx, int op, int dtype, void* c, const void* a
   const size_t es = hydra::dtype_size(dtype);
   const int variant = g_variant.load(std::memory_order_relaxed);
   const size_t nbytes = n * es;
+  const bool tracing = g_trace_on.load(std::memory_order_relaxed);
+  const Clock::time_point t_call = tracing ? Clock::now() : Clock::time_point();
+  hydra_host_call_t rec{};
+  rec.n = n;
+  rec.elem_bytes = es;
   // Each operand's mapped windows (host_map.h): the parts the kernel reads / writes in place
   // over PCIe -- a registered bucket (hydra_host_register), a pinned block (hydra_malloc_host,
   // e.g. the ring's receive slots after setScratchAllocator(pinnedAlloc)) or the caller's own
@@ -389,7 +405,22 @@ int hydra_reduce_host(hydra_ctx_t ctx, int op, int dtype, void* c, const void* a
   size_t used[3] = {0, 0, 0};  // bytes of the current buffer's a, b, c slots
   int buf = 0;
   bool pending = false;  // the other buffer's round is in flight
+  auto timed = [&](double* acc, const std::function<void()>& f) {  // (tracing only)
+    if (!tracing) return f();
+    const Clock::time_point t0 = Clock::now();
+    f();
+    *acc += us_since(t0);
+  };
   auto wait_round = [&](int k) -> int {
+    const Clock::time_point t0 = tracing ? Clock::now() : Clock::time_point();
+    struct Acc {
+      bool on;
+      Clock::time_point t0;
+      double* acc;
+      ~Acc() {
+        if (on) *acc += us_since(t0);
+      }
+    } acc_{tracing, t0, &rec.wait_us};
     if (lease) {
       if (int r = hydra::resident_wait(lease, &poisoned)) {
         if (poisoned) guard_.k = 0;  // the grid may still touch them: they stay mapped
@@ -409,7 +440,8 @@ int hydra_reduce_host(hydra_ctx_t ctx, int op, int dtype, void* c, const void* a
   auto flush = [&]() -> int {  // submit the current buffer's round
     if (segs.empty() && outs[buf].empty()) return HYDRA_OK;
     const int other = buf ^ 1;
-    hydra::copy_all(ins.data(), ins.size());  // the staged operands (fanned out when large)
+    // the staged operands (fanned out when large)
+    timed(&rec.copy_in_us, [&] { hydra::copy_all(ins.data(), ins.size()); });
     ins.clear();
     if (pending) {
       if (int r = wait_round(other)) return r;
@@ -426,6 +458,7 @@ int hydra_reduce_host(hydra_ctx_t ctx, int op, int dtype, void* c, const void* a
         HIP_TRY(hipEventRecord(ctx->done[buf], ctx->stream));
       }
       pending = true;
+      rec.rounds++;
       if (!drain_.f) {
         drain_.f = lease ? std::function<void()>([lease, &guard_] {
                              bool p = false;
@@ -438,7 +471,7 @@ int hydra_reduce_host(hydra_ctx_t ctx, int op, int dtype, void* c, const void* a
       }
     }
     // the previous round is done: its staged results back to c (overlapping this round)
-    hydra::copy_all(outs[other].data(), outs[other].size());
+    timed(&rec.copy_out_us, [&] { hydra::copy_all(outs[other].data(), outs[other].size()); });
     outs[other].clear();
     segs.clear();
     used[0] = used[1] = used[2] = 0;
@@ -464,6 +497,7 @@ int hydra_reduce_host(hydra_ctx_t ctx, int op, int dtype, void* c, const void* a
       char* db = B->dev(off, end, es);
       if (dc && da && db) {  // in place over PCIe
         segs.push_back({dc, da, db, end - off});
+        for (int k = 0; k < 3; k++) rec.zero_copy_bytes[k] += (end - off) * es;
         off = end;
         continue;
       }
@@ -476,6 +510,10 @@ int hydra_reduce_host(hydra_ctx_t ctx, int op, int dtype, void* c, const void* a
       const size_t cnt = std::min(end - off, room / es);
       const size_t bytes = cnt * es;
       const size_t ob = off * es;
+      if (tracing) {  // which operands of this interval the kernel touches in place
+        const bool m[3] = {dc != nullptr, da != nullptr, db != nullptr};
+        for (int k = 0; k < 3; k++) (m[k] ? rec.zero_copy_bytes[k] : rec.staged_bytes[k]) += bytes;
+      }
       char* host_st = ctx->stage[buf];
       char* dev_st = ctx->stage_dev[buf];
       auto slot = [&](int k, const char* src, bool fill) -> char* {  // k: 0 a, 1 b, 2 c
@@ -514,10 +552,33 @@ int hydra_reduce_host(hydra_ctx_t ctx, int op, int dtype, void* c, const void* a
   if (pending) {  // the last round: done, results back
     if ((rc = wait_round(buf ^ 1))) return rc;
     pending = false;
-    hydra::copy_all(outs[buf ^ 1].data(), outs[buf ^ 1].size());
+    timed(&rec.copy_out_us,
+          [&] { hydra::copy_all(outs[buf ^ 1].data(), outs[buf ^ 1].size()); });
   }
   drain_.f = nullptr;
+  if (tracing) {
+    rec.intervals = (uint32_t)(cut.size() - 1);
+    rec.resident = lease ? 1u : 0u;
+    rec.total_us = us_since(t_call);
+    std::lock_guard<std::mutex> g(g_trace_mu);
+    if (g_trace->size() < kTraceCap) g_trace->push_back(rec);
+  }
   return ok();  // the windows are released here, after every round finished
+}
+
+int hydra_host_trace(int enable) {
+  std::lock_guard<std::mutex> g(g_trace_mu);
+  if (enable) g_trace->clear();
+  g_trace_on.store(enable != 0);
+  return ok();
+}
+
+int hydra_host_trace_read(hydra_host_call_t* out, size_t cap, size_t* count) {
+  std::lock_guard<std::mutex> g(g_trace_mu);
+  if (count) *count = g_trace->size();
+  if (out)
+    std::memcpy(out, g_trace->data(), std::min(cap, g_trace->size()) * sizeof(hydra_host_call_t));
+  return ok();
 }
 
 int hydra_ctx_stats(hydra_ctx_t ctx, uint64_t* resident_calls, uint64_t* resident_launches) {

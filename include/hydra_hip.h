@@ -155,6 +155,21 @@ int hydra_chunk_sum_host(hydra_ctx_t ctx, int dtype, void* c, const void* a, con
  * HYDRA_RESIDENT=0 turns it off (every round is one launch on the context's stream).  Stats
  * (tests): rounds this context had served by it, and instances launched on its device. */
 int hydra_ctx_stats(hydra_ctx_t ctx, uint64_t* resident_calls, uint64_t* resident_launches);
+/* Per-call trace of hydra_reduce_host (measurement: where a call's time goes).  While enabled,
+ * every call appends one record (at most 1 Mi records are kept): its size, how many intervals
+ * and rounds it was cut into, the bytes of each operand the kernel touched in place (zero-copy)
+ * and the bytes staged through the context's pinned buffers, whether the rounds went to the
+ * resident reducer, and the call's wall time split into CPU copies in, waits for the GPU and
+ * CPU copies out.  hydra_host_trace(1) clears and starts, (0) stops. */
+typedef struct {
+  uint64_t n, elem_bytes;
+  uint32_t intervals, rounds, resident, reserved;
+  uint64_t zero_copy_bytes[3]; /* c, a, b */
+  uint64_t staged_bytes[3];    /* c, a, b (c: staged results copied back) */
+  double total_us, copy_in_us, wait_us, copy_out_us;
+} hydra_host_call_t;
+int hydra_host_trace(int enable);
+int hydra_host_trace_read(hydra_host_call_t* out, size_t cap, size_t* count);
 /* Which host memory the kernel reads / writes in place (zero-copy over PCIe), per operand: a
  * range registered with hydra_host_register, a pinned block from hydra_malloc_host, or memory
  * the caller pinned / registered itself (hipHostMalloc, hipHostRegister, torch pinned tensors;

@@ -23,16 +23,21 @@ for n in sizes:
     for reg in ("0", "1"):  # the hydra Func alone; and with the bucket registered once
         r = subprocess.run([EXE, "new_ring", "2", str(n), "f32", str(iters)],
                            capture_output=True, text=True, timeout=600,
-                           env=dict(os.environ, HYDRA_DROPIN_REGISTER=reg))
+                           env=dict(os.environ, HYDRA_DROPIN_REGISTER=reg,
+                                    HYDRA_DROPIN_TRACE=os.environ.get("TRACE", "0")))
         if r.returncode:
             row["error"] = (r.stdout + r.stderr)[-500:]
             break
         j = json.loads(r.stdout.strip().splitlines()[-1])
         if reg == "0":
             row.update({k: j[k] for k in ("mismatched_bytes", "iters", "ref_ms", "hydra_ms")})
+            if j.get("hydra_trace"):
+                row["hydra_trace"] = j["hydra_trace"]
         else:
             row["mismatched_bytes_registered"] = j["mismatched_bytes"]
             row["hydra_registered_ms"] = j["hydra_ms"]
+            if j.get("hydra_trace"):
+                row["hydra_registered_trace"] = j["hydra_trace"]
     rows.append(row)
     if "error" in row:
         break

@@ -257,7 +257,41 @@ int run_all(const std::string& mode, int P, size_t n, int iters, size_t ms, cons
   const char* ro = std::getenv("HYDRA_DROPIN_REF_ONLY");
   const bool ref_only = ro && ro[0] == '1';
   RunOut ref = run_case<T>(mode, P, n, false, iters, ms);
+  // HYDRA_DROPIN_TRACE=1: every hydra Func call of the hydra run recorded (hydra_host_trace):
+  // which operands went zero-copy or staged, rounds, resident or launched, and the time split
+  const char* tr = std::getenv("HYDRA_DROPIN_TRACE");
+  const bool trace = !ref_only && tr && tr[0] == '1';
+  if (trace) hydra_host_trace(1);
   RunOut hyd = run_case<T>(mode, P, n, !ref_only, iters, ms);
+  std::string trace_json = "null";
+  if (trace) {
+    hydra_host_trace(0);
+    size_t cnt = 0;
+    hydra_host_trace_read(nullptr, 0, &cnt);
+    std::vector<hydra_host_call_t> v(cnt);
+    hydra_host_trace_read(v.data(), cnt, &cnt);
+    double tot = 0, cin = 0, wt = 0, cout = 0, iv = 0, rd = 0, res = 0, elems = 0;
+    double zc[3] = {0, 0, 0}, st[3] = {0, 0, 0};
+    std::vector<double> totals;
+    for (const auto& c : v) {
+      tot += c.total_us, cin += c.copy_in_us, wt += c.wait_us, cout += c.copy_out_us;
+      iv += c.intervals, rd += c.rounds, res += c.resident, elems += (double)c.n;
+      for (int k = 0; k < 3; k++) zc[k] += (double)c.zero_copy_bytes[k], st[k] += (double)c.staged_bytes[k];
+      totals.push_back(c.total_us);
+    }
+    const double k = cnt ? (double)cnt : 1.0;
+    char b[1024];
+    std::snprintf(b, sizeof b,
+                  "{\"calls\": %zu, \"elements_avg\": %.1f, \"intervals_avg\": %.3f, "
+                  "\"rounds_avg\": %.3f, \"resident_frac\": %.3f, \"total_us_avg\": %.2f, "
+                  "\"total_us_p50\": %.2f, \"copy_in_us_avg\": %.2f, \"wait_us_avg\": %.2f, "
+                  "\"copy_out_us_avg\": %.2f, \"zero_copy_MB\": [%.3f, %.3f, %.3f], "
+                  "\"staged_MB\": [%.3f, %.3f, %.3f]}",
+                  cnt, elems / k, iv / k, rd / k, res / k, tot / k, pct(totals, 50), cin / k,
+                  wt / k, cout / k, zc[0] / k / 1e6, zc[1] / k / 1e6, zc[2] / k / 1e6,
+                  st[0] / k / 1e6, st[1] / k / 1e6, st[2] / k / 1e6);
+    trace_json = b;
+  }
   size_t mism = 0, first = (size_t)-1;
   int first_rank = -1;
   for (int r = 0; r < P; r++)
@@ -280,12 +314,13 @@ int run_all(const std::string& mode, int P, size_t n, int iters, size_t ms, cons
       "\"mismatched_bytes\": %zu, \"first_mismatch\": [%d, %lld], \"ref_ranks_equal\": %s, "
       "\"fnv_ref\": \"%016llx\", \"fnv_hydra\": \"%016llx\", \"iters\": %d, "
       "\"ref_ms\": {\"p50\": %.4f, \"p99\": %.4f, \"avg\": %.4f, \"GiBps_avg\": %.4f}, "
-      "\"hydra_ms\": {\"p50\": %.4f, \"p99\": %.4f, \"avg\": %.4f, \"GiBps_avg\": %.4f}}\n",
+      "\"hydra_ms\": {\"p50\": %.4f, \"p99\": %.4f, \"avg\": %.4f, \"GiBps_avg\": %.4f}, "
+      "\"hydra_trace\": %s}\n",
       mode.c_str(), P, n, dt, ms, mism, first_rank, mism ? (long long)first : -1LL,
       ranks_equal ? "true" : "false", (unsigned long long)fnv1a(ref.bytes),
       (unsigned long long)fnv1a(hyd.bytes), iters, pct(ref.iter_ms, 50), pct(ref.iter_ms, 99),
       avg(ref.iter_ms), gib(avg(ref.iter_ms)), pct(hyd.iter_ms, 50), pct(hyd.iter_ms, 99),
-      avg(hyd.iter_ms), gib(avg(hyd.iter_ms)));
+      avg(hyd.iter_ms), gib(avg(hyd.iter_ms)), trace_json.c_str());
   return 0;
 }
 

@@ -164,11 +164,12 @@ def _worker(rank, world, port, q):
             comm.profile(False)
             ok = (ph["calls"] == 1 and ph["link_ms"] > 0 and ph["fold_ms"] > 0
                   and ph["span_ms"] >= 0.999 * max(ph["link_ms"], ph["fold_ms"])
-                  and ph["sent_bytes"] == ph["recv_bytes"] and ph["fold_hbm_bytes"] > 0
+                  and ph["fold_hbm_bytes"] > 0
                   and ph["peers"] == (1 if algo == "ring" else world - 1)
-                  and torch.cuda.current_device() == dev_before)
-            if world != 3:  # equal blocks: exactly the reference ring's link bytes
-                ok = ok and ph["sent_bytes"] == 2 * (world - 1) * n * 4 // world
+                  and torch.cuda.current_device() == dev_before
+                  # the reference ring's 2(P-1)/P*n*E per rank (clipped segments: a few bytes)
+                  and abs(ph["sent_bytes"] - 2 * (world - 1) * n * 4 / world) <= 64
+                  and abs(ph["recv_bytes"] - 2 * (world - 1) * n * 4 / world) <= 64)
             if algo != "ring" and world != 3:  # one P-way fold per block
                 ok = ok and ph["fold_hbm_bytes"] == (world + 1) * n * 4 // world
             if algo == "ring" and world != 3:  # P-1 fused 2R1W hops: SURVEY 8(d)'s (P-1)/P*n*12
@@ -212,7 +213,10 @@ def _spawn(target, world, *extra, timeout=150):
 @pytest.mark.parametrize("world", [2, 3, 4, 8])
 def test_rccl_executor_across_ranks(gpu, world):
     res = _spawn(_worker, world)
-    bad = {r: v for r, v in res.items() if not (isinstance(v, dict) and all(v.values()))}
+    bad = {r: (v if not isinstance(v, dict) else
+               {k: x for k, x in v.items() if not x or k.endswith("_detail")})
+           for r, v in res.items() if not (isinstance(v, dict) and all(v.values())
+                                           and not any(k.endswith("_detail") for k in v))}
     assert not bad, bad
     assert "reduce_root" in res[world - 1]
     assert len(res[0]) >= 15, res[0]

@@ -357,6 +357,9 @@ def test_resident_device_drains_are_bounded(gpu, O):
 
     import ctypes
 
+    # (what earlier tests left in the caches is really freed first: unpinning gigabytes takes
+    # time of its own, which is not a drain)
+    _lib.check(L.hydra_cache_trim())
     th = threading.Thread(target=loop)
     th.start()
     times = {}
