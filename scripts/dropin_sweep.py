@@ -1,12 +1,21 @@
 #!/usr/bin/env python3
 """BASELINE config 1 inside the reference itself: tests/cpp/dropin_gloo runs the reference's own
 gloo::allreduce ring (2 thread-ranks, loopback TCP) with gloo::sum<float> and, on identical
-inputs, with the hydra gfx950 Func plugged into setReduceFunction, over the benchmark's whole
-doubling sweep 4 .. 67 108 864 elements (runner.cc:338-362).  Per size: bit-equality of every
-rank's output, and rank 0's per-iteration p50/avg and GiB/s (runner.cc:631-635) for both.
+inputs, with the hydra gfx950 Func plugged into setReduceFunction, over the benchmark's doubling
+sweep 4 .. 67 108 864 elements (runner.cc:338-362).  Per size: bit-equality of every rank's
+output, rank 0's per-iteration p50 / avg (runner.cc:631-635) for gloo::sum, for the hydra Func,
+and for the hydra Func with the bucket registered once (HYDRA_DROPIN_REGISTER=1).
+
+The loopback ring on a shared host is noisy from process to process, so every size runs REPS
+times (default 3) with the two hydra settings interleaved (unregistered, registered,
+unregistered, ...), each process timing gloo::sum beside it; the row reports the median over
+repetitions of each setting's p50, and every repetition.  TRACE=1 adds the per-call trace of the
+hydra Func (hydra_host_trace: zero-copy vs staged bytes per operand, rounds, resident, and the
+call's time split into CPU copies in / GPU wait / CPU copies out).
 Prints one JSON document (progress on stderr)."""
 import json
 import os
+import statistics
 import subprocess
 import sys
 
@@ -14,34 +23,48 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 EXE = os.path.join(ROOT, "tests", "cpp", "dropin_gloo")
 sizes = ([int(x) for x in os.environ["SIZES"].split(",")] if os.environ.get("SIZES")
          else [4 << k for k in range(25)])
+REPS = int(os.environ.get("REPS", "3"))
 rows = []
 for n in sizes:
     iters = max(5, min(50, (1 << 27) // n))
-    sys.stderr.write(f"[dropin_sweep] n={n} iters={iters}\n")
+    sys.stderr.write(f"[dropin_sweep] n={n} iters={iters} reps={REPS}\n")
     sys.stderr.flush()
-    row = {"n": n}
-    for reg in ("0", "1"):  # the hydra Func alone; and with the bucket registered once
-        r = subprocess.run([EXE, "new_ring", "2", str(n), "f32", str(iters)],
-                           capture_output=True, text=True, timeout=600,
-                           env=dict(os.environ, HYDRA_DROPIN_REGISTER=reg,
-                                    HYDRA_DROPIN_TRACE=os.environ.get("TRACE", "0")))
-        if r.returncode:
-            row["error"] = (r.stdout + r.stderr)[-500:]
+    row = {"n": n, "iters": iters, "reps": []}
+    for rep in range(REPS):
+        for reg in ("0", "1"):
+            r = subprocess.run([EXE, "new_ring", "2", str(n), "f32", str(iters)],
+                               capture_output=True, text=True, timeout=600,
+                               env=dict(os.environ, HYDRA_DROPIN_REGISTER=reg,
+                                        HYDRA_DROPIN_TRACE=os.environ.get("TRACE", "0")))
+            if r.returncode:
+                row["error"] = (r.stdout + r.stderr)[-500:]
+                break
+            j = json.loads(r.stdout.strip().splitlines()[-1])
+            row["reps"].append({"registered": reg == "1", "mismatched_bytes": j["mismatched_bytes"],
+                                "ref_ms": j["ref_ms"], "hydra_ms": j["hydra_ms"],
+                                "hydra_trace": j.get("hydra_trace")})
+        if "error" in row:
             break
-        j = json.loads(r.stdout.strip().splitlines()[-1])
-        if reg == "0":
-            row.update({k: j[k] for k in ("mismatched_bytes", "iters", "ref_ms", "hydra_ms")})
-            if j.get("hydra_trace"):
-                row["hydra_trace"] = j["hydra_trace"]
-        else:
-            row["mismatched_bytes_registered"] = j["mismatched_bytes"]
-            row["hydra_registered_ms"] = j["hydra_ms"]
-            if j.get("hydra_trace"):
-                row["hydra_registered_trace"] = j["hydra_trace"]
+    if "error" not in row:
+        def med(reg, key):
+            return statistics.median(x[key]["p50"] for x in row["reps"]
+                                     if x["registered"] == reg)
+        row["p50_median_ms"] = {"gloo_sum": statistics.median(x["ref_ms"]["p50"]
+                                                              for x in row["reps"]),
+                                "hydra": med(False, "hydra_ms"),
+                                "hydra_registered": med(True, "hydra_ms")}
+        row["mismatched_bytes"] = sum(x["mismatched_bytes"] for x in row["reps"])
+        for reg, name in ((False, "hydra"), (True, "hydra_registered")):
+            tr = [x["hydra_trace"] for x in row["reps"] if x["registered"] == reg
+                  and x["hydra_trace"]]
+            if tr:
+                row[f"{name}_call_us_p50_median"] = statistics.median(t["total_us_p50"]
+                                                                      for t in tr)
     rows.append(row)
     if "error" in row:
         break
 print(json.dumps({"harness": "tests/cpp/dropin_gloo new_ring P=2 f32 (reference ring, "
                              "gloo::sum<float> vs hydra Func; hydra_registered: the bucket "
-                             "hydra_host_register'ed once, HYDRA_DROPIN_REGISTER=1)",
-                  "rows": rows}))
+                             "hydra_host_register'ed once, HYDRA_DROPIN_REGISTER=1); REPS "
+                             "interleaved processes per size, medians of the per-process p50",
+                  "reps": REPS, "rows": rows}))
