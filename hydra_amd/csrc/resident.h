@@ -92,7 +92,7 @@ struct alignas(64) ResDev {  // device memory, zeroed at creation
 // `blocks` workgroups; each issues the loads of `batch` tiles (1, 2 or 4) together; a call of at
 // most `solo` tiles is served by workgroup 0 alone; a larger job wakes ceil(tiles /
 // tiles_per_block) workgroups (each workgroup's system-scope fences cost).
-struct ResidentShape {  // defaults from scripts/gpu_r03s.sh (profiles/r03_resident_shape_ab.json)
+struct ResidentShape {  // defaults from the round-3 A/B (profiles/r03_resident_shape_ab.json)
   int blocks = kResidentBlocks;
   int batch = 4;
   uint32_t solo = 4;

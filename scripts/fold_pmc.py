@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Drive the default P-way fold kernel (DIRECT/A2A owner step) at the BASELINE owner-block
-sizes, for rocprofv3 kernel-trace and PMC passes (scripts/gpu_fold_pmc.sh):
+sizes, for rocprofv3 kernel-trace and PMC passes (`scripts/gpu_session.sh TAG pyprof:fold_pmc`):
   config 4: P = 8, owner block of a 64 Mi fp32 bucket = 8 Mi fp32 -> 9 x 4 B per element;
   config 5: P = 8, owner block of a 256 Mi bf16 bucket = 32 Mi bf16, fp32 accumulation ->
             9 x 2 B per element.

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Summarise scripts/gpu_fold_pmc.sh output into profiles/<tag>_pmc_fold.json: per-launch kernel
+"""Summarise `scripts/gpu_session.sh TAG pyprof:fold_pmc` output into profiles/<tag>_pmc_fold.json: per-launch kernel
 time (trace median) and HBM bytes (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE, KiB x1024,
 MI355X_MICROARCH.md §HBM) of the P-way fold at the BASELINE owner-block sizes, against the
 algorithmic (P + 1) x E bytes per element."""
@@ -9,7 +9,7 @@ import os
 import statistics
 import sys
 
-src = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/fold_pmc"
+src = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/fold_pmc"  # gpurun_out/<TAG>
 tag = sys.argv[2] if len(sys.argv) > 2 else "r02"
 root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CASES = {  # kernel template marker -> (label, elements, algorithmic bytes per launch)
@@ -28,9 +28,9 @@ def rows(p):
 out = {"source": "rocprofv3 --kernel-trace --stats, then separate --pmc FETCH_SIZE and "
                  "--pmc WRITE_SIZE passes of scripts/fold_pmc.py (20 launches per case)",
        "cases": []}
-kt = rows("kt/run_kernel_trace.csv")
-fetch = rows("fetch/run_counter_collection.csv")
-write = rows("write/run_counter_collection.csv")
+kt = rows("fold_pmc_kt/run_kernel_trace.csv")
+fetch = rows("fold_pmc_fetch/run_counter_collection.csv")
+write = rows("fold_pmc_write/run_counter_collection.csv")
 for marker, (label, n, algo) in CASES.items():
     d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in kt
          if marker in r["Kernel_Name"]]

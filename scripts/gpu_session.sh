@@ -15,6 +15,8 @@
 #   rehearseN    the N>1 bench at world size N on this one GPU (HYDRA_BENCH_SHARED_GPU=1: real
 #                RCCL ranks over loopback sockets), 4 Mi fp32 / 16 Mi bf16 -> rehearse_nN.json
 #   py:NAME      python scripts/NAME.py $PY_ARGS (a measurement script) -> NAME.log
+#   pyprof:NAME  scripts/NAME.py under rocprofv3: a kernel trace, then separate FETCH_SIZE and
+#                WRITE_SIZE passes -> NAME_{kt,fetch,write}/ (e.g. pyprof:fold_pmc)
 #   bin:NAME     scripts/NAME $BIN_ARGS (a built probe) -> NAME.log
 # Output: gpurun_out/TAG/{status,<step>.log,...}
 set -u
@@ -84,6 +86,20 @@ for s in "$@"; do
       name=${s#py:}
       # shellcheck disable=SC2086
       step "$name" 900 python -u "scripts/$name.py" ${PY_ARGS:-}
+      rc=$?;;
+    pyprof:*)
+      name=${s#pyprof:}
+      # shellcheck disable=SC2086
+      step "${name}_kt" 300 rocprofv3 --kernel-trace --stats --output-format csv \
+          -d "$OUT/${name}_kt" -o run -- python3 "scripts/$name.py" ${PY_ARGS:-}
+      rc=$?
+      # shellcheck disable=SC2086
+      [ $rc -eq 0 ] && step "${name}_fetch" 200 timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE \
+          --output-format csv -d "$OUT/${name}_fetch" -o run -- python3 "scripts/$name.py" ${PY_ARGS:-}
+      rc=$?
+      # shellcheck disable=SC2086
+      [ $rc -eq 0 ] && step "${name}_write" 200 timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE \
+          --output-format csv -d "$OUT/${name}_write" -o run -- python3 "scripts/$name.py" ${PY_ARGS:-}
       rc=$?;;
     bin:*)
       name=${s#bin:}

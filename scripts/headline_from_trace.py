@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """The headline's HBM-resident launches, read back from a rocprofv3 --kernel-trace CSV of
-`bench.py --steps S --warmup W --no-cpu-baseline` (what scripts/gpu_check.sh profiles).
+`bench.py --steps S --warmup W --no-cpu-baseline` (what `scripts/gpu_session.sh TAG prof` profiles).
 
 bench.py's N = 1 run launches the 64 Mi fp32 chunk-sum (k_reduce<float ...>, 65 536 workgroups)
 in this order: W warmup, S headline (rotating over 4 buffer pairs), min(100, S) bracketed one by

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Summarise one gpu_check.sh session's rocprofv3 output into profiles/.
+"""Summarise one `gpu_session.sh TAG prof` session's rocprofv3 output into profiles/.
 
 Usage: python scripts/pmc_summary.py gpurun_out/<tag> <round-tag>
 Writes profiles/<round>_kernel_stats.csv (the --kernel-trace --stats summary),
@@ -21,7 +21,7 @@ root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 prof = os.path.join(root, "profiles")
 os.makedirs(prof, exist_ok=True)
 HOT = "k_reduce<float, 0"
-# the kernel sources the profiled run used: gpu_check.sh records their hash on the box (the same
+# the kernel sources the profiled run used: gpu_session.sh records their hash on the box (the same
 # hash bench.py's kernel_src_hash() computes); fall back to the working tree
 rec = os.path.join(src, "kernel_src.sha256")
 if os.path.exists(rec):
