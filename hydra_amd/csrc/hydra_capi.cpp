@@ -113,6 +113,20 @@ constexpr int kVariantForceStaging = 1000;  // hydra_set_variant value: host pat
 constexpr int kVariantSplit = 1100;         // hydra_set_variant 1101..1164: staging split (A/B)
 constexpr size_t kRoundMin = 512u << 10;    // smallest staging round per operand (probe_stage_split)
 
+// Calls of at most this many bytes per operand have their RESULT staged even where c is mapped:
+// the kernel writes the pinned staging and the CPU copies it into c, which leaves c's lines in
+// the CPU's cache for the ring's next read of them (a zero-copy write from the GPU invalidates
+// them).  HYDRA_STAGE_RESULT_MAX (bytes; default kStageResultMax).  Not for float16 (its store
+// quirk reads c's old bits).
+constexpr size_t kStageResultMax = 0;
+size_t stage_result_max() {
+  static const size_t k = [] {
+    const char* v = std::getenv("HYDRA_STAGE_RESULT_MAX");
+    return v ? (size_t)std::strtoull(v, nullptr, 10) : kStageResultMax;
+  }();
+  return k;
+}
+
 // Rounds a staged call is cut into (HYDRA_STAGE_SPLIT, default 4; 1 = one round per slot).
 size_t stage_split(int variant) {
   if (variant > kVariantSplit && variant <= kVariantSplit + 64) return variant - kVariantSplit;
@@ -392,6 +406,7 @@ int hydra_reduce_host(hydra_ctx_t ctx, int op, int dtype, void* c, const void* a
   cut.erase(std::unique(cut.begin(), cut.end()), cut.end());
 
   const bool c_old_bits = dtype == HYDRA_FLOAT16 && c != a && c != b;  // store quirk: read c
+  const bool stage_result = dtype != HYDRA_FLOAT16 && nbytes <= stage_result_max();
   // Rounds: a round is one batched call over at most kResidentSegs intervals and one staging
   // buffer's slots.  Round r is submitted once round r - 1 is done; its staged results go back
   // to c while round r runs, and the CPU fills the other buffer meanwhile.  Submitted to the
@@ -492,7 +507,7 @@ int hydra_reduce_host(hydra_ctx_t ctx, int op, int dtype, void* c, const void* a
       if (segs.size() == (size_t)hydra::kResidentSegs) {
         if ((rc = flush())) return rc;
       }
-      char* dc = oc.dev(off, end, es);
+      char* dc = stage_result ? nullptr : oc.dev(off, end, es);
       char* da = A->dev(off, end, es);
       char* db = B->dev(off, end, es);
       if (dc && da && db) {  // in place over PCIe
@@ -523,6 +538,7 @@ int hydra_reduce_host(hydra_ctx_t ctx, int op, int dtype, void* c, const void* a
         return dev_st + at;
       };
       const size_t mark_a = size_t(0) * kSlotBytes + used[0];
+      const bool a_staged = !da, b_staged = !db;
       if (!da) da = slot(0, oa.base + ob, true);
       if (!db) {
         if (B == A)
@@ -530,11 +546,11 @@ int hydra_reduce_host(hydra_ctx_t ctx, int op, int dtype, void* c, const void* a
         else
           db = slot(1, B->base + ob, true);
       }
-      if (!dc) {
-        if (c == a) {
+      if (!dc) {  // (c == a / c == b: in the staged copy of that operand, if it is staged)
+        if (c == a && a_staged) {
           dc = da;
           outs[buf].push_back({static_cast<char*>(c) + ob, host_st + mark_a, bytes});
-        } else if (c == b) {
+        } else if (c == b && b_staged) {
           dc = db;
           outs[buf].push_back({static_cast<char*>(c) + ob,
                                host_st + (size_t(dc - dev_st)), bytes});
