@@ -24,6 +24,11 @@ EXE = os.path.join(ROOT, "tests", "cpp", "dropin_gloo")
 sizes = ([int(x) for x in os.environ["SIZES"].split(",")] if os.environ.get("SIZES")
          else [4 << k for k in range(25)])
 REPS = int(os.environ.get("REPS", "3"))
+# (name, HYDRA_DROPIN_REGISTER, extra environment): the hydra Func alone, with the bucket
+# registered once, and (STAGE_RESULT_AB=1) registered with every call's result staged
+MODES = [("hydra", "0", {}), ("hydra_registered", "1", {})]
+if os.environ.get("STAGE_RESULT_AB") == "1":
+    MODES.append(("hydra_registered_staged_result", "1", {"HYDRA_STAGE_RESULT_MAX": str(1 << 30)}))
 rows = []
 for n in sizes:
     iters = max(5, min(50, (1 << 27) // n))
@@ -31,34 +36,30 @@ for n in sizes:
     sys.stderr.flush()
     row = {"n": n, "iters": iters, "reps": []}
     for rep in range(REPS):
-        for reg in ("0", "1"):
+        for mode, reg, env in MODES:
             r = subprocess.run([EXE, "new_ring", "2", str(n), "f32", str(iters)],
                                capture_output=True, text=True, timeout=600,
                                env=dict(os.environ, HYDRA_DROPIN_REGISTER=reg,
-                                        HYDRA_DROPIN_TRACE=os.environ.get("TRACE", "0")))
+                                        HYDRA_DROPIN_TRACE=os.environ.get("TRACE", "0"), **env))
             if r.returncode:
                 row["error"] = (r.stdout + r.stderr)[-500:]
                 break
             j = json.loads(r.stdout.strip().splitlines()[-1])
-            row["reps"].append({"registered": reg == "1", "mismatched_bytes": j["mismatched_bytes"],
+            row["reps"].append({"mode": mode, "mismatched_bytes": j["mismatched_bytes"],
                                 "ref_ms": j["ref_ms"], "hydra_ms": j["hydra_ms"],
                                 "hydra_trace": j.get("hydra_trace")})
         if "error" in row:
             break
     if "error" not in row:
-        def med(reg, key):
-            return statistics.median(x[key]["p50"] for x in row["reps"]
-                                     if x["registered"] == reg)
         row["p50_median_ms"] = {"gloo_sum": statistics.median(x["ref_ms"]["p50"]
-                                                              for x in row["reps"]),
-                                "hydra": med(False, "hydra_ms"),
-                                "hydra_registered": med(True, "hydra_ms")}
+                                                              for x in row["reps"])}
         row["mismatched_bytes"] = sum(x["mismatched_bytes"] for x in row["reps"])
-        for reg, name in ((False, "hydra"), (True, "hydra_registered")):
-            tr = [x["hydra_trace"] for x in row["reps"] if x["registered"] == reg
-                  and x["hydra_trace"]]
+        for mode, _, _ in MODES:
+            mine = [x for x in row["reps"] if x["mode"] == mode]
+            row["p50_median_ms"][mode] = statistics.median(x["hydra_ms"]["p50"] for x in mine)
+            tr = [x["hydra_trace"] for x in mine if x["hydra_trace"]]
             if tr:
-                row[f"{name}_call_us_p50_median"] = statistics.median(t["total_us_p50"]
+                row[f"{mode}_call_us_p50_median"] = statistics.median(t["total_us_p50"]
                                                                       for t in tr)
     rows.append(row)
     if "error" in row:
