@@ -90,6 +90,16 @@ class HostMapping(ctypes.Structure):
 MAP_REGISTER, MAP_PIN, MAP_PINNED_BLOCK = 1, 2, 3
 
 
+class HostCall(ctypes.Structure):
+    """hydra_host_call_t (include/hydra_hip.h): one traced hydra_reduce_host call."""
+    _fields_ = [("n", ctypes.c_uint64), ("elem_bytes", ctypes.c_uint64),
+                ("intervals", ctypes.c_uint32), ("rounds", ctypes.c_uint32),
+                ("resident", ctypes.c_uint32), ("reserved", ctypes.c_uint32),
+                ("zero_copy_bytes", ctypes.c_uint64 * 3), ("staged_bytes", ctypes.c_uint64 * 3),
+                ("total_us", ctypes.c_double), ("copy_in_us", ctypes.c_double),
+                ("wait_us", ctypes.c_double), ("copy_out_us", ctypes.c_double)]
+
+
 class CommPhases(ctypes.Structure):
     """hydra_comm_phases_t (include/hydra_hip.h): per-phase totals of profiled allreduces."""
     _fields_ = [("calls", ctypes.c_uint64), ("link_ops", ctypes.c_uint64),

@@ -153,3 +153,25 @@ def test_fault_lookup_names_the_mapping():
     assert "mapped by:" in r and "no block, registration or per-call pin" in r, r
     r0 = _lib.fault_lookup(8)
     assert "not mapped" in r0, r0
+
+
+def test_struct_layouts_match_the_header():
+    """The ctypes mirrors of the round-4 measurement structs match include/hydra_hip.h (sizes
+    computed by the C compiler from the header itself)."""
+    import subprocess
+    import tempfile
+
+    src = ('#include <stdio.h>\n#include "hydra_hip.h"\n#include <stddef.h>\nint main(void){'
+           'printf("%zu %zu %zu %zu\\n", sizeof(hydra_host_call_t), sizeof(hydra_comm_phases_t),'
+           ' offsetof(hydra_host_call_t, total_us), offsetof(hydra_comm_phases_t, peers));'
+           'return 0;}\n')
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, "s.c")
+        with open(c, "w") as f:
+            f.write(src)
+        subprocess.run(["gcc", "-std=c11", "-I", os.path.join(ROOT, "include"), "-o",
+                        os.path.join(d, "s"), c], check=True, capture_output=True)
+        got = [int(v) for v in subprocess.run([os.path.join(d, "s")], check=True,
+                                              capture_output=True, text=True).stdout.split()]
+    assert got == [ctypes.sizeof(_lib.HostCall), ctypes.sizeof(_lib.CommPhases),
+                   _lib.HostCall.total_us.offset, _lib.CommPhases.peers.offset], got

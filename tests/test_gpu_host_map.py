@@ -24,6 +24,8 @@ import pytest
 from hydra_amd import _lib, synth
 from hydra_amd.reduce import HostContext
 
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
 pytestmark = pytest.mark.gpu
 
 PAGE = os.sysconf("SC_PAGESIZE")
@@ -153,3 +155,60 @@ def test_window_outlives_an_unregister_by_its_owner(ctx, O, host_buf):
     regs, _ = live_registrations()
     lo, hi = bucket.ctypes.data, bucket.ctypes.data + bucket.nbytes
     assert not [r for r in regs if lo <= r["lo"] < hi], regs
+
+
+_STAGED_RESULT = r"""
+import ctypes, json, sys, numpy as np
+sys.path.insert(0, %r)
+import torch
+from hydra_amd import _lib, synth
+from hydra_amd.reduce import HostContext
+from oracle import oracle as O
+L = _lib.lib()
+c = HostContext(0)
+out = {}
+n = 300007
+buf = np.empty(n + 4096, np.float32)  # lives until exit: registered pages never go back
+x = buf[1000:1000 + n]
+_lib.check(L.hydra_host_register(x.ctypes.data, x.nbytes))
+for mode, (cc, aa) in {"in_place": ("x", "x"), "out_of_place": ("y", "x")}.items():
+    x[:] = synth.stress_f32(2, 0, n)
+    b = synth.stress_f32(2, 1, n)
+    exp = O.op(x.copy(), b, "sum", 6)
+    y = np.zeros(n, np.float32) if cc == "y" else x
+    _lib.check(L.hydra_host_trace(1))
+    _lib.check(L.hydra_reduce_host(c.handle, 0, 6, y.ctypes.data, x.ctypes.data, b.ctypes.data, n))
+    _lib.check(L.hydra_host_trace(0))
+    rec = (_lib.HostCall * 4)()
+    cnt = ctypes.c_size_t()
+    _lib.check(L.hydra_host_trace_read(rec, 4, ctypes.byref(cnt)))
+    out[mode] = {"exact": bool(np.array_equal(y.view(np.uint32), exp.view(np.uint32))),
+                 "calls": cnt.value, "zero_copy_c": rec[0].zero_copy_bytes[0],
+                 "zero_copy_a": rec[0].zero_copy_bytes[1], "staged_c": rec[0].staged_bytes[0]}
+_lib.check(L.hydra_host_unregister(x.ctypes.data))
+c.close()
+print(json.dumps(out))
+"""
+
+
+@pytest.mark.parametrize("stage_max", [0, 1 << 30])
+def test_staged_result_knob(gpu, stage_max):
+    """HYDRA_STAGE_RESULT_MAX: a registered c is written in place (0, the default) or its result
+    goes through the staging and the CPU copies it back (above: every call) -- the same bits
+    either way, in place (c == a, the ring's call) and out of place; a stays zero-copy."""
+    import json
+    import subprocess
+    import sys
+
+    p = subprocess.run([sys.executable, "-c", _STAGED_RESULT % ROOT], capture_output=True,
+                       text=True, timeout=120,
+                       env=dict(os.environ, HYDRA_STAGE_RESULT_MAX=str(stage_max)))
+    assert p.returncode == 0, p.stderr[-3000:]
+    r = json.loads(p.stdout.strip().splitlines()[-1])
+    for mode, v in r.items():
+        assert v["exact"] and v["calls"] == 1, (mode, v)
+        assert v["zero_copy_a"] > 0, (mode, v)  # the interior pages of a are read in place
+        if stage_max:
+            assert v["zero_copy_c"] == 0 and v["staged_c"] == 300007 * 4, (mode, v)
+    if not stage_max:
+        assert r["in_place"]["zero_copy_c"] > 0, r
