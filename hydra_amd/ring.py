@@ -394,6 +394,13 @@ HBM_PEAK_GBS = 8000.0
 XGMI_LINK_GBS = 153.0
 
 
+def _sig(x: float, digits: int = 4) -> float:
+    """x rounded to `digits` significant digits (slow test transports must not round to 0)."""
+    from math import floor, log10
+
+    return 0.0 if x == 0 else round(x, digits - 1 - int(floor(log10(abs(x)))))
+
+
 def phase_report(ph: dict, P: int, n: int, esize: int) -> dict:
     """The N>1 line's own roofline evidence from one profiled (untimed) allreduce: comm-stream
     (link) vs compute-stream (fold) busy time, their overlap, per-link GB/s against one xGMI
@@ -415,19 +422,19 @@ def phase_report(ph: dict, P: int, n: int, esize: int) -> dict:
         "link": {"sent_bytes": int(sent), "recv_bytes": int(ph["recv_bytes"] / calls),
                  "algorithmic_bytes": int(2 * (P - 1) / P * n * esize), "peers": peers,
                  "ops": int(ph["link_ops"] / calls),
-                 "aggregate_GBps": round(sent / (link * 1e-3) / 1e9, 2) if link > 0 else None,
-                 "per_link_GBps": (round(sent / peers / (link * 1e-3) / 1e9, 2)
+                 "aggregate_GBps": _sig(sent / (link * 1e-3) / 1e9) if link > 0 else None,
+                 "per_link_GBps": (_sig(sent / peers / (link * 1e-3) / 1e9)
                                    if link > 0 else None),
                  "link_peak_GBps": XGMI_LINK_GBS},
         "fold": {"kernel_hbm_bytes": int(kern), "fused_sum_bytes": int(fused),
                  "ops": int(ph["fold_ops"] / calls),
-                 "kernel_GBps": round(kern / (fold * 1e-3) / 1e9, 1) if fold > 0 else None,
+                 "kernel_GBps": _sig(kern / (fold * 1e-3) / 1e9) if fold > 0 else None,
                  "hbm_peak_GBps": HBM_PEAK_GBS},
     }
     if out["link"]["per_link_GBps"] is not None:
-        out["link"]["frac_of_link"] = round(out["link"]["per_link_GBps"] / XGMI_LINK_GBS, 4)
+        out["link"]["frac_of_link"] = _sig(out["link"]["per_link_GBps"] / XGMI_LINK_GBS)
     if out["fold"]["kernel_GBps"] is not None:
-        out["fold"]["frac_of_hbm"] = round(out["fold"]["kernel_GBps"] / HBM_PEAK_GBS, 4)
+        out["fold"]["frac_of_hbm"] = _sig(out["fold"]["kernel_GBps"] / HBM_PEAK_GBS)
     return out
 
 
