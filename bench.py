@@ -261,13 +261,15 @@ def gpu_numa_node(device_index=0):
         return None
 
 
-def baseline_cores(k, device_index=0):
+def baseline_cores(k, device_index=0, node=-1):
     """k host CPUs for the CPU baselines: on the GPU's NUMA node (as a rank process runs,
     DESIGN.md 6.3), never CPU 0 (the housekeeping / interrupt core) nor its SMT sibling, one
     logical CPU per physical core while there are enough; within this process's affinity.
+    node: the GPU's NUMA node if the caller knows it (-1: look it up, which initialises HIP).
     Returns (cpus, node, note)."""
     aff = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else []
-    node = gpu_numa_node(device_index)
+    if node == -1:
+        node = gpu_numa_node(device_index)
     pool = [c for c in _cpulist(_read(f"/sys/devices/system/node/node{node}/cpulist"))
             if c in aff] if node is not None else []
     note = f"GPU NUMA node {node}" if pool else "GPU NUMA node unknown: process affinity"

@@ -29,6 +29,24 @@ REPS = int(os.environ.get("REPS", "3"))
 MODES = [("hydra", "0", {}), ("hydra_registered", "1", {})]
 if os.environ.get("STAGE_RESULT_AB") == "1":
     MODES.append(("hydra_registered_staged_result", "1", {"HYDRA_STAGE_RESULT_MAX": str(1 << 30)}))
+# every process of the sweep on the same CPUs: the GPU's NUMA node, never CPU 0 (bench.py's
+# placement for the CPU baselines); PIN=0 leaves the affinity alone
+sys.path.insert(0, ROOT)
+pinned = None
+if os.environ.get("PIN", "1") != "0" and hasattr(os, "sched_setaffinity"):
+    import bench  # (no torch import at module level)
+
+    # the GPU's NUMA node from a child process: this one never initialises HIP (it only starts
+    # the harness processes)
+    q = subprocess.run([sys.executable, "-c", "import bench; print(bench.gpu_numa_node())"],
+                       capture_output=True, text=True, timeout=300, cwd=ROOT)
+    try:
+        gnode = int(q.stdout.strip().splitlines()[-1])
+    except (ValueError, IndexError):
+        gnode = None
+    cores, node, note = bench.baseline_cores(int(os.environ.get("PIN_CORES", "8")), node=gnode)
+    os.sched_setaffinity(0, set(cores))
+    pinned = {"cpus": cores, "numa_node": node, "placement": note}
 rows = []
 for n in sizes:
     iters = max(5, min(50, (1 << 27) // n))
@@ -64,7 +82,26 @@ for n in sizes:
     rows.append(row)
     if "error" in row:
         break
-print(json.dumps({"harness": "tests/cpp/dropin_gloo new_ring P=2 f32 (reference ring, "
+# gloo::sum<float> per call at the Func's call sizes (the reference's own, oracle/_ref), on one
+# of the same CPUs, in place on warm buffers as the ring calls it: the per-call crossover
+per_call = {}
+try:
+    import numpy as np
+
+    from oracle import oracle as O
+
+    if O.ref_available():
+        os.sched_setaffinity(0, {pinned["cpus"][0]} if pinned else os.sched_getaffinity(0))
+        for m in sorted({int(x["hydra_trace"]["elements_avg"]) for r in rows
+                         for x in r.get("reps", []) if x.get("hydra_trace")}):
+            a = np.arange(m, dtype=np.float32)
+            b = np.ones(m, dtype=np.float32)
+            per = O.ref_time_sum(6, a, a, b, max(20, (1 << 26) // max(m, 1)), 5)
+            per_call[m] = round(per * 1e6, 2)
+except Exception as e:  # context only
+    per_call = {"error": str(e)}
+print(json.dumps({"pinned": pinned, "gloo_sum_call_us_by_elements": per_call,
+                  "harness": "tests/cpp/dropin_gloo new_ring P=2 f32 (reference ring, "
                              "gloo::sum<float> vs hydra Func; hydra_registered: the bucket "
                              "hydra_host_register'ed once, HYDRA_DROPIN_REGISTER=1); REPS "
                              "interleaved processes per size, medians of the per-process p50",
