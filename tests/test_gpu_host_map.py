@@ -212,3 +212,22 @@ def test_staged_result_knob(gpu, stage_max):
             assert v["zero_copy_c"] == 0 and v["staged_c"] == 300007 * 4, (mode, v)
     if not stage_max:
         assert r["in_place"]["zero_copy_c"] > 0, r
+
+
+def test_register_release_reuse_then_pageable_copies(gpu):
+    """the sequence profiles/r03_fault_report.txt points at, made
+    deterministic -- pages registered with hydra_host_register and used zero-copy by a kernel,
+    unregistered, unmapped, then FRESH pages mapped at the very same virtual addresses
+    (MAP_FIXED_NOREPLACE) and copied by the HIP runtime's pageable copy path (torch H2D of 8 MiB,
+    which locks the caller's pages, and D2H back into them).  No fault, no stale data: round 4's
+    probe ran 200 cycles clean (profiles/r04c2_register_reuse_probe.log), which refutes this
+    sequence as a deterministic cause; this test keeps 40 cycles of it in the suite."""
+    import json
+    import subprocess
+    import sys
+
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "probe_register_reuse.py"),
+                        "40", "8"], capture_output=True, text=True, timeout=180)
+    assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-3000:])
+    r = json.loads(p.stdout.strip().splitlines()[-1])
+    assert r["cycles"] == 40 and r["n_mismatches"] == 0 and r["gpu_faults_seen"] == 0, r
