@@ -111,7 +111,16 @@ double us_since(Clock::time_point t0) {
 constexpr size_t kSlotBytes = 4u << 20;  // per operand and staging buffer (3 slots: a, b, c)
 constexpr int kVariantForceStaging = 1000;  // hydra_set_variant value: host path always stages
 constexpr int kVariantSplit = 1100;         // hydra_set_variant 1101..1164: staging split (A/B)
-constexpr size_t kRoundMin = 512u << 10;    // smallest staging round per operand (probe_stage_split)
+// smallest staging round per operand (probe_stage_split); HYDRA_ROUND_MIN (bytes) for A/B
+constexpr size_t kRoundMin = 512u << 10;
+size_t round_min() {
+  static const size_t k = [] {
+    const char* v = std::getenv("HYDRA_ROUND_MIN");
+    const size_t x = v ? (size_t)std::strtoull(v, nullptr, 10) : kRoundMin;
+    return std::max<size_t>(16u << 10, std::min<size_t>(x, kSlotBytes));
+  }();
+  return k;
+}
 
 // Calls of at most this many bytes per operand have their RESULT staged even where c is mapped:
 // the kernel writes the pinned staging and the CPU copies it into c, which leaves c's lines in
@@ -499,7 +508,7 @@ int hydra_reduce_host(hydra_ctx_t ctx, int op, int dtype, void* c, const void* a
   // most a slot), so its copies overlap the GPU's rounds: in at round r + 1 and out at round
   // r - 1 while round r runs.
   const size_t round_cap =
-      std::min(kSlotBytes, std::max(kRoundMin, (nbytes / stage_split(variant) + 255) / 256 * 256));
+      std::min(kSlotBytes, std::max(round_min(), (nbytes / stage_split(variant) + 255) / 256 * 256));
   for (size_t q = 0; q + 1 < cut.size(); q++) {
     size_t off = cut[q];
     const size_t end = cut[q + 1];

@@ -2,7 +2,8 @@
 // what the reference ring pays per segment when its Func is the hydra host sum
 // (allreduce.cc:301-305: synchronous, c == a, b = the scratch slot).
 // Modes: registered (hydra_host_register'ed mmap buffers), pinned (hydra_malloc_host blocks),
-// pageable (malloc'ed, odd offsets: CPU-staged).  Sizes from argv (elements), default
+// pageable (malloc'ed, odd offsets: CPU-staged), mixed (a / c registered, b pageable: the drop-in
+// inside the reference's ring with a registered bucket).  Sizes from argv (elements), default
 // 64 1024 16384 262144.  Prints one JSON document: median / p10 / p90 microseconds per call.
 // Build: hydra_amd/csrc/Makefile (-> scripts/probe_host_floor).  Run on the GPU box.
 #include <sys/mman.h>
@@ -51,7 +52,11 @@ int main(int argc, char** argv) {
     float* b;
   } modes[] = {{"registered", ra + 1024, rb + 1024},
                {"pinned", static_cast<float*>(pa) + 1024, static_cast<float*>(pb) + 1024},
-               {"pageable", ga.data() + 3, gb.data() + 5}};
+               {"pageable", ga.data() + 3, gb.data() + 5},
+               // the reference ring's own call (allreduce.cc:301-305) after the maintainer
+               // registered the bucket: c == a in the registered bucket, b in the ring's
+               // pageable scratch (new uint8_t[], :225-229)
+               {"mixed", ra + 1024, gb.data() + 5}};
   for (auto& m : modes)
     for (size_t i = 0; i < big - 2048; i++) m.a[i] = 1.0f, m.b[i] = 0.5f;
   uint64_t calls0 = 0, launches0 = 0;
