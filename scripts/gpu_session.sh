@@ -11,7 +11,7 @@
 #   smoke        __graft_entry__.smoke()
 #   prof         rocprofv3 kernel trace + separate FETCH_SIZE / WRITE_SIZE passes of the N=1
 #                bench, the headline's dispatches from the trace, the PMC summary (ROUND=rNN)
-#   bench        python bench.py (BENCH_ARGS), JSON line -> bench.json
+#   bench[_X]    python bench.py (BENCH_ARGS), JSON line -> bench[_X].json (bench_2: a second run)
 #   rehearseN    the N>1 bench at world size N on this one GPU (HYDRA_BENCH_SHARED_GPU=1: real
 #                RCCL ranks over loopback sockets), 4 Mi fp32 / 16 Mi bf16 -> rehearse_nN.json
 #   py:NAME      python scripts/NAME.py $PY_ARGS (a measurement script) -> NAME.log
@@ -71,10 +71,10 @@ for s in "$@"; do
           -d "$OUT/prof_write" -o run -- python3 "$ROOT/bench.py" --steps 20 --warmup 2 --no-cpu-baseline
       rc=$?
       python3 scripts/pmc_summary.py "$OUT" "${ROUND:-r04}" > "$OUT/pmc_summary.json" 2>&1 || true;;
-    bench)
+    bench|bench_*)
       # shellcheck disable=SC2086
-      step bench 600 python bench.py ${BENCH_ARGS:-}
-      rc=$?; tail -1 "$OUT/bench.log" > "$OUT/bench.json" 2>/dev/null;;
+      step "$s" 600 python bench.py ${BENCH_ARGS:-}
+      rc=$?; tail -1 "$OUT/$s.log" > "$OUT/$s.json" 2>/dev/null;;
     rehearse*)
       n=${s#rehearse}
       step "rehearse_n$n" 600 env HYDRA_BENCH_SHARED_GPU=1 python -m torch.distributed.run --nnodes=1 \
