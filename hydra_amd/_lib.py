@@ -46,11 +46,11 @@ EXPORTS = [  # every symbol include/hydra_hip.h declares
 ]
 
 (ALGO_AUTO, ALGO_RING, ALGO_DIRECT, ALGO_RCCL, ALGO_A2A, ALGO_RING_OLD, ALGO_RING_CHUNKED,
- ALGO_BCUBE, ALGO_HALVING_DOUBLING) = range(9)
+ ALGO_BCUBE, ALGO_HALVING_DOUBLING, ALGO_RCCL_RS_AG) = range(10)
 ALGOS = {"auto": ALGO_AUTO, "ring": ALGO_RING, "direct": ALGO_DIRECT, "rccl": ALGO_RCCL,
          "a2a": ALGO_A2A, "ring_old": ALGO_RING_OLD,
          "ring_chunked": ALGO_RING_CHUNKED, "bcube": ALGO_BCUBE,
-         "halving_doubling": ALGO_HALVING_DOUBLING}
+         "halving_doubling": ALGO_HALVING_DOUBLING, "rccl_rs_ag": ALGO_RCCL_RS_AG}
 ACC_F32 = 1
 ALLOW_CAPTURE = 2
 ERR_UNSUPPORTED = 3

@@ -77,7 +77,7 @@ int check_plan_args(int algo, int op, int dtype, int flags, size_t* esize) {
   *esize = hydra::dtype_size(dtype);
   if (!*esize) return fail(HYDRA_ERR_INVALID, "invalid dtype");
   if (op < HYDRA_SUM || op > HYDRA_MIN) return fail(HYDRA_ERR_INVALID, "invalid op");
-  if (algo < HYDRA_ALGO_AUTO || algo > HYDRA_ALGO_HALVING_DOUBLING)
+  if (algo < HYDRA_ALGO_AUTO || algo > HYDRA_ALGO_RCCL_RS_AG)
     return fail(HYDRA_ERR_INVALID, "invalid algorithm");
   if (flags & HYDRA_ACC_F32) {
     if (dtype != HYDRA_BFLOAT16)
@@ -578,8 +578,11 @@ int prepare(hydra_comm* c, int* algo, int op, int dtype, int flags, void* buf, s
   if (reinterpret_cast<uintptr_t>(buf) % es)
     return fail(HYDRA_ERR_INVALID, "buffer not aligned to the element size");
   *algo = root >= 0 ? *algo : resolve_algo(*algo, c->nranks, n, es, max_segment);
-  if (*algo == HYDRA_ALGO_RCCL) {
+  if (*algo == HYDRA_ALGO_RCCL || *algo == HYDRA_ALGO_RCCL_RS_AG) {
     if (flags & HYDRA_ACC_F32) return fail(HYDRA_ERR_UNSUPPORTED, "ACC_F32 with RCCL");
+    if (root >= 0) return fail(HYDRA_ERR_UNSUPPORTED, "RCCL algorithms for gloo::reduce");
+    if (*algo == HYDRA_ALGO_RCCL_RS_AG && n % (size_t)c->nranks)
+      return fail(HYDRA_ERR_UNSUPPORTED, "RCCL_RS_AG needs n to be a multiple of the rank count");
     return HYDRA_OK;
   }
   const size_t ms = max_segment ? max_segment : (1u << 20);
@@ -625,6 +628,21 @@ int prepare(hydra_comm* c, int* algo, int op, int dtype, int flags, void* buf, s
 // Enqueue a prepared allreduce after `start`; ends recorded in c->ev_cs / c->ev_ks.
 int enqueue(hydra_comm* c, int algo, int op, int dtype, int flags, void* buf, size_t n,
             hipEvent_t start) {
+  if (algo == HYDRA_ALGO_RCCL_RS_AG) {  // RCCL's own reduce-scatter + all-gather, in place
+    HIP_TRY(hipStreamWaitEvent(c->cs, start, 0));
+    const size_t es = hydra::dtype_size(dtype), k = n / (size_t)c->nranks;
+    char* mine = static_cast<char*>(buf) + (size_t)c->rank * k * es;
+    const uint64_t link = (uint64_t)k * es * (c->nranks - 1);
+    ProfOp rs(c, c->cs, true, link, link, 0);
+    NCCL_TRY(ncclReduceScatter(buf, mine, k, nccl_type(dtype), nccl_op(op), c->nccl, c->cs));
+    HIP_TRY(rs.end());
+    ProfOp ag(c, c->cs, true, link, link, 0);
+    NCCL_TRY(ncclAllGather(mine, buf, k, nccl_type(dtype), c->nccl, c->cs));
+    HIP_TRY(ag.end());
+    HIP_TRY(hipEventRecord(c->ev_cs, c->cs));
+    HIP_TRY(hipEventRecord(c->ev_ks, c->ks));
+    return HYDRA_OK;
+  }
   if (algo == HYDRA_ALGO_RCCL) {
     HIP_TRY(hipStreamWaitEvent(c->cs, start, 0));
     // (RCCL's own ring: 2(P-1)/P of the bucket leaves this rank; its peers are RCCL's choice)
@@ -744,7 +762,8 @@ int plan_impl(int algo, int root, int P, int rank, size_t n, size_t esize, size_
     return fail(HYDRA_ERR_INVALID, "bad element size");
   if (root >= P) return fail(HYDRA_ERR_INVALID, "root out of range");
   algo = root >= 0 ? hydra::kAlgoReduce : resolve_algo(algo, P, n, esize, max_segment);
-  if (algo == HYDRA_ALGO_RCCL) return fail(HYDRA_ERR_UNSUPPORTED, "RCCL has no plan");
+  if (algo == HYDRA_ALGO_RCCL || algo == HYDRA_ALGO_RCCL_RS_AG)
+    return fail(HYDRA_ERR_UNSUPPORTED, "RCCL has no plan");
   const size_t ms = max_segment ? max_segment : (1u << 20);
   if (root >= 0 && ms < esize) return fail(HYDRA_ERR_INVALID, "max_segment below the element size");
   const hydra::PlanGeom g = root >= 0 ? hydra::make_geom_reduce(P, n, esize, ms, chunk_bytes, root)
@@ -801,7 +820,8 @@ int simulate_impl(int algo, int root, int op, int dtype, int flags, int P, void*
   if (P < 1 || P > hydra::kMaxRanks || !bufs) return fail(HYDRA_ERR_INVALID, "bad P/bufs");
   if (root >= P) return fail(HYDRA_ERR_INVALID, "root out of range");
   algo = root >= 0 ? hydra::kAlgoReduce : resolve_algo(algo, P, n, es, max_segment);
-  if (algo == HYDRA_ALGO_RCCL) return fail(HYDRA_ERR_UNSUPPORTED, "no RCCL in the simulator");
+  if (algo == HYDRA_ALGO_RCCL || algo == HYDRA_ALGO_RCCL_RS_AG)
+    return fail(HYDRA_ERR_UNSUPPORTED, "no RCCL in the simulator");
   if (n == 0 || P == 1) return ok();
   const bool acc32 = (flags & HYDRA_ACC_F32) != 0;
   const size_t ms = max_segment ? max_segment : (1u << 20);

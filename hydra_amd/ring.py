@@ -739,7 +739,8 @@ def bench_allreduce(args, dev, make_comm=None, sync=None, cpu_baseline=None) -> 
             check_parity("reduce_root", lambda t: comm.reduce_(t, world - 1),
                          expected_reduce_f32(xs) if rank == world - 1 else None)
         k = max(5, args.steps // 4)
-        legs = ("ring", "direct", "a2a", "rccl") + peer_algos
+        # context: RCCL's own allreduce and its own reduce-scatter + all-gather
+        legs = ("ring", "direct", "a2a", "rccl", "rccl_rs_ag") + peer_algos
         if extra_legs:
             legs += ("ring_old", "ring_chunked", "bcube", "halving_doubling")
         for a in legs:

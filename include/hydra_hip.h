@@ -276,6 +276,9 @@ void hydra_ring_plan(int P, size_t n, size_t esize, size_t max_segment, size_t* 
  *                      (allreduce_halving_doubling.h:37-358): recursive halving / doubling in
  *                      binary blocks of P, bit-reversed exchange between blocks; identical
  *                      bits on every rank (max_segment, chunk_bytes unused)
+ *   HYDRA_ALGO_RCCL_RS_AG  ncclReduceScatter in place + ncclAllGather in place: RCCL's own
+ *                      ring reduce-scatter / all-gather (SURVEY 8(e)'s comparison point; RCCL's
+ *                      order, a tolerance, not bit-exact; n a multiple of P)
  *   HYDRA_ALGO_AUTO    A2A when the reference blocks are equal (n*E a multiple of P*S*segmentBytes),
  *                      else DIRECT
  * max_segment: the reference's maxSegmentSize (0 = 1 MiB, allreduce.h:78) -- it fixes block
@@ -292,7 +295,8 @@ typedef enum {
   HYDRA_ALGO_RING_OLD = 5,
   HYDRA_ALGO_RING_CHUNKED = 6,
   HYDRA_ALGO_BCUBE = 7,
-  HYDRA_ALGO_HALVING_DOUBLING = 8
+  HYDRA_ALGO_HALVING_DOUBLING = 8,
+  HYDRA_ALGO_RCCL_RS_AG = 9
 } hydra_algo_t;
 typedef struct hydra_comm* hydra_comm_t;
 

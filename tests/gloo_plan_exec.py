@@ -283,10 +283,12 @@ class GlooPlanComm:
         code = self._code(t, dtype_code)
         if (code == BF16) != bool(flags):
             raise HydraError(2, "GlooPlanComm: bf16 only with ACC_F32, ACC_F32 only for bf16")
-        if code == BF16 and algo == "rccl":
+        if code == BF16 and algo in ("rccl", "rccl_rs_ag"):
             raise HydraError(2, "ACC_F32 with RCCL")
         n = t.numel()
-        if algo == "rccl":
+        if algo == "rccl_rs_ag" and n % self.world:
+            raise HydraError(3, "RCCL_RS_AG needs n to be a multiple of the rank count")
+        if algo in ("rccl", "rccl_rs_ag"):  # (RCCL's own orders: a tolerance, not the ring's)
             dist.all_reduce(t)
             return
         if n == 0 or self.world == 1:

@@ -123,6 +123,17 @@ def _worker(rank, world, port, q):
         st = np.stack(xs).astype(np.float64)
         tol = (world - 1) * 2.0 ** -24 * np.abs(st).sum(axis=0) + 1e-30
         res["rccl_f32_tol"] = bool(np.all(np.abs(got - st.sum(axis=0)) <= tol))
+        # RCCL's own reduce-scatter + all-gather in place (SURVEY 8(e)'s comparison point): the
+        # same tolerance; n a multiple of every world size here
+        n = 786432
+        xs = [synth.stress_f32(world, r, n) for r in range(world)]
+        t = torch.from_numpy(xs[rank].copy()).to(dev)
+        comm.allreduce_(t, algo="rccl_rs_ag")
+        comm.wait(60000)
+        got = t.cpu().numpy().astype(np.float64)
+        st = np.stack(xs).astype(np.float64)
+        tol = (world - 1) * 2.0 ** -24 * np.abs(st).sum(axis=0) + 1e-30
+        res["rccl_rs_ag_f32_tol"] = bool(np.all(np.abs(got - st.sum(axis=0)) <= tol))
         # gloo::reduce to a root (only the root's bucket is defined)
         root = world - 1
         n = 1_000_003
