@@ -164,13 +164,15 @@ void host_windows_acquire(const void* ptr, size_t bytes, HostWindows* out) {
   const uintptr_t p = reinterpret_cast<uintptr_t>(ptr);
   const uintptr_t end = p + bytes;
   std::unique_lock<std::mutex> g(r.m);
-  auto add = [&](uintptr_t lo, uintptr_t hi, char* dev, int kind, uintptr_t key) {
+  auto add = [&](uintptr_t lo, uintptr_t hi, char* dev, int kind, uintptr_t key,
+                 size_t entry_bytes) {
     HostWindow& w = out->w[out->count++];
     w.lo = reinterpret_cast<const char*>(lo);
     w.hi = reinterpret_cast<const char*>(hi);
     w.dev = dev;
     w.kind = kind;
     w.key = key;
+    w.entry_bytes = entry_bytes;
   };
   // hydra's own mappings inside the operand (one being (un)registered meanwhile is not used:
   // its bytes are staged)
@@ -181,14 +183,15 @@ void host_windows_acquire(const void* ptr, size_t bytes, HostWindows* out) {
     if (x.pending || x.dying || out->count == kMaxWindows) continue;
     const uintptr_t lo = std::max(p, it->first), hi = std::min(end, x.hi);
     x.users++;
-    add(lo, hi, x.dev + (lo - it->first), x.kind, it->first);
+    add(lo, hi, x.dev + (lo - it->first), x.kind, it->first, x.hi - it->first);
   }
   if (any) return;
   // none: a mapping the caller made (no reference: the caller keeps it for the call)
   uintptr_t s = 0;
   size_t sz = 0;
   char* d = nullptr;
-  if (caller_mapping(p, &s, &sz, &d, &out->device)) add(p, std::min(end, s + sz), d, kMapCaller, 0);
+  if (caller_mapping(p, &s, &sz, &d, &out->device))
+    add(p, std::min(end, s + sz), d, kMapCaller, 0, sz);
 }
 
 void host_windows_release(HostWindows* ws) {

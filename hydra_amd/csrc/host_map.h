@@ -54,6 +54,7 @@ struct HostWindow {
   char* dev = nullptr;
   int kind = kMapNone;
   uintptr_t key = 0;  // registry entry referenced by this window (0: none)
+  size_t entry_bytes = 0;  // the whole mapping's size (registry entry / caller mapping)
   bool empty() const { return lo >= hi; }
 };
 

@@ -122,17 +122,27 @@ size_t round_min() {
   return k;
 }
 
-// Calls of at most this many bytes per operand have their RESULT staged even where c is mapped:
-// the kernel writes the pinned staging and the CPU copies it into c, which leaves c's lines in
-// the CPU's cache for the ring's next read of them (a zero-copy write from the GPU invalidates
-// them).  HYDRA_STAGE_RESULT_MAX (bytes; default kStageResultMax).  Not for float16 (its store
-// quirk reads c's old bits).
+// Staged RESULT where c is mapped: the kernel writes the pinned staging and the CPU copies it
+// into c, which leaves c's lines in the CPU's cache for the caller's next read of them (a
+// zero-copy write from the GPU invalidates them).  Measured inside the reference's ring
+// (profiles/r04d_dropin_sweep.json): it pays while the registered bucket fits the CPU's cache
+// (4 MiB: 0.669 vs 0.714 ms per allreduce) and costs once it does not (16 MiB and up: the
+// zero-copy write wins, 2.94 vs 3.11 ms).  So a result goes through the staging when c lies in a
+// hydra_host_register'ed range of at most HYDRA_STAGE_RESULT_REG_MAX bytes (default 8 MiB), or
+// when the call itself is at most HYDRA_STAGE_RESULT_MAX bytes per operand (default 0, A/B).
+// Not for float16 (its store quirk reads c's old bits).
 constexpr size_t kStageResultMax = 0;
+constexpr size_t kStageResultRegMax = size_t(8) << 20;
+size_t env_bytes(const char* name, size_t dflt) {
+  const char* v = std::getenv(name);
+  return v ? (size_t)std::strtoull(v, nullptr, 10) : dflt;
+}
 size_t stage_result_max() {
-  static const size_t k = [] {
-    const char* v = std::getenv("HYDRA_STAGE_RESULT_MAX");
-    return v ? (size_t)std::strtoull(v, nullptr, 10) : kStageResultMax;
-  }();
+  static const size_t k = env_bytes("HYDRA_STAGE_RESULT_MAX", kStageResultMax);
+  return k;
+}
+size_t stage_result_reg_max() {
+  static const size_t k = env_bytes("HYDRA_STAGE_RESULT_REG_MAX", kStageResultRegMax);
   return k;
 }
 
@@ -415,7 +425,11 @@ int hydra_reduce_host(hydra_ctx_t ctx, int op, int dtype, void* c, const void* a
   cut.erase(std::unique(cut.begin(), cut.end()), cut.end());
 
   const bool c_old_bits = dtype == HYDRA_FLOAT16 && c != a && c != b;  // store quirk: read c
-  const bool stage_result = dtype != HYDRA_FLOAT16 && nbytes <= stage_result_max();
+  bool stage_result = dtype != HYDRA_FLOAT16 && nbytes <= stage_result_max();
+  if (dtype != HYDRA_FLOAT16 && !stage_result)  // c in a small (cache-resident) registration
+    for (int k = 0; k < oc.n; k++)
+      stage_result = stage_result || (oc.win.w[k].kind == hydra::kMapRegister &&
+                                       oc.win.w[k].entry_bytes <= stage_result_reg_max());
   // Rounds: a round is one batched call over at most kResidentSegs intervals and one staging
   // buffer's slots.  Round r is submitted once round r - 1 is done; its staged results go back
   // to c while round r runs, and the CPU fills the other buffer meanwhile.  Submitted to the

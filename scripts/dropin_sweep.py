@@ -25,10 +25,14 @@ sizes = ([int(x) for x in os.environ["SIZES"].split(",")] if os.environ.get("SIZ
          else [4 << k for k in range(25)])
 REPS = int(os.environ.get("REPS", "3"))
 # (name, HYDRA_DROPIN_REGISTER, extra environment): the hydra Func alone, with the bucket
-# registered once, and (STAGE_RESULT_AB=1) registered with every call's result staged
+# registered once (the library's default path choice: results staged while the registration is
+# at most HYDRA_STAGE_RESULT_REG_MAX, 8 MiB), and (STAGE_RESULT_AB=1) the two fixed choices:
+# every result written in place over PCIe, every result staged
 MODES = [("hydra", "0", {}), ("hydra_registered", "1", {})]
 if os.environ.get("STAGE_RESULT_AB") == "1":
-    MODES.append(("hydra_registered_staged_result", "1", {"HYDRA_STAGE_RESULT_MAX": str(1 << 30)}))
+    MODES.append(("hydra_registered_zero_copy_result", "1", {"HYDRA_STAGE_RESULT_REG_MAX": "0"}))
+    MODES.append(("hydra_registered_staged_result", "1",
+                  {"HYDRA_STAGE_RESULT_REG_MAX": "0", "HYDRA_STAGE_RESULT_MAX": str(1 << 30)}))
 # every process of the sweep on the same CPUs: the GPU's NUMA node, never CPU 0 (bench.py's
 # placement for the CPU baselines); PIN=0 leaves the affinity alone
 sys.path.insert(0, ROOT)
