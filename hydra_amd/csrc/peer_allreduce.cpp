@@ -216,6 +216,7 @@ int hydra_peer_create(int nranks, int rank, int device, hydra_peer_t* out, void*
 
 int hydra_peer_connect(hydra_peer_t p, const void* sig_handles) {
   if (!p || !sig_handles) return fail(HYDRA_ERR_INVALID, "null argument");
+  hydra::DeviceScope ds_(p->device);  // IPC mappings and drains on the group's device
   const char* h = static_cast<const char*>(sig_handles);
   for (int q = 0; q < p->P; q++) {
     Blob b;
@@ -233,12 +234,14 @@ int hydra_peer_connect(hydra_peer_t p, const void* sig_handles) {
 
 int hydra_peer_register(hydra_peer_t p, void* buf, size_t bytes, void* handle) {
   if (!p || !buf || !handle) return fail(HYDRA_ERR_INVALID, "null argument");
+  hydra::DeviceScope ds_(p->device);  // IPC mappings and drains on the group's device
   const int rc = export_blob(p, buf, bytes, handle);
   return rc ? rc : ok();
 }
 
 int hydra_peer_open(hydra_peer_t p, void* buf, size_t bytes, const void* handles) {
   if (!p || !buf || !handles) return fail(HYDRA_ERR_INVALID, "null argument");
+  hydra::DeviceScope ds_(p->device);  // IPC mappings and drains on the group's device
   const char* h = static_cast<const char*>(handles);
   hydra_peer::Reg reg{};
   reg.base = static_cast<char*>(buf);
@@ -278,6 +281,7 @@ int hydra_peer_open(hydra_peer_t p, void* buf, size_t bytes, const void* handles
 
 int hydra_peer_close(hydra_peer_t p, void* buf) {
   if (!p) return fail(HYDRA_ERR_INVALID, "null peer");
+  hydra::DeviceScope ds_(p->device);  // IPC mappings and drains on the group's device
   for (size_t i = 0; i < p->regs.size(); i++) {
     if (p->regs[i].base != buf) continue;
     (void)hydra::drain_device(p->device);  // no kernel may still read through the mappings
@@ -323,6 +327,7 @@ int hydra_peer_allreduce(hydra_peer_t p, int algo, int op, int dtype, int flags,
                          size_t n, size_t max_segment, hydra_stream_t stream) {
   hydra::TraceRange trace_("hydra_peer_allreduce");
   if (!p) return fail(HYDRA_ERR_INVALID, "null peer");
+  hydra::DeviceScope ds_(p->device);  // the group's device, restored on return
   if (p->detached) return fail(HYDRA_ERR_INVALID, "peer group detached");
   const size_t es = hydra::dtype_size(dtype);
   if (!es) return fail(HYDRA_ERR_INVALID, "invalid dtype");
@@ -398,6 +403,7 @@ int hydra_peer_allreduce(hydra_peer_t p, int algo, int op, int dtype, int flags,
 
 int hydra_peer_detach(hydra_peer_t p) {
   if (!p) return fail(HYDRA_ERR_INVALID, "null peer");
+  hydra::DeviceScope ds_(p->device);  // the group's device, restored on return
   if (p->detached) return ok();
   (void)hydra::drain_device(p->device);  // no kernel of ours may still read through the mappings
   for (auto& kv : p->opened) {
@@ -414,6 +420,7 @@ int hydra_peer_detach(hydra_peer_t p) {
 
 int hydra_peer_destroy(hydra_peer_t p) {
   if (!p) return ok();
+  hydra::DeviceScope ds_(p->device);  // the group's device, restored on return
   (void)hydra_peer_detach(p);  // local; callers detach + barrier first (hydra_hip.h)
   if (p->scratch) {
     (void)hipFree(p->scratch);

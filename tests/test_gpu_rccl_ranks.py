@@ -59,8 +59,10 @@ def _worker(rank, world, port, q):
     try:
         torch.cuda.set_device(0)
         dev = torch.device("cuda", 0)
+        dev0 = torch.cuda.current_device()
         comm = ring.XgmiComm(rank, world, 0, ring.exchange_unique_id(rank))
         comms.append(comm)
+        res["device_unchanged_by_init"] = torch.cuda.current_device() == dev0
         info = comm.info()
         res["comm_info"] = info == {"nccl_comm_count": world, "nccl_user_rank": rank,
                                     "nccl_device": 0}
@@ -345,9 +347,10 @@ def _capture_worker(rank, world, port, q):
         comm.allreduce_(t, algo="auto")  # outside the capture: works as before
         comm.wait(30000)
         res["after"] = float(t[0]) == float(world) and float(t[-1]) == float(world)
+        dev0 = torch.cuda.current_device()
         comm.close()
         comm = None
-        res["closed"] = True
+        res["closed"] = torch.cuda.current_device() == dev0  # destroy restores the device
     except Exception as e:  # report instead of hanging the parent
         import traceback
 
