@@ -87,21 +87,30 @@ def drainer(out, stop):
     rng = random.Random(7)
     while not stop.is_set():
         what = rng.choice(("free_pinned", "device_check", "ctx", "trim"))
+        times = {}
         t0 = time.perf_counter()
         if what == "free_pinned":
             p = ctypes.c_void_p()
             _lib.check(L.hydra_malloc_host(1 << 20, ctypes.byref(p)))
+            times["malloc_pinned"] = time.perf_counter() - t0
             t0 = time.perf_counter()
             _lib.check(L.hydra_free_host(p))
+            times["free_pinned"] = time.perf_counter() - t0
         elif what == "device_check":
             _lib.check(L.hydra_device_check(0))
+            times[what] = time.perf_counter() - t0
         elif what == "ctx":
-            HostContext(0).close()
+            c = HostContext(0)
+            times["ctx_create"] = time.perf_counter() - t0
+            t0 = time.perf_counter()
+            c.close()
+            times["ctx_destroy"] = time.perf_counter() - t0
         else:
             _lib.check(L.hydra_cache_trim())
-        dt = time.perf_counter() - t0
-        ops[what] = ops.get(what, 0) + 1
-        worst[what] = max(worst.get(what, 0.0), dt)
+            times[what] = time.perf_counter() - t0
+        for name, dt in times.items():
+            ops[name] = ops.get(name, 0) + 1
+            worst[name] = max(worst.get(name, 0.0), dt)
         n += 1
         time.sleep(0.02)
     out["drainer"] = {"ops": ops, "worst_ms": {k: round(v * 1e3, 2) for k, v in worst.items()}}
