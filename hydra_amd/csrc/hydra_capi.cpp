@@ -443,7 +443,7 @@ int hydra_reduce_host(hydra_ctx_t ctx, int op, int dtype, void* c, const void* a
   size_t used[3] = {0, 0, 0};  // bytes of the current buffer's a, b, c slots
   int buf = 0;
   bool pending = false;  // the other buffer's round is in flight
-  auto timed = [&](double* acc, const std::function<void()>& f) {  // (tracing only)
+  auto timed = [&](double* acc, auto&& f) {  // f's wall time into *acc while tracing
     if (!tracing) return f();
     const Clock::time_point t0 = Clock::now();
     f();
