@@ -220,6 +220,7 @@ struct hydra_comm {
     std::vector<ProfRec> ops;
   };
   bool profile = false;
+  bool prof_active = false;  // the call being enqueued is recorded
   std::vector<ProfCall> prof_calls;
   std::vector<hipEvent_t> prof_pool;  // timing events (created on `device`)
   hydra_comm_phases_t prof{};
@@ -247,9 +248,13 @@ hipError_t prof_event(hydra_comm* c, hipEvent_t* out) {
   return hipEventCreate(out);  // timing enabled; the caller holds a DeviceScope(c->device)
 }
 
-// Opens a profiled call: its start on the caller's stream.  No-op unless profiling is on.
+// Opens a profiled call: its start on the caller's stream.  No-op unless profiling is on; at
+// most kProfMaxCalls calls are held until hydra_comm_phases reads them (later ones go unrecorded,
+// so a caller that never reads cannot grow the event pool without bound).
+constexpr size_t kProfMaxCalls = 256;
 int prof_begin(hydra_comm* c, hipStream_t user_st) {
-  if (!c->profile) return HYDRA_OK;
+  c->prof_active = c->profile && c->prof_calls.size() < kProfMaxCalls;
+  if (!c->prof_active) return HYDRA_OK;
   hydra_comm::ProfCall call{};
   HIP_TRY(prof_event(c, &call.t0));
   HIP_TRY(hipEventRecord(call.t0, user_st));
@@ -265,7 +270,7 @@ struct ProfOp {
   bool on = false;
   ProfOp(hydra_comm* c_, hipStream_t st_, bool comm, uint64_t sent, uint64_t recv, uint64_t hbm)
       : c(c_), st(st_) {
-    if (!c->profile || c->prof_calls.empty()) return;
+    if (!c->profile || !c->prof_active || c->prof_calls.empty()) return;
     r.comm = comm;
     r.sent = sent;
     r.recv = recv;
