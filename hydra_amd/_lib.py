@@ -42,7 +42,7 @@ EXPORTS = [  # every symbol include/hydra_hip.h declares
     "hydra_peer_detach", "hydra_peer_destroy", "hydra_comm_wait",
     "hydra_reduce_root", "hydra_reduce_root_plan", "hydra_reduce_root_simulate",
     "hydra_comm_profile", "hydra_comm_phases", "hydra_stream_wait_event", "hydra_device_peer_access",
-    "hydra_host_trace", "hydra_host_trace_read",
+    "hydra_host_trace", "hydra_host_trace_read", "hydra_device_link",
 ]
 
 (ALGO_AUTO, ALGO_RING, ALGO_DIRECT, ALGO_RCCL, ALGO_A2A, ALGO_RING_OLD, ALGO_RING_CHUNKED,
@@ -227,6 +227,7 @@ def _declare(L) -> None:
     L.hydra_host_trace.argtypes = [i]
     L.hydra_host_trace_read.argtypes = [vp, sz, ctypes.POINTER(sz)]
     L.hydra_device_peer_access.argtypes = [i, i, ctypes.POINTER(i)]
+    L.hydra_device_link.argtypes = [i, i, ctypes.POINTER(i), ctypes.POINTER(i), ctypes.POINTER(i)]
     L.hydra_comm_profile.argtypes = [vp, i]
     L.hydra_comm_phases.argtypes = [vp, ctypes.POINTER(CommPhases)]
 
@@ -280,6 +281,26 @@ def host_mappings():
     live = [{f: getattr(buf[i], f) for f, _ in HostMapping._fields_}
             for i in range(min(cnt.value, cap))]
     return live, regs.value, out.value
+
+
+LINK_TYPES = {0: "hypertransport", 1: "qpi", 2: "pcie", 3: "infiniband", 4: "xgmi"}
+
+
+def device_links(device: int = 0) -> list:
+    """hydra_device_link from `device` to every other visible device: link type, hops, peer
+    access (an empty list on a one-GPU box)."""
+    import torch
+
+    out = []
+    for q in range(torch.cuda.device_count()):
+        if q == device:
+            continue
+        t, h, c = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        check(lib().hydra_device_link(device, q, ctypes.byref(t), ctypes.byref(h),
+                                      ctypes.byref(c)))
+        out.append({"peer": q, "link": LINK_TYPES.get(t.value, t.value), "hops": h.value,
+                    "peer_access": bool(c.value)})
+    return out
 
 
 def set_variant(v: int) -> int:

@@ -740,6 +740,22 @@ int hydra_device_peer_access(int device, int peer, int* can) {
   return ok();
 }
 
+int hydra_device_link(int device, int peer, int* link, int* hops, int* can_peer) {
+  if (!link || !hops || !can_peer) return fail(HYDRA_ERR_INVALID, "null out");
+  int count = 0;
+  HIP_TRY(hipGetDeviceCount(&count));
+  if (device < 0 || device >= count || peer < 0 || peer >= count || device == peer)
+    return fail(HYDRA_ERR_INVALID, "need two distinct visible devices");
+  uint32_t t = 0, h = 0;
+  HIP_TRY(hipExtGetLinkTypeAndHopCount(device, peer, &t, &h));
+  int c = 0;
+  HIP_TRY(hipDeviceCanAccessPeer(&c, device, peer));
+  *link = (int)t;
+  *hops = (int)h;
+  *can_peer = c;
+  return ok();
+}
+
 int hydra_malloc(int device, size_t bytes, void** out) {
   if (!out) return fail(HYDRA_ERR_INVALID, "null out");
   HIP_TRY(hydra::cached_malloc(device, bytes, out));

@@ -483,6 +483,13 @@ def bench_allreduce(args, dev, make_comm=None, sync=None, cpu_baseline=None) -> 
                  "backend": info.get("backend", "rccl")}
     if "error" in info:
         comm_seen["error"] = info["error"]
+    # the fabric between this rank's GPU and the node's others (xGMI vs PCIe, hops, peer
+    # access): the line shows what its links were (empty when the process sees one GPU)
+    try:
+        comm_seen["links_from_device"] = (_lib.device_links(dev.index)
+                                          if getattr(dev, "type", "") == "cuda" else [])
+    except (HydraError, RuntimeError) as e:
+        comm_seen["links_from_device"] = f"n/a: {e}"
     extra_legs = bool(getattr(args, "extra_legs", False))
     cpu_base = None
     from .peer import PeerComm

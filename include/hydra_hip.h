@@ -237,6 +237,11 @@ int hydra_stream_wait_event(hydra_stream_t s, hydra_event_t e);
  * `device`'s access to `peer`'s memory is enabled (idempotent; device == peer: *can = 1).  The
  * caller's current device is left as it was. */
 int hydra_device_peer_access(int device, int peer, int* can);
+/* Topology between two devices (inspection; the N>1 bench line records it, so a multi-GPU line
+ * shows which fabric its links were): *link = hipExtGetLinkTypeAndHopCount's link type
+ * (2 PCIe, 4 xGMI; hsa_amd_link_info_type_t), *hops its hop count, *can_peer =
+ * hipDeviceCanAccessPeer.  Changes no device state (peer access is not enabled here). */
+int hydra_device_link(int device, int peer, int* link, int* hops, int* can_peer);
 int hydra_malloc(int device, size_t bytes, void** out);
 int hydra_free(void* p);
 int hydra_memcpy(void* dst, const void* src, size_t bytes); /* hipMemcpyDefault, synchronous */
