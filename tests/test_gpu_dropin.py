@@ -22,10 +22,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 EXE = os.path.join(ROOT, "tests", "cpp", "dropin_gloo")
 
 
-def dropin(mode, P, n, dt="f32", iters=0, ms=0, timeout=240, register=False):
+def dropin(mode, P, n, dt="f32", iters=0, ms=0, timeout=240, register=False, env_extra=None):
     assert os.path.exists(EXE), "built with the reference by oracle/Makefile (build())"
     args = [EXE, mode, str(P), str(n), dt, str(iters)] + ([str(ms)] if ms else [])
-    env = dict(os.environ, HYDRA_DROPIN_REGISTER="1" if register else "0")
+    env = dict(os.environ, HYDRA_DROPIN_REGISTER="1" if register else "0", **(env_extra or {}))
     r = subprocess.run(args, capture_output=True, text=True, timeout=timeout, env=env)
     assert r.returncode == 0, r.stdout + r.stderr
     return json.loads(r.stdout.strip().splitlines()[-1])
@@ -96,12 +96,18 @@ def test_config1_full_size_inside_the_reference(gpu, n):
     assert j["mismatched_bytes"] == 0, j
 
 
+@pytest.mark.parametrize("result_path", ["default", "in_place", "staged"])
 @pytest.mark.parametrize("mode,P,n", [("new_ring", 2, 1 << 20), ("new_ring", 3, 4099),
-                                      ("new_ring2", 2, 262147), ("old_ring", 4, 100003)])
-def test_reference_with_hydra_func_registered_bucket(gpu, mode, P, n):
-    """The bucket registered once (hydra_host_register): the kernel reads and writes it in place
-    over PCIe while only the reference's pageable scratch is staged -- same bytes."""
-    j = dropin(mode, P, n, register=True)
+                                      ("new_ring2", 2, 262147), ("old_ring", 4, 100003),
+                                      ("new_ring", 2, (4 << 20) + 3)])
+def test_reference_with_hydra_func_registered_bucket(gpu, mode, P, n, result_path):
+    """The bucket registered once (hydra_host_register): the kernel reads it in place over PCIe
+    while only the reference's pageable scratch is staged, and writes its results either in place
+    (registrations above 8 MiB -- the last case's 16 MiB bucket -- or always with
+    HYDRA_STAGE_RESULT_REG_MAX=0) or through the staging (smaller ones, or always): same bytes."""
+    env = {"default": {}, "in_place": {"HYDRA_STAGE_RESULT_REG_MAX": "0"},
+           "staged": {"HYDRA_STAGE_RESULT_MAX": str(1 << 30)}}[result_path]
+    j = dropin(mode, P, n, register=True, env_extra=env)
     assert j["mismatched_bytes"] == 0, j
 
 
