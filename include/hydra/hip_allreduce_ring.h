@@ -39,6 +39,7 @@
 
 #include <algorithm>
 #include <climits>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <type_traits>
@@ -144,6 +145,12 @@ class LocalReduce {
   }
   void init(std::vector<LocalStep> steps, const std::vector<int>& dev, size_t bytes) {
     steps_ = std::move(steps);
+    // test hook: HYDRA_TEST_LOCAL_STAGE=1 stages every step as if its two pointers were on
+    // devices without peer access, so the one-GPU box runs the cross-device staging branch
+    // (copy to a buffer on the destination's device, event waits) with real kernels
+    if (const char* v = std::getenv("HYDRA_TEST_LOCAL_STAGE"))
+      if (v[0] == '1')
+        for (LocalStep& s : steps_) s.staged = true;
     ev_.assign(dev.size(), nullptr);
     for (size_t i = 0; i < dev.size(); i++) enforce(hydra_event_create_on(dev[i], &ev_[i]));
     stage_.clear();

@@ -161,11 +161,13 @@ def _tree(O, xs, code):
                                          (3, 2, 100003, "f32"), (4, 4, 4099, "f32"),
                                          (5, 3, 7, "f32"), (3, 2, 70001, "i32"),
                                          (2, 1, 0, "f32")])
-def test_hip_allreduce_ring(gpu, O, workspace, P, nptr, n, dt):
+def test_hip_allreduce_ring(gpu, O, workspace, P, nptr, n, dt, monkeypatch, stage=False):
     """hydra::HipAllreduceRing<T, W> (gloo::CudaAllreduceRing<T, W>): rank r ends with its own
     left fold x_r + x_{r-1} + ... of the locally reduced values (the AllreduceRing result,
     pinned to the reference by the old_ring fixtures); host workspace pre-reduces pointers as a
     left fold, device workspace as the pairwise tree; every pointer gets the result."""
+    if stage:  # every local-reduce step through the cross-device staging branch
+        monkeypatch.setenv("HYDRA_TEST_LOCAL_STAGE", "1")
     import torch
 
     code = {"f32": 6, "i32": 2}[dt]
@@ -287,11 +289,14 @@ def test_reduce_gpu_reducer_large(gpu, O, pinned):
                                          (3, 2, 100003, "f32"), (4, 4, 4099, "f32"),
                                          (5, 3, 7, "f32"), (3, 2, 70001, "i32"),
                                          (2, 1, 0, "f32")])
-def test_hip_allreduce_ring_chunked(gpu, O, workspace, P, nptr, n, dt):
+def test_hip_allreduce_ring_chunked(gpu, O, workspace, P, nptr, n, dt, monkeypatch=None,
+                                    stage=False):
     """hydra::HipAllreduceRingChunked<T, W> (gloo::CudaAllreduceRingChunked<T, W>): every rank
     ends with AllreduceRingChunked's result (pinned to the reference by the chunked_ring
     fixtures) over the locally reduced values -- CudaLocalNativeReduce's pairwise tree for both
     workspaces (cuda_collectives_device.h:29-56); every pointer gets the result."""
+    if stage:  # every local-reduce step through the cross-device staging branch
+        monkeypatch.setenv("HYDRA_TEST_LOCAL_STAGE", "1")
     import torch
 
     code = {"f32": 6, "i32": 2}[dt]
@@ -309,6 +314,18 @@ def test_hip_allreduce_ring_chunked(gpu, O, workspace, P, nptr, n, dt):
             for i in range(nptr):
                 got = ts[r][i].cpu().numpy()
                 assert_bits(got, exp[r][0], (r, i, user_streams))
+
+
+@pytest.mark.parametrize("workspace", ["host", "device"])
+@pytest.mark.parametrize("P,nptr,n,dt", [(1, 3, 1000, "f32"), (3, 2, 100003, "f32"),
+                                         (4, 4, 4099, "f32"), (3, 2, 70001, "i32")])
+def test_hip_rings_local_reduce_staged(gpu, O, workspace, P, nptr, n, dt, monkeypatch):
+    """The rings over several GPUs of one process: a local-reduce step whose two
+    pointers sit on devices without peer access copies the source to a buffer on the
+    destination's device first, ordered by events.  HYDRA_TEST_LOCAL_STAGE=1 takes that branch
+    for every step on the one GPU: the same bits as the reference semantics."""
+    test_hip_allreduce_ring(gpu, O, workspace, P, nptr, n, dt, monkeypatch, stage=True)
+    test_hip_allreduce_ring_chunked(gpu, O, workspace, P, nptr, n, dt, monkeypatch, stage=True)
 
 
 @pytest.mark.extra
