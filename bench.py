@@ -346,6 +346,53 @@ def cpu_baseline(n, seconds):
             "per_call_ms": round(per * 1e3, 3)}
 
 
+def host_path_leg(n=16 << 20, calls=5):
+    """Context: the same chunk-sum on HOST buffers through
+    hydra_reduce_host, c == a in place as the ring calls it -- the PCIe-inclusive rate, never
+    `value`.  pinned: hipHostMalloc'd operands read and written in place over PCIe (zero-copy);
+    pageable: plain heap operands, copied by the CPU through the context's pinned staging.  GB/s
+    of algorithmic bytes (12 B/element), median of `calls` calls after one untimed call."""
+    import ctypes
+
+    from hydra_amd import _lib
+    from hydra_amd.reduce import HostContext
+
+    L = _lib.lib()
+    out = {"elements": n, "bytes_per_element": 12, "calls": calls,
+           "note": "operands in host memory: bound by PCIe (DESIGN.md 6.3), context only"}
+    ctx = HostContext(0)
+    blocks = []
+    try:
+        def alloc_pinned():
+            p = ctypes.c_void_p()
+            _lib.check(L.hydra_malloc_host(n * 4, ctypes.byref(p)))
+            blocks.append(p)
+            return np.frombuffer((ctypes.c_char * (n * 4)).from_address(p.value), np.float32)
+
+        kinds = {"pinned_zero_copy": (alloc_pinned(), alloc_pinned()),
+                 "pageable_staged": (np.empty(n, np.float32), np.empty(n, np.float32))}
+        for name, (a, b) in kinds.items():
+            a[:] = np.arange(n, dtype=np.float32) % 1024
+            b[:] = 1.0
+            _lib.check(L.hydra_reduce_host(ctx.handle, 0, 6, a.ctypes.data, a.ctypes.data,
+                                           b.ctypes.data, n))
+            ok = bool(np.array_equal(a, (np.arange(n, dtype=np.float32) % 1024) + 1.0))
+            ts = []
+            for _ in range(calls):
+                t0 = time.perf_counter()
+                _lib.check(L.hydra_reduce_host(ctx.handle, 0, 6, a.ctypes.data, a.ctypes.data,
+                                               b.ctypes.data, n))
+                ts.append(time.perf_counter() - t0)
+            med = float(np.median(ts))
+            out[name] = {"ms_per_call": round(med * 1e3, 3),
+                         "GBps": round(12.0 * n / med / 1e9, 2), "first_call_exact": ok}
+    finally:
+        ctx.close()
+        for p in blocks:
+            L.hydra_free_host(p)
+    return out
+
+
 def run_single(args):
     import torch
 
@@ -435,6 +482,10 @@ def run_single(args):
             sweep.append({"elements": nn, "us_per_launch": round(us, 2),
                           "GBps": round(12.0 * nn / (us * 1e-6) / 1e9, 1)})
         out["sweep"] = sweep
+    try:  # row N2: the PCIe-inclusive host-buffer rate beside the HBM one (context only)
+        out["host_path"] = host_path_leg()
+    except Exception as e:  # context, never the product's headline
+        out["host_path"] = {"error": str(e)}
     if not args.no_cpu_baseline:
         try:
             out["cpu_baseline"] = cpu_baseline(n, args.cpu_seconds)
