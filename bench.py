@@ -45,6 +45,8 @@ def parse():
     p.add_argument("--elements", type=int, default=N_MICRO)
     p.add_argument("--dtype", default="f32", choices=["f32", "i32"])
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-host-path", action="store_true",
+                   help="N=1: skip the host-buffer (PCIe-inclusive) context leg")
     p.add_argument("--cpu-seconds", type=float, default=10.0,
                    help="bounded CPU-baseline sample (seconds of reference gloo::sum work)")
     p.add_argument("--sweep", action="store_true",
@@ -482,10 +484,11 @@ def run_single(args):
             sweep.append({"elements": nn, "us_per_launch": round(us, 2),
                           "GBps": round(12.0 * nn / (us * 1e-6) / 1e9, 1)})
         out["sweep"] = sweep
-    try:  # row N2: the PCIe-inclusive host-buffer rate beside the HBM one (context only)
-        out["host_path"] = host_path_leg()
-    except Exception as e:  # context, never the product's headline
-        out["host_path"] = {"error": str(e)}
+    if not args.no_host_path:
+        try:  # row N2: the PCIe-inclusive host-buffer rate beside the HBM one (context only)
+            out["host_path"] = host_path_leg()
+        except Exception as e:  # context, never the product's headline
+            out["host_path"] = {"error": str(e)}
     if not args.no_cpu_baseline:
         try:
             out["cpu_baseline"] = cpu_baseline(n, args.cpu_seconds)

@@ -60,15 +60,15 @@ for s in "$@"; do
       rc=$?; tail -1 "$OUT/smoke.log";;
     prof)
       step rocprof_kt 600 rocprofv3 --kernel-trace --stats --output-format csv \
-          -d "$OUT/prof_kt" -o run -- python3 "$ROOT/bench.py" --steps 100 --warmup 10 --no-cpu-baseline
+          -d "$OUT/prof_kt" -o run -- python3 "$ROOT/bench.py" --steps 100 --warmup 10 --no-cpu-baseline --no-host-path
       rc=$?
       python3 scripts/headline_from_trace.py "$OUT/prof_kt/run_kernel_trace.csv" 10 100 "$TAG" \
           > "$OUT/headline_from_trace.json" 2>&1 || true
       [ $rc -eq 0 ] && step rocprof_fetch 300 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv \
-          -d "$OUT/prof_fetch" -o run -- python3 "$ROOT/bench.py" --steps 20 --warmup 2 --no-cpu-baseline
+          -d "$OUT/prof_fetch" -o run -- python3 "$ROOT/bench.py" --steps 20 --warmup 2 --no-cpu-baseline --no-host-path
       rc=$?
       [ $rc -eq 0 ] && step rocprof_write 300 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --output-format csv \
-          -d "$OUT/prof_write" -o run -- python3 "$ROOT/bench.py" --steps 20 --warmup 2 --no-cpu-baseline
+          -d "$OUT/prof_write" -o run -- python3 "$ROOT/bench.py" --steps 20 --warmup 2 --no-cpu-baseline --no-host-path
       rc=$?
       python3 scripts/pmc_summary.py "$OUT" "${ROUND:-r04}" > "$OUT/pmc_summary.json" 2>&1 || true;;
     bench|bench_*)
