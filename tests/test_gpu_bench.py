@@ -65,3 +65,23 @@ def test_bench_multi_path_world1_extra_legs(gpu):
     for algo in ("ring_old", "ring_chunked", "bcube", "reduce_root"):
         assert parity[algo] == "bit-exact", (algo, parity)
     assert all(isinstance(v, float) for v in res["other_algos_ms"].values()), res
+
+
+def test_bench_single_gpu_line(gpu):
+    """bench.py at N = 1 (the driver's default command, smaller here): the contract's fields --
+    roofline with HIP-event achieved bytes, the CPU baseline pinned to the GPU's NUMA node with
+    every repetition, and the host-buffer (PCIe-inclusive) context leg, exact on its first call."""
+    p = subprocess.run([sys.executable, "-u", "bench.py", "--elements", str(1 << 22), "--steps",
+                        "20", "--warmup", "2", "--cpu-seconds", "0.5"],
+                       cwd=ROOT, capture_output=True, text=True, timeout=110)
+    assert p.returncode == 0, (p.returncode, p.stdout[-2000:], p.stderr[-2000:])
+    res = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    assert res["n_gpus"] == 1 and res["value"] > 0 and res["dtype"] == "f32", res
+    rf = res["roofline"]
+    assert rf["bound"] == "hbm" and rf["peak"] == 8000.0 and 0 < rf["frac"] < 1, rf
+    cb = res["cpu_baseline"]
+    assert cb["kind"] == "reference" and cb["cores"] == 1 and cb["value"] > 0, cb
+    assert len(cb["repetitions_GBps"]) == 3 and cb["pinned_cpu"] != 0, cb
+    hp = res["host_path"]
+    for kind in ("pinned_zero_copy", "pageable_staged"):
+        assert hp[kind]["first_call_exact"] and hp[kind]["GBps"] > 0, hp
