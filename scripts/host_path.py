@@ -9,11 +9,17 @@ lives in host memory, as it does in the reference's TCP ring.
      the GPU reducer (staged and zero-copy), in the same run
   3. config 3: bew_allreduce_a, 2 ranks x 2 loopback rails -- hydra host runtime with the
      reference's gloo::sum<float> as reducer vs the GPU reducer (H2D + sum + D2H per segment)
+Configs 1 and 3 run every size REPS times (default 3) with the implementations interleaved, and
+report per implementation the median over repetitions of rank 0's p50 / p99 / avg and GiB/s
+(and every repetition); the process is pinned to PIN_CORES (default 8) CPUs of the GPU's NUMA
+node, never CPU 0 (PIN=0 leaves the affinity alone), as scripts/dropin_sweep.py.
 Prints one JSON document.
 """
 import ctypes
 import json
 import os
+import statistics
+import subprocess
 import sys
 import time
 
@@ -21,6 +27,21 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+# pinned before this process touches HIP (its threads and the host runtime's inherit it); the
+# GPU's NUMA node comes from a child process
+pinned = None
+if os.environ.get("PIN", "1") != "0" and hasattr(os, "sched_setaffinity"):
+    import bench  # (no torch import at module level)
+
+    q = subprocess.run([sys.executable, "-c", "import bench; print(bench.gpu_numa_node())"],
+                       capture_output=True, text=True, timeout=300, cwd=ROOT)
+    try:
+        gnode = int(q.stdout.strip().splitlines()[-1])
+    except (ValueError, IndexError):
+        gnode = None
+    cores, node, note = bench.baseline_cores(int(os.environ.get("PIN_CORES", "8")), node=gnode)
+    os.sched_setaffinity(0, set(cores))
+    pinned = {"cpus": cores, "numa_node": node, "placement": note}
 import torch  # noqa: E402,F401
 
 from hydra_amd import _lib, host  # noqa: E402
@@ -28,7 +49,7 @@ from hydra_amd.reduce import HostContext  # noqa: E402
 from oracle import oracle as O  # noqa: E402  (CPU baseline only)
 
 L = _lib.lib()
-out = {"host": {"cpus": os.cpu_count()}}
+out = {"host": {"cpus": os.cpu_count()}, "pinned": pinned}
 try:
     out["host"]["model"] = [ln.split(":")[1].strip() for ln in open("/proc/cpuinfo")
                             if ln.startswith("model name")][0]
@@ -109,38 +130,59 @@ def keep(impl, n, samples):
     return samples
 
 
+REPS = int(os.environ.get("REPS", "3"))
+# (config, implementation, per-iteration ns of rank 0 for (n, iters)); interleaved per size
+impls = []
+if O.ref_available():
+    impls.append(("c1", "reference (gloo, CPU sum)", lambda n, it: O.ref_bench_ring(2, n, 3, it)))
+impls += [("c1", "hydra host runtime, GPU sum", lambda n, it: host.bench(1, 2, n, 3, it)),
+          ("c1", "hydra host runtime, GPU sum zero-copy (pinned slots, registered out)",
+           lambda n, it: host.bench(1, 2, n, 3, it, pinned=True))]
+if ref_fn:  # the same runtime with the reference's CPU sum: transport vs reducer
+    impls.append(("c1", "hydra host runtime + reference gloo::sum (CPU)",
+                  lambda n, it: host.bench(1, 2, n, 3, it, reducer_fn=ref_fn)))
+if ref_fn:  # one GPU per rank, approximated: only rank 0's reduces use the box's one GPU
+    impls.append(("c1", "hydra host runtime, GPU sum zero-copy on rank 0 only "
+                        "(rank 1: reference gloo::sum)",
+                  lambda n, it: host.bench(1, 2, n, 3, it, reducer_fn=ref_fn,
+                                           gpu_rank0_only=True)))
+    impls.append(("c3", "hydra split + reference gloo::sum (CPU)",
+                  lambda n, it: host.bench(3, 2, n, 3, it, reducer_fn=ref_fn)))
+impls += [("c3", "hydra split, GPU sum (H2D+sum+D2H)", lambda n, it: host.bench(3, 2, n, 3, it)),
+          ("c3", "hydra split, GPU sum zero-copy (pinned slots, registered out)",
+           lambda n, it: host.bench(3, 2, n, 3, it, pinned=True))]
+if ref_fn:
+    impls.append(("c3", "hydra split, GPU sum zero-copy on rank 0 only "
+                        "(rank 1: reference gloo::sum)",
+                  lambda n, it: host.bench(3, 2, n, 3, it, reducer_fn=ref_fn,
+                                           gpu_rank0_only=True)))
+table_key = {"reference (gloo, CPU sum)": "c1 reference",
+             "hydra host runtime, GPU sum": "c1 hydra GPU sum",
+             "hydra host runtime, GPU sum zero-copy (pinned slots, registered out)":
+                 "c1 hydra GPU sum zero-copy",
+             "hydra split + reference gloo::sum (CPU)": "c3 hydra split + reference sum",
+             "hydra split, GPU sum (H2D+sum+D2H)": "c3 hydra GPU sum"}
+
 for n in sizes:
     iters = max(5, min(50, (1 << 27) // max(n, 1)))
-    sys.stderr.write(f"[host_path] n={n} iters={iters}\n")
+    sys.stderr.write(f"[host_path] n={n} iters={iters} reps={REPS}\n")
     sys.stderr.flush()
-    if O.ref_available():
-        c1.append({"impl": "reference (gloo, CPU sum)",
-                   **dist(keep("c1 reference", n, O.ref_bench_ring(2, n, 3, iters)), n)})
-    c1.append({"impl": "hydra host runtime, GPU sum",
-               **dist(keep("c1 hydra GPU sum", n, host.bench(1, 2, n, 3, iters)), n)})
-    c1.append({"impl": "hydra host runtime, GPU sum zero-copy (pinned slots, registered out)",
-               **dist(keep("c1 hydra GPU sum zero-copy", n,
-                           host.bench(1, 2, n, 3, iters, pinned=True)), n)})
-    if ref_fn:  # one GPU per rank, approximated: only rank 0's reduces use the box's one GPU
-        c1.append({"impl": "hydra host runtime, GPU sum zero-copy on rank 0 only "
-                           "(rank 1: reference gloo::sum)",
-                   **dist(host.bench(1, 2, n, 3, iters, reducer_fn=ref_fn,
-                                     gpu_rank0_only=True), n)})
-    if ref_fn:
-        c3.append({"impl": "hydra split + reference gloo::sum (CPU)",
-                   **dist(keep("c3 hydra split + reference sum", n,
-                               host.bench(3, 2, n, 3, iters, reducer_fn=ref_fn)), n)})
-    c3.append({"impl": "hydra split, GPU sum (H2D+sum+D2H)",
-               **dist(keep("c3 hydra GPU sum", n, host.bench(3, 2, n, 3, iters)), n)})
-    c3.append({"impl": "hydra split, GPU sum zero-copy (pinned slots, registered out)",
-               **dist(host.bench(3, 2, n, 3, iters, pinned=True), n)})
-    if ref_fn:
-        c3.append({"impl": "hydra split, GPU sum zero-copy on rank 0 only "
-                           "(rank 1: reference gloo::sum)",
-                   **dist(host.bench(3, 2, n, 3, iters, reducer_fn=ref_fn,
-                                     gpu_rank0_only=True), n)})
+    runs = {(tag, label): [] for tag, label, _ in impls}
+    for rep in range(REPS):
+        for tag, label, fn in impls:
+            samples = fn(n, iters)
+            if rep == 0 and label in table_key:
+                keep(table_key[label], n, samples)
+            runs[(tag, label)].append(dist(samples, n))
+    for (tag, label), ds in runs.items():
+        med = {k: round(statistics.median(d[k] for d in ds), 3 if k == "GiBps" else 1)
+               for k in ("p50_us", "p99_us", "avg_us", "GiBps")}
+        (c1 if tag == "c1" else c3).append(
+            {"impl": label, "elements": n, "min_us": min(d["min_us"] for d in ds), **med,
+             "reps": [{k: d[k] for k in ("p50_us", "avg_us", "GiBps")} for d in ds]})
 out["config1_new_allreduce_ring_P2"] = c1
 out["config3_bew_allreduce_a_P2"] = c3
+out["reps"] = REPS
 if os.environ.get("TABLE"):  # the reference benchmark's own table per implementation
     from hydra_amd import report
 
