@@ -18,7 +18,9 @@
 #include <chrono>
 #include <cstring>
 #include <deque>
+#include <iterator>
 #include <thread>
+#include <utility>
 #include <map>
 #include <set>
 #include <string>
@@ -287,21 +289,37 @@ struct ProfOp {
   }
 };
 
-// Reads back every finished profiled call into the totals and recycles its events.
+// Reads back every finished profiled call into the totals and recycles its events.  A call is
+// read whole before anything of it is counted or recycled: on an error it stays (with the calls
+// after it) in prof_calls, so no event is ever both pending and pooled (teardown destroys each
+// once).
 int prof_collect(hydra_comm* c) {
-  for (auto& call : c->prof_calls) {
+  std::vector<hydra_comm::ProfCall> calls;
+  calls.swap(c->prof_calls);
+  for (size_t i = 0; i < calls.size(); i++) {
+    const hydra_comm::ProfCall& call = calls[i];
+    std::vector<std::pair<float, float>> t(call.ops.size());  // (duration, end after t0)
+    hipError_t e = hipSuccess;
+    for (size_t k = 0; k < call.ops.size() && e == hipSuccess; k++) {
+      const hydra_comm::ProfRec& r = call.ops[k];
+      e = hipEventSynchronize(r.e);
+      if (e == hipSuccess) e = hipEventElapsedTime(&t[k].first, r.s, r.e);
+      if (e == hipSuccess) e = hipEventElapsedTime(&t[k].second, call.t0, r.e);
+    }
+    if (e != hipSuccess) {
+      c->prof_calls.assign(std::make_move_iterator(calls.begin() + i),
+                           std::make_move_iterator(calls.end()));
+      return hydra::hip_fail(e, "hydra_comm_phases: reading a profiled call's events");
+    }
     float last = 0.f;
-    for (auto& r : call.ops) {
-      HIP_TRY(hipEventSynchronize(r.e));
-      float d = 0.f, end = 0.f;
-      HIP_TRY(hipEventElapsedTime(&d, r.s, r.e));
-      HIP_TRY(hipEventElapsedTime(&end, call.t0, r.e));
-      (r.comm ? c->prof.link_ms : c->prof.fold_ms) += d;
+    for (size_t k = 0; k < call.ops.size(); k++) {
+      const hydra_comm::ProfRec& r = call.ops[k];
+      (r.comm ? c->prof.link_ms : c->prof.fold_ms) += t[k].first;
       (r.comm ? c->prof.link_ops : c->prof.fold_ops) += 1;
       c->prof.sent_bytes += r.sent;
       c->prof.recv_bytes += r.recv;
       c->prof.fold_hbm_bytes += r.hbm;
-      last = std::max(last, end);
+      last = std::max(last, t[k].second);
       c->prof_pool.push_back(r.s);
       c->prof_pool.push_back(r.e);
     }
@@ -309,7 +327,6 @@ int prof_collect(hydra_comm* c) {
     c->prof.calls += 1;
     c->prof_pool.push_back(call.t0);
   }
-  c->prof_calls.clear();
   c->prof.peers = (int32_t)c->prof_peers.size();
   return HYDRA_OK;
 }
