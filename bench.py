@@ -305,8 +305,6 @@ def cpu_baseline(n, seconds):
     repetitions, every one reported."""
     from oracle import oracle as O
 
-    a = np.arange(n, dtype=np.float32)
-    b = np.ones(n, dtype=np.float32)
     kind = "reference" if O.ref_available() else "port"
     prev_aff = os.sched_getaffinity(0) if hasattr(os, "sched_getaffinity") else None
     cores, node, note = baseline_cores(1)
@@ -314,6 +312,12 @@ def cpu_baseline(n, seconds):
     if core is not None:
         os.sched_setaffinity(0, {core})
     try:
+        # the operands are first touched by the pinned core, so their pages are on its NUMA node:
+        # the same loop reads 70-72 GB/s from local pages and 44-45 GB/s from the other socket's
+        # (scripts/probe_cpu_baseline.py, profiles/r04za_cpu_baseline_numa.json), which is what
+        # made rounds 3-4's baseline read ~45 or ~70 GB/s depending on where the process started
+        a = np.arange(n, dtype=np.float32)
+        b = np.ones(n, dtype=np.float32)
         # calibrate, then ~`seconds` of work as 3 timed repetitions (mean per call of each)
         reps = []
         if kind == "reference":
@@ -343,6 +347,7 @@ def cpu_baseline(n, seconds):
             "spread": round((max(rates) - min(rates)) / float(np.median(rates)), 4),
             "sample": f"gloo::sum<float> in place over {n} fp32 elements (the headline's size, "
                       f"12 B/element), single thread pinned to host CPU {core} ({note}), "
+                      "operands first-touched by that core (NUMA-local pages), "
                       f"{iters} calls x 3 repetitions (~{seconds:.0f} s); value = the median "
                       "repetition",
             "per_call_ms": round(per * 1e3, 3)}
