@@ -19,11 +19,11 @@
 #include <cstring>
 #include <deque>
 #include <iterator>
-#include <thread>
-#include <utility>
 #include <map>
 #include <set>
 #include <string>
+#include <thread>
+#include <utility>
 #include <vector>
 
 #include "../../include/hydra_hip.h"
