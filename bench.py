@@ -367,6 +367,13 @@ def host_path_leg(n=16 << 20, calls=5):
     L = _lib.lib()
     out = {"elements": n, "bytes_per_element": 12, "calls": calls,
            "note": "operands in host memory: bound by PCIe (DESIGN.md 6.3), context only"}
+    # as a rank process runs: on CPUs of the GPU's NUMA node, operands allocated
+    # there (the copy helpers the staged path starts inherit the placement)
+    prev_aff = os.sched_getaffinity(0) if hasattr(os, "sched_getaffinity") else None
+    cores, node, note = baseline_cores(8)
+    if cores:
+        os.sched_setaffinity(0, set(cores))
+        out["placement"] = {"cpus": cores, "numa_node": node, "note": note}
     ctx = HostContext(0)
     blocks = []
     try:
@@ -397,6 +404,8 @@ def host_path_leg(n=16 << 20, calls=5):
         ctx.close()
         for p in blocks:
             L.hydra_free_host(p)
+        if cores and prev_aff:
+            os.sched_setaffinity(0, prev_aff)
     return out
 
 
