@@ -359,8 +359,6 @@ def host_path_leg(n=16 << 20, calls=5):
     `value`.  pinned: hipHostMalloc'd operands read and written in place over PCIe (zero-copy);
     pageable: plain heap operands, copied by the CPU through the context's pinned staging.  GB/s
     of algorithmic bytes (12 B/element), median of `calls` calls after one untimed call."""
-    import ctypes
-
     from hydra_amd import _lib
     from hydra_amd.reduce import HostContext
 
@@ -374,6 +372,18 @@ def host_path_leg(n=16 << 20, calls=5):
     if cores:
         os.sched_setaffinity(0, set(cores))
         out["placement"] = {"cpus": cores, "numa_node": node, "note": note}
+    try:
+        return _host_path_calls(L, HostContext, n, calls, out)
+    finally:
+        if cores and prev_aff:
+            os.sched_setaffinity(0, prev_aff)
+
+
+def _host_path_calls(L, HostContext, n, calls, out):
+    import ctypes
+
+    from hydra_amd import _lib
+
     ctx = HostContext(0)
     blocks = []
     try:
@@ -404,8 +414,6 @@ def host_path_leg(n=16 << 20, calls=5):
         ctx.close()
         for p in blocks:
             L.hydra_free_host(p)
-        if cores and prev_aff:
-            os.sched_setaffinity(0, prev_aff)
     return out
 
 
