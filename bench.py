@@ -8,11 +8,14 @@ Metric (BASELINE.json): chunk-sum GB/s (fp32) vs HBM peak; ring-allreduce GB/s a
          form), HBM-resident: launch k works on buffer pair k mod 4 (2 GiB cycled, 8x the
          Infinity Cache).  value = 12 B/element x elements x steps / wall time of the timed
          region; roofline.mall_assisted reports one pair back to back beside it.
-         --sweep adds config 2's 4 Ki..64 Mi size sweep to the line.
+         The line carries config 2's 4 Ki..64 Mi size sweep (HBM-resident and MALL-assisted
+         rates per size; --no-sweep skips it).
   N > 1  (BASELINE config 4): one step = one allreduce of a 64 Mi-element fp32 bucket per rank
          over xGMI in the reference's block ownership and fold order -- the fastest bit-exact
-         schedule of RCCL p2p with the HIP sum fused per hop (DIRECT / A2A / RING) and the
-         peer-access kernel (hydra_amd.ring, hydra_amd.peer).  value = N x bucket bytes / time
+         schedule of RCCL p2p with the HIP sum fused per hop (DIRECT / A2A / RING), and last
+         the peer-access kernel that reads the peers' blocks over xGMI and folds them in one
+         pass (hydra_amd.ring, hydra_amd.peer; it becomes the headline when bit-exact and
+         faster).  value = N x bucket bytes / time
          (whole-job bucket bytes reduced per second); algbw and busbw = algbw x 2(N-1)/N are
          reported beside it.
 
@@ -49,9 +52,9 @@ def parse():
                    help="N=1: skip the host-buffer (PCIe-inclusive) context leg")
     p.add_argument("--cpu-seconds", type=float, default=10.0,
                    help="bounded CPU-baseline sample (seconds of reference gloo::sum work)")
-    p.add_argument("--sweep", action="store_true",
-                   help="add the 4 Ki..64 Mi size sweep (BASELINE config 2's range); off by "
-                        "default so a kernel trace of the default command holds one size only")
+    p.add_argument("--no-sweep", action="store_true",
+                   help="skip the 4 Ki..64 Mi size sweep (BASELINE config 2's range), e.g. so a "
+                        "kernel trace of the command holds the headline size only")
     p.add_argument("--algo", default="auto", help="ring algorithm for N>1 (see hydra_amd.ring)")
     p.add_argument("--watchdog-s", type=float, default=420.0,
                    help="N>1: abort (exit 3) if the run exceeds this many seconds")
@@ -59,9 +62,11 @@ def parse():
     p.add_argument("--config5-elements", type=int, default=256 << 20,
                    help="N>1: bf16 elements of the config-5 leg (a multiple of 1 Mi; "
                         "BASELINE: 256 Mi)")
-    p.add_argument("--peer", action="store_true",
-                   help="N>1: also check, autotune and time the peer-access (IPC) schedules; "
-                        "off by default -- the cross-GPU IPC path has not run on an xGMI node")
+    p.add_argument("--peer", nargs="?", const="on", default="auto",
+                   choices=["auto", "on", "off"],
+                   help="N>1: the peer-access (IPC, reduce-on-read) leg, run last: auto (default) "
+                        "when every peer GPU is reached over xGMI with peer access; on: always "
+                        "(e.g. ranks sharing one GPU); off: never")
     p.add_argument("--extra-legs", action="store_true",
                    help="N>1: also check and time the schedules outside north_star's path "
                         "(old-style rings, BCUBE, halving-doubling, gloo::reduce to a root)")
@@ -205,6 +210,79 @@ def hbm_ceiling(torch, dev, pairs, launches=40, rounds=3):
                 rates.append(8.0 * n / (e0.elapsed_time(e1) / launches * 1e-3) / 1e9)
         out[name] = round(float(np.median(rates)), 1)
     return out
+
+
+SWEEP_POOL_BYTES = 1 << 30  # per operand: the HBM-resident sweep cycles 2 GiB (8x the MALL)
+
+
+def sweep_leg(torch, L, dev, code, lo=12, hi=26):
+    """BASELINE config 2's range (runner.cc:338-362 sweeps sizes the same way): the in-place
+    chunk-sum at 4 Ki, 16 Ki, ..., 64 Mi elements, back-to-back launches on the headline's
+    stream, timed by HIP events over each run (event span / launches: what a caller issuing one
+    segment after another sees, launch gaps included).
+      hbm_resident   launch k works on slot k of two 1 GiB pools (operands a, b), so no launch
+                     reuses another's lines until the 2 GiB cycle wraps
+      mall_assisted  one slot back to back (its operands stay in the 256 MiB Infinity Cache
+                     while they fit)
+    bound: "dispatch" when moving the launch's 12 B/element at the 8 TB/s peak would take less
+    than the smallest size's per-launch time (the launch floor), else "hbm"."""
+    from hydra_amd import _lib
+
+    esz = 4
+    pool_a = torch.empty(SWEEP_POOL_BYTES // esz, dtype=torch.float32, device=dev)
+    pool_b = torch.empty_like(pool_a)
+    pool_a.copy_(torch.arange(pool_a.numel(), device=dev, dtype=torch.float32) % 1024)
+    pool_b.fill_(1.0)
+    if code != _lib.FLOAT32:
+        pool_a, pool_b = pool_a.view(torch.int32), pool_b.view(torch.int32)
+    s = torch.cuda.current_stream(dev)
+    sp = s.cuda_stream
+    pa, pb = pool_a.data_ptr(), pool_b.data_ptr()
+
+    def run(nn, launches, slots):
+        step = nn * esz
+        for k in range(8):  # warm-up (code, TLB, clocks)
+            _lib.check(L.hydra_chunk_sum(code, pa + (k % slots) * step, pa + (k % slots) * step,
+                                         pb + (k % slots) * step, nn, sp))
+        torch.cuda.synchronize(dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        for k in range(launches):
+            off = (k % slots) * step
+            _lib.check(L.hydra_chunk_sum(code, pa + off, pa + off, pb + off, nn, sp))
+        e1.record(s)
+        torch.cuda.synchronize(dev)
+        return e0.elapsed_time(e1) / launches  # ms per launch
+
+    rows, floor_us = [], None
+    for k in range(lo, hi + 1, 2):
+        nn = 1 << k
+        slots = max(1, SWEEP_POOL_BYTES // (nn * esz))
+        launches = 400 if nn <= (1 << 20) else 200 if nn <= (1 << 22) else 100 if nn <= (1 << 24) \
+            else 40
+        hbm_ms = run(nn, launches, slots)
+        mall_ms = run(nn, launches, 1)
+        us = hbm_ms * 1e3
+        floor_us = us if floor_us is None else floor_us
+        ideal_us = 12.0 * nn / (HBM_PEAK_GBS * 1e9) * 1e6
+        hbm_gbs = 12.0 * nn / (hbm_ms * 1e-3) / 1e9
+        mall_gbs = 12.0 * nn / (mall_ms * 1e-3) / 1e9
+        rows.append({"elements": nn, "launches": launches, "hbm_slots": min(slots, launches),
+                     "hbm_resident": {"us_per_launch": round(us, 2), "GBps": round(hbm_gbs, 1),
+                                      "frac_of_peak": round(hbm_gbs / HBM_PEAK_GBS, 4)},
+                     "mall_assisted": {"us_per_launch": round(mall_ms * 1e3, 2),
+                                       "GBps": round(mall_gbs, 1),
+                                       "frac_of_peak": round(mall_gbs / HBM_PEAK_GBS, 4)},
+                     "ideal_us_at_peak": round(ideal_us, 3),
+                     "bound": "dispatch" if ideal_us < floor_us else "hbm"})
+    del pool_a, pool_b
+    return {"rows": rows, "launch_floor_us": round(floor_us, 2), "bytes_per_element": 12,
+            "peak_GBps": HBM_PEAK_GBS,
+            "timing": "HIP events around back-to-back launches on one stream (event span / "
+                      "launches): launch gaps are included, which is what makes the small sizes "
+                      "dispatch-bound",
+            "note": "context: the headline value is the 64 Mi line; hbm_resident cycles two "
+                    "1 GiB pools, mall_assisted repeats one slot"}
 
 
 def pmc_traffic():
@@ -492,20 +570,11 @@ def run_single(args):
     elif ceil:
         out["roofline"]["measured_ceiling"] = ceil
     del pairs
-    if args.sweep:
-        # config 2's size range: back-to-back launches, wall time per launch (what a caller
-        # issuing one segment after another sees: dispatch-bound below ~1 Mi elements)
-        sweep = []
-        for k in range(12, 27, 2):
-            nn = 1 << k
-            reps = 400 if nn <= (1 << 22) else 100
-            pp = make_pairs(torch, dev, nn, code, 1)
-            w, _, _, _ = time_chunk_sum(torch, L, dev, pp, code, reps, 20)
-            del pp
-            us = w / reps * 1e6
-            sweep.append({"elements": nn, "us_per_launch": round(us, 2),
-                          "GBps": round(12.0 * nn / (us * 1e-6) / 1e9, 1)})
-        out["sweep"] = sweep
+    if not args.no_sweep:
+        try:  # config 2's whole size range (context: the headline is the 64 Mi line above)
+            out["sweep"] = sweep_leg(torch, L, dev, code)
+        except Exception as e:
+            out["sweep"] = {"error": str(e)}
     if not args.no_host_path:
         try:  # row N2: the PCIe-inclusive host-buffer rate beside the HBM one (context only)
             out["host_path"] = host_path_leg()

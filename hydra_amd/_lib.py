@@ -43,6 +43,7 @@ EXPORTS = [  # every symbol include/hydra_hip.h declares
     "hydra_reduce_root", "hydra_reduce_root_plan", "hydra_reduce_root_simulate",
     "hydra_comm_profile", "hydra_comm_phases", "hydra_stream_wait_event", "hydra_device_peer_access",
     "hydra_host_trace", "hydra_host_trace_read", "hydra_device_link",
+    "hydra_test_set", "hydra_test_get",
 ]
 
 (ALGO_AUTO, ALGO_RING, ALGO_DIRECT, ALGO_RCCL, ALGO_A2A, ALGO_RING_OLD, ALGO_RING_CHUNKED,
@@ -230,6 +231,8 @@ def _declare(L) -> None:
     L.hydra_device_link.argtypes = [i, i, ctypes.POINTER(i), ctypes.POINTER(i), ctypes.POINTER(i)]
     L.hydra_comm_profile.argtypes = [vp, i]
     L.hydra_comm_phases.argtypes = [vp, ctypes.POINTER(CommPhases)]
+    L.hydra_test_set.argtypes = [i, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]
+    L.hydra_test_get.argtypes = [i, ctypes.POINTER(ctypes.c_int64)]
 
 
 def lib():
@@ -305,3 +308,20 @@ def device_links(device: int = 0) -> list:
 
 def set_variant(v: int) -> int:
     return lib().hydra_set_variant(v)
+
+
+# hydra_test_key_t (include/hydra_hip.h): test switches, 0 in production
+TEST_LOCAL_STAGE, TEST_RESIDENT_GEN_STRIDE, TEST_RESIDENT_REGRESSIONS = 1, 2, 3
+
+
+def test_set(key: int, value: int) -> int:
+    """hydra_test_set: sets a test switch, returns its previous value."""
+    prev = ctypes.c_int64()
+    check(lib().hydra_test_set(key, value, ctypes.byref(prev)))
+    return prev.value
+
+
+def test_get(key: int) -> int:
+    v = ctypes.c_int64()
+    check(lib().hydra_test_get(key, ctypes.byref(v)))
+    return v.value

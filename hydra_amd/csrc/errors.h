@@ -9,6 +9,9 @@ int ok();                                     // clears the thread's message, re
 int fail(int code, const std::string& msg);   // sets the thread's message, returns code
 int hip_fail(hipError_t e, const char* what);
 int current_variant();
+// hydra_test_set / hydra_test_get's values (hydra_hip.h), readable from every translation unit
+int64_t test_value(int key);
+void test_count(int key);  // a read-only counter key += 1
 }  // namespace hydra
 
 #define HIP_TRY(expr)                                           \

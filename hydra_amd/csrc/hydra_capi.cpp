@@ -46,6 +46,17 @@ int hip_fail(hipError_t e, const char* what) {
   return fail(HYDRA_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
 }
 int current_variant() { return g_variant.load(std::memory_order_relaxed); }
+
+namespace {
+constexpr int kTestKeys = 4;  // hydra_test_key_t values 1..3
+std::atomic<int64_t> g_test[kTestKeys] = {};
+}  // namespace
+int64_t test_value(int key) {
+  return key > 0 && key < kTestKeys ? g_test[key].load(std::memory_order_relaxed) : 0;
+}
+void test_count(int key) {
+  if (key > 0 && key < kTestKeys) g_test[key].fetch_add(1, std::memory_order_relaxed);
+}
 }  // namespace hydra
 
 using hydra::fail;
@@ -210,6 +221,22 @@ int hydra_device_check(int device) {
 
 int hydra_set_variant(int variant) { return g_variant.exchange(variant); }
 
+int hydra_test_set(int key, int64_t value, int64_t* prev) {
+  if (key != HYDRA_TEST_LOCAL_STAGE && key != HYDRA_TEST_RESIDENT_GEN_STRIDE)
+    return fail(HYDRA_ERR_INVALID, "hydra_test_set: unknown or read-only key " + std::to_string(key));
+  const int64_t old = hydra::g_test[key].exchange(value);
+  if (prev) *prev = old;
+  return ok();
+}
+
+int hydra_test_get(int key, int64_t* value) {
+  if (!value) return fail(HYDRA_ERR_INVALID, "null value");
+  if (key < HYDRA_TEST_LOCAL_STAGE || key > HYDRA_TEST_RESIDENT_REGRESSIONS)
+    return fail(HYDRA_ERR_INVALID, "hydra_test_get: unknown key " + std::to_string(key));
+  *value = hydra::test_value(key);
+  return ok();
+}
+
 int hydra_reduce(int op, int dtype, void* c, const void* a, const void* b, size_t n,
                  hydra_stream_t stream) {
   int rc = check_args(op, dtype, c, a, b, n);
@@ -338,11 +365,16 @@ struct Operand {
   hydra::HostWindows win;
   size_t lo[hydra::kMaxWindows] = {}, hi[hydra::kMaxWindows] = {};
   int n = 0;
+  // the window [i, j) lies in, or -1
+  int window_of(size_t i, size_t j) const {
+    for (int k = 0; k < n; k++)
+      if (lo[k] <= i && j <= hi[k]) return k;
+    return -1;
+  }
   // device address of element i if [i, j) lies in one window, else null
   char* dev(size_t i, size_t j, size_t es) const {
-    for (int k = 0; k < n; k++)
-      if (lo[k] <= i && j <= hi[k]) return win.w[k].dev + (base + i * es - win.w[k].lo);
-    return nullptr;
+    const int k = window_of(i, j);
+    return k >= 0 ? win.w[k].dev + (base + i * es - win.w[k].lo) : nullptr;
   }
 };
 
@@ -425,11 +457,17 @@ int hydra_reduce_host(hydra_ctx_t ctx, int op, int dtype, void* c, const void* a
   cut.erase(std::unique(cut.begin(), cut.end()), cut.end());
 
   const bool c_old_bits = dtype == HYDRA_FLOAT16 && c != a && c != b;  // store quirk: read c
-  bool stage_result = dtype != HYDRA_FLOAT16 && nbytes <= stage_result_max();
-  if (dtype != HYDRA_FLOAT16 && !stage_result)  // c in a small (cache-resident) registration
-    for (int k = 0; k < oc.n; k++)
-      stage_result = stage_result || (oc.win.w[k].kind == hydra::kMapRegister &&
-                                       oc.win.w[k].entry_bytes <= stage_result_reg_max());
+  const bool stage_result_all = dtype != HYDRA_FLOAT16 && nbytes <= stage_result_max();
+  // per interval: its result goes through the staging when the window holding that interval of
+  // c is a small (cache-resident) registration; a large registration or a caller mapping keeps
+  // the zero-copy write
+  auto stage_result_in = [&](size_t i, size_t j) {
+    if (dtype == HYDRA_FLOAT16) return false;
+    if (stage_result_all) return true;
+    const int k = oc.window_of(i, j);
+    return k >= 0 && oc.win.w[k].kind == hydra::kMapRegister &&
+           oc.win.w[k].entry_bytes <= stage_result_reg_max();
+  };
   // Rounds: a round is one batched call over at most kResidentSegs intervals and one staging
   // buffer's slots.  Round r is submitted once round r - 1 is done; its staged results go back
   // to c while round r runs, and the CPU fills the other buffer meanwhile.  Submitted to the
@@ -449,6 +487,12 @@ int hydra_reduce_host(hydra_ctx_t ctx, int op, int dtype, void* c, const void* a
     f();
     *acc += us_since(t0);
   };
+  struct Drain {  // an early return waits for the round in flight before the windows go
+    std::function<void()> f;
+    ~Drain() {
+      if (f) f();
+    }
+  } drain_;
   auto wait_round = [&](int k) -> int {
     const Clock::time_point t0 = tracing ? Clock::now() : Clock::time_point();
     struct Acc {
@@ -462,6 +506,9 @@ int hydra_reduce_host(hydra_ctx_t ctx, int op, int dtype, void* c, const void* a
     if (lease) {
       if (int r = hydra::resident_wait(lease, &poisoned)) {
         if (poisoned) guard_.k = 0;  // the grid may still touch them: they stay mapped
+        // the failed wait already stopped the instance (or poisoned the server): there is no
+        // round left to drain, so an early return must not wait for it a second time
+        drain_.f = nullptr;
         return r;
       }
     } else {
@@ -469,12 +516,6 @@ int hydra_reduce_host(hydra_ctx_t ctx, int op, int dtype, void* c, const void* a
     }
     return HYDRA_OK;
   };
-  struct Drain {  // an early return waits for the round in flight before the windows go
-    std::function<void()> f;
-    ~Drain() {
-      if (f) f();
-    }
-  } drain_;
   auto flush = [&]() -> int {  // submit the current buffer's round
     if (segs.empty() && outs[buf].empty()) return HYDRA_OK;
     const int other = buf ^ 1;
@@ -530,7 +571,7 @@ int hydra_reduce_host(hydra_ctx_t ctx, int op, int dtype, void* c, const void* a
       if (segs.size() == (size_t)hydra::kResidentSegs) {
         if ((rc = flush())) return rc;
       }
-      char* dc = stage_result ? nullptr : oc.dev(off, end, es);
+      char* dc = stage_result_in(off, end) ? nullptr : oc.dev(off, end, es);
       char* da = A->dev(off, end, es);
       char* db = B->dev(off, end, es);
       if (dc && da && db) {  // in place over PCIe

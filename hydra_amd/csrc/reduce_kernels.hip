@@ -20,6 +20,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <atomic>
 #include <type_traits>
 
 #include "errors.h"
@@ -472,18 +473,29 @@ __global__ __launch_bounds__(kBlock) void k_reduce_batch(const BatchArgs args) {
 // -------------------------------------------------------------------------------------------
 // launch
 // -------------------------------------------------------------------------------------------
-int g_cu_count = 0;
+// CUs of the current device (the launches go to the current device's streams), looked up once
+// per device; racing first calls store the same value (was one process-wide
+// value for whichever device asked first)
+constexpr int kCuDevices = 64;
+std::atomic<int> g_cu_count[kCuDevices] = {};
 
 int cu_count() {
-  if (!g_cu_count) {
-    int dev = 0, cus = 0;
-    if (hipGetDevice(&dev) == hipSuccess &&
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
-      g_cu_count = cus;
-    else
-      g_cu_count = 256;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0) dev = 0;
+  if (dev >= kCuDevices) {
+    int cus = 0;
+    return hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess
+               ? cus : 256;
   }
-  return g_cu_count;
+  int c = g_cu_count[dev].load(std::memory_order_relaxed);
+  if (!c) {
+    int cus = 0;
+    c = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+                cus > 0
+            ? cus : 256;
+    g_cu_count[dev].store(c, std::memory_order_relaxed);
+  }
+  return c;
 }
 
 struct Split {  // head / vector body / tail of one call, aligned on c

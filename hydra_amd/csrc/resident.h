@@ -79,7 +79,7 @@ struct ResJob {  // a call spread over workgroups 0 .. nwg-1 (device memory)
   ResDesc desc;
 };
 
-struct alignas(64) ResDev {  // device memory, zeroed at creation
+struct alignas(64) ResDev {  // device memory, zeroed before every launch (ensure_running)
   uint64_t pub;              // the last job published: tag | workgroups | job number (resident.hip)
   uint64_t exit_gen;
   alignas(64) uint64_t beat;  // workgroup 0's heartbeat: calls served by the running instance

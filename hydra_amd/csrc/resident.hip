@@ -10,8 +10,10 @@ namespace hydra {
 namespace {
 
 // The device word workgroup 0 publishes a job in: the instance's generation tag in the top 16
-// bits, the job's workgroup count in the next 12, the job number in the low 36.  A word another
-// instance left behind (its tag differs) never wakes this one's workers, and a worker learns
+// bits, the job's workgroup count in the next 12, the job number in the low 36.  The host zeroes
+// the device record before every launch (resident_host.cpp ensure_running), so no word another
+// instance left behind reaches this one's workers even when the 16-bit tag has wrapped; the tag
+// is a second guard on top of that.  A worker learns
 // from ONE load both which job is current and whether it takes part: it never pairs a job
 // number with another job's record (a worker delayed between two loads once could).
 constexpr int kTagShift = 48;

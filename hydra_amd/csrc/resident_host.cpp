@@ -39,6 +39,7 @@ struct ResidentLease {
   int slot;
   uint64_t seq;    // the slot's last sequence number rung
   uint64_t calls;  // calls submitted through this lease
+  uint64_t seen;   // the highest completion word a wait saw (a lower one later: a regression)
 };
 
 namespace {
@@ -211,15 +212,18 @@ int ensure_running(ResidentServer* v) {
   int prev = -1;
   (void)hipGetDevice(&prev);
   if (prev != v->device) (void)hipSetDevice(v->device);
-  hipError_t e = hipSuccess;
-  if (vol(v->h->err) != 0u) {
-    // the last instance left on an expired wait: its job counter may hold a partial count, so
-    // the device record starts over (ordered after that instance on the same stream)
-    e = hipMemsetAsync(v->d, 0, sizeof(ResDev), v->s);
-    vol(v->h->err) = 0u;
-  }
+  // Every instance starts from a zeroed device record, ordered after the last instance on the
+  // same stream: no job word, `finished` word or arrival count an earlier instance left behind
+  // can reach this one's workers, whatever its generation tag (the job word keeps 16 bits of the
+  // generation, which wraps after 65536 launches).  After an expired wait
+  // this also discards the partial arrival count that instance left.
+  hipError_t e = hipMemsetAsync(v->d, 0, sizeof(ResDev), v->s);
+  vol(v->h->err) = 0u;
+  // (test switch HYDRA_TEST_RESIDENT_GEN_STRIDE: wrap the tag on every launch)
+  const int64_t stride = test_value(HYDRA_TEST_RESIDENT_GEN_STRIDE);
+  v->gen += stride > 0 ? (uint64_t)stride : 1u;
   if (e == hipSuccess)
-    e = launch_resident(v->h_dev, v->d, ++v->gen, idle_ticks(), grace_ticks(), shape(), v->s);
+    e = launch_resident(v->h_dev, v->d, v->gen, idle_ticks(), grace_ticks(), shape(), v->s);
   if (prev >= 0 && prev != v->device) (void)hipSetDevice(prev);
   if (e != hipSuccess) {
     vol(v->h->alive) = 0u;
@@ -254,7 +258,7 @@ int resident_lease(int device, ResidentLease** out) {
     if (v->leased & (1u << k)) continue;
     v->leased |= 1u << k;
     // numbering continues from the slot's last doorbell (a slot is reused by later contexts)
-    *out = new ResidentLease{v, k, vol(v->h->slot[k].doorbell), 0};
+    *out = new ResidentLease{v, k, vol(v->h->slot[k].doorbell), 0, vol(v->h->slot[k].done)};
     return HYDRA_OK;
   }
   return HYDRA_OK;  // every slot leased: this context launches
@@ -327,6 +331,7 @@ int resident_wait(ResidentLease* l, bool* poisoned) {
     }
     if (stop_instance(v, std::chrono::seconds(2))) {
       done = seq;
+      l->seen = std::max(l->seen, seq);
     } else {
       v->poisoned.store(true);
       if (poisoned) *poisoned = true;
@@ -339,7 +344,10 @@ int resident_wait(ResidentLease* l, bool* poisoned) {
     return fail(code, msg);
   };
   for (uint32_t spins = 0;; spins++) {
-    if (done >= seq) break;
+    const uint64_t now_done = done;
+    if (now_done < l->seen) test_count(HYDRA_TEST_RESIDENT_REGRESSIONS);  // (never, by design)
+    l->seen = std::max(l->seen, now_done);
+    if (now_done >= seq) break;
     if (vol(v->h->alive) == 0u && done < seq) {  // it left without serving us: a new instance
       if (vol(v->h->err))  // (it left on an expired wait: report that, do not relaunch)
         return give_up(HYDRA_ERR_HIP, "resident reducer: a wait inside the grid expired");

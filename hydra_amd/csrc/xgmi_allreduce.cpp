@@ -259,7 +259,11 @@ int prof_begin(hydra_comm* c, hipStream_t user_st) {
   if (!c->prof_active) return HYDRA_OK;
   hydra_comm::ProfCall call{};
   HIP_TRY(prof_event(c, &call.t0));
-  HIP_TRY(hipEventRecord(call.t0, user_st));
+  if (hipError_t e = hipEventRecord(call.t0, user_st); e != hipSuccess) {
+    c->prof_pool.push_back(call.t0);  // never recorded: back to the pool
+    c->prof_active = false;
+    return hydra::hip_fail(e, "hipEventRecord (profiled call start)");
+  }
   c->prof_calls.push_back(std::move(call));
   return HYDRA_OK;
 }
@@ -277,14 +281,32 @@ struct ProfOp {
     r.sent = sent;
     r.recv = recv;
     r.hbm = hbm;
-    on = prof_event(c, &r.s) == hipSuccess && hipEventRecord(r.s, st) == hipSuccess;
+    if (prof_event(c, &r.s) != hipSuccess) return;
+    on = hipEventRecord(r.s, st) == hipSuccess;
+    if (!on) c->prof_pool.push_back(r.s);
   }
+  // an op that returned before end() (a failed enqueue): its start event is not in any profiled
+  // call, so it goes back to the pool rather than leaking
+  ~ProfOp() {
+    if (on) c->prof_pool.push_back(r.s);
+  }
+  ProfOp(const ProfOp&) = delete;
+  ProfOp& operator=(const ProfOp&) = delete;
   hipError_t end() {
     if (!on) return hipSuccess;
     on = false;
     hipError_t e = prof_event(c, &r.e);
-    if (e == hipSuccess) e = hipEventRecord(r.e, st);
-    if (e == hipSuccess) c->prof_calls.back().ops.push_back(r);
+    if (e != hipSuccess) {
+      c->prof_pool.push_back(r.s);
+      return e;
+    }
+    e = hipEventRecord(r.e, st);
+    if (e == hipSuccess) {
+      c->prof_calls.back().ops.push_back(r);
+    } else {
+      c->prof_pool.push_back(r.s);
+      c->prof_pool.push_back(r.e);
+    }
     return e;
   }
 };
@@ -528,13 +550,29 @@ int hydra_comm_info(hydra_comm_t c, int* nranks, int* rank, int* device) {
 int hydra_comm_profile(hydra_comm_t c, int enable) {
   if (!c) return fail(HYDRA_ERR_INVALID, "null comm");
   hydra::DeviceScope ds(c->device);
-  if (int rc = prof_collect(c)) return rc;  // recycle what an earlier session left
+  // recycle what an earlier session left; the switch applies whatever that gives:
+  // calls whose events cannot be read are dropped -- after a drain of the communicator's
+  // streams, nothing pending records them any more -- so profiling can always be turned off
+  const int rc = prof_collect(c);
+  if (rc) {
+    (void)hipStreamSynchronize(c->cs);
+    (void)hipStreamSynchronize(c->ks);
+    for (auto& call : c->prof_calls) {
+      (void)hipEventDestroy(call.t0);
+      for (auto& r : call.ops) {
+        (void)hipEventDestroy(r.s);
+        (void)hipEventDestroy(r.e);
+      }
+    }
+    c->prof_calls.clear();
+  }
   c->profile = enable != 0;
+  c->prof_active = false;
   if (c->profile) {
     c->prof = hydra_comm_phases_t{};
     c->prof_peers.clear();
   }
-  return ok();
+  return rc ? rc : ok();  // (the collection error is still reported, with the switch applied)
 }
 
 int hydra_comm_phases(hydra_comm_t c, hydra_comm_phases_t* out) {

@@ -438,15 +438,29 @@ def phase_report(ph: dict, P: int, n: int, esize: int) -> dict:
     return out
 
 
-def bench_allreduce(args, dev, make_comm=None, sync=None, cpu_baseline=None) -> dict:
+def _peer_mode(args) -> str:
+    """bench.py --peer: "auto" (default: the peer leg runs when every peer GPU of this node is
+    reached over xGMI with peer access), "on" (always: e.g. the one-GPU rehearsal, where the
+    ranks share a GPU) or "off".  (A bool from older callers: True = on, False = off.)"""
+    v = getattr(args, "peer", "auto")
+    if v is True:
+        return "on"
+    if v is False or v is None:
+        return "off"
+    return str(v)
+
+
+def bench_allreduce(args, dev, make_comm=None, sync=None, cpu_baseline=None,
+                    make_peer=None) -> dict:
     """bench.py --gpus N (N > 1): BASELINE config 4 (fp32 64 Mi per rank) on this rank.
 
     make_comm() -> a communicator with XgmiComm's allreduce_ / reduce_ / apipe_allreduce_ /
     close (default: an RCCL XgmiComm over this rank's GPU, its unique id broadcast over the
-    process group); sync() waits for this rank's enqueued work (default: the device).  The two
+    process group); sync() waits for this rank's enqueued work (default: the device);
+    make_peer() -> the peer-access group of the last leg (default: hydra_amd.peer.PeerComm).  The
     hooks let tests/test_bench_gloo.py run this whole orchestration -- parity self-checks,
-    autotune, timed region, context legs, JSON line -- at world size 2 and 3 on the CPU, with
-    the same plans executed over gloo p2p."""
+    autotune, timed region, context legs, the peer leg, JSON line -- at world size 2 to 8 on the
+    CPU, with the same plans executed over gloo p2p."""
     import torch
     import torch.distributed as dist
 
@@ -492,16 +506,16 @@ def bench_allreduce(args, dev, make_comm=None, sync=None, cpu_baseline=None) -> 
         comm_seen["links_from_device"] = f"n/a: {e}"
     extra_legs = bool(getattr(args, "extra_legs", False))
     cpu_base = None
-    from .peer import PeerComm
+    if make_peer is None:
+        def make_peer():
+            from .peer import PeerComm
 
-    pg = {"peer": None, "err": None}  # IPC-mapped buckets, one kernel per allreduce
-    if getattr(args, "peer", False):
-        try:  # (hydra_amd.peer; setup fails collectively, so every rank takes the same branch)
-            pg["peer"] = PeerComm(rank, world, dev.index)
-        except HydraError as e:
-            pg["err"] = str(e)
-    else:  # opt-in until the cross-GPU IPC path has run on an xGMI node
-        pg["err"] = "disabled (bench.py --peer enables the peer-access schedules)"
+            return PeerComm(rank, world, dev.index)
+
+    # IPC-mapped buckets, one kernel per allreduce: set up in the LAST leg only (7 below), after
+    # every other field of the line is measured
+    pg = {"peer": None, "err": "not set up yet"}
+    peer_leg = {}
     n = args.elements
     algo = getattr(args, "algo", "auto")
 
@@ -515,18 +529,6 @@ def bench_allreduce(args, dev, make_comm=None, sync=None, cpu_baseline=None) -> 
         else:
             comm.allreduce_(t, algo=a, chunk_bytes=ch, **kw)
 
-    def peer_register(t):
-        if pg["peer"] is not None:
-            try:
-                pg["peer"].register(t)
-            except HydraError as e:  # collective failure: drop the peer algorithms
-                pg["peer"].close()
-                pg["peer"], pg["err"] = None, str(e)
-
-    def peer_ok():  # collective; a barrier timeout poisons the group: report, never hang
-        p = pg["peer"]
-        return max_over_ranks(float(p.error()) if p is not None else 1.0, dev) == 0.0
-
     try:
         # 1) parity self-check on fold-order-sensitive inputs (small bucket), every algorithm
         pn = 1 << 20  # equal blocks at P = 2..8, so A2A is checked too
@@ -534,9 +536,7 @@ def bench_allreduce(args, dev, make_comm=None, sync=None, cpu_baseline=None) -> 
         exp = expected_fold_f32(xs)
         parity = {}
         tp = torch.empty(pn, dtype=torch.float32, device=dev)
-        peer_register(tp)
-        peer_algos = ("peer2", "peer1") if getattr(args, "peer", False) else ()
-        for a in ("direct", "ring", "a2a") + peer_algos:
+        for a in ("direct", "ring", "a2a"):
             tp.copy_(torch.from_numpy(xs[rank]))
             try:
                 run(a, tp)
@@ -546,15 +546,11 @@ def bench_allreduce(args, dev, make_comm=None, sync=None, cpu_baseline=None) -> 
             sync()
             ok = bool(np.array_equal(tp.cpu().numpy().view(np.uint32), exp.view(np.uint32)))
             ok_all = max_over_ranks(0.0 if ok else 1.0, dev) == 0.0
-            if a.startswith("peer") and not peer_ok():
-                parity[a] = "barrier timeout"
-                continue
             parity[a] = "bit-exact" if ok_all else "MISMATCH"
         # 2) exactness at full size: integer-valued inputs whose sums are exact in fp32
         j = np.arange(n, dtype=np.int64)
         x0 = torch.from_numpy(((j % 1024) * (rank + 1)).astype(np.float32)).to(dev)
         x = x0.clone()
-        peer_register(x)
         full_exp = torch.from_numpy(((j % 1024) * (world * (world + 1) // 2))
                                     .astype(np.float32)).to(dev)
         def full_exact(a, ch=0):
@@ -596,8 +592,9 @@ def bench_allreduce(args, dev, make_comm=None, sync=None, cpu_baseline=None) -> 
             state["result"] = lambda: _bench_result(
                 n, world, args, "direct", 0, dict(tuning), parity, full_ok, ms_safe, lat_safe,
                 {}, None, comm_seen)
-        # 3) pick the algorithm: "auto" = the fastest bit-exact schedule on this node
-        #    (DIRECT / A2A / RING / PEER two-shot), chosen on a few untimed steps
+        # 3) pick the algorithm: "auto" = the fastest bit-exact RCCL schedule on this node
+        #    (DIRECT / A2A / RING), chosen on a few untimed steps; the peer-access kernel is
+        #    checked and timed last (7) and replaces this headline only if it is faster
         chosen, chunk = algo, 0
         stall = float(os.environ.get("HYDRA_BENCH_STALL_AUTOTUNE", "0"))
         if stall > 0:  # test hook: an autotune candidate that hangs
@@ -605,8 +602,7 @@ def bench_allreduce(args, dev, make_comm=None, sync=None, cpu_baseline=None) -> 
         if algo == "auto":
             best = None
             for a, ch in (("direct", 1 << 20), ("direct", 4 << 20), ("direct", 16 << 20),
-                          ("direct", 64 << 20), ("a2a", 0), ("ring", 4 << 20), ("peer2", 0),
-                          ("peer2", 256), ("peer2", 128)):
+                          ("direct", 64 << 20), ("a2a", 0), ("ring", 4 << 20)):
                 if parity.get(a) != "bit-exact":
                     continue  # only schedules that reproduced the reference are eligible
                 try:
@@ -616,10 +612,7 @@ def bench_allreduce(args, dev, make_comm=None, sync=None, cpu_baseline=None) -> 
                     tw = max_over_ranks(timed_steps(tstep, 5, 2, sync, dist.barrier), dev) / 5
                 except _lib.HydraError:
                     continue
-                if a.startswith("peer") and not peer_ok():
-                    continue
-                tuning[f"{a}/{ch}wg" if a in _lib.PEER_ALGOS else f"{a}/{ch >> 20}MiB"] = \
-                    round(tw * 1e3, 4)
+                tuning[f"{a}/{ch >> 20}MiB"] = round(tw * 1e3, 4)
                 if best is None or tw < best[0]:
                     best = (tw, a, ch)
             chosen, chunk = (best[1], best[2]) if best is not None else ("direct", 0)
@@ -662,7 +655,8 @@ def bench_allreduce(args, dev, make_comm=None, sync=None, cpu_baseline=None) -> 
 
         def _result(ms_, lat_, others_, c5_):
             return _bench_result(n, world, args, chosen, chunk, tuning, parity, full_ok, ms_,
-                                 lat_, dict(others_), c5_, comm_seen, cpu_base, phases)
+                                 lat_, dict(others_), c5_, comm_seen, cpu_base, phases,
+                                 dict(peer_leg))
 
         # the reference's own ring on this host's cores (bench.py's baseline leg: rank 0 only,
         # outside every timed region; the other ranks wait at the barrier)
@@ -747,7 +741,7 @@ def bench_allreduce(args, dev, make_comm=None, sync=None, cpu_baseline=None) -> 
                          expected_reduce_f32(xs) if rank == world - 1 else None)
         k = max(5, args.steps // 4)
         # context: RCCL's own allreduce and its own reduce-scatter + all-gather
-        legs = ("ring", "direct", "a2a", "rccl", "rccl_rs_ag") + peer_algos
+        legs = ("ring", "direct", "a2a", "rccl", "rccl_rs_ag")
         if extra_legs:
             legs += ("ring_old", "ring_chunked", "bcube", "halving_doubling")
         for a in legs:
@@ -773,15 +767,10 @@ def bench_allreduce(args, dev, make_comm=None, sync=None, cpu_baseline=None) -> 
             xb = torch.from_numpy(synth.bf16_bits(base.astype(np.float32)).view(np.int16)) \
                 .to(dev).repeat(n5 >> 20)
 
-            c5_algo = chosen if chosen in ("direct", "a2a", "peer2") else "direct"
-            if c5_algo == "peer2":
-                if peer_ok():
-                    peer_register(xb)
-                if pg["peer"] is None or not peer_ok():
-                    c5_algo = "direct"
+            c5_algo = chosen if chosen in ("direct", "a2a") else "direct"
 
             def bstep():
-                run(c5_algo, xb, chunk if c5_algo in ("direct", "peer2") else 0,
+                run(c5_algo, xb, chunk if c5_algo == "direct" else 0,
                     dtype_code=_lib.BFLOAT16, flags=_lib.ACC_F32)
 
             k5 = max(5, args.steps // 10)
@@ -804,8 +793,7 @@ def bench_allreduce(args, dev, make_comm=None, sync=None, cpu_baseline=None) -> 
                 full_ok["config5_bf16_acc32"] = max_over_ranks(0.0 if good else 1.0, dev) == 0.0
                 r5 = context_leg(bstep, k5, warm=2)
                 if not isinstance(r5, str):
-                    profile_step("config5", c5_algo, xb,
-                                 chunk if c5_algo in ("direct", "peer2") else 0, 2,
+                    profile_step("config5", c5_algo, xb, chunk if c5_algo == "direct" else 0, 2,
                                  dtype_code=_lib.BFLOAT16, flags=_lib.ACC_F32)
                 if isinstance(r5, str):
                     c5 = {"elements": n5, "algo": c5_algo, "error": r5}
@@ -842,6 +830,25 @@ def bench_allreduce(args, dev, make_comm=None, sync=None, cpu_baseline=None) -> 
             context_leg(lambda: comm.apipe_allreduce_(rail2, x, algo="direct"), k,
                         wait=rails_wait))
         state["result"] = lambda: _result(ms, lat_ms, others, c5)
+
+        # 7) the reduce-on-read schedule (precedent cuda_collectives_native.h:
+        #    63-120): ONE gfx950 kernel per allreduce reads the peers' IPC-mapped blocks over
+        #    xGMI and folds them in the reference order.  On by default when every peer GPU is
+        #    reached over xGMI with peer access; last, so every field above is already measured.
+        #    Its barriers are bounded on the device (a peer that never arrives ends the kernel
+        #    with an error word, hydra_peer_error) and every step's outcome is agreed over the
+        #    ranks: a failure becomes an error entry of this leg, never a failed line.
+        peer_leg.update(_peer_eligibility(args, comm_seen, world, dev))
+        if peer_leg["enabled"]:
+            pr = _peer_leg(make_peer, pg, run, measure, sync, dev, rank, world, xs, exp, x, x0,
+                           full_exp, tp, peer_leg)
+            peer_leg["headline_ms"] = round(ms, 4)
+            peer_leg["promoted"] = bool(pr is not None and pr[2] < ms)
+            if peer_leg["promoted"]:  # bit-exact at full size and faster: the new headline
+                others[chosen] = round(ms, 4)
+                chosen, chunk, ms, lat_ms = pr
+                full_ok[chosen] = True
+        state["result"] = lambda: _result(ms, lat_ms, others, c5)
     finally:
         errs = []
         for closer in ((pg["peer"].close if pg["peer"] is not None else None), comm.close,
@@ -858,8 +865,187 @@ def bench_allreduce(args, dev, make_comm=None, sync=None, cpu_baseline=None) -> 
     return _result(ms, lat_ms, others, c5)
 
 
+def _peer_eligibility(args, comm_seen, world, dev) -> dict:
+    """Whether the peer leg runs on this node, agreed over the ranks: --peer on / off, or (auto)
+    every other rank's GPU reached from this one over xGMI with peer access
+    (rccl_comm.links_from_device: hydra_device_link)."""
+    mode = _peer_mode(args)
+    if mode == "off":
+        return {"enabled": False, "mode": mode, "reason": "disabled (--peer off)"}
+    if mode == "on":
+        return {"enabled": True, "mode": mode, "reason": "forced (--peer on)"}
+    links = comm_seen.get("links_from_device")
+    reason = None
+    if world < 2:
+        reason = "one rank: no peer to read from"
+    elif not isinstance(links, list) or getattr(dev, "type", "") != "cuda":
+        reason = "no GPU peer links visible to this process"
+    else:
+        mine = [lk for lk in links if lk.get("peer", -1) < world]
+        if len(mine) < world - 1:
+            reason = (f"this process sees {len(links) + 1} GPU(s) for {world} ranks (ranks share "
+                      "a GPU: no xGMI between them)")
+        elif not all(lk.get("link") == "xgmi" and lk.get("peer_access") for lk in mine):
+            reason = "not every peer GPU is reached over xGMI with peer access: " + \
+                     ", ".join(f"{lk.get('peer')}:{lk.get('link')}/"
+                               f"{'peer' if lk.get('peer_access') else 'no-peer'}" for lk in mine)
+    bad = max_over_ranks(1.0 if reason else 0.0, dev) > 0
+    if not bad:
+        return {"enabled": True, "mode": mode,
+                "reason": "every peer GPU over xGMI with peer access (hydra_device_link)"}
+    return {"enabled": False, "mode": mode,
+            "reason": f"skipped: {reason or 'another rank has no xGMI peer access'}"}
+
+
+def _peer_leg(make_peer, pg, run, measure, sync, dev, rank, world, xs, exp, x, x0, full_exp, tp,
+              leg):
+    """The peer leg's steps, each agreed over the ranks before the next: set up the IPC group,
+    register the two buckets, parity of both schedules on the fold-order stress bucket, exactness
+    at full size, a workgroup-count autotune, the timed region (bench.py's contract: exactly
+    `steps` allreduces, barrier + sync on both sides, max over ranks) and one event-timed call as
+    its phase entry.  Fills `leg`; returns (algo, workgroups, ms, latency) when the schedule is
+    bit-exact and faster than the RCCL headline (the caller promotes it), else None."""
+    import torch
+    import torch.distributed as dist
+
+    def agreed(err):
+        return max_over_ranks(1.0 if err else 0.0, dev) == 0.0
+
+    def peer_ok():
+        p = pg["peer"]
+        return max_over_ranks(float(p.error()) if p is not None else 1.0, dev) == 0.0
+
+    err = None
+    try:
+        pg["peer"] = make_peer()  # collective; fails on every rank together
+    except HydraError as e:
+        err = str(e)
+    if not agreed(err):
+        pg["peer"] = None
+        leg["error"] = f"setup: {err or 'another rank failed'}"
+        return None
+    try:
+        for t in (tp, x):
+            try:
+                pg["peer"].register(t)
+            except HydraError as e:
+                err = str(e)
+            if not agreed(err):
+                leg["error"] = f"register: {err or 'another rank failed'}"
+                return None
+        par = {}
+        for a in ("peer2", "peer1"):
+            ok = False
+            try:
+                tp.copy_(torch.from_numpy(xs[rank]))
+                run(a, tp)
+                sync()
+                ok = bool(np.array_equal(tp.cpu().numpy().view(np.uint32), exp.view(np.uint32)))
+            except HydraError as e:
+                err = str(e)
+            if not agreed(err) or not peer_ok():
+                par[a] = f"n/a: {err or 'a barrier expired or another rank failed'}"
+                err = None
+                continue
+            par[a] = "bit-exact" if max_over_ranks(0.0 if ok else 1.0, dev) == 0.0 else "MISMATCH"
+        leg["parity_fold_order_1M"] = par
+        if par.get("peer2") != "bit-exact":
+            leg["error"] = "peer2 did not reproduce the reference bits; not timed"
+            return None
+        good = False
+        try:
+            x.copy_(x0)
+            run("peer2", x)
+            sync()
+            good = bool(torch.equal(x, full_exp))
+        except HydraError as e:
+            err = str(e)
+        if not agreed(err) or not peer_ok():
+            leg["error"] = f"full size: {err or 'a barrier expired or another rank failed'}"
+            return None
+        leg["full_size_exact"] = max_over_ranks(0.0 if good else 1.0, dev) == 0.0
+        if not leg["full_size_exact"]:
+            return None
+        tune = {}
+        for wg in (0, 256, 128):  # 0: derived from the bucket
+            tw = None
+            try:
+                def tstep(wg=wg):
+                    run("peer2", x, wg)
+
+                tw = max_over_ranks(timed_steps(tstep, 5, 2, sync, dist.barrier), dev) / 5
+            except HydraError as e:
+                err = str(e)
+            if not agreed(err) or not peer_ok():
+                leg["error"] = f"autotune: {err or 'a barrier expired or another rank failed'}"
+                return None
+            tune[f"peer2/{wg}wg"] = round(tw * 1e3, 4)
+        leg["autotune_ms"] = tune
+        wg = int(min(tune, key=tune.get).split("/")[1][:-2])
+        try:
+            ms_p, lat_p = measure("peer2", wg)
+        except HydraError as e:
+            err = str(e)
+        if not agreed(err) or not peer_ok():
+            leg["error"] = f"timed region: {err or 'a barrier expired or another rank failed'}"
+            return None
+        leg.update(algo="peer2", workgroups=wg, ms_per_step=round(ms_p, 4), latency_ms=lat_p)
+        leg["phases"] = _peer_phases(run, sync, dev, x, wg, world)
+        return "peer2", wg, ms_p, lat_p
+    finally:
+        p, pg["peer"] = pg["peer"], None
+        if p is not None:
+            try:
+                p.close()
+            except HydraError as e:  # a teardown failure is reported, after every rank closed
+                leg.setdefault("error", f"teardown: {e}")
+
+
+def _peer_phases(run, sync, dev, x, wg, world) -> dict:
+    """One event-timed peer allreduce (untimed otherwise): the kernel IS both phases -- it reads
+    the peers' blocks over xGMI (link) and folds them as they arrive (fold) -- so the entry gives
+    the one kernel's time against both rooflines: per-rank link bytes 2(P-1)/P x n x E (the
+    owner block's P-1 remote reads + the P-1 finished blocks pulled back) over P-1 links, and
+    the fused sum's algorithmic HBM bytes (P-1)/P x n x 3E."""
+    import torch
+
+    n, esize = x.numel(), x.element_size()
+    ms = None
+    if getattr(dev, "type", "") == "cuda":
+        s = torch.cuda.current_stream(dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        sync()
+        e0.record(s)
+        run("peer2", x, wg)
+        e1.record(s)
+        sync()
+        ms = max_over_ranks(e0.elapsed_time(e1), dev)
+    else:  # (the CPU rehearsal: wall time of one synchronous call)
+        sync()
+        t0 = time.perf_counter()
+        run("peer2", x, wg)
+        sync()
+        ms = max_over_ranks((time.perf_counter() - t0) * 1e3, dev)
+    link_bytes = 2 * (world - 1) / world * n * esize
+    fused = (world - 1) / world * n * 3 * esize
+    links = max(1, world - 1)
+    per_link = link_bytes / links / (ms * 1e-3) / 1e9 if ms > 0 else None
+    kern = fused / (ms * 1e-3) / 1e9 if ms > 0 else None
+    return {"calls": 1, "kernel_ms": round(ms, 4), "link_ms": round(ms, 4),
+            "fold_ms": round(ms, 4), "span_ms": round(ms, 4), "overlap_ms": round(ms, 4),
+            "note": "one kernel: link reads and folds overlap completely (link = fold = span)",
+            "link": {"algorithmic_bytes": int(link_bytes), "peers": links,
+                     "per_link_GBps": _sig(per_link) if per_link else None,
+                     "frac_of_link": _sig(per_link / XGMI_LINK_GBS) if per_link else None,
+                     "link_peak_GBps": XGMI_LINK_GBS},
+            "fold": {"fused_sum_bytes": int(fused),
+                     "kernel_GBps": _sig(kern) if kern else None,
+                     "frac_of_hbm": _sig(kern / HBM_PEAK_GBS) if kern else None,
+                     "hbm_peak_GBps": HBM_PEAK_GBS}}
+
+
 def _bench_result(n, world, args, chosen, chunk, tuning, parity, full_ok, ms, lat_ms, others,
-                  c5, comm_seen=None, cpu_base=None, phases=None) -> dict:
+                  c5, comm_seen=None, cpu_base=None, phases=None, peer_leg=None) -> dict:
     """The N>1 bench JSON line (bench_allreduce; also printed by its watchdog once the headline
     is measured)."""
     bucket = 4.0 * n
@@ -908,4 +1094,5 @@ def _bench_result(n, world, args, chosen, chunk, tuning, parity, full_ok, ms, la
         "parity": {"fold_order_1M": parity, "full_size_exact": full_ok},
         "rccl_comm": comm_seen,
         "cpu_baseline": cpu_base,
+        "peer_leg": peer_leg or {"enabled": False, "reason": "not reached"},
     }

@@ -64,3 +64,39 @@ def bf16_bits(x: np.ndarray) -> np.ndarray:
 
 def bf16_to_f32(h: np.ndarray) -> np.ndarray:
     return (h.astype(np.uint32) << np.uint32(16)).view(np.float32)
+
+
+# ---- order-sensitive values at arbitrary element indices (numpy or torch, any device) ----------
+_MASK32 = 0xFFFFFFFF
+
+
+def _mul32(h, c: int):
+    """(h * c) mod 2^32 for 0 <= h < 2^32 in int64 arithmetic: no partial product reaches 2^49,
+    so numpy and torch (CPU or GPU) give the same bits with no signed overflow."""
+    return (h * (c & 0xFFFF) + (((h * (c >> 16)) & 0xFFFF) << 16)) & _MASK32
+
+
+def _fmix32(h):
+    """murmur3's 32-bit finaliser."""
+    h = h ^ (h >> 16)
+    h = _mul32(h, 0x85EBCA6B)
+    h = h ^ (h >> 13)
+    h = _mul32(h, 0xC2B2AE35)
+    return h ^ (h >> 16)
+
+
+def stress_at(P: int, rank: int, idx, seed: int = 77):
+    """stress_f32's distribution -- uniform[-1, 1) with 24 random mantissa bits, times
+    2^(3r mod 17) -- at element indices `idx` (an int64 numpy array or torch tensor): the same
+    fp32 bits from numpy and from torch on any device, so a full-size bucket is generated on the
+    GPU and any sample of it re-derived on the CPU (BASELINE configs 4/5 at full size)."""
+    s = (seed * 1000003 + P * 1009 + rank * 7919) & _MASK32
+    h = _fmix32((_mul32(idx & _MASK32, 0x9E3779B1) + s) & _MASK32)
+    m = h >> 8  # 24 bits
+    scale = float(2.0 ** ((3 * rank) % 17))
+    if isinstance(idx, np.ndarray):
+        f = m.astype(np.float32) * np.float32(2.0 ** -23) - np.float32(1.0)
+        return f * np.float32(scale)
+    import torch
+
+    return (m.to(torch.float32) * (2.0 ** -23) - 1.0) * scale

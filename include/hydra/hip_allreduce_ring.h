@@ -145,12 +145,13 @@ class LocalReduce {
   }
   void init(std::vector<LocalStep> steps, const std::vector<int>& dev, size_t bytes) {
     steps_ = std::move(steps);
-    // test hook: HYDRA_TEST_LOCAL_STAGE=1 stages every step as if its two pointers were on
-    // devices without peer access, so the one-GPU box runs the cross-device staging branch
-    // (copy to a buffer on the destination's device, event waits) with real kernels
-    if (const char* v = std::getenv("HYDRA_TEST_LOCAL_STAGE"))
-      if (v[0] == '1')
-        for (LocalStep& s : steps_) s.staged = true;
+    // test switch HYDRA_TEST_LOCAL_STAGE (hydra_test_set): every step staged as if its two
+    // pointers were on devices without peer access, so the one-GPU box runs the cross-device
+    // staging branch (copy to a buffer on the destination's device, event waits) with real
+    // kernels
+    int64_t stage_all = 0;
+    if (hydra_test_get(HYDRA_TEST_LOCAL_STAGE, &stage_all) == HYDRA_OK && stage_all == 1)
+      for (LocalStep& s : steps_) s.staged = true;
     ev_.assign(dev.size(), nullptr);
     for (size_t i = 0; i < dev.size(); i++) enforce(hydra_event_create_on(dev[i], &ev_[i]));
     stage_.clear();

@@ -132,6 +132,26 @@ int hydra_fold(int op, int dtype, int flags, void* dst, const void* const* srcs,
 /* Kernel variant selection for measurement (0 = tuned default).  Returns the previous value. */
 int hydra_set_variant(int variant);
 
+/* Test switches: process-wide values the library reads at the point they apply, so tests can
+ * drive branches a one-GPU box never takes on its own.  Every switch is 0 in production (the
+ * library never sets one itself).  hydra_test_set returns HYDRA_ERR_INVALID for an unknown or
+ * read-only key; *prev (if given) receives the old value.
+ *   HYDRA_TEST_LOCAL_STAGE         1: HipAllreduceRing's local steps are staged as if their two
+ *                                  pointers were on devices without peer access (the
+ *                                  cross-device staging branch on one GPU)
+ *   HYDRA_TEST_RESIDENT_GEN_STRIDE >0: each resident-reducer launch advances the generation by
+ *                                  this much instead of 1 (65536 wraps the job word's 16-bit
+ *                                  generation tag on every launch)
+ *   HYDRA_TEST_RESIDENT_REGRESSIONS  (read-only) completion words the resident reducer's waits
+ *                                  saw move backwards, over every slot of every device */
+typedef enum {
+  HYDRA_TEST_LOCAL_STAGE = 1,
+  HYDRA_TEST_RESIDENT_GEN_STRIDE = 2,
+  HYDRA_TEST_RESIDENT_REGRESSIONS = 3
+} hydra_test_key_t;
+int hydra_test_set(int key, int64_t value, int64_t* prev);
+int hydra_test_get(int key, int64_t* value);
+
 /* ---- host-resident reduction --------------------------------------------------------------
  * Same contract on HOST buffers, synchronous like gloo::sum<T>: the kernel reads and writes the
  * mapped parts of a, b and c in place over PCIe (see below) and the rest through the context's

@@ -14,6 +14,7 @@
 #   bench[_X]    python bench.py (BENCH_ARGS), JSON line -> bench[_X].json (bench_2: a second run)
 #   rehearseN    the N>1 bench at world size N on this one GPU (HYDRA_BENCH_SHARED_GPU=1: real
 #                RCCL ranks over loopback sockets), 4 Mi fp32 / 16 Mi bf16 -> rehearse_nN.json
+#                (REHEARSE_ARGS: extra bench.py flags, e.g. "--peer on" for the peer leg)
 #   py:NAME      python scripts/NAME.py $PY_ARGS (a measurement script) -> NAME.log
 #   pyprof:NAME  scripts/NAME.py under rocprofv3: a kernel trace, then separate FETCH_SIZE and
 #                WRITE_SIZE passes -> NAME_{kt,fetch,write}/ (e.g. pyprof:fold_pmc)
@@ -60,15 +61,15 @@ for s in "$@"; do
       rc=$?; tail -1 "$OUT/smoke.log";;
     prof)
       step rocprof_kt 600 rocprofv3 --kernel-trace --stats --output-format csv \
-          -d "$OUT/prof_kt" -o run -- python3 "$ROOT/bench.py" --steps 100 --warmup 10 --no-cpu-baseline --no-host-path
+          -d "$OUT/prof_kt" -o run -- python3 "$ROOT/bench.py" --steps 100 --warmup 10 --no-cpu-baseline --no-host-path --no-sweep
       rc=$?
       python3 scripts/headline_from_trace.py "$OUT/prof_kt/run_kernel_trace.csv" 10 100 "$TAG" \
           > "$OUT/headline_from_trace.json" 2>&1 || true
       [ $rc -eq 0 ] && step rocprof_fetch 300 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv \
-          -d "$OUT/prof_fetch" -o run -- python3 "$ROOT/bench.py" --steps 20 --warmup 2 --no-cpu-baseline --no-host-path
+          -d "$OUT/prof_fetch" -o run -- python3 "$ROOT/bench.py" --steps 20 --warmup 2 --no-cpu-baseline --no-host-path --no-sweep
       rc=$?
       [ $rc -eq 0 ] && step rocprof_write 300 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --output-format csv \
-          -d "$OUT/prof_write" -o run -- python3 "$ROOT/bench.py" --steps 20 --warmup 2 --no-cpu-baseline --no-host-path
+          -d "$OUT/prof_write" -o run -- python3 "$ROOT/bench.py" --steps 20 --warmup 2 --no-cpu-baseline --no-host-path --no-sweep
       rc=$?
       python3 scripts/pmc_summary.py "$OUT" "${ROUND:-r04}" > "$OUT/pmc_summary.json" 2>&1 || true;;
     bench|bench_*)
@@ -80,7 +81,7 @@ for s in "$@"; do
       step "rehearse_n$n" 600 env HYDRA_BENCH_SHARED_GPU=1 python -m torch.distributed.run --nnodes=1 \
           --nproc-per-node "$n" --master-addr 127.0.0.1 --master-port $((29600 + n)) bench.py \
           --gpus "$n" --steps 20 --warmup 3 --elements $((4 << 20)) --config5-elements $((16 << 20)) \
-          --cpu-seconds 2
+          --cpu-seconds 2 ${REHEARSE_ARGS:-}
       rc=$?; grep '^{' "$OUT/rehearse_n$n.log" | tail -1 > "$OUT/rehearse_n$n.json";;
     py:*)
       name=${s#py:}

@@ -25,7 +25,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q, stall_rank=-1, stall_waits=0, extra_legs=False):
+def _worker(rank, world, port, q, stall_rank=-1, stall_waits=0, extra_legs=False, peer="auto"):
     import sys
 
     sys.path.insert(0, ROOT)
@@ -59,14 +59,44 @@ def _worker(rank, world, port, q, stall_rank=-1, stall_waits=0, extra_legs=False
         comms.append((Stalled if rank == stall_rank else GlooPlanComm)(O))
         return comms[-1]
 
+    class FakePeer:
+        """hydra_amd.peer.PeerComm's interface over the gloo plans (DIRECT: the same reference
+        fold order as the peer kernel): the peer leg's orchestration on the CPU."""
+
+        def __init__(self):
+            self.comm, self.closed = GlooPlanComm(O), False
+            self.registered = []
+
+        def register(self, t):
+            self.registered.append(t.data_ptr())
+
+        def set_option(self, key, value):
+            pass
+
+        def allreduce_(self, t, algo="peer2", **kw):
+            assert t.data_ptr() in self.registered, "allreduce of an unregistered bucket"
+            self.comm.allreduce_(t, algo="direct", **kw)
+
+        def error(self):
+            return 0
+
+        def close(self):
+            self.closed = True
+
+    peers = []
+
+    def make_peer():
+        peers.append(FakePeer())
+        return peers[-1]
+
     try:
         args = argparse.Namespace(elements=1 << 16, steps=3, warmup=1, algo="auto",
                                   watchdog_s=600.0, no_config5=False, config5_elements=1 << 20,
-                                  peer=False, extra_legs=extra_legs)
+                                  peer=peer, extra_legs=extra_legs)
         base = ((lambda P, n: bench.ring_cpu_baseline(P, n, 0.5)) if O.ref_available() else None)
         res = ring.bench_allreduce(args, torch.device("cpu"), make_comm=make_comm,
-                                   sync=lambda: None, cpu_baseline=base)
-        q.put((rank, res, all(c.closed for c in comms) and len(comms) == 2))
+                                   sync=lambda: None, cpu_baseline=base, make_peer=make_peer)
+        q.put((rank, res, all(c.closed for c in comms + peers) and len(comms) == 2))
     except Exception as e:  # report instead of hanging the parent
         import traceback
 
@@ -75,12 +105,12 @@ def _worker(rank, world, port, q, stall_rank=-1, stall_waits=0, extra_legs=False
         dist.destroy_process_group()
 
 
-def _start(world, stall_rank=-1, stall_waits=0, extra_legs=False):
+def _start(world, stall_rank=-1, stall_waits=0, extra_legs=False, peer="auto"):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_worker, args=(r, world, port, q, stall_rank, stall_waits,
-                                               extra_legs))
+                                               extra_legs, peer))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -156,6 +186,38 @@ def test_bench_allreduce_orchestration(world):
         assert "frac_of_link" in lk and "frac_of_hbm" in fd, ph
         assert fd["fused_sum_bytes"] == int((world - 1) / world * n * 3 * esize), fd
         assert fd["kernel_hbm_bytes"] > 0 and fd["ops"] >= 1, fd
+    # the peer leg (auto): no GPU peer links here, so it states why it did not run
+    pl = res["peer_leg"]
+    assert pl["enabled"] is False and pl["mode"] == "auto", pl
+    assert pl["reason"].startswith("skipped: no GPU peer links"), pl
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_bench_peer_leg_orchestration(world):
+    """the reduce-on-read leg (forced on here; on an xGMI node "auto" turns
+    it on) runs last -- parity of both schedules, full-size exactness, workgroup autotune, the
+    timed region under the bench contract, and one event-timed phase entry against the link and
+    HBM rooflines -- and replaces the headline only when it is faster."""
+    out = _start(world, peer="on")
+    for r, (res, closed) in out.items():
+        assert isinstance(res, dict), res
+        assert closed, f"rank {r} left a communicator or peer group open"
+    res = out[0][0]
+    pl = res["peer_leg"]
+    assert pl["enabled"] and pl["mode"] == "on" and "error" not in pl, pl
+    assert pl["parity_fold_order_1M"] == {"peer2": "bit-exact", "peer1": "bit-exact"}, pl
+    assert pl["full_size_exact"] is True and pl["ms_per_step"] > 0, pl
+    assert set(pl["autotune_ms"]) == {"peer2/0wg", "peer2/256wg", "peer2/128wg"}, pl
+    ph = pl["phases"]
+    assert ph["kernel_ms"] > 0 and ph["link"]["algorithmic_bytes"] == int(
+        2 * (world - 1) / world * (1 << 16) * 4), ph
+    assert ph["link"]["peers"] == world - 1 and ph["fold"]["frac_of_hbm"] > 0, ph
+    if pl["promoted"]:
+        assert res["config"]["algo"] == "peer2" and res["ms_per_step"] == pl["ms_per_step"]
+        assert res["parity"]["full_size_exact"]["peer2"] is True
+    else:
+        assert res["config"]["algo"] != "peer2" and res["ms_per_step"] <= pl["ms_per_step"]
+    assert all(out[r][0]["peer_leg"]["promoted"] == pl["promoted"] for r in out)
 
 
 def test_bench_allreduce_extra_legs():

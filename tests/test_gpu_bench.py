@@ -56,6 +56,9 @@ def test_bench_multi_path_world1(gpu):
     assert rc["backend"] == "rccl" and rc["device"] == 0, rc
     cb = res["cpu_baseline"]
     assert cb["kind"] == "reference" and cb["value"] > 0 and cb["cores"] == 2, cb
+    # the peer leg states why it did not run at world 1 (auto mode)
+    pl = res["peer_leg"]
+    assert pl["enabled"] is False and pl["reason"] == "skipped: one rank: no peer to read from", pl
 
 
 @pytest.mark.extra
@@ -85,3 +88,12 @@ def test_bench_single_gpu_line(gpu):
     hp = res["host_path"]
     for kind in ("pinned_zero_copy", "pageable_staged"):
         assert hp[kind]["first_call_exact"] and hp[kind]["GBps"] > 0, hp
+    # config 2's size range: every size 4 Ki .. 64 Mi, both residencies,
+    # the smallest labelled dispatch-bound and the largest HBM-bound
+    sw = res["sweep"]
+    assert "error" not in sw, sw
+    assert [r["elements"] for r in sw["rows"]] == [1 << k for k in range(12, 27, 2)], sw
+    for r in sw["rows"]:
+        for kind in ("hbm_resident", "mall_assisted"):
+            assert r[kind]["GBps"] > 0 and 0 < r[kind]["frac_of_peak"] < 3, r
+    assert sw["rows"][0]["bound"] == "dispatch" and sw["rows"][-1]["bound"] == "hbm", sw

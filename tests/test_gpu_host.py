@@ -166,8 +166,6 @@ def test_hip_allreduce_ring(gpu, O, workspace, P, nptr, n, dt, monkeypatch, stag
     left fold x_r + x_{r-1} + ... of the locally reduced values (the AllreduceRing result,
     pinned to the reference by the old_ring fixtures); host workspace pre-reduces pointers as a
     left fold, device workspace as the pairwise tree; every pointer gets the result."""
-    if stage:  # every local-reduce step through the cross-device staging branch
-        monkeypatch.setenv("HYDRA_TEST_LOCAL_STAGE", "1")
     import torch
 
     code = {"f32": 6, "i32": 2}[dt]
@@ -295,8 +293,6 @@ def test_hip_allreduce_ring_chunked(gpu, O, workspace, P, nptr, n, dt, monkeypat
     ends with AllreduceRingChunked's result (pinned to the reference by the chunked_ring
     fixtures) over the locally reduced values -- CudaLocalNativeReduce's pairwise tree for both
     workspaces (cuda_collectives_device.h:29-56); every pointer gets the result."""
-    if stage:  # every local-reduce step through the cross-device staging branch
-        monkeypatch.setenv("HYDRA_TEST_LOCAL_STAGE", "1")
     import torch
 
     code = {"f32": 6, "i32": 2}[dt]
@@ -322,10 +318,17 @@ def test_hip_allreduce_ring_chunked(gpu, O, workspace, P, nptr, n, dt, monkeypat
 def test_hip_rings_local_reduce_staged(gpu, O, workspace, P, nptr, n, dt, monkeypatch):
     """The rings over several GPUs of one process: a local-reduce step whose two
     pointers sit on devices without peer access copies the source to a buffer on the
-    destination's device first, ordered by events.  HYDRA_TEST_LOCAL_STAGE=1 takes that branch
+    destination's device first, ordered by events.  The test switch HYDRA_TEST_LOCAL_STAGE (hydra_test_set) takes that branch
     for every step on the one GPU: the same bits as the reference semantics."""
-    test_hip_allreduce_ring(gpu, O, workspace, P, nptr, n, dt, monkeypatch, stage=True)
-    test_hip_allreduce_ring_chunked(gpu, O, workspace, P, nptr, n, dt, monkeypatch, stage=True)
+    from hydra_amd import _lib
+
+    prev = _lib.test_set(_lib.TEST_LOCAL_STAGE, 1)  # every local-reduce step staged
+    try:
+        test_hip_allreduce_ring(gpu, O, workspace, P, nptr, n, dt, monkeypatch, stage=True)
+        test_hip_allreduce_ring_chunked(gpu, O, workspace, P, nptr, n, dt, monkeypatch,
+                                        stage=True)
+    finally:
+        _lib.test_set(_lib.TEST_LOCAL_STAGE, prev)
 
 
 @pytest.mark.extra

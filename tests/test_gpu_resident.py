@@ -394,3 +394,77 @@ def test_resident_device_drains_are_bounded(gpu, O):
     assert still_serving and calls[0] > 50, calls
     slow = {k: round(v * 1e3, 2) for k, v in times.items() if v > 0.05}
     assert not slow, (slow, {k: round(v * 1e3, 2) for k, v in times.items()})
+
+
+_GEN_WRAP = r"""
+import ctypes, json, sys, time, numpy as np
+sys.path.insert(0, %r)
+import torch
+from hydra_amd import _lib, synth
+from hydra_amd.reduce import HostContext
+from oracle import oracle as O
+L = _lib.lib()
+# every launch advances the generation by 2^16: the job word's 16-bit tag is the same for every
+# instance, so only the zeroed device record keeps an old job word from a new instance's workers
+_lib.test_set(_lib.TEST_RESIDENT_GEN_STRIDE, 65536)
+blocks = []
+def pinned(n, fill):
+    p = ctypes.c_void_p()
+    _lib.check(L.hydra_malloc_host(n * 4, ctypes.byref(p)))
+    blocks.append(p)
+    x = np.frombuffer((ctypes.c_char * (n * 4)).from_address(p.value), np.float32)
+    x[:] = fill
+    return x
+c = HostContext(0)
+big, G = 40000, 4096  # 10 tiles: a published job; guard elements on both sides
+buf = pinned(big + 2 * G, np.float32(3.25))
+guard = np.float32(3.25)
+a0 = pinned(big, 0); a0[:] = synth.stress_f32(2, 0, big)
+b0 = pinned(big, 0); b0[:] = synth.stress_f32(2, 1, big)
+out0 = buf[G:G + big]
+_lib.check(L.hydra_reduce_host(c.handle, 0, 6, out0.ctypes.data, a0.ctypes.data, b0.ctypes.data, big))
+assert np.array_equal(out0.view(np.uint32), O.op(a0, b0, "sum", 6).view(np.uint32))
+out0[:] = np.float32(-7.0)  # canary: a replay of the first job would rewrite it
+l0 = c.stats()["resident_launches"]
+calls = 0
+for rnd in range(12):
+    time.sleep(0.004)  # past the 300 us idle limit: the next call launches a new instance
+    for i, n in enumerate((100, 3000, 50000, 17, 4096, 70001)):
+        a = synth.stress_f32(2, 0, n, seed=rnd * 10 + i)
+        b = synth.stress_f32(2, 1, n, seed=rnd * 10 + i)
+        e = O.op(a, b, "sum", 6)
+        _lib.check(L.hydra_reduce_host(c.handle, 0, 6, a.ctypes.data, a.ctypes.data,
+                                       b.ctypes.data, n))
+        assert np.array_equal(a.view(np.uint32), e.view(np.uint32)), (rnd, n)
+        calls += 1
+_lib.check(L.hydra_device_check(0))
+res = {"calls": calls, "launches": c.stats()["resident_launches"] - l0,
+       "canary_intact": bool((out0 == np.float32(-7.0)).all()),
+       "guards_intact": bool((buf[:G] == guard).all() and (buf[G + big:] == guard).all()),
+       "done_regressions": _lib.test_get(_lib.TEST_RESIDENT_REGRESSIONS),
+       "gen_stride": _lib.test_get(_lib.TEST_RESIDENT_GEN_STRIDE)}
+c.close()
+for p in blocks:
+    _lib.check(L.hydra_free_host(p))
+print(json.dumps(res))
+"""
+
+
+def test_resident_generation_tag_wrap(gpu):
+    """VERDICT r04 next #1 / ADVICE r04 (high): the job word carries 16 bits of the instance's
+    generation.  With the test switch HYDRA_TEST_RESIDENT_GEN_STRIDE = 65536 every instance has
+    the same tag, so a new instance's workers would take the job word the previous one published
+    and replay its descriptor -- unless the device record is zeroed before every launch.  A
+    published job, then 12 idle-outs, each followed by solo and spread calls on a new instance:
+    every result bit-exact, the first job's output (pinned, still mapped) and the guard elements
+    around it untouched, and no slot's completion word ever seen moving backwards."""
+    import json
+
+    p = subprocess.run([sys.executable, "-c", _GEN_WRAP % ROOT], capture_output=True, text=True,
+                       timeout=120, env=dict(os.environ, HYDRA_RESIDENT_IDLE_US="300"))
+    assert p.returncode == 0, (p.stdout[-1000:], p.stderr[-3000:])
+    r = json.loads(p.stdout.strip().splitlines()[-1])
+    assert r["gen_stride"] == 65536 and r["calls"] == 72, r
+    assert r["launches"] >= 12, r  # every round ran on a fresh instance with the same tag
+    assert r["canary_intact"] and r["guards_intact"], r
+    assert r["done_regressions"] == 0, r

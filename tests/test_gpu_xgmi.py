@@ -561,6 +561,85 @@ def test_simulated_config5_full_size(gpu):
         assert torch.equal(b.view(torch.bfloat16), exp), r
 
 
+@pytest.fixture(scope="module")
+def config4_full(gpu, O):
+    """BASELINE config 4 at its full size with fold-order-sensitive values: 8 ranks x 64 Mi fp32
+    of synth.stress_at (stress_f32's distribution, scales 2^0 .. 2^21 across ranks, generated on
+    the GPU), and the C restatement's ring result (O.ring_result, pinned to the reference) on the
+    same values: at this size the reference geometry is 256 segments of 1 MiB, S = 32 per rank
+    (allreduce.cc:199-221), so every one of the 8 blocks is 32 segments long."""
+    import torch
+
+    P, n = 8, 64 << 20
+    idx = torch.arange(n, device=gpu, dtype=torch.int64)
+    xs = [synth.stress_at(P, r, idx) for r in range(P)]
+    del idx
+    host = [x.cpu().numpy() for x in xs]
+    exp = torch.from_numpy(O.ring_result(host)).to(gpu)
+    # the values are order-sensitive: a plain left fold x_0 + x_1 + ... differs from the
+    # reference's per-block order on a large share of the elements
+    left = host[0].copy()
+    for h in host[1:]:
+        left += h
+    differ = float(np.mean(left.view(np.uint32) != exp.cpu().numpy().view(np.uint32)))
+    del host, left
+    yield xs, exp, differ
+    del xs, exp
+
+
+@pytest.mark.parametrize("algo", ["direct", "ring", "a2a"])
+def test_simulated_config4_full_size_order_sensitive(gpu, config4_full, algo):
+    """config 4 (8 x 64 Mi fp32) bit-exact at its BASELINE size on values
+    whose sums depend on the fold order -- every rank of RING, DIRECT and A2A equals the C
+    restatement of the reference ring (block ownership and chunking at S = 32)."""
+    import torch
+
+    xs, exp, differ = config4_full
+    assert differ > 0.2, differ  # the check can tell fold orders apart
+    bufs = [x.clone() for x in xs]
+    ring.simulate(bufs, algo=algo)
+    for r, b in enumerate(bufs):
+        assert torch.equal(b.view(torch.int32), exp.view(torch.int32)), (algo, r)
+
+
+@pytest.mark.parametrize("algo", ["direct", "a2a"])
+def test_simulated_config5_full_size_sampled(gpu, O, algo):
+    """config 5 (8 x 256 Mi bf16, fp32 accumulation) at its BASELINE size on
+    order-sensitive values: >= 1 Mi sampled elements -- every owner block's and every segment's
+    first two and last two elements, plus random ones spread over the bucket -- on every rank
+    equal the C restatement's fold on the widened values with the bf16 geometry (512 segments
+    of 1 MiB, S = 64 per rank)."""
+    import torch
+
+    P, n = 8, 256 << 20
+    idx_t = torch.arange(n, device=gpu, dtype=torch.int64)
+    bufs = []
+    for r in range(P):
+        bufs.append(synth.stress_at(P, r, idx_t).to(torch.bfloat16).view(torch.int16))
+    del idx_t
+    ns, sb, S = O.ring_plan(P, n, 2)
+    seg = sb // 2
+    edges = np.concatenate([np.arange(ns + 1, dtype=np.int64) * seg + d for d in (-2, -1, 0, 1)])
+    rnd = np.random.default_rng(55).integers(0, n, 1 << 20, dtype=np.int64)
+    idx = np.unique(np.concatenate([edges, rnd, [0, 1, n - 2, n - 1]]))
+    idx = idx[(idx >= 0) & (idx < n)]
+    from fold_expect import bf16_acc32_expected
+
+    exp, vals, geom = bf16_acc32_expected(O, P, n, idx)
+    assert geom == (512, 1 << 20, 64) and idx.size > (1 << 20) - 4096, (geom, idx.size)
+    # the check can tell fold orders apart: a plain left fold differs on many samples
+    left = synth.bf16_to_f32(vals[0]).astype(np.float32)
+    for v in vals[1:]:
+        left = O.acc_bf16_f32(left, v)
+    assert float(np.mean(synth.bf16_bits(left) != exp)) > 0.05
+    ring.simulate(bufs, algo=algo, dtype_code=_lib.BFLOAT16, flags=_lib.ACC_F32)
+    it = torch.from_numpy(idx).to(gpu)
+    for r, b in enumerate(bufs):
+        got = b[it].cpu().numpy().view(np.uint16)
+        bad = np.flatnonzero(got != exp)
+        assert bad.size == 0, (algo, r, bad.size, idx[bad[:5]].tolist())
+
+
 @pytest.mark.parametrize("P,n,ms,ch", [(2, 1, 0, 0), (2, 1000, 128, 256), (3, 4099, 128, 1024),
                                        (4, 262145, 0, 0), (5, 1 << 20, 0, 1 << 18),
                                        (8, 3000001, 0, 0), (8, 5003, 64, 128)])
