@@ -100,3 +100,35 @@ def stress_at(P: int, rank: int, idx, seed: int = 77):
     import torch
 
     return (m.to(torch.float32) * (2.0 ** -23) - 1.0) * scale
+
+
+def stress_cancel_at(P: int, rank: int, idx, seed: int = 91):
+    """Fold-order stress for buckets that are rounded once more after the fold (config 5: fp32
+    accumulation of bf16 data, one rounding to bf16).  stress_at's values differ between fold
+    orders only in fp32's last bits, which the final bf16 rounding hides; here, per element, two
+    ranks i != j (the same choice on every rank) hold +B and -B, B = 2^k with k in [20, 27], and
+    every other rank a small value u * 2^(0..4): the small values added while B is in the running
+    sum are rounded to B's fp32 grid, and which of them are depends on the order, so after B
+    cancels the difference survives the bf16 rounding.  Exact in bf16 (B is a power of two; the
+    caller rounds the small values).  numpy or torch, as stress_at."""
+    h = _fmix32((_mul32(idx & _MASK32, 0x9E3779B1) + (seed * 7919 + P * 104729)) & _MASK32)
+    i = h % P
+    j = (i + 1 + (h >> 8) % max(1, P - 1)) % P
+    k = 20 + (h >> 16) % 8
+    bbits = (k + 127) << 23  # the fp32 bit pattern of 2^k
+    small = stress_at(P, rank, idx, seed=seed + 1)  # u * 2^((3r) mod 17): rescaled below
+    hr = _fmix32((_mul32(idx & _MASK32, 0x85EBCA77) + rank * 2654435761 + seed) & _MASK32)
+    e = hr % 5
+    if isinstance(idx, np.ndarray):
+        big = bbits.astype(np.int32).view(np.float32)
+        ebits = ((e + 127) << 23).astype(np.int32).view(np.float32)  # 2^e
+        u = small / np.float32(2.0 ** ((3 * rank) % 17))
+        v = (u * ebits).astype(np.float32)
+        return np.where(rank == i, big, np.where(rank == j, -big, v)).astype(np.float32)
+    import torch
+
+    big = bbits.to(torch.int32).view(torch.float32)
+    ebits = ((e + 127) << 23).to(torch.int32).view(torch.float32)
+    u = small / float(2.0 ** ((3 * rank) % 17))
+    v = u * ebits
+    return torch.where(i == rank, big, torch.where(j == rank, -big, v))

@@ -1,6 +1,6 @@
 """Expected results of the reference ring's fold at sampled element indices (test helper).
 
-The bucket values are synth.stress_at's, so any sample of a full-size bucket generated on the GPU
+The bucket values come from synth's index-addressable generators, so any sample of a full-size bucket generated on the GPU
 is re-derived on the CPU; the fold itself runs in the C restatement (oracle/), which
 tests/test_oracle.py pins to the reference."""
 import numpy as np
@@ -8,14 +8,16 @@ import numpy as np
 from hydra_amd import synth
 
 
-def bf16_acc32_expected(O, P, n, idx, max_segment=1 << 20):
+def bf16_acc32_expected(O, P, n, idx, max_segment=1 << 20, gen=synth.stress_cancel_at):
     """The reference ring's fold on bf16 values widened to fp32, at element indices idx, with
     the bf16 bucket's block geometry (O.ring_plan, the C restatement of allreduce.cc:199-221 at
     E = 2): owner block q = x_q + (x_{q+1} + (... + x_{q-1})) accumulated in fp32 by the C
-    restatement (orc_acc_bf16_f32: acc + (float)b), rounded once to bf16 (RNE)."""
+    restatement (orc_acc_bf16_f32: acc + (float)b), rounded once to bf16 (RNE).  gen(P, r, idx):
+    rank r's fp32 values before the bf16 rounding (synth.stress_cancel_at by default: the
+    values whose bf16 result still depends on the fold order)."""
     ns, sb, S = O.ring_plan(P, n, 2, max_segment)
     block = S * sb // 2  # elements per owner block
-    vals = [synth.bf16_bits(synth.stress_at(P, r, idx)) for r in range(P)]
+    vals = [synth.bf16_bits(gen(P, r, idx)) for r in range(P)]
     owner = np.minimum(idx // block, P - 1)
     out = np.empty(idx.size, np.uint16)
     for q in range(P):

@@ -605,7 +605,8 @@ def test_simulated_config4_full_size_order_sensitive(gpu, config4_full, algo):
 @pytest.mark.parametrize("algo", ["direct", "a2a"])
 def test_simulated_config5_full_size_sampled(gpu, O, algo):
     """config 5 (8 x 256 Mi bf16, fp32 accumulation) at its BASELINE size on
-    order-sensitive values: >= 1 Mi sampled elements -- every owner block's and every segment's
+    order-sensitive values (synth.stress_cancel_at: +-2^k pivots that cancel, so the one bf16
+    rounding does not hide the fp32 fold order): >= 1 Mi sampled elements -- every owner block's and every segment's
     first two and last two elements, plus random ones spread over the bucket -- on every rank
     equal the C restatement's fold on the widened values with the bf16 geometry (512 segments
     of 1 MiB, S = 64 per rank)."""
@@ -615,7 +616,7 @@ def test_simulated_config5_full_size_sampled(gpu, O, algo):
     idx_t = torch.arange(n, device=gpu, dtype=torch.int64)
     bufs = []
     for r in range(P):
-        bufs.append(synth.stress_at(P, r, idx_t).to(torch.bfloat16).view(torch.int16))
+        bufs.append(synth.stress_cancel_at(P, r, idx_t).to(torch.bfloat16).view(torch.int16))
     del idx_t
     ns, sb, S = O.ring_plan(P, n, 2)
     seg = sb // 2
@@ -631,7 +632,7 @@ def test_simulated_config5_full_size_sampled(gpu, O, algo):
     left = synth.bf16_to_f32(vals[0]).astype(np.float32)
     for v in vals[1:]:
         left = O.acc_bf16_f32(left, v)
-    assert float(np.mean(synth.bf16_bits(left) != exp)) > 0.05
+    assert float(np.mean(synth.bf16_bits(left) != exp)) > 0.3
     ring.simulate(bufs, algo=algo, dtype_code=_lib.BFLOAT16, flags=_lib.ACC_F32)
     it = torch.from_numpy(idx).to(gpu)
     for r, b in enumerate(bufs):
