@@ -94,6 +94,6 @@ def test_bench_single_gpu_line(gpu):
     assert "error" not in sw, sw
     assert [r["elements"] for r in sw["rows"]] == [1 << k for k in range(12, 27, 2)], sw
     for r in sw["rows"]:
-        for kind in ("hbm_resident", "mall_assisted"):
+        for kind in ("hbm_resident", "mall_assisted", "hbm_resident_graph"):
             assert r[kind]["GBps"] > 0 and 0 < r[kind]["frac_of_peak"] < 3, r
     assert sw["rows"][0]["bound"] == "dispatch" and sw["rows"][-1]["bound"] == "hbm", sw
