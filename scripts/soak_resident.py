@@ -119,6 +119,12 @@ def drainer(out, stop):
 def main():
     seconds = float(sys.argv[1]) if len(sys.argv) > 1 else 20.0
     threads = int(sys.argv[2]) if len(sys.argv) > 2 else 4
+    # HYDRA_SOAK_GEN_STRIDE=65536: every instance gets the same 16-bit generation tag (the test
+    # switch of include/hydra_hip.h), so only the per-launch zeroing of the device record keeps an
+    # old job word from a new instance's workers
+    stride = int(os.environ.get("HYDRA_SOAK_GEN_STRIDE", "0"))
+    if stride:
+        _lib.test_set(_lib.TEST_RESIDENT_GEN_STRIDE, stride)
     out, stop = {}, threading.Event()
     ws = [threading.Thread(target=worker, args=(k, seconds, out, stop)) for k in range(threads)]
     d = threading.Thread(target=drainer, args=(out, stop))
@@ -137,9 +143,11 @@ def main():
            "calls": sum(out[k]["calls"] for k in range(threads)),
            "resident_calls": sum(out[k]["resident_calls"] for k in range(threads)),
            "launches": max(out[k]["launches"] for k in range(threads)),
+           "gen_stride": stride or 1,
+           "done_regressions": _lib.test_get(_lib.TEST_RESIDENT_REGRESSIONS),
            "errors": bad[:5], "drainer": out.get("drainer")}
     print(json.dumps(res), flush=True)
-    return 1 if bad else 0
+    return 1 if bad or res["done_regressions"] else 0
 
 
 if __name__ == "__main__":
