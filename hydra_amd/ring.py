@@ -918,7 +918,7 @@ def _peer_leg(make_peer, pg, run, measure, sync, dev, rank, world, xs, exp, x, x
     err = None
     try:
         pg["peer"] = make_peer()  # collective; fails on every rank together
-    except HydraError as e:
+    except Exception as e:  # (any failure: recorded, ranks stay in step)
         err = str(e)
     if not agreed(err):
         pg["peer"] = None
@@ -928,7 +928,7 @@ def _peer_leg(make_peer, pg, run, measure, sync, dev, rank, world, xs, exp, x, x
         for t in (tp, x):
             try:
                 pg["peer"].register(t)
-            except HydraError as e:
+            except Exception as e:
                 err = str(e)
             if not agreed(err):
                 leg["error"] = f"register: {err or 'another rank failed'}"
@@ -941,7 +941,7 @@ def _peer_leg(make_peer, pg, run, measure, sync, dev, rank, world, xs, exp, x, x
                 run(a, tp)
                 sync()
                 ok = bool(np.array_equal(tp.cpu().numpy().view(np.uint32), exp.view(np.uint32)))
-            except HydraError as e:
+            except Exception as e:
                 err = str(e)
             if not agreed(err) or not peer_ok():
                 par[a] = f"n/a: {err or 'a barrier expired or another rank failed'}"
@@ -958,7 +958,7 @@ def _peer_leg(make_peer, pg, run, measure, sync, dev, rank, world, xs, exp, x, x
             run("peer2", x)
             sync()
             good = bool(torch.equal(x, full_exp))
-        except HydraError as e:
+        except Exception as e:
             err = str(e)
         if not agreed(err) or not peer_ok():
             leg["error"] = f"full size: {err or 'a barrier expired or another rank failed'}"
@@ -974,7 +974,7 @@ def _peer_leg(make_peer, pg, run, measure, sync, dev, rank, world, xs, exp, x, x
                     run("peer2", x, wg)
 
                 tw = max_over_ranks(timed_steps(tstep, 5, 2, sync, dist.barrier), dev) / 5
-            except HydraError as e:
+            except Exception as e:
                 err = str(e)
             if not agreed(err) or not peer_ok():
                 leg["error"] = f"autotune: {err or 'a barrier expired or another rank failed'}"
@@ -984,7 +984,7 @@ def _peer_leg(make_peer, pg, run, measure, sync, dev, rank, world, xs, exp, x, x
         wg = int(min(tune, key=tune.get).split("/")[1][:-2])
         try:
             ms_p, lat_p = measure("peer2", wg)
-        except HydraError as e:
+        except Exception as e:
             err = str(e)
         if not agreed(err) or not peer_ok():
             leg["error"] = f"timed region: {err or 'a barrier expired or another rank failed'}"
@@ -997,7 +997,7 @@ def _peer_leg(make_peer, pg, run, measure, sync, dev, rank, world, xs, exp, x, x
         if p is not None:
             try:
                 p.close()
-            except HydraError as e:  # a teardown failure is reported, after every rank closed
+            except Exception as e:  # a teardown failure is reported, after every rank closed
                 leg.setdefault("error", f"teardown: {e}")
 
 
@@ -1010,22 +1010,29 @@ def _peer_phases(run, sync, dev, x, wg, world) -> dict:
     import torch
 
     n, esize = x.numel(), x.element_size()
-    ms = None
-    if getattr(dev, "type", "") == "cuda":
-        s = torch.cuda.current_stream(dev)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        sync()
-        e0.record(s)
-        run("peer2", x, wg)
-        e1.record(s)
-        sync()
-        ms = max_over_ranks(e0.elapsed_time(e1), dev)
-    else:  # (the CPU rehearsal: wall time of one synchronous call)
-        sync()
-        t0 = time.perf_counter()
-        run("peer2", x, wg)
-        sync()
-        ms = max_over_ranks((time.perf_counter() - t0) * 1e3, dev)
+    local, err = -1.0, None
+    try:
+        if getattr(dev, "type", "") == "cuda":
+            s = torch.cuda.current_stream(dev)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            sync()
+            e0.record(s)
+            run("peer2", x, wg)
+            e1.record(s)
+            sync()
+            local = e0.elapsed_time(e1)
+        else:  # (the CPU rehearsal: wall time of one synchronous call)
+            sync()
+            t0 = time.perf_counter()
+            run("peer2", x, wg)
+            sync()
+            local = (time.perf_counter() - t0) * 1e3
+    except Exception as e:  # every rank still reaches the collective below
+        err = str(e)
+    failed = max_over_ranks(1.0 if err else 0.0, dev) > 0
+    ms = max_over_ranks(local, dev)
+    if failed:
+        return {"error": err or "another rank failed"}
     link_bytes = 2 * (world - 1) / world * n * esize
     fused = (world - 1) / world * n * 3 * esize
     links = max(1, world - 1)
