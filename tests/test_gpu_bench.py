@@ -61,6 +61,34 @@ def test_bench_multi_path_world1(gpu):
     assert pl["enabled"] is False and pl["reason"] == "skipped: one rank: no peer to read from", pl
 
 
+def test_bench_rehearsal_world2_peer_leg(gpu):
+    """The N>1 line at world 2 with two real RCCL ranks sharing the one GPU
+    (HYDRA_BENCH_SHARED_GPU=1: each rank its own NCCL_HOSTID, sockets), as the driver launches it
+    (torch.distributed.run), with the peer-access leg forced on: every schedule bit-exact, and the
+    peer leg's parity, full-size check, autotune, timed region and phase entry all present."""
+    env = dict(os.environ, HYDRA_BENCH_SHARED_GPU="1")
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node", "2", "--master-addr", "127.0.0.1", "--master-port",
+                        str(_free_port()), "bench.py", "--gpus", "2", "--steps", "5", "--warmup",
+                        "1", "--elements", str(1 << 20), "--config5-elements", str(1 << 20),
+                        "--cpu-seconds", "1", "--watchdog-s", "150", "--peer", "on"],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=170)
+    assert p.returncode == 0, (p.returncode, p.stdout[-2000:], p.stderr[-3000:])
+    res = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    assert res["n_gpus"] == 2 and res["value"] > 0 and "rehearsal" in res, res
+    assert res["rccl_comm"]["nccl_comm_count"] == 2, res["rccl_comm"]
+    par = res["parity"]["fold_order_1M"]
+    for algo in ("direct", "ring", "a2a", "apipe"):
+        assert par[algo] == "bit-exact", (algo, par)
+    pl = res["peer_leg"]
+    assert pl["enabled"] and "error" not in pl, pl
+    assert pl["parity_fold_order_1M"] == {"peer2": "bit-exact", "peer1": "bit-exact"}, pl
+    assert pl["full_size_exact"] is True and pl["ms_per_step"] > 0, pl
+    assert pl["phases"]["kernel_ms"] > 0 and pl["phases"]["link"]["peers"] == 1, pl
+    if pl["promoted"]:
+        assert res["config"]["algo"] == "peer2", res["config"]
+
+
 @pytest.mark.extra
 def test_bench_multi_path_world1_extra_legs(gpu):
     res = _run(["--extra-legs"])
