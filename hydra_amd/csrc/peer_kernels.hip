@@ -34,7 +34,21 @@
 namespace hydra {
 namespace {
 
+constexpr int kPeerVariantBase = 2000;  // hydra_set_variant 2001..2007: peer kernel A/B
 constexpr int kPU = 2;  // 16-B vectors per lane per source in flight
+
+// Measurement variants (hydra_set_variant 2001..2007, f32 sum only; 0 = the shipped kernel):
+// bit 0 nontemporal loads, bit 1 nontemporal stores, bit 2 twice the loads in flight.
+template <int V>
+__device__ __forceinline__ u32x4 pld(const char* p) {
+  if constexpr ((V & 1) != 0) return ld<kNT>(p, rsrc<kNT>(nullptr, 0), 0);
+  else return ld_u(p);
+}
+template <int V>
+__device__ __forceinline__ void pst(char* p, u32x4 v) {
+  if constexpr ((V & 2) != 0) st<kNT>(p, rsrc<kNT>(nullptr, 0), 0, v);
+  else st_a(p, v);
+}
 
 // dst = fold of nsrc 16-B sources in the reference order
 template <typename E, int OP, bool ACC32>
@@ -110,8 +124,9 @@ __device__ __forceinline__ E fold_one(const PeerSrcs& S, int nsrc, size_t i) {
 
 // One workgroup folds `count` elements: dst[i] = fold(S.p[0][i], ..., S.p[nsrc-1][i]).
 // Aligned on dst (16 B); sources may sit at any element alignment (gfx950 unaligned mode).
-template <typename E, int OP, bool ACC32>
+template <typename E, int OP, bool ACC32, int V = 0>
 __device__ __forceinline__ void slab_fold(char* dst, const PeerSrcs& S, int nsrc, size_t count) {
+  constexpr int PU = (V & 4) ? 2 * kPU : kPU;
   constexpr int N = Vec<E>::N;
   const int t = threadIdx.x;
   size_t head = ((16 - (reinterpret_cast<uintptr_t>(dst) & 15)) & 15) / sizeof(E);
@@ -125,21 +140,21 @@ __device__ __forceinline__ void slab_fold(char* dst, const PeerSrcs& S, int nsrc
     de[i] = fold_one<E, OP, ACC32>(S, nsrc, i);
   }
   const size_t base = head * sizeof(E);
-  for (size_t v0 = 0; v0 < nvec; v0 += (size_t)kBlock * kPU) {
-    u32x4 r[kPU][kPeerMaxRanks];
+  for (size_t v0 = 0; v0 < nvec; v0 += (size_t)kBlock * PU) {
+    u32x4 r[PU][kPeerMaxRanks];
 #pragma unroll
-    for (int u = 0; u < kPU; u++) {
+    for (int u = 0; u < PU; u++) {
       const size_t v = v0 + (size_t)u * kBlock + t;
       if (v < nvec) {
 #pragma unroll
         for (int j = 0; j < kPeerMaxRanks; j++)
-          if (j < nsrc) r[u][j] = ld_u(S.p[j] + base + v * 16);
+          if (j < nsrc) r[u][j] = pld<V>(S.p[j] + base + v * 16);
       }
     }
 #pragma unroll
-    for (int u = 0; u < kPU; u++) {
+    for (int u = 0; u < PU; u++) {
       const size_t v = v0 + (size_t)u * kBlock + t;
-      if (v < nvec) st_a(dst + base + v * 16, fold_regs<E, OP, ACC32>(r[u], nsrc));
+      if (v < nvec) pst<V>(dst + base + v * 16, fold_regs<E, OP, ACC32>(r[u], nsrc));
     }
   }
 }
@@ -147,8 +162,9 @@ __device__ __forceinline__ void slab_fold(char* dst, const PeerSrcs& S, int nsrc
 // One workgroup copies `count` elements src -> dst (phase 2 / copy-back): raw 16-B vectors,
 // kCU of them per lane in flight (one source only, so deeper than the fold's kPU).
 constexpr int kCU = 8;
-template <typename E>
+template <typename E, int V = 0>
 __device__ __forceinline__ void slab_copy(char* dst, const char* src, size_t count) {
+  constexpr int CU = (V & 4) ? 2 * kCU : kCU;
   constexpr int N = Vec<E>::N;
   const int t = threadIdx.x;
   size_t head = ((16 - (reinterpret_cast<uintptr_t>(dst) & 15)) & 15) / sizeof(E);
@@ -160,17 +176,17 @@ __device__ __forceinline__ void slab_copy(char* dst, const char* src, size_t cou
   if ((size_t)t < head) de[t] = se[t];
   if ((size_t)t < tail) de[head + nvec * N + t] = se[head + nvec * N + t];
   const size_t base = head * sizeof(E);
-  for (size_t v0 = 0; v0 < nvec; v0 += (size_t)kBlock * kCU) {
-    u32x4 r[kCU];
+  for (size_t v0 = 0; v0 < nvec; v0 += (size_t)kBlock * CU) {
+    u32x4 r[CU];
 #pragma unroll
-    for (int u = 0; u < kCU; u++) {
+    for (int u = 0; u < CU; u++) {
       const size_t v = v0 + (size_t)u * kBlock + t;
-      if (v < nvec) r[u] = ld_u(src + base + v * 16);
+      if (v < nvec) r[u] = pld<V>(src + base + v * 16);
     }
 #pragma unroll
-    for (int u = 0; u < kCU; u++) {
+    for (int u = 0; u < CU; u++) {
       const size_t v = v0 + (size_t)u * kBlock + t;
-      if (v < nvec) st_a(dst + base + v * 16, r[u]);
+      if (v < nvec) pst<V>(dst + base + v * 16, r[u]);
     }
   }
 }
@@ -185,7 +201,7 @@ __device__ __forceinline__ bool group_broken(const PeerSync& S) {
   return __syncthreads_or(bad) != 0;
 }
 
-template <typename E, int OP, bool ACC32>
+template <typename E, int OP, bool ACC32, int V = 0>
 __global__ __launch_bounds__(kBlock) void k_peer_two_shot(PeerLaunch A) {
   const size_t SL = A.slab_bytes / sizeof(E);
   const PeerSync& Y = A.sync;
@@ -202,7 +218,7 @@ __global__ __launch_bounds__(kBlock) void k_peer_two_shot(PeerLaunch A) {
 #pragma unroll
       for (int j = 0; j < kPeerMaxRanks; j++)
         if (j < P) S.p[j] = A.x[(r + j) % P] + s * sizeof(E);
-      slab_fold<E, OP, ACC32>(A.x[r] + s * sizeof(E), S, P, hi - s < SL ? hi - s : SL);
+      slab_fold<E, OP, ACC32, V>(A.x[r] + s * sizeof(E), S, P, hi - s < SL ? hi - s : SL);
     }
   }
   // workgroup b of every rank has finished ITS slabs (k = b mod G) of its own block
@@ -214,14 +230,14 @@ __global__ __launch_bounds__(kBlock) void k_peer_two_shot(PeerLaunch A) {
     const size_t lo = A.lo[q], hi = A.lo[q + 1];
     for (size_t k = blockIdx.x; lo + k * SL < hi; k += G) {
       const size_t s = lo + k * SL;
-      slab_copy<E>(A.x[r] + s * sizeof(E), A.x[q] + s * sizeof(E), hi - s < SL ? hi - s : SL);
+      slab_copy<E, V>(A.x[r] + s * sizeof(E), A.x[q] + s * sizeof(E), hi - s < SL ? hi - s : SL);
     }
   }
   // nobody leaves (and lets its caller overwrite the bucket) while a peer may still read it
   peer_barrier(Y, 3);
 }
 
-template <typename E, int OP, bool ACC32>
+template <typename E, int OP, bool ACC32, int V = 0>
 __global__ __launch_bounds__(kBlock) void k_peer_one_shot(PeerLaunch A) {
   const size_t SL = A.slab_bytes / sizeof(E);
   const PeerSync& Y = A.sync;
@@ -241,7 +257,7 @@ __global__ __launch_bounds__(kBlock) void k_peer_one_shot(PeerLaunch A) {
 #pragma unroll
       for (int j = 0; j < kPeerMaxRanks; j++)
         if (j < P) S.p[j] = A.x[(q + j) % P] + s * sizeof(E);
-      slab_fold<E, OP, ACC32>(A.scratch + s * sizeof(E), S, P, hi - s < SL ? hi - s : SL);
+      slab_fold<E, OP, ACC32, V>(A.scratch + s * sizeof(E), S, P, hi - s < SL ? hi - s : SL);
     }
   }
   // every rank's workgroup b has read its slabs of every bucket -> safe to overwrite ours
@@ -253,18 +269,31 @@ __global__ __launch_bounds__(kBlock) void k_peer_one_shot(PeerLaunch A) {
     for (size_t k = 0; k < nsl; k++, w++) {
       if (w % G != blockIdx.x) continue;
       const size_t s = lo + k * SL;
-      slab_copy<E>(A.x[r] + s * sizeof(E), A.scratch + s * sizeof(E), hi - s < SL ? hi - s : SL);
+      slab_copy<E, V>(A.x[r] + s * sizeof(E), A.scratch + s * sizeof(E), hi - s < SL ? hi - s : SL);
     }
   }
 }
 
-template <typename E, int OP, bool ACC32>
+template <typename E, int OP, bool ACC32, int V = 0>
 hipError_t launch_t(int algo, const PeerLaunch& A, unsigned grid, hipStream_t s) {
   if (algo == kPeerOneShot)
-    hipLaunchKernelGGL((k_peer_one_shot<E, OP, ACC32>), dim3(grid), dim3(kBlock), 0, s, A);
+    hipLaunchKernelGGL((k_peer_one_shot<E, OP, ACC32, V>), dim3(grid), dim3(kBlock), 0, s, A);
   else
-    hipLaunchKernelGGL((k_peer_two_shot<E, OP, ACC32>), dim3(grid), dim3(kBlock), 0, s, A);
+    hipLaunchKernelGGL((k_peer_two_shot<E, OP, ACC32, V>), dim3(grid), dim3(kBlock), 0, s, A);
   return hipGetLastError();
+}
+
+hipError_t launch_variant(int v, int algo, const PeerLaunch& A, unsigned grid, hipStream_t s) {
+  switch (v) {
+    case 1: return launch_t<float, kSum, false, 1>(algo, A, grid, s);
+    case 2: return launch_t<float, kSum, false, 2>(algo, A, grid, s);
+    case 3: return launch_t<float, kSum, false, 3>(algo, A, grid, s);
+    case 4: return launch_t<float, kSum, false, 4>(algo, A, grid, s);
+    case 5: return launch_t<float, kSum, false, 5>(algo, A, grid, s);
+    case 6: return launch_t<float, kSum, false, 6>(algo, A, grid, s);
+    case 7: return launch_t<float, kSum, false, 7>(algo, A, grid, s);
+  }
+  return hipErrorInvalidValue;
 }
 
 template <int OP>
@@ -296,6 +325,9 @@ hipError_t launch_peer(int algo, int op, int dtype, bool acc32, const PeerLaunch
   if (A.sync.P < 1 || A.sync.P > kPeerMaxRanks || grid < 1 || grid > (unsigned)kPeerMaxBlocks ||
       A.slab_bytes < 16 || A.slab_bytes % 16)
     return hipErrorInvalidValue;
+  const int v = current_variant() - kPeerVariantBase;  // (measurement only)
+  if (v >= 1 && v <= 7 && op == kSum && dtype == kF32 && !acc32)
+    return launch_variant(v, algo, A, grid, s);
   switch (op) {
     case kSum: return dispatch<kSum>(algo, dtype, acc32, A, grid, s);
     case kProduct: return dispatch<kProduct>(algo, dtype, acc32, A, grid, s);

@@ -37,31 +37,47 @@ def worker(a):
     dist.init_process_group("gloo", rank=a.rank, world_size=a.P)
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
+    from hydra_amd import _lib
+
     peer = PeerComm(a.rank, a.P, 0, blocks=a.blocks or None)
     out = {}
     try:
         for n in a.n:
-            x = torch.from_numpy(synth.stress_f32(a.P, a.rank, n)).to(dev)
+            x0 = torch.from_numpy(synth.stress_f32(a.P, a.rank, n)).to(dev)
+            x = x0.clone()
             peer.register(x)
             for algo in a.algos:
-                for _ in range(a.warmup):
+                ref = None
+                for var in a.variants:  # hydra_set_variant: 0 = shipped, 2001.. = peer A/B
+                    _lib.lib().hydra_set_variant(var)
+                    x.copy_(x0)  # one checked call first: every variant must give the same bits
                     peer.allreduce_(x, algo=algo)
-                torch.cuda.synchronize(dev)
-                dist.barrier()
-                s = torch.cuda.current_stream(dev)
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                t0 = time.perf_counter()
-                e0.record(s)
-                for _ in range(a.iters):
-                    peer.allreduce_(x, algo=algo)
-                e1.record(s)
-                torch.cuda.synchronize(dev)
-                wall = time.perf_counter() - t0
-                out[f"{algo}/{n}"] = {"event_ms": e0.elapsed_time(e1) / a.iters,
-                                      "wall_ms": wall * 1e3 / a.iters, "err": peer.error()}
-                dist.barrier()
+                    torch.cuda.synchronize(dev)
+                    got = x.cpu().numpy()
+                    same = True if ref is None else bool((got.view("u4") == ref.view("u4")).all())
+                    ref = got if ref is None else ref
+                    for _ in range(a.warmup):
+                        peer.allreduce_(x, algo=algo)
+                    torch.cuda.synchronize(dev)
+                    dist.barrier()
+                    s = torch.cuda.current_stream(dev)
+                    e0 = torch.cuda.Event(enable_timing=True)
+                    e1 = torch.cuda.Event(enable_timing=True)
+                    t0 = time.perf_counter()
+                    e0.record(s)
+                    for _ in range(a.iters):
+                        peer.allreduce_(x, algo=algo)
+                    e1.record(s)
+                    torch.cuda.synchronize(dev)
+                    wall = time.perf_counter() - t0
+                    key = f"{algo}/{n}" + (f"/v{var}" if len(a.variants) > 1 else "")
+                    out[key] = {"event_ms": e0.elapsed_time(e1) / a.iters,
+                                "wall_ms": wall * 1e3 / a.iters, "err": peer.error(),
+                                "same_bits_as_first_variant": same}
+                    dist.barrier()
+                _lib.lib().hydra_set_variant(0)
             peer.unregister(x)
-            del x
+            del x, x0
     finally:
         peer.close()
     dist.barrier()
@@ -77,6 +93,7 @@ def main():
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--blocks", type=int, default=0)
+    ap.add_argument("--variants", type=int, nargs="+", default=[0])
     ap.add_argument("--rank", type=int, default=-1)
     ap.add_argument("--port", type=int, default=0)
     a = ap.parse_args()
@@ -90,7 +107,8 @@ def main():
     for r in range(a.P):
         cmd = [sys.executable, "-u", os.path.abspath(__file__), "--rank", str(r), "--port",
                str(port), "--P", str(a.P), "--iters", str(a.iters), "--warmup", str(a.warmup),
-               "--blocks", str(a.blocks), "--n", *map(str, a.n), "--algos", *a.algos]
+               "--blocks", str(a.blocks), "--n", *map(str, a.n), "--algos", *a.algos,
+               "--variants", *map(str, a.variants)]
         procs.append(subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
     res = []
     for p in procs:
@@ -102,7 +120,7 @@ def main():
         res.append(json.loads([ln for ln in o.splitlines() if ln.startswith("RESULT ")][-1][7:]))
     summary = {"P": a.P, "note": "all ranks on one GPU: remote reads are local HBM reads"}
     for key in res[0]:
-        algo, n = key.split("/")
+        algo, n = key.split("/")[:2]
         n = int(n)
         ms = max(r[key]["wall_ms"] for r in res)
         ev = max(r[key]["event_ms"] for r in res)
@@ -110,7 +128,8 @@ def main():
         summary[key] = {"ms": round(ms, 4), "event_ms": round(ev, 4),
                         "hbm_bytes": hbm, "hbm_GBps": round(hbm / (ev * 1e-3) / 1e9, 1),
                         "algbw_GBps": round(n * 4 / (ev * 1e-3) / 1e9, 1),
-                        "err": max(r[key]["err"] for r in res)}
+                        "err": max(r[key]["err"] for r in res),
+                        "same_bits": all(r[key]["same_bits_as_first_variant"] for r in res)}
     print(json.dumps(summary), flush=True)
 
 
