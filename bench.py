@@ -602,10 +602,15 @@ def run_single(args):
         out["roofline"]["measured_ceiling"] = ceil
     del pairs
     if not args.no_sweep:
-        try:  # config 2's whole size range (context: the headline is the 64 Mi line above)
-            out["sweep"] = sweep_leg(torch, L, dev, code)
-        except Exception as e:
-            out["sweep"] = {"error": str(e)}
+        # config 2's whole size range (context: the headline is the 64 Mi line above), for the
+        # line's dtype and for int32 (the microbench runs fp32 and int32)
+        other = _lib.INT32 if code == _lib.FLOAT32 else _lib.FLOAT32
+        for key, c in (("sweep", code), ("sweep_" + ("int32" if other == _lib.INT32 else "f32"),
+                                         other)):
+            try:
+                out[key] = sweep_leg(torch, L, dev, c)
+            except Exception as e:
+                out[key] = {"error": str(e)}
     if not args.no_host_path:
         try:  # row N2: the PCIe-inclusive host-buffer rate beside the HBM one (context only)
             out["host_path"] = host_path_leg()

@@ -125,3 +125,5 @@ def test_bench_single_gpu_line(gpu):
         for kind in ("hbm_resident", "mall_assisted", "hbm_resident_graph"):
             assert r[kind]["GBps"] > 0 and 0 < r[kind]["frac_of_peak"] < 3, r
     assert sw["rows"][0]["bound"] == "dispatch" and sw["rows"][-1]["bound"] == "hbm", sw
+    si = res["sweep_int32"]  # the same range for int32 (SURVEY 8(d) names both dtypes)
+    assert "error" not in si and len(si["rows"]) == len(sw["rows"]), si
