@@ -199,6 +199,7 @@ int validate_plan(const std::vector<hydra::PlanOp>& plan, int nranks, size_t es,
 struct hydra_comm {
   int rank = 0, nranks = 1, device = 0;
   bool aborted = false;  // hydra_comm_wait timed out: nccl was aborted
+  bool ran = false;      // a plan ran: ev_ks marks the end of its folds (scratch reads)
   ncclComm_t nccl = nullptr;
   hipStream_t cs = nullptr, ks = nullptr;  // comm stream, compute stream
   void* scratch = nullptr;
@@ -386,12 +387,22 @@ void wait_on(hipStream_t st, const hydra::PlanOp& o, const std::vector<hydra::Pl
 
 // Enqueue the cached plan after `start` (recorded on the caller's stream); the caller joins
 // with join_streams().  Two communicators forked from one event run concurrently (apipe).
-int run_plan_rccl(hydra_comm* c, int op, int dtype, bool acc32, char* user, hipEvent_t start) {
+int run_plan_rccl(hydra_comm* c, int op, int dtype, bool acc32, char* user, hipEvent_t start,
+                  hipStream_t user_st) {
   const auto& ops = c->plan;
   const size_t es = hydra::dtype_size(dtype);
   char* scratch = static_cast<char*>(c->scratch);
   HIP_TRY(hipStreamWaitEvent(c->cs, start, 0));
   HIP_TRY(hipStreamWaitEvent(c->ks, start, 0));
+  // The scratch belongs to the communicator: this call's first receive into it (comm stream)
+  // must not overtake the previous call's folds still reading it (compute stream, ended by
+  // ev_ks) -- also when the caller issues consecutive calls on different streams, which the
+  // join onto one caller stream would otherwise be the only thing to order.  (Not under
+  // capture: a captured graph orders its own nodes, and may not wait on an outside event.)
+  hipStreamCaptureStatus cs_state = hipStreamCaptureStatusNone;
+  HIP_TRY(hipStreamIsCapturing(user_st, &cs_state));
+  if (c->ran && cs_state == hipStreamCaptureStatusNone)
+    HIP_TRY(hipStreamWaitEvent(c->cs, c->ev_ks, 0));
   size_t i = 0;
   while (i < ops.size()) {
     const hydra::PlanOp& o = ops[i];
@@ -456,6 +467,7 @@ int run_plan_rccl(hydra_comm* c, int op, int dtype, bool acc32, char* user, hipE
   }
   HIP_TRY(hipEventRecord(c->ev_cs, c->cs));
   HIP_TRY(hipEventRecord(c->ev_ks, c->ks));
+  c->ran = true;
   return HYDRA_OK;
 }
 
@@ -687,7 +699,7 @@ int prepare(hydra_comm* c, int* algo, int op, int dtype, int flags, void* buf, s
 
 // Enqueue a prepared allreduce after `start`; ends recorded in c->ev_cs / c->ev_ks.
 int enqueue(hydra_comm* c, int algo, int op, int dtype, int flags, void* buf, size_t n,
-            hipEvent_t start) {
+            hipEvent_t start, hipStream_t user_st) {
   if (algo == HYDRA_ALGO_RCCL_RS_AG) {  // RCCL's own reduce-scatter + all-gather, in place
     HIP_TRY(hipStreamWaitEvent(c->cs, start, 0));
     const size_t es = hydra::dtype_size(dtype), k = n / (size_t)c->nranks;
@@ -714,7 +726,8 @@ int enqueue(hydra_comm* c, int algo, int op, int dtype, int flags, void* buf, si
     HIP_TRY(hipEventRecord(c->ev_ks, c->ks));
     return HYDRA_OK;
   }
-  return run_plan_rccl(c, op, dtype, (flags & HYDRA_ACC_F32) != 0, static_cast<char*>(buf), start);
+  return run_plan_rccl(c, op, dtype, (flags & HYDRA_ACC_F32) != 0, static_cast<char*>(buf), start,
+                       user_st);
 }
 
 }  // namespace
@@ -734,7 +747,7 @@ int hydra_allreduce(hydra_comm_t c, int algo, int op, int dtype, int flags, void
   if (rc || skip) return rc ? rc : ok();
   if ((rc = prof_begin(c, st))) return rc;
   HIP_TRY(hipEventRecord(c->ev_start, st));
-  rc = enqueue(c, algo, op, dtype, flags, buf, n, c->ev_start);
+  rc = enqueue(c, algo, op, dtype, flags, buf, n, c->ev_start, st);
   if (rc) return rc;
   rc = join_streams(c, st);
   return rc ? rc : ok();
@@ -756,7 +769,7 @@ int hydra_reduce_root(hydra_comm_t c, int root, int op, int dtype, int flags, vo
   if (rc || skip) return rc ? rc : ok();
   if ((rc = prof_begin(c, st))) return rc;
   HIP_TRY(hipEventRecord(c->ev_start, st));
-  rc = enqueue(c, algo, op, dtype, flags, buf, n, c->ev_start);
+  rc = enqueue(c, algo, op, dtype, flags, buf, n, c->ev_start, st);
   if (rc) return rc;
   rc = join_streams(c, st);
   return rc ? rc : ok();
@@ -805,8 +818,8 @@ int hydra_apipe_allreduce(hydra_comm_t rail1, hydra_comm_t rail2, int table, int
   // both rails fork from one event on the caller's stream and run concurrently on their own
   // streams (the two std::threads of pipeallreduce-a.cc:32-50); the caller's stream joins both
   HIP_TRY(hipEventRecord(rail1->ev_start, st));
-  rc = enqueue(rail1, a1, op, dtype, flags, buf, e1, rail1->ev_start);
-  if (!rc) rc = enqueue(rail2, a2, op, dtype, flags, p2, e2, rail1->ev_start);
+  rc = enqueue(rail1, a1, op, dtype, flags, buf, e1, rail1->ev_start, st);
+  if (!rc) rc = enqueue(rail2, a2, op, dtype, flags, p2, e2, rail1->ev_start, st);
   if (!rc) rc = join_streams(rail1, st);
   if (!rc) rc = join_streams(rail2, st);
   return rc ? rc : ok();
@@ -1105,7 +1118,7 @@ int hydra_comm_run_plan(hydra_comm_t c, const hydra_plan_op_t* ops, size_t nops,
   if ((rc = prof_begin(c, st))) return rc;
   HIP_TRY(hipEventRecord(c->ev_start, st));
   rc = run_plan_rccl(c, op, dtype, (flags & HYDRA_ACC_F32) != 0, static_cast<char*>(buf),
-                     c->ev_start);
+                     c->ev_start, st);
   if (!rc) rc = join_streams(c, st);
   return rc ? rc : ok();
 }

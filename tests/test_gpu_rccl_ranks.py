@@ -115,6 +115,23 @@ def _worker(rank, world, port, q):
             for algo in ("direct", "a2a"):
                 run(f"{algo}_bf16_acc32_vs_ref_n{c['n']}", xb, gnpz[c["key"]], algo=algo,
                     dtype_code=_lib.BFLOAT16, flags=_lib.ACC_F32)
+        # consecutive allreduces issued on alternating caller streams with no ordering between
+        # them: the communicator's scratch is reused by every call, so each call's receives
+        # into it must wait for the previous call's folds (xgmi_allreduce.cpp run_plan_rccl)
+        streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+        n = 1 << 20
+        batches = [[synth.stress_f32(world, r, n, seed=500 + i) for r in range(world)]
+                   for i in range(6)]
+        ts = [torch.from_numpy(b[rank].copy()).to(dev) for b in batches]
+        torch.cuda.synchronize(dev)
+        for i, t in enumerate(ts):
+            comm.allreduce_(t, algo="direct", chunk_bytes=1 << 18,
+                            stream=streams[i % 2].cuda_stream)
+        for st in streams:
+            comm.wait(60000, stream=st.cuda_stream)
+        res["alternating_streams"] = all(
+            np.array_equal(_bits(t.cpu().numpy()), _bits(O.ring_result(b)))
+            for t, b in zip(ts, batches))
         # ncclAllReduce (RCCL's order): |got - sum| <= (P-1) * 2^-24 * sum|x| per element
         n = 1 << 20
         xs = [synth.stress_f32(world, r, n) for r in range(world)]
