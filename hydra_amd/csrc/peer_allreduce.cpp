@@ -77,6 +77,11 @@ struct hydra_peer {
   std::map<std::string, Mapping> opened;  // (rank, allocation id, ipc bytes) -> mapping
   std::map<const void*, uint64_t> exported;  // own allocation base -> allocation id exported
   bool detached = false;                  // hydra_peer_detach ran: no mappings left
+  // the last call's completion: the next call's kernel waits for it, so two calls issued on
+  // different streams never run at once (their workgroups share the barrier epochs and the
+  // one-shot scratch)
+  hipEvent_t last = nullptr;
+  bool last_valid = false;
 };
 
 namespace {
@@ -199,6 +204,7 @@ int hydra_peer_create(int nranks, int rank, int device, hydra_peer_t* out, void*
     *p->err_host = 0;
     e = hipHostGetDevicePointer(reinterpret_cast<void**>(&p->err_dev), p->err_host, 0);
   }
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&p->last, hipEventDisableTiming);
   if (e == hipSuccess) e = hydra::drain_device(device);
   if (e != hipSuccess) {
     hydra_peer_destroy(p);
@@ -394,10 +400,21 @@ int hydra_peer_allreduce(hydra_peer_t p, int algo, int op, int dtype, int flags,
     }
     A.scratch = p->scratch;
   }
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  // Calls on one group run one after another on the device whatever streams they are issued
+  // on (a graph being captured orders its own nodes, and may not wait on an outside event).
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  HIP_TRY(hipStreamIsCapturing(st, &cap));
+  const bool capturing = cap != hipStreamCaptureStatusNone;
+  if (!capturing && p->last_valid) HIP_TRY(hipStreamWaitEvent(st, p->last, 0));
   const hipError_t e = hydra::launch_peer(
       algo == HYDRA_PEER_ONE_SHOT ? hydra::kPeerOneShot : hydra::kPeerTwoShot, op, dtype, acc32,
-      A, (unsigned)grid, static_cast<hipStream_t>(stream));
+      A, (unsigned)grid, st);
   if (e != hipSuccess) return hydra::hip_fail(e, "peer allreduce kernel launch");
+  if (!capturing) {
+    HIP_TRY(hipEventRecord(p->last, st));
+    p->last_valid = true;
+  }
   return ok();
 }
 
@@ -431,6 +448,7 @@ int hydra_peer_destroy(hydra_peer_t p) {
     hydra::ledger_release(hydra::kLedgerPeerLocal, p->sig);
   }
   if (p->err_host) (void)hipHostFree(p->err_host);
+  if (p->last) (void)hipEventDestroy(p->last);
   delete p;
   return ok();
 }

@@ -442,7 +442,8 @@ int hydra_reduce_root_simulate(int root, int op, int dtype, int flags, int P, vo
  * each bucket: hydra_peer_register -> exchange -> hydra_peer_open.  Every rank must then issue
  * the same sequence of hydra_peer_allreduce calls (like any collective).  A call is one kernel
  * launch and is graph-capturable: barrier epochs live on the device, so replays need no new
- * arguments.  A peer that never arrives ends the kernel after the timeout (default 20 s) and
+ * arguments.  Eager calls on one group run one after another on the device even when issued on
+ * different streams (each waits for the previous one's completion event).  A peer that never arrives ends the kernel after the timeout (default 20 s) and
  * leaves an error code readable with hydra_peer_error; later calls on the group fail with
  * HYDRA_ERR_HIP.  1 <= nranks <= 8. */
 #define HYDRA_PEER_HANDLE_BYTES 128

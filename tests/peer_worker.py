@@ -56,6 +56,35 @@ def stress(peer, arena, c, rank, world, dev):
     return bad
 
 
+def alternating_streams(peer, arena, c, rank, world, dev):
+    """`iters` allreduces issued alternately on two streams with no ordering between them, on
+    two buckets at different offsets of the arena: the group's calls must still run one after
+    another on the device (they share barrier epochs and scratch).  Small integer inputs, so
+    every result is exact in fp32; every word checked.  Returns the number of wrong words."""
+    import torch
+
+    n = c["n"]
+    views = [arena[0:4 * n].view(torch.float32), arena[8 * n:12 * n].view(torch.float32)]
+    streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+    base = torch.arange(n, device=dev, dtype=torch.int64) % 100
+    for k, v in enumerate(views):
+        v.copy_((base * (rank + 1) + k).to(torch.float32))
+    torch.cuda.synchronize(dev)
+    for it in range(c["iters"]):
+        k = it % 2
+        peer.allreduce_(views[k], algo=c["algo"], dtype_code=c["dtype"],
+                        stream=streams[k].cuda_stream)
+    torch.cuda.synchronize(dev)
+    bad = 0
+    for k, v in enumerate(views):
+        calls = (c["iters"] + 1 - k) // 2
+        # the first call sums the ranks' inputs; each later one sums `world` equal copies
+        first = base * (world * (world + 1) // 2) + k * world
+        exp = first.to(torch.float64) * float(world) ** (calls - 1)
+        bad += int((v.to(torch.float64) != exp).sum().item())
+    return bad
+
+
 def reregister(peer, c, rank, world, dev):
     """`iters` rounds of: a FRESH allocation (the caching allocator emptied first), register,
     allreduce with inputs that change every round, every word checked, collective unregister,
@@ -119,6 +148,9 @@ def main():
                 continue
             if c["data"] == "reregister":  # fresh allocations, register/unregister loop
                 status[name] = reregister(peer, c, a.rank, a.world, dev)
+                continue
+            if c["data"] == "streams":  # calls on two unordered streams
+                status[name] = alternating_streams(peer, arena, c, a.rank, a.world, dev)
                 continue
             if c.get("timeout_ms"):
                 peer.set_option(_lib.PEER_OPT_TIMEOUT_MS, c["timeout_ms"])
