@@ -35,7 +35,6 @@ namespace hydra {
 namespace {
 
 constexpr int kPeerVariantBase = 2000;  // hydra_set_variant 2001..2007: peer kernel A/B
-constexpr int kPU = 2;  // 16-B vectors per lane per source in flight
 
 // Measurement variants (hydra_set_variant 2001..2007, f32 sum only; 0 = the shipped kernel):
 // bit 0 nontemporal loads, bit 1 nontemporal stores, bit 2 twice the loads in flight.
@@ -50,25 +49,25 @@ __device__ __forceinline__ void pst(char* p, u32x4 v) {
   else st_a(p, v);
 }
 
-// dst = fold of nsrc 16-B sources in the reference order
-template <typename E, int OP, bool ACC32>
-__device__ __forceinline__ u32x4 fold_regs(const u32x4 (&v)[kPeerMaxRanks], int nsrc) {
+// dst = fold of NP 16-B sources in the reference order: v[NP-1] innermost,
+// acc = v[j] op acc for j = NP-2 .. 0 (c = local + received, in place on local).  NP is a
+// compile-time count: with a runtime count every load sat behind a scalar branch, and the
+// compiler waited for each load before issuing the next (one load in flight per wave).
+template <typename E, int OP, bool ACC32, int NP>
+__device__ __forceinline__ u32x4 fold_n(const u32x4 (&v)[NP]) {
   if constexpr (ACC32) {
     float a[8];
 #pragma unroll
-    for (int j = kPeerMaxRanks - 1; j >= 0; j--) {
-      if (j < nsrc) {
+    for (int k = 0; k < 4; k++) {
+      a[2 * k] = bitsf(v[NP - 1][k] << 16);
+      a[2 * k + 1] = bitsf(v[NP - 1][k] & 0xffff0000u);
+    }
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-          const float lo = bitsf(v[j][k] << 16), hi = bitsf(v[j][k] & 0xffff0000u);
-          if (j == nsrc - 1) {
-            a[2 * k] = lo;
-            a[2 * k + 1] = hi;
-          } else {
-            a[2 * k] = fop<OP>(lo, a[2 * k]);
-            a[2 * k + 1] = fop<OP>(hi, a[2 * k + 1]);
-          }
-        }
+    for (int j = NP - 2; j >= 0; j--) {
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        a[2 * k] = fop<OP>(bitsf(v[j][k] << 16), a[2 * k]);
+        a[2 * k + 1] = fop<OP>(bitsf(v[j][k] & 0xffff0000u), a[2 * k + 1]);
       }
     }
     u32x4 o;
@@ -77,14 +76,9 @@ __device__ __forceinline__ u32x4 fold_regs(const u32x4 (&v)[kPeerMaxRanks], int 
       o[k] = (uint32_t)f2bf(a[2 * k]) | ((uint32_t)f2bf(a[2 * k + 1]) << 16);
     return o;
   } else {
-    u32x4 acc = v[0];
+    u32x4 acc = v[NP - 1];
 #pragma unroll
-    for (int j = kPeerMaxRanks - 1; j >= 0; j--) {
-      if (j < nsrc) {
-        if (j == nsrc - 1) acc = v[j];
-        else acc = vapply<E, OP>(v[j], acc, v[j]);  // c = local + received, in place on local
-      }
-    }
+    for (int j = NP - 2; j >= 0; j--) acc = vapply<E, OP>(v[j], acc, v[j]);
     return acc;
   }
 }
@@ -93,7 +87,7 @@ struct PeerSrcs {
   const char* p[kPeerMaxRanks];
 };
 
-// one element, same order as fold_regs (static source indices: no scratch spills)
+// one element, same order as fold_n (static source indices: no scratch spills)
 template <typename E, int OP, bool ACC32>
 __device__ __forceinline__ E fold_one(const PeerSrcs& S, int nsrc, size_t i) {
   if constexpr (ACC32) {
@@ -122,11 +116,14 @@ __device__ __forceinline__ E fold_one(const PeerSrcs& S, int nsrc, size_t i) {
   }
 }
 
-// One workgroup folds `count` elements: dst[i] = fold(S.p[0][i], ..., S.p[nsrc-1][i]).
+// One workgroup folds `count` elements: dst[i] = fold(S.p[0][i], ..., S.p[NP-1][i]).
 // Aligned on dst (16 B); sources may sit at any element alignment (gfx950 unaligned mode).
-template <typename E, int OP, bool ACC32, int V = 0>
-__device__ __forceinline__ void slab_fold(char* dst, const PeerSrcs& S, int nsrc, size_t count) {
-  constexpr int PU = (V & 4) ? 2 * kPU : kPU;
+// The main loop issues PU x NP unpredicated 16-B loads per lane before its first store (8-16
+// in flight: the grid is small -- every workgroup pays barriers -- so the depth has to come from
+// each wave); the last partial round is predicated.
+template <typename E, int OP, bool ACC32, int V, int NP>
+__device__ __forceinline__ void slab_fold_n(char* dst, const PeerSrcs& S, size_t count) {
+  constexpr int PU = ((V & 4) ? 2 : 1) * (NP >= 4 ? 2 : 8 / NP);
   constexpr int N = Vec<E>::N;
   const int t = threadIdx.x;
   size_t head = ((16 - (reinterpret_cast<uintptr_t>(dst) & 15)) & 15) / sizeof(E);
@@ -134,28 +131,48 @@ __device__ __forceinline__ void slab_fold(char* dst, const PeerSrcs& S, int nsrc
   const size_t nvec = (count - head) / N;
   const size_t tail = count - head - nvec * N;
   E* de = reinterpret_cast<E*>(dst);
-  if ((size_t)t < head) de[t] = fold_one<E, OP, ACC32>(S, nsrc, t);
+  if ((size_t)t < head) de[t] = fold_one<E, OP, ACC32>(S, NP, t);
   if ((size_t)t < tail) {
     const size_t i = head + nvec * N + t;
-    de[i] = fold_one<E, OP, ACC32>(S, nsrc, i);
+    de[i] = fold_one<E, OP, ACC32>(S, NP, i);
   }
-  const size_t base = head * sizeof(E);
-  for (size_t v0 = 0; v0 < nvec; v0 += (size_t)kBlock * PU) {
-    u32x4 r[PU][kPeerMaxRanks];
+  const char* src[NP];
+#pragma unroll
+  for (int j = 0; j < NP; j++) src[j] = S.p[j] + head * sizeof(E);
+  char* out = dst + head * sizeof(E);
+  constexpr size_t kStep = (size_t)kBlock * PU;
+  const size_t full = nvec / kStep * kStep;
+  for (size_t v0 = 0; v0 < full; v0 += kStep) {
+    u32x4 r[PU][NP];
 #pragma unroll
     for (int u = 0; u < PU; u++) {
-      const size_t v = v0 + (size_t)u * kBlock + t;
-      if (v < nvec) {
+      const size_t o = (v0 + (size_t)u * kBlock + t) * 16;
 #pragma unroll
-        for (int j = 0; j < kPeerMaxRanks; j++)
-          if (j < nsrc) r[u][j] = pld<V>(S.p[j] + base + v * 16);
-      }
+      for (int j = 0; j < NP; j++) r[u][j] = pld<V>(src[j] + o);
     }
 #pragma unroll
-    for (int u = 0; u < PU; u++) {
-      const size_t v = v0 + (size_t)u * kBlock + t;
-      if (v < nvec) pst<V>(dst + base + v * 16, fold_regs<E, OP, ACC32>(r[u], nsrc));
-    }
+    for (int u = 0; u < PU; u++)
+      pst<V>(out + (v0 + (size_t)u * kBlock + t) * 16, fold_n<E, OP, ACC32, NP>(r[u]));
+  }
+  for (size_t v = full + t; v < nvec; v += kBlock) {  // the last partial round
+    u32x4 r[NP];
+#pragma unroll
+    for (int j = 0; j < NP; j++) r[j] = pld<V>(src[j] + v * 16);
+    pst<V>(out + v * 16, fold_n<E, OP, ACC32, NP>(r));
+  }
+}
+
+template <typename E, int OP, bool ACC32, int V = 0>
+__device__ __forceinline__ void slab_fold(char* dst, const PeerSrcs& S, int nsrc, size_t count) {
+  switch (nsrc) {  // uniform over the grid: one branch per slab, none in the loop
+    case 1: slab_fold_n<E, OP, ACC32, V, 1>(dst, S, count); break;
+    case 2: slab_fold_n<E, OP, ACC32, V, 2>(dst, S, count); break;
+    case 3: slab_fold_n<E, OP, ACC32, V, 3>(dst, S, count); break;
+    case 4: slab_fold_n<E, OP, ACC32, V, 4>(dst, S, count); break;
+    case 5: slab_fold_n<E, OP, ACC32, V, 5>(dst, S, count); break;
+    case 6: slab_fold_n<E, OP, ACC32, V, 6>(dst, S, count); break;
+    case 7: slab_fold_n<E, OP, ACC32, V, 7>(dst, S, count); break;
+    case 8: slab_fold_n<E, OP, ACC32, V, 8>(dst, S, count); break;
   }
 }
 
