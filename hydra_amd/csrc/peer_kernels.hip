@@ -118,12 +118,14 @@ __device__ __forceinline__ E fold_one(const PeerSrcs& S, int nsrc, size_t i) {
 
 // One workgroup folds `count` elements: dst[i] = fold(S.p[0][i], ..., S.p[NP-1][i]).
 // Aligned on dst (16 B); sources may sit at any element alignment (gfx950 unaligned mode).
-// The main loop issues PU x NP unpredicated 16-B loads per lane before its first store (8-16
+// The main loop issues PU x NP unpredicated 16-B loads per lane before its first store (15-32
 // in flight: the grid is small -- every workgroup pays barriers -- so the depth has to come from
-// each wave); the last partial round is predicated.
+// each wave; round 5's A/B on one GPU, profiles/r05k_*: twice the r05j depth was as fast or
+// faster at every size >= 16 Mi); the last partial round is predicated.
 template <typename E, int OP, bool ACC32, int V, int NP>
 __device__ __forceinline__ void slab_fold_n(char* dst, const PeerSrcs& S, size_t count) {
-  constexpr int PU = ((V & 4) ? 2 : 1) * (NP >= 4 ? 2 : 8 / NP);
+  // (1-byte elements: half the depth -- their per-byte max / min unpack needs the registers)
+  constexpr int PU = ((V & 4) ? 2 : 1) * (NP >= 4 ? 4 : 16 / NP) / (sizeof(E) == 1 ? 2 : 1);
   constexpr int N = Vec<E>::N;
   const int t = threadIdx.x;
   size_t head = ((16 - (reinterpret_cast<uintptr_t>(dst) & 15)) & 15) / sizeof(E);
@@ -178,7 +180,7 @@ __device__ __forceinline__ void slab_fold(char* dst, const PeerSrcs& S, int nsrc
 
 // One workgroup copies `count` elements src -> dst (phase 2 / copy-back): raw 16-B vectors,
 // kCU of them per lane in flight (one source only, so deeper than the fold's kPU).
-constexpr int kCU = 8;
+constexpr int kCU = 16;
 template <typename E, int V = 0>
 __device__ __forceinline__ void slab_copy(char* dst, const char* src, size_t count) {
   constexpr int CU = (V & 4) ? 2 * kCU : kCU;
