@@ -382,9 +382,13 @@ int hydra_peer_allreduce(hydra_peer_t p, int algo, int op, int dtype, int flags,
     for (int q = 0; q < p->P; q++) work += (g.block_bytes(q) + slab - 1) / slab;
   else
     work = (g.max_block() + slab - 1) / slab;
-  // grid: one workgroup per slab, at most 512 (2 per CU: every workgroup resident)
+  // grid: one workgroup per slab, at most 256 (one per CU).  The deep fold holds ~250 VGPRs,
+  // so a CU runs two of these workgroups at once: every workgroup of the grid is resident, with
+  // room for the same grid of a second rank when ranks share a GPU (the one-GPU tests); the
+  // depth comes from each wave (peer_kernels.hip slab_fold_n), not from more workgroups, which
+  // measured no faster (profiles/r05h, r05m)
   const size_t grid =
-      p->blocks > 0 ? (size_t)p->blocks : std::min<size_t>(std::max<size_t>(work, 1), 512);
+      p->blocks > 0 ? (size_t)p->blocks : std::min<size_t>(std::max<size_t>(work, 1), 256);
   if (algo == HYDRA_PEER_ONE_SHOT) {
     if (p->scratch_bytes < n * es) {
       HIP_TRY(hydra::drain_device(p->device));  // first call at a new size: outside any capture

@@ -352,33 +352,6 @@ __global__ __launch_bounds__(kBlock) void k_fold(E* dst, FoldSrcs S, int nsrc, s
   }
 }
 
-// The same with the source count a compile-time constant (reduce_ops.h fold_vec_np).
-template <typename E, int OP, bool ACC32, bool NT, int MAP, int NP>
-__global__ __launch_bounds__(kBlock) void k_fold_np(E* dst, FoldSrcs S, size_t nvec, int head,
-                                                    int tail) {
-  constexpr int N = Vec<E>::N;
-  const int t = threadIdx.x;
-  if (blockIdx.x == 0) {
-    if (t < head) {
-      dst[t - head] = fold_elem<E, OP, ACC32>(S, NP, (ptrdiff_t)t - head);
-    } else if (t >= 64 && t - 64 < tail) {
-      const ptrdiff_t i = (ptrdiff_t)(nvec * N) + (t - 64);
-      dst[i] = fold_elem<E, OP, ACC32>(S, NP, i);
-    }
-  }
-  char* d = reinterpret_cast<char*>(dst);
-  const size_t stride = (size_t)gridDim.x * kBlock;
-  size_t first = blockIdx.x;
-  if (MAP == 1 && (gridDim.x & 7) == 0) first = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
-  for (size_t vb = first * kBlock; vb < nvec; vb += stride) {  // wave-uniform
-    const size_t v = vb + t;
-    const auto w = __builtin_amdgcn_make_buffer_rsrc(d + vb * 16, 0, kBlock * 16, 0x00020000);
-    if (v < nvec)
-      __builtin_amdgcn_raw_buffer_store_b128(fold_vec_np<E, OP, ACC32, NT, NP>(S, v * 16), w,
-                                             (uint32_t)t * 16, 0, 16);
-  }
-}
-
 // -------------------------------------------------------------------------------------------
 // Persistent, software-pipelined variant (measurement: variants 45-47).  A capped grid of
 // CUs x W workgroups; each workgroup streams ONE contiguous range of tiles (XCD-contiguous
@@ -755,54 +728,12 @@ hipError_t launch_fold_v(void* dst, const void* const* srcs, int nsrc, size_t n,
   return hipGetLastError();
 }
 
-template <typename E, int OP, bool ACC32, int MAP, int NP>
-hipError_t launch_fold_np(void* dst, const void* const* srcs, size_t n, hipStream_t s) {
-  const Split sp = split_call<E>(dst, n);
-  FoldSrcs S;
-  for (int j = 0; j < kMaxRanks; j++)
-    S.p[j] = j < NP ? reinterpret_cast<const char*>(srcs[j]) + (size_t)sp.head * sizeof(E)
-                    : nullptr;
-  E* d = reinterpret_cast<E*>(dst) + sp.head;
-  size_t blocks = (sp.nvec + kBlock - 1) / kBlock;
-  if (blocks == 0) blocks = 1;
-  hipLaunchKernelGGL((k_fold_np<E, OP, ACC32, true, MAP, NP>), dim3((unsigned)blocks),
-                     dim3(kBlock), 0, s, d, S, sp.nvec, sp.head, sp.tail);
-  return hipGetLastError();
-}
-
-// The compile-time-count fold for the allreduce's own folds (sum of fp32 / int32 buckets, and
-// config 5's bf16 with fp32 accumulation) at 2-8 sources; other cases keep the runtime loop.
-// Returns hipErrorNotSupported when it has no instance for the call.
-template <typename E, int OP, bool ACC32>
-hipError_t launch_fold_fixed(void* dst, const void* const* srcs, int nsrc, size_t n,
-                             hipStream_t s) {
-  if constexpr (OP == kSum && (ACC32 || std::is_same_v<E, float> || std::is_same_v<E, int32_t>)) {
-    constexpr int MAP = ACC32 ? 0 : 1;
-    switch (nsrc) {
-      case 2: return launch_fold_np<E, OP, ACC32, MAP, 2>(dst, srcs, n, s);
-      case 3: return launch_fold_np<E, OP, ACC32, MAP, 3>(dst, srcs, n, s);
-      case 4: return launch_fold_np<E, OP, ACC32, MAP, 4>(dst, srcs, n, s);
-      case 5: return launch_fold_np<E, OP, ACC32, MAP, 5>(dst, srcs, n, s);
-      case 6: return launch_fold_np<E, OP, ACC32, MAP, 6>(dst, srcs, n, s);
-      case 7: return launch_fold_np<E, OP, ACC32, MAP, 7>(dst, srcs, n, s);
-      case 8: return launch_fold_np<E, OP, ACC32, MAP, 8>(dst, srcs, n, s);
-    }
-  }
-  return hipErrorNotSupported;
-}
-
 // Fold variants (hydra_set_variant, measurement only; 0 = default): 1 plain loads, grid capped
 // at 8 blocks/CU; 2 nontemporal loads, capped; 3 nontemporal, one block per 256 vectors;
-// 4-7 = 1, plain full grid, 3, 2 with XCD-contiguous blocks; 8 the compile-time-count fold
-// (launch_fold_fixed) where it has an instance.
+// 4-7 = 1, plain full grid, 3, 2 with XCD-contiguous blocks.
 template <typename E, int OP, bool ACC32>
 hipError_t launch_fold_t(void* dst, const void* const* srcs, int nsrc, size_t n, hipStream_t s) {
-  const int variant = current_variant();
-  if (variant == 8) {
-    const hipError_t e = launch_fold_fixed<E, OP, ACC32>(dst, srcs, nsrc, n, s);
-    if (e != hipErrorNotSupported) return e;
-  }
-  switch (variant) {
+  switch (current_variant()) {
     case 1: return launch_fold_v<E, OP, ACC32, false>(dst, srcs, nsrc, n, s, 8);
     case 2: return launch_fold_v<E, OP, ACC32, true>(dst, srcs, nsrc, n, s, 8);
     case 3: return launch_fold_v<E, OP, ACC32, true>(dst, srcs, nsrc, n, s, 0);

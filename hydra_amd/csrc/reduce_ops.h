@@ -237,42 +237,6 @@ __device__ __forceinline__ u32x4 fold_vec(const FoldSrcs& S, int nsrc, size_t of
   }
 }
 
-// The same fold over a compile-time source count: all NP loads issued before the first add
-// (the runtime loop above waits for each source's load before issuing the next one).
-template <typename E, int OP, bool ACC32, bool NT, int NP>
-__device__ __forceinline__ u32x4 fold_vec_np(const FoldSrcs& S, size_t off) {
-  u32x4 x[NP];
-#pragma unroll
-  for (int j = 0; j < NP; j++) x[j] = ld_src<NT>(S.p[j] + off);
-  if constexpr (ACC32) {
-    static_assert(sizeof(E) == 2, "ACC32 is the bf16 form");
-    float acc[8];
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      acc[2 * k] = bitsf(x[NP - 1][k] << 16);
-      acc[2 * k + 1] = bitsf(x[NP - 1][k] & 0xffff0000u);
-    }
-#pragma unroll
-    for (int j = NP - 2; j >= 0; j--) {
-#pragma unroll
-      for (int k = 0; k < 4; k++) {
-        acc[2 * k] = fop<OP>(bitsf(x[j][k] << 16), acc[2 * k]);
-        acc[2 * k + 1] = fop<OP>(bitsf(x[j][k] & 0xffff0000u), acc[2 * k + 1]);
-      }
-    }
-    u32x4 o;
-#pragma unroll
-    for (int k = 0; k < 4; k++)
-      o[k] = (uint32_t)f2bf(acc[2 * k]) | ((uint32_t)f2bf(acc[2 * k + 1]) << 16);
-    return o;
-  } else {
-    u32x4 acc = x[NP - 1];
-#pragma unroll
-    for (int j = NP - 2; j >= 0; j--) acc = vapply<E, OP>(x[j], acc, x[j]);
-    return acc;
-  }
-}
-
 template <typename E, int OP, bool ACC32>
 __device__ __forceinline__ E fold_elem(const FoldSrcs& S, int nsrc, ptrdiff_t i) {
   if constexpr (ACC32) {

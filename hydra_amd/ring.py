@@ -967,7 +967,7 @@ def _peer_leg(make_peer, pg, run, measure, sync, dev, rank, world, xs, exp, x, x
         if not leg["full_size_exact"]:
             return None
         tune = {}
-        for wg in (0, 256, 128):  # 0: derived from the bucket
+        for wg in (0, 128, 64):  # 0: derived from the bucket (one per slab, <= 256)
             tw = None
             try:
                 def tstep(wg=wg):
