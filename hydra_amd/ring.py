@@ -519,11 +519,18 @@ def bench_allreduce(args, dev, make_comm=None, sync=None, cpu_baseline=None,
     n = args.elements
     algo = getattr(args, "algo", "auto")
 
+    # ranks sharing ONE GPU (the rehearsal, HYDRA_BENCH_SHARED_GPU=1): the peer kernel's
+    # barriers need every rank's grid resident at once, and a GPU holds 512 of its workgroups
+    # (two per CU at its register count), so each rank's grid is capped at 512 / world there
+    shared_cap = max(1, 512 // world) if os.environ.get("HYDRA_BENCH_SHARED_GPU") == "1" else 0
+
     def run(a, t, ch=0, **kw):
         """ch: RCCL plans' pipelining chunk in bytes; peer algorithms' workgroup count."""
         if a in _lib.PEER_ALGOS:
             if pg["peer"] is None:
                 raise HydraError(3, f"peer group unavailable: {pg['err']}")
+            if shared_cap:
+                ch = min(ch, shared_cap) if ch else shared_cap
             pg["peer"].set_option(_lib.PEER_OPT_BLOCKS, ch)
             pg["peer"].allreduce_(t, algo=a, **kw)
         else:
@@ -839,6 +846,8 @@ def bench_allreduce(args, dev, make_comm=None, sync=None, cpu_baseline=None,
         #    with an error word, hydra_peer_error) and every step's outcome is agreed over the
         #    ranks: a failure becomes an error entry of this leg, never a failed line.
         peer_leg.update(_peer_eligibility(args, comm_seen, world, dev))
+        if shared_cap:
+            peer_leg["shared_gpu_workgroup_cap"] = shared_cap
         if peer_leg["enabled"]:
             pr = _peer_leg(make_peer, pg, run, measure, sync, dev, rank, world, xs, exp, x, x0,
                            full_exp, tp, peer_leg)
