@@ -2,6 +2,7 @@
 #include "resident.h"
 
 #include <algorithm>
+#include <type_traits>
 
 #include "reduce_kernels.h"
 #include "reduce_ops.h"
@@ -44,65 +45,97 @@ __device__ __forceinline__ void res_edges(const ResSeg& g, int t) {
   }
 }
 
-// This workgroup's tiles first, first + stride, ... of the call, kResidentBatch at a time: all
-// of a batch's loads are issued before its first store, so a workgroup with several tiles pays
-// one PCIe round trip per batch rather than per tile (host operands are latency-bound).
+// Global-address-space 16-B accesses: the descriptor's pointers come from LDS, so plain
+// dereferences compile to FLAT instructions, which count on lgkmcnt as well -- and every LDS
+// read of the next tile's descriptor then waited for the previous tile's loads (round 4's kernel
+// kept one tile in flight per wave).  Host-mapped and device operands are both global memory.
+typedef __attribute__((address_space(1))) const u32x4_u* gld_t;
+typedef __attribute__((address_space(1))) u32x4* gst_t;
+__device__ __forceinline__ u32x4 ld_g(const char* p) { return *(gld_t)(p); }
+__device__ __forceinline__ void st_g(char* p, u32x4 v) { *(gst_t)(p) = v; }
+
+// This workgroup's tiles first, first + stride, ... of the call, B at a time: every tile's
+// pointers first (the LDS descriptor reads), then all of the batch's loads, then the stores, so
+// a workgroup with several tiles pays one PCIe round trip per batch rather than per tile (host
+// operands are latency-bound).  The loads are unconditional -- a lane with nothing to do in a
+// tile reads `dummy` (16 B of device memory) and stores nothing -- so no register merge at a
+// branch join waits for them either.
 template <int B, typename E, int OP>
-__device__ __forceinline__ void res_run(const ResDesc& D, uint32_t first, uint32_t stride,
-                                        int t) {
+__device__ __forceinline__ void res_run(const ResDesc& D, uint32_t first, uint32_t stride, int t,
+                                        const char* dummy) {
+  constexpr bool kF16 = std::is_same_v<E, f16_t>;  // only float16 reads c's old bits (c_old)
   for (uint32_t base = first; base < D.tiles; base += stride * B) {
-    u32x4 x[B], y[B], z[B];
+    const char* pa[B];
+    const char* pb[B];
+    const char* pc[B];
     char* cp[B];
+    bool old_c[B];
 #pragma unroll
     for (int u = 0; u < B; u++) {
+      pa[u] = pb[u] = pc[u] = dummy;
       cp[u] = nullptr;
+      old_c[u] = false;
       const uint32_t tile = base + u * stride;
-      if (tile >= D.tiles) continue;
-      int k = 0;  // the last segment whose first tile is <= this tile (uniform)
-      for (int j = 1; j < D.count; j++)
-        if (D.s[j].tile0 <= tile) k = j;
-      const ResSeg& g = D.s[k];
-      const uint32_t lt = tile - g.tile0;
-      if (lt == 0 && (g.head | g.tail)) res_edges<E, OP>(g, t);
-      const size_t v = (size_t)lt * kBlock + t;
-      if (v < g.nvec) {
-        const size_t o = v * 16;
-        x[u] = ld_u(g.a + o);
-        y[u] = ld_u(g.b + o);
-        z[u] = g.c_old ? ld_u(g.c + o) : x[u];
-        cp[u] = g.c + o;
+      if (tile < D.tiles) {
+        int k = 0;  // the last segment whose first tile is <= this tile (uniform)
+        for (int j = 1; j < D.count; j++)
+          if (D.s[j].tile0 <= tile) k = j;
+        const ResSeg& g = D.s[k];
+        const uint32_t lt = tile - g.tile0;
+        if (lt == 0 && (g.head | g.tail)) res_edges<E, OP>(g, t);
+        const size_t v = (size_t)lt * kBlock + t;
+        if (v < g.nvec) {
+          const size_t o = v * 16;
+          pa[u] = g.a + o;
+          pb[u] = g.b + o;
+          cp[u] = g.c + o;
+          if (kF16 && g.c_old) {
+            pc[u] = g.c + o;
+            old_c[u] = true;
+          }
+        }
       }
     }
+    u32x4 x[B], y[B], z[B];
 #pragma unroll
-    for (int u = 0; u < B; u++)
-      if (cp[u]) st_a(cp[u], vapply<E, OP>(x[u], y[u], z[u]));
+    for (int u = 0; u < B; u++) {
+      x[u] = ld_g(pa[u]);
+      y[u] = ld_g(pb[u]);
+      if constexpr (kF16) z[u] = ld_g(pc[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < B; u++) {
+      // the float16 store quirk compares with c's old bits: c's own when c != a (c_old), else a's
+      if (cp[u]) st_g(cp[u], vapply<E, OP>(x[u], y[u], (kF16 && old_c[u]) ? z[u] : x[u]));
+    }
   }
 }
 
 template <int B, typename E>
-__device__ __forceinline__ void res_op(const ResDesc& D, uint32_t first, uint32_t stride, int t) {
+__device__ __forceinline__ void res_op(const ResDesc& D, uint32_t first, uint32_t stride, int t,
+                                       const char* dummy) {
   switch (D.op) {
-    case kSum: res_run<B, E, kSum>(D, first, stride, t); break;
-    case kProduct: res_run<B, E, kProduct>(D, first, stride, t); break;
-    case kMax: res_run<B, E, kMax>(D, first, stride, t); break;
-    case kMin: res_run<B, E, kMin>(D, first, stride, t); break;
+    case kSum: res_run<B, E, kSum>(D, first, stride, t, dummy); break;
+    case kProduct: res_run<B, E, kProduct>(D, first, stride, t, dummy); break;
+    case kMax: res_run<B, E, kMax>(D, first, stride, t, dummy); break;
+    case kMin: res_run<B, E, kMin>(D, first, stride, t, dummy); break;
   }
 }
 
 template <int B>
 __device__ __forceinline__ void res_tiles(const ResDesc& D, uint32_t first, uint32_t stride,
-                                          int t) {
+                                          int t, const char* dummy) {
   switch (D.dtype) {
-    case kI8: res_op<B, int8_t>(D, first, stride, t); break;
-    case kU8: res_op<B, uint8_t>(D, first, stride, t); break;
-    case kI32: res_op<B, int32_t>(D, first, stride, t); break;
-    case kU32: res_op<B, uint32_t>(D, first, stride, t); break;
-    case kI64: res_op<B, int64_t>(D, first, stride, t); break;
-    case kU64: res_op<B, uint64_t>(D, first, stride, t); break;
-    case kF32: res_op<B, float>(D, first, stride, t); break;
-    case kF64: res_op<B, double>(D, first, stride, t); break;
-    case kF16: res_op<B, f16_t>(D, first, stride, t); break;
-    case kBF16: res_op<B, bf16_t>(D, first, stride, t); break;
+    case kI8: res_op<B, int8_t>(D, first, stride, t, dummy); break;
+    case kU8: res_op<B, uint8_t>(D, first, stride, t, dummy); break;
+    case kI32: res_op<B, int32_t>(D, first, stride, t, dummy); break;
+    case kU32: res_op<B, uint32_t>(D, first, stride, t, dummy); break;
+    case kI64: res_op<B, int64_t>(D, first, stride, t, dummy); break;
+    case kU64: res_op<B, uint64_t>(D, first, stride, t, dummy); break;
+    case kF32: res_op<B, float>(D, first, stride, t, dummy); break;
+    case kF64: res_op<B, double>(D, first, stride, t, dummy); break;
+    case kF16: res_op<B, f16_t>(D, first, stride, t, dummy); break;
+    case kBF16: res_op<B, bf16_t>(D, first, stride, t, dummy); break;
   }
 }
 
@@ -159,6 +192,8 @@ __global__ __launch_bounds__(kBlock) void k_resident(ResCtl* h, ResDev* d, uint6
   __shared__ ResDesc s_desc;
   const int t = threadIdx.x;
   const uint64_t gtag = gen & ((uint64_t(1) << (64 - kTagShift)) - 1);
+  // 16 readable bytes of device memory for the loads of lanes without an element (res_run)
+  const char* dummy = reinterpret_cast<const char*>(&d->job);
   uint64_t job = 0;  // the last job published (workgroup 0) / seen (the others)
   uint64_t beat = 0;  // workgroup 0: calls served by this instance
   // workgroup 0, wave 0: lane i < kResidentSlots tracks slot i's last served sequence number
@@ -297,7 +332,7 @@ __global__ __launch_bounds__(kBlock) void k_resident(ResCtl* h, ResDev* d, uint6
       continue;
     }
     if (mode == 1) {  // workgroup 0 alone: every tile here, then the slot's completion word
-      res_tiles<B>(s_desc, 0, 1, t);
+      res_tiles<B>(s_desc, 0, 1, t, dummy);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (t == 0) {
@@ -316,7 +351,7 @@ __global__ __launch_bounds__(kBlock) void k_resident(ResCtl* h, ResDev* d, uint6
       for (int q = t; q < kDescWords; q += kBlock) dst[q] = ld_agent(src + kHead + q);
     }
     __syncthreads();
-    res_tiles<B>(s_desc, blockIdx.x, s_nwg, t);
+    res_tiles<B>(s_desc, blockIdx.x, s_nwg, t, dummy);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (t == 0) {
