@@ -332,6 +332,7 @@ __global__ __launch_bounds__(kBlock) void k_resident(ResCtl* h, ResDev* d, uint6
       continue;
     }
     if (mode == 1) {  // workgroup 0 alone: every tile here, then the slot's completion word
+      // (<= solo tiles, B of them in flight at once: one PCIe round trip for a 4-tile call)
       res_tiles<B>(s_desc, 0, 1, t, dummy);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
@@ -351,7 +352,10 @@ __global__ __launch_bounds__(kBlock) void k_resident(ResCtl* h, ResDev* d, uint6
       for (int q = t; q < kDescWords; q += kBlock) dst[q] = ld_agent(src + kHead + q);
     }
     __syncthreads();
-    res_tiles<B>(s_desc, blockIdx.x, s_nwg, t, dummy);
+    // a published job: one tile at a time per wave -- its store then overlaps the next tile's
+    // loads on the full-duplex link; batching B tiles' loads ahead of their stores measured
+    // 2-9 % slower for jobs of 16 tiles and up (profiles/r05o_resident_batch_ab.json)
+    res_tiles<1>(s_desc, blockIdx.x, s_nwg, t, dummy);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (t == 0) {
