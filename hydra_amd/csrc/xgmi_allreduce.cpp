@@ -199,7 +199,7 @@ int validate_plan(const std::vector<hydra::PlanOp>& plan, int nranks, size_t es,
 struct hydra_comm {
   int rank = 0, nranks = 1, device = 0;
   bool aborted = false;  // hydra_comm_wait timed out: nccl was aborted
-  bool ran = false;      // a plan ran: ev_ks marks the end of its folds (scratch reads)
+  bool ran = false;      // the last plan ran eagerly: ev_ks marks the end of its folds
   ncclComm_t nccl = nullptr;
   hipStream_t cs = nullptr, ks = nullptr;  // comm stream, compute stream
   void* scratch = nullptr;
@@ -401,8 +401,8 @@ int run_plan_rccl(hydra_comm* c, int op, int dtype, bool acc32, char* user, hipE
   // capture: a captured graph orders its own nodes, and may not wait on an outside event.)
   hipStreamCaptureStatus cs_state = hipStreamCaptureStatusNone;
   HIP_TRY(hipStreamIsCapturing(user_st, &cs_state));
-  if (c->ran && cs_state == hipStreamCaptureStatusNone)
-    HIP_TRY(hipStreamWaitEvent(c->cs, c->ev_ks, 0));
+  const bool capturing = cs_state != hipStreamCaptureStatusNone;
+  if (c->ran && !capturing) HIP_TRY(hipStreamWaitEvent(c->cs, c->ev_ks, 0));
   size_t i = 0;
   while (i < ops.size()) {
     const hydra::PlanOp& o = ops[i];
@@ -467,7 +467,7 @@ int run_plan_rccl(hydra_comm* c, int op, int dtype, bool acc32, char* user, hipE
   }
   HIP_TRY(hipEventRecord(c->ev_cs, c->cs));
   HIP_TRY(hipEventRecord(c->ev_ks, c->ks));
-  c->ran = true;
+  c->ran = !capturing;  // (an ev_ks recorded inside a capture is a graph node, not a marker)
   return HYDRA_OK;
 }
 
