@@ -501,6 +501,14 @@ def test_executor_graph_replay(gpu, O):
         torch.cuda.synchronize()
         assert np.array_equal(t.cpu().numpy().view(np.uint32), exp.view(np.uint32))
         assert np.array_equal(u.cpu().numpy().view(np.uint32), x.view(np.uint32))
+        # eager calls after the captured one, on two different streams (the executor orders
+        # its scratch across calls only after eager calls: a captured ev_ks is a graph node)
+        for k, st in enumerate((torch.cuda.Stream(gpu), torch.cuda.Stream(gpu))):
+            t.copy_(xin)
+            torch.cuda.synchronize()
+            comm.run_plan_(ops, t, 2 * B, op="max", stream=st.cuda_stream)
+            st.synchronize()
+            assert np.array_equal(t.cpu().numpy().view(np.uint32), exp.view(np.uint32)), k
     finally:
         comm.close()
 
