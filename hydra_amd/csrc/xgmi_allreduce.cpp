@@ -1113,8 +1113,15 @@ int hydra_comm_run_plan(hydra_comm_t c, const hydra_plan_op_t* ops, size_t nops,
   rc = ensure_events(c, c->plan.size());
   if (rc) return rc;
   hipStream_t st = static_cast<hipStream_t>(stream);
-  // deterministic scratch for the hook (slots a 1-rank collective leaves untouched read as 0)
-  if (scratch_bytes) HIP_TRY(hipMemsetAsync(c->scratch, 0, scratch_bytes, st));
+  // deterministic scratch for the hook (slots a 1-rank collective leaves untouched read as 0),
+  // after the previous eager call's folds are done reading it (that call may be on another
+  // stream)
+  if (scratch_bytes) {
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    HIP_TRY(hipStreamIsCapturing(st, &cap));
+    if (c->ran && cap == hipStreamCaptureStatusNone) HIP_TRY(hipStreamWaitEvent(st, c->ev_ks, 0));
+    HIP_TRY(hipMemsetAsync(c->scratch, 0, scratch_bytes, st));
+  }
   if ((rc = prof_begin(c, st))) return rc;
   HIP_TRY(hipEventRecord(c->ev_start, st));
   rc = run_plan_rccl(c, op, dtype, (flags & HYDRA_ACC_F32) != 0, static_cast<char*>(buf),
