@@ -976,7 +976,12 @@ def _peer_leg(make_peer, pg, run, measure, sync, dev, rank, world, xs, exp, x, x
         if not leg["full_size_exact"]:
             return None
         tune = {}
-        for wg in (0, 128, 64):  # 0: derived from the bucket (one per slab, <= 256)
+        # 0: derived from the bucket (one per slab, <= 256, one per CU).  With a GPU per rank,
+        # 512 too: two per CU, still all resident at the fold's register count (peer_allreduce.cpp),
+        # twice the remote loads in flight for xGMI's longer read latency.  Ranks sharing one GPU
+        # (the rehearsal) are capped at 512 / world by run(), so 512 is not a candidate there.
+        cands = (0, 128, 64) if leg.get("shared_gpu_workgroup_cap") else (0, 512, 128, 64)
+        for wg in cands:
             tw = None
             try:
                 def tstep(wg=wg):

@@ -30,6 +30,18 @@ def inputs(case, P, r):
         return v.view(np.uint16).copy()
     if kind == "bf16":
         return synth.bf16_bits(synth.uniform_f32(n, 100 + r) * 4)
+    if kind == "typed":  # every other Gloo element type: full-range integers (the sums wrap),
+        # fp64 at stress_f32's rank-dependent scales (fold-order-sensitive)
+        rng = np.random.default_rng(7000 + 31 * r)
+        dt = np.dtype(case["np"])
+        if dt.kind in "iu":
+            info = np.iinfo(dt)
+            return rng.integers(info.min, info.max, n, dtype=dt, endpoint=True)
+        return rng.uniform(-1, 1, n) * 2.0 ** ((3 * r) % 17)
+    if kind == "bf16_native":  # bf16 arithmetic (each hop rounds to bf16; no ACC_F32)
+        return synth.bf16_bits(synth.uniform_f32(n, 300 + r) * 8)
+    if kind == "bf16_cancel":  # config 5's fold-order stress (the bf16 result shows the order)
+        return synth.bf16_bits(synth.stress_cancel_at(P, r, np.arange(n, dtype=np.int64)))
     raise ValueError(kind)
 
 

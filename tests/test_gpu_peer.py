@@ -2,8 +2,10 @@
 hipIpc handles, one kernel per allreduce reading the peers' data directly.  On the one-GPU box
 all ranks share cuda:0 (IPC across processes on one device: the same handles, signal flags,
 system-scope fences and per-workgroup barriers the xGMI node uses).  Bar: bit-exact vs the
-reference ring (oracle) for fp32 (fold-order-sensitive inputs), int32 and float16; bf16 with
-fp32 accumulation within one bf16 rounding of the fp64 sum, identical on every rank."""
+reference ring (oracle) for every Gloo element type (fp32 and fp64 on fold-order-sensitive
+inputs, full-range integers that wrap, float16 with its store quirk) and hydra's bf16; bf16 with
+fp32 accumulation bit-exact vs the reference ring's fp32 fold + one rounding on config 5's
+order-sensitive values (plus a tolerance check on plain uniform values)."""
 import json
 import os
 import socket
@@ -14,6 +16,7 @@ import numpy as np
 import pytest
 
 from hydra_amd import _lib, synth
+from peer_worker import inputs
 
 pytestmark = pytest.mark.gpu
 
@@ -70,6 +73,18 @@ def expected(O, c, P):
     if c["data"] == "f16":
         return O.ring_result(f16_inputs(P, n), c.get("ms") or (1 << 20),
                              dtype_code=_lib.FLOAT16).view(np.uint8)
+    if c["data"] in ("typed", "bf16_native"):  # the worker's own generator, the oracle's ring
+        code = c["dtype"] if c["data"] == "bf16_native" else None
+        xs = [inputs(c, P, r) for r in range(P)]
+        return O.ring_result(xs, c.get("ms") or (1 << 20), kind=c.get("op", "sum"),
+                             dtype_code=code).view(np.uint8)
+    if c["data"] == "bf16_cancel":  # the reference ring's fp32 fold on the widened values,
+        # bf16 block geometry, one RNE rounding (tests/fold_expect.py, pinned in test_oracle.py)
+        from fold_expect import bf16_acc32_expected
+
+        exp, _, _ = bf16_acc32_expected(O, P, n, np.arange(n, dtype=np.int64),
+                                        c.get("ms") or (1 << 20))
+        return exp.view(np.uint8)
     raise ValueError(c["data"])
 
 
@@ -107,6 +122,29 @@ def cases_for(P):
     cs.append(dict(name="streams1", algo="peer1", data="streams", dtype=F32, n=30011, iters=8))
     cs.append(dict(name="bf16_acc32", algo="peer2", data="bf16", dtype=BF16, n=1 << 20,
                    flags=_lib.ACC_F32))
+    # config 5's arithmetic bit-exact: fold-order-sensitive bf16 values, fp32 accumulation in
+    # the reference order, one rounding (both schedules; 2P-misaligned sizes, small segments)
+    for algo, n, ms, off in (("peer2", (1 << 20) + 3, 0, 2), ("peer2", 100003, 4096, 0),
+                             ("peer1", 30011, 1024, 6)):
+        cs.append(dict(name=f"{algo}_bf16_acc32_cancel_{n}", algo=algo, data="bf16_cancel",
+                       dtype=BF16, n=n, ms=ms, offset_bytes=off, flags=_lib.ACC_F32))
+    # every other element type the kernels instantiate, both schedules
+    for nm, npt, code in (("i8", "int8", _lib.INT8), ("u8", "uint8", _lib.UINT8),
+                          ("i64", "int64", _lib.INT64), ("u64", "uint64", _lib.UINT64),
+                          ("f64", "float64", _lib.FLOAT64)):
+        for algo, n, ms, off in (("peer2", 65543, 4096, 8), ("peer1", 4099, 128, 0)):
+            cs.append(dict(name=f"{algo}_{nm}_{n}", algo=algo, data="typed", np=npt, dtype=code,
+                           n=n, ms=ms, offset_bytes=off))
+    cs.append(dict(name="peer2_i8_max", algo="peer2", data="typed", np="int8", dtype=_lib.INT8,
+                   n=70001, ms=4096, op="max"))
+    cs.append(dict(name="peer2_u64_min", algo="peer2", data="typed", np="uint64",
+                   dtype=_lib.UINT64, n=30011, ms=4096, op="min"))
+    cs.append(dict(name="peer2_f64_product", algo="peer2", data="typed", np="float64",
+                   dtype=_lib.FLOAT64, n=30011, ms=4096, op="product"))
+    cs.append(dict(name="peer2_bf16_native", algo="peer2", data="bf16_native", dtype=BF16,
+                   n=100003, ms=4096, offset_bytes=2))
+    cs.append(dict(name="peer1_bf16_native", algo="peer1", data="bf16_native", dtype=BF16,
+                   n=20011, ms=1024))
     cs.append(dict(name="reregister", algo="peer2", data="reregister", dtype=F32,
                    n=(1 << 20) + 3, iters=12))
     return cs
