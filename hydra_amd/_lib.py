@@ -143,7 +143,9 @@ def build(force: bool = False) -> str:
     """Compile libhydra_hip.so for gfx950 (hipcc cross-compiles without a GPU)."""
     if force:
         subprocess.check_call(["make", "-s", "-C", CSRC, "clean"])
-    subprocess.check_call(["make", "-s", "-j4", "-C", CSRC])
+    # the peer kernels build as one translation unit per op: -j up to 8 runs them side by side
+    jobs = max(1, min(8, os.cpu_count() or 1))
+    subprocess.check_call(["make", "-s", f"-j{jobs}", "-C", CSRC])
     return LIB_PATH
 
 

@@ -1,0 +1,309 @@
+// peer_fold.h -- the peer-access allreduce's device code (fold, copy, the two schedules), as
+// templates.  Included by the per-op translation units only (peer_kernels_{sum,product,max,
+// min}.hip and, for the measurement variants, peer_kernels.hip): each compiles one reduction
+// op's kernels, so the ~100 instantiations build in parallel instead of one 5-minute file.
+// The schedules and their protocol are described in peer_kernels.hip.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "errors.h"
+#include "peer_kernels.h"
+#include "peer_sync.h"
+#include "reduce_kernels.h"
+#include "reduce_ops.h"
+
+namespace hydra {
+namespace {
+
+// Measurement variants (hydra_set_variant 2001..2007, f32 sum only; 0 = the shipped kernel):
+// bit 0 nontemporal loads, bit 1 nontemporal stores, bit 2 twice the loads in flight.
+template <int V>
+__device__ __forceinline__ u32x4 pld(const char* p) {
+  if constexpr ((V & 1) != 0) return ld<kNT>(p, rsrc<kNT>(nullptr, 0), 0);
+  else return ld_u(p);
+}
+template <int V>
+__device__ __forceinline__ void pst(char* p, u32x4 v) {
+  if constexpr ((V & 2) != 0) st<kNT>(p, rsrc<kNT>(nullptr, 0), 0, v);
+  else st_a(p, v);
+}
+
+// dst = fold of NP 16-B sources in the reference order: v[NP-1] innermost,
+// acc = v[j] op acc for j = NP-2 .. 0 (c = local + received, in place on local).  NP is a
+// compile-time count: with a runtime count every load sat behind a scalar branch, and the
+// compiler waited for each load before issuing the next (one load in flight per wave).
+template <typename E, int OP, bool ACC32, int NP>
+__device__ __forceinline__ u32x4 fold_n(const u32x4 (&v)[NP]) {
+  if constexpr (ACC32) {
+    float a[8];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      a[2 * k] = bitsf(v[NP - 1][k] << 16);
+      a[2 * k + 1] = bitsf(v[NP - 1][k] & 0xffff0000u);
+    }
+#pragma unroll
+    for (int j = NP - 2; j >= 0; j--) {
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        a[2 * k] = fop<OP>(bitsf(v[j][k] << 16), a[2 * k]);
+        a[2 * k + 1] = fop<OP>(bitsf(v[j][k] & 0xffff0000u), a[2 * k + 1]);
+      }
+    }
+    u32x4 o;
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+      o[k] = (uint32_t)f2bf(a[2 * k]) | ((uint32_t)f2bf(a[2 * k + 1]) << 16);
+    return o;
+  } else {
+    u32x4 acc = v[NP - 1];
+#pragma unroll
+    for (int j = NP - 2; j >= 0; j--) acc = vapply<E, OP>(v[j], acc, v[j]);
+    return acc;
+  }
+}
+
+struct PeerSrcs {
+  const char* p[kPeerMaxRanks];
+};
+
+// one element, same order as fold_n (static source indices: no scratch spills)
+template <typename E, int OP, bool ACC32>
+__device__ __forceinline__ E fold_one(const PeerSrcs& S, int nsrc, size_t i) {
+  if constexpr (ACC32) {
+    float a = 0.f;
+#pragma unroll
+    for (int j = kPeerMaxRanks - 1; j >= 0; j--) {
+      if (j < nsrc) {
+        const float x = bf2f(reinterpret_cast<const uint16_t*>(S.p[j])[i]);
+        a = (j == nsrc - 1) ? x : fop<OP>(x, a);
+      }
+    }
+    E r;
+    const uint16_t h = f2bf(a);
+    __builtin_memcpy(&r, &h, 2);
+    return r;
+  } else {
+    E acc = reinterpret_cast<const E*>(S.p[0])[i];
+#pragma unroll
+    for (int j = kPeerMaxRanks - 1; j >= 0; j--) {
+      if (j < nsrc) {
+        const E x = reinterpret_cast<const E*>(S.p[j])[i];
+        acc = (j == nsrc - 1) ? x : Elem<E, OP>::apply(x, acc, x);
+      }
+    }
+    return acc;
+  }
+}
+
+// One workgroup folds `count` elements: dst[i] = fold(S.p[0][i], ..., S.p[NP-1][i]).
+// Aligned on dst (16 B); sources may sit at any element alignment (gfx950 unaligned mode).
+// The main loop issues PU x NP unpredicated 16-B loads per lane before its first store (15-32
+// in flight: the grid is small -- every workgroup pays barriers -- so the depth has to come from
+// each wave; round 5's A/B on one GPU, profiles/r05k_*: twice the r05j depth was as fast or
+// faster at every size >= 16 Mi); the last partial round is predicated.
+template <typename E, int OP, bool ACC32, int V, int NP>
+__device__ __forceinline__ void slab_fold_n(char* dst, const PeerSrcs& S, size_t count) {
+  // (1-byte elements: half the depth -- their per-byte max / min unpack needs the registers)
+  constexpr int PU = ((V & 4) ? 2 : 1) * (NP >= 4 ? 4 : 16 / NP) / (sizeof(E) == 1 ? 2 : 1);
+  constexpr int N = Vec<E>::N;
+  const int t = threadIdx.x;
+  size_t head = ((16 - (reinterpret_cast<uintptr_t>(dst) & 15)) & 15) / sizeof(E);
+  if (head > count) head = count;
+  const size_t nvec = (count - head) / N;
+  const size_t tail = count - head - nvec * N;
+  E* de = reinterpret_cast<E*>(dst);
+  if ((size_t)t < head) de[t] = fold_one<E, OP, ACC32>(S, NP, t);
+  if ((size_t)t < tail) {
+    const size_t i = head + nvec * N + t;
+    de[i] = fold_one<E, OP, ACC32>(S, NP, i);
+  }
+  const char* src[NP];
+#pragma unroll
+  for (int j = 0; j < NP; j++) src[j] = S.p[j] + head * sizeof(E);
+  char* out = dst + head * sizeof(E);
+  constexpr size_t kStep = (size_t)kBlock * PU;
+  const size_t full = nvec / kStep * kStep;
+  for (size_t v0 = 0; v0 < full; v0 += kStep) {
+    u32x4 r[PU][NP];
+#pragma unroll
+    for (int u = 0; u < PU; u++) {
+      const size_t o = (v0 + (size_t)u * kBlock + t) * 16;
+#pragma unroll
+      for (int j = 0; j < NP; j++) r[u][j] = pld<V>(src[j] + o);
+    }
+#pragma unroll
+    for (int u = 0; u < PU; u++)
+      pst<V>(out + (v0 + (size_t)u * kBlock + t) * 16, fold_n<E, OP, ACC32, NP>(r[u]));
+  }
+  for (size_t v = full + t; v < nvec; v += kBlock) {  // the last partial round
+    u32x4 r[NP];
+#pragma unroll
+    for (int j = 0; j < NP; j++) r[j] = pld<V>(src[j] + v * 16);
+    pst<V>(out + v * 16, fold_n<E, OP, ACC32, NP>(r));
+  }
+}
+
+template <typename E, int OP, bool ACC32, int V = 0>
+__device__ __forceinline__ void slab_fold(char* dst, const PeerSrcs& S, int nsrc, size_t count) {
+  switch (nsrc) {  // uniform over the grid: one branch per slab, none in the loop
+    case 1: slab_fold_n<E, OP, ACC32, V, 1>(dst, S, count); break;
+    case 2: slab_fold_n<E, OP, ACC32, V, 2>(dst, S, count); break;
+    case 3: slab_fold_n<E, OP, ACC32, V, 3>(dst, S, count); break;
+    case 4: slab_fold_n<E, OP, ACC32, V, 4>(dst, S, count); break;
+    case 5: slab_fold_n<E, OP, ACC32, V, 5>(dst, S, count); break;
+    case 6: slab_fold_n<E, OP, ACC32, V, 6>(dst, S, count); break;
+    case 7: slab_fold_n<E, OP, ACC32, V, 7>(dst, S, count); break;
+    case 8: slab_fold_n<E, OP, ACC32, V, 8>(dst, S, count); break;
+  }
+}
+
+// One workgroup copies `count` elements src -> dst (phase 2 / copy-back): raw 16-B vectors,
+// kCU of them per lane in flight (one source only, so deeper than the fold's kPU).
+constexpr int kCU = 16;
+template <typename E, int V = 0>
+__device__ __forceinline__ void slab_copy(char* dst, const char* src, size_t count) {
+  constexpr int CU = (V & 4) ? 2 * kCU : kCU;
+  constexpr int N = Vec<E>::N;
+  const int t = threadIdx.x;
+  size_t head = ((16 - (reinterpret_cast<uintptr_t>(dst) & 15)) & 15) / sizeof(E);
+  if (head > count) head = count;
+  const size_t nvec = (count - head) / N;
+  const size_t tail = count - head - nvec * N;
+  E* de = reinterpret_cast<E*>(dst);
+  const E* se = reinterpret_cast<const E*>(src);
+  if ((size_t)t < head) de[t] = se[t];
+  if ((size_t)t < tail) de[head + nvec * N + t] = se[head + nvec * N + t];
+  const size_t base = head * sizeof(E);
+  for (size_t v0 = 0; v0 < nvec; v0 += (size_t)kBlock * CU) {
+    u32x4 r[CU];
+#pragma unroll
+    for (int u = 0; u < CU; u++) {
+      const size_t v = v0 + (size_t)u * kBlock + t;
+      if (v < nvec) r[u] = pld<V>(src + base + v * 16);
+    }
+#pragma unroll
+    for (int u = 0; u < CU; u++) {
+      const size_t v = v0 + (size_t)u * kBlock + t;
+      if (v < nvec) pst<V>(dst + base + v * 16, r[u]);
+    }
+  }
+}
+
+// The group already failed (an earlier timeout here or on a peer): leave at once.
+__device__ __forceinline__ bool group_broken(const PeerSync& S) {
+  int bad = 0;
+  if (threadIdx.x == 0 && peer_aborted(S)) {
+    if (peer_ld(S.err) == 0) peer_st(S.err, kPeerErrAborted);
+    bad = 1;
+  }
+  return __syncthreads_or(bad) != 0;
+}
+
+template <typename E, int OP, bool ACC32, int V = 0>
+__global__ __launch_bounds__(kBlock) void k_peer_two_shot(PeerLaunch A) {
+  const size_t SL = A.slab_bytes / sizeof(E);
+  const PeerSync& Y = A.sync;
+  const int P = Y.P, r = Y.rank;
+  const uint32_t G = gridDim.x;
+  if (group_broken(Y)) return;
+  if (!peer_barrier(Y, 1)) return;  // every rank's bucket is ready
+  PeerSrcs S;
+  // phase 1: own block r, slabs k = b, b+G, ...; all P sources, in place
+  {
+    const size_t lo = A.lo[r], hi = A.lo[r + 1];
+    for (size_t k = blockIdx.x; lo + k * SL < hi; k += G) {
+      const size_t s = lo + k * SL;
+#pragma unroll
+      for (int j = 0; j < kPeerMaxRanks; j++)
+        if (j < P) S.p[j] = A.x[(r + j) % P] + s * sizeof(E);
+      slab_fold<E, OP, ACC32, V>(A.x[r] + s * sizeof(E), S, P, hi - s < SL ? hi - s : SL);
+    }
+  }
+  // workgroup b of every rank has finished ITS slabs (k = b mod G) of its own block
+  if (!peer_barrier(Y, 2)) return;
+  // phase 2: the same slab indices of every other block, pulled from their owners; the start
+  // peer rotates with b so the workgroups of one rank read from all P-1 links at once
+  for (int i = 0; i < P - 1; i++) {
+    const int q = (r + 1 + (int)((blockIdx.x + i) % (uint32_t)(P - 1))) % P;
+    const size_t lo = A.lo[q], hi = A.lo[q + 1];
+    for (size_t k = blockIdx.x; lo + k * SL < hi; k += G) {
+      const size_t s = lo + k * SL;
+      slab_copy<E, V>(A.x[r] + s * sizeof(E), A.x[q] + s * sizeof(E), hi - s < SL ? hi - s : SL);
+    }
+  }
+  // nobody leaves (and lets its caller overwrite the bucket) while a peer may still read it
+  peer_barrier(Y, 3);
+}
+
+template <typename E, int OP, bool ACC32, int V = 0>
+__global__ __launch_bounds__(kBlock) void k_peer_one_shot(PeerLaunch A) {
+  const size_t SL = A.slab_bytes / sizeof(E);
+  const PeerSync& Y = A.sync;
+  const int P = Y.P, r = Y.rank;
+  const uint32_t G = gridDim.x;
+  if (group_broken(Y)) return;
+  if (!peer_barrier(Y, 1)) return;
+  PeerSrcs S;
+  // slab list over all owner blocks: (q, k) enumerated block by block; slab w -> workgroup w%G
+  size_t w = 0;
+  for (int q = 0; q < P; q++) {
+    const size_t lo = A.lo[q], hi = A.lo[q + 1];
+    const size_t nsl = (hi - lo + SL - 1) / SL;
+    for (size_t k = 0; k < nsl; k++, w++) {
+      if (w % G != blockIdx.x) continue;
+      const size_t s = lo + k * SL;
+#pragma unroll
+      for (int j = 0; j < kPeerMaxRanks; j++)
+        if (j < P) S.p[j] = A.x[(q + j) % P] + s * sizeof(E);
+      slab_fold<E, OP, ACC32, V>(A.scratch + s * sizeof(E), S, P, hi - s < SL ? hi - s : SL);
+    }
+  }
+  // every rank's workgroup b has read its slabs of every bucket -> safe to overwrite ours
+  if (!peer_barrier(Y, 2)) return;
+  w = 0;
+  for (int q = 0; q < P; q++) {
+    const size_t lo = A.lo[q], hi = A.lo[q + 1];
+    const size_t nsl = (hi - lo + SL - 1) / SL;
+    for (size_t k = 0; k < nsl; k++, w++) {
+      if (w % G != blockIdx.x) continue;
+      const size_t s = lo + k * SL;
+      slab_copy<E, V>(A.x[r] + s * sizeof(E), A.scratch + s * sizeof(E), hi - s < SL ? hi - s : SL);
+    }
+  }
+}
+
+template <typename E, int OP, bool ACC32, int V = 0>
+hipError_t launch_t(int algo, const PeerLaunch& A, unsigned grid, hipStream_t s) {
+  if (algo == kPeerOneShot)
+    hipLaunchKernelGGL((k_peer_one_shot<E, OP, ACC32, V>), dim3(grid), dim3(kBlock), 0, s, A);
+  else
+    hipLaunchKernelGGL((k_peer_two_shot<E, OP, ACC32, V>), dim3(grid), dim3(kBlock), 0, s, A);
+  return hipGetLastError();
+}
+
+// every dtype of one op (the per-op translation units' whole content)
+template <int OP>
+hipError_t dispatch(int algo, int dtype, bool acc32, const PeerLaunch& A, unsigned grid,
+                    hipStream_t s) {
+  if (acc32) {
+    if (dtype != kBF16) return hipErrorInvalidValue;
+    return launch_t<bf16_t, OP, true>(algo, A, grid, s);
+  }
+  switch (dtype) {
+    case kI8: return launch_t<int8_t, OP, false>(algo, A, grid, s);
+    case kU8: return launch_t<uint8_t, OP, false>(algo, A, grid, s);
+    case kI32: return launch_t<int32_t, OP, false>(algo, A, grid, s);
+    case kU32: return launch_t<uint32_t, OP, false>(algo, A, grid, s);
+    case kI64: return launch_t<int64_t, OP, false>(algo, A, grid, s);
+    case kU64: return launch_t<uint64_t, OP, false>(algo, A, grid, s);
+    case kF32: return launch_t<float, OP, false>(algo, A, grid, s);
+    case kF64: return launch_t<double, OP, false>(algo, A, grid, s);
+    case kF16: return launch_t<f16_t, OP, false>(algo, A, grid, s);
+    case kBF16: return launch_t<bf16_t, OP, false>(algo, A, grid, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+}  // namespace
+}  // namespace hydra

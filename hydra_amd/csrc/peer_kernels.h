@@ -23,4 +23,14 @@ struct PeerLaunch {
 hipError_t launch_peer(int algo, int op, int dtype, bool acc32, const PeerLaunch& A,
                        unsigned grid, hipStream_t s);
 
+// one reduction op's kernels, every dtype (peer_kernels_<op>.hip; launch_peer dispatches)
+hipError_t launch_peer_sum(int algo, int dtype, bool acc32, const PeerLaunch& A, unsigned grid,
+                           hipStream_t s);
+hipError_t launch_peer_product(int algo, int dtype, bool acc32, const PeerLaunch& A, unsigned grid,
+                               hipStream_t s);
+hipError_t launch_peer_max(int algo, int dtype, bool acc32, const PeerLaunch& A, unsigned grid,
+                           hipStream_t s);
+hipError_t launch_peer_min(int algo, int dtype, bool acc32, const PeerLaunch& A, unsigned grid,
+                           hipStream_t s);
+
 }  // namespace hydra

@@ -3,7 +3,7 @@
 The MI355X-first form of gloo::allreduce RING (allreduce.cc:147-422) for device-resident
 buckets: every rank maps the other ranks' buckets by hipIpc handles, and ONE gfx950 kernel per
 allreduce reads the peers' blocks straight over xGMI and folds them in the reference's order
-(hydra_amd/csrc/peer_kernels.hip), so the result is bit-identical to RING / DIRECT.
+(hydra_amd/csrc/peer_fold.h), so the result is bit-identical to RING / DIRECT.
 
 Handle exchange rides on torch.distributed (all_gather_object: gloo or nccl process groups);
 the library itself only produces and consumes byte blobs.
