@@ -29,3 +29,29 @@ def bf16_acc32_expected(O, P, n, idx, max_segment=1 << 20, gen=synth.stress_canc
             acc = O.acc_bf16_f32(acc, vals[(q + d) % P][sel])
         out[sel] = synth.bf16_bits(acc)
     return out, vals, (ns, sb, S)
+
+
+def sample_indices(n, ns, seg, count=1 << 20, seed=55):
+    """>= `count` sorted element indices of an n-element bucket: every segment boundary's two
+    elements either side (ns segments of `seg` elements -- so every owner block's first and last
+    elements too), the bucket's ends, and `count` uniform random ones."""
+    edges = np.concatenate([np.arange(ns + 1, dtype=np.int64) * seg + d for d in (-2, -1, 0, 1)])
+    rnd = np.random.default_rng(seed).integers(0, n, count, dtype=np.int64)
+    idx = np.unique(np.concatenate([edges, rnd, [0, 1, n - 2, n - 1]]))
+    return idx[(idx >= 0) & (idx < n)]
+
+
+def device_bucket(gen, P, rank, n, dev, out_dtype, chunk=16 << 20, out=None):
+    """gen(P, rank, idx) (synth.stress_at / stress_cancel_at) over all n indices, generated on
+    the GPU `chunk` elements at a time (the int64 index and hashing temporaries of a 256 Mi
+    bucket would otherwise take several GiB per rank) and stored as out_dtype (torch.float32,
+    or torch.bfloat16 -- RNE, as synth.bf16_bits).  Writes into `out` when given."""
+    import torch
+
+    if out is None:
+        out = torch.empty(n, dtype=out_dtype, device=dev)
+    for lo in range(0, n, chunk):
+        hi = min(n, lo + chunk)
+        idx = torch.arange(lo, hi, device=dev, dtype=torch.int64)
+        out[lo:hi] = gen(P, rank, idx).to(out_dtype)
+    return out

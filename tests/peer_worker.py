@@ -120,6 +120,34 @@ def reregister(peer, c, rank, world, dev):
     return bad
 
 
+def full_size(peer, arena, c, rank, world, dev):
+    """BASELINE configs 4 / 5 at their full size: the bucket is generated on the GPU from the
+    index-addressable order-sensitive generators (fp32 synth.stress_at; bf16 synth.stress_cancel_at
+    for ACC_F32), allreduced once, and reported as the sha256 of the whole result (fp32) or its
+    values at the parent's sample indices (bf16, checked against the reference fold there)."""
+    import hashlib
+
+    import torch
+
+    from fold_expect import device_bucket
+    from hydra_amd import synth
+
+    n, off = c["n"], c.get("offset_bytes", 0)
+    if c["data"] == "full_stress":
+        view = arena[off:off + 4 * n].view(torch.float32)
+        device_bucket(synth.stress_at, world, rank, n, dev, torch.float32, out=view)
+    else:  # full_cancel_bf16
+        view = arena[off:off + 2 * n].view(torch.bfloat16)
+        device_bucket(synth.stress_cancel_at, world, rank, n, dev, torch.bfloat16, out=view)
+    torch.cuda.synchronize(dev)
+    peer.allreduce_(view, algo=c["algo"], dtype_code=c["dtype"], flags=c.get("flags", 0))
+    torch.cuda.synchronize(dev)
+    if c["data"] == "full_stress":
+        return hashlib.sha256(view.cpu().numpy().tobytes()).hexdigest(), None
+    idx = torch.from_numpy(np.load(c["idx_file"], allow_pickle=False)).to(dev)
+    return None, view.view(torch.int16)[idx].cpu().numpy().view(np.uint16).copy()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rank", type=int, required=True)
@@ -128,6 +156,7 @@ def main():
     ap.add_argument("--out", required=True)
     ap.add_argument("--cases", required=True)
     ap.add_argument("--blocks", type=int, default=64)
+    ap.add_argument("--arena-bytes", type=int, default=64 << 20)
     a = ap.parse_args()
     import torch
     import torch.distributed as dist
@@ -147,7 +176,7 @@ def main():
     try:
         # one large registered arena; buckets are views at a per-case element offset (same on
         # every rank), so sub-allocation offsets and 16-B misalignment are exercised
-        arena = torch.zeros(64 << 20, dtype=torch.uint8, device=dev)
+        arena = torch.zeros(a.arena_bytes, dtype=torch.uint8, device=dev)
         peer.register(arena)
         for c in cases:
             name = c["name"]
@@ -163,6 +192,14 @@ def main():
                 continue
             if c["data"] == "streams":  # calls on two unordered streams
                 status[name] = alternating_streams(peer, arena, c, a.rank, a.world, dev)
+                continue
+            if c["data"] in ("full_stress", "full_cancel_bf16"):  # configs 4 / 5, full size
+                digest, sample = full_size(peer, arena, c, a.rank, a.world, dev)
+                status[name] = peer.error()
+                if digest is not None:
+                    status[name + "#sha256"] = digest
+                if sample is not None:
+                    results[name] = sample
                 continue
             if c.get("timeout_ms"):
                 peer.set_option(_lib.PEER_OPT_TIMEOUT_MS, c["timeout_ms"])

@@ -30,14 +30,15 @@ def free_port() -> int:
         return s.getsockname()[1]
 
 
-def run_ranks(tmp_path, P, cases, blocks=64, timeout=150):
+def run_ranks(tmp_path, P, cases, blocks=64, timeout=150, arena_bytes=64 << 20):
     cpath = tmp_path / "cases.json"
     cpath.write_text(json.dumps(cases))
     port = free_port()
     procs = []
     for r in range(P):
         cmd = [sys.executable, "-u", WORKER, "--rank", str(r), "--world", str(P), "--port",
-               str(port), "--out", str(tmp_path), "--cases", str(cpath), "--blocks", str(blocks)]
+               str(port), "--out", str(tmp_path), "--cases", str(cpath), "--blocks", str(blocks),
+               "--arena-bytes", str(arena_bytes)]
         procs.append(subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
                                       start_new_session=True))
     outs = []
@@ -175,13 +176,84 @@ def test_peer_allreduce_bit_exact(gpu, O, tmp_path, P):
 
 
 def test_peer_default_grid(gpu, O, tmp_path):
-    """The derived grid (one workgroup per 64 KiB slab, up to 512) at P = 2."""
+    """The derived grid (one workgroup per 64 KiB slab, up to 256 per rank) at P = 2."""
     P = 2
     cases = [dict(name="big", algo="peer2", data="stress_f32", dtype=_lib.FLOAT32,
                   n=(8 << 20) + 5, ms=0, offset_bytes=4)]
     res, st = run_ranks(tmp_path, P, cases, blocks=0)
     exp = expected(O, cases[0], P)
     assert all(np.array_equal(r["big"], exp) for r in res)
+
+
+@pytest.mark.parametrize("P", [2, 4, 8])
+def test_peer_config4_full_size_order_sensitive(gpu, O, tmp_path, P):
+    """BASELINE config 4 at its full size through the peer-access kernel --
+    P ranks x 64 Mi fp32 of fold-order-sensitive values (synth.stress_at, generated on the GPU),
+    every rank's whole bucket (sha256 of its bytes) equal to the C restatement of the reference
+    ring (O.ring_result), for the two-shot schedule (the one the N>1 line may promote) and the
+    one-shot one.  Reference geometry at this size: 256 segments of 1 MiB, S = 256/P per rank
+    (allreduce.cc:212-221, 253-258): S = 128 / 64 / 32 at P = 2 / 4 / 8.  The ranks share the
+    one GPU, so each rank's grid is 512 / P workgroups (all of them resident at once)."""
+    import hashlib
+
+    import torch
+
+    from fold_expect import device_bucket
+
+    n = 64 << 20
+    ns, sb, S = O.ring_plan(P, n, 4)
+    assert (ns, sb, S) == (256, 1 << 20, 256 // P)
+    F32 = _lib.FLOAT32
+    cases = [dict(name=f"{a}_full", algo=a, data="full_stress", dtype=F32, n=n)
+             for a in ("peer2", "peer1")]
+    res, st = run_ranks(tmp_path, P, cases, blocks=512 // P, timeout=240,
+                        arena_bytes=4 * n)
+    xs = [device_bucket(synth.stress_at, P, r, n, gpu, torch.float32).cpu().numpy()
+          for r in range(P)]
+    want = O.ring_result(xs)
+    if P > 2:  # the data can tell fold orders apart: a plain left fold differs on many
+        # elements (at P = 2 every order is the one commutative sum x_0 + x_1)
+        left = xs[0].copy()
+        for x in xs[1:]:
+            left += x
+        assert float(np.mean(left.view(np.uint32) != want.view(np.uint32))) > 0.1
+        del left
+    digest = hashlib.sha256(want.tobytes()).hexdigest()
+    del xs, want
+    for c in cases:
+        for r in range(P):
+            assert st[r][c["name"]] == 0, (c["name"], r, st[r])
+            assert st[r][c["name"] + "#sha256"] == digest, (c["name"], r)
+
+
+def test_peer_config5_full_size_sampled(gpu, O, tmp_path):
+    """BASELINE config 5 at its full size through the peer-access kernel --
+    8 ranks x 256 Mi bf16 with fp32 accumulation (HYDRA_ACC_F32) on synth.stress_cancel_at
+    (+-2^k pivots that cancel, so the one bf16 rounding does not hide the fp32 fold order), two-shot
+    schedule; >= 1 Mi sampled elements of every rank (every segment boundary, random ones) equal
+    the C restatement's fold on the widened values with the bf16 geometry (512 segments of 1 MiB,
+    S = 64 per rank), rounded once."""
+    from fold_expect import bf16_acc32_expected, sample_indices
+
+    P, n = 8, 256 << 20
+    ns, sb, S = O.ring_plan(P, n, 2)
+    assert (ns, sb, S) == (512, 1 << 20, 64)
+    idx = sample_indices(n, ns, sb // 2)
+    ipath = tmp_path / "idx.npy"
+    np.save(ipath, idx)
+    cases = [dict(name="peer2_bf16_full", algo="peer2", data="full_cancel_bf16",
+                  dtype=_lib.BFLOAT16, n=n, flags=_lib.ACC_F32, idx_file=str(ipath))]
+    res, st = run_ranks(tmp_path, P, cases, blocks=512 // P, timeout=240, arena_bytes=2 * n)
+    exp, vals, _ = bf16_acc32_expected(O, P, n, idx)
+    left = synth.bf16_to_f32(vals[0]).astype(np.float32)
+    for v in vals[1:]:
+        left = O.acc_bf16_f32(left, v)
+    assert float(np.mean(synth.bf16_bits(left) != exp)) > 0.3  # the check sees fold orders
+    for r in range(P):
+        assert st[r]["peer2_bf16_full"] == 0, (r, st[r])
+        got = res[r]["peer2_bf16_full"]
+        bad = np.flatnonzero(got != exp)
+        assert bad.size == 0, (r, bad.size, idx[bad[:5]].tolist())
 
 
 def test_peer_timeout_reports_and_poisons(gpu, tmp_path):

@@ -320,6 +320,86 @@ def test_rccl_executor_config4_full_size_8_ranks(gpu):
         assert res[r] == {"ring": True, "direct": True, "a2a": True}, (r, res[r])
 
 
+def _config5_full_worker(rank, world, port, q, idx_path):
+    """BASELINE config 5 at its full size through the REAL RCCL executor: 8 ranks x 256 Mi bf16 of
+    synth.stress_cancel_at (generated on the GPU), fp32 accumulation (HYDRA_ACC_F32), DIRECT and
+    A2A; every rank's values at the parent's >= 1 Mi sample indices compared with the C
+    restatement's fold on the widened values with the bf16 geometry (tests/fold_expect.py)."""
+    import sys
+
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    os.environ.update(RANK_ENV)
+    os.environ["NCCL_HOSTID"] = f"hydra-test-rank-{rank}"
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch
+    import torch.distributed as dist
+
+    from fold_expect import device_bucket
+    from hydra_amd import _lib, ring, synth
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    res, comm = {}, None
+    try:
+        torch.cuda.set_device(0)
+        dev = torch.device("cuda", 0)
+        n = 256 << 20
+        mine = device_bucket(synth.stress_cancel_at, world, rank, n, dev, torch.bfloat16)
+        idx = torch.from_numpy(np.load(idx_path, allow_pickle=False)).to(dev)
+        comm = ring.XgmiComm(rank, world, 0, ring.exchange_unique_id(rank))
+        for algo in ("direct", "a2a"):
+            t = mine.clone()
+            comm.allreduce_(t, algo=algo, dtype_code=_lib.BFLOAT16, flags=_lib.ACC_F32)
+            comm.wait(240000)
+            res[algo] = t.view(torch.int16)[idx].cpu().numpy().view(np.uint16).copy()
+            del t
+        q.put((rank, res))
+    except Exception as e:  # report instead of hanging the parent
+        import traceback
+
+        q.put((rank, repr(e) + traceback.format_exc()[-1500:]))
+    finally:
+        if comm is not None:
+            try:
+                comm.close()
+            except Exception:
+                pass
+        dist.destroy_process_group()
+
+
+def test_rccl_executor_config5_full_size_8_ranks(gpu, O, tmp_path):
+    """config 5's full 8 x 256 Mi bf16 (fp32 accumulation) through 8 real
+    RCCL ranks, order-sensitive data (synth.stress_cancel_at), DIRECT and A2A; >= 1 Mi sampled
+    elements of every rank equal the reference ring's fp32 fold on the widened values with the
+    bf16 geometry (512 segments of 1 MiB, S = 64 per rank: allreduce.cc:199-221 at E = 2),
+    rounded once."""
+    import sys
+
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from fold_expect import bf16_acc32_expected, sample_indices
+
+    from hydra_amd import synth
+
+    P, n = 8, 256 << 20
+    ns, sb, S = O.ring_plan(P, n, 2)
+    assert (ns, sb, S) == (512, 1 << 20, 64)
+    idx = sample_indices(n, ns, sb // 2)
+    ipath = str(tmp_path / "idx.npy")
+    np.save(ipath, idx)
+    exp, vals, _ = bf16_acc32_expected(O, P, n, idx)
+    left = synth.bf16_to_f32(vals[0]).astype(np.float32)
+    for v in vals[1:]:
+        left = O.acc_bf16_f32(left, v)
+    assert float(np.mean(synth.bf16_bits(left) != exp)) > 0.3  # the check sees fold orders
+    res = _spawn(_config5_full_worker, P, ipath, timeout=420)
+    for r in range(P):
+        assert isinstance(res[r], dict), (r, res[r])
+        for algo in ("direct", "a2a"):
+            bad = np.flatnonzero(res[r][algo] != exp)
+            assert bad.size == 0, (algo, r, bad.size, idx[bad[:5]].tolist())
+
+
 def _fault_worker(rank, world, port, q, mode):
     """The reference's TestTimeout (allreduce_test.cc:381-397) on the device allreduce across
     real RCCL ranks: rank 1 never joins ("absent") or exits abruptly ("dead"); rank 0's
