@@ -3,6 +3,11 @@
 The library is built in-tree (hydra_amd/csrc/Makefile -> hydra_amd/libhydra_hip.so).  There is no
 fallback: if the shared object is missing or fails to load, every entry point raises
 HydraError -- the hot path never silently runs on the CPU.
+
+measure_lib() loads libhydra_measure.so instead: the same library built with -DHYDRA_MEASURE,
+which adds the A/B kernel variants and the peer kernel's phase clocks (include/hydra_measure.h).
+Only scripts/ and the variant parity tests use it; select_measure() makes lib() return it for a
+whole measurement process (so hydra_amd.peer / .ring / .reduce run on it).
 """
 from __future__ import annotations
 
@@ -13,6 +18,7 @@ import threading
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libhydra_hip.so")
+MEASURE_LIB_PATH = os.path.join(HERE, "libhydra_measure.so")
 CSRC = os.path.join(HERE, "csrc")
 
 # hydra_dtype_t / hydra_op_t
@@ -28,7 +34,8 @@ EXPORTS = [  # every symbol include/hydra_hip.h declares
     "hydra_event_create", "hydra_event_create_on", "hydra_event_record", "hydra_event_synchronize",
     "hydra_event_destroy",
     "hydra_reduce", "hydra_chunk_sum", "hydra_reduce_batch", "hydra_acc_bf16_f32", "hydra_f32_to_bf16",
-    "hydra_set_variant", "hydra_ctx_create", "hydra_ctx_destroy", "hydra_reduce_host",
+    "hydra_set_option", "hydra_get_option", "hydra_ctx_set_option",
+    "hydra_ctx_create", "hydra_ctx_destroy", "hydra_reduce_host",
     "hydra_chunk_sum_host", "hydra_host_register", "hydra_host_unregister",
     "hydra_page_interior", "hydra_host_mappings", "hydra_ctx_stats",
     "hydra_stream_create", "hydra_stream_destroy", "hydra_stream_synchronize", "hydra_malloc",
@@ -45,6 +52,14 @@ EXPORTS = [  # every symbol include/hydra_hip.h declares
     "hydra_host_trace", "hydra_host_trace_read", "hydra_device_link",
     "hydra_test_set", "hydra_test_get",
 ]
+MEASURE_EXPORTS = ["hydra_set_variant", "hydra_measure_peer_stamps"]  # include/hydra_measure.h
+
+# hydra_opt_t (include/hydra_hip.h): library options, no environment variables
+(OPT_RESIDENT, OPT_STAGE_SPLIT, OPT_ROUND_MIN, OPT_STAGE_RESULT_MAX, OPT_STAGE_RESULT_REG_MAX,
+ OPT_FORCE_STAGING, OPT_COPY_THREADS, OPT_RESIDENT_IDLE_US, OPT_RESIDENT_GRACE_US,
+ OPT_RESIDENT_QUEUE, OPT_RESIDENT_BLOCKS, OPT_RESIDENT_BATCH, OPT_RESIDENT_SOLO,
+ OPT_RESIDENT_TILES) = range(1, 15)
+PEER_STAMPS = 6  # hydra_measure_peer_stamps: clocks per workgroup
 
 (ALGO_AUTO, ALGO_RING, ALGO_DIRECT, ALGO_RCCL, ALGO_A2A, ALGO_RING_OLD, ALGO_RING_CHUNKED,
  ALGO_BCUBE, ALGO_HALVING_DOUBLING, ALGO_RCCL_RS_AG) = range(10)
@@ -169,7 +184,9 @@ def _declare(L) -> None:
     L.hydra_reduce_batch.argtypes = [i, i, vp, sz, vp]
     L.hydra_acc_bf16_f32.argtypes = [vp, vp, sz, vp]
     L.hydra_f32_to_bf16.argtypes = [vp, vp, sz, vp]
-    L.hydra_set_variant.argtypes = [i]
+    L.hydra_set_option.argtypes = [i, ctypes.c_longlong]
+    L.hydra_get_option.argtypes = [i, ctypes.POINTER(ctypes.c_longlong)]
+    L.hydra_ctx_set_option.argtypes = [vp, i, ctypes.c_longlong]
     L.hydra_ctx_create.argtypes = [i, ctypes.POINTER(vp)]
     L.hydra_ctx_destroy.argtypes = [vp]
     L.hydra_reduce_host.argtypes = [vp, i, i, vp, vp, vp, sz]
@@ -237,6 +254,16 @@ def _declare(L) -> None:
     L.hydra_test_get.argtypes = [i, ctypes.POINTER(ctypes.c_int64)]
 
 
+def _load(path):
+    if not os.path.exists(path):
+        raise HydraError(-1, f"{path} is not built (hydra_amd._lib.build())")
+    try:
+        import torch  # noqa: F401  (bind to torch's libamdhip64 when present)
+    except ImportError:
+        pass
+    return ctypes.CDLL(path)
+
+
 def lib():
     """Load (once) and return the ctypes handle.  torch must be imported first on a GPU box so
     that this library binds to the same HIP runtime as torch (same soname)."""
@@ -244,21 +271,53 @@ def lib():
     if _lib is None:
         with _lock:
             if _lib is None:
-                if not os.path.exists(LIB_PATH):
-                    raise HydraError(-1, f"{LIB_PATH} is not built (hydra_amd._lib.build())")
-                try:
-                    import torch  # noqa: F401  (bind to torch's libamdhip64 when present)
-                except ImportError:
-                    pass
-                L = ctypes.CDLL(LIB_PATH)
+                L = _load(LIB_PATH)
                 _declare(L)
                 _lib = L
     return _lib
 
 
+_measure = None
+
+
+def measure_lib():
+    """libhydra_measure.so (measurement build: hydra_set_variant, hydra_measure_peer_stamps)."""
+    global _measure
+    if _measure is None:
+        with _lock:
+            if _measure is None:
+                M = _load(MEASURE_LIB_PATH)
+                _declare(M)
+                M.hydra_set_variant.argtypes = [ctypes.c_int]
+                M.hydra_measure_peer_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p,
+                                                        ctypes.c_size_t]
+                _measure = M
+    return _measure
+
+
+def select_measure() -> None:
+    """Measurement processes only (scripts/): lib() returns the measurement build from now on.
+    Call before anything has loaded the product library."""
+    global _lib
+    if _lib is not None and _lib is not _measure:
+        raise HydraError(-1, "select_measure: the product library is already loaded")
+    _lib = measure_lib()
+
+
 def check(rc: int) -> None:
     if rc != 0:
         raise HydraError(rc, lib().hydra_last_error().decode(errors="replace"))
+
+
+def set_option(key: int, value: int) -> None:
+    """hydra_set_option: a process-wide library option (hydra_opt_t)."""
+    check(lib().hydra_set_option(key, int(value)))
+
+
+def get_option(key: int) -> int:
+    v = ctypes.c_longlong()
+    check(lib().hydra_get_option(key, ctypes.byref(v)))
+    return v.value
 
 
 def ring_plan(P: int, n: int, esize: int, max_segment: int = 1 << 20):
@@ -309,7 +368,8 @@ def device_links(device: int = 0) -> list:
 
 
 def set_variant(v: int) -> int:
-    return lib().hydra_set_variant(v)
+    """hydra_set_variant of the measurement build (measure_lib()); returns the previous value."""
+    return measure_lib().hydra_set_variant(v)
 
 
 # hydra_test_key_t (include/hydra_hip.h): test switches, 0 in production

@@ -1,5 +1,6 @@
 // copy_pool.cpp -- see copy_pool.h.
 #include "copy_pool.h"
+#include "options.h"
 
 #include <algorithm>
 #include <atomic>
@@ -78,12 +79,8 @@ class Pool {
   std::deque<Batch*> q_;
 };
 
-int helper_count() {
-  static const int n = [] {
-    const char* v = std::getenv("HYDRA_COPY_THREADS");
-    const int k = v ? std::atoi(v) : 4;
-    return std::max(0, std::min(k, 32));
-  }();
+int helper_count() {  // HYDRA_OPT_COPY_THREADS when the pool starts (the first large copy)
+  static const int n = (int)opt(HYDRA_OPT_COPY_THREADS);
   return n;
 }
 

@@ -23,6 +23,7 @@
 #include "errors.h"
 #include "fault_report.h"
 #include "host_map.h"
+#include "options.h"
 #include "resource_cache.h"
 #include "reduce_kernels.h"
 #include "resident.h"
@@ -30,7 +31,9 @@
 
 namespace {
 thread_local std::string g_err;
+#ifdef HYDRA_MEASURE
 std::atomic<int> g_variant{0};
+#endif
 }  // namespace
 
 namespace hydra {
@@ -45,7 +48,9 @@ int fail(int code, const std::string& msg) {
 int hip_fail(hipError_t e, const char* what) {
   return fail(HYDRA_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
 }
+#ifdef HYDRA_MEASURE
 int current_variant() { return g_variant.load(std::memory_order_relaxed); }
+#endif
 
 namespace {
 constexpr int kTestKeys = 4;  // hydra_test_key_t values 1..3
@@ -99,6 +104,7 @@ int check_args(int op, int dtype, const void* c, const void* a, const void* b, s
 // buffers alternate, so the CPU fills round r + 1 while the GPU reduces round r.
 struct hydra_ctx {
   int device = 0;
+  hydra::CtxOpts opts;  // the [ctx] options (hydra_ctx_set_option), from the process-wide values
   hipStream_t stream = nullptr;
   hipEvent_t done[2] = {nullptr, nullptr};
   char* stage[2] = {nullptr, nullptr};      // host address
@@ -120,18 +126,8 @@ double us_since(Clock::time_point t0) {
 }
 
 constexpr size_t kSlotBytes = 4u << 20;  // per operand and staging buffer (3 slots: a, b, c)
-constexpr int kVariantForceStaging = 1000;  // hydra_set_variant value: host path always stages
-constexpr int kVariantSplit = 1100;         // hydra_set_variant 1101..1164: staging split (A/B)
-// smallest staging round per operand (probe_stage_split); HYDRA_ROUND_MIN (bytes) for A/B
-constexpr size_t kRoundMin = 512u << 10;
-size_t round_min() {
-  static const size_t k = [] {
-    const char* v = std::getenv("HYDRA_ROUND_MIN");
-    const size_t x = v ? (size_t)std::strtoull(v, nullptr, 10) : kRoundMin;
-    return std::max<size_t>(16u << 10, std::min<size_t>(x, kSlotBytes));
-  }();
-  return k;
-}
+// (the smallest staging round per operand, HYDRA_OPT_ROUND_MIN, defaults to 512 KiB:
+// scripts/probe_stage_split.cc's A/B)
 
 // Staged RESULT where c is mapped: the kernel writes the pinned staging and the CPU copies it
 // into c, which leaves c's lines in the CPU's cache for the caller's next read of them (a
@@ -139,34 +135,9 @@ size_t round_min() {
 // (profiles/r04d_dropin_sweep.json): it pays while the registered bucket fits the CPU's cache
 // (4 MiB: 0.669 vs 0.714 ms per allreduce) and costs once it does not (16 MiB and up: the
 // zero-copy write wins, 2.94 vs 3.11 ms).  So a result goes through the staging when c lies in a
-// hydra_host_register'ed range of at most HYDRA_STAGE_RESULT_REG_MAX bytes (default 8 MiB), or
-// when the call itself is at most HYDRA_STAGE_RESULT_MAX bytes per operand (default 0, A/B).
-// Not for float16 (its store quirk reads c's old bits).
-constexpr size_t kStageResultMax = 0;
-constexpr size_t kStageResultRegMax = size_t(8) << 20;
-size_t env_bytes(const char* name, size_t dflt) {
-  const char* v = std::getenv(name);
-  return v ? (size_t)std::strtoull(v, nullptr, 10) : dflt;
-}
-size_t stage_result_max() {
-  static const size_t k = env_bytes("HYDRA_STAGE_RESULT_MAX", kStageResultMax);
-  return k;
-}
-size_t stage_result_reg_max() {
-  static const size_t k = env_bytes("HYDRA_STAGE_RESULT_REG_MAX", kStageResultRegMax);
-  return k;
-}
-
-// Rounds a staged call is cut into (HYDRA_STAGE_SPLIT, default 4; 1 = one round per slot).
-size_t stage_split(int variant) {
-  if (variant > kVariantSplit && variant <= kVariantSplit + 64) return variant - kVariantSplit;
-  static const size_t k = [] {
-    const char* v = std::getenv("HYDRA_STAGE_SPLIT");
-    const long x = v ? std::atol(v) : 4;
-    return (size_t)std::max(1L, std::min(x, 64L));
-  }();
-  return k;
-}
+// hydra_host_register'ed range of at most HYDRA_OPT_STAGE_RESULT_REG_MAX bytes (default 8 MiB),
+// or when the call itself is at most HYDRA_OPT_STAGE_RESULT_MAX bytes per operand (default 0,
+// A/B).  Not for float16 (its store quirk reads c's old bits).
 
 void ctx_release(hydra_ctx* x) {
   if (x->stream) (void)hydra::release_stream(x->stream);
@@ -219,7 +190,29 @@ int hydra_device_check(int device) {
   return ok();
 }
 
+#ifdef HYDRA_MEASURE  // libhydra_measure.so only (include/hydra_measure.h)
 int hydra_set_variant(int variant) { return g_variant.exchange(variant); }
+#endif
+
+int hydra_set_option(int key, long long value) {
+  if (key <= 0 || key >= hydra::kOptCount)
+    return fail(HYDRA_ERR_INVALID, "hydra_set_option: unknown key " + std::to_string(key));
+  const hydra::OptSpec& sp = hydra::opt_spec(key);
+  if (value < sp.lo || value > sp.hi)
+    return fail(HYDRA_ERR_INVALID, "hydra_set_option: value " + std::to_string(value) +
+                                       " of key " + std::to_string(key) + " outside [" +
+                                       std::to_string(sp.lo) + ", " + std::to_string(sp.hi) + "]");
+  hydra::opt_set(key, value);
+  return ok();
+}
+
+int hydra_get_option(int key, long long* value) {
+  if (!value) return fail(HYDRA_ERR_INVALID, "null value");
+  if (key <= 0 || key >= hydra::kOptCount)
+    return fail(HYDRA_ERR_INVALID, "hydra_get_option: unknown key " + std::to_string(key));
+  *value = hydra::opt(key);
+  return ok();
+}
 
 int hydra_test_set(int key, int64_t value, int64_t* prev) {
   if (key != HYDRA_TEST_LOCAL_STAGE && key != HYDRA_TEST_RESIDENT_GEN_STRIDE)
@@ -242,7 +235,7 @@ int hydra_reduce(int op, int dtype, void* c, const void* a, const void* b, size_
   int rc = check_args(op, dtype, c, a, b, n);
   if (rc) return rc;
   if (n == 0) return ok();
-  hipError_t e = hydra::launch_reduce(g_variant.load(std::memory_order_relaxed), op, dtype, c, a,
+  hipError_t e = hydra::launch_reduce(hydra::current_variant(), op, dtype, c, a,
                                       b, n, static_cast<hipStream_t>(stream));
   if (e != hipSuccess) return hip_fail(e, "reduce kernel launch");
   return ok();
@@ -322,6 +315,7 @@ int hydra_ctx_create(int device, hydra_ctx_t* out) {
   hydra::DeviceScope ds(device);  // the caller's current device is left as it was
   auto* x = new hydra_ctx();
   x->device = device;
+  x->opts.load();
   hipError_t e = ds.err;
   if (e == hipSuccess) e = hydra::cached_stream(device, &x->stream);
   for (int i = 0; i < 2 && e == hipSuccess; i++) {
@@ -338,12 +332,33 @@ int hydra_ctx_create(int device, hydra_ctx_t* out) {
     delete x;
     return hip_fail(e, "hydra_ctx_create");
   }
-  if (int rc = hydra::resident_lease(device, &x->lease)) {
+  if (x->opts[HYDRA_OPT_RESIDENT] == 0) {
+    // no slot of the resident reducer: every round is one launch on the context's stream
+  } else if (int rc = hydra::resident_lease(device, &x->lease)) {
     ctx_release(x);
     delete x;
     return rc;
   }
   *out = x;
+  return ok();
+}
+
+int hydra_ctx_set_option(hydra_ctx_t ctx, int key, long long value) {
+  if (!ctx) return fail(HYDRA_ERR_INVALID, "null context");
+  if (key <= 0 || key >= hydra::kOptCount || !hydra::opt_spec(key).per_ctx)
+    return fail(HYDRA_ERR_INVALID, "hydra_ctx_set_option: not a per-context key " + std::to_string(key));
+  const hydra::OptSpec& sp = hydra::opt_spec(key);
+  if (value < sp.lo || value > sp.hi)
+    return fail(HYDRA_ERR_INVALID, "hydra_ctx_set_option: value out of range");
+  if (key == HYDRA_OPT_RESIDENT) {
+    if (value == 0 && ctx->lease) {  // its calls were synchronous: the slot holds nothing
+      hydra::resident_release(ctx->lease);
+      ctx->lease = nullptr;
+    } else if (value != 0 && !ctx->lease) {
+      if (int rc = hydra::resident_lease(ctx->device, &ctx->lease)) return rc;
+    }
+  }
+  ctx->opts.v[key] = value;
   return ok();
 }
 
@@ -413,7 +428,7 @@ int hydra_reduce_host(hydra_ctx_t ctx, int op, int dtype, void* c, const void* a
   if (rc) return rc;
   if (n == 0) return ok();
   const size_t es = hydra::dtype_size(dtype);
-  const int variant = g_variant.load(std::memory_order_relaxed);
+  const hydra::CtxOpts& opts = ctx->opts;
   const size_t nbytes = n * es;
   const bool tracing = g_trace_on.load(std::memory_order_relaxed);
   const Clock::time_point t_call = tracing ? Clock::now() : Clock::time_point();
@@ -427,7 +442,7 @@ int hydra_reduce_host(hydra_ctx_t ctx, int op, int dtype, void* c, const void* a
   // page of a registered range -- is copied by the CPU into the context's pinned staging and
   // reduced there (pageable memory is never pinned for a call: DESIGN.md §10).  The whole call
   // is one batched kernel launch per staging round (one round unless more than kSlotBytes per
-  // operand must be staged).  kVariantForceStaging stages everything (A/B).
+  // operand must be staged).  HYDRA_OPT_FORCE_STAGING stages everything (A/B).
   Operand oc, oa, ob;
   oc.base = static_cast<const char*>(c);
   oa.base = static_cast<const char*>(a);
@@ -435,7 +450,7 @@ int hydra_reduce_host(hydra_ctx_t ctx, int op, int dtype, void* c, const void* a
   Operand* A = a == c ? &oc : &oa;
   Operand* B = b == c ? &oc : b == a ? A : &ob;
   WindowsGuard guard_;
-  if (variant != kVariantForceStaging) {
+  if (opts[HYDRA_OPT_FORCE_STAGING] == 0) {
     for (Operand* o : {&oc, A, B}) {
       bool seen = false;
       for (int i = 0; i < guard_.k; i++) seen = seen || guard_.w[i] == &o->win;
@@ -457,7 +472,8 @@ int hydra_reduce_host(hydra_ctx_t ctx, int op, int dtype, void* c, const void* a
   cut.erase(std::unique(cut.begin(), cut.end()), cut.end());
 
   const bool c_old_bits = dtype == HYDRA_FLOAT16 && c != a && c != b;  // store quirk: read c
-  const bool stage_result_all = dtype != HYDRA_FLOAT16 && nbytes <= stage_result_max();
+  const bool stage_result_all =
+      dtype != HYDRA_FLOAT16 && nbytes <= (size_t)opts[HYDRA_OPT_STAGE_RESULT_MAX];
   // per interval: its result goes through the staging when the window holding that interval of
   // c is a small (cache-resident) registration; a large registration or a caller mapping keeps
   // the zero-copy write
@@ -466,7 +482,7 @@ int hydra_reduce_host(hydra_ctx_t ctx, int op, int dtype, void* c, const void* a
     if (stage_result_all) return true;
     const int k = oc.window_of(i, j);
     return k >= 0 && oc.win.w[k].kind == hydra::kMapRegister &&
-           oc.win.w[k].entry_bytes <= stage_result_reg_max();
+           oc.win.w[k].entry_bytes <= (size_t)opts[HYDRA_OPT_STAGE_RESULT_REG_MAX];
   };
   // Rounds: a round is one batched call over at most kResidentSegs intervals and one staging
   // buffer's slots.  Round r is submitted once round r - 1 is done; its staged results go back
@@ -559,11 +575,13 @@ int hydra_reduce_host(hydra_ctx_t ctx, int op, int dtype, void* c, const void* a
   };
   hydra::DeviceScope ds(lease ? -1 : ctx->device);  // launches go to the context's device
   HIP_TRY(ds.err);
-  // A staged call is cut into about stage_split() rounds (>= kRoundMin bytes per operand, at
-  // most a slot), so its copies overlap the GPU's rounds: in at round r + 1 and out at round
-  // r - 1 while round r runs.
-  const size_t round_cap =
-      std::min(kSlotBytes, std::max(round_min(), (nbytes / stage_split(variant) + 255) / 256 * 256));
+  // A staged call is cut into about HYDRA_OPT_STAGE_SPLIT rounds (>= HYDRA_OPT_ROUND_MIN bytes
+  // per operand, at most a slot), so its copies overlap the GPU's rounds: in at round r + 1 and
+  // out at round r - 1 while round r runs.
+  const size_t round_min = std::min<size_t>((size_t)opts[HYDRA_OPT_ROUND_MIN], kSlotBytes);
+  const size_t round_cap = std::min(
+      kSlotBytes,
+      std::max(round_min, (nbytes / (size_t)opts[HYDRA_OPT_STAGE_SPLIT] + 255) / 256 * 256));
   for (size_t q = 0; q + 1 < cut.size(); q++) {
     size_t off = cut[q];
     const size_t end = cut[q + 1];

@@ -39,12 +39,14 @@ static_assert(kIpcBytes <= 64, "hipIpcMemHandle_t larger than the blob slot");
 // Blob layout (HYDRA_PEER_HANDLE_BYTES): [0,64) hipIpcMemHandle_t of the allocation base,
 // [64,72) offset of the buffer in it, [72,80) buffer bytes, [80,88) magic, [88,92) rank,
 // [96,104) the exporter's allocation id (HIP_POINTER_ATTRIBUTE_BUFFER_ID: unique per
-// allocation, so a freed-and-reallocated bucket whose IPC handle bytes repeat is a NEW mapping).
+// allocation, so a freed-and-reallocated bucket whose IPC handle bytes repeat is a NEW mapping),
+// [104,116) the exporter's GPU (PCI domain, bus, device: ranks on the same GPU share its CUs).
 struct Blob {
   unsigned char ipc[64];
   uint64_t offset, bytes, magic;
   int32_t rank, pad;
   uint64_t alloc_id;
+  int32_t pci[3];
 };
 static_assert(sizeof(Blob) <= HYDRA_PEER_HANDLE_BYTES, "blob too large");
 
@@ -57,6 +59,9 @@ struct Mapping {
 
 struct hydra_peer {
   int P = 1, rank = 0, device = 0;
+  int pci[3] = {0, 0, 0};  // this rank's GPU (PCI domain, bus, device)
+  int cus = 0;             // its compute units
+  int colocated = 1;       // ranks of the group on this GPU, this one included (connect)
   hydra::PeerSignals* sig = nullptr;  // own signal area (uncached device memory)
   hydra::PeerSigPtrs sigs{};          // every rank's, mapped
   uint32_t* err_host = nullptr;       // host-mapped error word the kernels write
@@ -82,6 +87,10 @@ struct hydra_peer {
   // one-shot scratch)
   hipEvent_t last = nullptr;
   bool last_valid = false;
+#ifdef HYDRA_MEASURE
+  uint64_t* stamps = nullptr;  // hydra_measure_peer_stamps: per-workgroup phase clocks
+  size_t stamps_cap = 0;       // workgroups it holds
+#endif
 };
 
 namespace {
@@ -94,9 +103,6 @@ int export_blob(hydra_peer* p, void* ptr, size_t bytes, void* out) {
   const char* q = static_cast<const char*>(ptr);
   if (q < b || q + bytes > b + size)
     return fail(HYDRA_ERR_INVALID, "buffer is not inside one device allocation");
-  if (std::getenv("HYDRA_PEER_DEBUG"))
-    std::fprintf(stderr, "[hydra_peer] rank %d export %p (+%zu) in allocation [%p, +%zu)\n",
-                 p->rank, ptr, bytes, base, size);
   unsigned long long id = 0;
   HIP_TRY(hipPointerGetAttribute(&id, HIP_POINTER_ATTRIBUTE_BUFFER_ID,
                                  reinterpret_cast<hipDeviceptr_t>(base)));
@@ -118,6 +124,7 @@ int export_blob(hydra_peer* p, void* ptr, size_t bytes, void* out) {
   blob.magic = kMagic;
   blob.rank = p->rank;
   blob.alloc_id = (uint64_t)id;
+  std::memcpy(blob.pci, p->pci, sizeof(blob.pci));
   std::memset(out, 0, HYDRA_PEER_HANDLE_BYTES);
   std::memcpy(out, &blob, sizeof(blob));
   return HYDRA_OK;
@@ -151,9 +158,6 @@ int open_mapping(hydra_peer* p, const Blob& b, std::string* key, char** base) {
       }
       hydra::ledger_add(hydra::kLedgerPeerMapping, m, msz);
     }
-    if (std::getenv("HYDRA_PEER_DEBUG"))
-      std::fprintf(stderr, "[hydra_peer] rank %d mapped rank %d's allocation (+%llu B) at %p\n",
-                   p->rank, b.rank, (unsigned long long)b.bytes, m);
     it = p->opened.emplace(*key, Mapping{m, 0}).first;
   }
   it->second.refs++;
@@ -169,6 +173,18 @@ void close_mapping(hydra_peer* p, const std::string& key) {
     hydra::ledger_release(hydra::kLedgerPeerMapping, it->second.base);
     p->opened.erase(it);
   }
+}
+
+// Workgroups of one peer kernel each rank may launch: when ranks of the group share a GPU, every
+// rank's whole grid must be resident at once (workgroup b of one rank waits for workgroup b of
+// the others, so a grid that fills the CUs while a peer's waits behind it never finishes), so
+// colocated x grid <= CUs x (workgroups of that kernel per CU).  0 = no limit (a GPU per rank).
+int colocated_cap(const hydra_peer* p, int algo, int op, int dtype, bool acc32) {
+  if (p->colocated <= 1) return 0;
+  int per_cu = 0;
+  if (hydra::peer_occupancy(algo, op, dtype, acc32, &per_cu) != hipSuccess || per_cu < 1)
+    per_cu = 1;
+  return std::max(1, p->cus * per_cu / p->colocated);
 }
 
 const hydra_peer::Reg* find_reg(const hydra_peer* p, const void* buf, size_t bytes) {
@@ -193,7 +209,12 @@ int hydra_peer_create(int nranks, int rank, int device, hydra_peer_t* out, void*
   p->P = nranks;
   p->rank = rank;
   p->device = device;
-  hipError_t e = hipExtMallocWithFlags(reinterpret_cast<void**>(&p->sig),
+  hipError_t e = hipDeviceGetAttribute(&p->pci[0], hipDeviceAttributePciDomainID, device);
+  if (e == hipSuccess) e = hipDeviceGetAttribute(&p->pci[1], hipDeviceAttributePciBusId, device);
+  if (e == hipSuccess) e = hipDeviceGetAttribute(&p->pci[2], hipDeviceAttributePciDeviceId, device);
+  if (e == hipSuccess)
+    e = hipDeviceGetAttribute(&p->cus, hipDeviceAttributeMultiprocessorCount, device);
+  if (e == hipSuccess) e = hipExtMallocWithFlags(reinterpret_cast<void**>(&p->sig),
                                        sizeof(hydra::PeerSignals), hipDeviceMallocUncached);
   if (e == hipSuccess) hydra::ledger_add(hydra::kLedgerPeerLocal, p->sig, sizeof(hydra::PeerSignals));
   if (e == hipSuccess) e = hipMemset(p->sig, 0, sizeof(hydra::PeerSignals));
@@ -224,10 +245,12 @@ int hydra_peer_connect(hydra_peer_t p, const void* sig_handles) {
   if (!p || !sig_handles) return fail(HYDRA_ERR_INVALID, "null argument");
   hydra::DeviceScope ds_(p->device);  // IPC mappings and drains on the group's device
   const char* h = static_cast<const char*>(sig_handles);
+  int colocated = 1;
   for (int q = 0; q < p->P; q++) {
     Blob b;
     int rc = parse_blob(h + (size_t)q * HYDRA_PEER_HANDLE_BYTES, q, &b);
     if (rc) return rc;
+    if (q != p->rank && std::memcmp(b.pci, p->pci, sizeof(p->pci)) == 0) colocated++;
     if (q == p->rank || p->sigs.p[q]) continue;
     std::string key;
     char* base = nullptr;
@@ -235,6 +258,7 @@ int hydra_peer_connect(hydra_peer_t p, const void* sig_handles) {
     if (rc) return rc;
     p->sigs.p[q] = reinterpret_cast<hydra::PeerSignals*>(base + b.offset);
   }
+  p->colocated = colocated;
   return ok();
 }
 
@@ -310,11 +334,20 @@ int hydra_peer_set_option(hydra_peer_t p, int key, long long value) {
       if (value <= 0) return fail(HYDRA_ERR_INVALID, "timeout must be positive");
       p->timeout_ticks = (uint64_t)value * 100000ull;
       return ok();
-    case HYDRA_PEER_OPT_BLOCKS:
+    case HYDRA_PEER_OPT_BLOCKS: {
       if (value < 0 || value > hydra::kPeerMaxBlocks)
         return fail(HYDRA_ERR_INVALID, "blocks out of range");
+      // ranks sharing this GPU: refuse a grid they cannot all hold at once (checked again for
+      // the kernel each call launches) instead of a barrier timeout later
+      const int cap = colocated_cap(p, hydra::kPeerTwoShot, HYDRA_SUM, HYDRA_FLOAT32, false);
+      if (cap && value > cap)
+        return fail(HYDRA_ERR_INVALID,
+                    "blocks " + std::to_string(value) + " x " + std::to_string(p->colocated) +
+                        " ranks sharing this GPU exceeds its resident capacity (at most " +
+                        std::to_string(cap) + " workgroups per rank)");
       p->blocks = (int)value;
       return ok();
+    }
     case HYDRA_PEER_OPT_ONE_SHOT_MAX:
       if (value < 0) return fail(HYDRA_ERR_INVALID, "negative size");
       p->one_shot_max = (size_t)value;
@@ -387,8 +420,17 @@ int hydra_peer_allreduce(hydra_peer_t p, int algo, int op, int dtype, int flags,
   // room for the same grid of a second rank when ranks share a GPU (the one-GPU tests); the
   // depth comes from each wave (peer_kernels.hip slab_fold_n), not from more workgroups, which
   // measured no faster (profiles/r05h, r05m)
-  const size_t grid =
+  size_t grid =
       p->blocks > 0 ? (size_t)p->blocks : std::min<size_t>(std::max<size_t>(work, 1), 256);
+  const int kalgo = algo == HYDRA_PEER_ONE_SHOT ? hydra::kPeerOneShot : hydra::kPeerTwoShot;
+  if (const int cap = colocated_cap(p, kalgo, op, dtype, acc32)) {
+    if (p->blocks > 0 && grid > (size_t)cap)
+      return fail(HYDRA_ERR_INVALID,
+                  "blocks " + std::to_string(grid) + " x " + std::to_string(p->colocated) +
+                      " ranks sharing this GPU exceeds its resident capacity for this kernel (at "
+                      "most " + std::to_string(cap) + " workgroups per rank)");
+    grid = std::min(grid, (size_t)cap);  // the derived grid shrinks to fit
+  }
   if (algo == HYDRA_PEER_ONE_SHOT) {
     if (p->scratch_bytes < n * es) {
       HIP_TRY(hydra::drain_device(p->device));  // first call at a new size: outside any capture
@@ -406,14 +448,21 @@ int hydra_peer_allreduce(hydra_peer_t p, int algo, int op, int dtype, int flags,
   }
   hipStream_t st = static_cast<hipStream_t>(stream);
   // Calls on one group run one after another on the device whatever streams they are issued
-  // on (a graph being captured orders its own nodes, and may not wait on an outside event).
+  // on: each EAGER call waits for the group's completion marker and records it.  A call being
+  // captured neither waits (a capture may not wait on an outside event) nor records (an event
+  // recorded inside a capture is a graph node, not a marker an eager call can wait on), so a
+  // graph's replays must be ordered by the caller against each other and against eager calls
+  // on other streams (hydra_hip.h).
   hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
   HIP_TRY(hipStreamIsCapturing(st, &cap));
   const bool capturing = cap != hipStreamCaptureStatusNone;
   if (!capturing && p->last_valid) HIP_TRY(hipStreamWaitEvent(st, p->last, 0));
-  const hipError_t e = hydra::launch_peer(
-      algo == HYDRA_PEER_ONE_SHOT ? hydra::kPeerOneShot : hydra::kPeerTwoShot, op, dtype, acc32,
-      A, (unsigned)grid, st);
+#ifdef HYDRA_MEASURE
+  if (p->stamps && grid > p->stamps_cap)
+    return fail(HYDRA_ERR_INVALID, "stamp buffer smaller than the grid");
+  A.stamps = p->stamps;
+#endif
+  const hipError_t e = hydra::launch_peer(kalgo, op, dtype, acc32, A, (unsigned)grid, st);
   if (e != hipSuccess) return hydra::hip_fail(e, "peer allreduce kernel launch");
   if (!capturing) {
     HIP_TRY(hipEventRecord(p->last, st));
@@ -421,6 +470,15 @@ int hydra_peer_allreduce(hydra_peer_t p, int algo, int op, int dtype, int flags,
   }
   return ok();
 }
+
+#ifdef HYDRA_MEASURE  // libhydra_measure.so only (include/hydra_measure.h)
+int hydra_measure_peer_stamps(hydra_peer_t p, void* dev_buf, size_t max_workgroups) {
+  if (!p) return fail(HYDRA_ERR_INVALID, "null peer");
+  p->stamps = static_cast<uint64_t*>(dev_buf);
+  p->stamps_cap = dev_buf ? max_workgroups : 0;
+  return ok();
+}
+#endif
 
 int hydra_peer_detach(hydra_peer_t p) {
   if (!p) return fail(HYDRA_ERR_INVALID, "null peer");

@@ -16,8 +16,9 @@
 namespace hydra {
 namespace {
 
-// Measurement variants (hydra_set_variant 2001..2007, f32 sum only; 0 = the shipped kernel):
-// bit 0 nontemporal loads, bit 1 nontemporal stores, bit 2 twice the loads in flight.
+// Measurement variants (libhydra_measure.so only: hydra_set_variant 2001..2007 and the phase
+// clocks of hydra_measure_peer_stamps, f32 sum; 0 = the shipped kernel): bit 0 nontemporal
+// loads, bit 1 nontemporal stores, bit 2 twice the loads in flight, bit 3 phase clocks.
 template <int V>
 __device__ __forceinline__ u32x4 pld(const char* p) {
   if constexpr ((V & 1) != 0) return ld<kNT>(p, rsrc<kNT>(nullptr, 0), 0);
@@ -200,14 +201,26 @@ __device__ __forceinline__ bool group_broken(const PeerSync& S) {
   return __syncthreads_or(bad) != 0;
 }
 
+// (V & 8) workgroup's phase clock k (kPeerStamps per workgroup), after its own stores are done
+template <int V>
+__device__ __forceinline__ void stamp(const PeerLaunch& A, int k) {
+  if constexpr ((V & 8) != 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) A.stamps[(size_t)blockIdx.x * kPeerStamps + k] = peer_clock();
+  }
+}
+
 template <typename E, int OP, bool ACC32, int V = 0>
 __global__ __launch_bounds__(kBlock) void k_peer_two_shot(PeerLaunch A) {
   const size_t SL = A.slab_bytes / sizeof(E);
   const PeerSync& Y = A.sync;
   const int P = Y.P, r = Y.rank;
   const uint32_t G = gridDim.x;
+  stamp<V>(A, 0);
   if (group_broken(Y)) return;
   if (!peer_barrier(Y, 1)) return;  // every rank's bucket is ready
+  stamp<V>(A, 1);
   PeerSrcs S;
   // phase 1: own block r, slabs k = b, b+G, ...; all P sources, in place
   {
@@ -221,7 +234,9 @@ __global__ __launch_bounds__(kBlock) void k_peer_two_shot(PeerLaunch A) {
     }
   }
   // workgroup b of every rank has finished ITS slabs (k = b mod G) of its own block
+  stamp<V>(A, 2);
   if (!peer_barrier(Y, 2)) return;
+  stamp<V>(A, 3);
   // phase 2: the same slab indices of every other block, pulled from their owners; the start
   // peer rotates with b so the workgroups of one rank read from all P-1 links at once
   for (int i = 0; i < P - 1; i++) {
@@ -233,7 +248,9 @@ __global__ __launch_bounds__(kBlock) void k_peer_two_shot(PeerLaunch A) {
     }
   }
   // nobody leaves (and lets its caller overwrite the bucket) while a peer may still read it
+  stamp<V>(A, 4);
   peer_barrier(Y, 3);
+  stamp<V>(A, 5);
 }
 
 template <typename E, int OP, bool ACC32, int V = 0>
@@ -242,8 +259,10 @@ __global__ __launch_bounds__(kBlock) void k_peer_one_shot(PeerLaunch A) {
   const PeerSync& Y = A.sync;
   const int P = Y.P, r = Y.rank;
   const uint32_t G = gridDim.x;
+  stamp<V>(A, 0);
   if (group_broken(Y)) return;
   if (!peer_barrier(Y, 1)) return;
+  stamp<V>(A, 1);
   PeerSrcs S;
   // slab list over all owner blocks: (q, k) enumerated block by block; slab w -> workgroup w%G
   size_t w = 0;
@@ -260,7 +279,9 @@ __global__ __launch_bounds__(kBlock) void k_peer_one_shot(PeerLaunch A) {
     }
   }
   // every rank's workgroup b has read its slabs of every bucket -> safe to overwrite ours
+  stamp<V>(A, 2);
   if (!peer_barrier(Y, 2)) return;
+  stamp<V>(A, 3);
   w = 0;
   for (int q = 0; q < P; q++) {
     const size_t lo = A.lo[q], hi = A.lo[q + 1];
@@ -271,10 +292,19 @@ __global__ __launch_bounds__(kBlock) void k_peer_one_shot(PeerLaunch A) {
       slab_copy<E, V>(A.x[r] + s * sizeof(E), A.scratch + s * sizeof(E), hi - s < SL ? hi - s : SL);
     }
   }
+  stamp<V>(A, 4);
+  stamp<V>(A, 5);
 }
 
 template <typename E, int OP, bool ACC32, int V = 0>
-hipError_t launch_t(int algo, const PeerLaunch& A, unsigned grid, hipStream_t s) {
+hipError_t launch_t(int algo, const PeerLaunch& A, unsigned grid, hipStream_t s,
+                    int* occ = nullptr) {
+  if (occ)  // workgroups per CU of the kernel this call would launch
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        occ,
+        algo == kPeerOneShot ? reinterpret_cast<const void*>(&k_peer_one_shot<E, OP, ACC32, V>)
+                             : reinterpret_cast<const void*>(&k_peer_two_shot<E, OP, ACC32, V>),
+        kBlock, 0);
   if (algo == kPeerOneShot)
     hipLaunchKernelGGL((k_peer_one_shot<E, OP, ACC32, V>), dim3(grid), dim3(kBlock), 0, s, A);
   else
@@ -285,22 +315,22 @@ hipError_t launch_t(int algo, const PeerLaunch& A, unsigned grid, hipStream_t s)
 // every dtype of one op (the per-op translation units' whole content)
 template <int OP>
 hipError_t dispatch(int algo, int dtype, bool acc32, const PeerLaunch& A, unsigned grid,
-                    hipStream_t s) {
+                    hipStream_t s, int* occ) {
   if (acc32) {
     if (dtype != kBF16) return hipErrorInvalidValue;
-    return launch_t<bf16_t, OP, true>(algo, A, grid, s);
+    return launch_t<bf16_t, OP, true>(algo, A, grid, s, occ);
   }
   switch (dtype) {
-    case kI8: return launch_t<int8_t, OP, false>(algo, A, grid, s);
-    case kU8: return launch_t<uint8_t, OP, false>(algo, A, grid, s);
-    case kI32: return launch_t<int32_t, OP, false>(algo, A, grid, s);
-    case kU32: return launch_t<uint32_t, OP, false>(algo, A, grid, s);
-    case kI64: return launch_t<int64_t, OP, false>(algo, A, grid, s);
-    case kU64: return launch_t<uint64_t, OP, false>(algo, A, grid, s);
-    case kF32: return launch_t<float, OP, false>(algo, A, grid, s);
-    case kF64: return launch_t<double, OP, false>(algo, A, grid, s);
-    case kF16: return launch_t<f16_t, OP, false>(algo, A, grid, s);
-    case kBF16: return launch_t<bf16_t, OP, false>(algo, A, grid, s);
+    case kI8: return launch_t<int8_t, OP, false>(algo, A, grid, s, occ);
+    case kU8: return launch_t<uint8_t, OP, false>(algo, A, grid, s, occ);
+    case kI32: return launch_t<int32_t, OP, false>(algo, A, grid, s, occ);
+    case kU32: return launch_t<uint32_t, OP, false>(algo, A, grid, s, occ);
+    case kI64: return launch_t<int64_t, OP, false>(algo, A, grid, s, occ);
+    case kU64: return launch_t<uint64_t, OP, false>(algo, A, grid, s, occ);
+    case kF32: return launch_t<float, OP, false>(algo, A, grid, s, occ);
+    case kF64: return launch_t<double, OP, false>(algo, A, grid, s, occ);
+    case kF16: return launch_t<f16_t, OP, false>(algo, A, grid, s, occ);
+    case kBF16: return launch_t<bf16_t, OP, false>(algo, A, grid, s, occ);
   }
   return hipErrorInvalidValue;
 }

@@ -31,6 +31,7 @@
 namespace hydra {
 namespace {
 
+#ifdef HYDRA_MEASURE
 constexpr int kPeerVariantBase = 2000;  // hydra_set_variant 2001..2007: peer kernel A/B
 
 // (measurement only) the f32-sum kernels with nontemporal loads / stores / deeper pipelining
@@ -46,6 +47,7 @@ hipError_t launch_variant(int v, int algo, const PeerLaunch& A, unsigned grid, h
   }
   return hipErrorInvalidValue;
 }
+#endif  // HYDRA_MEASURE
 
 }  // namespace
 
@@ -54,14 +56,31 @@ hipError_t launch_peer(int algo, int op, int dtype, bool acc32, const PeerLaunch
   if (A.sync.P < 1 || A.sync.P > kPeerMaxRanks || grid < 1 || grid > (unsigned)kPeerMaxBlocks ||
       A.slab_bytes < 16 || A.slab_bytes % 16)
     return hipErrorInvalidValue;
+#ifdef HYDRA_MEASURE
   const int v = current_variant() - kPeerVariantBase;  // (measurement only)
   if (v >= 1 && v <= 7 && op == kSum && dtype == kF32 && !acc32)
     return launch_variant(v, algo, A, grid, s);
+  if (A.stamps) {  // hydra_measure_peer_stamps: the shipped kernel plus its phase clocks
+    if (op != kSum || dtype != kF32 || acc32) return hipErrorInvalidValue;
+    return launch_t<float, kSum, false, 8>(algo, A, grid, s);
+  }
+#endif
   switch (op) {  // one translation unit per op (peer_kernels_<op>.hip)
-    case kSum: return launch_peer_sum(algo, dtype, acc32, A, grid, s);
-    case kProduct: return launch_peer_product(algo, dtype, acc32, A, grid, s);
-    case kMax: return launch_peer_max(algo, dtype, acc32, A, grid, s);
-    case kMin: return launch_peer_min(algo, dtype, acc32, A, grid, s);
+    case kSum: return launch_peer_sum(algo, dtype, acc32, A, grid, s, nullptr);
+    case kProduct: return launch_peer_product(algo, dtype, acc32, A, grid, s, nullptr);
+    case kMax: return launch_peer_max(algo, dtype, acc32, A, grid, s, nullptr);
+    case kMin: return launch_peer_min(algo, dtype, acc32, A, grid, s, nullptr);
+  }
+  return hipErrorInvalidValue;
+}
+
+hipError_t peer_occupancy(int algo, int op, int dtype, bool acc32, int* per_cu) {
+  const PeerLaunch A{};
+  switch (op) {
+    case kSum: return launch_peer_sum(algo, dtype, acc32, A, 1, nullptr, per_cu);
+    case kProduct: return launch_peer_product(algo, dtype, acc32, A, 1, nullptr, per_cu);
+    case kMax: return launch_peer_max(algo, dtype, acc32, A, 1, nullptr, per_cu);
+    case kMin: return launch_peer_min(algo, dtype, acc32, A, 1, nullptr, per_cu);
   }
   return hipErrorInvalidValue;
 }

@@ -5,8 +5,8 @@
 namespace hydra {
 
 hipError_t launch_peer_product(int algo, int dtype, bool acc32, const PeerLaunch& A, unsigned grid,
-                        hipStream_t s) {
-  return dispatch<kProduct>(algo, dtype, acc32, A, grid, s);
+                        hipStream_t s, int* occ) {
+  return dispatch<kProduct>(algo, dtype, acc32, A, grid, s, occ);
 }
 
 }  // namespace hydra

@@ -106,6 +106,7 @@ __global__ __launch_bounds__(BS) void k_reduce(E* c_, const E* a_, const E* b_, 
   }
 }
 
+#ifdef HYDRA_MEASURE  // k_reduce_lds / k_reduce_shfl: measurement variants 13, 18, 44 (libhydra_measure.so)
 // -------------------------------------------------------------------------------------------
 // LDS-DMA double-buffered variant (the staging the north star names; A/B'd against k_reduce).
 // Each wave streams its own wave-tiles (64 lanes x 16 B x U per operand) with
@@ -285,6 +286,8 @@ __global__ __launch_bounds__(kBlock) void k_reduce_shfl(E* c_, const E* a_, cons
   }
 }
 
+#endif  // HYDRA_MEASURE
+
 // -------------------------------------------------------------------------------------------
 // bf16 bucket, fp32 accumulate (BASELINE config 5): acc[i] += float(b[i]); 10 B / element.
 // acc 16-B aligned (we own it), b element-aligned.  8 elements per lane per step.
@@ -352,6 +355,7 @@ __global__ __launch_bounds__(kBlock) void k_fold(E* dst, FoldSrcs S, int nsrc, s
   }
 }
 
+#ifdef HYDRA_MEASURE  // k_reduce_pers: measurement variants 45-47
 // -------------------------------------------------------------------------------------------
 // Persistent, software-pipelined variant (measurement: variants 45-47).  A capped grid of
 // CUs x W workgroups; each workgroup streams ONE contiguous range of tiles (XCD-contiguous
@@ -406,6 +410,8 @@ __global__ __launch_bounds__(kBlock) void k_reduce_pers(E* c_, const E* a_, cons
     }
   }
 }
+
+#endif  // HYDRA_MEASURE
 
 // -------------------------------------------------------------------------------------------
 // Batched chunk-sum: K independent segments c_k = op(a_k, b_k) in ONE launch.  A caller that
@@ -538,6 +544,7 @@ hipError_t launch_t(void* c, const void* a, const void* b, size_t n, hipStream_t
   return hipGetLastError();
 }
 
+#ifdef HYDRA_MEASURE  // launchers of the measurement variants
 template <typename E, int OP, int U>
 hipError_t launch_lds(void* c, const void* a, const void* b, size_t n, hipStream_t s,
                       int blocks_per_cu) {
@@ -592,6 +599,8 @@ hipError_t launch_shfl(void* c, const void* a, const void* b, size_t n, hipStrea
   return hipGetLastError();
 }
 
+#endif  // HYDRA_MEASURE
+
 // The tuned default: one 16-B vector per lane per operand, nontemporal loads,
 // write-through sc1 stores, tiles mapped XCD-contiguously (variant 40).  Fully HBM-resident
 // (bench.py's headline, 4 rotating buffer pairs; profiles/r02_tune_rotate*.json) nontemporal
@@ -604,6 +613,7 @@ hipError_t launch_default(void* c, const void* a, const void* b, size_t n, hipSt
   return launch_t<E, OP, 1, kNT, kBuf | 16, kBlock, 1>(c, a, b, n, s, 0);
 }
 
+#ifdef HYDRA_MEASURE  // hydra_set_variant 1..52
 template <typename E, int OP>
 hipError_t launch_tuning(int variant, void* c, const void* a, const void* b, size_t n,
                           hipStream_t s) {
@@ -665,6 +675,8 @@ hipError_t launch_tuning(int variant, void* c, const void* a, const void* b, siz
   }
 }
 
+#endif  // HYDRA_MEASURE
+
 // Measurement variants exist only for the fp32/int32 sum (the benchmarked path); every other
 // dtype/op combination always runs the tuned default.
 template <typename E, int OP>
@@ -672,9 +684,14 @@ hipError_t launch_variant(int variant, void* c, const void* a, const void* b, si
                           hipStream_t s) {
   constexpr bool kTunable = OP == kSum && (std::is_same<E, float>::value ||
                                           std::is_same<E, int32_t>::value);
+#ifdef HYDRA_MEASURE
   if constexpr (kTunable) {
     if (variant != 0) return launch_tuning<E, OP>(variant, c, a, b, n, s);
   }
+#else
+  (void)variant;
+  (void)kTunable;
+#endif
   return launch_default<E, OP>(c, a, b, n, s);
 }
 
@@ -734,6 +751,7 @@ hipError_t launch_fold_v(void* dst, const void* const* srcs, int nsrc, size_t n,
 template <typename E, int OP, bool ACC32>
 hipError_t launch_fold_t(void* dst, const void* const* srcs, int nsrc, size_t n, hipStream_t s) {
   switch (current_variant()) {
+#ifdef HYDRA_MEASURE
     case 1: return launch_fold_v<E, OP, ACC32, false>(dst, srcs, nsrc, n, s, 8);
     case 2: return launch_fold_v<E, OP, ACC32, true>(dst, srcs, nsrc, n, s, 8);
     case 3: return launch_fold_v<E, OP, ACC32, true>(dst, srcs, nsrc, n, s, 0);
@@ -741,6 +759,7 @@ hipError_t launch_fold_t(void* dst, const void* const* srcs, int nsrc, size_t n,
     case 5: return launch_fold_v<E, OP, ACC32, false, 1>(dst, srcs, nsrc, n, s, 0);  // full grid
     case 6: return launch_fold_v<E, OP, ACC32, true, 1>(dst, srcs, nsrc, n, s, 0);   // 3, XCD map
     case 7: return launch_fold_v<E, OP, ACC32, true, 1>(dst, srcs, nsrc, n, s, 8);   // 2, XCD map
+#endif
     default:  // tuned HBM-resident (profiles/r02_tune_fold_rot.json, 3 rotating source sets):
               // same-type folds nontemporal loads, full grid, XCD-contiguous (variant 6: P=8
               // fp32 46.5 us = 6.49 TB/s, vs 55.3 us for round 1's plain-load choice, which had

@@ -39,7 +39,7 @@ namespace hydra {
 
 constexpr int kResidentSegs = 16;
 constexpr int kResidentBlocks = 128;
-constexpr int kResidentMaxBlocks = 1024;  // HYDRA_RESIDENT_SHAPE's bound (the job word holds nwg)
+constexpr int kResidentMaxBlocks = 1024;  // HYDRA_OPT_RESIDENT_BLOCKS's bound (the job word holds nwg)
 constexpr int kResidentSlots = 32;  // contexts served at once per device (lanes of wave 0)
 
 struct ResSeg {  // one c = op(a, b): vector body + ragged head / tail, split on c (as the batch)
@@ -109,7 +109,6 @@ hipError_t launch_resident(ResCtl* h, ResDev* d, uint64_t gen, uint64_t idle_tic
 // thread at a time and are synchronous per round: submit, then wait, then the next submit.
 struct ResidentLease;
 
-bool resident_enabled();  // HYDRA_RESIDENT != "0"
 // A slot of `device`'s reducer, or null when it is off or every slot is leased (the caller
 // then launches).  Errors (device setup) are returned as HYDRA codes with the message set.
 int resident_lease(int device, ResidentLease** out);

@@ -14,6 +14,7 @@
 
 #include "../../include/hydra_hip.h"
 #include "errors.h"
+#include "options.h"
 #include "resident.h"
 #include "resource_cache.h"
 
@@ -50,40 +51,20 @@ std::mutex g_mu;
 std::atomic<ResidentServer*> g_srv[kMaxDevices] = {};  // set once each (under g_mu)
 std::atomic<bool> g_exiting{false};
 
-uint64_t idle_ticks() {  // s_memrealtime runs at 100 MHz
-  static const uint64_t t = [] {
-    const char* v = std::getenv("HYDRA_RESIDENT_IDLE_US");
-    const long us = v ? std::atol(v) : 2000;
-    return (uint64_t)std::max(50L, std::min(us, 1000000L)) * 100;
-  }();
-  return t;
-}
+// Settings of an instance, read at each launch (hydra_set_option, options.h; s_memrealtime
+// ticks run at 100 MHz): leave after HYDRA_OPT_RESIDENT_IDLE_US without a call (2 ms); bound
+// every wait inside the grid by HYDRA_OPT_RESIDENT_GRACE_US (10 s).
+uint64_t idle_ticks() { return (uint64_t)opt(HYDRA_OPT_RESIDENT_IDLE_US) * 100; }
+uint64_t grace_ticks() { return (uint64_t)opt(HYDRA_OPT_RESIDENT_GRACE_US) * 100; }
 
-uint64_t grace_ticks() {  // the bound of every wait inside the grid (default 10 s)
-  static const uint64_t t = [] {
-    const char* v = std::getenv("HYDRA_RESIDENT_GRACE_US");
-    const long us = v ? std::atol(v) : 10000000L;
-    return (uint64_t)std::max(1000L, std::min(us, 600000000L)) * 100;
-  }();
-  return t;
-}
-
-const ResidentShape& shape() {
-  static const ResidentShape sh = [] {
-    ResidentShape r;
-    if (const char* v = std::getenv("HYDRA_RESIDENT_SHAPE")) {
-      int b = r.blocks, u = r.batch;
-      unsigned so = r.solo, tp = r.tiles_per_block;
-      if (std::sscanf(v, "%d,%d,%u,%u", &b, &u, &so, &tp) >= 1) {
-        r.blocks = std::max(1, std::min(b, kResidentMaxBlocks));
-        r.batch = u >= 4 ? 4 : u >= 2 ? 2 : 1;
-        r.solo = std::min(so, 64u);
-        r.tiles_per_block = std::max(1u, std::min(tp, 64u));
-      }
-    }
-    return r;
-  }();
-  return sh;
+ResidentShape shape() {  // HYDRA_OPT_RESIDENT_BLOCKS / _BATCH / _SOLO / _TILES
+  ResidentShape r;
+  r.blocks = (int)std::min<int64_t>(opt(HYDRA_OPT_RESIDENT_BLOCKS), kResidentMaxBlocks);
+  const int64_t u = opt(HYDRA_OPT_RESIDENT_BATCH);
+  r.batch = u >= 4 ? 4 : u >= 2 ? 2 : 1;
+  r.solo = (uint32_t)opt(HYDRA_OPT_RESIDENT_SOLO);
+  r.tiles_per_block = (uint32_t)opt(HYDRA_OPT_RESIDENT_TILES);
+  return r;
 }
 
 template <typename T>
@@ -115,13 +96,12 @@ void quit_all() {
 //    per priority level among a process's streams, so a plain stream can land behind the grid.
 //    The greatest-priority level has a pool of its own, which ordinary code (torch's default
 //    and pool streams, RCCL) does not use.
-// HYDRA_RESIDENT_QUEUE=shared (a plain non-blocking stream) and =cumask (a CU-masked stream:
-// a queue of its own, but blocking) are A/B settings only (scripts/probe_queue_block.py).
+// HYDRA_OPT_RESIDENT_QUEUE 1 (a plain non-blocking stream) and 2 (a CU-masked stream: a queue
+// of its own, but blocking) are A/B settings only (scripts/probe_queue_block.py).
 hipError_t make_stream(int device, hipStream_t* out) {
-  const char* v = std::getenv("HYDRA_RESIDENT_QUEUE");
-  if (v && std::strcmp(v, "shared") == 0)
-    return hipStreamCreateWithFlags(out, hipStreamNonBlocking);
-  if (v && std::strcmp(v, "cumask") == 0) {
+  const int64_t q = opt(HYDRA_OPT_RESIDENT_QUEUE);
+  if (q == 1) return hipStreamCreateWithFlags(out, hipStreamNonBlocking);
+  if (q == 2) {
     hipDeviceProp_t p;
     hipError_t e = hipGetDeviceProperties(&p, device);
     if (e != hipSuccess) return e;
@@ -240,17 +220,8 @@ ResidentServer* find_server(int device) {
 }
 }  // namespace
 
-bool resident_enabled() {
-  static const bool on = [] {
-    const char* v = std::getenv("HYDRA_RESIDENT");
-    return !(v && v[0] == '0');
-  }();
-  return on;
-}
-
 int resident_lease(int device, ResidentLease** out) {
   *out = nullptr;
-  if (!resident_enabled()) return HYDRA_OK;
   ResidentServer* v = nullptr;
   if (int rc = server(device, &v)) return rc;
   std::lock_guard<std::mutex> g(v->mu);

@@ -199,13 +199,15 @@ int validate_plan(const std::vector<hydra::PlanOp>& plan, int nranks, size_t es,
 struct hydra_comm {
   int rank = 0, nranks = 1, device = 0;
   bool aborted = false;  // hydra_comm_wait timed out: nccl was aborted
-  bool ran = false;      // the last plan ran eagerly: ev_ks marks the end of its folds
+  // the end of the last EAGER call's folds on ks (ev_mark, recorded only outside a capture, so a
+  // captured call in between never clears it: ADVICE r05)
+  bool marked = false;
   ncclComm_t nccl = nullptr;
   hipStream_t cs = nullptr, ks = nullptr;  // comm stream, compute stream
   void* scratch = nullptr;
   size_t scratch_bytes = 0;
   std::vector<hipEvent_t> events;
-  hipEvent_t ev_start = nullptr, ev_cs = nullptr, ev_ks = nullptr;
+  hipEvent_t ev_start = nullptr, ev_cs = nullptr, ev_ks = nullptr, ev_mark = nullptr;
   // plan cache
   int key_algo = -1;
   size_t key_n = 0, key_es = 0, key_ms = 0, key_chunk = 0;
@@ -402,7 +404,7 @@ int run_plan_rccl(hydra_comm* c, int op, int dtype, bool acc32, char* user, hipE
   hipStreamCaptureStatus cs_state = hipStreamCaptureStatusNone;
   HIP_TRY(hipStreamIsCapturing(user_st, &cs_state));
   const bool capturing = cs_state != hipStreamCaptureStatusNone;
-  if (c->ran && !capturing) HIP_TRY(hipStreamWaitEvent(c->cs, c->ev_ks, 0));
+  if (c->marked && !capturing) HIP_TRY(hipStreamWaitEvent(c->cs, c->ev_mark, 0));
   size_t i = 0;
   while (i < ops.size()) {
     const hydra::PlanOp& o = ops[i];
@@ -467,7 +469,10 @@ int run_plan_rccl(hydra_comm* c, int op, int dtype, bool acc32, char* user, hipE
   }
   HIP_TRY(hipEventRecord(c->ev_cs, c->cs));
   HIP_TRY(hipEventRecord(c->ev_ks, c->ks));
-  c->ran = !capturing;  // (an ev_ks recorded inside a capture is a graph node, not a marker)
+  if (!capturing) {  // (an event recorded inside a capture is a graph node, not a marker)
+    HIP_TRY(hipEventRecord(c->ev_mark, c->ks));
+    c->marked = true;
+  }
   return HYDRA_OK;
 }
 
@@ -512,6 +517,7 @@ int hydra_comm_init(hydra_comm_t* out, int nranks, int rank, const void* id, int
   if (e == hipSuccess) e = hydra::cached_event(device, &c->ev_start);
   if (e == hipSuccess) e = hydra::cached_event(device, &c->ev_cs);
   if (e == hipSuccess) e = hydra::cached_event(device, &c->ev_ks);
+  if (e == hipSuccess) e = hydra::cached_event(device, &c->ev_mark);
   if (e != hipSuccess) {
     hydra_comm_destroy(c);
     return hydra::hip_fail(e, "hydra_comm_init streams");
@@ -616,7 +622,7 @@ int hydra_comm_destroy(hydra_comm_t c) {
                                    ncclGetErrorString(r));
   }
   for (auto e : c->events) step(hydra::release_event(e), "comm teardown: release event");
-  for (auto e : {c->ev_start, c->ev_cs, c->ev_ks})
+  for (auto e : {c->ev_start, c->ev_cs, c->ev_ks, c->ev_mark})
     if (e) step(hydra::release_event(e), "comm teardown: release event");
   if (c->cs) step(hydra::release_stream(c->cs), "comm teardown: release stream");
   if (c->ks) step(hydra::release_stream(c->ks), "comm teardown: release stream");
@@ -1119,7 +1125,7 @@ int hydra_comm_run_plan(hydra_comm_t c, const hydra_plan_op_t* ops, size_t nops,
   if (scratch_bytes) {
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     HIP_TRY(hipStreamIsCapturing(st, &cap));
-    if (c->ran && cap == hipStreamCaptureStatusNone) HIP_TRY(hipStreamWaitEvent(st, c->ev_ks, 0));
+    if (c->marked && cap == hipStreamCaptureStatusNone) HIP_TRY(hipStreamWaitEvent(st, c->ev_mark, 0));
     HIP_TRY(hipMemsetAsync(c->scratch, 0, scratch_bytes, st));
   }
   if ((rc = prof_begin(c, st))) return rc;

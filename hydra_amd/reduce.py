@@ -110,6 +110,10 @@ class HostContext:
     def handle(self) -> int:
         return self._h.value
 
+    def set_option(self, key: int, value: int) -> None:
+        """hydra_ctx_set_option: a per-context option (_lib.OPT_*, e.g. OPT_FORCE_STAGING)."""
+        check(_lib.lib().hydra_ctx_set_option(self._h, key, int(value)))
+
     def stats(self) -> dict:
         """Calls the resident reducer served and instances launched (hydra_ctx_stats)."""
         calls, launches = ctypes.c_uint64(), ctypes.c_uint64()

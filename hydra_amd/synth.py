@@ -102,6 +102,21 @@ def stress_at(P: int, rank: int, idx, seed: int = 77):
     return (m.to(torch.float32) * (2.0 ** -23) - 1.0) * scale
 
 
+def fill_at(gen, P: int, rank: int, n: int, device, dtype, chunk: int = 16 << 20, out=None):
+    """gen(P, rank, idx) (stress_at / stress_cancel_at) over all n indices as a torch tensor of
+    `dtype` on `device` (bf16: RNE, as bf16_bits), generated `chunk` elements at a time: the
+    int64 indices and hashing temporaries of a 256 Mi bucket would otherwise take several GiB.
+    Writes into `out` when given."""
+    import torch
+
+    if out is None:
+        out = torch.empty(n, dtype=dtype, device=device)
+    for lo in range(0, n, chunk):
+        hi = min(n, lo + chunk)
+        out[lo:hi] = gen(P, rank, torch.arange(lo, hi, device=device, dtype=torch.int64)).to(dtype)
+    return out
+
+
 def stress_cancel_at(P: int, rank: int, idx, seed: int = 91):
     """Fold-order stress for buckets that are rounded once more after the fold (config 5: fp32
     accumulation of bf16 data, one rounding to bf16).  stress_at's values differ between fold

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define HYDRA_ABI_VERSION 1
+#define HYDRA_ABI_VERSION 2
 
 typedef enum {
   HYDRA_INT8 = 0,
@@ -129,8 +129,49 @@ int hydra_f32_to_bf16(void* out_bf16, const float* acc, size_t n, hydra_stream_t
 int hydra_fold(int op, int dtype, int flags, void* dst, const void* const* srcs, int nsrc,
                size_t n, hydra_stream_t stream);
 
-/* Kernel variant selection for measurement (0 = tuned default).  Returns the previous value. */
-int hydra_set_variant(int variant);
+/* ---- library options -----------------------------------------------------------------------
+ * The library reads no environment variable: every tunable is an option with the tuned default
+ * (the reference's benchmark takes its settings as flags, benchmark/options.cc:144-172).
+ * hydra_set_option sets the process-wide value, which applies to what starts afterwards (a
+ * resident reducer instance, the staging copy pool, contexts created later); the keys marked
+ * [ctx] are copied into each context at hydra_ctx_create and hydra_ctx_set_option overrides them
+ * for that context alone.  Out-of-range values and unknown keys: HYDRA_ERR_INVALID.
+ *   HYDRA_OPT_RESIDENT             [ctx] 1 (default): host calls are served by the device's
+ *                                  resident reducer; 0: one batched launch per round
+ *   HYDRA_OPT_STAGE_SPLIT          [ctx] rounds a staged call is cut into (4; 1..64)
+ *   HYDRA_OPT_ROUND_MIN            [ctx] smallest staging round per operand, bytes (512 KiB;
+ *                                  16 KiB..4 MiB)
+ *   HYDRA_OPT_STAGE_RESULT_MAX     [ctx] results of calls of at most this many bytes per operand
+ *                                  go through the pinned staging (0)
+ *   HYDRA_OPT_STAGE_RESULT_REG_MAX [ctx] ... and results inside a hydra_host_register'ed range of
+ *                                  at most this many bytes (8 MiB: such a bucket stays in the
+ *                                  CPU's cache for the ring's next send)
+ *   HYDRA_OPT_FORCE_STAGING        [ctx] 1: stage every operand, mapped or not (A/B; 0)
+ *   HYDRA_OPT_COPY_THREADS         helper threads of the staging copies (4; 0..32: 0 = the
+ *                                  calling thread alone); fixed once the first large copy ran
+ *   HYDRA_OPT_RESIDENT_IDLE_US     a resident instance leaves after this long idle (2000)
+ *   HYDRA_OPT_RESIDENT_GRACE_US    bound of every wait inside the resident grid (10 s)
+ *   HYDRA_OPT_RESIDENT_QUEUE       0 (default): a greatest-priority queue of its own;
+ *                                  1 a plain non-blocking stream; 2 a CU-masked stream (A/B)
+ *   HYDRA_OPT_RESIDENT_BLOCKS, _BATCH, _SOLO, _TILES: the resident grid's shape (128, 4, 4, 4) */
+typedef enum {
+  HYDRA_OPT_RESIDENT = 1,
+  HYDRA_OPT_STAGE_SPLIT = 2,
+  HYDRA_OPT_ROUND_MIN = 3,
+  HYDRA_OPT_STAGE_RESULT_MAX = 4,
+  HYDRA_OPT_STAGE_RESULT_REG_MAX = 5,
+  HYDRA_OPT_FORCE_STAGING = 6,
+  HYDRA_OPT_COPY_THREADS = 7,
+  HYDRA_OPT_RESIDENT_IDLE_US = 8,
+  HYDRA_OPT_RESIDENT_GRACE_US = 9,
+  HYDRA_OPT_RESIDENT_QUEUE = 10,
+  HYDRA_OPT_RESIDENT_BLOCKS = 11,
+  HYDRA_OPT_RESIDENT_BATCH = 12,
+  HYDRA_OPT_RESIDENT_SOLO = 13,
+  HYDRA_OPT_RESIDENT_TILES = 14
+} hydra_opt_t;
+int hydra_set_option(int key, long long value);
+int hydra_get_option(int key, long long* value);
 
 /* Test switches: process-wide values the library reads at the point they apply, so tests can
  * drive branches a one-GPU box never takes on its own.  Every switch is 0 in production (the
@@ -159,9 +200,12 @@ int hydra_test_get(int key, int64_t* value);
  * staged bytes per operand, or per 16 intervals, beyond that: the CPU fills round r + 1 while
  * round r runs).  Device pointers are rejected (HYDRA_ERR_INVALID: use hydra_reduce).  One
  * context per calling thread (bew_allreduce_a runs two rails concurrently: one context each).
- * hydra_set_variant(1000) stages every operand (A/B measurements). */
+ * hydra_ctx_set_option: a [ctx] key of hydra_opt_t for this context alone (e.g.
+ * HYDRA_OPT_FORCE_STAGING stages every operand for A/B measurements; HYDRA_OPT_RESIDENT 0
+ * returns the context's resident slot). */
 int hydra_ctx_create(int device, hydra_ctx_t* out);
 int hydra_ctx_destroy(hydra_ctx_t ctx);
+int hydra_ctx_set_option(hydra_ctx_t ctx, int key, long long value);
 int hydra_reduce_host(hydra_ctx_t ctx, int op, int dtype, void* c, const void* a, const void* b,
                       size_t n);
 int hydra_chunk_sum_host(hydra_ctx_t ctx, int dtype, void* c, const void* a, const void* b,
@@ -171,8 +215,8 @@ int hydra_chunk_sum_host(hydra_ctx_t ctx, int dtype, void* c, const void* a, con
  * hardware queue of its own (no other stream's work waits behind it), woken by a host-mapped
  * doorbell instead of a fresh dispatch.  Each context leases one of its 32 slots at
  * hydra_ctx_create (a context created when all are leased launches instead).  The instance
- * leaves after HYDRA_RESIDENT_IDLE_US (default 2000) without a call and at process exit.
- * HYDRA_RESIDENT=0 turns it off (every round is one launch on the context's stream).  Stats
+ * leaves after HYDRA_OPT_RESIDENT_IDLE_US (default 2000) without a call and at process exit.
+ * HYDRA_OPT_RESIDENT 0 turns it off (every round is one launch on the context's stream).  Stats
  * (tests): rounds this context had served by it, and instances launched on its device. */
 int hydra_ctx_stats(hydra_ctx_t ctx, uint64_t* resident_calls, uint64_t* resident_launches);
 /* Per-call trace of hydra_reduce_host (measurement: where a call's time goes).  While enabled,

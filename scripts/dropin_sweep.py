@@ -26,13 +26,14 @@ sizes = ([int(x) for x in os.environ["SIZES"].split(",")] if os.environ.get("SIZ
 REPS = int(os.environ.get("REPS", "3"))
 # (name, HYDRA_DROPIN_REGISTER, extra environment): the hydra Func alone, with the bucket
 # registered once (the library's default path choice: results staged while the registration is
-# at most HYDRA_STAGE_RESULT_REG_MAX, 8 MiB), and (STAGE_RESULT_AB=1) the two fixed choices:
-# every result written in place over PCIe, every result staged
+# at most HYDRA_OPT_STAGE_RESULT_REG_MAX, 8 MiB), and (STAGE_RESULT_AB=1) the two fixed choices:
+# every result written in place over PCIe, every result staged (library options passed to the
+# harness as HYDRA_DROPIN_OPT="key=value,...": keys 4 = STAGE_RESULT_MAX, 5 = _REG_MAX)
 MODES = [("hydra", "0", {}), ("hydra_registered", "1", {})]
 if os.environ.get("STAGE_RESULT_AB") == "1":
-    MODES.append(("hydra_registered_zero_copy_result", "1", {"HYDRA_STAGE_RESULT_REG_MAX": "0"}))
+    MODES.append(("hydra_registered_zero_copy_result", "1", {"HYDRA_DROPIN_OPT": "5=0"}))
     MODES.append(("hydra_registered_staged_result", "1",
-                  {"HYDRA_STAGE_RESULT_REG_MAX": "0", "HYDRA_STAGE_RESULT_MAX": str(1 << 30)}))
+                  {"HYDRA_DROPIN_OPT": f"5=0,4={1 << 30}"}))
 # every process of the sweep on the same CPUs: the GPU's NUMA node, never CPU 0 (bench.py's
 # placement for the CPU baselines); PIN=0 leaves the affinity alone
 sys.path.insert(0, ROOT)

@@ -32,6 +32,8 @@ from hydra_amd import _lib  # noqa: E402
 from hydra_amd.reduce import HostContext  # noqa: E402
 
 L = _lib.lib()
+# HYDRA_RESIDENT=0 in this script's environment: the library option HYDRA_OPT_RESIDENT = 0
+_lib.set_option(_lib.OPT_RESIDENT, 0 if os.environ.get("HYDRA_RESIDENT") == "0" else 1)
 SIZES = [int(x) for x in os.environ.get("FLOOR_SIZES", "64,1024,16384,262144").split(",")]
 
 
@@ -80,12 +82,12 @@ def main():
             ops["pageable"] = (xa.ctypes.data, xb.ctypes.data)
             ops["registered_staged"] = ops["registered"]
             for mode, (a, b) in ops.items():
-                prev = L.hydra_set_variant(1000 if mode == "registered_staged" else 0)
+                ctx.set_option(_lib.OPT_FORCE_STAGING, 1 if mode == "registered_staged" else 0)
                 try:
                     r = timed(lambda: _lib.check(
                         L.hydra_reduce_host(ctx.handle, 0, 6, a, a, b, n)), n)
                 finally:
-                    L.hydra_set_variant(prev)
+                    ctx.set_option(_lib.OPT_FORCE_STAGING, 0)
                 rows.append(dict(elements=n, mode=mode, **r))
                 print(json.dumps(rows[-1]), file=sys.stderr, flush=True)
 

@@ -72,11 +72,11 @@ for n in iso_sizes:
                  "bucket_registered_b_pageable"):
         # "pageable": copied by the CPU through the context's pinned staging (hydra never pins
         # pageable memory for a call); "registered_staged": registered, but forced through the
-        # staging (variant 1000); "_zero_copy": the kernel reads and writes the registered host
+        # staging (HYDRA_OPT_FORCE_STAGING); "_zero_copy": the kernel reads and writes the registered host
         # ranges over PCIe directly (hydra_reduce_host's default whenever all three ranges are
         # pinned/registered); "bucket_registered_b_pageable": only c == a registered (a bucket
         # registered once), b pageable like the reference ring's scratch
-        prev = L.hydra_set_variant(1000 if mode == "registered_staged" else 0)
+        ctx.set_option(_lib.OPT_FORCE_STAGING, 1 if mode == "registered_staged" else 0)
         bb = b if mode != "bucket_registered_b_pageable" else np.ones(n, np.float32)
         if mode != "pageable":
             _lib.check(L.hydra_host_register(a.ctypes.data, a.nbytes))
@@ -90,7 +90,7 @@ for n in iso_sizes:
             _lib.check(L.hydra_reduce_host(ctx.handle, 0, 6, a.ctypes.data, a.ctypes.data,
                                            bb.ctypes.data, n))
         dt = (time.perf_counter() - t0) / reps
-        L.hydra_set_variant(prev)
+        ctx.set_option(_lib.OPT_FORCE_STAGING, 0)
         if mode != "pageable":
             L.hydra_host_unregister(a.ctypes.data)
         if mode in ("registered_staged", "registered_zero_copy"):
@@ -184,7 +184,7 @@ out["config1_new_allreduce_ring_P2"] = c1
 out["config3_bew_allreduce_a_P2"] = c3
 out["reps"] = REPS
 if os.environ.get("TABLE"):  # the reference benchmark's own table per implementation
-    from hydra_amd import report
+    from benchkit import report
 
     algo = {"c1": "new_allreduce_ring", "c3": "bew_allreduce_a"}
     with open(os.environ["TABLE"], "w") as f:

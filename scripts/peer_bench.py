@@ -39,6 +39,7 @@ def worker(a):
     torch.cuda.set_device(dev)
     from hydra_amd import _lib
 
+    _lib.select_measure()  # the peer A/B variants (hydra_set_variant) live in libhydra_measure.so
     # every rank's grid must be resident at once on the one GPU (512 of the kernel's workgroups
     # fit): --blocks 0 = 512 / P per rank
     peer = PeerComm(a.rank, a.P, 0, blocks=a.blocks or max(1, 512 // a.P))

@@ -34,6 +34,11 @@ int main(int argc, char** argv) {
   size_t big = 1 << 22;  // elements per buffer (room for the largest size + the offsets)
   for (size_t n : sizes) big = std::max(big, (n + 4096 + 1023) / 1024 * 1024);
   hydra_ctx_t ctx;
+  // HYDRA_RESIDENT=0 in this probe's environment: the same calls with the resident reducer
+  // off (the library itself reads no environment; HYDRA_OPT_RESIDENT is its option)
+  const char* env = std::getenv("HYDRA_RESIDENT");
+  const bool resident = !(env && env[0] == '0');
+  CK(hydra_set_option(HYDRA_OPT_RESIDENT, resident ? 1 : 0));
   CK(hydra_ctx_create(0, &ctx));
   // registered: mmap'ed, never returned to the allocator
   float* ra = static_cast<float*>(mmap(nullptr, big * 4, PROT_READ | PROT_WRITE,
@@ -83,9 +88,8 @@ int main(int argc, char** argv) {
     }
   uint64_t calls = 0, launches = 0;
   CK(hydra_ctx_stats(ctx, &calls, &launches));
-  const char* env = std::getenv("HYDRA_RESIDENT");
   std::printf("], \"resident\": %s, \"resident_calls\": %llu, \"resident_launches\": %llu}\n",
-              (env && env[0] == '0') ? "false" : "true", (unsigned long long)(calls - calls0),
+              resident ? "true" : "false", (unsigned long long)(calls - calls0),
               (unsigned long long)(launches - launches0));
   CK(hydra_host_unregister(ra));
   CK(hydra_host_unregister(rb));

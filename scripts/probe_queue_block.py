@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Does the resident reducer's persistent grid hold up other streams' work?  With an instance
 alive (idle limit 1 s), time a tiny torch kernel on each of 24 fresh streams and on the default
-stream.  Run once per HYDRA_RESIDENT_QUEUE setting: the default (a non-blocking stream of the
+stream.  Run once per HYDRA_OPT_RESIDENT_QUEUE setting: the default (a non-blocking stream of the
 greatest priority), `cumask` (a CU-masked stream: a hardware queue of its own, but blocking)
 and `shared` (a plain non-blocking stream, which the runtime may put on a hardware queue another
 stream uses); the default once more with 8 of torch's high-priority streams added.  Prints one
@@ -14,12 +14,15 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-from tests.test_gpu_resident import _BLOCKING_PROBE  # noqa: E402
+from hydra_amd import _lib  # noqa: E402
+from tests.test_gpu_resident import _BLOCKING_PROBE, _with_opts  # noqa: E402
 
+QUEUE = {"priority": 0, "shared": 1, "cumask": 2}  # HYDRA_OPT_RESIDENT_QUEUE
 for mode, hi in (("priority", 0), ("cumask", 0), ("shared", 0), ("priority", 8)):
-    env = dict(os.environ, HYDRA_RESIDENT_IDLE_US="1000000", HYDRA_RESIDENT_QUEUE=mode)
-    p = subprocess.run([sys.executable, "-c", _BLOCKING_PROBE % ROOT, str(hi)],
-                       capture_output=True, text=True, timeout=120, env=env)
+    code = _with_opts(_BLOCKING_PROBE % ROOT, {_lib.OPT_RESIDENT_IDLE_US: 1000000,
+                                                _lib.OPT_RESIDENT_QUEUE: QUEUE[mode]})
+    p = subprocess.run([sys.executable, "-c", code, str(hi)],
+                       capture_output=True, text=True, timeout=120)
     row = {"queue": mode, "torch_high_priority_streams": hi, "rc": p.returncode}
     if p.returncode == 0:
         row.update(json.loads(p.stdout.strip().splitlines()[-1]))

@@ -1,5 +1,5 @@
 // probe_stage_split.cc -- interleaved A/B of how many rounds a staged (pageable) host call is
-// cut into (hydra_set_variant 1100 + split; HYDRA_STAGE_SPLIT is the default's knob).  For each
+// cut into (hydra_ctx_set_option HYDRA_OPT_STAGE_SPLIT; the default is 4).  For each
 // size the splits take turns in short blocks, rotated every repetition, so drift on the box
 // (page cache, helper-thread placement, other tenants) lands on every setting alike.  c == a,
 // both pageable, as the ring calls an unregistered Func.  Prints one JSON document: median and
@@ -42,7 +42,7 @@ int main(int argc, char** argv) {
     for (int r = 0; r < reps; r++)
       for (int j = 0; j < S; j++) {
         const int k = (j + r) % S;
-        hydra_set_variant(1100 + splits[k]);
+        CK(hydra_ctx_set_option(ctx, HYDRA_OPT_STAGE_SPLIT, splits[k]));
         CK(hydra_reduce_host(ctx, HYDRA_SUM, HYDRA_FLOAT32, pa, pa, pb, n));  // settle
         for (int i = 0; i < block; i++) {
           const auto t0 = std::chrono::steady_clock::now();
@@ -52,7 +52,7 @@ int main(int argc, char** argv) {
                   .count());
         }
       }
-    hydra_set_variant(0);
+    CK(hydra_ctx_set_option(ctx, HYDRA_OPT_STAGE_SPLIT, 4));
     for (int k = 0; k < S; k++) {
       std::sort(us[k].begin(), us[k].end());
       const size_t m = us[k].size();

@@ -30,6 +30,11 @@ from hydra_amd.reduce import HostContext  # noqa: E402
 from oracle import oracle as O  # noqa: E402
 
 L = _lib.lib()
+# the script's HYDRA_RESIDENT_IDLE_US / HYDRA_RESIDENT_GRACE_US -> the library's options
+for _k, _e in ((_lib.OPT_RESIDENT_IDLE_US, "HYDRA_RESIDENT_IDLE_US"),
+               (_lib.OPT_RESIDENT_GRACE_US, "HYDRA_RESIDENT_GRACE_US")):
+    if os.environ.get(_e):
+        _lib.set_option(_k, int(os.environ[_e]))
 POOL_ELEMS = 3 << 20  # registered pool per worker (lives for the process)
 
 

@@ -11,7 +11,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from hydra_amd import _lib  # noqa: E402
 
-L = _lib.lib()
+L = _lib.measure_lib()  # the A/B variants live in the measurement build
 dev = torch.device("cuda", 0)
 variants = [int(v) for v in os.environ.get("VARIANTS", ",".join(map(str, range(20)))).split(",")]
 sizes = [int(s) for s in os.environ.get("SIZES", str(64 << 20)).split(",")]

@@ -12,7 +12,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from hydra_amd import _lib  # noqa: E402
 
-L = _lib.lib()
+L = _lib.measure_lib()  # the A/B variants live in the measurement build
 dev = torch.device("cuda", 0)
 s = torch.cuda.current_stream(dev)
 res = {}

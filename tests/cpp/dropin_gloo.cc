@@ -399,6 +399,25 @@ int run_errors(size_t n) {
 }  // namespace
 
 int main(int argc, char** argv) {
+  // HYDRA_DROPIN_OPT="key=value,...": hydra_set_option calls before anything runs (the test's
+  // way to pick a library option for this process; the library itself reads no environment)
+  if (const char* o = std::getenv("HYDRA_DROPIN_OPT")) {
+    std::string spec(o);
+    size_t at = 0;
+    while (at < spec.size()) {
+      size_t end = spec.find(',', at);
+      if (end == std::string::npos) end = spec.size();
+      const std::string kv = spec.substr(at, end - at);
+      const size_t eq = kv.find('=');
+      if (eq != std::string::npos &&
+          hydra_set_option(std::atoi(kv.substr(0, eq).c_str()),
+                           std::strtoll(kv.substr(eq + 1).c_str(), nullptr, 10)) != 0) {
+        std::fprintf(stderr, "hydra_set_option(%s): %s\n", kv.c_str(), hydra_last_error());
+        return 2;
+      }
+      at = end + 1;
+    }
+  }
   if (argc >= 2 && std::string(argv[1]) == "errors")
     return run_errors(argc > 3 ? std::strtoull(argv[3], nullptr, 10) : 1000);
   if (argc < 5) {

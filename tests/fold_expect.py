@@ -42,16 +42,5 @@ def sample_indices(n, ns, seg, count=1 << 20, seed=55):
 
 
 def device_bucket(gen, P, rank, n, dev, out_dtype, chunk=16 << 20, out=None):
-    """gen(P, rank, idx) (synth.stress_at / stress_cancel_at) over all n indices, generated on
-    the GPU `chunk` elements at a time (the int64 index and hashing temporaries of a 256 Mi
-    bucket would otherwise take several GiB per rank) and stored as out_dtype (torch.float32,
-    or torch.bfloat16 -- RNE, as synth.bf16_bits).  Writes into `out` when given."""
-    import torch
-
-    if out is None:
-        out = torch.empty(n, dtype=out_dtype, device=dev)
-    for lo in range(0, n, chunk):
-        hi = min(n, lo + chunk)
-        idx = torch.arange(lo, hi, device=dev, dtype=torch.int64)
-        out[lo:hi] = gen(P, rank, idx).to(out_dtype)
-    return out
+    """gen(P, rank, idx) over all n indices on `dev` (synth.fill_at, chunked)."""
+    return synth.fill_at(gen, P, rank, n, dev, out_dtype, chunk=chunk, out=out)

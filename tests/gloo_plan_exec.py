@@ -11,7 +11,7 @@ alltoall), ALLGATHER through all_gather.  REDUCE / FOLD run
     one GPU of the test box (RCCL refuses two ranks on one GPU), so the plans run across
     processes with the product kernels (tests/test_gpu_dist_plans.py).
 `GlooPlanComm` wraps the CPU form in XgmiComm's interface, so the N>1 bench orchestration
-(hydra_amd.ring.bench_allreduce) runs unchanged at world size 2 and 3 on the CPU."""
+(benchkit.allreduce.bench_allreduce) runs unchanged at world size 2 and 3 on the CPU."""
 import numpy as np
 
 SEND, RECV, GROUP, REDUCE, FOLD, ALLTOALL, ALLGATHER = 1, 2, 3, 4, 5, 6, 7

@@ -193,6 +193,17 @@ def main():
             if c["data"] == "streams":  # calls on two unordered streams
                 status[name] = alternating_streams(peer, arena, c, a.rank, a.world, dev)
                 continue
+            if c["data"] == "set_blocks":  # the co-residency rule: refused at once, or accepted
+                import time
+
+                t0 = time.perf_counter()
+                try:
+                    peer.set_option(_lib.PEER_OPT_BLOCKS, c["blocks"])
+                    status[name] = "accepted"
+                except _lib.HydraError as e:
+                    status[name] = f"refused in {time.perf_counter() - t0:.3f} s: {e}"
+                peer.set_option(_lib.PEER_OPT_BLOCKS, 0)
+                continue
             if c["data"] in ("full_stress", "full_cancel_bf16"):  # configs 4 / 5, full size
                 digest, sample = full_size(peer, arena, c, a.rank, a.world, dev)
                 status[name] = peer.error()

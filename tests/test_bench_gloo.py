@@ -1,4 +1,4 @@
-"""The N>1 bench orchestration (hydra_amd.ring.bench_allreduce, what `bench.py --gpus N` runs on
+"""The N>1 bench orchestration (benchkit.allreduce.bench_allreduce, what `bench.py --gpus N` runs on
 each rank) at world size 2, 3, 4 and 8 (the driver's node) on the CPU: the same code path the driver's 8-GPU run takes --
 fold-order parity self-checks of every schedule, the safe DIRECT headline, the autotune over
 bit-exact candidates, full-size exactness, the timed region with max over ranks, the context
@@ -25,7 +25,8 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q, stall_rank=-1, stall_waits=0, extra_legs=False, peer="auto"):
+def _worker(rank, world, port, q, stall_rank=-1, stall_waits=0, extra_legs=False, peer="auto",
+            peer_fail_at=-1):
     import sys
 
     sys.path.insert(0, ROOT)
@@ -37,7 +38,7 @@ def _worker(rank, world, port, q, stall_rank=-1, stall_waits=0, extra_legs=False
 
     import bench
     from gloo_plan_exec import GlooPlanComm
-    from hydra_amd import ring
+    from benchkit import allreduce as bench_ar
     from oracle import oracle as O
 
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -66,6 +67,12 @@ def _worker(rank, world, port, q, stall_rank=-1, stall_waits=0, extra_legs=False
         def __init__(self):
             self.comm, self.closed = GlooPlanComm(O), False
             self.registered = []
+            self.calls, self.err = 0, 0
+            if peer_fail_at >= 0:  # the device group's bounded barriers: a gloo group whose
+                # collectives time out when a peer never arrives (then the group is poisoned)
+                from datetime import timedelta
+
+                self.group = dist.new_group(backend="gloo", timeout=timedelta(seconds=3))
 
         def register(self, t):
             self.registered.append(t.data_ptr())
@@ -75,10 +82,26 @@ def _worker(rank, world, port, q, stall_rank=-1, stall_waits=0, extra_legs=False
 
         def allreduce_(self, t, algo="peer2", **kw):
             assert t.data_ptr() in self.registered, "allreduce of an unregistered bucket"
-            self.comm.allreduce_(t, algo="direct", **kw)
+            from hydra_amd._lib import HydraError
+
+            self.calls += 1
+            if peer_fail_at < 0:
+                self.comm.allreduce_(t, algo="direct", **kw)
+                return
+            if self.err:  # a poisoned group refuses at once (hydra_peer_allreduce)
+                raise HydraError(3, "peer group is broken: an earlier barrier timed out")
+            if rank == 1 and peer_fail_at < self.calls:  # this rank's call fails locally
+                raise HydraError(1, f"injected failure at peer call {self.calls}")
+            got = [torch.empty_like(t) for _ in range(world)]
+            try:  # every rank's bucket, then the reference fold (the peer kernel's result)
+                dist.all_gather(got, t, group=self.group)
+            except RuntimeError:
+                self.err = 1  # the barrier timed out: the kernel's error word
+                return
+            t.copy_(torch.from_numpy(bench_ar.expected_fold_f32([g.numpy() for g in got])))
 
         def error(self):
-            return 0
+            return self.err
 
         def close(self):
             self.closed = True
@@ -94,7 +117,7 @@ def _worker(rank, world, port, q, stall_rank=-1, stall_waits=0, extra_legs=False
                                   watchdog_s=600.0, no_config5=False, config5_elements=1 << 20,
                                   peer=peer, extra_legs=extra_legs)
         base = ((lambda P, n: bench.ring_cpu_baseline(P, n, 0.5)) if O.ref_available() else None)
-        res = ring.bench_allreduce(args, torch.device("cpu"), make_comm=make_comm,
+        res = bench_ar.bench_allreduce(args, torch.device("cpu"), make_comm=make_comm,
                                    sync=lambda: None, cpu_baseline=base, make_peer=make_peer)
         q.put((rank, res, all(c.closed for c in comms + peers) and len(comms) == 2))
     except Exception as e:  # report instead of hanging the parent
@@ -105,12 +128,12 @@ def _worker(rank, world, port, q, stall_rank=-1, stall_waits=0, extra_legs=False
         dist.destroy_process_group()
 
 
-def _start(world, stall_rank=-1, stall_waits=0, extra_legs=False, peer="auto"):
+def _start(world, stall_rank=-1, stall_waits=0, extra_legs=False, peer="auto", peer_fail_at=-1):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_worker, args=(r, world, port, q, stall_rank, stall_waits,
-                                               extra_legs, peer))
+                                               extra_legs, peer, peer_fail_at))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -149,6 +172,12 @@ def test_bench_allreduce_orchestration(world):
     # A2A needs P equal reference blocks: 1 Mi fp32 has them at P = 2, 4 and 8, not at P = 3
     assert (par["a2a"] == "bit-exact" if world != 3 else par["a2a"].startswith("n/a")), par
     assert all(res["parity"]["full_size_exact"].values()), res["parity"]
+    # the full-size gate is fold-order-sensitive -- DIRECT's bucket on
+    # synth.stress_at data, pinned to the reference fold on sampled indices and equal across
+    # ranks; every other schedule must equal it bit for bit
+    g = res["parity"]["full_size_gate"]
+    assert g["ok"] and g["data"] == "stress_at" and g["sampled_equal_reference_fold"], g
+    assert g["sha256_equal_across_ranks"] and g["sampled_indices"] >= (1 << 16) // 2, g
     assert res["config"]["algo"] in ("direct", "a2a", "ring")
     assert res["config"]["autotune_ms"], res["config"]
     for a in ("ring", "direct", "rccl", "rccl_rs_ag", "apipe_direct"):
@@ -159,6 +188,8 @@ def test_bench_allreduce_orchestration(world):
     c5 = res["config5_bf16"]  # config 5's leg (bf16, fp32 accumulate) ran, at 1 Mi here
     assert "error" not in c5 and c5["elements"] == 1 << 20 and c5["ms"] > 0, c5
     assert res["parity"]["full_size_exact"]["config5_bf16_acc32"] is True, res["parity"]
+    g5 = c5["full_size_gate"]  # config 5's gate: stress_cancel_at, bf16 acc32 reference fold
+    assert g5["ok"] and g5["data"] == "stress_cancel_at", g5
     # the communicator's own rank count, the same on every rank
     rc = res["rccl_comm"]
     assert rc["nccl_comm_count"] == rc["min_over_ranks"] == rc["max_over_ranks"] == world, rc
@@ -213,12 +244,33 @@ def test_bench_peer_leg_orchestration(world):
     assert ph["kernel_ms"] > 0 and ph["link"]["algorithmic_bytes"] == int(
         2 * (world - 1) / world * (1 << 16) * 4), ph
     assert ph["link"]["peers"] == world - 1 and ph["fold"]["frac_of_hbm"] > 0, ph
+    assert pl["full_size_gate"].startswith("equal to this run's DIRECT bucket"), pl
     if pl["promoted"]:
         assert res["config"]["algo"] == "peer2" and res["ms_per_step"] == pl["ms_per_step"]
         assert res["parity"]["full_size_exact"]["peer2"] is True
+        # the promoted headline carries its own phase entry and parity
+        assert res["roofline"]["phases"] == ph, res["roofline"]
+        assert res["parity"]["fold_order_1M"]["peer2"] == "bit-exact", res["parity"]
     else:
         assert res["config"]["algo"] != "peer2" and res["ms_per_step"] <= pl["ms_per_step"]
     assert all(out[r][0]["peer_leg"]["promoted"] == pl["promoted"] for r in out)
+
+
+@pytest.mark.parametrize("fail_at,stage", [(4, "autotune"), (32, "timed region")])
+def test_bench_peer_leg_one_rank_fails_mid_loop(fail_at, stage):
+    """a peer call that fails on ONE rank inside the autotune (its 5th call) or the
+    timed region (its 33rd: the first timed step) -- that rank records it and keeps issuing the
+    same collectives; its peers' calls end at their bounded barrier (the fake group's 3 s
+    timeout, the kernel's error word on a GPU) -- so the leg ends with an error entry of that
+    stage on every rank, nobody is stranded and the RCCL headline stands."""
+    out = _start(2, peer="on", peer_fail_at=fail_at)
+    for r, (res, closed) in out.items():
+        assert isinstance(res, dict), res
+        assert closed, f"rank {r} left a communicator or peer group open"
+        pl = res["peer_leg"]
+        assert pl.get("error", "").startswith(stage) and not pl.get("promoted"), pl
+        assert res["config"]["algo"] != "peer2" and res["value"] > 0, res["config"]
+    assert "injected failure" in out[1][0]["peer_leg"]["error"], out[1][0]["peer_leg"]
 
 
 def test_bench_allreduce_extra_legs():

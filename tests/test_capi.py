@@ -29,7 +29,58 @@ def test_header_symbols_exported():
     L = _lib.lib()
     for f in declared:
         assert hasattr(L, f)
-    assert L.hydra_abi_version() == 1
+    assert L.hydra_abi_version() == 2
+
+
+def test_measurement_symbols_only_in_the_measurement_build():
+    """the product library exports no measurement entry point (the A/B
+    variants and phase clocks are built into libhydra_measure.so only), and the measurement
+    build exports the whole product ABI plus include/hydra_measure.h."""
+    def exported(path):
+        out = subprocess.check_output(["nm", "-D", "--defined-only", path], text=True)
+        return {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
+
+    prod, meas = exported(_lib.LIB_PATH), exported(_lib.MEASURE_LIB_PATH)
+    assert not [f for f in _lib.MEASURE_EXPORTS if f in prod]
+    txt = open(os.path.join(ROOT, "include", "hydra_measure.h")).read()
+    declared = set(re.findall(r"\b(hydra_[a-z0-9_]+)\s*\(", re.sub(r"/\*.*?\*/", "", txt, flags=re.S)))
+    assert declared == set(_lib.MEASURE_EXPORTS)
+    assert set(_lib.EXPORTS) | declared <= meas
+
+
+def test_library_reads_no_environment():
+    """every tunable is a documented option on the C-ABI (hydra_set_option
+    / hydra_ctx_set_option), never an environment variable: no getenv in the library's sources,
+    and getenv is not among the product library's undefined symbols."""
+    csrc = os.path.join(ROOT, "hydra_amd", "csrc")
+    hits = []
+    for dp, _, fs in os.walk(csrc):
+        if "build" in dp:
+            continue
+        for f in fs:
+            if f.endswith((".cpp", ".h", ".hip")):
+                if "getenv" in open(os.path.join(dp, f), errors="replace").read():
+                    hits.append(f)
+    assert not hits, hits
+    und = subprocess.check_output(["nm", "-D", "--undefined-only", _lib.LIB_PATH], text=True)
+    assert not [ln for ln in und.splitlines() if ln.split()[-1].startswith("getenv")]
+
+
+def test_options_validate_and_round_trip():
+    """hydra_set_option / hydra_get_option: defaults, range checks, unknown keys; per-context
+    keys only through hydra_ctx_set_option (its null-context check needs no GPU)."""
+    L = _lib.lib()
+    assert _lib.get_option(_lib.OPT_STAGE_SPLIT) == 4
+    assert _lib.get_option(_lib.OPT_RESIDENT_IDLE_US) == 2000
+    assert L.hydra_set_option(99, 1) == _lib.ERR_INVALID
+    assert L.hydra_set_option(_lib.OPT_STAGE_SPLIT, 0) == _lib.ERR_INVALID  # 1..64
+    assert b"outside" in L.hydra_last_error()
+    _lib.set_option(_lib.OPT_STAGE_SPLIT, 8)
+    try:
+        assert _lib.get_option(_lib.OPT_STAGE_SPLIT) == 8
+    finally:
+        _lib.set_option(_lib.OPT_STAGE_SPLIT, 4)
+    assert L.hydra_ctx_set_option(None, _lib.OPT_STAGE_SPLIT, 2) == _lib.ERR_INVALID
 
 
 def test_no_hip_types_in_abi():

@@ -28,6 +28,7 @@ def _worker(rank, world, port, algo, n, ms, ch, q):
 
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from gloo_plan_exec import execute
+    from benchkit import allreduce as bench_ar
     from hydra_amd import ring, synth
     from oracle import oracle as O
 
@@ -45,9 +46,9 @@ def _worker(rank, world, port, algo, n, ms, ch, q):
         # harness helpers
         uid = ring.exchange_unique_id(rank, make_id=lambda: bytes(range(128)))
         assert uid == bytes(range(128))
-        mx = ring.max_over_ranks(float(rank + 1))
+        mx = bench_ar.max_over_ranks(float(rank + 1))
         assert mx == float(world)
-        wall = ring.timed_steps(lambda: None, 3, 1, lambda: None, dist.barrier)
+        wall = bench_ar.timed_steps(lambda: None, 3, 1, lambda: None, dist.barrier)
         assert wall >= 0
         xs = [synth.stress_f32(world, r, n) for r in range(world)]
         if algo in ("ring_old", "ring_chunked", "halving_doubling"):  # the Algorithm classes

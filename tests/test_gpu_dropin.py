@@ -16,6 +16,8 @@ import subprocess
 
 import pytest
 
+from hydra_amd import _lib
+
 pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -103,10 +105,12 @@ def test_config1_full_size_inside_the_reference(gpu, n):
 def test_reference_with_hydra_func_registered_bucket(gpu, mode, P, n, result_path):
     """The bucket registered once (hydra_host_register): the kernel reads it in place over PCIe
     while only the reference's pageable scratch is staged, and writes its results either in place
-    (registrations above 8 MiB -- the last case's 16 MiB bucket -- or always with
-    HYDRA_STAGE_RESULT_REG_MAX=0) or through the staging (smaller ones, or always): same bytes."""
-    env = {"default": {}, "in_place": {"HYDRA_STAGE_RESULT_REG_MAX": "0"},
-           "staged": {"HYDRA_STAGE_RESULT_MAX": str(1 << 30)}}[result_path]
+    (registrations above 8 MiB -- the last case's 16 MiB bucket -- or always with the option
+    HYDRA_OPT_STAGE_RESULT_REG_MAX = 0) or through the staging (smaller ones, or always): same
+    bytes."""
+    opt = {"default": "", "in_place": f"{_lib.OPT_STAGE_RESULT_REG_MAX}=0",
+           "staged": f"{_lib.OPT_STAGE_RESULT_MAX}={1 << 30}"}[result_path]
+    env = {"HYDRA_DROPIN_OPT": opt} if opt else {}
     j = dropin(mode, P, n, register=True, env_extra=env)
     assert j["mismatched_bytes"] == 0, j
 

@@ -166,6 +166,8 @@ from hydra_amd.reduce import HostContext
 from oracle import oracle as O
 L = _lib.lib()
 c = HostContext(0)
+for k, v in %r.items():
+    c.set_option(k, v)
 out = {}
 n = 300007
 buf = np.empty(n + 4096, np.float32)  # lives until exit: registered pages never go back
@@ -191,12 +193,12 @@ print(json.dumps(out))
 """
 
 
-@pytest.mark.parametrize("env,staged", [
-    ({}, True),  # default: a 1.2 MiB registration is below HYDRA_STAGE_RESULT_REG_MAX (8 MiB)
-    ({"HYDRA_STAGE_RESULT_REG_MAX": "0"}, False),  # zero-copy result writes
-    ({"HYDRA_STAGE_RESULT_REG_MAX": "0", "HYDRA_STAGE_RESULT_MAX": str(1 << 30)}, True),
+@pytest.mark.parametrize("opts,staged", [
+    ({}, True),  # default: a 1.2 MiB registration is below HYDRA_OPT_STAGE_RESULT_REG_MAX (8 MiB)
+    ({_lib.OPT_STAGE_RESULT_REG_MAX: 0}, False),  # zero-copy result writes
+    ({_lib.OPT_STAGE_RESULT_REG_MAX: 0, _lib.OPT_STAGE_RESULT_MAX: 1 << 30}, True),
 ])
-def test_staged_result_path_choice(gpu, env, staged):
+def test_staged_result_path_choice(gpu, opts, staged):
     """Where a registered c's result goes: through the staging (the CPU copies it back, c stays
     in the CPU's cache) for a small registration -- the default -- or written in place over PCIe.
     The same bits either way, in place (c == a, the ring's call) and out of place; a's interior
@@ -205,8 +207,8 @@ def test_staged_result_path_choice(gpu, env, staged):
     import subprocess
     import sys
 
-    p = subprocess.run([sys.executable, "-c", _STAGED_RESULT % ROOT], capture_output=True,
-                       text=True, timeout=120, env=dict(os.environ, **env))
+    p = subprocess.run([sys.executable, "-c", _STAGED_RESULT % (ROOT, opts)],
+                       capture_output=True, text=True, timeout=120)
     assert p.returncode == 0, p.stderr[-3000:]
     r = json.loads(p.stdout.strip().splitlines()[-1])
     for mode, v in r.items():

@@ -256,6 +256,30 @@ def test_peer_config5_full_size_sampled(gpu, O, tmp_path):
         assert bad.size == 0, (r, bad.size, idx[bad[:5]].tolist())
 
 
+@pytest.mark.parametrize("P", [4, 8])
+def test_peer_colocated_grid_rule(gpu, O, tmp_path, P):
+    """ranks of one group on the same GPU (every rank here shares cuda:0)
+    must all have their grids resident at once.  The library knows which ranks share a GPU (the
+    PCI identity travels in the signal handle) and enforces it: an explicit grid of 512
+    workgroups at P = 4 / 8 is refused at once (HYDRA_ERR_INVALID, no barrier timeout), one that
+    fits (512 / P) is accepted, and the derived grid (blocks = 0: up to 256 per rank with a GPU
+    each) shrinks to fit -- an 8 Mi+5 bucket, which round 5's r05e session saw time out at P = 4,
+    completes bit-exact."""
+    cases = [dict(name="too_many", data="set_blocks", blocks=512),
+             dict(name="fits", data="set_blocks", blocks=512 // P),
+             dict(name="derived", algo="peer2", data="stress_f32", dtype=_lib.FLOAT32,
+                  n=(8 << 20) + 5, ms=0, offset_bytes=4)]
+    res, st = run_ranks(tmp_path, P, cases, blocks=0, timeout=120)
+    for r in range(P):
+        msg = st[r]["too_many"]
+        assert msg.startswith("refused in ") and "resident capacity" in msg, msg
+        assert float(msg.split()[2]) < 1.0, msg  # immediately, not after a barrier timeout
+        assert st[r]["fits"] == "accepted", st[r]
+        assert st[r]["derived"] == 0, st[r]
+    exp = expected(O, cases[2], P)
+    assert all(np.array_equal(r["derived"], exp) for r in res)
+
+
 def test_peer_timeout_reports_and_poisons(gpu, tmp_path):
     """A rank that never arrives: the kernel leaves after the timeout (every wave drains), the
     error word is set, and the group refuses further allreduces."""

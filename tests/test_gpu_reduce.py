@@ -54,8 +54,9 @@ class Dev:
 
 
 def dev_reduce(dev, kind, code, a, b, c0=None, offs=(0, 0, 0), inplace=True, variant=None):
-    """Run hydra_reduce on device copies; returns c.  inplace: c is a's buffer."""
-    L = _lib.lib()
+    """Run hydra_reduce on device copies; returns c.  inplace: c is a's buffer.  variant: a
+    measurement variant, run through the measurement build (libhydra_measure.so)."""
+    L = _lib.measure_lib() if variant is not None else _lib.lib()
     ta, pa = dev.put(a, offs[1])
     tb, pb = dev.put(b, offs[2])
     if inplace:
@@ -245,16 +246,16 @@ def test_ring_call_pattern(dev, O):
                 assert np.array_equal(bits(out[lo:hi]), bits(exp[lo:hi])), (P, n, q)
 
 
-@pytest.mark.parametrize("variant", [0, 1000])
+@pytest.mark.parametrize("force", [0, 1])
 @pytest.mark.parametrize("n", [1, 1000, 3 * (1 << 20) + 7, 9 * (1 << 20)])
-def test_host_path(gpu, O, n, variant):
+def test_host_path(gpu, O, n, force):
     """hydra_reduce_host on pageable buffers: copied by the CPU through the context's pinned
     staging (never pinned for the call), 4 MiB per operand per round, double-buffered -- and the
-    same with everything forced through staging (variant 1000)."""
+    same with everything forced through staging (HYDRA_OPT_FORCE_STAGING)."""
     a = synth.stress_f32(2, 0, n)
     b = synth.stress_f32(2, 1, n)
     ctx = HostContext(0)
-    prev = _lib.lib().hydra_set_variant(variant)
+    ctx.set_option(_lib.OPT_FORCE_STAGING, force)
     try:
         c = a.copy()
         _lib.check(_lib.lib().hydra_reduce_host(ctx.handle, 0, 6, c.ctypes.data, c.ctypes.data,
@@ -265,7 +266,6 @@ def test_host_path(gpu, O, n, variant):
                                                 b.ctypes.data, n))
         assert np.array_equal(bits(c), bits(O.op(a, b, "sum", 6)))
     finally:
-        _lib.lib().hydra_set_variant(prev)
         ctx.close()
 
 
@@ -462,8 +462,8 @@ def test_reduce_batch_argument_checks(dev):
 @pytest.mark.parametrize("n", [1, 4099, 262144, (9 << 20) + 3])
 @pytest.mark.parametrize("pinned", ["a", "b", "c", "ab", "ac", "bc"])
 @pytest.mark.parametrize("code", [6, 8])
-@pytest.mark.parametrize("variant", [0, 1000])
-def test_host_path_mixed_pinned(gpu, O, n, pinned, code, variant, host_buf):
+@pytest.mark.parametrize("force", [0, 1])
+def test_host_path_mixed_pinned(gpu, O, n, pinned, code, force, host_buf):
     """hydra_reduce_host with SOME operands registered: those are read / written by the kernel in
     place over PCIe, the pageable ones staged -- e.g. a registered bucket with the reference
     ring's pageable scratch (allreduce.cc:225) stages only b.  In place (c == a) and out of
@@ -480,7 +480,7 @@ def test_host_path_mixed_pinned(gpu, O, n, pinned, code, variant, host_buf):
           else np.full(n, 3, np.float32))
     ctx = HostContext(0)
     regs = []
-    prev = L.hydra_set_variant(variant)  # 1000: every operand staged, registered or not
+    ctx.set_option(_lib.OPT_FORCE_STAGING, force)  # 1: every operand staged, registered or not
     try:
         for inplace in (True, False):
             ha, hb = host_buf(n, a.dtype, a), host_buf(n, b.dtype, b)
@@ -510,7 +510,6 @@ def test_host_path_mixed_pinned(gpu, O, n, pinned, code, variant, host_buf):
                 L.hydra_host_unregister(r.ctypes.data)
             regs.clear()
     finally:
-        L.hydra_set_variant(prev)
         for r in regs:
             L.hydra_host_unregister(r.ctypes.data)
         ctx.close()

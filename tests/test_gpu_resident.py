@@ -5,7 +5,7 @@ reference's own outputs (golden fixtures: every Gloo dtype x {sum, product, max,
 oracle, through every lifecycle edge: back-to-back calls on one instance, idle gaps long enough
 for an instance to leave (the next call launches a new one), two contexts at once, more
 contexts than slots, a context destroyed while the instance runs, calls of several staging
-rounds, HYDRA_RESIDENT=0 -- and the persistent grid never holds up another stream's work."""
+rounds, HYDRA_OPT_RESIDENT = 0 -- and the persistent grid never holds up another stream's work."""
 import os
 import subprocess
 import sys
@@ -78,7 +78,7 @@ def test_resident_back_to_back_and_idle_gaps(ctx, O):
         elif i % 10 == 9:
             time.sleep(0.001)
     st = ctx.stats()
-    # (a staged call of more than 256 KiB per operand is served as 2+ rounds: HYDRA_STAGE_SPLIT)
+    # (a staged call of more than 256 KiB per operand is served as 2+ rounds: HYDRA_OPT_STAGE_SPLIT)
     assert 200 <= st["resident_calls"] - s0["resident_calls"] < 400, (s0, st)
     assert 2 <= st["resident_launches"] - s0["resident_launches"] < 60, (s0, st)
 
@@ -129,8 +129,17 @@ def test_resident_destroy_while_running(gpu, O):
     _lib.check(L.hydra_device_check(0))
 
 
-def test_resident_off_by_environment(gpu):
-    """HYDRA_RESIDENT=0: every call is one batched launch on the context's stream; same bits."""
+def _with_opts(code, opts):
+    """`code` run after hydra_set_option(key, value) for each of `opts` (library options: the
+    library reads no environment variable)."""
+    pre = ("import sys; sys.path.insert(0, %r)\nimport torch\nfrom hydra_amd import _lib\n"
+           "for _k, _v in %r.items():\n    _lib.set_option(_k, _v)\n" % (ROOT, opts))
+    return pre + code
+
+
+def test_resident_off_by_option(gpu):
+    """HYDRA_OPT_RESIDENT = 0 (process-wide): every call is one batched launch on the context's
+    stream; same bits."""
     code = (
         "import sys, numpy as np; sys.path.insert(0, %r)\n"
         "import torch\n"
@@ -146,8 +155,8 @@ def test_resident_off_by_environment(gpu):
         "    assert np.array_equal(a.view(np.uint32), e.view(np.uint32)), n\n"
         "assert c.stats()['resident_calls'] == 0, c.stats()\n"
         "c.close(); print('ok')\n" % ROOT)
-    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120,
-                       env=dict(os.environ, HYDRA_RESIDENT="0"))
+    p = subprocess.run([sys.executable, "-c", _with_opts(code, {_lib.OPT_RESIDENT: 0})],
+                       capture_output=True, text=True, timeout=120)
     assert p.returncode == 0 and "ok" in p.stdout, (p.stdout, p.stderr[-2000:])
 
 
@@ -223,8 +232,9 @@ def test_resident_instance_never_blocks_other_streams(gpu):
     in milliseconds -- on a shared queue it would wait for the instance to leave."""
     import json
 
-    p = subprocess.run([sys.executable, "-c", _BLOCKING_PROBE % ROOT], capture_output=True,
-                       text=True, timeout=120, env=dict(os.environ, HYDRA_RESIDENT_IDLE_US="1000000"))
+    p = subprocess.run([sys.executable, "-c",
+                        _with_opts(_BLOCKING_PROBE % ROOT, {_lib.OPT_RESIDENT_IDLE_US: 1000000})],
+                       capture_output=True, text=True, timeout=120)
     assert p.returncode == 0, p.stderr[-2000:]
     r = json.loads(p.stdout.strip().splitlines()[-1])
     assert r["launches"] == 1, json.dumps(r)  # one instance stayed alive through the probe
@@ -315,15 +325,15 @@ def test_resident_solo_calls_past_the_grace_period(gpu):
     """a steady stream of solo calls (workgroup 0 alone, nothing published)
     longer than idle + grace must not make the waiting workers give up -- they follow workgroup
     0's heartbeat -- and a large call afterwards is served by the same instance, exactly.
-    Grace shortened to 20 ms and the idle limit to 50 ms (HYDRA_RESIDENT_GRACE_US / _IDLE_US):
+    Grace shortened to 20 ms and the idle limit to 50 ms (HYDRA_OPT_RESIDENT_GRACE_US / _IDLE_US):
     0.4 s of solo calls crosses idle + grace more than 5 times, and a scheduling hiccup shorter
     than 50 ms between two calls cannot end the instance."""
     import json
 
-    p = subprocess.run([sys.executable, "-c", _SOLO_STREAM % ROOT], capture_output=True,
-                       text=True, timeout=120,
-                       env=dict(os.environ, HYDRA_RESIDENT_GRACE_US="20000",
-                                HYDRA_RESIDENT_IDLE_US="50000"))
+    p = subprocess.run([sys.executable, "-c",
+                        _with_opts(_SOLO_STREAM % ROOT, {_lib.OPT_RESIDENT_GRACE_US: 20000,
+                                                         _lib.OPT_RESIDENT_IDLE_US: 50000})],
+                       capture_output=True, text=True, timeout=120)
     assert p.returncode == 0, (p.stdout[-1000:], p.stderr[-3000:])
     r = json.loads(p.stdout.strip().splitlines()[-1])
     assert r["solo_calls"] > 100, r
@@ -460,8 +470,9 @@ def test_resident_generation_tag_wrap(gpu):
     around it untouched, and no slot's completion word ever seen moving backwards."""
     import json
 
-    p = subprocess.run([sys.executable, "-c", _GEN_WRAP % ROOT], capture_output=True, text=True,
-                       timeout=120, env=dict(os.environ, HYDRA_RESIDENT_IDLE_US="300"))
+    p = subprocess.run([sys.executable, "-c",
+                        _with_opts(_GEN_WRAP % ROOT, {_lib.OPT_RESIDENT_IDLE_US: 300})],
+                       capture_output=True, text=True, timeout=120)
     assert p.returncode == 0, (p.stdout[-1000:], p.stderr[-3000:])
     r = json.loads(p.stdout.strip().splitlines()[-1])
     assert r["gen_stride"] == 65536 and r["calls"] == 72, r

@@ -223,12 +223,15 @@ def test_fold_abi_reference_order(gpu, O, P, variant):
                 for r, x in enumerate(xs)]
         ptrs = (ctypes.c_void_p * P)(*[b.data_ptr() + 4 * (r % 4) for r, b in enumerate(bufs)])
         dst = torch.zeros(n + 3, dtype=torch.float32, device=gpu)
-        L = _lib.lib()
-        prev = L.hydra_set_variant(variant)
-        try:
-            _lib.check(L.hydra_fold(0, 6, 0, dst.data_ptr() + 4, ptrs, P, n, None))
-        finally:
-            L.hydra_set_variant(prev)
+        if variant:  # the fold variants live in the measurement build
+            L = _lib.measure_lib()
+            prev = L.hydra_set_variant(variant)
+            try:
+                _lib.check(L.hydra_fold(0, 6, 0, dst.data_ptr() + 4, ptrs, P, n, None))
+            finally:
+                L.hydra_set_variant(prev)
+        else:  # the shipped fold, product library
+            _lib.check(_lib.lib().hydra_fold(0, 6, 0, dst.data_ptr() + 4, ptrs, P, n, None))
         torch.cuda.synchronize()
         acc = xs[P - 1].copy()
         for j in range(P - 2, -1, -1):

@@ -10,6 +10,7 @@
 import numpy as np
 import pytest
 
+from benchkit import allreduce as bench_ar
 from hydra_amd import _lib, ring, synth
 
 from plan_interp import (ALLGATHER, ALLTOALL, FOLD, GROUP, RECV, REDUCE, SEND,  # noqa: E402,F401
@@ -232,18 +233,18 @@ def test_bench_self_check_helpers(O):
     xs = [synth.stress_f32(P, r, n) for r in range(P)]
     a = [[x.copy()] for x in xs]
     O.allreduce_ring_chunked(a)
-    assert np.array_equal(ring.expected_chunked_ring_f32(xs).view(np.uint32),
+    assert np.array_equal(bench_ar.expected_chunked_ring_f32(xs).view(np.uint32),
                           a[0][0].view(np.uint32))
     b = [[x.copy()] for x in xs]
     O.allreduce_ring_old(b)
     for r in range(P):
-        assert np.array_equal(ring.expected_old_ring_f32(xs, r).view(np.uint32),
+        assert np.array_equal(bench_ar.expected_old_ring_f32(xs, r).view(np.uint32),
                               b[r][0].view(np.uint32))
-    assert np.array_equal(ring.expected_fold_f32(xs).view(np.uint32),
+    assert np.array_equal(bench_ar.expected_fold_f32(xs).view(np.uint32),
                           O.ring_result(xs).view(np.uint32))
     for P2 in (1, 2, 6, 8, 12):
         ys = [synth.stress_f32(P2, r, n) for r in range(P2)]
-        assert np.array_equal(ring.expected_bcube_f32(ys).view(np.uint32),
+        assert np.array_equal(bench_ar.expected_bcube_f32(ys).view(np.uint32),
                               O.bcube_result(ys).view(np.uint32)), P2
 
 
@@ -319,14 +320,14 @@ def test_reduce_root_geometry_is_gloo_reduce():
 
 
 def test_bench_reduce_self_check_helper(O):
-    """bench.py's gloo::reduce self-check (ring.expected_reduce_f32, not the oracle) equals the
+    """bench.py's gloo::reduce self-check (bench_ar.expected_reduce_f32, not the oracle) equals the
     oracle's root result, and its geometry helper equals the oracle's."""
     for P, n in [(1, 100), (2, 1 << 20), (3, 1_000_003), (8, 1 << 20), (5, 77)]:
-        assert ring.reduce_geometry(P, n, 4) == O.reduce_plan(P, n, 4, 1 << 20)
+        assert bench_ar.reduce_geometry(P, n, 4) == O.reduce_plan(P, n, 4, 1 << 20)
         xs = [synth.stress_f32(P, r, n) for r in range(P)]
         exp = [x.copy() for x in xs]
         O.reduce(exp, None, P - 1)
-        assert np.array_equal(ring.expected_reduce_f32(xs).view(np.uint32),
+        assert np.array_equal(bench_ar.expected_reduce_f32(xs).view(np.uint32),
                               exp[P - 1].view(np.uint32)), (P, n)
 
 

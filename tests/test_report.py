@@ -1,7 +1,7 @@
-"""hydra_amd.report: the reference benchmark's table (runner.cc:563-649, timer.h:68-102)."""
+"""benchkit.report: the reference benchmark's table (runner.cc:563-649, timer.h:68-102)."""
 import numpy as np
 
-from hydra_amd import report
+from benchkit import report
 
 # The header line of the reference's published tables (README.md:61, :98).
 REF_HEADER = ("   elements   min (us)   p50 (us)   p99 (us)  p995 (us)   max (us)   avg (us)"

@@ -37,7 +37,8 @@ def test_copy_pool_sanitized(tmp_path, san):
     helper threads, every byte and the guard bytes checked, under TSan and ASan + UBSan."""
     exe = tmp_path / f"copy_pool_{san.split(',')[0]}"
     srcs = [os.path.join(ROOT, "tests", "cpp", "copy_pool_stress.cc"),
-            os.path.join(ROOT, "hydra_amd", "csrc", "copy_pool.cpp")]
+            os.path.join(ROOT, "hydra_amd", "csrc", "copy_pool.cpp"),
+            os.path.join(ROOT, "hydra_amd", "csrc", "options.cpp")]
     subprocess.check_call(["g++", "-std=c++17", "-O1", "-g", "-pthread", f"-fsanitize={san}",
                            "-fno-omit-frame-pointer", *srcs, "-o", str(exe)])
     env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1",

@@ -11,7 +11,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PROG = """
 import sys, time
 sys.path.insert(0, {root!r})
-from hydra_amd import watchdog
+from benchkit import watchdog
 state = {{}}
 if {measured}:
     state["result"] = lambda: {{"metric": "m", "value": 1.0}}
