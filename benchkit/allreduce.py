@@ -803,7 +803,7 @@ def _peer_leg(make_peer, pg, run, measure, sync, dev, rank, world, xs, exp, x, x
                 leg["error"] = f"register: {err or 'another rank failed'}"
                 return None
         par = {}
-        for a in ("peer2", "peer1"):
+        for a in ("peer2", "peer2w", "peer1"):
             ok = False
             try:
                 tp.copy_(torch.from_numpy(xs[rank]))
@@ -818,26 +818,33 @@ def _peer_leg(make_peer, pg, run, measure, sync, dev, rank, world, xs, exp, x, x
                 continue
             par[a] = "bit-exact" if max_over_ranks(0.0 if ok else 1.0, dev) == 0.0 else "MISMATCH"
         leg["parity_fold_order_1M"] = par
-        if par.get("peer2") != "bit-exact":
-            leg["error"] = "peer2 did not reproduce the reference bits; not timed"
+        # the two-shot schedules (pull: peer2; push: peer2w) are the candidates for config 4's
+        # bucket; only those that reproduced the reference bits go on
+        algos = [a for a in ("peer2w", "peer2") if par.get(a) == "bit-exact"]
+        if not algos:
+            leg["error"] = "no two-shot schedule reproduced the reference bits; not timed"
             return None
         # the full-size gate: this run's DIRECT bucket on the order-sensitive data (_full_size_gate
-        # pinned it to the reference fold), bit for bit, on every rank
-        good = False
-        try:
-            x.copy_(x0)
-            run("peer2", x)
-            sync()
-            good = bool(torch.equal(x.view(torch.int32), ref.view(torch.int32)))
-        except Exception as e:
-            err = str(e)
-        if not agreed(err) or not peer_ok():
-            leg["error"] = f"full size: {err or 'a barrier expired or another rank failed'}"
-            return None
-        leg["full_size_exact"] = bool(gate["ok"]) and \
-            max_over_ranks(0.0 if good else 1.0, dev) == 0.0
+        # pinned it to the reference fold), bit for bit, on every rank -- per schedule
+        exact = {}
+        for a in algos:
+            good = False
+            try:
+                x.copy_(x0)
+                run(a, x)
+                sync()
+                good = bool(torch.equal(x.view(torch.int32), ref.view(torch.int32)))
+            except Exception as e:
+                err = str(e)
+            if not agreed(err) or not peer_ok():
+                leg["error"] = f"full size: {err or 'a barrier expired or another rank failed'}"
+                return None
+            exact[a] = bool(gate["ok"]) and max_over_ranks(0.0 if good else 1.0, dev) == 0.0
+        leg["full_size_exact_by_algo"] = exact
+        algos = [a for a in algos if exact[a]]
+        leg["full_size_exact"] = bool(algos)
         leg["full_size_gate"] = "equal to this run's DIRECT bucket (synth.stress_at), every rank"
-        if not leg["full_size_exact"]:
+        if not algos:
             return None
         tune = {}
         # 0: derived from the bucket (one per slab, <= 256, one per CU).  With a GPU per rank,
@@ -845,33 +852,35 @@ def _peer_leg(make_peer, pg, run, measure, sync, dev, rank, world, xs, exp, x, x
         # twice the remote loads in flight for xGMI's longer read latency.  Ranks sharing one GPU
         # (the rehearsal) are capped at 512 / world by run(), so 512 is not a candidate there.
         cands = (0, 128, 64) if leg.get("shared_gpu_workgroup_cap") else (0, 512, 128, 64)
-        for wg in cands:
-            tw = None
-            try:
-                def tstep(wg=wg):
-                    guarded("peer2", x, wg)
+        for a in algos:
+            for wg in cands:
+                tw = None
+                try:
+                    def tstep(a=a, wg=wg):
+                        guarded(a, x, wg)
 
-                tw = max_over_ranks(timed_steps(tstep, 5, 2, sync, dist.barrier), dev) / 5
-            except Exception as e:
-                err = str(e)
-            err = err or (failed[0] if failed else None)
-            if not agreed(err) or not peer_ok():
-                leg["error"] = f"autotune: {err or 'a barrier expired or another rank failed'}"
-                return None
-            tune[f"peer2/{wg}wg"] = round(tw * 1e3, 4)
+                    tw = max_over_ranks(timed_steps(tstep, 5, 2, sync, dist.barrier), dev) / 5
+                except Exception as e:
+                    err = str(e)
+                err = err or (failed[0] if failed else None)
+                if not agreed(err) or not peer_ok():
+                    leg["error"] = f"autotune: {err or 'a barrier expired or another rank failed'}"
+                    return None
+                tune[f"{a}/{wg}wg"] = round(tw * 1e3, 4)
         leg["autotune_ms"] = tune
-        wg = int(min(tune, key=tune.get).split("/")[1][:-2])
+        best = min(tune, key=tune.get)
+        algo, wg = best.split("/")[0], int(best.split("/")[1][:-2])
         try:
-            ms_p, lat_p = measure("peer2", wg, runner=guarded)
+            ms_p, lat_p = measure(algo, wg, runner=guarded)
         except Exception as e:
             err = str(e)
         err = err or (failed[0] if failed else None)
         if not agreed(err) or not peer_ok():
             leg["error"] = f"timed region: {err or 'a barrier expired or another rank failed'}"
             return None
-        leg.update(algo="peer2", workgroups=wg, ms_per_step=round(ms_p, 4), latency_ms=lat_p)
-        leg["phases"] = _peer_phases(run, sync, dev, x, wg, world)
-        return "peer2", wg, ms_p, lat_p
+        leg.update(algo=algo, workgroups=wg, ms_per_step=round(ms_p, 4), latency_ms=lat_p)
+        leg["phases"] = _peer_phases(run, sync, dev, x, wg, world, algo)
+        return algo, wg, ms_p, lat_p
     finally:
         p, pg["peer"] = pg["peer"], None
         if p is not None:
@@ -881,12 +890,13 @@ def _peer_leg(make_peer, pg, run, measure, sync, dev, rank, world, xs, exp, x, x
                 leg.setdefault("error", f"teardown: {e}")
 
 
-def _peer_phases(run, sync, dev, x, wg, world) -> dict:
+def _peer_phases(run, sync, dev, x, wg, world, algo="peer2") -> dict:
     """One event-timed peer allreduce (untimed otherwise): the kernel IS both phases -- it reads
     the peers' blocks over xGMI (link) and folds them as they arrive (fold) -- so the entry gives
     the one kernel's time against both rooflines: per-rank link bytes 2(P-1)/P x n x E (the
-    owner block's P-1 remote reads + the P-1 finished blocks pulled back) over P-1 links, and
-    the fused sum's algorithmic HBM bytes (P-1)/P x n x 3E."""
+    owner block's P-1 remote reads + the P-1 finished blocks pulled back, or pushed: peer2w)
+    over P-1 links, and the fused sum's algorithmic HBM bytes (P-1)/P x n x 3E (SURVEY.md
+    8(d))."""
     import torch
 
     n, esize = x.numel(), x.element_size()
@@ -897,14 +907,14 @@ def _peer_phases(run, sync, dev, x, wg, world) -> dict:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             sync()
             e0.record(s)
-            run("peer2", x, wg)
+            run(algo, x, wg)
             e1.record(s)
             sync()
             local = e0.elapsed_time(e1)
         else:  # (the CPU rehearsal: wall time of one synchronous call)
             sync()
             t0 = time.perf_counter()
-            run("peer2", x, wg)
+            run(algo, x, wg)
             sync()
             local = (time.perf_counter() - t0) * 1e3
     except Exception as e:  # every rank still reaches the collective below
@@ -918,7 +928,7 @@ def _peer_phases(run, sync, dev, x, wg, world) -> dict:
     links = max(1, world - 1)
     per_link = link_bytes / links / (ms * 1e-3) / 1e9 if ms > 0 else None
     kern = fused / (ms * 1e-3) / 1e9 if ms > 0 else None
-    return {"calls": 1, "kernel_ms": round(ms, 4), "link_ms": round(ms, 4),
+    return {"calls": 1, "algo": algo, "kernel_ms": round(ms, 4), "link_ms": round(ms, 4),
             "fold_ms": round(ms, 4), "span_ms": round(ms, 4), "overlap_ms": round(ms, 4),
             "note": "one kernel: link reads and folds overlap completely (link = fold = span)",
             "link": {"algorithmic_bytes": int(link_bytes), "peers": links,

@@ -75,7 +75,8 @@ ERR_TIMEOUT = 5
 UNIQUE_ID_BYTES = 128
 # peer-access allreduce (hydra_peer_*)
 PEER_HANDLE_BYTES = 128
-PEER_ALGOS = {"peer": 0, "peer2": 1, "peer1": 2}  # AUTO, TWO_SHOT, ONE_SHOT
+PEER_ALGOS = {"peer": 0, "peer2": 1, "peer1": 2, "peer2w": 3}  # AUTO, TWO_SHOT, ONE_SHOT,
+# TWO_SHOT_PUSH (the fold writes the result into every rank's bucket)
 PEER_OPT_TIMEOUT_MS, PEER_OPT_BLOCKS, PEER_OPT_ONE_SHOT_MAX = 1, 2, 3
 
 

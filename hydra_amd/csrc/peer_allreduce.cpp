@@ -371,7 +371,7 @@ int hydra_peer_allreduce(hydra_peer_t p, int algo, int op, int dtype, int flags,
   const size_t es = hydra::dtype_size(dtype);
   if (!es) return fail(HYDRA_ERR_INVALID, "invalid dtype");
   if (op < HYDRA_SUM || op > HYDRA_MIN) return fail(HYDRA_ERR_INVALID, "invalid op");
-  if (algo < HYDRA_PEER_AUTO || algo > HYDRA_PEER_ONE_SHOT)
+  if (algo < HYDRA_PEER_AUTO || algo > HYDRA_PEER_TWO_SHOT_PUSH)
     return fail(HYDRA_ERR_INVALID, "invalid peer algorithm");
   const bool acc32 = (flags & HYDRA_ACC_F32) != 0;
   if (acc32 && dtype != HYDRA_BFLOAT16)
@@ -388,7 +388,7 @@ int hydra_peer_allreduce(hydra_peer_t p, int algo, int op, int dtype, int flags,
   const hydra_peer::Reg* reg = find_reg(p, buf, n * es);
   if (!reg) return fail(HYDRA_ERR_INVALID, "bucket is not inside a buffer opened by hydra_peer_open");
   if (algo == HYDRA_PEER_AUTO)
-    algo = n * es <= p->one_shot_max ? HYDRA_PEER_ONE_SHOT : HYDRA_PEER_TWO_SHOT;
+    algo = n * es <= p->one_shot_max ? HYDRA_PEER_ONE_SHOT : HYDRA_PEER_TWO_SHOT_PUSH;
 
   const hydra::PlanGeom g =
       hydra::make_geom(p->P, n, es, max_segment ? max_segment : (1u << 20), 0);
@@ -422,7 +422,17 @@ int hydra_peer_allreduce(hydra_peer_t p, int algo, int op, int dtype, int flags,
   // measured no faster (profiles/r05h, r05m)
   size_t grid =
       p->blocks > 0 ? (size_t)p->blocks : std::min<size_t>(std::max<size_t>(work, 1), 256);
-  const int kalgo = algo == HYDRA_PEER_ONE_SHOT ? hydra::kPeerOneShot : hydra::kPeerTwoShot;
+  if (algo == HYDRA_PEER_TWO_SHOT_PUSH) {
+    // the push stores the folded vectors into every bucket at the local bucket's alignment:
+    // every rank's bucket must sit at the same address mod 16 (true for the usual 256-B aligned
+    // allocations); otherwise TWO_SHOT, which every rank decides alike (congruence is shared)
+    for (int q = 0; q < p->P; q++)
+      if ((reinterpret_cast<uintptr_t>(A.x[q]) & 15) != (reinterpret_cast<uintptr_t>(A.x[p->rank]) & 15))
+        algo = HYDRA_PEER_TWO_SHOT;
+  }
+  const int kalgo = algo == HYDRA_PEER_ONE_SHOT        ? hydra::kPeerOneShot
+                    : algo == HYDRA_PEER_TWO_SHOT_PUSH ? hydra::kPeerTwoShotPush
+                                                       : hydra::kPeerTwoShot;
   if (const int cap = colocated_cap(p, kalgo, op, dtype, acc32)) {
     if (p->blocks > 0 && grid > (size_t)cap)
       return fail(HYDRA_ERR_INVALID,

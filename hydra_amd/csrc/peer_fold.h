@@ -67,6 +67,9 @@ __device__ __forceinline__ u32x4 fold_n(const u32x4 (&v)[NP]) {
 struct PeerSrcs {
   const char* p[kPeerMaxRanks];
 };
+struct PeerDsts {  // where a folded slab is stored: the local bucket, and (push) every peer's
+  char* p[kPeerMaxRanks];
+};
 
 // one element, same order as fold_n (static source indices: no scratch spills)
 template <typename E, int OP, bool ACC32>
@@ -97,32 +100,42 @@ __device__ __forceinline__ E fold_one(const PeerSrcs& S, int nsrc, size_t i) {
   }
 }
 
-// One workgroup folds `count` elements: dst[i] = fold(S.p[0][i], ..., S.p[NP-1][i]).
-// Aligned on dst (16 B); sources may sit at any element alignment (gfx950 unaligned mode).
+// One workgroup folds `count` elements: D.p[d][i] = fold(S.p[0][i], ..., S.p[NP-1][i]) for each
+// of the ND destinations (1: in place on the local bucket; NP: push -- the same result stored
+// into every rank's bucket).  Aligned on D.p[0] (16 B; push requires every destination at the
+// same alignment, checked by the launcher); sources may sit at any element alignment (gfx950
+// unaligned mode).
 // The main loop issues PU x NP unpredicated 16-B loads per lane before its first store (15-32
 // in flight: the grid is small -- every workgroup pays barriers -- so the depth has to come from
 // each wave; round 5's A/B on one GPU, profiles/r05k_*: twice the r05j depth was as fast or
 // faster at every size >= 16 Mi); the last partial round is predicated.
-template <typename E, int OP, bool ACC32, int V, int NP>
-__device__ __forceinline__ void slab_fold_n(char* dst, const PeerSrcs& S, size_t count) {
+template <typename E, int OP, bool ACC32, int V, int NP, int ND>
+__device__ __forceinline__ void slab_fold_n(const PeerDsts& D, const PeerSrcs& S, size_t count) {
   // (1-byte elements: half the depth -- their per-byte max / min unpack needs the registers)
   constexpr int PU = ((V & 4) ? 2 : 1) * (NP >= 4 ? 4 : 16 / NP) / (sizeof(E) == 1 ? 2 : 1);
   constexpr int N = Vec<E>::N;
   const int t = threadIdx.x;
-  size_t head = ((16 - (reinterpret_cast<uintptr_t>(dst) & 15)) & 15) / sizeof(E);
+  size_t head = ((16 - (reinterpret_cast<uintptr_t>(D.p[0]) & 15)) & 15) / sizeof(E);
   if (head > count) head = count;
   const size_t nvec = (count - head) / N;
   const size_t tail = count - head - nvec * N;
-  E* de = reinterpret_cast<E*>(dst);
-  if ((size_t)t < head) de[t] = fold_one<E, OP, ACC32>(S, NP, t);
+  if ((size_t)t < head) {
+    const E v = fold_one<E, OP, ACC32>(S, NP, t);
+#pragma unroll
+    for (int d = 0; d < ND; d++) reinterpret_cast<E*>(D.p[d])[t] = v;
+  }
   if ((size_t)t < tail) {
     const size_t i = head + nvec * N + t;
-    de[i] = fold_one<E, OP, ACC32>(S, NP, i);
+    const E v = fold_one<E, OP, ACC32>(S, NP, i);
+#pragma unroll
+    for (int d = 0; d < ND; d++) reinterpret_cast<E*>(D.p[d])[i] = v;
   }
   const char* src[NP];
 #pragma unroll
   for (int j = 0; j < NP; j++) src[j] = S.p[j] + head * sizeof(E);
-  char* out = dst + head * sizeof(E);
+  char* out[ND];
+#pragma unroll
+  for (int d = 0; d < ND; d++) out[d] = D.p[d] + head * sizeof(E);
   constexpr size_t kStep = (size_t)kBlock * PU;
   const size_t full = nvec / kStep * kStep;
   for (size_t v0 = 0; v0 < full; v0 += kStep) {
@@ -134,28 +147,38 @@ __device__ __forceinline__ void slab_fold_n(char* dst, const PeerSrcs& S, size_t
       for (int j = 0; j < NP; j++) r[u][j] = pld<V>(src[j] + o);
     }
 #pragma unroll
-    for (int u = 0; u < PU; u++)
-      pst<V>(out + (v0 + (size_t)u * kBlock + t) * 16, fold_n<E, OP, ACC32, NP>(r[u]));
+    for (int u = 0; u < PU; u++) {
+      const u32x4 o = fold_n<E, OP, ACC32, NP>(r[u]);
+#pragma unroll
+      for (int d = 0; d < ND; d++) pst<V>(out[d] + (v0 + (size_t)u * kBlock + t) * 16, o);
+    }
   }
   for (size_t v = full + t; v < nvec; v += kBlock) {  // the last partial round
     u32x4 r[NP];
 #pragma unroll
     for (int j = 0; j < NP; j++) r[j] = pld<V>(src[j] + v * 16);
-    pst<V>(out + v * 16, fold_n<E, OP, ACC32, NP>(r));
+    const u32x4 o = fold_n<E, OP, ACC32, NP>(r);
+#pragma unroll
+    for (int d = 0; d < ND; d++) pst<V>(out[d] + v * 16, o);
   }
 }
 
-template <typename E, int OP, bool ACC32, int V = 0>
-__device__ __forceinline__ void slab_fold(char* dst, const PeerSrcs& S, int nsrc, size_t count) {
+// PUSH: every source is also a destination (the result is stored into all P buckets)
+template <typename E, int OP, bool ACC32, int V = 0, bool PUSH = false>
+__device__ __forceinline__ void slab_fold(const PeerDsts& D, const PeerSrcs& S, int nsrc,
+                                          size_t count) {
   switch (nsrc) {  // uniform over the grid: one branch per slab, none in the loop
-    case 1: slab_fold_n<E, OP, ACC32, V, 1>(dst, S, count); break;
-    case 2: slab_fold_n<E, OP, ACC32, V, 2>(dst, S, count); break;
-    case 3: slab_fold_n<E, OP, ACC32, V, 3>(dst, S, count); break;
-    case 4: slab_fold_n<E, OP, ACC32, V, 4>(dst, S, count); break;
-    case 5: slab_fold_n<E, OP, ACC32, V, 5>(dst, S, count); break;
-    case 6: slab_fold_n<E, OP, ACC32, V, 6>(dst, S, count); break;
-    case 7: slab_fold_n<E, OP, ACC32, V, 7>(dst, S, count); break;
-    case 8: slab_fold_n<E, OP, ACC32, V, 8>(dst, S, count); break;
+#define HYDRA_SLAB_FOLD_CASE(k) \
+  case k: slab_fold_n<E, OP, ACC32, V, k, PUSH ? k : 1>(D, S, count); break;
+    HYDRA_SLAB_FOLD_CASE(1)
+    HYDRA_SLAB_FOLD_CASE(2)
+    HYDRA_SLAB_FOLD_CASE(3)
+    HYDRA_SLAB_FOLD_CASE(4)
+    HYDRA_SLAB_FOLD_CASE(5)
+    HYDRA_SLAB_FOLD_CASE(6)
+    HYDRA_SLAB_FOLD_CASE(7)
+    HYDRA_SLAB_FOLD_CASE(8)
+#undef HYDRA_SLAB_FOLD_CASE
   }
 }
 
@@ -227,10 +250,12 @@ __global__ __launch_bounds__(kBlock) void k_peer_two_shot(PeerLaunch A) {
     const size_t lo = A.lo[r], hi = A.lo[r + 1];
     for (size_t k = blockIdx.x; lo + k * SL < hi; k += G) {
       const size_t s = lo + k * SL;
+      PeerDsts D;
+      D.p[0] = A.x[r] + s * sizeof(E);
 #pragma unroll
       for (int j = 0; j < kPeerMaxRanks; j++)
         if (j < P) S.p[j] = A.x[(r + j) % P] + s * sizeof(E);
-      slab_fold<E, OP, ACC32, V>(A.x[r] + s * sizeof(E), S, P, hi - s < SL ? hi - s : SL);
+      slab_fold<E, OP, ACC32, V>(D, S, P, hi - s < SL ? hi - s : SL);
     }
   }
   // workgroup b of every rank has finished ITS slabs (k = b mod G) of its own block
@@ -253,6 +278,45 @@ __global__ __launch_bounds__(kBlock) void k_peer_two_shot(PeerLaunch A) {
   stamp<V>(A, 5);
 }
 
+// TWO_SHOT_PUSH: rank r folds its own block r pulling slab k from all P buckets (as TWO_SHOT's
+// phase 1) and stores the result into EVERY rank's bucket -- in place locally, over xGMI into
+// the P-1 peers' -- so TWO_SHOT's phase 2 (pulling the other blocks back) and its barrier are
+// gone: per rank n E read and n E written instead of (3P-1)/P n E, link bytes unchanged
+// (2(P-1)/P n E: (P-1)/P n read, (P-1)/P n written).  Safe without more synchronisation: block
+// r of any bucket is read only by rank r (its fold), and each slab is read and then written by
+// the same workgroup; a peer's push into my bucket touches only ITS block.  Barrier 2: every
+// peer's workgroup b has pushed its slabs k = b mod G into my bucket and read my slabs of its
+// block -- after it my bucket is final and nobody reads it.
+template <typename E, int OP, bool ACC32, int V = 0>
+__global__ __launch_bounds__(kBlock) void k_peer_push(PeerLaunch A) {
+  const size_t SL = A.slab_bytes / sizeof(E);
+  const PeerSync& Y = A.sync;
+  const int P = Y.P, r = Y.rank;
+  const uint32_t G = gridDim.x;
+  stamp<V>(A, 0);
+  if (group_broken(Y)) return;
+  if (!peer_barrier(Y, 1)) return;  // every rank's bucket is ready
+  stamp<V>(A, 1);
+  const size_t lo = A.lo[r], hi = A.lo[r + 1];
+  for (size_t k = blockIdx.x; lo + k * SL < hi; k += G) {
+    const size_t s = lo + k * SL;
+    PeerSrcs S;
+    PeerDsts D;
+#pragma unroll
+    for (int j = 0; j < kPeerMaxRanks; j++)
+      if (j < P) {
+        S.p[j] = A.x[(r + j) % P] + s * sizeof(E);
+        D.p[j] = A.x[(r + j) % P] + s * sizeof(E);  // D.p[0]: the local bucket
+      }
+    slab_fold<E, OP, ACC32, V, true>(D, S, P, hi - s < SL ? hi - s : SL);
+  }
+  stamp<V>(A, 2);
+  peer_barrier(Y, 2);
+  stamp<V>(A, 3);
+  stamp<V>(A, 4);
+  stamp<V>(A, 5);
+}
+
 template <typename E, int OP, bool ACC32, int V = 0>
 __global__ __launch_bounds__(kBlock) void k_peer_one_shot(PeerLaunch A) {
   const size_t SL = A.slab_bytes / sizeof(E);
@@ -272,10 +336,12 @@ __global__ __launch_bounds__(kBlock) void k_peer_one_shot(PeerLaunch A) {
     for (size_t k = 0; k < nsl; k++, w++) {
       if (w % G != blockIdx.x) continue;
       const size_t s = lo + k * SL;
+      PeerDsts D;
+      D.p[0] = A.scratch + s * sizeof(E);
 #pragma unroll
       for (int j = 0; j < kPeerMaxRanks; j++)
         if (j < P) S.p[j] = A.x[(q + j) % P] + s * sizeof(E);
-      slab_fold<E, OP, ACC32, V>(A.scratch + s * sizeof(E), S, P, hi - s < SL ? hi - s : SL);
+      slab_fold<E, OP, ACC32, V>(D, S, P, hi - s < SL ? hi - s : SL);
     }
   }
   // every rank's workgroup b has read its slabs of every bucket -> safe to overwrite ours
@@ -303,10 +369,13 @@ hipError_t launch_t(int algo, const PeerLaunch& A, unsigned grid, hipStream_t s,
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(
         occ,
         algo == kPeerOneShot ? reinterpret_cast<const void*>(&k_peer_one_shot<E, OP, ACC32, V>)
-                             : reinterpret_cast<const void*>(&k_peer_two_shot<E, OP, ACC32, V>),
+        : algo == kPeerTwoShotPush ? reinterpret_cast<const void*>(&k_peer_push<E, OP, ACC32, V>)
+                                   : reinterpret_cast<const void*>(&k_peer_two_shot<E, OP, ACC32, V>),
         kBlock, 0);
   if (algo == kPeerOneShot)
     hipLaunchKernelGGL((k_peer_one_shot<E, OP, ACC32, V>), dim3(grid), dim3(kBlock), 0, s, A);
+  else if (algo == kPeerTwoShotPush)
+    hipLaunchKernelGGL((k_peer_push<E, OP, ACC32, V>), dim3(grid), dim3(kBlock), 0, s, A);
   else
     hipLaunchKernelGGL((k_peer_two_shot<E, OP, ACC32, V>), dim3(grid), dim3(kBlock), 0, s, A);
   return hipGetLastError();

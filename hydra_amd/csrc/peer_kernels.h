@@ -8,7 +8,7 @@
 
 namespace hydra {
 
-enum PeerAlgo { kPeerAuto = 0, kPeerTwoShot = 1, kPeerOneShot = 2 };
+enum PeerAlgo { kPeerAuto = 0, kPeerTwoShot = 1, kPeerOneShot = 2, kPeerTwoShotPush = 3 };
 constexpr size_t kPeerSlabBytes = 64 << 10;  // largest work unit: 64 KiB of one owner block
 constexpr size_t kPeerMinSlabBytes = 4 << 10;
 

@@ -113,7 +113,8 @@ class PeerComm:
     def allreduce_(self, t, algo: str = "peer2", op: str = "sum", dtype_code: int | None = None,
                    flags: int = 0, max_segment: int = 0, stream: int | None = None) -> None:
         """In-place allreduce of registered device tensor t on the current (or given) stream.
-        algo: "peer2" (two-shot), "peer1" (one-shot), "peer" (auto by size)."""
+        algo: "peer2" (two-shot), "peer2w" (two-shot push: the fold stores into every bucket),
+        "peer1" (one-shot), "peer" (auto by size)."""
         import torch
 
         from .reduce import _torch_dtype_code

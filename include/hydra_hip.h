@@ -480,18 +480,36 @@ int hydra_reduce_root_simulate(int root, int op, int dtype, int flags, int P, vo
  *                        then pulls the other finished blocks (2(P-1)/P * n * E link bytes)
  *   HYDRA_PEER_ONE_SHOT  each rank folds the whole bucket into scratch, then copies it back
  *                        ((P-1) * n * E link bytes, 2 barriers: small buckets)
- *   HYDRA_PEER_AUTO      ONE_SHOT up to HYDRA_PEER_OPT_ONE_SHOT_MAX bytes (256 KiB), else TWO_SHOT
+ *   HYDRA_PEER_TWO_SHOT_PUSH  each rank folds its own block pulling from all P buckets and
+ *                        stores the result into EVERY bucket (its own in place, the peers' over
+ *                        xGMI): no second pull, 2 barriers, the same link bytes as TWO_SHOT and
+ *                        n * E read + n * E written per rank.  Needs every rank's bucket at the
+ *                        same address modulo 16 (else it runs as TWO_SHOT, on every rank alike)
+ *   HYDRA_PEER_AUTO      ONE_SHOT up to HYDRA_PEER_OPT_ONE_SHOT_MAX bytes (256 KiB), else
+ *                        TWO_SHOT_PUSH
  * Setup (every rank, same order; the byte blobs travel over any channel the caller has, e.g.
  * the rendezvous store): hydra_peer_create -> exchange sig handles -> hydra_peer_connect; for
  * each bucket: hydra_peer_register -> exchange -> hydra_peer_open.  Every rank must then issue
  * the same sequence of hydra_peer_allreduce calls (like any collective).  A call is one kernel
  * launch and is graph-capturable: barrier epochs live on the device, so replays need no new
  * arguments.  Eager calls on one group run one after another on the device even when issued on
- * different streams (each waits for the previous one's completion event).  A peer that never arrives ends the kernel after the timeout (default 20 s) and
- * leaves an error code readable with hydra_peer_error; later calls on the group fail with
- * HYDRA_ERR_HIP.  1 <= nranks <= 8. */
+ * different streams (each waits for the previous eager call's completion event).  A captured
+ * call neither waits for nor records that event (a capture cannot wait on an outside event):
+ * the caller orders a graph's replays against each other and against eager calls of the same
+ * group on other streams (e.g. one stream for all of them).  A peer that never arrives ends
+ * the kernel after the timeout (default 20 s) and leaves an error code readable with
+ * hydra_peer_error; later calls on the group fail with HYDRA_ERR_HIP.  1 <= nranks <= 8.
+ * Ranks of one group on the same GPU (each rank's GPU travels in its signal handle) must have
+ * every rank's whole grid resident at once: an explicit HYDRA_PEER_OPT_BLOCKS beyond the GPU's
+ * capacity / (ranks on it) is refused with HYDRA_ERR_INVALID, and the derived grid shrinks to
+ * fit. */
 #define HYDRA_PEER_HANDLE_BYTES 128
-typedef enum { HYDRA_PEER_AUTO = 0, HYDRA_PEER_TWO_SHOT = 1, HYDRA_PEER_ONE_SHOT = 2 } hydra_peer_algo_t;
+typedef enum {
+  HYDRA_PEER_AUTO = 0,
+  HYDRA_PEER_TWO_SHOT = 1,
+  HYDRA_PEER_ONE_SHOT = 2,
+  HYDRA_PEER_TWO_SHOT_PUSH = 3
+} hydra_peer_algo_t;
 typedef enum {
   HYDRA_PEER_OPT_TIMEOUT_MS = 1,  /* barrier timeout (default 20000) */
   HYDRA_PEER_OPT_BLOCKS = 2,      /* workgroups per launch (0 = derived from the bucket, <= 1024) */

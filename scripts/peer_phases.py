@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Where the peer-access allreduce's time goes: P rank processes share the
 one GPU's cuda:0 (the one-GPU proxy of scripts/peer_bench.py: every "remote" read is a local
-HBM read), each running the shipped two-shot kernel with its phase clocks on
+HBM read), each running the shipped two-shot kernel (--algo peer2: pull, peer2w: push) with its phase
+clocks on
 (hydra_measure_peer_stamps, libhydra_measure.so): per workgroup b of every rank, s_memrealtime
 (100 MHz, one clock for the whole GPU, so ranks compare directly) at
 
@@ -58,7 +59,7 @@ def worker(a):
         x = synth.fill_at(synth.stress_at, a.P, a.rank, a.n, dev, torch.float32)
         peer.register(x)
         for _ in range(a.warmup):
-            peer.allreduce_(x, algo="peer2")
+            peer.allreduce_(x, algo=a.algo)
         torch.cuda.synchronize(dev)
         # the event-timed kernel without clocks (the shipped kernel exactly), then with them
         dist.barrier()
@@ -66,14 +67,14 @@ def worker(a):
         s = torch.cuda.current_stream(dev)
         e0.record(s)
         for _ in range(a.iters):
-            peer.allreduce_(x, algo="peer2")
+            peer.allreduce_(x, algo=a.algo)
         e1.record(s)
         torch.cuda.synchronize(dev)
         out["event_ms_plain"] = e0.elapsed_time(e1) / a.iters
         _lib.check(L.hydra_measure_peer_stamps(peer._h, ctypes.c_void_p(stamps.data_ptr()), grid))
         for _ in range(a.iters):
             dist.barrier()
-            peer.allreduce_(x, algo="peer2")
+            peer.allreduce_(x, algo=a.algo)
             torch.cuda.synchronize(dev)
             out["calls"].append(stamps.view(grid, _lib.PEER_STAMPS).cpu().numpy().tolist())
         _lib.check(L.hydra_measure_peer_stamps(peer._h, None, 0))
@@ -87,14 +88,18 @@ def worker(a):
     dist.destroy_process_group()
 
 
-def summarize(P, n, res):
+def summarize(P, n, res, algo="peer2"):
     import numpy as np
 
     E = 4
     grid = res[0]["grid"]
-    fold_bytes = (P + 1) * n * E           # all ranks: P reads + 1 write of each owner block
-    copy_bytes = 2 * (P - 1) * n * E       # all ranks: (P-1)/P n read + written, each
-    total_bytes = (3 * P - 1) * n * E      # peer_bench.py's two-shot HBM bytes
+    if algo == "peer2w":  # push: the fold writes every bucket; no copy phase
+        fold_bytes = 2 * P * n * E         # all ranks: P reads + P writes of each owner block
+        copy_bytes = 0
+    else:
+        fold_bytes = (P + 1) * n * E       # all ranks: P reads + 1 write of each owner block
+        copy_bytes = 2 * (P - 1) * n * E   # all ranks: (P-1)/P n read + written, each
+    total_bytes = fold_bytes + copy_bytes  # peer_bench.py's two-shot HBM bytes
     rows = []
     for c in range(len(res[0]["calls"])):
         t = np.array([r["calls"][c] for r in res], dtype=np.int64)  # [rank, wg, 6]
@@ -108,7 +113,8 @@ def summarize(P, n, res):
             "rank_start_skew_us": float((t[:, :, 0].min(axis=1).max() -
                                          t[:, :, 0].min(axis=1).min()) * TICK_S * 1e6),
             "fold_window_us": fold_w * 1e6, "copy_window_us": copy_w * 1e6,
-            "fold_GBps": fold_bytes / fold_w / 1e9, "copy_GBps": copy_bytes / copy_w / 1e9,
+            "fold_GBps": fold_bytes / fold_w / 1e9,
+            "copy_GBps": copy_bytes / copy_w / 1e9 if copy_w > 0 else 0.0,
             "span_GBps": total_bytes / span / 1e9,
             **{f"{k}_median_us": float(np.median(v)) * 1e6 for k, v in per_wg.items()},
             **{f"{k}_max_us": float(v.max()) * 1e6 for k, v in per_wg.items()},
@@ -116,7 +122,8 @@ def summarize(P, n, res):
     med = {k: float(np.median([r[k] for r in rows])) for k in rows[0]}
     plain = max(r["event_ms_plain"] for r in res)
     out = {
-        "P": P, "elements": n, "dtype": "f32", "workgroups_per_rank": grid, "calls": len(rows),
+        "P": P, "algo": algo, "elements": n, "dtype": "f32", "workgroups_per_rank": grid,
+        "calls": len(rows),
         "proxy": "all ranks on one GPU (IPC between processes on one device): remote reads are "
                  "local HBM reads; one clock for the whole GPU",
         "bytes": {"fold_all_ranks": fold_bytes, "copy_all_ranks": copy_bytes,
@@ -141,6 +148,7 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--blocks", type=int, default=0)
+    ap.add_argument("--algo", default="peer2", choices=["peer2", "peer2w"])
     ap.add_argument("--rocprof", default="")
     ap.add_argument("--rank", type=int, default=-1)
     ap.add_argument("--port", type=int, default=0)
@@ -155,10 +163,11 @@ def main():
     for r in range(a.P):
         cmd = ["python3", "-u", os.path.abspath(__file__), "--rank", str(r), "--port", str(port),
                "--P", str(a.P), "--n", str(a.n), "--iters", str(a.iters), "--warmup",
-               str(a.warmup), "--blocks", str(a.blocks)]
+               str(a.warmup), "--blocks", str(a.blocks), "--algo", a.algo]
         if a.rocprof:  # the profiler wraps the rank program itself (nothing in between)
             d = os.path.join(a.rocprof, f"rank{r}")
-            cmd = ["rocprofv3", "--kernel-trace", "--stats", "-d", d, "-o", f"rank{r}", "--"] + cmd
+            cmd = ["rocprofv3", "--kernel-trace", "--stats", "--output-format", "csv", "-d", d,
+                   "-o", f"rank{r}", "--"] + cmd
         procs.append(subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
     res = []
     for p in procs:
@@ -168,7 +177,7 @@ def main():
             print(o[-3000:], file=sys.stderr)
             raise SystemExit(p.returncode)
         res.append(json.loads([ln for ln in o.splitlines() if ln.startswith("RESULT ")][-1][7:]))
-    print(json.dumps(summarize(a.P, a.n, res)), flush=True)
+    print(json.dumps(summarize(a.P, a.n, res, a.algo)), flush=True)
 
 
 if __name__ == "__main__":

@@ -128,6 +128,11 @@ def _worker(rank, world, port, q, stall_rank=-1, stall_waits=0, extra_legs=False
         dist.destroy_process_group()
 
 
+def ph_algo_ok(pl):
+    """the phase entry is the timed schedule's"""
+    return pl["phases"].get("algo") == pl["algo"]
+
+
 def _start(world, stall_rank=-1, stall_waits=0, extra_legs=False, peer="auto", peer_fail_at=-1):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -236,30 +241,38 @@ def test_bench_peer_leg_orchestration(world):
     res = out[0][0]
     pl = res["peer_leg"]
     assert pl["enabled"] and pl["mode"] == "on" and "error" not in pl, pl
-    assert pl["parity_fold_order_1M"] == {"peer2": "bit-exact", "peer1": "bit-exact"}, pl
+    assert pl["parity_fold_order_1M"] == {"peer2": "bit-exact", "peer2w": "bit-exact",
+                                          "peer1": "bit-exact"}, pl
     assert pl["full_size_exact"] is True and pl["ms_per_step"] > 0, pl
-    # a GPU per rank (no shared-GPU cap): two workgroups per CU is a candidate too
-    assert set(pl["autotune_ms"]) == {"peer2/0wg", "peer2/512wg", "peer2/128wg", "peer2/64wg"}, pl
+    assert pl["full_size_exact_by_algo"] == {"peer2w": True, "peer2": True}, pl
+    # both two-shot schedules x the workgroup counts; a GPU per rank (no shared-GPU cap): two
+    # workgroups per CU is a candidate too
+    assert set(pl["autotune_ms"]) == {f"{a}/{w}wg" for a in ("peer2", "peer2w")
+                                      for w in (0, 512, 128, 64)}, pl
+    assert pl["algo"] in ("peer2", "peer2w") and ph_algo_ok(pl), pl
     ph = pl["phases"]
     assert ph["kernel_ms"] > 0 and ph["link"]["algorithmic_bytes"] == int(
         2 * (world - 1) / world * (1 << 16) * 4), ph
     assert ph["link"]["peers"] == world - 1 and ph["fold"]["frac_of_hbm"] > 0, ph
     assert pl["full_size_gate"].startswith("equal to this run's DIRECT bucket"), pl
     if pl["promoted"]:
-        assert res["config"]["algo"] == "peer2" and res["ms_per_step"] == pl["ms_per_step"]
-        assert res["parity"]["full_size_exact"]["peer2"] is True
+        a = pl["algo"]
+        assert res["config"]["algo"] == a and res["ms_per_step"] == pl["ms_per_step"]
+        assert res["parity"]["full_size_exact"][a] is True
         # the promoted headline carries its own phase entry and parity
         assert res["roofline"]["phases"] == ph, res["roofline"]
-        assert res["parity"]["fold_order_1M"]["peer2"] == "bit-exact", res["parity"]
+        assert res["parity"]["fold_order_1M"][a] == "bit-exact", res["parity"]
     else:
-        assert res["config"]["algo"] != "peer2" and res["ms_per_step"] <= pl["ms_per_step"]
+        assert not res["config"]["algo"].startswith("peer") and \
+            res["ms_per_step"] <= pl["ms_per_step"]
     assert all(out[r][0]["peer_leg"]["promoted"] == pl["promoted"] for r in out)
 
 
-@pytest.mark.parametrize("fail_at,stage", [(4, "autotune"), (32, "timed region")])
+@pytest.mark.parametrize("fail_at,stage", [(5, "autotune"), (61, "timed region")])
 def test_bench_peer_leg_one_rank_fails_mid_loop(fail_at, stage):
-    """a peer call that fails on ONE rank inside the autotune (its 5th call) or the
-    timed region (its 33rd: the first timed step) -- that rank records it and keeps issuing the
+    """a peer call that fails on ONE rank inside the autotune (its 6th call: after 3
+    parity and 2 full-size calls) or the timed region (its 62nd: after 2 x 4 x 7 autotune calls,
+    the first timed step) -- that rank records it and keeps issuing the
     same collectives; its peers' calls end at their bounded barrier (the fake group's 3 s
     timeout, the kernel's error word on a GPU) -- so the leg ends with an error entry of that
     stage on every rank, nobody is stranded and the RCCL headline stands."""

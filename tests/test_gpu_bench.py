@@ -80,13 +80,18 @@ def test_bench_rehearsal_world2_peer_leg(gpu):
     par = res["parity"]["fold_order_1M"]
     for algo in ("direct", "ring", "a2a", "apipe"):
         assert par[algo] == "bit-exact", (algo, par)
+    # the full-size gate on fold-order-sensitive data
+    g = res["parity"]["full_size_gate"]
+    assert g["ok"] and g["data"] == "stress_at" and g["sha256_equal_across_ranks"], g
     pl = res["peer_leg"]
     assert pl["enabled"] and "error" not in pl, pl
-    assert pl["parity_fold_order_1M"] == {"peer2": "bit-exact", "peer1": "bit-exact"}, pl
+    assert pl["parity_fold_order_1M"] == {"peer2": "bit-exact", "peer2w": "bit-exact",
+                                          "peer1": "bit-exact"}, pl
     assert pl["full_size_exact"] is True and pl["ms_per_step"] > 0, pl
+    assert pl["full_size_exact_by_algo"] == {"peer2w": True, "peer2": True}, pl
     assert pl["phases"]["kernel_ms"] > 0 and pl["phases"]["link"]["peers"] == 1, pl
     if pl["promoted"]:
-        assert res["config"]["algo"] == "peer2", res["config"]
+        assert res["config"]["algo"] == pl["algo"] in ("peer2", "peer2w"), res["config"]
 
 
 @pytest.mark.extra

@@ -92,7 +92,7 @@ def expected(O, c, P):
 def cases_for(P):
     F32, I32, F16, BF16 = _lib.FLOAT32, _lib.INT32, _lib.FLOAT16, _lib.BFLOAT16
     cs = []
-    for algo in ("peer2", "peer1"):
+    for algo in ("peer2", "peer2w", "peer1"):
         for n, ms, off in ((1, 0, 0), (7, 0, 4), (1000, 128, 0), (4099, 128, 12),
                            (262145, 0, 0), (1 << 20, 0, 4), (3000001, 0, 0)):
             if algo == "peer1" and n > (1 << 20):
@@ -101,39 +101,53 @@ def cases_for(P):
                            dtype=F32, n=n, ms=ms, offset_bytes=off))
     cs.append(dict(name="peer2_i32", algo="peer2", data="int32", dtype=I32, n=100003, ms=4096,
                    offset_bytes=8))
+    cs.append(dict(name="peer2w_i32", algo="peer2w", data="int32", dtype=I32, n=100003, ms=4096,
+                   offset_bytes=8))
+    cs.append(dict(name="peer2w_f16", algo="peer2w", data="f16", dtype=F16, n=20011, ms=1024,
+                   offset_bytes=2))
     cs.append(dict(name="peer1_i32", algo="peer1", data="int32", dtype=I32, n=100003, ms=4096))
     cs.append(dict(name="peer2_f16", algo="peer2", data="f16", dtype=F16, n=20011, ms=1024,
                    offset_bytes=2))
     cs.append(dict(name="peer1_f16", algo="peer1", data="f16", dtype=F16, n=20011, ms=1024))
     for op in ("max", "min", "product"):
-        cs.append(dict(name=f"peer2_{op}", algo="peer2", data="stress_f32", dtype=F32, n=70001,
-                       ms=4096, op=op))
+        for algo in ("peer2", "peer2w"):
+            cs.append(dict(name=f"{algo}_{op}", algo=algo, data="stress_f32", dtype=F32,
+                           n=70001, ms=4096, op=op))
     cs.append(dict(name="auto_small", algo="peer", data="stress_f32", dtype=F32, n=5000))
     cs.append(dict(name="repeat", algo="peer2", data="stress_f32", dtype=F32, n=262147,
                    repeat=25))
     cs.append(dict(name="graph2", algo="peer2", data="stress_f32", dtype=F32, n=300007,
                    graph=True))
+    cs.append(dict(name="graph2w", algo="peer2w", data="stress_f32", dtype=F32, n=300007,
+                   graph=True))
+    cs.append(dict(name="repeat2w", algo="peer2w", data="stress_f32", dtype=F32, n=262147,
+                   repeat=25))
     cs.append(dict(name="graph1", algo="peer1", data="int32", dtype=I32, n=30011, ms=4096,
                    graph=True))
     cs.append(dict(name="stress2", algo="peer2", data="stress", dtype=F32, n=200003, iters=40,
                    offset_bytes=4))
     cs.append(dict(name="stress1", algo="peer1", data="stress", dtype=F32, n=50021, iters=40))
+    cs.append(dict(name="stress2w", algo="peer2w", data="stress", dtype=F32, n=200003, iters=40,
+                   offset_bytes=4))
     # calls on two streams with no ordering between them: serialized by the library
     cs.append(dict(name="streams2", algo="peer2", data="streams", dtype=F32, n=100003, iters=8))
     cs.append(dict(name="streams1", algo="peer1", data="streams", dtype=F32, n=30011, iters=8))
+    cs.append(dict(name="streams2w", algo="peer2w", data="streams", dtype=F32, n=100003,
+                   iters=8))
     cs.append(dict(name="bf16_acc32", algo="peer2", data="bf16", dtype=BF16, n=1 << 20,
                    flags=_lib.ACC_F32))
     # config 5's arithmetic bit-exact: fold-order-sensitive bf16 values, fp32 accumulation in
     # the reference order, one rounding (both schedules; 2P-misaligned sizes, small segments)
     for algo, n, ms, off in (("peer2", (1 << 20) + 3, 0, 2), ("peer2", 100003, 4096, 0),
-                             ("peer1", 30011, 1024, 6)):
+                             ("peer2w", (1 << 20) + 3, 0, 2), ("peer1", 30011, 1024, 6)):
         cs.append(dict(name=f"{algo}_bf16_acc32_cancel_{n}", algo=algo, data="bf16_cancel",
                        dtype=BF16, n=n, ms=ms, offset_bytes=off, flags=_lib.ACC_F32))
     # every other element type the kernels instantiate, both schedules
     for nm, npt, code in (("i8", "int8", _lib.INT8), ("u8", "uint8", _lib.UINT8),
                           ("i64", "int64", _lib.INT64), ("u64", "uint64", _lib.UINT64),
                           ("f64", "float64", _lib.FLOAT64)):
-        for algo, n, ms, off in (("peer2", 65543, 4096, 8), ("peer1", 4099, 128, 0)):
+        for algo, n, ms, off in (("peer2", 65543, 4096, 8), ("peer2w", 65543, 4096, 8),
+                                 ("peer1", 4099, 128, 0)):
             cs.append(dict(name=f"{algo}_{nm}_{n}", algo=algo, data="typed", np=npt, dtype=code,
                            n=n, ms=ms, offset_bytes=off))
     cs.append(dict(name="peer2_i8_max", algo="peer2", data="typed", np="int8", dtype=_lib.INT8,
@@ -143,6 +157,8 @@ def cases_for(P):
     cs.append(dict(name="peer2_f64_product", algo="peer2", data="typed", np="float64",
                    dtype=_lib.FLOAT64, n=30011, ms=4096, op="product"))
     cs.append(dict(name="peer2_bf16_native", algo="peer2", data="bf16_native", dtype=BF16,
+                   n=100003, ms=4096, offset_bytes=2))
+    cs.append(dict(name="peer2w_bf16_native", algo="peer2w", data="bf16_native", dtype=BF16,
                    n=100003, ms=4096, offset_bytes=2))
     cs.append(dict(name="peer1_bf16_native", algo="peer1", data="bf16_native", dtype=BF16,
                    n=20011, ms=1024))
@@ -190,8 +206,8 @@ def test_peer_config4_full_size_order_sensitive(gpu, O, tmp_path, P):
     """BASELINE config 4 at its full size through the peer-access kernel --
     P ranks x 64 Mi fp32 of fold-order-sensitive values (synth.stress_at, generated on the GPU),
     every rank's whole bucket (sha256 of its bytes) equal to the C restatement of the reference
-    ring (O.ring_result), for the two-shot schedule (the one the N>1 line may promote) and the
-    one-shot one.  Reference geometry at this size: 256 segments of 1 MiB, S = 256/P per rank
+    ring (O.ring_result), for both two-shot schedules (pull and push: the ones the N>1 line may
+    promote) and the one-shot one.  Reference geometry at this size: 256 segments of 1 MiB, S = 256/P per rank
     (allreduce.cc:212-221, 253-258): S = 128 / 64 / 32 at P = 2 / 4 / 8.  The ranks share the
     one GPU, so each rank's grid is 512 / P workgroups (all of them resident at once)."""
     import hashlib
@@ -205,7 +221,7 @@ def test_peer_config4_full_size_order_sensitive(gpu, O, tmp_path, P):
     assert (ns, sb, S) == (256, 1 << 20, 256 // P)
     F32 = _lib.FLOAT32
     cases = [dict(name=f"{a}_full", algo=a, data="full_stress", dtype=F32, n=n)
-             for a in ("peer2", "peer1")]
+             for a in ("peer2", "peer2w", "peer1")]
     res, st = run_ranks(tmp_path, P, cases, blocks=512 // P, timeout=240,
                         arena_bytes=4 * n)
     xs = [device_bucket(synth.stress_at, P, r, n, gpu, torch.float32).cpu().numpy()
@@ -229,8 +245,8 @@ def test_peer_config4_full_size_order_sensitive(gpu, O, tmp_path, P):
 def test_peer_config5_full_size_sampled(gpu, O, tmp_path):
     """BASELINE config 5 at its full size through the peer-access kernel --
     8 ranks x 256 Mi bf16 with fp32 accumulation (HYDRA_ACC_F32) on synth.stress_cancel_at
-    (+-2^k pivots that cancel, so the one bf16 rounding does not hide the fp32 fold order), two-shot
-    schedule; >= 1 Mi sampled elements of every rank (every segment boundary, random ones) equal
+    (+-2^k pivots that cancel, so the one bf16 rounding does not hide the fp32 fold order), both
+    two-shot schedules (pull, push); >= 1 Mi sampled elements of every rank (every segment boundary, random ones) equal
     the C restatement's fold on the widened values with the bf16 geometry (512 segments of 1 MiB,
     S = 64 per rank), rounded once."""
     from fold_expect import bf16_acc32_expected, sample_indices
@@ -241,19 +257,21 @@ def test_peer_config5_full_size_sampled(gpu, O, tmp_path):
     idx = sample_indices(n, ns, sb // 2)
     ipath = tmp_path / "idx.npy"
     np.save(ipath, idx)
-    cases = [dict(name="peer2_bf16_full", algo="peer2", data="full_cancel_bf16",
-                  dtype=_lib.BFLOAT16, n=n, flags=_lib.ACC_F32, idx_file=str(ipath))]
+    cases = [dict(name=f"{a}_bf16_full", algo=a, data="full_cancel_bf16",
+                  dtype=_lib.BFLOAT16, n=n, flags=_lib.ACC_F32, idx_file=str(ipath))
+             for a in ("peer2", "peer2w")]
     res, st = run_ranks(tmp_path, P, cases, blocks=512 // P, timeout=240, arena_bytes=2 * n)
     exp, vals, _ = bf16_acc32_expected(O, P, n, idx)
     left = synth.bf16_to_f32(vals[0]).astype(np.float32)
     for v in vals[1:]:
         left = O.acc_bf16_f32(left, v)
     assert float(np.mean(synth.bf16_bits(left) != exp)) > 0.3  # the check sees fold orders
-    for r in range(P):
-        assert st[r]["peer2_bf16_full"] == 0, (r, st[r])
-        got = res[r]["peer2_bf16_full"]
-        bad = np.flatnonzero(got != exp)
-        assert bad.size == 0, (r, bad.size, idx[bad[:5]].tolist())
+    for c in cases:
+        for r in range(P):
+            assert st[r][c["name"]] == 0, (r, st[r])
+            got = res[r][c["name"]]
+            bad = np.flatnonzero(got != exp)
+            assert bad.size == 0, (c["name"], r, bad.size, idx[bad[:5]].tolist())
 
 
 @pytest.mark.parametrize("P", [4, 8])
