@@ -35,15 +35,16 @@ namespace {
 constexpr int kPeerVariantBase = 2000;  // hydra_set_variant 2001..2007: peer kernel A/B
 
 // (measurement only) the f32-sum kernels with nontemporal loads / stores / deeper pipelining
-hipError_t launch_variant(int v, int algo, const PeerLaunch& A, unsigned grid, hipStream_t s) {
+hipError_t launch_variant(int v, int algo, const PeerLaunch& A, unsigned grid, hipStream_t s,
+                          int* occ = nullptr) {
   switch (v) {
-    case 1: return launch_t<float, kSum, false, 1>(algo, A, grid, s);
-    case 2: return launch_t<float, kSum, false, 2>(algo, A, grid, s);
-    case 3: return launch_t<float, kSum, false, 3>(algo, A, grid, s);
-    case 4: return launch_t<float, kSum, false, 4>(algo, A, grid, s);
-    case 5: return launch_t<float, kSum, false, 5>(algo, A, grid, s);
-    case 6: return launch_t<float, kSum, false, 6>(algo, A, grid, s);
-    case 7: return launch_t<float, kSum, false, 7>(algo, A, grid, s);
+    case 1: return launch_t<float, kSum, false, 1>(algo, A, grid, s, occ);
+    case 2: return launch_t<float, kSum, false, 2>(algo, A, grid, s, occ);
+    case 3: return launch_t<float, kSum, false, 3>(algo, A, grid, s, occ);
+    case 4: return launch_t<float, kSum, false, 4>(algo, A, grid, s, occ);
+    case 5: return launch_t<float, kSum, false, 5>(algo, A, grid, s, occ);
+    case 6: return launch_t<float, kSum, false, 6>(algo, A, grid, s, occ);
+    case 7: return launch_t<float, kSum, false, 7>(algo, A, grid, s, occ);
   }
   return hipErrorInvalidValue;
 }
@@ -76,6 +77,11 @@ hipError_t launch_peer(int algo, int op, int dtype, bool acc32, const PeerLaunch
 
 hipError_t peer_occupancy(int algo, int op, int dtype, bool acc32, int* per_cu) {
   const PeerLaunch A{};
+#ifdef HYDRA_MEASURE  // a variant's own register count (the deeper ones hold fewer per CU)
+  const int v = current_variant() - kPeerVariantBase;
+  if (v >= 1 && v <= 7 && op == kSum && dtype == kF32 && !acc32)
+    return launch_variant(v, algo, A, 1, nullptr, per_cu);
+#endif
   switch (op) {
     case kSum: return launch_peer_sum(algo, dtype, acc32, A, 1, nullptr, per_cu);
     case kProduct: return launch_peer_product(algo, dtype, acc32, A, 1, nullptr, per_cu);
