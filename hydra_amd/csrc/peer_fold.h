@@ -18,7 +18,8 @@ namespace {
 
 // Measurement variants (libhydra_measure.so only: hydra_set_variant 2001..2007 and the phase
 // clocks of hydra_measure_peer_stamps, f32 sum; 0 = the shipped kernel): bit 0 nontemporal
-// loads, bit 1 nontemporal stores, bit 2 twice the loads in flight, bit 3 phase clocks.
+// loads, bit 1 nontemporal stores, bit 2 twice the loads in flight, bit 3 phase clocks, bit 4
+// the 1-3-source folds as deep as the others.
 template <int V>
 __device__ __forceinline__ u32x4 pld(const char* p) {
   if constexpr ((V & 1) != 0) return ld<kNT>(p, rsrc<kNT>(nullptr, 0), 0);
@@ -112,7 +113,10 @@ __device__ __forceinline__ E fold_one(const PeerSrcs& S, int nsrc, size_t i) {
 template <typename E, int OP, bool ACC32, int V, int NP, int ND>
 __device__ __forceinline__ void slab_fold_n(const PeerDsts& D, const PeerSrcs& S, size_t count) {
   // (1-byte elements: half the depth -- their per-byte max / min unpack needs the registers)
-  constexpr int PU = ((V & 4) ? 2 : 1) * (NP >= 4 ? 4 : 16 / NP) / (sizeof(E) == 1 ? 2 : 1);
+  // (V & 16: the small-NP cases as deep as NP >= 4's 32 vectors -- free in registers, which the
+  // NP = 8 case sets for the whole kernel)
+  constexpr int PU = ((V & 4) ? 2 : 1) * (NP >= 4 ? 4 : ((V & 16) ? 32 : 16) / NP) /
+                     (sizeof(E) == 1 ? 2 : 1);
   constexpr int N = Vec<E>::N;
   const int t = threadIdx.x;
   size_t head = ((16 - (reinterpret_cast<uintptr_t>(D.p[0]) & 15)) & 15) / sizeof(E);

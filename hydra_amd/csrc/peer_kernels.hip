@@ -45,6 +45,7 @@ hipError_t launch_variant(int v, int algo, const PeerLaunch& A, unsigned grid, h
     case 5: return launch_t<float, kSum, false, 5>(algo, A, grid, s, occ);
     case 6: return launch_t<float, kSum, false, 6>(algo, A, grid, s, occ);
     case 7: return launch_t<float, kSum, false, 7>(algo, A, grid, s, occ);
+    case 16: return launch_t<float, kSum, false, 16>(algo, A, grid, s, occ);
   }
   return hipErrorInvalidValue;
 }
@@ -59,7 +60,7 @@ hipError_t launch_peer(int algo, int op, int dtype, bool acc32, const PeerLaunch
     return hipErrorInvalidValue;
 #ifdef HYDRA_MEASURE
   const int v = current_variant() - kPeerVariantBase;  // (measurement only)
-  if (v >= 1 && v <= 7 && op == kSum && dtype == kF32 && !acc32)
+  if (((v >= 1 && v <= 7) || v == 16) && op == kSum && dtype == kF32 && !acc32)
     return launch_variant(v, algo, A, grid, s);
   if (A.stamps) {  // hydra_measure_peer_stamps: the shipped kernel plus its phase clocks
     if (op != kSum || dtype != kF32 || acc32) return hipErrorInvalidValue;
@@ -79,7 +80,7 @@ hipError_t peer_occupancy(int algo, int op, int dtype, bool acc32, int* per_cu) 
   const PeerLaunch A{};
 #ifdef HYDRA_MEASURE  // a variant's own register count (the deeper ones hold fewer per CU)
   const int v = current_variant() - kPeerVariantBase;
-  if (v >= 1 && v <= 7 && op == kSum && dtype == kF32 && !acc32)
+  if (((v >= 1 && v <= 7) || v == 16) && op == kSum && dtype == kF32 && !acc32)
     return launch_variant(v, algo, A, 1, nullptr, per_cu);
 #endif
   switch (op) {

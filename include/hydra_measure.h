@@ -18,7 +18,8 @@ extern "C" {
  *   1..52      hydra_reduce / hydra_chunk_sum (fp32 / int32 sum): unroll, cache policy, grid,
  *              LDS-DMA double buffering (13, 18), wave-shuffle tail (44), persistent (45-47)
  *   1..7       hydra_fold (the DIRECT / A2A owner fold): load policy, grid cap, XCD map
- *   2001..2007 hydra_peer_allreduce (fp32 sum): nontemporal loads / stores, deeper pipelining */
+ *   2001..2007 hydra_peer_allreduce (fp32 sum): nontemporal loads / stores, deeper pipelining;
+ *   2016       the same with the 1-3-source folds as deep as the others */
 int hydra_set_variant(int variant);
 
 /* Phase clocks of the peer-access allreduce (fp32 sum only while set): every later

@@ -218,6 +218,11 @@ def main():
             nbytes = x.nbytes
             off = c.get("offset_bytes", 0)
             view = arena[off:off + nbytes]
+            own = None
+            if c.get("rank_shift"):  # a bucket of its own, at a rank-dependent address mod 16
+                own = torch.zeros(nbytes + 64, dtype=torch.uint8, device=dev)
+                view = own[a.rank * c["rank_shift"]:a.rank * c["rank_shift"] + nbytes]
+                peer.register(view)
             view.copy_(torch.from_numpy(x.view(np.uint8)))
             code = c["dtype"]
             kw = dict(algo=c["algo"], op=c.get("op", "sum"), dtype_code=code,
@@ -249,6 +254,9 @@ def main():
                 continue
             results[name] = view.cpu().numpy().copy()
             status[name] = peer.error()
+            if own is not None:
+                peer.unregister(view)
+                del view, own
         dist.barrier()
     finally:
         peer.close()

@@ -120,6 +120,12 @@ def cases_for(P):
                    graph=True))
     cs.append(dict(name="graph2w", algo="peer2w", data="stress_f32", dtype=F32, n=300007,
                    graph=True))
+    # buckets at different addresses mod 16 on different ranks: the push cannot store at the
+    # local alignment everywhere, so every rank runs the pull schedule instead (same bits)
+    cs.append(dict(name="peer2w_rank_shift", algo="peer2w", data="stress_f32", dtype=F32,
+                   n=262147, rank_shift=4))
+    cs.append(dict(name="auto_rank_shift", algo="peer", data="stress_f32", dtype=F32,
+                   n=(1 << 20) + 1, rank_shift=8))
     cs.append(dict(name="repeat2w", algo="peer2w", data="stress_f32", dtype=F32, n=262147,
                    repeat=25))
     cs.append(dict(name="graph1", algo="peer1", data="int32", dtype=I32, n=30011, ms=4096,
