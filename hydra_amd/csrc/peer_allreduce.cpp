@@ -40,13 +40,15 @@ static_assert(kIpcBytes <= 64, "hipIpcMemHandle_t larger than the blob slot");
 // [64,72) offset of the buffer in it, [72,80) buffer bytes, [80,88) magic, [88,92) rank,
 // [96,104) the exporter's allocation id (HIP_POINTER_ATTRIBUTE_BUFFER_ID: unique per
 // allocation, so a freed-and-reallocated bucket whose IPC handle bytes repeat is a NEW mapping),
-// [104,116) the exporter's GPU (PCI domain, bus, device: ranks on the same GPU share its CUs).
+// [104,116) the exporter's GPU (PCI domain, bus, device: ranks on the same GPU share its CUs),
+// [116,120) its compute units.
 struct Blob {
   unsigned char ipc[64];
   uint64_t offset, bytes, magic;
   int32_t rank, pad;
   uint64_t alloc_id;
   int32_t pci[3];
+  int32_t cus;
 };
 static_assert(sizeof(Blob) <= HYDRA_PEER_HANDLE_BYTES, "blob too large");
 
@@ -61,7 +63,9 @@ struct hydra_peer {
   int P = 1, rank = 0, device = 0;
   int pci[3] = {0, 0, 0};  // this rank's GPU (PCI domain, bus, device)
   int cus = 0;             // its compute units
-  int colocated = 1;       // ranks of the group on this GPU, this one included (connect)
+  // (connect) the most ranks of the group on any one GPU, and the fewest CUs of the group's
+  // GPUs: the same on every rank, so every rank derives the same grid
+  int colocated = 1, group_cus = 0;
   hydra::PeerSignals* sig = nullptr;  // own signal area (uncached device memory)
   hydra::PeerSigPtrs sigs{};          // every rank's, mapped
   uint32_t* err_host = nullptr;       // host-mapped error word the kernels write
@@ -125,6 +129,7 @@ int export_blob(hydra_peer* p, void* ptr, size_t bytes, void* out) {
   blob.rank = p->rank;
   blob.alloc_id = (uint64_t)id;
   std::memcpy(blob.pci, p->pci, sizeof(blob.pci));
+  blob.cus = p->cus;
   std::memset(out, 0, HYDRA_PEER_HANDLE_BYTES);
   std::memcpy(out, &blob, sizeof(blob));
   return HYDRA_OK;
@@ -184,7 +189,7 @@ int colocated_cap(const hydra_peer* p, int algo, int op, int dtype, bool acc32) 
   int per_cu = 0;
   if (hydra::peer_occupancy(algo, op, dtype, acc32, &per_cu) != hipSuccess || per_cu < 1)
     per_cu = 1;
-  return std::max(1, p->cus * per_cu / p->colocated);
+  return std::max(1, p->group_cus * per_cu / p->colocated);
 }
 
 const hydra_peer::Reg* find_reg(const hydra_peer* p, const void* buf, size_t bytes) {
@@ -245,12 +250,27 @@ int hydra_peer_connect(hydra_peer_t p, const void* sig_handles) {
   if (!p || !sig_handles) return fail(HYDRA_ERR_INVALID, "null argument");
   hydra::DeviceScope ds_(p->device);  // IPC mappings and drains on the group's device
   const char* h = static_cast<const char*>(sig_handles);
-  int colocated = 1;
+  // every rank sees the same blobs: the busiest GPU's rank count and the smallest CU count
+  // decide the co-resident grid alike everywhere (a rank with a GPU of its own in a group
+  // where others share one must still launch the same grid: workgroup b meets workgroup b)
+  int colocated = 1, group_cus = p->cus;
+  for (int q = 0; q < p->P; q++) {
+    Blob bq;
+    int rc = parse_blob(h + (size_t)q * HYDRA_PEER_HANDLE_BYTES, q, &bq);
+    if (rc) return rc;
+    int same = 0;
+    for (int j = 0; j < p->P; j++) {
+      Blob bj;
+      std::memcpy(&bj, h + (size_t)j * HYDRA_PEER_HANDLE_BYTES, sizeof(Blob));
+      if (std::memcmp(bj.pci, bq.pci, sizeof(bq.pci)) == 0) same++;
+    }
+    colocated = std::max(colocated, same);
+    if (bq.cus > 0) group_cus = std::min(group_cus, (int)bq.cus);
+  }
   for (int q = 0; q < p->P; q++) {
     Blob b;
     int rc = parse_blob(h + (size_t)q * HYDRA_PEER_HANDLE_BYTES, q, &b);
     if (rc) return rc;
-    if (q != p->rank && std::memcmp(b.pci, p->pci, sizeof(p->pci)) == 0) colocated++;
     if (q == p->rank || p->sigs.p[q]) continue;
     std::string key;
     char* base = nullptr;
@@ -259,6 +279,7 @@ int hydra_peer_connect(hydra_peer_t p, const void* sig_handles) {
     p->sigs.p[q] = reinterpret_cast<hydra::PeerSignals*>(base + b.offset);
   }
   p->colocated = colocated;
+  p->group_cus = group_cus;
   return ok();
 }
 

@@ -501,8 +501,8 @@ int hydra_reduce_root_simulate(int root, int op, int dtype, int flags, int P, vo
  * hydra_peer_error; later calls on the group fail with HYDRA_ERR_HIP.  1 <= nranks <= 8.
  * Ranks of one group on the same GPU (each rank's GPU travels in its signal handle) must have
  * every rank's whole grid resident at once: an explicit HYDRA_PEER_OPT_BLOCKS beyond the GPU's
- * capacity / (ranks on it) is refused with HYDRA_ERR_INVALID, and the derived grid shrinks to
- * fit. */
+ * capacity / (the most ranks of the group on one GPU) is refused with HYDRA_ERR_INVALID, and the
+ * derived grid shrinks to fit -- the same grid on every rank of the group. */
 #define HYDRA_PEER_HANDLE_BYTES 128
 typedef enum {
   HYDRA_PEER_AUTO = 0,
