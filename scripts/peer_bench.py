@@ -9,6 +9,7 @@ HBM bytes per allreduce, all ranks together (they share one HBM):
           = (P + 1 + 2(P-1)) n E
   one-shot: P x [ P reads of n + 1 write of n (scratch) + n read + n write (copy back) ] x E
           = P (P + 3) n E
+  push (peer2w): P x [ P reads + P writes of n/P ] x E = 2 P n E
 
 Usage: python scripts/peer_bench.py [--P 2 --n 16777216 --iters 50]   (spawns the ranks)
 """
@@ -127,7 +128,8 @@ def main():
         n = int(n)
         ms = max(r[key]["wall_ms"] for r in res)
         ev = max(r[key]["event_ms"] for r in res)
-        hbm = (a.P + 1 + 2 * (a.P - 1)) * n * 4 if algo == "peer2" else a.P * (a.P + 3) * n * 4
+        hbm = {"peer2": (a.P + 1 + 2 * (a.P - 1)) * n * 4, "peer2w": 2 * a.P * n * 4}.get(
+            algo, a.P * (a.P + 3) * n * 4)
         summary[key] = {"ms": round(ms, 4), "event_ms": round(ev, 4),
                         "hbm_bytes": hbm, "hbm_GBps": round(hbm / (ev * 1e-3) / 1e9, 1),
                         "algbw_GBps": round(n * 4 / (ev * 1e-3) / 1e9, 1),
