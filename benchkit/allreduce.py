@@ -265,7 +265,7 @@ def bench_allreduce(args, dev, make_comm=None, sync=None, cpu_baseline=None,
 
     rank, world = dist.get_rank(), dist.get_world_size()
     # a hung collective must fail the run, not stall it: hard exit (status 3) after `watchdog_s`,
-    # printing the measured headline flagged when there is one (hydra_amd/watchdog.py)
+    # printing the measured headline flagged when there is one (benchkit/watchdog.py)
     from . import watchdog
 
     state = {}  # "result": builds the JSON line once the headline measurement is complete

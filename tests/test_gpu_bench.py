@@ -1,4 +1,4 @@
-"""bench.py's N>1 path (hydra_amd/ring.py bench_allreduce) at world size 1 on the GPU: the same
+"""bench.py's N>1 path (benchkit/allreduce.py bench_allreduce) at world size 1 on the GPU: the same
 code the driver's multi-GPU scale run executes per rank -- RCCL communicators, the fold-order
 parity self-check of every schedule, the full-size exactness check, the autotune and the
 context phase -- must finish with rc 0 and a JSON line whose parity entries are all bit-exact

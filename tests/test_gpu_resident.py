@@ -137,6 +137,42 @@ def _with_opts(code, opts):
     return pre + code
 
 
+def test_resident_per_context_options(gpu, O):
+    """hydra_ctx_set_option (round 6): one context turns the resident reducer off (its slot is
+    returned; every round becomes one launch on its stream) and cuts staged calls into more
+    rounds, while a second context keeps the process-wide defaults -- same bits on both; the
+    option comes back on for the first and it is served resident again.  Invalid keys / values
+    are refused."""
+    L = _lib.lib()
+    a_ctx, b_ctx = HostContext(0), HostContext(0)
+    try:
+        a_ctx.set_option(_lib.OPT_RESIDENT, 0)
+        a_ctx.set_option(_lib.OPT_STAGE_SPLIT, 16)
+        for k, (c, n) in enumerate(((a_ctx, 3000), (b_ctx, 3000), (a_ctx, 2_000_003),
+                                    (b_ctx, 2_000_003))):
+            s0 = c.stats()
+            x, y = synth.stress_f32(2, 0, n, seed=k), synth.stress_f32(2, 1, n, seed=k)
+            e = O.op(x, y, "sum", 6)
+            _lib.check(L.hydra_reduce_host(c.handle, 0, 6, x.ctypes.data, x.ctypes.data,
+                                           y.ctypes.data, n))
+            assert np.array_equal(bits(x), bits(e)), (k, n)
+            served = c.stats()["resident_calls"] - s0["resident_calls"]
+            assert (served == 0) if c is a_ctx else (served > 0), (k, served)
+        a_ctx.set_option(_lib.OPT_RESIDENT, 1)  # leases a slot again
+        s0 = a_ctx.stats()
+        x, y = synth.stress_f32(2, 0, 5000), synth.stress_f32(2, 1, 5000)
+        _lib.check(L.hydra_reduce_host(a_ctx.handle, 0, 6, x.ctypes.data, x.ctypes.data,
+                                       y.ctypes.data, 5000))
+        assert a_ctx.stats()["resident_calls"] > s0["resident_calls"]
+        with pytest.raises(_lib.HydraError):
+            a_ctx.set_option(_lib.OPT_COPY_THREADS, 2)  # process-wide only
+        with pytest.raises(_lib.HydraError):
+            a_ctx.set_option(_lib.OPT_STAGE_SPLIT, 0)
+    finally:
+        a_ctx.close()
+        b_ctx.close()
+
+
 def test_resident_off_by_option(gpu):
     """HYDRA_OPT_RESIDENT = 0 (process-wide): every call is one batched launch on the context's
     stream; same bits."""

@@ -1,4 +1,4 @@
-"""bench.py --gpus N watchdog (hydra_amd/watchdog.py): a hang after the headline still prints the
+"""bench.py --gpus N watchdog (benchkit/watchdog.py): a hang after the headline still prints the
 measured line, flagged, but the process exits non-zero; a hang before it exits non-zero with no
 line.  A hung GPU process must never read as rc 0 to the driver."""
 import json
