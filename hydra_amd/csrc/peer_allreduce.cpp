@@ -358,9 +358,12 @@ int hydra_peer_set_option(hydra_peer_t p, int key, long long value) {
     case HYDRA_PEER_OPT_BLOCKS: {
       if (value < 0 || value > hydra::kPeerMaxBlocks)
         return fail(HYDRA_ERR_INVALID, "blocks out of range");
-      // ranks sharing this GPU: refuse a grid they cannot all hold at once (checked again for
-      // the kernel each call launches) instead of a barrier timeout later
-      const int cap = colocated_cap(p, hydra::kPeerTwoShot, HYDRA_SUM, HYDRA_FLOAT32, false);
+      // ranks sharing this GPU: refuse a grid that none of the schedules' kernels could hold
+      // at once on it (each call checks again for the kernel it launches) instead of a barrier
+      // timeout later
+      int cap = 0;
+      for (int k : {hydra::kPeerTwoShotPush, hydra::kPeerTwoShot, hydra::kPeerOneShot})
+        cap = std::max(cap, colocated_cap(p, k, HYDRA_SUM, HYDRA_FLOAT32, false));
       if (cap && value > cap)
         return fail(HYDRA_ERR_INVALID,
                     "blocks " + std::to_string(value) + " x " + std::to_string(p->colocated) +

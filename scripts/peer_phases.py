@@ -18,7 +18,10 @@ the kernel span give the proxy's overall fraction of HBM (peer_bench.py's 0.49 /
 Usage (parent: touches no GPU; every rank is a child process):
   python scripts/peer_phases.py --P 2 --n 67108864 [--iters 20] [--rocprof DIR]
 --rocprof DIR wraps every rank in `rocprofv3 --kernel-trace --stats -d DIR/rank<r> --`, so the
-kernel trace's average duration can be set beside the clocks.  Prints one JSON document.
+kernel trace's average duration can be set beside the clocks; --pmc COUNTER (with --rocprof DIR)
+collects one counter per dispatch instead (FETCH_SIZE or WRITE_SIZE, one pass each: the TCC
+counters are device-wide, so each rank's dispatch counts every rank's traffic while their
+kernels overlap).  Prints one JSON document.
 """
 import argparse
 import json
@@ -150,6 +153,7 @@ def main():
     ap.add_argument("--blocks", type=int, default=0)
     ap.add_argument("--algo", default="peer2", choices=["peer2", "peer2w"])
     ap.add_argument("--rocprof", default="")
+    ap.add_argument("--pmc", default="")
     ap.add_argument("--rank", type=int, default=-1)
     ap.add_argument("--port", type=int, default=0)
     a = ap.parse_args()
@@ -166,7 +170,8 @@ def main():
                str(a.warmup), "--blocks", str(a.blocks), "--algo", a.algo]
         if a.rocprof:  # the profiler wraps the rank program itself (nothing in between)
             d = os.path.join(a.rocprof, f"rank{r}")
-            cmd = ["rocprofv3", "--kernel-trace", "--stats", "--output-format", "csv", "-d", d,
+            mode = ["--pmc", a.pmc] if a.pmc else ["--kernel-trace", "--stats"]
+            cmd = ["rocprofv3", *mode, "--output-format", "csv", "-d", d,
                    "-o", f"rank{r}", "--"] + cmd
         procs.append(subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
     res = []
