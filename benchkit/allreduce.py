@@ -574,6 +574,7 @@ def bench_allreduce(args, dev, make_comm=None, sync=None, cpu_baseline=None,
             others["reduce_root0"] = context_leg(rstep, k)
 
         # 5) BASELINE config 5: bf16 bucket of 256 Mi elements, fp32 accumulation
+        c5_ref = {}  # its gated DIRECT bucket, for the peer leg's config-5 schedule (7)
         if not getattr(args, "no_config5", False):
             n5 = int(getattr(args, "config5_elements", 256 << 20))
             # fold-order-sensitive bf16 values (+-2^k pivots that cancel: the one bf16 rounding
@@ -602,6 +603,8 @@ def bench_allreduce(args, dev, make_comm=None, sync=None, cpu_baseline=None,
             else:
                 g5 = _full_size_gate(xb, world, n5, synth.stress_cancel_at, 2, dev)
                 full_ok["config5_bf16_acc32"] = g5["ok"]
+                if g5["ok"]:  # the gated bucket: the peer leg's config-5 schedule must equal it
+                    c5_ref.update(n5=n5, ref=xb.clone(), k5=k5)
                 r5 = context_leg(bstep, k5, warm=2)
                 if not isinstance(r5, str):
                     profile_step("config5", c5_algo, xb, chunk if c5_algo == "direct" else 0, 2,
@@ -614,6 +617,7 @@ def bench_allreduce(args, dev, make_comm=None, sync=None, cpu_baseline=None,
                           "algo": c5_algo, "ms": r5, "algbw_GBps": round(b_alg, 2),
                           "busbw_GBps": round(b_alg * 2 * (world - 1) / world, 2),
                           "full_size_gate": g5}
+                    c5_ref["rccl_ms"] = r5
             state["result"] = lambda: _result(ms, lat_ms, others, c5)
             del xb
         # 6) two rails (bew_allreduce_a, calculateElements_AA, DIRECT on each): the only leg in
@@ -655,7 +659,8 @@ def bench_allreduce(args, dev, make_comm=None, sync=None, cpu_baseline=None,
             peer_leg["shared_gpu_workgroup_cap"] = shared_cap
         if peer_leg["enabled"]:
             pr = _peer_leg(make_peer, pg, run, measure, sync, dev, rank, world, xs, exp, x, x0,
-                           ref, gate, tp, peer_leg)
+                           ref, gate, tp, peer_leg, c5_ref)
+            c5_ref.clear()
             peer_leg["headline_ms"] = round(ms, 4)
             # promoted only when bit-exact with this run's DIRECT bucket at full size on the
             # order-sensitive data (the gate) and faster
@@ -756,7 +761,7 @@ def _peer_eligibility(args, comm_seen, world, dev) -> dict:
 
 
 def _peer_leg(make_peer, pg, run, measure, sync, dev, rank, world, xs, exp, x, x0, ref, gate, tp,
-              leg):
+              leg, c5_ref=None):
     """The peer leg's steps, each agreed over the ranks before the next: set up the IPC group,
     register the two buckets, parity of both schedules on the fold-order stress bucket, exactness
     at full size, a workgroup-count autotune, the timed region (bench.py's contract: exactly
@@ -880,6 +885,9 @@ def _peer_leg(make_peer, pg, run, measure, sync, dev, rank, world, xs, exp, x, x
             return None
         leg.update(algo=algo, workgroups=wg, ms_per_step=round(ms_p, 4), latency_ms=lat_p)
         leg["phases"] = _peer_phases(run, sync, dev, x, wg, world, algo)
+        if c5_ref and c5_ref.get("ref") is not None:  # config 5 through the same schedule
+            leg["config5"] = _peer_config5(pg, run, guarded, failed, sync, dev, rank, world,
+                                           algo, wg, c5_ref, agreed, peer_ok)
         return algo, wg, ms_p, lat_p
     finally:
         p, pg["peer"] = pg["peer"], None
@@ -888,6 +896,62 @@ def _peer_leg(make_peer, pg, run, measure, sync, dev, rank, world, xs, exp, x, x
                 p.close()
             except Exception as e:  # a teardown failure is reported, after every rank closed
                 leg.setdefault("error", f"teardown: {e}")
+
+
+def _peer_config5(pg, run, guarded, failed, sync, dev, rank, world, algo, wg, c5, agreed,
+                  peer_ok) -> dict:
+    """BASELINE config 5 (bf16, fp32 accumulation) through the peer leg's schedule: a fresh
+    bucket of the same stress_cancel_at values, registered, allreduced once and compared bit
+    for bit with the config-5 leg's gated DIRECT bucket on every rank; only then timed (k5
+    allreduces, barrier + sync on both sides, max over ranks).  Every step agreed over the
+    ranks; a failure becomes this entry's error."""
+    import torch
+    import torch.distributed as dist
+
+    from hydra_amd import synth
+
+    n5, kw = c5["n5"], dict(dtype_code=_lib.BFLOAT16, flags=_lib.ACC_F32)
+    out = {"algo": algo, "workgroups": wg, "elements": n5,
+           "gate": "equal to this run's config-5 DIRECT bucket (synth.stress_cancel_at), every rank"}
+    err, t5 = None, None
+    try:
+        t5 = synth.fill_at(synth.stress_cancel_at, world, rank, n5, dev,
+                           torch.bfloat16).view(torch.int16)
+    except Exception as e:
+        err = str(e)
+    if not agreed(err):
+        return dict(out, error=f"inputs: {err or 'another rank failed'}")
+    try:
+        pg["peer"].register(t5)  # collective
+    except Exception as e:
+        err = str(e)
+    if not agreed(err):
+        return dict(out, error=f"register: {err or 'another rank failed'}")
+    good = False
+    try:
+        run(algo, t5, wg, **kw)
+        sync()
+        good = bool(torch.equal(t5, c5["ref"]))
+    except Exception as e:
+        err = str(e)
+    if not agreed(err) or not peer_ok():
+        return dict(out, error=f"full size: {err or 'a barrier expired or another rank failed'}")
+    out["full_size_exact"] = max_over_ranks(0.0 if good else 1.0, dev) == 0.0
+    if not out["full_size_exact"]:
+        return out
+    tw = None
+    try:
+        tw = max_over_ranks(timed_steps(lambda: guarded(algo, t5, wg, **kw), c5["k5"], 2, sync,
+                                        dist.barrier), dev) / c5["k5"]
+    except Exception as e:
+        err = str(e)
+    err = err or (failed[0] if failed else None)
+    if not agreed(err) or not peer_ok():
+        return dict(out, error=f"timed: {err or 'a barrier expired or another rank failed'}")
+    b_alg = 2.0 * n5 / tw / 1e9
+    out.update(ms=round(tw * 1e3, 4), algbw_GBps=round(b_alg, 2),
+               busbw_GBps=round(b_alg * 2 * (world - 1) / world, 2), rccl_ms=c5.get("rccl_ms"))
+    return out
 
 
 def _peer_phases(run, sync, dev, x, wg, world, algo="peer2") -> dict:
@@ -987,7 +1051,8 @@ def _bench_result(n, world, args, chosen, chunk, tuning, parity, full_ok, ms, la
         "other_algos_busbw_GBps": {a: round(bucket / (v * 1e-3) / 1e9 * 2 * (world - 1) / world, 2)
                                    for a, v in others.items()
                                    if isinstance(v, float) and a != "reduce_root0"},
-        "config5_bf16": (dict(c5, phases=(phases or {}).get("config5"))
+        "config5_bf16": (dict(c5, phases=(phases or {}).get("config5"),
+                              peer=(peer_leg or {}).get("config5"))
                          if isinstance(c5, dict) else c5),
         "parity": {"fold_order_1M": parity, "full_size_exact": full_ok,
                    "full_size_gate": gate},

@@ -255,6 +255,10 @@ def test_bench_peer_leg_orchestration(world):
         2 * (world - 1) / world * (1 << 16) * 4), ph
     assert ph["link"]["peers"] == world - 1 and ph["fold"]["frac_of_hbm"] > 0, ph
     assert pl["full_size_gate"].startswith("equal to this run's DIRECT bucket"), pl
+    # config 5 through the peer schedule too: gated against config 5's DIRECT bucket, timed
+    p5 = pl["config5"]
+    assert p5["full_size_exact"] is True and p5["ms"] > 0 and p5["algo"] == pl["algo"], p5
+    assert res["config5_bf16"]["peer"] == p5, res["config5_bf16"]
     if pl["promoted"]:
         a = pl["algo"]
         assert res["config"]["algo"] == a and res["ms_per_step"] == pl["ms_per_step"]

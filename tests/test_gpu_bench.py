@@ -90,6 +90,11 @@ def test_bench_rehearsal_world2_peer_leg(gpu):
     assert pl["full_size_exact"] is True and pl["ms_per_step"] > 0, pl
     assert pl["full_size_exact_by_algo"] == {"peer2w": True, "peer2": True}, pl
     assert pl["phases"]["kernel_ms"] > 0 and pl["phases"]["link"]["peers"] == 1, pl
+    # BASELINE config 5 (bf16, fp32 accumulate) through the chosen peer schedule, gated against
+    # the config-5 DIRECT bucket before it is timed
+    p5 = pl["config5"]
+    assert "error" not in p5 and p5["full_size_exact"] is True and p5["ms"] > 0, p5
+    assert res["config5_bf16"]["peer"] == p5, res["config5_bf16"]
     if pl["promoted"]:
         assert res["config"]["algo"] == pl["algo"] in ("peer2", "peer2w"), res["config"]
 
