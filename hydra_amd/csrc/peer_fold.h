@@ -19,7 +19,8 @@ namespace {
 // Measurement variants (libhydra_measure.so only: hydra_set_variant 2001..2007 and the phase
 // clocks of hydra_measure_peer_stamps, f32 sum; 0 = the shipped kernel): bit 0 nontemporal
 // loads, bit 1 nontemporal stores, bit 2 twice the loads in flight, bit 3 phase clocks, bit 4
-// the 1-3-source folds as deep as the others.
+// the 1-3-source folds as deep as the others, bit 5 the push's slabs handed out by a ticket
+// counter instead of k = b mod G.
 template <int V>
 __device__ __forceinline__ u32x4 pld(const char* p) {
   if constexpr ((V & 1) != 0) return ld<kNT>(p, rsrc<kNT>(nullptr, 0), 0);
@@ -302,7 +303,7 @@ __global__ __launch_bounds__(kBlock) void k_peer_push(PeerLaunch A) {
   if (!peer_barrier(Y, 1)) return;  // every rank's bucket is ready
   stamp<V>(A, 1);
   const size_t lo = A.lo[r], hi = A.lo[r + 1];
-  for (size_t k = blockIdx.x; lo + k * SL < hi; k += G) {
+  auto fold_slab = [&](size_t k) {
     const size_t s = lo + k * SL;
     PeerSrcs S;
     PeerDsts D;
@@ -313,6 +314,35 @@ __global__ __launch_bounds__(kBlock) void k_peer_push(PeerLaunch A) {
         D.p[j] = A.x[(r + j) % P] + s * sizeof(E);  // D.p[0]: the local bucket
       }
     slab_fold<E, OP, ACC32, V, true>(D, S, P, hi - s < SL ? hi - s : SL);
+  };
+  if constexpr ((V & 32) != 0) {
+    // Dynamic slabs: workgroup b takes slab b, then tickets G, G+1, ... from this rank's
+    // counter (drawn one slab ahead, so the atomic's round trip hides behind the fold), so a
+    // slow workgroup takes fewer slabs.  Barrier 2 stays per workgroup index: a rank's kernel
+    // ends only when every workgroup of it has met workgroup b of every peer there, i.e. after
+    // every peer workgroup finished whatever slabs it took.
+    __shared__ uint32_t next_s;
+    PeerSignals* own = Y.sig.p[r];
+    const size_t nsl = (hi - lo + SL - 1) / SL;
+    for (size_t k = blockIdx.x; k < nsl;) {
+      uint32_t nk = 0;
+      if (threadIdx.x == 0)
+        nk = G + __hip_atomic_fetch_add(&own->ticket, 1u, __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_SYSTEM);
+      fold_slab(k);
+      if (threadIdx.x == 0) next_s = nk;
+      __syncthreads();
+      k = next_s;
+      __syncthreads();
+    }
+    if (threadIdx.x == 0 &&  // the last workgroup out: every ticket of this call is drawn
+        __hip_atomic_fetch_add(&own->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) ==
+            G - 1) {
+      __hip_atomic_store(&own->ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&own->done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  } else {
+    for (size_t k = blockIdx.x; lo + k * SL < hi; k += G) fold_slab(k);
   }
   stamp<V>(A, 2);
   peer_barrier(Y, 2);

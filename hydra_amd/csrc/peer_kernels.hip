@@ -46,6 +46,7 @@ hipError_t launch_variant(int v, int algo, const PeerLaunch& A, unsigned grid, h
     case 6: return launch_t<float, kSum, false, 6>(algo, A, grid, s, occ);
     case 7: return launch_t<float, kSum, false, 7>(algo, A, grid, s, occ);
     case 16: return launch_t<float, kSum, false, 16>(algo, A, grid, s, occ);
+    case 32: return launch_t<float, kSum, false, 32>(algo, A, grid, s, occ);
   }
   return hipErrorInvalidValue;
 }
@@ -60,12 +61,13 @@ hipError_t launch_peer(int algo, int op, int dtype, bool acc32, const PeerLaunch
     return hipErrorInvalidValue;
 #ifdef HYDRA_MEASURE
   const int v = current_variant() - kPeerVariantBase;  // (measurement only)
-  if (((v >= 1 && v <= 7) || v == 16) && op == kSum && dtype == kF32 && !acc32)
-    return launch_variant(v, algo, A, grid, s);
-  if (A.stamps) {  // hydra_measure_peer_stamps: the shipped kernel plus its phase clocks
+  if (A.stamps) {  // hydra_measure_peer_stamps: the shipped kernel (or 32) plus phase clocks
     if (op != kSum || dtype != kF32 || acc32) return hipErrorInvalidValue;
+    if (v == 32) return launch_t<float, kSum, false, 40>(algo, A, grid, s);
     return launch_t<float, kSum, false, 8>(algo, A, grid, s);
   }
+  if (((v >= 1 && v <= 7) || v == 16 || v == 32) && op == kSum && dtype == kF32 && !acc32)
+    return launch_variant(v, algo, A, grid, s);
 #endif
   switch (op) {  // one translation unit per op (peer_kernels_<op>.hip)
     case kSum: return launch_peer_sum(algo, dtype, acc32, A, grid, s, nullptr);
@@ -80,7 +82,7 @@ hipError_t peer_occupancy(int algo, int op, int dtype, bool acc32, int* per_cu) 
   const PeerLaunch A{};
 #ifdef HYDRA_MEASURE  // a variant's own register count (the deeper ones hold fewer per CU)
   const int v = current_variant() - kPeerVariantBase;
-  if (((v >= 1 && v <= 7) || v == 16) && op == kSum && dtype == kF32 && !acc32)
+  if (((v >= 1 && v <= 7) || v == 16 || v == 32) && op == kSum && dtype == kF32 && !acc32)
     return launch_variant(v, algo, A, 1, nullptr, per_cu);
 #endif
   switch (op) {

@@ -31,6 +31,9 @@ constexpr uint32_t kPeerErrAborted = 5;
 struct PeerSignals {
   uint32_t flag[kPeerMaxBlocks][kPeerMaxRanks];  // flag[block][source rank] = last epoch seen
   uint32_t abort;                                // non-zero: some rank gave up (its code)
+  // (push with dynamic slabs) this rank's slab tickets and finished workgroups of the running
+  // call; the last workgroup out zeroes both for the next call
+  uint32_t ticket, done;
 };
 
 struct PeerSigPtrs {

@@ -19,11 +19,12 @@ extern "C" {
  *              LDS-DMA double buffering (13, 18), wave-shuffle tail (44), persistent (45-47)
  *   1..7       hydra_fold (the DIRECT / A2A owner fold): load policy, grid cap, XCD map
  *   2001..2007 hydra_peer_allreduce (fp32 sum): nontemporal loads / stores, deeper pipelining;
- *   2016       the same with the 1-3-source folds as deep as the others */
+ *   2016       the same with the 1-3-source folds as deep as the others;
+ *   2032       the push schedule's slabs handed out by a ticket counter (dynamic balance) */
 int hydra_set_variant(int variant);
 
 /* Phase clocks of the peer-access allreduce (fp32 sum only while set): every later
- * hydra_peer_allreduce on `peer` runs the shipped kernel plus, per workgroup b, kPeerStamps = 6
+ * hydra_peer_allreduce on `peer` runs the shipped kernel (or variant 2032's) plus, per workgroup b, kPeerStamps = 6
  * s_memrealtime values (100 MHz) written to dev_buf[6 b + k]: kernel entry, after barrier 1,
  * end of the fold phase, after barrier 2, end of the copy phase, after barrier 3.  dev_buf
  * holds max_workgroups x 6 uint64 (device memory); a larger grid is refused.  NULL: off. */

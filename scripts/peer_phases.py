@@ -48,6 +48,9 @@ def worker(a):
     _lib.select_measure()  # the phase clocks exist in libhydra_measure.so only
     from hydra_amd.peer import PeerComm
 
+    if a.variant:  # a measurement variant's kernel (2032: the push with dynamic slabs)
+        _lib.lib().hydra_set_variant(a.variant)
+
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(a.port)
     dist.init_process_group("gloo", rank=a.rank, world_size=a.P)
@@ -152,6 +155,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--blocks", type=int, default=0)
     ap.add_argument("--algo", default="peer2", choices=["peer2", "peer2w"])
+    ap.add_argument("--variant", type=int, default=0)
     ap.add_argument("--rocprof", default="")
     ap.add_argument("--pmc", default="")
     ap.add_argument("--rank", type=int, default=-1)
@@ -167,7 +171,7 @@ def main():
     for r in range(a.P):
         cmd = ["python3", "-u", os.path.abspath(__file__), "--rank", str(r), "--port", str(port),
                "--P", str(a.P), "--n", str(a.n), "--iters", str(a.iters), "--warmup",
-               str(a.warmup), "--blocks", str(a.blocks), "--algo", a.algo]
+               str(a.warmup), "--blocks", str(a.blocks), "--algo", a.algo, "--variant", str(a.variant)]
         if a.rocprof:  # the profiler wraps the rank program itself (nothing in between)
             d = os.path.join(a.rocprof, f"rank{r}")
             mode = ["--pmc", a.pmc] if a.pmc else ["--kernel-trace", "--stats"]
@@ -182,7 +186,9 @@ def main():
             print(o[-3000:], file=sys.stderr)
             raise SystemExit(p.returncode)
         res.append(json.loads([ln for ln in o.splitlines() if ln.startswith("RESULT ")][-1][7:]))
-    print(json.dumps(summarize(a.P, a.n, res, a.algo)), flush=True)
+    out = summarize(a.P, a.n, res, a.algo)
+    out["variant"] = a.variant
+    print(json.dumps(out), flush=True)
 
 
 if __name__ == "__main__":
