@@ -68,7 +68,7 @@ def _worker(rank, world, port, q, stall_rank=-1, stall_waits=0, extra_legs=False
             self.comm, self.closed = GlooPlanComm(O), False
             self.registered = []
             self.calls, self.err = 0, 0
-            if peer_fail_at >= 0:  # the device group's bounded barriers: a gloo group whose
+            if peer_fail_at != -1:  # the device group's bounded barriers: a gloo group whose
                 # collectives time out when a peer never arrives (then the group is poisoned)
                 from datetime import timedelta
 
@@ -85,13 +85,22 @@ def _worker(rank, world, port, q, stall_rank=-1, stall_waits=0, extra_legs=False
             from hydra_amd._lib import HydraError
 
             self.calls += 1
-            if peer_fail_at < 0:
+            bf16 = kw.get("dtype_code") is not None
+            if peer_fail_at == -1 or (peer_fail_at == -2 and not bf16):
                 self.comm.allreduce_(t, algo="direct", **kw)
                 return
             if self.err:  # a poisoned group refuses at once (hydra_peer_allreduce)
                 raise HydraError(3, "peer group is broken: an earlier barrier timed out")
-            if rank == 1 and peer_fail_at < self.calls:  # this rank's call fails locally
+            if rank == 1 and (peer_fail_at == -2 or peer_fail_at < self.calls):
+                # this rank's call fails locally (-2: its first config-5 call)
                 raise HydraError(1, f"injected failure at peer call {self.calls}")
+            if bf16:  # (-2) the other rank's call: its barrier waits for rank 1, and expires
+                try:
+                    dist.all_gather([torch.empty_like(t) for _ in range(world)], t,
+                                    group=self.group)
+                except RuntimeError:
+                    self.err = 1
+                return
             got = [torch.empty_like(t) for _ in range(world)]
             try:  # every rank's bucket, then the reference fold (the peer kernel's result)
                 dist.all_gather(got, t, group=self.group)
@@ -288,6 +297,22 @@ def test_bench_peer_leg_one_rank_fails_mid_loop(fail_at, stage):
         assert pl.get("error", "").startswith(stage) and not pl.get("promoted"), pl
         assert res["config"]["algo"] != "peer2" and res["value"] > 0, res["config"]
     assert "injected failure" in out[1][0]["peer_leg"]["error"], out[1][0]["peer_leg"]
+
+
+def test_bench_peer_leg_config5_fails_on_one_rank():
+    """Config 5 through the peer schedule fails on ONE rank (its first bf16 call, the gate): the
+    other rank's call ends at its bounded barrier, both record the error in the config-5 entry,
+    and the config-4 peer result -- gated and timed before -- stands."""
+    out = _start(2, peer="on", peer_fail_at=-2)
+    for r, (res, closed) in out.items():
+        assert isinstance(res, dict), res
+        assert closed, f"rank {r} left a communicator or peer group open"
+        pl = res["peer_leg"]
+        assert "error" not in pl and pl["full_size_exact"] and pl["ms_per_step"] > 0, pl
+        p5 = pl["config5"]
+        assert p5["error"].startswith("full size") and "ms" not in p5, p5
+        assert res["config5_bf16"]["peer"] == p5 and res["config5_bf16"]["ms"] > 0
+    assert "injected failure" in out[1][0]["peer_leg"]["config5"]["error"]
 
 
 def test_bench_allreduce_extra_legs():
