@@ -20,7 +20,9 @@ namespace {
 // clocks of hydra_measure_peer_stamps, f32 sum; 0 = the shipped kernel): bit 0 nontemporal
 // loads, bit 1 nontemporal stores, bit 2 twice the loads in flight, bit 3 phase clocks, bit 4
 // the 1-3-source folds as deep as the others, bit 5 the push's slabs handed out by a ticket
-// counter instead of k = b mod G.
+// counter instead of k = b mod G, bit 6 barrier 1 WITH a release fence (the kernel before
+// r06u), bit 7 barrier 1 with an agent-scope acquire, bit 8 the entry check reading the
+// host-mapped error word too (the kernel before r06w).
 template <int V>
 __device__ __forceinline__ u32x4 pld(const char* p) {
   if constexpr ((V & 1) != 0) return ld<kNT>(p, rsrc<kNT>(nullptr, 0), 0);
@@ -219,10 +221,23 @@ __device__ __forceinline__ void slab_copy(char* dst, const char* src, size_t cou
   }
 }
 
+// Barrier 1 (every rank's bucket is ready) publishes nothing this kernel wrote: the buckets
+// were produced before the kernel started, by stream-ordered work whose completion already put
+// them in memory (a kernel's end-of-kernel release writes its XCD L2s back -- the L2s of one
+// GPU are not coherent with each other, so that writeback is what makes any kernel's output
+// readable by the next kernel's other XCDs, and by a peer GPU reading this HBM over xGMI; a
+// copy engine writes memory directly).  So its signal carries no release fence: 512 workgroups
+// each writing their XCD's L2 back cost 13 us of the 36 us barrier at P = 2 (profiles/r06u).
+// The acquire stays (a peer's bucket may sit stale in this GPU's caches).  Barriers 2 and 3
+// publish this kernel's stores and keep the release.
+template <int V>
+constexpr bool kStartRelease = (V & 64) != 0;
+
 // The group already failed (an earlier timeout here or on a peer): leave at once.
+template <int V>
 __device__ __forceinline__ bool group_broken(const PeerSync& S) {
   int bad = 0;
-  if (threadIdx.x == 0 && peer_aborted(S)) {
+  if (threadIdx.x == 0 && peer_aborted(S, (V & 256) != 0)) {
     if (peer_ld(S.err) == 0) peer_st(S.err, kPeerErrAborted);
     bad = 1;
   }
@@ -246,8 +261,8 @@ __global__ __launch_bounds__(kBlock) void k_peer_two_shot(PeerLaunch A) {
   const int P = Y.P, r = Y.rank;
   const uint32_t G = gridDim.x;
   stamp<V>(A, 0);
-  if (group_broken(Y)) return;
-  if (!peer_barrier(Y, 1)) return;  // every rank's bucket is ready
+  if (group_broken<V>(Y)) return;
+  if (!peer_barrier(Y, 1, kStartRelease<V>, (V & 128) == 0)) return;  // every bucket is ready
   stamp<V>(A, 1);
   PeerSrcs S;
   // phase 1: own block r, slabs k = b, b+G, ...; all P sources, in place
@@ -299,8 +314,8 @@ __global__ __launch_bounds__(kBlock) void k_peer_push(PeerLaunch A) {
   const int P = Y.P, r = Y.rank;
   const uint32_t G = gridDim.x;
   stamp<V>(A, 0);
-  if (group_broken(Y)) return;
-  if (!peer_barrier(Y, 1)) return;  // every rank's bucket is ready
+  if (group_broken<V>(Y)) return;
+  if (!peer_barrier(Y, 1, kStartRelease<V>, (V & 128) == 0)) return;  // every bucket is ready
   stamp<V>(A, 1);
   const size_t lo = A.lo[r], hi = A.lo[r + 1];
   auto fold_slab = [&](size_t k) {
@@ -358,8 +373,8 @@ __global__ __launch_bounds__(kBlock) void k_peer_one_shot(PeerLaunch A) {
   const int P = Y.P, r = Y.rank;
   const uint32_t G = gridDim.x;
   stamp<V>(A, 0);
-  if (group_broken(Y)) return;
-  if (!peer_barrier(Y, 1)) return;
+  if (group_broken<V>(Y)) return;
+  if (!peer_barrier(Y, 1, kStartRelease<V>, (V & 128) == 0)) return;
   stamp<V>(A, 1);
   PeerSrcs S;
   // slab list over all owner blocks: (q, k) enumerated block by block; slab w -> workgroup w%G

@@ -19,7 +19,8 @@
 // Work unit: a slab (4-64 KiB, fixed per call from (P, n, dtype)) of one owner block.  Slab k of
 // every block is handled by workgroup k mod G on every rank (G identical on every rank), so
 // workgroup b only ever synchronises with workgroup b of the other ranks (peer_sync.h):
-//   start barrier: every rank's bucket is ready;
+//   start barrier: every rank's bucket is ready (no release fence: nothing this kernel stored
+//                  is published by it -- peer_fold.h kStartRelease);
 //   phase 1 -> 2 barrier: workgroup b's phase-1 slabs are final on every rank;
 //   end barrier (two-shot): nobody leaves while a peer may still read its bucket.
 // Every wait is bounded (timeout -> error word + abort broadcast), so the grid always drains.
@@ -47,6 +48,10 @@ hipError_t launch_variant(int v, int algo, const PeerLaunch& A, unsigned grid, h
     case 7: return launch_t<float, kSum, false, 7>(algo, A, grid, s, occ);
     case 16: return launch_t<float, kSum, false, 16>(algo, A, grid, s, occ);
     case 32: return launch_t<float, kSum, false, 32>(algo, A, grid, s, occ);
+    case 64: return launch_t<float, kSum, false, 64>(algo, A, grid, s, occ);
+    case 128: return launch_t<float, kSum, false, 128>(algo, A, grid, s, occ);
+    case 192: return launch_t<float, kSum, false, 192>(algo, A, grid, s, occ);
+    case 256: return launch_t<float, kSum, false, 256>(algo, A, grid, s, occ);
   }
   return hipErrorInvalidValue;
 }
@@ -64,9 +69,13 @@ hipError_t launch_peer(int algo, int op, int dtype, bool acc32, const PeerLaunch
   if (A.stamps) {  // hydra_measure_peer_stamps: the shipped kernel (or 32) plus phase clocks
     if (op != kSum || dtype != kF32 || acc32) return hipErrorInvalidValue;
     if (v == 32) return launch_t<float, kSum, false, 40>(algo, A, grid, s);
+    if (v == 64) return launch_t<float, kSum, false, 72>(algo, A, grid, s);
+    if (v == 128) return launch_t<float, kSum, false, 136>(algo, A, grid, s);
+    if (v == 192) return launch_t<float, kSum, false, 200>(algo, A, grid, s);
+    if (v == 256) return launch_t<float, kSum, false, 264>(algo, A, grid, s);
     return launch_t<float, kSum, false, 8>(algo, A, grid, s);
   }
-  if (((v >= 1 && v <= 7) || v == 16 || v == 32) && op == kSum && dtype == kF32 && !acc32)
+  if (((v >= 1 && v <= 7) || v == 16 || v == 32 || v == 64 || v == 128 || v == 192 || v == 256) && op == kSum && dtype == kF32 && !acc32)
     return launch_variant(v, algo, A, grid, s);
 #endif
   switch (op) {  // one translation unit per op (peer_kernels_<op>.hip)
@@ -82,7 +91,7 @@ hipError_t peer_occupancy(int algo, int op, int dtype, bool acc32, int* per_cu) 
   const PeerLaunch A{};
 #ifdef HYDRA_MEASURE  // a variant's own register count (the deeper ones hold fewer per CU)
   const int v = current_variant() - kPeerVariantBase;
-  if (((v >= 1 && v <= 7) || v == 16 || v == 32) && op == kSum && dtype == kF32 && !acc32)
+  if (((v >= 1 && v <= 7) || v == 16 || v == 32 || v == 64 || v == 128 || v == 192 || v == 256) && op == kSum && dtype == kF32 && !acc32)
     return launch_variant(v, algo, A, 1, nullptr, per_cu);
 #endif
   switch (op) {

@@ -57,9 +57,13 @@ __device__ __forceinline__ void peer_st(uint32_t* p, uint32_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// Is the group already broken?  (one lane; cheap: own uncached area + host word)
-__device__ __forceinline__ bool peer_aborted(const PeerSync& S) {
-  return peer_ld(&S.sig.p[S.rank]->abort) != 0 || peer_ld(S.err) != 0;
+// Is the group already broken?  (one lane.)  The own abort word alone answers it: every failure
+// writes it -- peer_fail stores the code into every rank's abort word, this rank's included --
+// and it is never cleared, so the host-mapped error word adds nothing but a read over PCIe,
+// which 512 workgroups issuing at once at kernel entry cost ~20 us per call (profiles/r06w).
+// (host = true: that read too -- the measurement variant of the kernel before r06w.)
+__device__ __forceinline__ bool peer_aborted(const PeerSync& S, bool host = false) {
+  return peer_ld(&S.sig.p[S.rank]->abort) != 0 || (host && peer_ld(S.err) != 0);
 }
 
 // Give up: record `code` here and tell every peer.
@@ -78,11 +82,14 @@ __device__ __forceinline__ uint32_t peer_next_epoch(const PeerSync& S) {
 
 // Release this workgroup's finished stores and publish `epoch` as flag[blockIdx.x][rank] in
 // every rank's signal area.  Call from all threads.
-__device__ __forceinline__ void peer_signal(const PeerSync& S, uint32_t epoch) {
+// (release = false: this workgroup has stored nothing a peer will read since the kernel
+// started -- the start barrier, peer_fold.h kStartRelease)
+__device__ __forceinline__ void peer_signal(const PeerSync& S, uint32_t epoch,
+                                            bool release = true) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x < 64) {  // wave 0
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope
+    if (release) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if ((int)threadIdx.x < S.P) peer_st(&S.sig.p[threadIdx.x]->flag[blockIdx.x][S.rank], epoch);
   }
@@ -90,7 +97,8 @@ __device__ __forceinline__ void peer_signal(const PeerSync& S, uint32_t epoch) {
 
 // Wait until every rank's workgroup blockIdx.x has published `epoch`, then acquire.  Returns
 // false (group broken) on timeout or abort; every wave still leaves, so the grid drains.
-__device__ __forceinline__ bool peer_wait(const PeerSync& S, uint32_t epoch, uint32_t code) {
+__device__ __forceinline__ bool peer_wait(const PeerSync& S, uint32_t epoch, uint32_t code,
+                                          bool sys_acquire = true) {
   int ok = 1;
   if (threadIdx.x < 64) {  // wave 0: lane q polls rank q's arrival
     const int q = threadIdx.x;
@@ -114,20 +122,23 @@ __device__ __forceinline__ bool peer_wait(const PeerSync& S, uint32_t epoch, uin
         }
       }
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope
+    if (sys_acquire) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope
+    else __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // (measurement variant only)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   return __syncthreads_and(ok) != 0;
 }
 
 // Workgroup-level barrier with the same workgroup index on every rank.
-__device__ __forceinline__ bool peer_barrier(const PeerSync& S, uint32_t code) {
+// release / sys_acquire: see peer_signal / peer_wait (both true but in measurement variants)
+__device__ __forceinline__ bool peer_barrier(const PeerSync& S, uint32_t code,
+                                             bool release = true, bool sys_acquire = true) {
   __shared__ uint32_t epoch_s;
   if (threadIdx.x == 0) epoch_s = peer_next_epoch(S);
   __syncthreads();
   const uint32_t epoch = epoch_s;
-  peer_signal(S, epoch);
-  return peer_wait(S, epoch, code);
+  peer_signal(S, epoch, release);
+  return peer_wait(S, epoch, code, sys_acquire);
 }
 
 }  // namespace hydra

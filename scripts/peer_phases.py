@@ -59,7 +59,9 @@ def worker(a):
     grid = a.blocks or max(1, 512 // a.P)  # every rank's grid resident at once on the one GPU
     peer = PeerComm(a.rank, a.P, 0, blocks=grid)
     L = _lib.lib()
-    stamps = torch.zeros(grid * _lib.PEER_STAMPS, dtype=torch.int64, device=dev)
+    per_call = grid * _lib.PEER_STAMPS
+    stamps = torch.zeros(per_call * (a.iters if a.back_to_back else 1), dtype=torch.int64,
+                         device=dev)
     out = {"calls": []}
     try:
         x = synth.fill_at(synth.stress_at, a.P, a.rank, a.n, dev, torch.float32)
@@ -77,8 +79,19 @@ def worker(a):
         e1.record(s)
         torch.cuda.synchronize(dev)
         out["event_ms_plain"] = e0.elapsed_time(e1) / a.iters
-        _lib.check(L.hydra_measure_peer_stamps(peer._h, ctypes.c_void_p(stamps.data_ptr()), grid))
-        for _ in range(a.iters):
+        if a.back_to_back:  # steady state: each call its own stamp slice, no host barrier between
+            dist.barrier()
+            for i in range(a.iters):
+                _lib.check(L.hydra_measure_peer_stamps(
+                    peer._h, ctypes.c_void_p(stamps.data_ptr() + i * per_call * 8), grid))
+                peer.allreduce_(x, algo=a.algo)
+            torch.cuda.synchronize(dev)
+            v = stamps.view(a.iters, grid, _lib.PEER_STAMPS).cpu().numpy()
+            out["calls"] = [v[i].tolist() for i in range(a.iters)]
+        else:
+            _lib.check(L.hydra_measure_peer_stamps(peer._h, ctypes.c_void_p(stamps.data_ptr()),
+                                                   grid))
+        for _ in range(0 if a.back_to_back else a.iters):
             dist.barrier()
             peer.allreduce_(x, algo=a.algo)
             torch.cuda.synchronize(dev)
@@ -119,6 +132,11 @@ def summarize(P, n, res, algo="peer2"):
             "rank_start_skew_us": float((t[:, :, 0].min(axis=1).max() -
                                          t[:, :, 0].min(axis=1).min()) * TICK_S * 1e6),
             "fold_window_us": fold_w * 1e6, "copy_window_us": copy_w * 1e6,
+            # within one rank: how far apart its workgroups start (t0) and leave barrier 1 (t1)
+            "wg_start_spread_us": float((t[:, :, 0].max(axis=1) - t[:, :, 0].min(axis=1)).max()
+                                        * TICK_S * 1e6),
+            "wg_barrier1_exit_spread_us": float((t[:, :, 1].max(axis=1) -
+                                                 t[:, :, 1].min(axis=1)).max() * TICK_S * 1e6),
             "fold_GBps": fold_bytes / fold_w / 1e9,
             "copy_GBps": copy_bytes / copy_w / 1e9 if copy_w > 0 else 0.0,
             "span_GBps": total_bytes / span / 1e9,
@@ -156,6 +174,8 @@ def main():
     ap.add_argument("--blocks", type=int, default=0)
     ap.add_argument("--algo", default="peer2", choices=["peer2", "peer2w"])
     ap.add_argument("--variant", type=int, default=0)
+    ap.add_argument("--back-to-back", action="store_true",
+                    help="stamped calls issued back to back (steady state), not after host barriers")
     ap.add_argument("--rocprof", default="")
     ap.add_argument("--pmc", default="")
     ap.add_argument("--rank", type=int, default=-1)
@@ -171,7 +191,7 @@ def main():
     for r in range(a.P):
         cmd = ["python3", "-u", os.path.abspath(__file__), "--rank", str(r), "--port", str(port),
                "--P", str(a.P), "--n", str(a.n), "--iters", str(a.iters), "--warmup",
-               str(a.warmup), "--blocks", str(a.blocks), "--algo", a.algo, "--variant", str(a.variant)]
+               str(a.warmup), "--blocks", str(a.blocks), "--algo", a.algo, "--variant", str(a.variant)] + (["--back-to-back"] if a.back_to_back else [])
         if a.rocprof:  # the profiler wraps the rank program itself (nothing in between)
             d = os.path.join(a.rocprof, f"rank{r}")
             mode = ["--pmc", a.pmc] if a.pmc else ["--kernel-trace", "--stats"]
@@ -188,6 +208,7 @@ def main():
         res.append(json.loads([ln for ln in o.splitlines() if ln.startswith("RESULT ")][-1][7:]))
     out = summarize(a.P, a.n, res, a.algo)
     out["variant"] = a.variant
+    out["stamped_calls"] = "back to back (steady state)" if a.back_to_back else "each after a host barrier"
     print(json.dumps(out), flush=True)
 
 
