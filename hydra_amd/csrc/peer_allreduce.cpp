@@ -72,7 +72,9 @@ struct hydra_peer {
   uint32_t* err_dev = nullptr;
   uint64_t timeout_ticks = 20ull * 100000000ull;  // 20 s at 100 MHz
   int blocks = 0;                                 // 0 = derived from the bucket
-  size_t one_shot_max = 256u << 10;               // AUTO: ONE_SHOT up to this many bytes
+  // AUTO: ONE_SHOT up to this many bytes -- 0 since round 6: the push is as fast or faster at
+  // every size measured, 1 KiB up (profiles/r06z), so ONE_SHOT is an explicit choice
+  size_t one_shot_max = 0;
   char* scratch = nullptr;
   size_t scratch_bytes = 0;
   struct Reg {

@@ -114,7 +114,7 @@ class PeerComm:
                    flags: int = 0, max_segment: int = 0, stream: int | None = None) -> None:
         """In-place allreduce of registered device tensor t on the current (or given) stream.
         algo: "peer2" (two-shot), "peer2w" (two-shot push: the fold stores into every bucket),
-        "peer1" (one-shot), "peer" (auto by size)."""
+        "peer1" (one-shot), "peer" (AUTO: the push, or one-shot up to PEER_OPT_ONE_SHOT_MAX bytes)."""
         import torch
 
         from .reduce import _torch_dtype_code

@@ -479,13 +479,13 @@ int hydra_reduce_root_simulate(int root, int op, int dtype, int flags, int P, vo
  *   HYDRA_PEER_TWO_SHOT  each rank folds its own block pulling from all P buckets (in place),
  *                        then pulls the other finished blocks (2(P-1)/P * n * E link bytes)
  *   HYDRA_PEER_ONE_SHOT  each rank folds the whole bucket into scratch, then copies it back
- *                        ((P-1) * n * E link bytes, 2 barriers: small buckets)
+ *                        ((P-1) * n * E link bytes, 2 barriers)
  *   HYDRA_PEER_TWO_SHOT_PUSH  each rank folds its own block pulling from all P buckets and
  *                        stores the result into EVERY bucket (its own in place, the peers' over
  *                        xGMI): no second pull, 2 barriers, the same link bytes as TWO_SHOT and
  *                        n * E read + n * E written per rank.  Needs every rank's bucket at the
  *                        same address modulo 16 (else it runs as TWO_SHOT, on every rank alike)
- *   HYDRA_PEER_AUTO      ONE_SHOT up to HYDRA_PEER_OPT_ONE_SHOT_MAX bytes (256 KiB), else
+ *   HYDRA_PEER_AUTO      ONE_SHOT up to HYDRA_PEER_OPT_ONE_SHOT_MAX bytes (default 0), else
  *                        TWO_SHOT_PUSH
  * Setup (every rank, same order; the byte blobs travel over any channel the caller has, e.g.
  * the rendezvous store): hydra_peer_create -> exchange sig handles -> hydra_peer_connect; for
@@ -513,7 +513,7 @@ typedef enum {
 typedef enum {
   HYDRA_PEER_OPT_TIMEOUT_MS = 1,  /* barrier timeout (default 20000) */
   HYDRA_PEER_OPT_BLOCKS = 2,      /* workgroups per launch (0 = derived from the bucket, <= 1024) */
-  HYDRA_PEER_OPT_ONE_SHOT_MAX = 3 /* AUTO threshold in bytes */
+  HYDRA_PEER_OPT_ONE_SHOT_MAX = 3 /* AUTO threshold in bytes (default 0: always the push) */
 } hydra_peer_opt_t;
 typedef struct hydra_peer* hydra_peer_t;
 /* sig_handle: HYDRA_PEER_HANDLE_BYTES out, to be gathered in rank order for hydra_peer_connect */
