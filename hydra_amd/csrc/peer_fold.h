@@ -7,6 +7,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "errors.h"
 #include "peer_kernels.h"
 #include "peer_sync.h"
@@ -22,7 +24,8 @@ namespace {
 // the 1-3-source folds as deep as the others, bit 5 the push's slabs handed out by a ticket
 // counter instead of k = b mod G, bit 6 barrier 1 WITH a release fence (the kernel before
 // r06u), bit 7 barrier 1 with an agent-scope acquire, bit 8 the entry check reading the
-// host-mapped error word too (the kernel before r06w).
+// host-mapped error word too (the kernel before r06w), bit 9 the push's stores plain and its
+// barrier 2 with the L2 writeback (the kernel before r06zc).
 template <int V>
 __device__ __forceinline__ u32x4 pld(const char* p) {
   if constexpr ((V & 1) != 0) return ld<kNT>(p, rsrc<kNT>(nullptr, 0), 0);
@@ -32,6 +35,24 @@ template <int V>
 __device__ __forceinline__ void pst(char* p, u32x4 v) {
   if constexpr ((V & 2) != 0) st<kNT>(p, rsrc<kNT>(nullptr, 0), 0, v);
   else st_a(p, v);
+}
+
+// SYS: system-coherent stores (sc0 sc1: written through to memory, the line dropped from L2) --
+// the push's, so its barrier 2 needs no L2 writeback before the flag: the stores are complete
+// once `s_waitcnt vmcnt(0)` returns (profiles/r06zc: barrier 2 21 -> 11 us at P = 2, the push
+// 11-30 % faster there, 2-10 % at P = 8).  The element form:
+template <bool SYS, typename E>
+__device__ __forceinline__ void est(E* p, E v) {
+  if constexpr (SYS) {
+    using U = std::conditional_t<sizeof(E) == 1, uint8_t,
+              std::conditional_t<sizeof(E) == 2, uint16_t,
+              std::conditional_t<sizeof(E) == 4, uint32_t, uint64_t>>>;
+    U b;
+    __builtin_memcpy(&b, &v, sizeof(E));
+    __hip_atomic_store(reinterpret_cast<U*>(p), b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  } else {
+    *p = v;
+  }
 }
 
 // dst = fold of NP 16-B sources in the reference order: v[NP-1] innermost,
@@ -113,7 +134,7 @@ __device__ __forceinline__ E fold_one(const PeerSrcs& S, int nsrc, size_t i) {
 // in flight: the grid is small -- every workgroup pays barriers -- so the depth has to come from
 // each wave; round 5's A/B on one GPU, profiles/r05k_*: twice the r05j depth was as fast or
 // faster at every size >= 16 Mi); the last partial round is predicated.
-template <typename E, int OP, bool ACC32, int V, int NP, int ND>
+template <typename E, int OP, bool ACC32, int V, int NP, int ND, bool SYS>
 __device__ __forceinline__ void slab_fold_n(const PeerDsts& D, const PeerSrcs& S, size_t count) {
   // (1-byte elements: half the depth -- their per-byte max / min unpack needs the registers)
   // (V & 16: the small-NP cases as deep as NP >= 4's 32 vectors -- free in registers, which the
@@ -129,13 +150,13 @@ __device__ __forceinline__ void slab_fold_n(const PeerDsts& D, const PeerSrcs& S
   if ((size_t)t < head) {
     const E v = fold_one<E, OP, ACC32>(S, NP, t);
 #pragma unroll
-    for (int d = 0; d < ND; d++) reinterpret_cast<E*>(D.p[d])[t] = v;
+    for (int d = 0; d < ND; d++) est<SYS>(reinterpret_cast<E*>(D.p[d]) + t, v);
   }
   if ((size_t)t < tail) {
     const size_t i = head + nvec * N + t;
     const E v = fold_one<E, OP, ACC32>(S, NP, i);
 #pragma unroll
-    for (int d = 0; d < ND; d++) reinterpret_cast<E*>(D.p[d])[i] = v;
+    for (int d = 0; d < ND; d++) est<SYS>(reinterpret_cast<E*>(D.p[d]) + i, v);
   }
   const char* src[NP];
 #pragma unroll
@@ -143,6 +164,18 @@ __device__ __forceinline__ void slab_fold_n(const PeerDsts& D, const PeerSrcs& S
   char* out[ND];
 #pragma unroll
   for (int d = 0; d < ND; d++) out[d] = D.p[d] + head * sizeof(E);
+  // (SYS) buffer stores with sc0 sc1 (aux 17), one resource per destination
+  __amdgpu_buffer_rsrc_t R[ND];
+#pragma unroll
+  for (int d = 0; d < ND; d++)
+    R[d] = SYS ? __builtin_amdgcn_make_buffer_rsrc(out[d], 0, (int)(nvec * 16), 0x00020000)
+               : __builtin_amdgcn_make_buffer_rsrc(nullptr, 0, 0, 0);
+  auto vst = [&](int d, size_t vi, u32x4 o) {
+    if constexpr (SYS)
+      __builtin_amdgcn_raw_buffer_store_b128(o, R[d], (uint32_t)(vi * 16), 0, 17);
+    else
+      pst<V>(out[d] + vi * 16, o);
+  };
   constexpr size_t kStep = (size_t)kBlock * PU;
   const size_t full = nvec / kStep * kStep;
   for (size_t v0 = 0; v0 < full; v0 += kStep) {
@@ -157,7 +190,7 @@ __device__ __forceinline__ void slab_fold_n(const PeerDsts& D, const PeerSrcs& S
     for (int u = 0; u < PU; u++) {
       const u32x4 o = fold_n<E, OP, ACC32, NP>(r[u]);
 #pragma unroll
-      for (int d = 0; d < ND; d++) pst<V>(out[d] + (v0 + (size_t)u * kBlock + t) * 16, o);
+      for (int d = 0; d < ND; d++) vst(d, v0 + (size_t)u * kBlock + t, o);
     }
   }
   for (size_t v = full + t; v < nvec; v += kBlock) {  // the last partial round
@@ -166,7 +199,7 @@ __device__ __forceinline__ void slab_fold_n(const PeerDsts& D, const PeerSrcs& S
     for (int j = 0; j < NP; j++) r[j] = pld<V>(src[j] + v * 16);
     const u32x4 o = fold_n<E, OP, ACC32, NP>(r);
 #pragma unroll
-    for (int d = 0; d < ND; d++) pst<V>(out[d] + v * 16, o);
+    for (int d = 0; d < ND; d++) vst(d, v, o);
   }
 }
 
@@ -176,7 +209,7 @@ __device__ __forceinline__ void slab_fold(const PeerDsts& D, const PeerSrcs& S, 
                                           size_t count) {
   switch (nsrc) {  // uniform over the grid: one branch per slab, none in the loop
 #define HYDRA_SLAB_FOLD_CASE(k) \
-  case k: slab_fold_n<E, OP, ACC32, V, k, PUSH ? k : 1>(D, S, count); break;
+  case k: slab_fold_n<E, OP, ACC32, V, k, PUSH ? k : 1, PUSH && (V & 512) == 0>(D, S, count); break;
     HYDRA_SLAB_FOLD_CASE(1)
     HYDRA_SLAB_FOLD_CASE(2)
     HYDRA_SLAB_FOLD_CASE(3)
@@ -360,7 +393,7 @@ __global__ __launch_bounds__(kBlock) void k_peer_push(PeerLaunch A) {
     for (size_t k = blockIdx.x; lo + k * SL < hi; k += G) fold_slab(k);
   }
   stamp<V>(A, 2);
-  peer_barrier(Y, 2);
+  peer_barrier(Y, 2, (V & 512) != 0);  // no L2 writeback: the stores were system-coherent
   stamp<V>(A, 3);
   stamp<V>(A, 4);
   stamp<V>(A, 5);

@@ -52,6 +52,7 @@ hipError_t launch_variant(int v, int algo, const PeerLaunch& A, unsigned grid, h
     case 128: return launch_t<float, kSum, false, 128>(algo, A, grid, s, occ);
     case 192: return launch_t<float, kSum, false, 192>(algo, A, grid, s, occ);
     case 256: return launch_t<float, kSum, false, 256>(algo, A, grid, s, occ);
+    case 512: return launch_t<float, kSum, false, 512>(algo, A, grid, s, occ);
   }
   return hipErrorInvalidValue;
 }
@@ -73,9 +74,10 @@ hipError_t launch_peer(int algo, int op, int dtype, bool acc32, const PeerLaunch
     if (v == 128) return launch_t<float, kSum, false, 136>(algo, A, grid, s);
     if (v == 192) return launch_t<float, kSum, false, 200>(algo, A, grid, s);
     if (v == 256) return launch_t<float, kSum, false, 264>(algo, A, grid, s);
+    if (v == 512) return launch_t<float, kSum, false, 520>(algo, A, grid, s);
     return launch_t<float, kSum, false, 8>(algo, A, grid, s);
   }
-  if (((v >= 1 && v <= 7) || v == 16 || v == 32 || v == 64 || v == 128 || v == 192 || v == 256) && op == kSum && dtype == kF32 && !acc32)
+  if (((v >= 1 && v <= 7) || v == 16 || v == 32 || v == 64 || v == 128 || v == 192 || v == 256 || v == 512) && op == kSum && dtype == kF32 && !acc32)
     return launch_variant(v, algo, A, grid, s);
 #endif
   switch (op) {  // one translation unit per op (peer_kernels_<op>.hip)
@@ -91,7 +93,7 @@ hipError_t peer_occupancy(int algo, int op, int dtype, bool acc32, int* per_cu) 
   const PeerLaunch A{};
 #ifdef HYDRA_MEASURE  // a variant's own register count (the deeper ones hold fewer per CU)
   const int v = current_variant() - kPeerVariantBase;
-  if (((v >= 1 && v <= 7) || v == 16 || v == 32 || v == 64 || v == 128 || v == 192 || v == 256) && op == kSum && dtype == kF32 && !acc32)
+  if (((v >= 1 && v <= 7) || v == 16 || v == 32 || v == 64 || v == 128 || v == 192 || v == 256 || v == 512) && op == kSum && dtype == kF32 && !acc32)
     return launch_variant(v, algo, A, 1, nullptr, per_cu);
 #endif
   switch (op) {
