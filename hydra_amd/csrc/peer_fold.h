@@ -24,8 +24,8 @@ namespace {
 // the 1-3-source folds as deep as the others, bit 5 the push's slabs handed out by a ticket
 // counter instead of k = b mod G, bit 6 barrier 1 WITH a release fence (the kernel before
 // r06u), bit 7 barrier 1 with an agent-scope acquire, bit 8 the entry check reading the
-// host-mapped error word too (the kernel before r06w), bit 9 the push's stores plain and its
-// barrier 2 with the L2 writeback (the kernel before r06zc).
+// host-mapped error word too (the kernel before r06w), bit 9 plain stores and a release at
+// every barrier after the first (the kernels before r06zc / r06zh).
 template <int V>
 __device__ __forceinline__ u32x4 pld(const char* p) {
   if constexpr ((V & 1) != 0) return ld<kNT>(p, rsrc<kNT>(nullptr, 0), 0);
@@ -204,12 +204,14 @@ __device__ __forceinline__ void slab_fold_n(const PeerDsts& D, const PeerSrcs& S
 }
 
 // PUSH: every source is also a destination (the result is stored into all P buckets)
-template <typename E, int OP, bool ACC32, int V = 0, bool PUSH = false>
+// SYS: system-coherent stores (est / vst above) -- for results a peer reads (push, and the
+// pull's phase 1)
+template <typename E, int OP, bool ACC32, int V = 0, bool PUSH = false, bool SYS = PUSH>
 __device__ __forceinline__ void slab_fold(const PeerDsts& D, const PeerSrcs& S, int nsrc,
                                           size_t count) {
   switch (nsrc) {  // uniform over the grid: one branch per slab, none in the loop
 #define HYDRA_SLAB_FOLD_CASE(k) \
-  case k: slab_fold_n<E, OP, ACC32, V, k, PUSH ? k : 1, PUSH && (V & 512) == 0>(D, S, count); break;
+  case k: slab_fold_n<E, OP, ACC32, V, k, PUSH ? k : 1, SYS && (V & 512) == 0>(D, S, count); break;
     HYDRA_SLAB_FOLD_CASE(1)
     HYDRA_SLAB_FOLD_CASE(2)
     HYDRA_SLAB_FOLD_CASE(3)
@@ -308,12 +310,13 @@ __global__ __launch_bounds__(kBlock) void k_peer_two_shot(PeerLaunch A) {
 #pragma unroll
       for (int j = 0; j < kPeerMaxRanks; j++)
         if (j < P) S.p[j] = A.x[(r + j) % P] + s * sizeof(E);
-      slab_fold<E, OP, ACC32, V>(D, S, P, hi - s < SL ? hi - s : SL);
+      slab_fold<E, OP, ACC32, V, false, true>(D, S, P, hi - s < SL ? hi - s : SL);
     }
   }
-  // workgroup b of every rank has finished ITS slabs (k = b mod G) of its own block
+  // workgroup b of every rank has finished ITS slabs (k = b mod G) of its own block (stored
+  // system-coherent: no L2 writeback before the flag)
   stamp<V>(A, 2);
-  if (!peer_barrier(Y, 2)) return;
+  if (!peer_barrier(Y, 2, (V & 512) != 0)) return;
   stamp<V>(A, 3);
   // phase 2: the same slab indices of every other block, pulled from their owners; the start
   // peer rotates with b so the workgroups of one rank read from all P-1 links at once
@@ -327,7 +330,7 @@ __global__ __launch_bounds__(kBlock) void k_peer_two_shot(PeerLaunch A) {
   }
   // nobody leaves (and lets its caller overwrite the bucket) while a peer may still read it
   stamp<V>(A, 4);
-  peer_barrier(Y, 3);
+  peer_barrier(Y, 3, (V & 512) != 0);  // publishes no store (its own bucket only): no release
   stamp<V>(A, 5);
 }
 
@@ -426,9 +429,11 @@ __global__ __launch_bounds__(kBlock) void k_peer_one_shot(PeerLaunch A) {
       slab_fold<E, OP, ACC32, V>(D, S, P, hi - s < SL ? hi - s : SL);
     }
   }
-  // every rank's workgroup b has read its slabs of every bucket -> safe to overwrite ours
+  // every rank's workgroup b has read its slabs of every bucket -> safe to overwrite ours.  It
+  // publishes no store (the scratch slabs are copied back by the workgroup that wrote them):
+  // no release
   stamp<V>(A, 2);
-  if (!peer_barrier(Y, 2)) return;
+  if (!peer_barrier(Y, 2, (V & 512) != 0)) return;
   stamp<V>(A, 3);
   w = 0;
   for (int q = 0; q < P; q++) {
