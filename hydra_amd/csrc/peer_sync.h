@@ -5,11 +5,14 @@
 // grid-wide barrier (and no co-residency requirement across workgroups) is needed.
 //
 // Memory model (LLVM AMDGPU, gfx950; MI355X_MICROARCH.md "inter-workgroup visibility"):
-//   producer: every storing wave `s_waitcnt vmcnt(0)` -> workgroup barrier -> one wave:
-//             system-scope release fence (buffer_wbl2 sc0 sc1: this XCD's dirty L2 lines --
-//             the workgroup's results -- reach memory) -> explicit `s_waitcnt vmcnt(0)` (the
-//             compiler may drop the wait after buffer_wbl2, letting the flag overtake the
-//             write-back) -> relaxed system-scope flag stores into every rank's signal area;
+//   producer: the results a peer reads are stored system-coherent (sc0 sc1: written through
+//             to memory, peer_fold.h est / vst) -> every storing wave `s_waitcnt vmcnt(0)` (the
+//             stores are complete) -> workgroup barrier -> relaxed system-scope flag stores
+//             into every rank's signal area.  (release = true adds a system-scope fence --
+//             buffer_wbl2 sc0 sc1: this XCD's dirty L2 lines reach memory -- and a second
+//             explicit wait before the flags: the form plain stores need, kept for the
+//             measurement variants of the pre-round-6 kernels; a barrier that publishes no
+//             store needs neither);
 //   consumer: relaxed polls of its own (uncached) signal area -> system-scope acquire fence
 //             (buffer_inv sc0 sc1: drops stale L1 / non-coherent L2 copies of peer lines) ->
 //             `s_waitcnt vmcnt(0)` -> workgroup barrier -> plain loads.
